@@ -1,0 +1,143 @@
+/*
+ * oracle.h -- CPU restatement of veneur's per-flush sketch path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in veneur_amd/ links, loads or calls this
+ * code; only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg do,
+ * and only as the checker.  It restates, in plain C, the Go reference (the Go
+ * toolchain is absent from this image, so the reference itself cannot be run):
+ *
+ *   vendor/github.com/dgryski/go-metro/metro64.go:7-85       (MetroHash64)
+ *   vendor/github.com/dgryski/go-bits/clz.go:6-37            (Clz; amd64 asm: 0 -> 64)
+  *   vendor/github.com/axiomhq/hyperloglog/ (all .go files)          (HLL-TailCut sketch)
+ *   tdigest/merging_digest.go:21-412                         (MergingDigest)
+ *   samplers/samplers.go:125-526                             (Counter/Gauge/Set/Histo)
+ *   samplers/parser.go:213-304, http.go:77-90                (FNV-1a-32 digest)
+ *   Go 1.9 stdlib: math.Log (log.go), math.Pow (pow.go), math.Asin (asin.go,
+ *   atan.go), sort.Sort (sort.go quickSort) -- restated, see go_math section.
+ *
+ * Pinning: tests/test_oracle_kats.py checks this file against every known-answer
+ * vector the reference's own tests hold for the path.
+ */
+#ifndef VENEUR_ORACLE_H
+#define VENEUR_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- hashing ------------------------------------------------------------ */
+uint64_t or_metro_hash64(const uint8_t* buf, size_t len, uint64_t seed);
+uint64_t or_clz64(uint64_t x);
+uint32_t or_fnv1a32(const uint8_t* buf, size_t len, uint32_t h /* 2166136261 to start */);
+
+/* ---- Go 1.9 math restatements ------------------------------------------- */
+double or_go_log(double x);
+double or_go_pow(double x, double y);
+double or_go_asin(double x);
+int64_t or_go_f64_to_i64(double x);   /* amd64 CVTTSD2SQ semantics */
+uint64_t or_go_f64_to_u64(double x);  /* Go amd64 uint64(float64) */
+
+/* ---- axiomhq/hyperloglog Sketch ------------------------------------------ */
+typedef struct or_hll or_hll;
+or_hll* or_hll_new(uint8_t precision);          /* NULL if p outside [4,18] */
+void or_hll_free(or_hll* sk);
+or_hll* or_hll_clone(const or_hll* sk);
+void or_hll_insert_hash(or_hll* sk, uint64_t x); /* Insert with hash(e) == x (nopHash tests) */
+void or_hll_insert(or_hll* sk, const uint8_t* e, size_t len); /* metro64 seed 1337 */
+uint64_t or_hll_estimate(or_hll* sk);
+int or_hll_merge(or_hll* sk, const or_hll* other); /* 0 ok, -1 precision mismatch */
+void or_hll_to_normal(or_hll* sk);
+void or_hll_merge_sparse(or_hll* sk);
+int or_hll_is_sparse(const or_hll* sk);
+void or_hll_set_sparse_flag(or_hll* sk, int sparse);
+uint8_t or_hll_p(const or_hll* sk);
+uint8_t or_hll_b(const or_hll* sk);
+void or_hll_set_b(or_hll* sk, uint8_t b);
+uint32_t or_hll_nz(const or_hll* sk);
+uint8_t or_hll_reg_get(const or_hll* sk, uint32_t i);
+void or_hll_reg_set(or_hll* sk, uint32_t i, uint8_t v);   /* registers.set (with nz bookkeeping) */
+void or_hll_reg_rebase(or_hll* sk, uint8_t delta);
+uint32_t or_hll_m(const or_hll* sk);
+/* sparse state: decoded compressed list (sorted, as stored) and tmpSet (sorted ascending) */
+size_t or_hll_list_codes(const or_hll* sk, uint32_t* out, size_t cap);
+size_t or_hll_list_bytes(const or_hll* sk);
+uint32_t or_hll_list_count(const or_hll* sk);
+size_t or_hll_tmp_codes(const or_hll* sk, uint32_t* out, size_t cap);
+size_t or_hll_tmp_len(const or_hll* sk);
+void or_hll_tmp_add(or_hll* sk, uint32_t code);
+void or_hll_list_append(or_hll* sk, uint32_t code);   /* compressedList.Append */
+/* registers as packed tailcuts (byte i: high nibble = reg 2i, low nibble = reg 2i+1) */
+size_t or_hll_tailcuts(const or_hll* sk, uint8_t* out, size_t cap);
+/* MarshalBinary / UnmarshalBinary (tmpSet written in ascending order: Go uses map order) */
+size_t or_hll_marshal(const or_hll* sk, uint8_t* out, size_t cap);
+int or_hll_unmarshal(or_hll* sk, const uint8_t* data, size_t len);
+uint32_t or_hll_encode_hash(uint64_t x, uint8_t p, uint8_t pp);
+void or_hll_decode_hash(uint32_t k, uint8_t p, uint8_t pp, uint32_t* idx, uint8_t* r);
+void or_hll_get_pos_val(uint64_t x, uint8_t p, uint64_t* idx, uint8_t* rho);
+
+/* ---- tdigest.MergingDigest ------------------------------------------------ */
+typedef struct or_td or_td;
+or_td* or_td_new(double compression);
+void or_td_free(or_td* td);
+int or_td_add(or_td* td, double value, double weight);   /* -1 where Go panics */
+double or_td_quantile(or_td* td, double q);              /* NaN where Go panics/empty */
+double or_td_cdf(or_td* td, double x);
+double or_td_min(const or_td* td);
+double or_td_max(const or_td* td);
+double or_td_count(const or_td* td);
+/* Merge: perm = order in which other's main centroids are re-Added (rand.Perm in Go);
+ * NULL -> identity order. */
+void or_td_merge(or_td* td, or_td* other, const int64_t* perm);
+size_t or_td_centroids(or_td* td, double* means, double* weights, size_t cap); /* merges temps */
+size_t or_td_temp_len(const or_td* td);
+/* gob codec of (Centroids, compression, min, max); encode returns bytes written (0 = cap short) */
+size_t or_td_gob_encode(or_td* td, uint8_t* out, size_t cap);
+int or_td_gob_decode(or_td* td, const uint8_t* data, size_t len);
+void or_td_set_state(or_td* td, const double* means, const double* weights, size_t n,
+                     double compression, double min, double max);
+
+/* ---- samplers + Worker (per-class slot tables, arrival order) ----------- */
+typedef struct or_worker or_worker;
+or_worker* or_worker_new(uint32_t n_counter, uint32_t n_gauge, uint32_t n_histo, uint32_t n_set);
+void or_worker_free(or_worker* w);
+/* Counter.Sample / Gauge.Sample / Histo.Sample / Set.Sample in arrival order */
+void or_worker_counter(or_worker* w, const uint32_t* slot, const double* value, const float* rate, size_t n);
+void or_worker_gauge(or_worker* w, const uint32_t* slot, const double* value, size_t n);
+void or_worker_histo(or_worker* w, const uint32_t* slot, const double* value, const float* rate, size_t n);
+void or_worker_set(or_worker* w, const uint32_t* slot, const uint32_t* member_off,
+                   const uint8_t* member_bytes, size_t n);
+void or_worker_set_hashed(or_worker* w, const uint32_t* slot, const uint64_t* hashes, size_t n);
+/* imports (Combine) */
+void or_worker_import_counter(or_worker* w, uint32_t slot, int64_t v);
+void or_worker_import_gauge(or_worker* w, uint32_t slot, double v);
+int or_worker_import_set(or_worker* w, uint32_t slot, const uint8_t* data, size_t len);
+int or_worker_import_histo(or_worker* w, uint32_t slot, const uint8_t* gob, size_t len, const int64_t* perm);
+/* accessors (touched = Upsert happened for this slot) */
+int or_worker_touched(const or_worker* w, int cls, uint32_t slot);
+int64_t or_worker_counter_value(const or_worker* w, uint32_t slot);
+double or_worker_gauge_value(const or_worker* w, uint32_t slot);
+/* stats: weight, min, max, sum, rsum, digest min, digest max, digest count */
+void or_worker_histo_stats(const or_worker* w, uint32_t slot, double* out8);
+double or_worker_histo_quantile(or_worker* w, uint32_t slot, double q);
+size_t or_worker_histo_centroids(or_worker* w, uint32_t slot, double* means, double* weights, size_t cap);
+uint64_t or_worker_set_estimate(or_worker* w, uint32_t slot);
+or_td* or_worker_histo_digest(or_worker* w, uint32_t slot);
+or_hll* or_worker_set_sketch(or_worker* w, uint32_t slot);
+
+/* Multi-threaded CPU baseline: nthreads workers, records routed by digest % nthreads.
+ * Runs ProcessMetric for every record, then the flush (quantiles for every touched histo
+ * at the given percentiles, Estimate for every touched set).  Returns seconds elapsed. */
+double or_baseline_run(int nthreads,
+                       uint32_t n_counter_slots, uint32_t n_gauge_slots, uint32_t n_histo_slots, uint32_t n_set_slots,
+                       const uint32_t* c_slot, const double* c_val, const float* c_rate, size_t n_c,
+                       const uint32_t* g_slot, const double* g_val, size_t n_g,
+                       const uint32_t* h_slot, const double* h_val, const float* h_rate, size_t n_h,
+                       const uint32_t* s_slot, const uint32_t* s_off, const uint8_t* s_bytes, size_t n_s,
+                       const double* percentiles, int n_pct, double* checksum_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
