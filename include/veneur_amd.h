@@ -1,0 +1,203 @@
+/*
+ * veneur_amd.h -- C-ABI of the MI355X-native per-flush sketch aggregation engine.
+ *
+ * This is the drop-in boundary for veneur's aggregation hot path.  Each entry point
+ * replaces the body of a Go function on that path (the Go signatures stay; the cgo
+ * binding a maintainer adds is in INTEGRATION.md):
+ *
+ *   vn_engine_create     NewWorker / NewWorkerMetrics / samplers.New*        worker.go:63-76,141-154
+ *   vn_stage_acquire     (new) pinned SoA staging the Go side appends to       --
+ *   vn_submit            Worker.ProcessMetric body for a staged batch          worker.go:187-227
+ *                          Counter.Sample samplers.go:132-134, Gauge.Sample 198-200,
+ *                          Set.Sample 265-267 (-> hyperloglog.Insert), Histo.Sample 346-356
+ *                          (-> tdigest.MergingDigest.Add merging_digest.go:97-118)
+ *   vn_ingest            same, batch already resident in device memory (HBM)
+ *   vn_import            Worker.ImportMetric body (decoded JSONMetric values)    worker.go:230-268
+ *                          Counter.Combine 171-183, Gauge.Combine 237-249
+ *   vn_flush             Worker.Flush + the per-sampler flush math               worker.go:271-298
+ *                          Counter.Flush 137-148, Gauge.Flush 203-214,
+ *                          Histo.Flush 373-498 (-> MergingDigest.Quantile 283-313),
+ *                          Set.Flush 282-293 (-> hyperloglog.Estimate 203-227)
+ *   vn_read_histo/_set   state introspection (Histo.Value centroids, Set.Hll registers)
+ *   vn_metro64           metro.Hash64 batch (go-metro metro64.go:7-85)
+ *
+ * Conventions: every function returns 0 on success or a negative VN_E* code; the
+ * message is available from vn_last_error(engine).  All buffers handed out by the
+ * engine are owned by the engine (the Go side never passes Go-heap pointers for C to
+ * retain).  Calls on one engine are serialised by the caller (veneur's Worker mutex).
+ * Slots are class-local dense indices assigned by the host's MetricKey interning
+ * (one slot table per sampler map: counters, gauges, histograms+timers, sets).
+ */
+#ifndef VENEUR_AMD_H
+#define VENEUR_AMD_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VN_ABI_VERSION 1
+
+enum {
+  VN_OK = 0,
+  VN_EINVAL = -1,   /* bad argument (out-of-range slot, capacity exceeded, ...) */
+  VN_EHIP = -2,     /* HIP runtime error */
+  VN_ENOMEM = -3,   /* device / pinned allocation failed */
+  VN_EDECODE = -4,  /* malformed import payload */
+};
+
+enum { VN_COUNTER = 0, VN_GAUGE = 1, VN_HISTO = 2, VN_SET = 3, VN_NCLASS = 4 };
+
+#define VN_MAX_PERCENTILES 16
+
+typedef struct vn_engine vn_engine;
+
+typedef struct {
+  int32_t device;                   /* HIP device ordinal */
+  uint32_t capacity[VN_NCLASS];     /* slots per class */
+  double compression;               /* t-digest delta; veneur uses 100 (samplers.go:364) */
+  uint32_t n_percentiles;           /* quantiles evaluated at flush, e.g. .5 .9 .99 .999 */
+  double percentiles[VN_MAX_PERCENTILES];
+  uint64_t max_batch_records;       /* largest batch per class passed to one ingest call */
+  uint64_t max_batch_member_bytes;  /* largest set member blob per ingest call */
+  /* t-digest: a key's first `histo_exact_threshold` samples of a window replay
+   * MergingDigest's 42-sample incremental merge bit-for-bit; samples beyond it are merged
+   * in one batch per ingest (rank-error parity).  0 -> 32768; UINT32_MAX -> always exact. */
+  uint32_t histo_exact_threshold;
+} vn_config;
+
+/* One ingest batch: per-class SoA streams in arrival order (the order ProcessMetric saw
+ * them).  Pointers are host pointers for vn_submit / vn_ingest_host and device pointers
+ * for vn_ingest.  A class with n == 0 may leave its pointers NULL.
+ * Sets: either member_off (n+1 offsets into member_bytes) + member_bytes, hashed with
+ * metro64(seed 1337), or set_hash (one precomputed 64-bit hash per record, the path the
+ * reference's nopHash tests take). */
+typedef struct {
+  uint64_t n_counter;
+  const uint32_t* counter_slot;
+  const double* counter_value;
+  const float* counter_rate;
+
+  uint64_t n_gauge;
+  const uint32_t* gauge_slot;
+  const double* gauge_value;
+
+  uint64_t n_histo;
+  const uint32_t* histo_slot;
+  const double* histo_value;
+  const float* histo_rate;
+
+  uint64_t n_set;
+  const uint32_t* set_slot;
+  const uint32_t* set_member_off;
+  const uint8_t* set_member_bytes;
+  const uint64_t* set_hash;
+} vn_batch;
+
+/* Counts for a batch the caller wrote into the engine's pinned stage. */
+typedef struct {
+  uint64_t n_counter, n_gauge, n_histo, n_set, n_set_member_bytes;
+} vn_batch_counts;
+
+/* Writable views of the engine-owned pinned staging buffers (capacity = max_batch_*). */
+typedef struct {
+  uint64_t capacity;
+  uint64_t member_bytes_capacity;
+  uint32_t* counter_slot; double* counter_value; float* counter_rate;
+  uint32_t* gauge_slot; double* gauge_value;
+  uint32_t* histo_slot; double* histo_value; float* histo_rate;
+  uint32_t* set_slot; uint32_t* set_member_off; uint8_t* set_member_bytes;
+} vn_stage;
+
+/* Flush result: one entry per slot touched in the window (Upsert semantics), in ascending
+ * slot order per class.  Engine-owned host memory, valid until the next vn_flush. */
+typedef struct {
+  uint64_t n_counter;
+  const uint32_t* counter_slot;
+  const int64_t* counter_value;        /* Counter.value (Flush emits float64(value)) */
+
+  uint64_t n_gauge;
+  const uint32_t* gauge_slot;
+  const double* gauge_value;
+
+  uint64_t n_histo;
+  const uint32_t* histo_slot;
+  /* per histo, VN_HISTO_STATS doubles: LocalWeight, LocalMin, LocalMax, LocalSum,
+   * LocalReciprocalSum, digest min, digest max, digest count (mainWeight) */
+  const double* histo_stats;
+  /* per histo, n_percentiles doubles: MergingDigest.Quantile(p) (NaN when empty) */
+  const double* histo_quantiles;
+  uint32_t n_percentiles;
+
+  uint64_t n_set;
+  const uint32_t* set_slot;
+  const uint64_t* set_estimate;        /* Sketch.Estimate() */
+  const uint8_t* set_sparse;           /* 1 = sparse representation at flush */
+
+  uint64_t samples_processed;          /* records ingested this window (worker.processed) */
+  uint64_t samples_imported;           /* imported values this window (worker.imported) */
+} vn_flush_result;
+#define VN_HISTO_STATS 8
+
+/* Sparse / dense sketch state of one set slot (axiomhq Sketch fields). */
+typedef struct {
+  uint8_t touched, sparse, b, pad;
+  uint32_t nz;            /* registers.nz (dense) */
+  uint32_t list_count;    /* compressedList.count (sparse) */
+  uint32_t list_bytes;    /* len(compressedList.b) (sparse) */
+  uint32_t list_last;     /* compressedList.last */
+  uint32_t tmp_count;     /* len(tmpSet) */
+} vn_set_state;
+
+int vn_engine_create(const vn_config* cfg, vn_engine** out);
+void vn_engine_destroy(vn_engine* eng);
+const char* vn_last_error(const vn_engine* eng);
+int vn_abi_version(void);
+
+int vn_stage_acquire(vn_engine* eng, vn_stage* out);
+int vn_submit(vn_engine* eng, const vn_batch_counts* counts);  /* stage -> HBM -> ingest */
+int vn_ingest_host(vn_engine* eng, const vn_batch* host_batch);  /* copies through the stage */
+int vn_ingest(vn_engine* eng, const vn_batch* device_batch);     /* inputs already in HBM */
+
+/* ImportMetric for decoded values (Counter.Combine adds int64, Gauge.Combine overwrites in
+ * arrival order); they target the GlobalOnly slot tables the host chose. */
+int vn_import_counters(vn_engine* eng, const uint32_t* slot, const int64_t* value, uint64_t n);
+int vn_import_gauges(vn_engine* eng, const uint32_t* slot, const double* value, uint64_t n);
+
+int vn_flush(vn_engine* eng, vn_flush_result* out);
+int vn_sync(vn_engine* eng);
+
+/* Introspection of the current (unflushed) window. */
+int vn_read_histo(vn_engine* eng, uint32_t slot, double* means, double* weights, uint32_t cap,
+                  uint32_t* n_centroids, double* stats /* VN_HISTO_STATS */);
+int vn_read_set(vn_engine* eng, uint32_t slot, vn_set_state* st, uint32_t* list_codes,
+                uint32_t list_cap, uint32_t* tmp_codes, uint32_t tmp_cap, uint8_t* registers /* 16384 */);
+
+/* Kernel-level entry points (known-answer checks of the HIP primitives). */
+int vn_metro64(int device, const uint8_t* bytes, const uint32_t* off, uint64_t n, uint64_t seed,
+               uint64_t* out);
+
+/* Device memory helpers for callers without another HIP binding (bench / tests). */
+int vn_device_alloc(int device, uint64_t bytes, void** out);
+int vn_device_free(void* p);
+int vn_copy_to_device(int device, void* dst, const void* src, uint64_t bytes);
+int vn_device_count(int* n);
+
+/* Timing of the last ingest+flush's kernels on the engine's stream (HIP events):
+ * milliseconds of the histo sort passes, of everything, and per-phase counters. */
+typedef struct {
+  float ms_ingest_counter, ms_ingest_gauge, ms_ingest_histo, ms_ingest_set, ms_flush;
+  float ms_sort_histo, ms_sort_set;
+  uint64_t sort_passes_histo, sort_passes_set;
+  float ms_radix_scatter_total;   /* sum over radix scatter launches */
+  uint64_t radix_scatter_launches;
+  uint64_t radix_scatter_bytes;   /* algorithmic bytes moved by those launches */
+} vn_timing;
+int vn_timing_enable(vn_engine* eng, int enable);
+int vn_get_timing(vn_engine* eng, vn_timing* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

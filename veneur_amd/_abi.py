@@ -1,0 +1,137 @@
+"""ctypes binding of include/veneur_amd.h and include/veneur_amd_synth.h.
+
+The shared library is built in-tree (veneur_amd/libveneur_amd.so, `make -C veneur_amd`
+or __graft_entry__.build()).  There is no fallback: if the HIP library is missing the
+import fails.
+"""
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libveneur_amd.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        "veneur_amd: %s is missing -- build the HIP engine first (make -C veneur_amd, or "
+        "python -c 'import __graft_entry__; __graft_entry__.build()')" % LIB_PATH)
+
+lib = C.CDLL(LIB_PATH)
+
+VN_OK, VN_EINVAL, VN_EHIP, VN_ENOMEM, VN_EDECODE = 0, -1, -2, -3, -4
+VN_COUNTER, VN_GAUGE, VN_HISTO, VN_SET = 0, 1, 2, 3
+VN_MAX_PERCENTILES = 16
+VN_HISTO_STATS = 8
+HLL_M = 16384
+
+u8p, u32p, u64p, i64p, f32p, f64p = (C.POINTER(t) for t in (C.c_uint8, C.c_uint32, C.c_uint64, C.c_int64,
+                                                             C.c_float, C.c_double))
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("capacity", C.c_uint32 * 4), ("compression", C.c_double),
+                ("n_percentiles", C.c_uint32), ("percentiles", C.c_double * VN_MAX_PERCENTILES),
+                ("max_batch_records", C.c_uint64), ("max_batch_member_bytes", C.c_uint64),
+                ("histo_exact_threshold", C.c_uint32)]
+
+
+class Batch(C.Structure):
+    _fields_ = [("n_counter", C.c_uint64), ("counter_slot", C.c_void_p), ("counter_value", C.c_void_p),
+                ("counter_rate", C.c_void_p),
+                ("n_gauge", C.c_uint64), ("gauge_slot", C.c_void_p), ("gauge_value", C.c_void_p),
+                ("n_histo", C.c_uint64), ("histo_slot", C.c_void_p), ("histo_value", C.c_void_p),
+                ("histo_rate", C.c_void_p),
+                ("n_set", C.c_uint64), ("set_slot", C.c_void_p), ("set_member_off", C.c_void_p),
+                ("set_member_bytes", C.c_void_p), ("set_hash", C.c_void_p)]
+
+
+class BatchCounts(C.Structure):
+    _fields_ = [("n_counter", C.c_uint64), ("n_gauge", C.c_uint64), ("n_histo", C.c_uint64),
+                ("n_set", C.c_uint64), ("n_set_member_bytes", C.c_uint64)]
+
+
+class Stage(C.Structure):
+    _fields_ = [("capacity", C.c_uint64), ("member_bytes_capacity", C.c_uint64),
+                ("counter_slot", u32p), ("counter_value", f64p), ("counter_rate", f32p),
+                ("gauge_slot", u32p), ("gauge_value", f64p),
+                ("histo_slot", u32p), ("histo_value", f64p), ("histo_rate", f32p),
+                ("set_slot", u32p), ("set_member_off", u32p), ("set_member_bytes", u8p)]
+
+
+class FlushResult(C.Structure):
+    _fields_ = [("n_counter", C.c_uint64), ("counter_slot", u32p), ("counter_value", i64p),
+                ("n_gauge", C.c_uint64), ("gauge_slot", u32p), ("gauge_value", f64p),
+                ("n_histo", C.c_uint64), ("histo_slot", u32p), ("histo_stats", f64p),
+                ("histo_quantiles", f64p), ("n_percentiles", C.c_uint32),
+                ("n_set", C.c_uint64), ("set_slot", u32p), ("set_estimate", u64p), ("set_sparse", u8p),
+                ("samples_processed", C.c_uint64), ("samples_imported", C.c_uint64)]
+
+
+class SetState(C.Structure):
+    _fields_ = [("touched", C.c_uint8), ("sparse", C.c_uint8), ("b", C.c_uint8), ("pad", C.c_uint8),
+                ("nz", C.c_uint32), ("list_count", C.c_uint32), ("list_bytes", C.c_uint32),
+                ("list_last", C.c_uint32), ("tmp_count", C.c_uint32)]
+
+
+class Timing(C.Structure):
+    _fields_ = [("ms_ingest_counter", C.c_float), ("ms_ingest_gauge", C.c_float), ("ms_ingest_histo", C.c_float),
+                ("ms_ingest_set", C.c_float), ("ms_flush", C.c_float), ("ms_sort_histo", C.c_float),
+                ("ms_sort_set", C.c_float), ("sort_passes_histo", C.c_uint64), ("sort_passes_set", C.c_uint64),
+                ("ms_radix_scatter_total", C.c_float), ("radix_scatter_launches", C.c_uint64),
+                ("radix_scatter_bytes", C.c_uint64)]
+
+
+class SynthConfig(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_keys", C.c_uint32), ("zipf_s", C.c_double), ("mix", C.c_double * 4),
+                ("n_samples", C.c_uint64), ("shard", C.c_uint32), ("n_shards", C.c_uint32),
+                ("member_universe", C.c_uint64), ("rate_half", C.c_double), ("rate_tenth", C.c_double),
+                ("histo_mu", C.c_double), ("histo_sigma", C.c_double), ("threads", C.c_int)]
+
+
+class SynthOut(C.Structure):
+    _fields_ = [("n_slots", C.c_uint32 * 4), ("n", C.c_uint64 * 4),
+                ("c_slot", u32p), ("c_val", f64p), ("c_rate", f32p),
+                ("g_slot", u32p), ("g_val", f64p),
+                ("h_slot", u32p), ("h_val", f64p), ("h_rate", f32p),
+                ("s_slot", u32p), ("s_off", u32p), ("s_bytes", u8p), ("s_nbytes", C.c_uint64),
+                ("key_of_slot", u32p * 4), ("digest_of_slot", u32p * 4)]
+
+
+def _sig(name, res, *args):
+    f = getattr(lib, name)
+    f.restype = res
+    f.argtypes = list(args)
+    return f
+
+
+vp = C.c_void_p
+_sig("vn_abi_version", C.c_int)
+_sig("vn_engine_create", C.c_int, C.POINTER(Config), C.POINTER(vp))
+_sig("vn_engine_destroy", None, vp)
+_sig("vn_last_error", C.c_char_p, vp)
+_sig("vn_stage_acquire", C.c_int, vp, C.POINTER(Stage))
+_sig("vn_submit", C.c_int, vp, C.POINTER(BatchCounts))
+_sig("vn_ingest_host", C.c_int, vp, C.POINTER(Batch))
+_sig("vn_ingest", C.c_int, vp, C.POINTER(Batch))
+_sig("vn_import_counters", C.c_int, vp, u32p, i64p, C.c_uint64)
+_sig("vn_import_gauges", C.c_int, vp, u32p, f64p, C.c_uint64)
+_sig("vn_flush", C.c_int, vp, C.POINTER(FlushResult))
+_sig("vn_sync", C.c_int, vp)
+_sig("vn_read_histo", C.c_int, vp, C.c_uint32, f64p, f64p, C.c_uint32, u32p, f64p)
+_sig("vn_read_set", C.c_int, vp, C.c_uint32, C.POINTER(SetState), u32p, C.c_uint32, u32p, C.c_uint32, u8p)
+_sig("vn_metro64", C.c_int, C.c_int, u8p, u32p, C.c_uint64, C.c_uint64, u64p)
+_sig("vn_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(vp))
+_sig("vn_device_free", C.c_int, vp)
+_sig("vn_copy_to_device", C.c_int, C.c_int, vp, vp, C.c_uint64)
+_sig("vn_device_count", C.c_int, C.POINTER(C.c_int))
+_sig("vn_timing_enable", C.c_int, vp, C.c_int)
+_sig("vn_get_timing", C.c_int, vp, C.POINTER(Timing))
+_sig("vn_synth_generate", C.c_int, C.POINTER(SynthConfig), C.POINTER(SynthOut))
+_sig("vn_synth_free", None, C.POINTER(SynthOut))
+
+# every symbol include/*.h declares (checked by tests/test_abi.py on CPU)
+EXPORTED = [
+    "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
+    "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_flush", "vn_sync",
+    "vn_read_histo", "vn_read_set", "vn_metro64", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
+    "vn_device_count", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
+]

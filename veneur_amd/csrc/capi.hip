@@ -1,0 +1,565 @@
+// capi.hip -- engine lifetime and the C-ABI of include/veneur_amd.h.
+#include <cstring>
+#include <stdexcept>
+
+#include "histo.h"
+
+using namespace vn;
+
+namespace {
+
+template <class T>
+void dalloc(T*& p, size_t count) {
+  if (count == 0) count = 1;
+  VN_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)));
+}
+template <class T>
+void dzero(T* p, size_t count, hipStream_t st) {
+  if (count) VN_HIP_CHECK(hipMemsetAsync(p, 0, count * sizeof(T), st));
+}
+template <class T>
+void halloc(T*& p, size_t count) {
+  if (count == 0) count = 1;
+  VN_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p), count * sizeof(T), hipHostMallocDefault));
+}
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+template <class T>
+void hfree(T*& p) {
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+}
+
+int bits_for(uint32_t cap) {
+  int b = 1;
+  while (b < 32 && (1u << b) < cap) b++;
+  return b;
+}
+
+int fail(vn_engine* e, int code, const std::string& msg) {
+  if (e) e->err = msg;
+  return code;
+}
+
+template <class F>
+int guarded(vn_engine* e, F&& f) {
+  try {
+    f();
+    return VN_OK;
+  } catch (const HipError& h) {
+    return fail(e, VN_EHIP, std::string(hipGetErrorString(h.err)) + " at " + h.file + ":" + std::to_string(h.line) +
+                                ": " + h.expr);
+  } catch (const std::invalid_argument& x) {
+    return fail(e, VN_EINVAL, x.what());
+  } catch (const std::bad_alloc&) {
+    return fail(e, VN_ENOMEM, "out of memory");
+  } catch (const std::exception& x) {
+    return fail(e, VN_EINVAL, x.what());
+  }
+}
+
+void check_slots_host(const uint32_t* slot, uint64_t n, uint32_t cap, const char* what) {
+  for (uint64_t i = 0; i < n; i++)
+    if (slot[i] >= cap) throw std::invalid_argument(std::string(what) + " slot out of range");
+}
+
+void create_impl(vn_engine* e) {
+  VN_HIP_CHECK(hipSetDevice(e->device));
+  VN_HIP_CHECK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+  hipStream_t st = e->st;
+  const uint64_t R = e->max_records;
+  const uint32_t cc = e->cap[VN_COUNTER], cg = e->cap[VN_GAUGE], ch = e->cap[VN_HISTO], cs = e->cap[VN_SET];
+  const uint32_t capc = e->cap_cent;
+  const uint32_t capmax = std::max(std::max(cc, cg), std::max(ch, cs));
+
+  dalloc(e->cval, cc); dzero(e->cval, cc, st);
+  dalloc(e->ctouch, cc); dzero(e->ctouch, cc, st);
+  dalloc(e->gseq, cg); dzero(e->gseq, cg, st);
+  dalloc(e->gval, cg); dzero(e->gval, cg, st);
+  dalloc(e->gtouch, cg); dzero(e->gtouch, cg, st);
+
+  dalloc(e->hst, (size_t)ch * VN_HISTO_STATS);
+  dalloc(e->hncent, ch); dzero(e->hncent, ch, st);
+  dalloc(e->hcur, ch); dzero(e->hcur, ch, st);
+  dalloc(e->htouch, ch); dzero(e->htouch, ch, st);
+  for (int b = 0; b < 2; b++) {
+    dalloc(e->cmean[b], (size_t)ch * capc);
+    dalloc(e->cw[b], (size_t)ch * capc);
+  }
+  dalloc(e->h_bt, ch); dzero(e->h_bt, ch, st);
+  dalloc(e->h_pos, (size_t)ch + 1);
+  dalloc(e->h_tl, ch);
+  dalloc(e->h_cnt, 8);
+  dalloc(e->h_oldcnt, (size_t)ch + 1);
+  dalloc(e->h_oldoff, (size_t)ch + 2);
+  const uint64_t touch_max = ch ? std::min<uint64_t>(ch, R) : 0;
+  e->h_sort_cap = ch ? R + touch_max * capc : 0;
+  dalloc(e->hA0, e->h_sort_cap); dalloc(e->hB0, e->h_sort_cap);
+  dalloc(e->hA1, e->h_sort_cap); dalloc(e->hB1, e->h_sort_cap);
+  dalloc(e->h_w, e->h_sort_cap);
+  dalloc(e->h_wk, e->h_sort_cap);
+  dalloc(e->h_start, ch);
+  dalloc(e->h_end, ch);
+  dalloc(e->h_nch, (size_t)touch_max + 1);
+  dalloc(e->h_chb, (size_t)touch_max + 2);
+  e->h_max_chunks = ch ? e->h_sort_cap / kTile + touch_max + 2 : 0;
+  dalloc(e->ch_sum, e->h_max_chunks);
+  dalloc(e->ch_pre, e->h_max_chunks);
+  dalloc(e->ch_stats, e->h_max_chunks * 5);
+  dalloc(e->ch_lastk, e->h_max_chunks);
+  dalloc(e->seg_T, touch_max);
+  dalloc(e->starts, (size_t)touch_max * capc);
+  dalloc(e->nc_new, touch_max);
+  dalloc(e->acc_xw, (size_t)touch_max * capc);
+  dalloc(e->acc_w, (size_t)touch_max * capc);
+  dalloc(e->h_err, 4); dzero(e->h_err, 4, st);
+  dalloc(e->hseen, ch); dzero(e->hseen, ch, st);
+  dalloc(e->hpend, ch); dzero(e->hpend, ch, st);
+  dalloc(e->hpv, (size_t)ch * e->temp_cap);
+  dalloc(e->hpw, (size_t)ch * e->temp_cap);
+  dalloc(e->h_ex, touch_max);
+  dalloc(e->h_hotflag, touch_max);
+  dalloc(e->h_hotcnt, touch_max);
+  dalloc(e->h_hotoff, (size_t)touch_max + 1);
+  dalloc(e->h_hotlist, touch_max);
+  dalloc(e->h_tl2, touch_max);
+
+  dalloc(e->smode, cs); dzero(e->smode, cs, st);
+  dalloc(e->sbase, cs); dzero(e->sbase, cs, st);
+  dalloc(e->snz, cs);
+  dalloc(e->slc, cs); dzero(e->slc, cs, st);
+  dalloc(e->slb, cs); dzero(e->slb, cs, st);
+  dalloc(e->slast, cs); dzero(e->slast, cs, st);
+  dalloc(e->stc, cs); dzero(e->stc, cs, st);
+  dalloc(e->stouch, cs); dzero(e->stouch, cs, st);
+  dalloc(e->stmp, (size_t)cs * kTmpCap);
+  dalloc(e->sarena, (size_t)cs * kArenaWords);
+  dalloc(e->sR0, cs ? R : 0);
+  dalloc(e->sR1, cs ? R : 0);
+  dalloc(e->s_bt, cs); dzero(e->s_bt, cs, st);
+  dalloc(e->s_pos, (size_t)cs + 1);
+  dalloc(e->s_tl, cs);
+  dalloc(e->s_cnt, 4);
+  dalloc(e->s_start, cs);
+  dalloc(e->s_end, cs);
+
+  // staging (device) and pinned host stage
+  DeviceBatch& d = e->dstage;
+  dalloc(d.c_slot, R); dalloc(d.c_val, R); dalloc(d.c_rate, R);
+  dalloc(d.g_slot, R); dalloc(d.g_val, R);
+  dalloc(d.h_slot, R); dalloc(d.h_val, R); dalloc(d.h_rate, R);
+  dalloc(d.s_slot, R); dalloc(d.s_off, R + 1); dalloc(d.s_bytes, e->max_member_bytes);
+  vn_stage& p = e->pstage;
+  p.capacity = R;
+  p.member_bytes_capacity = e->max_member_bytes;
+  halloc(p.counter_slot, R); halloc(p.counter_value, R); halloc(p.counter_rate, R);
+  halloc(p.gauge_slot, R); halloc(p.gauge_value, R);
+  halloc(p.histo_slot, R); halloc(p.histo_value, R); halloc(p.histo_rate, R);
+  halloc(p.set_slot, R); halloc(p.set_member_off, R + 1); halloc(p.set_member_bytes, e->max_member_bytes);
+
+  // flush outputs
+  dalloc(e->f_pos, (size_t)capmax + 1);
+  for (int c = 0; c < VN_NCLASS; c++) {
+    dalloc(e->f_list[c], e->cap[c]);
+    halloc(e->hf_list[c], e->cap[c]);
+  }
+  dalloc(e->f_cnt, 4);
+  dalloc(e->f_cval, cc); halloc(e->hf_cval, cc);
+  dalloc(e->f_gval, cg); halloc(e->hf_gval, cg);
+  dalloc(e->f_hstats, (size_t)ch * VN_HISTO_STATS); halloc(e->hf_hstats, (size_t)ch * VN_HISTO_STATS);
+  dalloc(e->f_hq, (size_t)ch * std::max<uint32_t>(1, e->cfg.n_percentiles));
+  halloc(e->hf_hq, (size_t)ch * std::max<uint32_t>(1, e->cfg.n_percentiles));
+  dalloc(e->f_sest, cs); halloc(e->hf_sest, cs);
+  dalloc(e->f_ssparse, cs); halloc(e->hf_ssparse, cs);
+  dalloc(e->d_pct, VN_MAX_PERCENTILES);
+  VN_HIP_CHECK(hipMemcpyAsync(e->d_pct, e->cfg.percentiles, sizeof(double) * VN_MAX_PERCENTILES,
+                              hipMemcpyHostToDevice, st));
+  halloc(e->hf_cnt, 16);
+
+  radix_scratch_reserve(e->rs, std::max<uint64_t>(e->h_sort_cap, cs ? R : 0));
+  init_state(e);
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+}
+
+void destroy_impl(vn_engine* e) {
+  if (e->st) (void)hipStreamSynchronize(e->st);
+  dfree(e->cval); dfree(e->ctouch); dfree(e->gseq); dfree(e->gval); dfree(e->gtouch);
+  dfree(e->hst); dfree(e->hncent); dfree(e->hcur); dfree(e->htouch);
+  for (int b = 0; b < 2; b++) { dfree(e->cmean[b]); dfree(e->cw[b]); }
+  dfree(e->h_bt); dfree(e->h_pos); dfree(e->h_tl); dfree(e->h_cnt); dfree(e->h_oldcnt); dfree(e->h_oldoff);
+  dfree(e->hA0); dfree(e->hB0); dfree(e->hA1); dfree(e->hB1); dfree(e->h_w); dfree(e->h_wk);
+  dfree(e->h_start); dfree(e->h_end); dfree(e->h_nch); dfree(e->h_chb);
+  dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->ch_lastk); dfree(e->seg_T);
+  dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
+  dfree(e->hseen); dfree(e->hpend); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
+  dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2);
+  dfree(e->smode); dfree(e->sbase); dfree(e->snz); dfree(e->slc); dfree(e->slb); dfree(e->slast); dfree(e->stc);
+  dfree(e->stouch); dfree(e->stmp); dfree(e->sarena); dfree(e->sR0); dfree(e->sR1); dfree(e->s_bt);
+  dfree(e->s_pos); dfree(e->s_tl); dfree(e->s_cnt); dfree(e->s_start); dfree(e->s_end);
+  DeviceBatch& d = e->dstage;
+  dfree(d.c_slot); dfree(d.c_val); dfree(d.c_rate); dfree(d.g_slot); dfree(d.g_val);
+  dfree(d.h_slot); dfree(d.h_val); dfree(d.h_rate); dfree(d.s_slot); dfree(d.s_off); dfree(d.s_bytes);
+  vn_stage& p = e->pstage;
+  hfree(p.counter_slot); hfree(p.counter_value); hfree(p.counter_rate); hfree(p.gauge_slot); hfree(p.gauge_value);
+  hfree(p.histo_slot); hfree(p.histo_value); hfree(p.histo_rate); hfree(p.set_slot); hfree(p.set_member_off);
+  hfree(p.set_member_bytes);
+  dfree(e->f_pos);
+  for (int c = 0; c < VN_NCLASS; c++) { dfree(e->f_list[c]); hfree(e->hf_list[c]); }
+  dfree(e->f_cnt); dfree(e->f_cval); hfree(e->hf_cval); dfree(e->f_gval); hfree(e->hf_gval);
+  dfree(e->f_hstats); hfree(e->hf_hstats); dfree(e->f_hq); hfree(e->hf_hq); dfree(e->f_sest); hfree(e->hf_sest);
+  dfree(e->f_ssparse); hfree(e->hf_ssparse); dfree(e->d_pct); hfree(e->hf_cnt);
+  radix_scratch_free(e->rs);
+  if (e->ss.partials) (void)hipFree(e->ss.partials);
+  for (auto ev : e->pool_storage) (void)hipEventDestroy(ev);
+  for (auto& ev : e->ev)
+    if (ev) (void)hipEventDestroy(ev);
+  if (e->st) (void)hipStreamDestroy(e->st);
+}
+
+void check_error_flags(vn_engine* e) {
+  uint32_t flags = 0;
+  VN_HIP_CHECK(hipMemcpy(&flags, e->h_err, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (flags & 1u) throw std::runtime_error("t-digest centroid tile overflow (compression too large for cap_cent)");
+  if (flags & 2u) throw std::runtime_error("HLL rebase invariant violated");
+}
+
+void ingest_device(vn_engine* e, const vn_batch* b) {
+  if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
+      b->n_set > e->max_records)
+    throw std::invalid_argument("batch larger than max_batch_records");
+  if ((b->n_counter && !e->cap[VN_COUNTER]) || (b->n_gauge && !e->cap[VN_GAUGE]) ||
+      (b->n_histo && !e->cap[VN_HISTO]) || (b->n_set && !e->cap[VN_SET]))
+    throw std::invalid_argument("records for a class with zero capacity");
+  hipStream_t st = e->st;
+  const bool tm = e->timing;
+  if (tm) {
+    e->pool.used = 0;
+    e->rstat_h = RadixStats{&e->pool, 0, 0};
+    e->rstat_s = RadixStats{&e->pool, 0, 0};
+    VN_HIP_CHECK(hipEventRecord(e->ev[0], st));
+  }
+  ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
+  if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[1], st));
+  ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
+  if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[2], st));
+  ingest_histos(e, b->n_histo, b->histo_slot, b->histo_value, b->histo_rate);
+  if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[3], st));
+  ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
+  if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[4], st));
+  e->processed += b->n_counter + b->n_gauge + b->n_histo + b->n_set;
+}
+
+template <class T>
+void h2d(T* dst, const T* src, uint64_t n, hipStream_t st) {
+  if (n) VN_HIP_CHECK(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, st));
+}
+
+void ingest_host(vn_engine* e, const vn_batch* b) {
+  if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
+      b->n_set > e->max_records)
+    throw std::invalid_argument("batch larger than max_batch_records");
+  check_slots_host(b->counter_slot, b->n_counter, e->cap[VN_COUNTER], "counter");
+  check_slots_host(b->gauge_slot, b->n_gauge, e->cap[VN_GAUGE], "gauge");
+  check_slots_host(b->histo_slot, b->n_histo, e->cap[VN_HISTO], "histo");
+  check_slots_host(b->set_slot, b->n_set, e->cap[VN_SET], "set");
+  for (uint64_t i = 0; i < b->n_histo; i++) {
+    double v = b->histo_value[i];
+    float r = b->histo_rate[i];
+    if (v != v || v - v != 0) throw std::invalid_argument("invalid value added");  // merging_digest.go:98-100
+    if (!(r > 0.0f && r <= 1.0f)) throw std::invalid_argument("sample rate must be >0 and <=1");
+  }
+  for (uint64_t i = 0; i < b->n_counter; i++)
+    if (!(b->counter_rate[i] > 0.0f && b->counter_rate[i] <= 1.0f))
+      throw std::invalid_argument("sample rate must be >0 and <=1");
+  hipStream_t st = e->st;
+  DeviceBatch& d = e->dstage;
+  vn_batch db{};
+  db.n_counter = b->n_counter;
+  h2d(d.c_slot, b->counter_slot, b->n_counter, st);
+  h2d(d.c_val, b->counter_value, b->n_counter, st);
+  h2d(d.c_rate, b->counter_rate, b->n_counter, st);
+  db.counter_slot = d.c_slot; db.counter_value = d.c_val; db.counter_rate = d.c_rate;
+  db.n_gauge = b->n_gauge;
+  h2d(d.g_slot, b->gauge_slot, b->n_gauge, st);
+  h2d(d.g_val, b->gauge_value, b->n_gauge, st);
+  db.gauge_slot = d.g_slot; db.gauge_value = d.g_val;
+  db.n_histo = b->n_histo;
+  h2d(d.h_slot, b->histo_slot, b->n_histo, st);
+  h2d(d.h_val, b->histo_value, b->n_histo, st);
+  h2d(d.h_rate, b->histo_rate, b->n_histo, st);
+  db.histo_slot = d.h_slot; db.histo_value = d.h_val; db.histo_rate = d.h_rate;
+  db.n_set = b->n_set;
+  uint64_t* dhash = nullptr;
+  if (b->n_set) {
+    h2d(d.s_slot, b->set_slot, b->n_set, st);
+    db.set_slot = d.s_slot;
+    if (b->set_hash) {
+      // hashes travel in the (u64-aligned) member byte staging area
+      if (b->n_set * 8 > e->max_member_bytes) throw std::invalid_argument("set hash batch exceeds staging");
+      dhash = reinterpret_cast<uint64_t*>(d.s_bytes);
+      h2d(dhash, b->set_hash, b->n_set, st);
+      db.set_hash = dhash;
+    } else {
+      uint64_t nb = b->set_member_off[b->n_set];
+      if (nb > e->max_member_bytes) throw std::invalid_argument("member bytes exceed max_batch_member_bytes");
+      h2d(d.s_off, b->set_member_off, b->n_set + 1, st);
+      h2d(d.s_bytes, b->set_member_bytes, nb, st);
+      db.set_member_off = d.s_off;
+      db.set_member_bytes = d.s_bytes;
+    }
+  }
+  ingest_device(e, &db);
+}
+
+}  // namespace
+
+extern "C" {
+
+int vn_abi_version(void) { return VN_ABI_VERSION; }
+
+int vn_engine_create(const vn_config* cfg, vn_engine** out) {
+  if (!cfg || !out) return VN_EINVAL;
+  *out = nullptr;
+  vn_engine* e = new vn_engine();
+  e->cfg = *cfg;
+  e->device = cfg->device;
+  for (int c = 0; c < VN_NCLASS; c++) {
+    e->cap[c] = cfg->capacity[c];
+    e->slot_bits[c] = bits_for(std::max<uint32_t>(1, cfg->capacity[c]));
+  }
+  if (e->cfg.compression <= 0) e->cfg.compression = 100.0;
+  if (e->cfg.n_percentiles > VN_MAX_PERCENTILES) {
+    delete e;
+    return VN_EINVAL;
+  }
+  uint32_t need = (uint32_t)(2.0 * e->cfg.compression) + 4;
+  e->cap_cent = ((need + 63) / 64) * 64;
+  if (e->cap_cent < 64) e->cap_cent = 64;
+  if (e->cap_cent > 2048 || (uint64_t)e->cap[VN_HISTO] * e->cap_cent >= (1ull << 31)) {
+    delete e;
+    return VN_EINVAL;
+  }
+  e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 32768u;
+  e->temp_cap = temp_buffer_cap(e->cfg.compression);
+  e->max_records = cfg->max_batch_records ? cfg->max_batch_records : (1u << 20);
+  e->max_member_bytes = cfg->max_batch_member_bytes ? cfg->max_batch_member_bytes : e->max_records * 16;
+  if (e->max_member_bytes < e->max_records * 8) e->max_member_bytes = e->max_records * 8;
+  int rc = guarded(e, [&] { create_impl(e); });
+  if (rc != VN_OK) {
+    destroy_impl(e);
+    *out = e;  // caller may read vn_last_error, then destroy
+    return rc;
+  }
+  *out = e;
+  return VN_OK;
+}
+
+void vn_engine_destroy(vn_engine* e) {
+  if (!e) return;
+  destroy_impl(e);
+  delete e;
+}
+
+const char* vn_last_error(const vn_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int vn_stage_acquire(vn_engine* e, vn_stage* out) {
+  if (!e || !out) return VN_EINVAL;
+  *out = e->pstage;
+  return VN_OK;
+}
+
+int vn_submit(vn_engine* e, const vn_batch_counts* c) {
+  if (!e || !c) return VN_EINVAL;
+  const vn_stage& p = e->pstage;
+  vn_batch b{};
+  b.n_counter = c->n_counter; b.counter_slot = p.counter_slot; b.counter_value = p.counter_value;
+  b.counter_rate = p.counter_rate;
+  b.n_gauge = c->n_gauge; b.gauge_slot = p.gauge_slot; b.gauge_value = p.gauge_value;
+  b.n_histo = c->n_histo; b.histo_slot = p.histo_slot; b.histo_value = p.histo_value; b.histo_rate = p.histo_rate;
+  b.n_set = c->n_set; b.set_slot = p.set_slot; b.set_member_off = p.set_member_off;
+  b.set_member_bytes = p.set_member_bytes;
+  return guarded(e, [&] { ingest_host(e, &b); });
+}
+
+int vn_ingest_host(vn_engine* e, const vn_batch* b) {
+  if (!e || !b) return VN_EINVAL;
+  return guarded(e, [&] { ingest_host(e, b); });
+}
+
+int vn_ingest(vn_engine* e, const vn_batch* b) {
+  if (!e || !b) return VN_EINVAL;
+  return guarded(e, [&] { ingest_device(e, b); });
+}
+
+int vn_import_counters(vn_engine* e, const uint32_t* slot, const int64_t* value, uint64_t n) {
+  if (!e) return VN_EINVAL;
+  return guarded(e, [&] {
+    if (n > e->max_records) throw std::invalid_argument("import batch too large");
+    check_slots_host(slot, n, e->cap[VN_COUNTER], "counter");
+    h2d(e->dstage.c_slot, slot, n, e->st);
+    h2d(reinterpret_cast<int64_t*>(e->dstage.c_val), value, n, e->st);
+    import_counters(e, n, e->dstage.c_slot, reinterpret_cast<const int64_t*>(e->dstage.c_val));
+    e->imported += n;
+  });
+}
+
+int vn_import_gauges(vn_engine* e, const uint32_t* slot, const double* value, uint64_t n) {
+  if (!e) return VN_EINVAL;
+  return guarded(e, [&] {
+    if (n > e->max_records) throw std::invalid_argument("import batch too large");
+    check_slots_host(slot, n, e->cap[VN_GAUGE], "gauge");
+    h2d(e->dstage.g_slot, slot, n, e->st);
+    h2d(e->dstage.g_val, value, n, e->st);
+    ingest_gauges(e, n, e->dstage.g_slot, e->dstage.g_val);
+    e->imported += n;
+  });
+}
+
+int vn_flush(vn_engine* e, vn_flush_result* out) {
+  if (!e || !out) return VN_EINVAL;
+  return guarded(e, [&] {
+    if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[5], e->st));
+    flush_all(e, out);
+    if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[6], e->st));
+    check_error_flags(e);
+    if (e->timing) {
+      VN_HIP_CHECK(hipEventSynchronize(e->ev[6]));
+      vn_timing& t = e->last;
+      t = vn_timing{};
+      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_counter, e->ev[0], e->ev[1]));
+      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_gauge, e->ev[1], e->ev[2]));
+      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_histo, e->ev[2], e->ev[3]));
+      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_set, e->ev[3], e->ev[4]));
+      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_flush, e->ev[5], e->ev[6]));
+      t.sort_passes_histo = e->rstat_h.launches;
+      t.sort_passes_set = e->rstat_s.launches;
+      float tot = 0;
+      for (int i = 0; i + 1 < e->pool.used; i += 2) {
+        float ms = 0;
+        VN_HIP_CHECK(hipEventElapsedTime(&ms, e->pool.ev[i], e->pool.ev[i + 1]));
+        tot += ms;
+      }
+      t.ms_radix_scatter_total = tot;
+      t.radix_scatter_launches = e->rstat_h.launches + e->rstat_s.launches;
+      t.radix_scatter_bytes = e->rstat_h.bytes + e->rstat_s.bytes;
+    }
+  });
+}
+
+int vn_sync(vn_engine* e) {
+  if (!e) return VN_EINVAL;
+  return guarded(e, [&] {
+    VN_HIP_CHECK(hipStreamSynchronize(e->st));
+    check_error_flags(e);
+  });
+}
+
+int vn_timing_enable(vn_engine* e, int enable) {
+  if (!e) return VN_EINVAL;
+  return guarded(e, [&] {
+    e->timing = enable != 0;
+    if (e->timing && !e->ev[0]) {
+      for (auto& ev : e->ev) VN_HIP_CHECK(hipEventCreate(&ev));
+      e->pool_storage.resize(256);
+      for (auto& ev : e->pool_storage) VN_HIP_CHECK(hipEventCreate(&ev));
+      e->pool.ev = e->pool_storage.data();
+      e->pool.cap = (int)e->pool_storage.size();
+    }
+  });
+}
+
+int vn_get_timing(vn_engine* e, vn_timing* out) {
+  if (!e || !out) return VN_EINVAL;
+  *out = e->last;
+  return VN_OK;
+}
+
+int vn_read_histo(vn_engine* e, uint32_t slot, double* means, double* weights, uint32_t cap, uint32_t* n_centroids,
+                  double* stats) {
+  if (!e || slot >= e->cap[VN_HISTO]) return VN_EINVAL;
+  return guarded(e, [&] {
+    VN_HIP_CHECK(hipStreamSynchronize(e->st));
+    uint32_t nc = 0;
+    uint8_t cur = 0;
+    VN_HIP_CHECK(hipMemcpy(&nc, e->hncent + slot, 4, hipMemcpyDeviceToHost));
+    VN_HIP_CHECK(hipMemcpy(&cur, e->hcur + slot, 1, hipMemcpyDeviceToHost));
+    if (n_centroids) *n_centroids = nc;
+    uint32_t m = std::min(nc, cap);
+    size_t off = (size_t)slot * e->cap_cent;
+    if (means && m) VN_HIP_CHECK(hipMemcpy(means, e->cmean[cur] + off, m * 8, hipMemcpyDeviceToHost));
+    if (weights && m) VN_HIP_CHECK(hipMemcpy(weights, e->cw[cur] + off, m * 8, hipMemcpyDeviceToHost));
+    if (stats)
+      VN_HIP_CHECK(hipMemcpy(stats, e->hst + (size_t)slot * VN_HISTO_STATS, VN_HISTO_STATS * 8, hipMemcpyDeviceToHost));
+  });
+}
+
+int vn_read_set(vn_engine* e, uint32_t slot, vn_set_state* st, uint32_t* list_codes, uint32_t list_cap,
+                uint32_t* tmp_codes, uint32_t tmp_cap, uint8_t* registers) {
+  if (!e || slot >= e->cap[VN_SET] || !st) return VN_EINVAL;
+  return guarded(e, [&] {
+    VN_HIP_CHECK(hipStreamSynchronize(e->st));
+    uint32_t touch = 0;
+    VN_HIP_CHECK(hipMemcpy(&touch, e->stouch + slot, 4, hipMemcpyDeviceToHost));
+    uint8_t mode = 0, b = 0;
+    VN_HIP_CHECK(hipMemcpy(&mode, e->smode + slot, 1, hipMemcpyDeviceToHost));
+    VN_HIP_CHECK(hipMemcpy(&b, e->sbase + slot, 1, hipMemcpyDeviceToHost));
+    st->touched = touch != 0;
+    st->sparse = mode == 0;
+    st->b = b;
+    VN_HIP_CHECK(hipMemcpy(&st->nz, e->snz + slot, 4, hipMemcpyDeviceToHost));
+    VN_HIP_CHECK(hipMemcpy(&st->list_count, e->slc + slot, 4, hipMemcpyDeviceToHost));
+    VN_HIP_CHECK(hipMemcpy(&st->list_bytes, e->slb + slot, 4, hipMemcpyDeviceToHost));
+    VN_HIP_CHECK(hipMemcpy(&st->list_last, e->slast + slot, 4, hipMemcpyDeviceToHost));
+    VN_HIP_CHECK(hipMemcpy(&st->tmp_count, e->stc + slot, 4, hipMemcpyDeviceToHost));
+    const uint32_t* ar = e->sarena + (size_t)slot * kArenaWords;
+    if (mode == 0) {
+      uint32_t m = std::min(st->list_count, list_cap);
+      if (list_codes && m) VN_HIP_CHECK(hipMemcpy(list_codes, ar, m * 4, hipMemcpyDeviceToHost));
+      uint32_t mt = std::min(st->tmp_count, tmp_cap);
+      if (tmp_codes && mt)
+        VN_HIP_CHECK(hipMemcpy(tmp_codes, e->stmp + (size_t)slot * kTmpCap, mt * 4, hipMemcpyDeviceToHost));
+    } else if (registers) {
+      VN_HIP_CHECK(hipMemcpy(registers, ar, kHllM, hipMemcpyDeviceToHost));
+    }
+  });
+}
+
+int vn_metro64(int device, const uint8_t* bytes, const uint32_t* off, uint64_t n, uint64_t seed, uint64_t* out) {
+  try {
+    VN_HIP_CHECK(hipSetDevice(device));
+    if (n == 0) return VN_OK;
+    uint64_t nb = off[n];
+    uint8_t* db = nullptr;
+    uint32_t* doff = nullptr;
+    uint64_t* dout = nullptr;
+    VN_HIP_CHECK(hipMalloc(&db, nb ? nb : 1));
+    VN_HIP_CHECK(hipMalloc(&doff, (n + 1) * 4));
+    VN_HIP_CHECK(hipMalloc(&dout, n * 8));
+    if (nb) VN_HIP_CHECK(hipMemcpy(db, bytes, nb, hipMemcpyHostToDevice));
+    VN_HIP_CHECK(hipMemcpy(doff, off, (n + 1) * 4, hipMemcpyHostToDevice));
+    metro64_batch(db, doff, n, seed, dout, nullptr);
+    VN_HIP_CHECK(hipMemcpy(out, dout, n * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(db);
+    (void)hipFree(doff);
+    (void)hipFree(dout);
+    return VN_OK;
+  } catch (const HipError&) {
+    return VN_EHIP;
+  }
+}
+
+int vn_device_alloc(int device, uint64_t bytes, void** out) {
+  if (hipSetDevice(device) != hipSuccess) return VN_EHIP;
+  return hipMalloc(out, bytes ? bytes : 1) == hipSuccess ? VN_OK : VN_ENOMEM;
+}
+int vn_device_free(void* p) { return hipFree(p) == hipSuccess ? VN_OK : VN_EHIP; }
+int vn_copy_to_device(int device, void* dst, const void* src, uint64_t bytes) {
+  if (hipSetDevice(device) != hipSuccess) return VN_EHIP;
+  return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? VN_OK : VN_EHIP;
+}
+int vn_device_count(int* n) { return hipGetDeviceCount(n) == hipSuccess ? VN_OK : VN_EHIP; }
+
+}  // extern "C"

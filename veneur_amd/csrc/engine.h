@@ -1,0 +1,153 @@
+// engine.h -- device state of one engine (one GPU, one veneur worker group).
+//
+// HBM layout (per class, indexed by the class-local slot the host interned):
+//   counters  cval[i64], ctouch[u32]
+//   gauges    gseq[u64] (arrival seq+1 of the winning write, 0 = untouched), gval[f64], gtouch
+//   histos    hst[8 x f64] = LocalWeight, LocalMin, LocalMax, LocalSum, LocalReciprocalSum,
+//             digest min, digest max, digest total weight; centroid tiles cmean/cw[2][slot][cap_cent]
+//             (double-buffered: an ingest writes the other buffer and flips hcur)
+//   sets      header SoA (mode, b, nz, list count/bytes/last, tmp count), tmpSet codes [slot][164],
+//             arena [slot][16640 u32]: the sorted unique sparse codes, or 16384 one-byte registers
+#pragma once
+#include <string>
+#include <vector>
+
+#include "../../include/veneur_amd.h"
+#include "primitives.h"
+
+namespace vn {
+
+constexpr uint32_t kArenaWords = 16640;  // == kHllListCap
+constexpr uint32_t kTmpCap = 164;
+
+struct DeviceBatch {  // device-resident staging for one ingest call
+  uint32_t *c_slot, *g_slot, *h_slot, *s_slot, *s_off;
+  double *c_val, *g_val, *h_val;
+  float *c_rate, *h_rate;
+  uint8_t* s_bytes;
+};
+
+}  // namespace vn
+
+struct vn_engine {
+  vn_config cfg{};
+  int device = 0;
+  hipStream_t st = nullptr;
+  std::string err;
+  uint32_t cap[VN_NCLASS] = {0, 0, 0, 0};
+  uint32_t cap_cent = 256;      // centroids per histo slot (>= 2*compression + 4)
+  int slot_bits[VN_NCLASS] = {1, 1, 1, 1};
+  uint64_t max_records = 0, max_member_bytes = 0;
+
+  // ---- counters
+  int64_t* cval = nullptr;
+  uint32_t* ctouch = nullptr;
+  // ---- gauges
+  uint64_t* gseq = nullptr;
+  double* gval = nullptr;
+  uint32_t* gtouch = nullptr;
+  uint64_t seq_base = 0;
+  // ---- histos
+  double* hst = nullptr;
+  uint32_t* hncent = nullptr;
+  uint8_t* hcur = nullptr;
+  uint32_t* htouch = nullptr;
+  double* cmean[2] = {nullptr, nullptr};
+  double* cw[2] = {nullptr, nullptr};
+  // histo ingest scratch
+  uint32_t* h_bt = nullptr;      // batch-touched flags
+  uint32_t* h_pos = nullptr;     // scan of flags (cap+1)
+  uint32_t* h_tl = nullptr;      // touched list
+  uint32_t* h_cnt = nullptr;     // device counters [8]
+  uint32_t* h_oldcnt = nullptr;  // per touched slot: existing centroids (cap)
+  uint32_t* h_oldoff = nullptr;  // scan (cap+1)
+  uint64_t *hA0 = nullptr, *hB0 = nullptr, *hA1 = nullptr, *hB1 = nullptr;
+  uint64_t h_sort_cap = 0;
+  double* h_w = nullptr;         // per record weight
+  double* h_wk = nullptr;        // per record local prefix weight, then k-index
+  uint32_t* h_start = nullptr;   // per slot segment start / end in the sorted batch
+  uint32_t* h_end = nullptr;
+  uint32_t* h_nch = nullptr;     // per touched segment: chunks
+  uint32_t* h_chb = nullptr;     // chunk base (cap+1)
+  uint64_t h_max_chunks = 0;
+  double* ch_sum = nullptr;
+  double* ch_pre = nullptr;
+  double* ch_stats = nullptr;    // [chunk][5]
+  double* ch_lastk = nullptr;
+  double* seg_T = nullptr;       // per touched seg
+  uint32_t* starts = nullptr;    // [touched][cap_cent]
+  uint32_t* nc_new = nullptr;
+  double* acc_xw = nullptr;      // [touched][cap_cent]
+  double* acc_w = nullptr;
+  uint32_t* h_err = nullptr;     // device error flags
+  // exact (Go-incremental) replay state and batch split
+  uint32_t exact_threshold = 32768;
+  uint32_t temp_cap = 42;        // estimateTempBuffer(compression)
+  uint32_t* hseen = nullptr;     // samples seen this window per slot
+  uint32_t* hpend = nullptr;     // pending temps per slot
+  double* hpv = nullptr;         // [slot][temp_cap] pending temp means
+  double* hpw = nullptr;         // [slot][temp_cap] pending temp weights
+  uint32_t* h_ex = nullptr;      // per touched key: samples replayed exactly
+  uint32_t* h_hotflag = nullptr;
+  uint32_t* h_hotcnt = nullptr;
+  uint32_t* h_hotoff = nullptr;
+  uint32_t* h_hotlist = nullptr;
+  uint32_t* h_tl2 = nullptr;     // slots of hot keys
+
+  // ---- sets
+  uint8_t* smode = nullptr;      // 0 sparse, 1 dense
+  uint8_t* sbase = nullptr;      // b
+  uint32_t* snz = nullptr;
+  uint32_t* slc = nullptr;
+  uint32_t* slb = nullptr;
+  uint32_t* slast = nullptr;
+  uint32_t* stc = nullptr;
+  uint32_t* stouch = nullptr;
+  uint32_t* stmp = nullptr;      // [cap][164]
+  uint32_t* sarena = nullptr;    // [cap][kArenaWords]
+  // set ingest scratch
+  uint64_t *sR0 = nullptr, *sR1 = nullptr;
+  uint32_t* s_bt = nullptr;
+  uint32_t* s_pos = nullptr;
+  uint32_t* s_tl = nullptr;
+  uint32_t* s_cnt = nullptr;
+  uint32_t* s_start = nullptr;
+  uint32_t* s_end = nullptr;
+
+  // ---- staging
+  vn::DeviceBatch dstage{};
+  vn_stage pstage{};             // pinned host views
+  // ---- flush outputs
+  uint32_t* f_pos = nullptr;     // scan scratch (max cap + 1)
+  uint32_t* f_list[VN_NCLASS] = {nullptr, nullptr, nullptr, nullptr};
+  uint32_t* f_cnt = nullptr;     // [4]
+  int64_t* f_cval = nullptr;
+  double* f_gval = nullptr;
+  double* f_hstats = nullptr;
+  double* f_hq = nullptr;
+  uint64_t* f_sest = nullptr;
+  uint8_t* f_ssparse = nullptr;
+  double* d_pct = nullptr;
+  // pinned host copies of the flush result
+  uint32_t* hf_list[VN_NCLASS] = {nullptr, nullptr, nullptr, nullptr};
+  int64_t* hf_cval = nullptr;
+  double* hf_gval = nullptr;
+  double* hf_hstats = nullptr;
+  double* hf_hq = nullptr;
+  uint64_t* hf_sest = nullptr;
+  uint8_t* hf_ssparse = nullptr;
+  uint32_t* hf_cnt = nullptr;    // pinned [8]
+
+  uint64_t processed = 0, imported = 0;
+
+  vn::RadixScratch rs;
+  vn::ScanScratch ss;
+
+  // ---- timing
+  bool timing = false;
+  hipEvent_t ev[16] = {};
+  vn::EventPool pool;
+  std::vector<hipEvent_t> pool_storage;
+  vn_timing last{};
+  vn::RadixStats rstat_h, rstat_s;
+};

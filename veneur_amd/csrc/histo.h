@@ -1,0 +1,39 @@
+// histo.h -- shared declarations of the t-digest (Histo) kernels.
+#pragma once
+#include "kernels.h"
+
+namespace vn {
+
+struct ExactCtx {
+  uint32_t nkeys;
+  const uint32_t* keys;      // slot of each processed key
+  const uint32_t* start;     // per slot: first record of its segment (arrival order)
+  const uint32_t* nex;       // per processed key: records to replay exactly (nullptr: none)
+  const uint32_t* hot;       // per processed key: 1 -> merge pending temps after the exact part
+  const uint64_t* A;         // raw float64 bits of the value
+  const uint64_t* B;         // slot<<32 | float32 bits of the sample rate
+  double delta;
+  uint32_t capc, tcap;
+  double* hst;
+  uint32_t* hncent;
+  const uint8_t* hcur;
+  double* cm0;
+  double* cm1;
+  double* cw0;
+  double* cw1;
+  uint32_t* hpend;
+  double* hpv;
+  double* hpw;
+  uint32_t* err;
+  int flush_mode;            // 1: only merge pending temps (Quantile's mergeAllTemps)
+};
+
+size_t exact_smem_bytes(uint32_t capc, uint32_t tcap);
+void launch_histo_exact(const ExactCtx& x, hipStream_t st);
+// estimateTempBuffer (merging_digest.go:87-93)
+inline uint32_t temp_buffer_cap(double compression) {
+  double c = compression < 20 ? 20 : (compression > 925 ? 925 : compression);
+  return (uint32_t)(int)(7.5 + 0.37 * c - 2e-4 * c * c);
+}
+
+}  // namespace vn

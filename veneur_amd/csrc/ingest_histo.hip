@@ -1,0 +1,646 @@
+// ingest_histo.hip -- Histo.Sample + MergingDigest for one ingest batch.
+//
+// Reference semantics (tdigest/merging_digest.go): samples are Add()ed to a temp list;
+// mergeAllTemps (121-205) sorts the temps and two-way merges them with the main
+// centroids by mean, feeding every element to mergeOne (210-236), which starts a new
+// centroid when  k(W_incl/T) - k(W_start/T) > 1,  k(q) = delta*(asin(2q-1)/pi + 0.5),
+// and otherwise folds the element into the last centroid with Welford's update.
+//
+// MI355X formulation, per batch:
+//   1. records -> (ordered(value), slot<<32 | tag) pairs; the key's existing centroids are
+//      appended as elements tagged with their centroid index (they are merged exactly like
+//      temps are merged with main in the reference);
+//   2. stable LSD radix sort by (slot, value)  -> one contiguous, value-sorted segment per key;
+//   3. per 4096-element chunk: weights, local inclusive prefix, Histo local statistics;
+//   4. per segment: chunk prefix (exact for veneur's integer weights), totals;
+//   5. per element: k = indexEstimate(W_incl / T);
+//   6. per segment: the greedy centroid chain -- each next start is the first element whose
+//      k exceeds the current start's k(W_excl/T) by more than 1 (binary search on the
+//      monotone k array, chunk-coarse index in LDS);
+//   7. centroid sums: one-chunk segments run the reference's Welford update per centroid
+//      (thread per centroid); larger segments reduce sum(x*w), sum(w) per centroid.
+// The greedy boundary rule is the reference's; the batch (rather than 42-sample chunks)
+// is the merge unit, which is why t-digest parity is judged by rank error.
+#include "histo.h"
+
+namespace vn {
+
+constexpr uint32_t kMaxCent = 2048;  // supports compression <= ~1000
+
+struct HistoCtx {
+  uint32_t ntouched;
+  uint32_t capc;
+  double delta;
+  const uint32_t* tl;
+  const uint32_t* start;
+  const uint32_t* end;
+  const uint32_t* chb;
+  const uint64_t* A;
+  const uint64_t* B;
+  double* w;
+  double* wk;
+  double* ch_sum;
+  double* ch_pre;
+  double* ch_stats;
+  double* ch_lastk;
+  double* seg_T;
+  uint32_t* starts;
+  uint32_t* nc_new;
+  double* acc_xw;
+  double* acc_w;
+  double* hst;
+  uint32_t* hncent;
+  uint8_t* hcur;
+  double* cm0;
+  double* cm1;
+  double* cw0;
+  double* cw1;
+  uint32_t* err;
+};
+
+__global__ void k_histo_append_old(const uint32_t* __restrict__ tl, const uint32_t* __restrict__ oldoff,
+                                   const uint32_t* __restrict__ hncent, const uint8_t* __restrict__ hcur,
+                                   const double* __restrict__ cm0, const double* __restrict__ cm1, uint32_t capc,
+                                   uint64_t n, uint64_t* __restrict__ A, uint64_t* __restrict__ B) {
+  uint32_t k = blockIdx.x;
+  uint32_t s = tl[k];
+  uint32_t nc = hncent[s];
+  const double* cm = hcur[s] ? cm1 : cm0;
+  uint64_t base = n + oldoff[k];
+  for (uint32_t j = threadIdx.x; j < nc; j += blockDim.x) {
+    uint32_t ref = s * capc + j;
+    A[base + j] = ordered_bits(cm[ref]);
+    B[base + j] = ((uint64_t)s << 32) | 0x80000000ull | (uint64_t)ref;
+  }
+}
+
+// segment [start, end) of every slot present in a sorted (slot<<32 | x) array
+__global__ void k_seg_mark(uint64_t n, const uint64_t* __restrict__ B, uint32_t* __restrict__ start,
+                           uint32_t* __restrict__ end) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = (uint32_t)(B[i] >> 32);
+  if (i == 0 || (uint32_t)(B[i - 1] >> 32) != s) start[s] = (uint32_t)i;
+  if (i == n - 1 || (uint32_t)(B[i + 1] >> 32) != s) end[s] = (uint32_t)(i + 1);
+}
+
+__global__ void k_seg_nch(uint32_t ntouched, const uint32_t* __restrict__ tl, const uint32_t* __restrict__ start,
+                          const uint32_t* __restrict__ end, uint32_t* __restrict__ nch) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= ntouched) return;
+  uint32_t s = tl[k];
+  nch[k] = (end[s] - start[s] + kTile - 1) / kTile;
+}
+
+__device__ __forceinline__ uint32_t find_seg(const uint32_t* chb, uint32_t ntouched, uint32_t c) {
+  uint32_t lo = 0, hi = ntouched;
+  while (hi - lo > 1) {
+    uint32_t mid = (lo + hi) >> 1;
+    if (chb[mid] <= c) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+struct ChunkRange {
+  uint32_t k, s, seg_lo, seg_hi, lo, hi, nch;
+};
+__device__ __forceinline__ bool chunk_range(const HistoCtx& x, ChunkRange& r, uint32_t* s_k) {
+  uint32_t c = blockIdx.x;
+  if (c >= x.chb[x.ntouched]) return false;
+  if (threadIdx.x == 0) *s_k = find_seg(x.chb, x.ntouched, c);
+  __syncthreads();
+  r.k = *s_k;
+  r.s = x.tl[r.k];
+  r.seg_lo = x.start[r.s];
+  r.seg_hi = x.end[r.s];
+  r.lo = r.seg_lo + (c - x.chb[r.k]) * kTile;
+  r.hi = min(r.seg_hi, r.lo + (uint32_t)kTile);
+  r.nch = x.chb[r.k + 1] - x.chb[r.k];
+  return true;
+}
+
+// 3. weights, local inclusive prefix, local statistics of the samples
+__global__ __launch_bounds__(kBlock) void k_chunk_prep(HistoCtx x) {
+  __shared__ uint32_t s_k;
+  __shared__ double s_tmp[4];
+  ChunkRange r;
+  if (!chunk_range(x, r, &s_k)) return;
+  const uint32_t c = blockIdx.x, t = threadIdx.x;
+  const double* cwo = x.hcur[r.s] ? x.cw1 : x.cw0;
+  double wv[kItems];
+  double run = 0.0, sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
+  const uint32_t base = r.lo + t * kItems;
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    uint32_t i = base + j;
+    wv[j] = 0.0;
+    if (i < r.hi) {
+      uint64_t b = x.B[i];
+      uint32_t tag = (uint32_t)b;
+      double xv = from_ordered_bits(x.A[i]);
+      double wt;
+      if (tag & 0x80000000u) {
+        wt = cwo[tag & 0x7fffffffu];
+      } else {
+        wt = (double)(1.0f / __uint_as_float(tag));  // float64(1/sampleRate) in float32
+        sw = dadd(sw, wt);
+        mn = min_go(mn, xv);
+        mx = max_go(mx, xv);
+        sxw = dadd(sxw, dmul(xv, wt));
+        srw = dadd(srw, dmul(ddiv(1.0, xv), wt));
+      }
+      wv[j] = wt;
+      run = dadd(run, wt);
+      x.w[i] = wt;
+    }
+  }
+  double tot;
+  double acc = block_excl_scan_d(run, s_tmp, tot);
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    uint32_t i = base + j;
+    if (i < r.hi) {
+      acc = dadd(acc, wv[j]);
+      x.wk[i] = acc;
+    }
+  }
+  sw = block_allreduce(sw, s_tmp, SumOp());
+  sxw = block_allreduce(sxw, s_tmp, SumOp());
+  srw = block_allreduce(srw, s_tmp, SumOp());
+  mn = block_allreduce(mn, s_tmp, MinGoOp());
+  mx = block_allreduce(mx, s_tmp, MaxGoOp());
+  if (t == 0) {
+    x.ch_sum[c] = tot;
+    double* st = x.ch_stats + (uint64_t)c * 5;
+    st[0] = sw; st[1] = mn; st[2] = mx; st[3] = sxw; st[4] = srw;
+  }
+}
+
+// 4. per segment: chunk prefix, totals, Histo local statistics into the state
+__global__ __launch_bounds__(kBlock) void k_seg_scan(HistoCtx x) {
+  __shared__ double s_tmp[4];
+  const uint32_t k = blockIdx.x, t = threadIdx.x;
+  const uint32_t s = x.tl[k];
+  const uint32_t cb = x.chb[k], ce = x.chb[k + 1];
+  double carry = 0.0, sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
+  for (uint32_t base = cb; base < ce; base += kBlock) {
+    uint32_t c = base + t;
+    double v = c < ce ? x.ch_sum[c] : 0.0;
+    double tot;
+    double ex = block_excl_scan_d(v, s_tmp, tot);
+    if (c < ce) {
+      x.ch_pre[c] = dadd(carry, ex);
+      const double* st = x.ch_stats + (uint64_t)c * 5;
+      sw = dadd(sw, st[0]);
+      mn = min_go(mn, st[1]);
+      mx = max_go(mx, st[2]);
+      sxw = dadd(sxw, st[3]);
+      srw = dadd(srw, st[4]);
+    }
+    carry = dadd(carry, tot);
+  }
+  sw = block_allreduce(sw, s_tmp, SumOp());
+  sxw = block_allreduce(sxw, s_tmp, SumOp());
+  srw = block_allreduce(srw, s_tmp, SumOp());
+  mn = block_allreduce(mn, s_tmp, MinGoOp());
+  mx = block_allreduce(mx, s_tmp, MaxGoOp());
+  if (t == 0) {
+    double* h = x.hst + (uint64_t)s * VN_HISTO_STATS;
+    h[0] = dadd(h[0], sw);
+    h[1] = min_go(h[1], mn);
+    h[2] = max_go(h[2], mx);
+    h[3] = dadd(h[3], sxw);
+    h[4] = dadd(h[4], srw);
+    h[5] = min_go(h[5], mn);
+    h[6] = max_go(h[6], mx);
+    h[7] = carry;
+    x.seg_T[k] = carry;
+  }
+}
+
+// 5. k-index of every element
+__global__ __launch_bounds__(kBlock) void k_chunk_kin(HistoCtx x) {
+  __shared__ uint32_t s_k;
+  ChunkRange r;
+  if (!chunk_range(x, r, &s_k)) return;
+  const uint32_t c = blockIdx.x;
+  const double pre = x.ch_pre[c];
+  const double T = x.seg_T[r.k];
+  for (uint32_t i = r.lo + threadIdx.x; i < r.hi; i += kBlock) {
+    double W = dadd(pre, x.wk[i]);
+    double kv = index_estimate(x.delta, ddiv(W, T));
+    x.wk[i] = kv;
+    if (i == r.hi - 1) x.ch_lastk[c] = kv;
+  }
+}
+
+// 6 (+7 for one-chunk segments). Greedy centroid chain of mergeOne.
+__global__ __launch_bounds__(kBlock) void k_chain(HistoCtx x) {
+  __shared__ double s_kv[kTile];
+  __shared__ uint32_t s_st[kMaxCent + 1];
+  __shared__ uint32_t s_nc, s_pos, s_q, s_g, s_next, s_done;
+  __shared__ double s_base;
+  const uint32_t k = blockIdx.x, t = threadIdx.x;
+  const uint32_t s = x.tl[k];
+  const uint32_t lo = x.start[s], n = x.end[s] - lo;
+  const uint32_t cb = x.chb[k], nch = x.chb[k + 1] - cb;
+  const double base0 = index_estimate(x.delta, 0.0);
+  const double* kin = x.wk + lo;
+  const uint32_t capc = x.capc;
+
+  if (nch == 1) {
+    for (uint32_t j = t; j < n; j += kBlock) s_kv[j] = kin[j];
+    __syncthreads();
+    if (t == 0) {
+      uint32_t nc = 0, pos = 0;
+      double base = base0;
+      for (;;) {
+        if (nc >= capc) { atomicOr(x.err, 1u); break; }
+        s_st[nc++] = pos;
+        uint32_t l = pos + 1, h = n;
+        while (l < h) {
+          uint32_t m = (l + h) >> 1;
+          if (dsub(s_kv[m], base) > 1.0) h = m;
+          else l = m + 1;
+        }
+        if (l >= n) break;
+        base = s_kv[l - 1];
+        pos = l;
+      }
+      s_nc = nc;
+      s_st[nc] = n;
+    }
+    __syncthreads();
+    // Welford per centroid, in element order, exactly as mergeOne does
+    const uint32_t nc = s_nc;
+    const uint8_t nb = x.hcur[s] ^ 1;
+    double* cm = nb ? x.cm1 : x.cm0;
+    double* cwn = nb ? x.cw1 : x.cw0;
+    for (uint32_t ci = t; ci < nc; ci += kBlock) {
+      uint32_t a = s_st[ci], b = s_st[ci + 1];
+      double mean = from_ordered_bits(x.A[lo + a]);
+      double W = x.w[lo + a];
+      for (uint32_t j = a + 1; j < b; j++) {
+        double xv = from_ordered_bits(x.A[lo + j]);
+        double wt = x.w[lo + j];
+        W = dadd(W, wt);
+        mean = dadd(mean, ddiv(dmul(dsub(xv, mean), wt), W));
+      }
+      cm[(uint64_t)s * capc + ci] = mean;
+      cwn[(uint64_t)s * capc + ci] = W;
+    }
+    if (t == 0) {
+      x.hncent[s] = nc;
+      x.hcur[s] = nb;
+      x.nc_new[k] = nc;
+    }
+    return;
+  }
+
+  // multi-chunk segment: coarse index of chunk-last k values in LDS
+  const double* lastk = x.ch_lastk + cb;
+  const bool coarse_lds = nch <= (uint32_t)kTile;
+  if (coarse_lds)
+    for (uint32_t q = t; q < nch; q += kBlock) s_kv[q] = lastk[q];
+  if (t == 0) {
+    s_nc = 0;
+    s_pos = 0;
+    s_base = base0;
+    s_done = 0;
+  }
+  __syncthreads();
+  for (;;) {
+    // thread 0: record the start, locate the chunk holding the next start
+    if (t == 0) {
+      if (s_nc >= capc) {
+        atomicOr(x.err, 1u);
+        s_done = 1;
+      } else {
+        s_st[s_nc++] = s_pos;
+        uint32_t from = s_pos + 1;
+        if (from >= n) s_done = 1;
+        else {
+          uint32_t l = from / kTile, h = nch;
+          const double base = s_base;
+          while (l < h) {
+            uint32_t m = (l + h) >> 1;
+            double v = coarse_lds ? s_kv[m] : lastk[m];
+            if (dsub(v, base) > 1.0) h = m;
+            else l = m + 1;
+          }
+          if (l >= nch) s_done = 1;
+          else s_q = l;
+        }
+      }
+      s_g = 0xffffffffu;
+      s_next = 0xffffffffu;
+    }
+    __syncthreads();
+    if (s_done) break;
+    const uint32_t pos = s_pos, q = s_q;
+    const double base = s_base;
+    const uint32_t qlo = q * kTile, qhi = min(n, qlo + (uint32_t)kTile);
+    {  // 256-ary probe of 16-element groups
+      uint32_t gl = qlo + t * kItems;
+      if (gl < qhi) {
+        uint32_t ge = min(qhi, gl + (uint32_t)kItems) - 1;
+        if (ge > pos && dsub(kin[ge], base) > 1.0) atomicMin(&s_g, t);
+      }
+    }
+    __syncthreads();
+    if (s_g != 0xffffffffu && t < (uint32_t)kItems) {
+      uint32_t p = qlo + s_g * kItems + t;
+      if (p < qhi && p > pos && dsub(kin[p], base) > 1.0) atomicMin(&s_next, p);
+    }
+    __syncthreads();
+    if (t == 0) {
+      if (s_next == 0xffffffffu) {
+        s_done = 1;  // not reachable for a monotone k array; stop safely
+      } else {
+        s_base = kin[s_next - 1];
+        s_pos = s_next;
+      }
+    }
+    __syncthreads();
+    if (s_done) break;
+  }
+  __syncthreads();
+  const uint32_t nc = s_nc;
+  for (uint32_t ci = t; ci < nc; ci += kBlock) {
+    x.starts[(uint64_t)k * capc + ci] = s_st[ci];
+    x.acc_xw[(uint64_t)k * capc + ci] = 0.0;
+    x.acc_w[(uint64_t)k * capc + ci] = 0.0;
+  }
+  if (t == 0) x.nc_new[k] = nc;
+}
+
+// 7. centroid sums of multi-chunk segments
+__global__ __launch_bounds__(kBlock) void k_chunk_cent(HistoCtx x) {
+  __shared__ uint32_t s_k;
+  __shared__ uint32_t s_st[kMaxCent + 1];
+  __shared__ double s_xw[kMaxCent];
+  __shared__ double s_w[kMaxCent];
+  ChunkRange r;
+  if (!chunk_range(x, r, &s_k)) return;
+  if (r.nch == 1) return;
+  const uint32_t t = threadIdx.x, capc = x.capc;
+  const uint32_t nc = x.nc_new[r.k];
+  const uint32_t n = r.seg_hi - r.seg_lo;
+  for (uint32_t ci = t; ci < nc; ci += kBlock) {
+    s_st[ci] = x.starts[(uint64_t)r.k * capc + ci];
+    s_xw[ci] = 0.0;
+    s_w[ci] = 0.0;
+  }
+  if (t == 0) s_st[nc] = n;
+  __syncthreads();
+  const uint32_t b0 = r.lo + t * kItems;
+  if (b0 < r.hi) {
+    uint32_t rel = b0 - r.seg_lo;
+    uint32_t l = 0, h = nc;  // last centroid with start <= rel
+    while (h - l > 1) {
+      uint32_t m = (l + h) >> 1;
+      if (s_st[m] <= rel) l = m;
+      else h = m;
+    }
+    uint32_t cid = l;
+    double axw = 0.0, aw = 0.0;
+    for (int j = 0; j < kItems; j++) {
+      uint32_t i = b0 + j;
+      if (i >= r.hi) break;
+      rel = i - r.seg_lo;
+      if (rel >= s_st[cid + 1]) {
+        atomicAdd(&s_xw[cid], axw);
+        atomicAdd(&s_w[cid], aw);
+        axw = 0.0;
+        aw = 0.0;
+        while (rel >= s_st[cid + 1]) cid++;
+      }
+      double wt = x.w[i];
+      axw = dadd(axw, dmul(from_ordered_bits(x.A[i]), wt));
+      aw = dadd(aw, wt);
+    }
+    atomicAdd(&s_xw[cid], axw);
+    atomicAdd(&s_w[cid], aw);
+  }
+  __syncthreads();
+  for (uint32_t ci = t; ci < nc; ci += kBlock) {
+    if (s_w[ci] != 0.0) {
+      unsafeAtomicAdd(&x.acc_w[(uint64_t)r.k * capc + ci], s_w[ci]);
+      unsafeAtomicAdd(&x.acc_xw[(uint64_t)r.k * capc + ci], s_xw[ci]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_finalize(HistoCtx x) {
+  const uint32_t k = blockIdx.x, t = threadIdx.x, capc = x.capc;
+  if (x.chb[k + 1] - x.chb[k] == 1) return;
+  const uint32_t s = x.tl[k];
+  const uint32_t nc = x.nc_new[k];
+  const uint8_t nb = x.hcur[s] ^ 1;
+  double* cm = nb ? x.cm1 : x.cm0;
+  double* cwn = nb ? x.cw1 : x.cw0;
+  for (uint32_t ci = t; ci < nc; ci += kBlock) {
+    double w = x.acc_w[(uint64_t)k * capc + ci];
+    cm[(uint64_t)s * capc + ci] = ddiv(x.acc_xw[(uint64_t)k * capc + ci], w);
+    cwn[(uint64_t)s * capc + ci] = w;
+  }
+  __syncthreads();
+  if (t == 0) {
+    x.hncent[s] = nc;
+    x.hcur[s] = nb;
+  }
+}
+
+__global__ void k_clear_flags(uint32_t n, const uint32_t* __restrict__ list, uint32_t* __restrict__ flags) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) flags[list[k]] = 0;
+}
+
+// raw (arrival-order) keys: A = float64 bits, B = slot<<32 | float32 rate bits
+__global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, const double* __restrict__ val,
+                                 const float* __restrict__ rate, uint64_t* __restrict__ A, uint64_t* __restrict__ B,
+                                 uint32_t* __restrict__ bt, uint32_t* __restrict__ htouch) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = slot[i];
+  A[i] = dbits(val[i]);
+  B[i] = ((uint64_t)s << 32) | (uint64_t)__float_as_uint(rate[i]);
+  bt[s] = 1;
+  htouch[s] = 1;
+}
+
+// how much of each key's batch is replayed exactly, and how much goes to the batch merge
+__global__ void k_histo_plan(uint32_t ntouched, const uint32_t* __restrict__ tl, const uint32_t* __restrict__ start,
+                             const uint32_t* __restrict__ end, uint32_t* __restrict__ hseen, uint32_t E,
+                             uint32_t* __restrict__ ex, uint32_t* __restrict__ hotflag, uint32_t* __restrict__ hotcnt) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= ntouched) return;
+  uint32_t s = tl[k];
+  uint32_t nk = end[s] - start[s];
+  uint32_t seen = hseen[s];
+  uint32_t e = seen >= E ? 0u : min(nk, E - seen);
+  ex[k] = e;
+  hotcnt[k] = nk - e;
+  hotflag[k] = nk > e;
+  hseen[s] = seen + nk;
+}
+
+__global__ void k_histo_hot_keys(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ hotlist,
+                                 const uint32_t* __restrict__ tl, const uint32_t* __restrict__ hncent,
+                                 uint32_t cap, uint32_t* __restrict__ tl2, uint32_t* __restrict__ oldcnt) {
+  uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cap) return;
+  if (j < cnt[0]) {
+    uint32_t s = tl[hotlist[j]];
+    tl2[j] = s;
+    oldcnt[j] = hncent[s];
+  } else {
+    oldcnt[j] = 0;
+  }
+}
+
+// copy the hot remainder of each hot key into the batch-merge sort input
+__global__ void k_histo_gather_hot(const uint32_t* __restrict__ hotlist, const uint32_t* __restrict__ tl,
+                                   const uint32_t* __restrict__ start, const uint32_t* __restrict__ ex,
+                                   const uint32_t* __restrict__ hotcnt, const uint32_t* __restrict__ hotoff,
+                                   const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
+                                   uint64_t* __restrict__ A2, uint64_t* __restrict__ B2) {
+  uint32_t k = hotlist[blockIdx.x];
+  uint32_t s = tl[k];
+  uint64_t src = (uint64_t)start[s] + ex[k];
+  uint64_t dst = hotoff[k];
+  uint32_t cnt = hotcnt[k];
+  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+    A2[dst + i] = ordered_bits(bitsd(A[src + i]));
+    B2[dst + i] = B[src + i];
+  }
+}
+
+void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate) {
+  if (!n) return;
+  hipStream_t st = e->st;
+  const uint32_t caph = e->cap[VN_HISTO];
+  // ---- 1. group by key, arrival order kept (stable radix by slot)
+  hipLaunchKernelGGL(k_histo_keys_raw, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, val, rate, e->hA0, e->hB0,
+                     e->h_bt, e->htouch);
+  RadixPass spass[4];
+  int nsp = 0;
+  for (int sh = 32; sh < 32 + e->slot_bits[VN_HISTO]; sh += 8) spass[nsp++] = RadixPass{true, sh};
+  bool fl = radix_sort(e->hA0, e->hB0, e->hA1, e->hB1, n, spass, nsp, e->rs, st, e->timing ? &e->rstat_h : nullptr);
+  uint64_t* As = fl ? e->hA1 : e->hA0;
+  uint64_t* Bs = fl ? e->hB1 : e->hB0;
+  uint64_t* Ao = fl ? e->hA0 : e->hA1;
+  uint64_t* Bo = fl ? e->hB0 : e->hB1;
+  hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, Bs, e->h_start, e->h_end);
+  compact_flags(e->h_bt, e->h_pos, e->h_tl, e->h_cnt, caph, e->ss, st);
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt, e->h_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  const uint32_t ntouched = e->hf_cnt[0];
+  if (!ntouched) return;
+
+  // ---- 2. exact replay of MergingDigest.Add for keys under the threshold
+  hipLaunchKernelGGL(k_histo_plan, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_start,
+                     e->h_end, e->hseen, e->exact_threshold, e->h_ex, e->h_hotflag, e->h_hotcnt);
+  ExactCtx xc{};
+  xc.nkeys = ntouched;
+  xc.keys = e->h_tl;
+  xc.start = e->h_start;
+  xc.nex = e->h_ex;
+  xc.hot = e->h_hotflag;
+  xc.A = As;
+  xc.B = Bs;
+  xc.delta = e->cfg.compression;
+  xc.capc = e->cap_cent;
+  xc.tcap = e->temp_cap;
+  xc.hst = e->hst;
+  xc.hncent = e->hncent;
+  xc.hcur = e->hcur;
+  xc.cm0 = e->cmean[0];
+  xc.cm1 = e->cmean[1];
+  xc.cw0 = e->cw[0];
+  xc.cw1 = e->cw[1];
+  xc.hpend = e->hpend;
+  xc.hpv = e->hpv;
+  xc.hpw = e->hpw;
+  xc.err = e->h_err;
+  xc.flush_mode = 0;
+  launch_histo_exact(xc, st);
+
+  // ---- 3. hot remainders: one-shot merge of (main centroids + samples) per key
+  compact_flags(e->h_hotflag, e->h_pos, e->h_hotlist, e->h_cnt + 1, ntouched, e->ss, st);
+  scan_exclusive_u32(e->h_hotcnt, e->h_hotoff, ntouched, e->ss, st);
+  hipLaunchKernelGGL(k_histo_hot_keys, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, e->h_cnt + 1,
+                     e->h_hotlist, e->h_tl, e->hncent, ntouched, e->h_tl2, e->h_oldcnt);
+  scan_exclusive_u32(e->h_oldcnt, e->h_oldoff, ntouched, e->ss, st);
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 1, e->h_cnt + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 2, e->h_hotoff + ntouched, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 3, e->h_oldoff + ntouched, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  const uint32_t nhot = e->hf_cnt[1];
+  const uint64_t nhotrec = e->hf_cnt[2];
+  const uint64_t nold = e->hf_cnt[3];
+  if (nhot == 0) {
+    hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
+    return;
+  }
+  const uint64_t n2 = nhotrec + nold;
+  if (n2 > e->h_sort_cap) throw std::runtime_error("histo batch exceeds sort capacity");
+  hipLaunchKernelGGL(k_histo_gather_hot, dim3(nhot), dim3(256), 0, st, e->h_hotlist, e->h_tl, e->h_start, e->h_ex,
+                     e->h_hotcnt, e->h_hotoff, As, Bs, Ao, Bo);
+  hipLaunchKernelGGL(k_histo_append_old, dim3(nhot), dim3(256), 0, st, e->h_tl2, e->h_oldoff, e->hncent, e->hcur,
+                     e->cmean[0], e->cmean[1], e->cap_cent, nhotrec, Ao, Bo);
+  RadixPass passes[16];
+  int np = 0;
+  for (int sh = 0; sh < 64; sh += 8) passes[np++] = RadixPass{false, sh};
+  for (int sh = 32; sh < 32 + e->slot_bits[VN_HISTO]; sh += 8) passes[np++] = RadixPass{true, sh};
+  bool fl2 = radix_sort(Ao, Bo, As, Bs, n2, passes, np, e->rs, st, e->timing ? &e->rstat_h : nullptr);
+  const uint64_t* A = fl2 ? As : Ao;
+  const uint64_t* B = fl2 ? Bs : Bo;
+
+  hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(n2, 256)), dim3(256), 0, st, n2, B, e->h_start, e->h_end);
+  hipLaunchKernelGGL(k_seg_nch, dim3(blocks_for(nhot, 256)), dim3(256), 0, st, nhot, e->h_tl2, e->h_start, e->h_end,
+                     e->h_nch);
+  scan_exclusive_u32(e->h_nch, e->h_chb, nhot, e->ss, st);
+  const uint64_t maxch = n2 / kTile + nhot + 1;
+  if (maxch > e->h_max_chunks) throw std::runtime_error("histo chunk capacity exceeded");
+
+  HistoCtx x;
+  x.ntouched = nhot;
+  x.capc = e->cap_cent;
+  x.delta = e->cfg.compression;
+  x.tl = e->h_tl2;
+  x.start = e->h_start;
+  x.end = e->h_end;
+  x.chb = e->h_chb;
+  x.A = A;
+  x.B = B;
+  x.w = e->h_w;
+  x.wk = e->h_wk;
+  x.ch_sum = e->ch_sum;
+  x.ch_pre = e->ch_pre;
+  x.ch_stats = e->ch_stats;
+  x.ch_lastk = e->ch_lastk;
+  x.seg_T = e->seg_T;
+  x.starts = e->starts;
+  x.nc_new = e->nc_new;
+  x.acc_xw = e->acc_xw;
+  x.acc_w = e->acc_w;
+  x.hst = e->hst;
+  x.hncent = e->hncent;
+  x.hcur = e->hcur;
+  x.cm0 = e->cmean[0];
+  x.cm1 = e->cmean[1];
+  x.cw0 = e->cw[0];
+  x.cw1 = e->cw[1];
+  x.err = e->h_err;
+  hipLaunchKernelGGL(k_chunk_prep, dim3(maxch), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_seg_scan, dim3(nhot), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_chunk_kin, dim3(maxch), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_chain, dim3(nhot), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_chunk_cent, dim3(maxch), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_finalize, dim3(nhot), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
+}
+
+}  // namespace vn

@@ -1,0 +1,466 @@
+// ingest_set.hip -- Set.Sample -> axiomhq/hyperloglog Sketch.Insert, bit-exact.
+//
+// Reference (vendor/github.com/axiomhq/hyperloglog/hyperloglog.go):
+//   Insert (186-200): x = metro64(member, 1337).  Sparse: tmpSet.add(encodeHash(x)); when
+//     len(tmpSet)*100 > m (len >= 164): mergeSparse (229-267: sorted union into the
+//     compressed list) and, if the list's varint byte length > m, toNormal (152-166).
+//     Dense: insert(getPosVal(x)) (168-183) -- 4-bit registers over a base b; a value that
+//     does not fit (uint8(r-b) >= 16) rebases by regs.min(), which is non-zero only once
+//     every register is non-zero (nz == 0).
+//
+// MI355X formulation:
+//   k_set_keys   one lane per record: metro64 + encodeHash -> (slot<<32 | code)
+//   radix sort   stable by slot: every key's codes contiguous, in arrival order
+//   k_set_segments  one workgroup per key touched in the batch, replaying the reference
+//     state machine exactly:
+//       sparse: the tmpSet is an LDS hash; one lane walks the arrival order to the next
+//         164th distinct code (the only order-dependent decision), then the workgroup
+//         merges the sorted tmpSet into the LDS copy of the sorted list in parallel and
+//         recomputes the varint byte length; > 16384 bytes -> registers built from the list.
+//       dense: registers live in LDS (one u32 per register).  Per 4096-record chunk the
+//         workgroup finds T_full (the record that fills the last zero register -- first
+//         filler per register via LDS atomic max on a marker) and the first rebase candidate
+//         after it; records before that point are plain commutative max updates (LDS atomic
+//         max), the rebase itself is a parallel min + subtract.  Identical to the
+//         sequential semantics, rebase epochs included.
+#include "kernels.h"
+
+namespace vn {
+
+struct SetCtx {
+  uint32_t ntouched;
+  const uint32_t* tl;
+  const uint32_t* start;
+  const uint32_t* end;
+  const uint64_t* R;
+  uint8_t* mode;
+  uint8_t* base;
+  uint32_t* nz;
+  uint32_t* lc;
+  uint32_t* lb;
+  uint32_t* last;
+  uint32_t* tc;
+  uint32_t* tmp;
+  uint32_t* arena;
+  uint32_t* err;
+};
+
+__global__ void k_set_keys(uint64_t n, const uint32_t* __restrict__ slot, const uint32_t* __restrict__ off,
+                           const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ hashes,
+                           uint64_t* __restrict__ R, uint32_t* __restrict__ bt, uint32_t* __restrict__ stouch) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = slot[i];
+  uint64_t x = hashes ? hashes[i] : metro64(bytes + off[i], off[i + 1] - off[i], kMetroSeed);
+  R[i] = ((uint64_t)s << 32) | (uint64_t)encode_hash(x);
+  bt[s] = 1;
+  stouch[s] = 1;
+}
+
+__global__ void k_set_seg_mark(uint64_t n, const uint64_t* __restrict__ R, uint32_t* __restrict__ start,
+                               uint32_t* __restrict__ end) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = (uint32_t)(R[i] >> 32);
+  if (i == 0 || (uint32_t)(R[i - 1] >> 32) != s) start[s] = (uint32_t)i;
+  if (i == n - 1 || (uint32_t)(R[i + 1] >> 32) != s) end[s] = (uint32_t)(i + 1);
+}
+
+constexpr uint32_t kHashSlots = 512;  // LDS open-addressing table for the tmpSet (<= 163 codes)
+constexpr uint32_t kMark = 0x80000000u;
+
+__device__ __forceinline__ uint32_t hslot(uint32_t c) { return (c * 2654435761u) >> 23; }  // 9 bits
+
+// sequential insert (single lane); returns true if the code was new
+__device__ __forceinline__ bool hash_insert_seq(uint32_t* h, uint32_t c) {
+  uint32_t i = hslot(c);
+  for (;;) {
+    uint32_t v = h[i];
+    if (v == c) return false;
+    if (v == kHllNoCode) {
+      h[i] = c;
+      return true;
+    }
+    i = (i + 1) & (kHashSlots - 1);
+  }
+}
+// parallel insert of distinct codes
+__device__ __forceinline__ void hash_insert_par(uint32_t* h, uint32_t c) {
+  uint32_t i = hslot(c);
+  for (;;) {
+    uint32_t prev = atomicCAS(&h[i], kHllNoCode, c);
+    if (prev == kHllNoCode || prev == c) return;
+    i = (i + 1) & (kHashSlots - 1);
+  }
+}
+
+// bitonic sort of 256 u32 in LDS, ascending (all 256 threads)
+__device__ __forceinline__ void bitonic256(uint32_t* a) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t k = 2; k <= 256; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      uint32_t ixj = t ^ j;
+      if (ixj > t) {
+        uint32_t x = a[t], y = a[ixj];
+        bool up = (t & k) == 0;
+        if ((x > y) == up) {
+          a[t] = y;
+          a[ixj] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t v) {
+  uint32_t l = 0, h = n;
+  while (l < h) {
+    uint32_t m = (l + h) >> 1;
+    if (a[m] < v) l = m + 1;
+    else h = m;
+  }
+  return l;
+}
+
+__global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
+  __shared__ uint32_t U[kArenaWords];   // sparse list (sorted codes) or dense registers (u32 each)
+  __shared__ uint32_t s_hash[kHashSlots];
+  __shared__ uint32_t s_tmp[256];       // tmpSet codes in insertion order, then sorted
+  __shared__ uint32_t s_new[256];       // tmp codes not yet in the list (sorted)
+  __shared__ uint32_t s_red[4];
+  __shared__ uint32_t s_pos, s_trig, s_tc, s_lc, s_mode, s_b, s_nz;
+  __shared__ uint32_t s_filled, s_tfull, s_pstar, s_newfill, s_min;
+
+  const uint32_t k = blockIdx.x, t = threadIdx.x;
+  const uint32_t slot = x.tl[k];
+  const uint32_t lo = x.start[slot], n = x.end[slot] - lo;
+  const uint64_t* R = x.R + lo;
+  uint32_t* arena = x.arena + (uint64_t)slot * kArenaWords;
+  uint8_t* regs8 = reinterpret_cast<uint8_t*>(arena);
+
+  if (t == 0) {
+    s_mode = x.mode[slot];
+    s_b = x.base[slot];
+    s_nz = x.nz[slot];
+    s_tc = x.tc[slot];
+    s_lc = x.lc[slot];
+    s_pos = 0;
+  }
+  __syncthreads();
+  bool list_in_lds = false, list_dirty = false;
+  uint32_t lbytes = x.lb[slot];
+
+  if (s_mode == 0) {
+    // ------------------------------------------------------------ sparse phase
+    for (uint32_t i = t; i < kHashSlots; i += kBlock) s_hash[i] = kHllNoCode;
+    __syncthreads();
+    const uint32_t tc0 = s_tc;
+    if (t < tc0) {
+      uint32_t c = x.tmp[(uint64_t)slot * kTmpCap + t];
+      s_tmp[t] = c;
+      hash_insert_par(s_hash, c);
+    }
+    __syncthreads();
+    while (s_pos < n && s_mode == 0) {
+      if (t == 0) {
+        uint32_t pos = s_pos, tc = s_tc, trig = 0;
+        while (pos < n) {
+          uint32_t c = (uint32_t)R[pos++];
+          if (hash_insert_seq(s_hash, c)) {
+            s_tmp[tc++] = c;
+            if (tc >= kHllTmpTrigger) {
+              trig = 1;
+              break;
+            }
+          }
+        }
+        s_pos = pos;
+        s_tc = tc;
+        s_trig = trig;
+      }
+      __syncthreads();
+      if (!s_trig) break;
+      // mergeSparse: sorted union of the list and the tmpSet
+      if (!list_in_lds) {
+        for (uint32_t i = t; i < s_lc; i += kBlock) U[i] = arena[i];
+        list_in_lds = true;
+      }
+      if (t >= kHllTmpTrigger) s_tmp[t] = kHllNoCode;
+      __syncthreads();
+      bitonic256(s_tmp);
+      const uint32_t lc = s_lc;
+      uint32_t isnew = 0, lb = 0, code = 0;
+      if (t < kHllTmpTrigger) {
+        code = s_tmp[t];
+        lb = lower_bound_u32(U, lc, code);
+        isnew = !(lb < lc && U[lb] == code);
+      }
+      // exclusive rank among new codes (ascending)
+      uint64_t bal = __ballot(isnew);
+      const int lane = t & 63, w = t >> 6;
+      if (lane == 0) s_red[w] = (uint32_t)__popcll(bal);
+      __syncthreads();
+      uint32_t before = 0;
+      for (int i = 0; i < w; i++) before += s_red[i];
+      const uint32_t nnew = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+      uint32_t rank = before + (uint32_t)__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+      if (isnew) s_new[rank] = code;
+      __syncthreads();
+      // move list elements up by the number of new codes below them
+      constexpr int kPer = (kArenaWords + kBlock - 1) / kBlock;
+      uint32_t keep[kPer];
+#pragma unroll
+      for (int j = 0; j < kPer; j++) {
+        uint32_t i = t + j * kBlock;
+        keep[j] = i < lc ? U[i] : 0u;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kPer; j++) {
+        uint32_t i = t + j * kBlock;
+        if (i < lc) U[i + lower_bound_u32(s_new, nnew, keep[j])] = keep[j];
+      }
+      if (isnew) U[lb + rank] = code;
+      __syncthreads();
+      const uint32_t nlc = lc + nnew;
+      // varint byte length of the delta-encoded list
+      uint32_t bytes = 0;
+      for (uint32_t i = t; i < nlc; i += kBlock) bytes += varint_len(U[i] - (i ? U[i - 1] : 0u));
+      bytes = block_allreduce_u32_sum(bytes, s_red);
+      lbytes = bytes;
+      list_dirty = true;
+      if (t == 0) {
+        s_lc = nlc;
+        s_tc = 0;
+      }
+      for (uint32_t i = t; i < kHashSlots; i += kBlock) s_hash[i] = kHllNoCode;
+      __syncthreads();
+      if (bytes > kHllM) {
+        // toNormal: registers from the merged list (b stays; nz > 0 so no rebase can occur)
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+          uint32_t i = t + j * kBlock;
+          keep[j] = i < nlc ? U[i] : kHllNoCode;
+        }
+        __syncthreads();
+        for (uint32_t i = t; i < kHllM; i += kBlock) U[i] = 0;
+        __syncthreads();
+        const uint32_t b = s_b;
+#pragma unroll
+        for (int j = 0; j < kPer; j++) {
+          if (keep[j] != kHllNoCode) {
+            uint32_t ri, r;
+            decode_hash(keep[j], &ri, &r);
+            if (r > b) atomicMax(&U[ri], min(r - b, kHllCapacity - 1));
+          }
+        }
+        __syncthreads();
+        uint32_t z = 0;
+        for (uint32_t i = t; i < kHllM; i += kBlock) z += U[i] == 0;
+        z = block_allreduce_u32_sum(z, s_red);
+        if (t == 0) {
+          s_nz = z;
+          s_mode = 1;
+        }
+        list_in_lds = false;
+        list_dirty = false;
+        __syncthreads();
+      }
+    }
+    __syncthreads();
+    if (s_mode == 0) {
+      // write back the sparse state
+      const uint32_t tc = s_tc;
+      if (t < tc) x.tmp[(uint64_t)slot * kTmpCap + t] = s_tmp[t];
+      if (list_dirty)
+        for (uint32_t i = t; i < s_lc; i += kBlock) arena[i] = U[i];
+      if (t == 0) {
+        x.tc[slot] = tc;
+        x.lc[slot] = s_lc;
+        x.lb[slot] = lbytes;
+        if (list_dirty && s_lc) x.last[slot] = U[s_lc - 1];
+      }
+      return;
+    }
+  } else {
+    // ------------------------------------------------------------ dense: registers to LDS
+    for (uint32_t i = t; i < kHllM; i += kBlock) U[i] = regs8[i];
+    __syncthreads();
+  }
+
+  // -------------------------------------------------------------- dense phase
+  for (uint32_t cpos0 = s_pos; cpos0 < n; cpos0 += kTile) {
+    const uint32_t cend = min(n, cpos0 + (uint32_t)kTile);
+    uint32_t ri[kItems], rr[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      uint32_t p = cpos0 + j * kBlock + t;
+      ri[j] = 0;
+      rr[j] = 0;
+      if (p < cend) decode_hash((uint32_t)R[p], &ri[j], &rr[j]);
+    }
+    uint32_t cpos = cpos0;
+    for (;;) {
+      const uint32_t b = s_b;
+      uint32_t tfull;
+      if (s_nz > 0) {
+        if (t == 0) {
+          s_filled = 0;
+          s_tfull = 0;
+        }
+        // phase A: mark the first filler of every zero register
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && rr[j] > b) {
+            uint32_t v = U[ri[j]];
+            if (v == 0 || (v & kMark)) atomicMax(&U[ri[j]], kMark | (0x7fffffffu - p));
+          }
+        }
+        __syncthreads();
+        // phase B: count first fillers, latest fill position
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == (kMark | (0x7fffffffu - p))) {
+            atomicAdd(&s_filled, 1u);
+            atomicMax(&s_tfull, p);
+          }
+        }
+        __syncthreads();
+        tfull = (s_filled == s_nz) ? s_tfull : 0xffffffffu;
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
+        }
+        __syncthreads();
+      } else {
+        tfull = cpos - 1;  // already full (cpos >= 1 whenever nz == 0 inside a key's stream)
+        if (cpos == 0) tfull = 0xfffffffeu;
+      }
+      if (t == 0) {
+        s_pstar = 0xffffffffu;
+        s_newfill = 0;
+      }
+      __syncthreads();
+      // phase C: first rebase candidate strictly after T_full
+      if (tfull != 0xffffffffu) {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          bool after = (tfull == 0xfffffffeu) ? true : (p > tfull);
+          if (p >= cpos && p < cend && after && ((rr[j] - b) & 0xffu) >= kHllCapacity) atomicMin(&s_pstar, p);
+        }
+      }
+      __syncthreads();
+      const uint32_t pstar = s_pstar;
+      // phase D: plain max updates before the rebase point
+#pragma unroll
+      for (int j = 0; j < kItems; j++) {
+        uint32_t p = cpos0 + j * kBlock + t;
+        if (p >= cpos && p < cend && p < pstar && rr[j] > b) {
+          uint32_t old = atomicMax(&U[ri[j]], min(rr[j] - b, kHllCapacity - 1));
+          if (old == 0) atomicAdd(&s_newfill, 1u);
+        }
+      }
+      __syncthreads();
+      if (t == 0) s_nz -= s_newfill;
+      __syncthreads();
+      if (pstar == 0xffffffffu) break;
+      // rebase at pstar (nz == 0 here): b += min(regs); regs -= min
+      if (t == 0) s_min = 0xffffffffu;
+      __syncthreads();
+      {
+        uint32_t mn = 0xffffffffu;
+        for (uint32_t i = t; i < kHllM; i += kBlock) mn = min(mn, U[i]);
+        atomicMin(&s_min, mn);
+      }
+      __syncthreads();
+      const uint32_t db = s_min;
+      uint32_t z = 0;
+      for (uint32_t i = t; i < kHllM; i += kBlock) {
+        uint32_t v = U[i] - db;
+        U[i] = v;
+        z += v == 0;
+      }
+      z = block_allreduce_u32_sum(z, s_red);
+      if (t == 0) {
+        if (db == 0 || db == 0xffffffffu) atomicOr(x.err, 2u);
+        uint32_t nb = b + db;
+        s_b = nb;
+        s_nz = z;
+        // the candidate record itself, after the rebase
+        uint32_t pi, pr;
+        decode_hash((uint32_t)R[pstar], &pi, &pr);
+        if (pr > nb) {
+          uint32_t v = min(pr - nb, kHllCapacity - 1);
+          if (v > U[pi]) {
+            if (U[pi] == 0) s_nz -= 1;
+            U[pi] = v;
+          }
+        }
+      }
+      __syncthreads();
+      cpos = pstar + 1;
+      if (cpos >= cend) break;
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < kHllM; i += kBlock) regs8[i] = (uint8_t)U[i];
+  if (t == 0) {
+    x.mode[slot] = 1;
+    x.base[slot] = (uint8_t)s_b;
+    x.nz[slot] = s_nz;
+    x.tc[slot] = 0;
+    x.lc[slot] = 0;
+    x.lb[slot] = 0;
+  }
+}
+
+__global__ void k_set_clear_flags(uint32_t n, const uint32_t* __restrict__ list, uint32_t* __restrict__ flags) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) flags[list[k]] = 0;
+}
+
+void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t* off, const uint8_t* bytes,
+                 const uint64_t* hashes) {
+  if (!n) return;
+  hipStream_t st = e->st;
+  const uint32_t caps = e->cap[VN_SET];
+  hipLaunchKernelGGL(k_set_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, off, bytes, hashes, e->sR0,
+                     e->s_bt, e->stouch);
+  RadixPass passes[4];
+  int np = 0;
+  for (int sh = 32; sh < 32 + e->slot_bits[VN_SET]; sh += 8) passes[np++] = RadixPass{false, sh};
+  bool fl = radix_sort(e->sR0, nullptr, e->sR1, nullptr, n, passes, np, e->rs, st,
+                       e->timing ? &e->rstat_s : nullptr);
+  const uint64_t* R = fl ? e->sR1 : e->sR0;
+  hipLaunchKernelGGL(k_set_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, R, e->s_start, e->s_end);
+  compact_flags(e->s_bt, e->s_pos, e->s_tl, e->s_cnt, caps, e->ss, st);
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 2, e->s_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  const uint32_t ntouched = e->hf_cnt[2];
+  if (!ntouched) return;
+  SetCtx x;
+  x.ntouched = ntouched;
+  x.tl = e->s_tl;
+  x.start = e->s_start;
+  x.end = e->s_end;
+  x.R = R;
+  x.mode = e->smode;
+  x.base = e->sbase;
+  x.nz = e->snz;
+  x.lc = e->slc;
+  x.lb = e->slb;
+  x.last = e->slast;
+  x.tc = e->stc;
+  x.tmp = e->stmp;
+  x.arena = e->sarena;
+  x.err = e->h_err;
+  hipLaunchKernelGGL(k_set_segments, dim3(ntouched), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_set_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->s_tl, e->s_bt);
+}
+
+}  // namespace vn

@@ -1,0 +1,81 @@
+// kernels.h -- host launchers of the engine's HIP kernels (one stream per engine).
+#pragma once
+#include "engine.h"
+#include "gomath.h"
+#include "sketch.h"
+
+namespace vn {
+
+// Counter.Sample (samplers.go:132-134) / Counter.Combine (171-183)
+void ingest_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate);
+void import_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const int64_t* val);
+// Gauge.Sample (198-200) / Gauge.Combine (237-249): last write in arrival order wins
+void ingest_gauges(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val);
+// Histo.Sample (346-356) + MergingDigest.Add/mergeAllTemps (merging_digest.go:97-236)
+void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate);
+// Set.Sample (265-267) -> Sketch.Insert (hyperloglog.go:186-200)
+void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t* off, const uint8_t* bytes,
+                 const uint64_t* hashes);
+// Worker.Flush + Counter/Gauge/Histo/Set.Flush math; resets the window
+void flush_all(vn_engine* e, vn_flush_result* out);
+// initial (empty-window) state of every slot
+void init_state(vn_engine* e);
+// metro64 over a batch (KAT entry point)
+void metro64_batch(const uint8_t* bytes, const uint32_t* off, uint64_t n, uint64_t seed, uint64_t* out,
+                   hipStream_t st);
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+struct SumOp {
+  __device__ double operator()(double a, double b) const { return dadd(a, b); }
+};
+struct MinGoOp {
+  __device__ double operator()(double a, double b) const { return min_go(a, b); }
+};
+struct MaxGoOp {
+  __device__ double operator()(double a, double b) const { return max_go(a, b); }
+};
+
+// all-reduce across a 256-thread block (4 waves); s_tmp holds 4 doubles
+template <class Op>
+__device__ __forceinline__ double block_allreduce(double v, double* s_tmp, Op op) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = op(v, __shfl_xor(v, d, 64));
+  if (lane_id() == 0) s_tmp[wave_id()] = v;
+  __syncthreads();
+  double r = op(op(s_tmp[0], s_tmp[1]), op(s_tmp[2], s_tmp[3]));
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ uint32_t block_allreduce_u32_sum(uint32_t v, uint32_t* s_tmp) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  if (lane_id() == 0) s_tmp[wave_id()] = v;
+  __syncthreads();
+  uint32_t r = s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
+  __syncthreads();
+  return r;
+}
+// exclusive prefix sum (double) of one value per thread in a 256-thread block
+__device__ __forceinline__ double block_excl_scan_d(double v, double* s_tmp, double& total) {
+  const int lane = lane_id(), w = wave_id();
+  double inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    double o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc = dadd(inc, o);
+  }
+  if (lane == 63) s_tmp[w] = inc;
+  __syncthreads();
+  double base = 0.0;
+  for (int i = 0; i < w; i++) base = dadd(base, s_tmp[i]);
+  total = dadd(dadd(dadd(s_tmp[0], s_tmp[1]), s_tmp[2]), s_tmp[3]);
+  __syncthreads();
+  double ex = __shfl_up(inc, 1, 64);
+  if (lane == 0) ex = 0.0;
+  return dadd(base, ex);
+}
+
+}  // namespace vn

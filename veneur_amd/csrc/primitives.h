@@ -1,0 +1,76 @@
+// primitives.h -- device-wide building blocks of the engine (HIP, gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vn {
+
+constexpr int kBlock = 256;               // 4 waves
+constexpr int kItems = 16;                // items per thread in a tile
+constexpr int kTile = kBlock * kItems;    // 4096 records per tile / chunk
+
+// ---- exclusive scan of u32 (out may alias nothing); out[n] receives the total.
+struct ScanScratch {
+  uint32_t* partials = nullptr;  // >= ceil(n / kTile) + 1
+  size_t cap = 0;
+};
+void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, ScanScratch& s, hipStream_t st);
+
+// ---- stable LSD radix sort over 64-bit words.
+// Records are (A[i], B[i]) pairs (B may be null for key-only sorts).  Each pass sorts
+// stably by an 8-bit digit taken from A (from_b = false) or B (from_b = true) at `shift`.
+struct RadixPass {
+  bool from_b;
+  int shift;
+};
+struct RadixScratch {
+  uint32_t* counts = nullptr;    // 256 * blocks
+  uint32_t* offsets = nullptr;   // 256 * blocks + 1
+  ScanScratch scan;
+  size_t blocks_cap = 0;
+};
+// Sorts n records; ping-pongs between (a0,b0) and (a1,b1).  Returns true if the result
+// ended in (a1, b1).  If timing events are supplied, the scatter kernels are bracketed.
+// Optional timing: the scatter launches are bracketed by events taken from a pool that the
+// caller resolves after its own synchronisation (no sync inside the sort).
+struct EventPool {
+  hipEvent_t* ev = nullptr;
+  int cap = 0, used = 0;
+  hipEvent_t next() { return used < cap ? ev[used++] : nullptr; }
+};
+struct RadixStats {
+  EventPool* pool = nullptr;     // pairs (begin, end) appended per scatter launch
+  uint64_t launches = 0;
+  uint64_t bytes = 0;            // algorithmic bytes of those launches (read + write)
+};
+bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t n,
+                const RadixPass* passes, int npasses, RadixScratch& s, hipStream_t st,
+                RadixStats* stats);
+
+void radix_scratch_reserve(RadixScratch& s, uint64_t max_n);
+void radix_scratch_free(RadixScratch& s);
+
+// ---- compaction: list[] receives the indices i < n with flag[i] != 0 (ascending);
+// count[0] receives the number of them.  pos must hold n+1 u32.
+void compact_flags(const uint32_t* flag, uint32_t* pos, uint32_t* list, uint32_t* count, uint64_t n,
+                   ScanScratch& s, hipStream_t st);
+
+inline int blocks_for(uint64_t n, int per_block) { return (int)((n + per_block - 1) / per_block); }
+
+}  // namespace vn
+
+#define VN_HIP_CHECK(expr)                                                   \
+  do {                                                                       \
+    hipError_t _e = (expr);                                                  \
+    if (_e != hipSuccess) throw vn::HipError(_e, #expr, __FILE__, __LINE__); \
+  } while (0)
+
+namespace vn {
+struct HipError {
+  hipError_t err;
+  const char* expr;
+  const char* file;
+  int line;
+  HipError(hipError_t e, const char* x, const char* f, int l) : err(e), expr(x), file(f), line(l) {}
+};
+}  // namespace vn

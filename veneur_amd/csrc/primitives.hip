@@ -1,0 +1,287 @@
+// primitives.hip -- scan, compaction and stable LSD radix sort for gfx950.
+//
+// Radix pass = reduce-then-scan:
+//   count:   each 4096-record tile builds its 256-bin digit histogram in LDS
+//   scan:    digit-major exclusive scan of the [256][tiles] histogram -> global offsets
+//   scatter: the tile ranks its records stably (wave64 ballot match per digit, per-wave
+//            counts in LDS), reorders them by digit in LDS, then writes each digit run
+//            contiguously so consecutive lanes store consecutive addresses.
+#include "primitives.h"
+
+namespace vn {
+
+// ---------------------------------------------------------------- block scan helpers
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t o = __shfl_up(v, d, 64);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+// exclusive scan of one value per thread across a 256-thread block; returns the total.
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = wave_incl_scan_u32(v);
+  if (lane == 63) s_wave[w] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int i = 0; i < w; i++) base += s_wave[i];
+  total = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+  __syncthreads();
+  return base + inc - v;
+}
+
+// ---------------------------------------------------------------- exclusive scan u32
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ in, uint64_t n,
+                                                        uint32_t* __restrict__ partials) {
+  __shared__ uint32_t s_wave[4];
+  uint64_t base = (uint64_t)blockIdx.x * kTile;
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+    if (i < n) sum += in[i];
+  }
+  uint32_t total;
+  (void)block_excl_scan_u32(sum, s_wave, total);
+  if (threadIdx.x == 0) partials[blockIdx.x] = total;
+}
+
+// single block: exclusive scan of the partials in place, total into partials[np]
+__global__ __launch_bounds__(kBlock) void k_scan_partials(uint32_t* partials, uint32_t np) {
+  __shared__ uint32_t s_wave[4];
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < np; base += kBlock) {
+    uint32_t i = base + threadIdx.x;
+    uint32_t v = i < np ? partials[i] : 0;
+    uint32_t total;
+    uint32_t ex = block_excl_scan_u32(v, s_wave, total);
+    if (i < np) partials[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) partials[np] = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                      uint64_t n, const uint32_t* __restrict__ partials,
+                                                      uint32_t np) {
+  __shared__ uint32_t s_wave[4];
+  // blocked layout: thread t owns items [t*16, t*16+16) of the tile
+  uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kItems;
+  uint32_t v[kItems];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    uint64_t i = base + j;
+    v[j] = i < n ? in[i] : 0;
+    sum += v[j];
+  }
+  uint32_t total;
+  uint32_t run = partials[blockIdx.x] + block_excl_scan_u32(sum, s_wave, total);
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    uint64_t i = base + j;
+    if (i < n) out[i] = run;
+    run += v[j];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = partials[np];
+}
+
+void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, ScanScratch& s, hipStream_t st) {
+  uint32_t np = (uint32_t)blocks_for(n ? n : 1, kTile);
+  if (s.cap < np + 1) {
+    if (s.partials) VN_HIP_CHECK(hipFree(s.partials));
+    s.cap = np + 1 + 1024;
+    VN_HIP_CHECK(hipMalloc(&s.partials, s.cap * sizeof(uint32_t)));
+  }
+  if (n == 0) {
+    VN_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(uint32_t), st));
+    return;
+  }
+  hipLaunchKernelGGL(k_scan_reduce, dim3(np), dim3(kBlock), 0, st, in, n, s.partials);
+  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kBlock), 0, st, s.partials, np);
+  hipLaunchKernelGGL(k_scan_down, dim3(np), dim3(kBlock), 0, st, in, out, n, s.partials, np);
+}
+
+// ---------------------------------------------------------------- compaction
+__global__ void k_flag_to_u32(const uint32_t* __restrict__ flag, uint32_t* __restrict__ f, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) f[i] = flag[i] != 0;
+}
+__global__ void k_compact_scatter(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos, uint64_t n,
+                                  uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && flag[i]) list[pos[i]] = (uint32_t)i;
+  if (i == 0) count[0] = pos[n];
+}
+void compact_flags(const uint32_t* flag, uint32_t* pos, uint32_t* list, uint32_t* count, uint64_t n,
+                   ScanScratch& s, hipStream_t st) {
+  // flags are 0/1 already (engine invariant), scan them directly
+  scan_exclusive_u32(flag, pos, n, s, st);
+  hipLaunchKernelGGL(k_compact_scatter, dim3(blocks_for(n ? n : 1, 256)), dim3(256), 0, st, flag, pos, n, list,
+                     count);
+}
+
+// ---------------------------------------------------------------- radix sort
+template <bool HASB>
+__device__ __forceinline__ uint32_t digit_of(uint64_t a, uint64_t b, bool from_b, int shift) {
+  uint64_t w = (HASB && from_b) ? b : a;
+  return (uint32_t)(w >> shift) & 0xffu;
+}
+
+template <bool HASB>
+__global__ __launch_bounds__(kBlock) void k_radix_count(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
+                                                        uint64_t n, bool from_b, int shift,
+                                                        uint32_t* __restrict__ counts, uint32_t nblocks) {
+  __shared__ uint32_t s_hist[4][256];
+  const int w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 4 * 256; i += kBlock) (&s_hist[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t* src = (HASB && from_b) ? B : A;
+  uint64_t base = (uint64_t)blockIdx.x * kTile;
+#pragma unroll 4
+  for (int j = 0; j < kItems; j++) {
+    uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+    if (i < n) atomicAdd(&s_hist[w][(uint32_t)(src[i] >> shift) & 0xffu], 1u);
+  }
+  __syncthreads();
+  uint32_t d = threadIdx.x;
+  counts[(uint64_t)d * nblocks + blockIdx.x] = s_hist[0][d] + s_hist[1][d] + s_hist[2][d] + s_hist[3][d];
+}
+
+// lanes of the wave holding the same 8-bit digit as this lane (among `active` lanes)
+__device__ __forceinline__ uint64_t match_digit8(uint32_t d, bool active) {
+  uint64_t m = __ballot(active);
+#pragma unroll
+  for (int bit = 0; bit < 8; bit++) {
+    uint64_t bb = __ballot(active && ((d >> bit) & 1u));
+    m &= ((d >> bit) & 1u) ? bb : ~bb;
+  }
+  return m;
+}
+
+template <bool HASB>
+__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
+                                                          uint64_t* __restrict__ A2, uint64_t* __restrict__ B2,
+                                                          uint64_t n, bool from_b, int shift,
+                                                          const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ offsets, uint32_t nblocks) {
+  __shared__ uint64_t s_a[kTile];
+  __shared__ uint64_t s_b[HASB ? kTile : 1];
+  __shared__ uint32_t s_wcnt[4][256];
+  __shared__ uint32_t s_run[256];
+  __shared__ uint32_t s_loc[256];   // tile-local start of each digit
+  __shared__ uint32_t s_glob[256];  // global start of each digit for this tile
+  __shared__ uint32_t s_wave[4];
+
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint64_t base = (uint64_t)blockIdx.x * kTile;
+  const uint32_t tile_n = (uint32_t)((n - base) < (uint64_t)kTile ? (n - base) : kTile);
+
+  {
+    uint32_t c = counts[(uint64_t)t * nblocks + blockIdx.x];
+    uint32_t total;
+    s_loc[t] = block_excl_scan_u32(c, s_wave, total);
+    s_glob[t] = offsets[(uint64_t)t * nblocks + blockIdx.x];
+    s_run[t] = 0;
+    s_wcnt[0][t] = s_wcnt[1][t] = s_wcnt[2][t] = s_wcnt[3][t] = 0;
+  }
+  __syncthreads();
+
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int j = 0; j < kItems; j++) {
+    const uint32_t li = (uint32_t)j * kBlock + t;
+    const bool active = li < tile_n;
+    uint64_t a = 0, b = 0;
+    uint32_t d = 0;
+    if (active) {
+      a = A[base + li];
+      if (HASB) b = B[base + li];
+      d = digit_of<HASB>(a, b, from_b, shift);
+    }
+    uint64_t peers = match_digit8(d, active);
+    uint32_t rank = __popcll(peers & lt);
+    if (active && rank == 0) s_wcnt[w][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (active) {
+      uint32_t before = s_run[d];
+      for (int ww = 0; ww < w; ww++) before += s_wcnt[ww][d];
+      uint32_t pos = s_loc[d] + before + rank;
+      s_a[pos] = a;
+      if (HASB) s_b[pos] = b;
+    }
+    __syncthreads();
+    s_run[t] += s_wcnt[0][t] + s_wcnt[1][t] + s_wcnt[2][t] + s_wcnt[3][t];
+    s_wcnt[0][t] = s_wcnt[1][t] = s_wcnt[2][t] = s_wcnt[3][t] = 0;
+    __syncthreads();
+  }
+
+  for (uint32_t li = t; li < tile_n; li += kBlock) {
+    uint64_t a = s_a[li];
+    uint64_t b = HASB ? s_b[li] : 0;
+    uint32_t d = digit_of<HASB>(a, b, from_b, shift);
+    uint64_t pos = (uint64_t)s_glob[d] + (li - s_loc[d]);
+    A2[pos] = a;
+    if (HASB) B2[pos] = b;
+  }
+}
+
+void radix_scratch_reserve(RadixScratch& s, uint64_t max_n) {
+  size_t blocks = (size_t)blocks_for(max_n ? max_n : 1, kTile);
+  if (s.blocks_cap >= blocks) return;
+  radix_scratch_free(s);
+  s.blocks_cap = blocks;
+  VN_HIP_CHECK(hipMalloc(&s.counts, 256 * blocks * sizeof(uint32_t)));
+  VN_HIP_CHECK(hipMalloc(&s.offsets, (256 * blocks + 1) * sizeof(uint32_t)));
+}
+
+void radix_scratch_free(RadixScratch& s) {
+  if (s.counts) (void)hipFree(s.counts);
+  if (s.offsets) (void)hipFree(s.offsets);
+  if (s.scan.partials) (void)hipFree(s.scan.partials);
+  s = RadixScratch{};
+}
+
+bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t n, const RadixPass* passes,
+                int npasses, RadixScratch& s, hipStream_t st, RadixStats* stats) {
+  if (n == 0 || npasses == 0) return false;
+  radix_scratch_reserve(s, n);
+  const uint32_t nblocks = (uint32_t)blocks_for(n, kTile);
+  const bool hasb = b0 != nullptr;
+  bool flipped = false;
+  for (int p = 0; p < npasses; p++) {
+    const RadixPass ps = passes[p];
+    uint64_t* sa = flipped ? a1 : a0;
+    uint64_t* sb = flipped ? b1 : b0;
+    uint64_t* da = flipped ? a0 : a1;
+    uint64_t* db = flipped ? b0 : b1;
+    if (hasb)
+      hipLaunchKernelGGL(k_radix_count<true>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, n, ps.from_b, ps.shift,
+                         s.counts, nblocks);
+    else
+      hipLaunchKernelGGL(k_radix_count<false>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, n, ps.from_b, ps.shift,
+                         s.counts, nblocks);
+    scan_exclusive_u32(s.counts, s.offsets, (uint64_t)256 * nblocks, s.scan, st);
+    hipEvent_t e0 = (stats && stats->pool) ? stats->pool->next() : nullptr;
+    hipEvent_t e1 = (stats && stats->pool) ? stats->pool->next() : nullptr;
+    if (e0 && e1) VN_HIP_CHECK(hipEventRecord(e0, st));
+    if (hasb)
+      hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, da, db, n, ps.from_b,
+                         ps.shift, s.counts, s.offsets, nblocks);
+    else
+      hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, da, db, n, ps.from_b,
+                         ps.shift, s.counts, s.offsets, nblocks);
+    if (e0 && e1) VN_HIP_CHECK(hipEventRecord(e1, st));
+    if (stats) {
+      stats->launches += 1;
+      stats->bytes += n * (hasb ? 32ull : 16ull);  // read + write of every record
+    }
+    flipped = !flipped;
+  }
+  return flipped;
+}
+
+}  // namespace vn

@@ -1,0 +1,266 @@
+"""Host-side handle of the MI355X engine (one per GPU / worker group).
+
+Mirrors the part of veneur's Worker the hot path owns: ProcessMetric batches go in with
+`ingest`, ImportMetric values with `import_*`, and `flush` returns what Worker.Flush +
+the samplers' Flush methods compute (worker.go:187-298, samplers/samplers.go:125-526).
+"""
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi as A
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _c(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+@dataclass
+class FlushOutput:
+    counter_slot: np.ndarray
+    counter_value: np.ndarray      # int64 Counter.value
+    gauge_slot: np.ndarray
+    gauge_value: np.ndarray
+    histo_slot: np.ndarray
+    histo_stats: np.ndarray        # [n, 8]: weight, min, max, sum, rsum, digest min/max/count
+    histo_quantiles: np.ndarray    # [n, n_percentiles]
+    set_slot: np.ndarray
+    set_estimate: np.ndarray       # uint64 Sketch.Estimate()
+    set_sparse: np.ndarray
+    samples_processed: int
+    samples_imported: int
+
+
+def _arr(ptr, n, dt, shape=None):
+    if n == 0:
+        return np.zeros((0,) if shape is None else (0,) + shape, dt)
+    a = np.ctypeslib.as_array(ptr, shape=(n * (int(np.prod(shape)) if shape else 1),)).copy()
+    a = a.view(dt) if a.dtype != dt else a
+    return a.reshape((n,) + shape) if shape else a
+
+
+class Engine:
+    def __init__(self, capacity, compression=100.0, percentiles=(0.5, 0.9, 0.99, 0.999), max_batch_records=1 << 20,
+                 max_batch_member_bytes=0, device=0, exact_threshold=0):
+        cfg = A.Config()
+        cfg.histo_exact_threshold = int(exact_threshold)
+        cfg.device = device
+        for i, c in enumerate(capacity):
+            cfg.capacity[i] = int(c)
+        cfg.compression = float(compression)
+        cfg.n_percentiles = len(percentiles)
+        for i, p in enumerate(percentiles):
+            cfg.percentiles[i] = float(p)
+        cfg.max_batch_records = int(max_batch_records)
+        cfg.max_batch_member_bytes = int(max_batch_member_bytes)
+        self.percentiles = tuple(float(p) for p in percentiles)
+        self.capacity = tuple(int(c) for c in capacity)
+        self.device = device
+        h = C.c_void_p()
+        rc = A.lib.vn_engine_create(C.byref(cfg), C.byref(h))
+        self.h = h
+        if rc != 0:
+            msg = A.lib.vn_last_error(h).decode() if h else "vn_engine_create failed"
+            if h:
+                A.lib.vn_engine_destroy(h)
+            self.h = None
+            raise EngineError("%s (rc=%d)" % (msg, rc))
+
+    def close(self):
+        if getattr(self, "h", None):
+            A.lib.vn_engine_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc):
+        if rc != 0:
+            raise EngineError("%s (rc=%d)" % (A.lib.vn_last_error(self.h).decode(), rc))
+
+    # ---------------------------------------------------------------- ingest
+    def ingest(self, counters=None, gauges=None, histos=None, sets=None, set_hashes=None):
+        """One ProcessMetric batch (host arrays, arrival order per class).
+
+        counters=(slot, value, rate), gauges=(slot, value), histos=(slot, value, rate),
+        sets=(slot, member_off[n+1], member_bytes) or set_hashes=(slot, hash64)."""
+        b = A.Batch()
+        keep = []
+        if counters is not None:
+            s, v, r = _c(counters[0], np.uint32), _c(counters[1], np.float64), _c(counters[2], np.float32)
+            keep += [s, v, r]
+            b.n_counter, b.counter_slot, b.counter_value, b.counter_rate = len(s), _p(s), _p(v), _p(r)
+        if gauges is not None:
+            s, v = _c(gauges[0], np.uint32), _c(gauges[1], np.float64)
+            keep += [s, v]
+            b.n_gauge, b.gauge_slot, b.gauge_value = len(s), _p(s), _p(v)
+        if histos is not None:
+            s, v, r = _c(histos[0], np.uint32), _c(histos[1], np.float64), _c(histos[2], np.float32)
+            keep += [s, v, r]
+            b.n_histo, b.histo_slot, b.histo_value, b.histo_rate = len(s), _p(s), _p(v), _p(r)
+        if sets is not None:
+            s, o, m = _c(sets[0], np.uint32), _c(sets[1], np.uint32), _c(sets[2], np.uint8)
+            if m.size == 0:
+                m = np.zeros(1, np.uint8)
+            keep += [s, o, m]
+            b.n_set, b.set_slot, b.set_member_off, b.set_member_bytes = len(s), _p(s), _p(o), _p(m)
+        elif set_hashes is not None:
+            s, hs = _c(set_hashes[0], np.uint32), _c(set_hashes[1], np.uint64)
+            keep += [s, hs]
+            b.n_set, b.set_slot, b.set_hash = len(s), _p(s), _p(hs)
+        self._check(A.lib.vn_ingest_host(self.h, C.byref(b)))
+
+    def ingest_device(self, batch):
+        """Ingest a batch whose arrays are already resident in device memory (A.Batch)."""
+        self._check(A.lib.vn_ingest(self.h, C.byref(batch)))
+
+    def import_counters(self, slot, values):
+        s, v = _c(slot, np.uint32), _c(values, np.int64)
+        self._check(A.lib.vn_import_counters(self.h, s.ctypes.data_as(A.u32p), v.ctypes.data_as(A.i64p), len(s)))
+
+    def import_gauges(self, slot, values):
+        s, v = _c(slot, np.uint32), _c(values, np.float64)
+        self._check(A.lib.vn_import_gauges(self.h, s.ctypes.data_as(A.u32p), v.ctypes.data_as(A.f64p), len(s)))
+
+    def sync(self):
+        self._check(A.lib.vn_sync(self.h))
+
+    # ---------------------------------------------------------------- flush
+    def flush_raw(self):
+        out = A.FlushResult()
+        self._check(A.lib.vn_flush(self.h, C.byref(out)))
+        return out
+
+    def flush(self) -> FlushOutput:
+        o = self.flush_raw()
+        npct = len(self.percentiles)
+        return FlushOutput(
+            counter_slot=_arr(o.counter_slot, o.n_counter, np.uint32),
+            counter_value=_arr(o.counter_value, o.n_counter, np.int64),
+            gauge_slot=_arr(o.gauge_slot, o.n_gauge, np.uint32),
+            gauge_value=_arr(o.gauge_value, o.n_gauge, np.float64),
+            histo_slot=_arr(o.histo_slot, o.n_histo, np.uint32),
+            histo_stats=_arr(o.histo_stats, o.n_histo, np.float64, (A.VN_HISTO_STATS,)),
+            histo_quantiles=(_arr(o.histo_quantiles, o.n_histo, np.float64, (npct,)) if npct
+                             else np.zeros((o.n_histo, 0))),
+            set_slot=_arr(o.set_slot, o.n_set, np.uint32),
+            set_estimate=_arr(o.set_estimate, o.n_set, np.uint64),
+            set_sparse=_arr(o.set_sparse, o.n_set, np.uint8),
+            samples_processed=o.samples_processed,
+            samples_imported=o.samples_imported,
+        )
+
+    # ---------------------------------------------------------------- introspection
+    def read_histo(self, slot, cap=4096):
+        m = np.zeros(cap)
+        w = np.zeros(cap)
+        st = np.zeros(A.VN_HISTO_STATS)
+        n = C.c_uint32()
+        self._check(A.lib.vn_read_histo(self.h, slot, m.ctypes.data_as(A.f64p), w.ctypes.data_as(A.f64p), cap,
+                                        C.byref(n), st.ctypes.data_as(A.f64p)))
+        return m[:n.value], w[:n.value], st
+
+    def read_set(self, slot):
+        st = A.SetState()
+        lc = np.zeros(16640, np.uint32)
+        tc = np.zeros(256, np.uint32)
+        regs = np.zeros(A.HLL_M, np.uint8)
+        self._check(A.lib.vn_read_set(self.h, slot, C.byref(st), lc.ctypes.data_as(A.u32p), len(lc),
+                                      tc.ctypes.data_as(A.u32p), len(tc), regs.ctypes.data_as(A.u8p)))
+        d = {k: getattr(st, k) for k, _ in A.SetState._fields_ if k != "pad"}
+        d["list"] = lc[:st.list_count].copy() if st.sparse else np.zeros(0, np.uint32)
+        d["tmp"] = np.sort(tc[:st.tmp_count]) if st.sparse else np.zeros(0, np.uint32)
+        d["registers"] = regs if not st.sparse else None
+        return d
+
+    # ---------------------------------------------------------------- timing
+    def timing_enable(self, on=True):
+        self._check(A.lib.vn_timing_enable(self.h, int(bool(on))))
+
+    def timing(self):
+        t = A.Timing()
+        self._check(A.lib.vn_get_timing(self.h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in A.Timing._fields_}
+
+
+def metro64_device(members, seed=1337, device=0):
+    """metro.Hash64 of every member on the GPU (kernel-level known-answer entry point)."""
+    blob = b"".join(members)
+    off = np.zeros(len(members) + 1, np.uint32)
+    off[1:] = np.cumsum([len(m) for m in members])
+    buf = np.frombuffer(blob if blob else b"\0", np.uint8).copy()
+    out = np.zeros(len(members), np.uint64)
+    rc = A.lib.vn_metro64(device, buf.ctypes.data_as(A.u8p), off.ctypes.data_as(A.u32p), len(members), seed,
+                          out.ctypes.data_as(A.u64p))
+    if rc != 0:
+        raise EngineError("vn_metro64 failed (rc=%d)" % rc)
+    return out
+
+
+def device_count():
+    n = C.c_int(0)
+    return n.value if A.lib.vn_device_count(C.byref(n)) == 0 else 0
+
+
+class DeviceBuffer:
+    """Device allocation owned by Python (bench inputs resident in HBM)."""
+
+    def __init__(self, host_array, device=0):
+        a = np.ascontiguousarray(host_array)
+        self.nbytes = a.nbytes
+        self.ptr = C.c_void_p()
+        if A.lib.vn_device_alloc(device, max(1, a.nbytes), C.byref(self.ptr)) != 0:
+            raise EngineError("device allocation of %d bytes failed" % a.nbytes)
+        if a.nbytes and A.lib.vn_copy_to_device(device, self.ptr, a.ctypes.data_as(C.c_void_p), a.nbytes) != 0:
+            raise EngineError("host to device copy failed")
+
+    def free(self):
+        if self.ptr:
+            A.lib.vn_device_free(self.ptr)
+            self.ptr = None
+
+    __del__ = free
+
+
+def synth(seed=1, n_keys=1000, zipf_s=1.0, mix=(0.4, 0.2, 0.25, 0.15), n_samples=100000, shard=0, n_shards=1,
+          member_universe=50_000_000, rate_half=0.05, rate_tenth=0.05, histo_mu=3.912023005428146,
+          histo_sigma=1.0, threads=0):
+    """Synthetic DogStatsD-shaped stream (include/veneur_amd_synth.h) as numpy arrays."""
+    cfg = A.SynthConfig(seed, n_keys, zipf_s, (C.c_double * 4)(*mix), n_samples, shard, n_shards, member_universe,
+                        rate_half, rate_tenth, histo_mu, histo_sigma, threads)
+    out = A.SynthOut()
+    rc = A.lib.vn_synth_generate(C.byref(cfg), C.byref(out))
+    if rc != 0:
+        raise EngineError("vn_synth_generate failed (rc=%d)" % rc)
+    try:
+        n = [int(out.n[i]) for i in range(4)]
+        cp = lambda p, k, dt: np.ctypeslib.as_array(p, shape=(k,)).astype(dt, copy=True) if k else np.zeros(0, dt)
+        d = {
+            "n_slots": tuple(int(out.n_slots[i]) for i in range(4)),
+            "c_slot": cp(out.c_slot, n[0], np.uint32), "c_val": cp(out.c_val, n[0], np.float64),
+            "c_rate": cp(out.c_rate, n[0], np.float32),
+            "g_slot": cp(out.g_slot, n[1], np.uint32), "g_val": cp(out.g_val, n[1], np.float64),
+            "h_slot": cp(out.h_slot, n[2], np.uint32), "h_val": cp(out.h_val, n[2], np.float64),
+            "h_rate": cp(out.h_rate, n[2], np.float32),
+            "s_slot": cp(out.s_slot, n[3], np.uint32), "s_off": cp(out.s_off, n[3] + 1, np.uint32),
+            "s_bytes": cp(out.s_bytes, int(out.s_nbytes), np.uint8),
+            "key_of_slot": [cp(out.key_of_slot[i], int(out.n_slots[i]), np.uint32) for i in range(4)],
+            "digest_of_slot": [cp(out.digest_of_slot[i], int(out.n_slots[i]), np.uint32) for i in range(4)],
+        }
+    finally:
+        A.lib.vn_synth_free(C.byref(out))
+    return d
