@@ -183,6 +183,7 @@ int vn_device_alloc(int device, uint64_t bytes, void** out);
 int vn_device_free(void* p);
 int vn_copy_to_device(int device, void* dst, const void* src, uint64_t bytes);
 int vn_device_count(int* n);
+int vn_device_synchronize(int device);
 
 /* Timing of the last ingest+flush's kernels on the engine's stream (HIP events):
  * milliseconds of the histo sort passes, of everything, and per-phase counters. */

@@ -445,3 +445,28 @@ def baseline_run(nthreads, nslots, streams, percentiles):
         ptr(arr["s_slot"], u32p), ptr(arr["s_off"], u32p), ptr(arr["s_bytes"], u8p), len(s["s_slot"]),
         ptr(pct, f64p), len(pct), ptr(cs, f64p))
     return secs, float(cs[0])
+
+
+class BaselineOut(C.Structure):
+    _fields_ = [("counter", i64p), ("gauge", f64p), ("histo_q", f64p), ("histo_stats", f64p), ("set_est", u64p),
+                ("touched", u8p * 4)]
+
+
+_sig("or_baseline_set_output", None, C.POINTER(BaselineOut))
+
+
+def baseline_run_full(nthreads, nslots, streams, percentiles):
+    """baseline_run that also returns every flushed value per slot (for full-scale parity)."""
+    nc, ng, nh, ns = (max(1, int(x)) for x in nslots)
+    out = {"counter": np.zeros(nc, np.int64), "gauge": np.zeros(ng), "histo_q": np.zeros((nh, len(percentiles))),
+           "histo_stats": np.zeros((nh, 8)), "set_est": np.zeros(ns, np.uint64),
+           "touched": [np.zeros(n, np.uint8) for n in (nc, ng, nh, ns)]}
+    bo = BaselineOut(ptr(out["counter"], i64p), ptr(out["gauge"], f64p), ptr(out["histo_q"], f64p),
+                     ptr(out["histo_stats"], f64p), ptr(out["set_est"], u64p),
+                     (u8p * 4)(*[ptr(t, u8p) for t in out["touched"]]))
+    lib.or_baseline_set_output(C.byref(bo))
+    try:
+        secs, cs = baseline_run(nthreads, nslots, streams, percentiles)
+    finally:
+        lib.or_baseline_set_output(None)
+    return secs, cs, out

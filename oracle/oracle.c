@@ -1383,6 +1383,7 @@ typedef struct {
   const double* pct; int n_pct;
   uint32_t nc, ng, nh, ns;
   double checksum;
+  const or_baseline_out* out;
 } bl_arg;
 static inline int owns(uint32_t slot, int cls, int tid, int n) {
   uint32_t h = (slot * 2654435761u) ^ (uint32_t)cls;
@@ -1401,17 +1402,47 @@ static void* bl_thread(void* p) {
     if (owns(a->s_slot[i], 3, a->tid, a->nthreads))
       or_hll_insert(worker_set(w, a->s_slot[i]), a->s_bytes + a->s_off[i], a->s_off[i + 1] - a->s_off[i]);
   /* flush (generateInterMetrics: Counter/Gauge value, Histo quantiles, Set Estimate) */
+  const or_baseline_out* o = a->out;
   double cs = 0;
-  for (uint32_t s = 0; s < a->nc; s++) if (w->ctouch[s]) cs += (double)w->cval[s];
-  for (uint32_t s = 0; s < a->ng; s++) if (w->gtouch[s]) cs += w->gval[s];
+  for (uint32_t s = 0; s < a->nc; s++)
+    if (w->ctouch[s]) {
+      cs += (double)w->cval[s];
+      if (o && o->counter) o->counter[s] = w->cval[s];
+      if (o && o->touched[0]) o->touched[0][s] = 1;
+    }
+  for (uint32_t s = 0; s < a->ng; s++)
+    if (w->gtouch[s]) {
+      cs += w->gval[s];
+      if (o && o->gauge) o->gauge[s] = w->gval[s];
+      if (o && o->touched[1]) o->touched[1][s] = 1;
+    }
   for (uint32_t s = 0; s < a->nh; s++)
     if (w->htouch[s]) {
       cs += w->h[s].weight;
-      for (int k = 0; k < a->n_pct; k++) cs += or_td_quantile(w->h[s].td, a->pct[k]);
+      for (int k = 0; k < a->n_pct; k++) {
+        double q = or_td_quantile(w->h[s].td, a->pct[k]);
+        cs += q;
+        if (o && o->histo_q) o->histo_q[(size_t)s * a->n_pct + k] = q;
+      }
+      if (o && o->histo_stats) or_worker_histo_stats(w, s, o->histo_stats + (size_t)s * 8);
+      if (o && o->touched[2]) o->touched[2][s] = 1;
     }
-  for (uint32_t s = 0; s < a->ns; s++) if (w->stouch[s]) cs += (double)or_hll_estimate(w->s[s]);
+  for (uint32_t s = 0; s < a->ns; s++)
+    if (w->stouch[s]) {
+      uint64_t est = or_hll_estimate(w->s[s]);
+      cs += (double)est;
+      if (o && o->set_est) o->set_est[s] = est;
+      if (o && o->touched[3]) o->touched[3][s] = 1;
+    }
   a->checksum = cs;
   return NULL;
+}
+
+static or_baseline_out g_bl_out;
+static int g_bl_out_set = 0;
+void or_baseline_set_output(const or_baseline_out* out) {
+  if (out) { g_bl_out = *out; g_bl_out_set = 1; }
+  else g_bl_out_set = 0;
 }
 double or_baseline_run(int nthreads, uint32_t nc, uint32_t ng, uint32_t nh, uint32_t ns,
                        const uint32_t* c_slot, const double* c_val, const float* c_rate, size_t n_c,
@@ -1432,6 +1463,7 @@ double or_baseline_run(int nthreads, uint32_t nc, uint32_t ng, uint32_t nh, uint
     a->s_slot = s_slot; a->s_off = s_off; a->s_bytes = s_bytes; a->n_s = n_s;
     a->pct = pct; a->n_pct = n_pct;
     a->nc = nc; a->ng = ng; a->nh = nh; a->ns = ns;
+    a->out = g_bl_out_set ? &g_bl_out : NULL;
   }
   struct timespec t0, t1;
   clock_gettime(CLOCK_MONOTONIC, &t0);

@@ -126,6 +126,19 @@ uint64_t or_worker_set_estimate(or_worker* w, uint32_t slot);
 or_td* or_worker_histo_digest(or_worker* w, uint32_t slot);
 or_hll* or_worker_set_sketch(or_worker* w, uint32_t slot);
 
+/* Optional outputs of or_baseline_run (any pointer may be NULL): per slot, the flushed
+ * Counter value, Gauge value, Histo quantiles [slot][n_pct] and stats [slot][8], Set
+ * estimate, and whether the slot was touched. */
+typedef struct {
+  int64_t* counter;
+  double* gauge;
+  double* histo_q;
+  double* histo_stats;
+  uint64_t* set_est;
+  uint8_t* touched[4];
+} or_baseline_out;
+void or_baseline_set_output(const or_baseline_out* out);
+
 /* Multi-threaded CPU baseline: nthreads workers, records routed by digest % nthreads.
  * Runs ProcessMetric for every record, then the flush (quantiles for every touched histo
  * at the given percentiles, Estimate for every touched set).  Returns seconds elapsed. */

@@ -123,6 +123,7 @@ _sig("vn_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(vp))
 _sig("vn_device_free", C.c_int, vp)
 _sig("vn_copy_to_device", C.c_int, C.c_int, vp, vp, C.c_uint64)
 _sig("vn_device_count", C.c_int, C.POINTER(C.c_int))
+_sig("vn_device_synchronize", C.c_int, C.c_int)
 _sig("vn_timing_enable", C.c_int, vp, C.c_int)
 _sig("vn_get_timing", C.c_int, vp, C.POINTER(Timing))
 _sig("vn_synth_generate", C.c_int, C.POINTER(SynthConfig), C.POINTER(SynthOut))
@@ -133,5 +134,5 @@ EXPORTED = [
     "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
     "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_flush", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
-    "vn_device_count", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
+    "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
 ]

@@ -146,19 +146,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->s_start, cs);
   dalloc(e->s_end, cs);
 
-  // staging (device) and pinned host stage
-  DeviceBatch& d = e->dstage;
-  dalloc(d.c_slot, R); dalloc(d.c_val, R); dalloc(d.c_rate, R);
-  dalloc(d.g_slot, R); dalloc(d.g_val, R);
-  dalloc(d.h_slot, R); dalloc(d.h_val, R); dalloc(d.h_rate, R);
-  dalloc(d.s_slot, R); dalloc(d.s_off, R + 1); dalloc(d.s_bytes, e->max_member_bytes);
-  vn_stage& p = e->pstage;
-  p.capacity = R;
-  p.member_bytes_capacity = e->max_member_bytes;
-  halloc(p.counter_slot, R); halloc(p.counter_value, R); halloc(p.counter_rate, R);
-  halloc(p.gauge_slot, R); halloc(p.gauge_value, R);
-  halloc(p.histo_slot, R); halloc(p.histo_value, R); halloc(p.histo_rate, R);
-  halloc(p.set_slot, R); halloc(p.set_member_off, R + 1); halloc(p.set_member_bytes, e->max_member_bytes);
+  // staging buffers are allocated on first use (ensure_device_stage / ensure_pinned_stage)
 
   // flush outputs
   dalloc(e->f_pos, (size_t)capmax + 1);
@@ -182,6 +170,30 @@ void create_impl(vn_engine* e) {
   radix_scratch_reserve(e->rs, std::max<uint64_t>(e->h_sort_cap, cs ? R : 0));
   init_state(e);
   VN_HIP_CHECK(hipStreamSynchronize(st));
+}
+
+// device staging for host-provided batches (vn_ingest_host / vn_submit / imports)
+void ensure_device_stage(vn_engine* e) {
+  DeviceBatch& d = e->dstage;
+  if (d.c_slot) return;
+  const uint64_t R = e->max_records;
+  dalloc(d.c_slot, R); dalloc(d.c_val, R); dalloc(d.c_rate, R);
+  dalloc(d.g_slot, R); dalloc(d.g_val, R);
+  dalloc(d.h_slot, R); dalloc(d.h_val, R); dalloc(d.h_rate, R);
+  dalloc(d.s_slot, R); dalloc(d.s_off, R + 1); dalloc(d.s_bytes, e->max_member_bytes);
+}
+
+// pinned host staging the Go side appends ProcessMetric records to (vn_stage_acquire)
+void ensure_pinned_stage(vn_engine* e) {
+  vn_stage& p = e->pstage;
+  if (p.counter_slot) return;
+  const uint64_t R = e->max_records;
+  p.capacity = R;
+  p.member_bytes_capacity = e->max_member_bytes;
+  halloc(p.counter_slot, R); halloc(p.counter_value, R); halloc(p.counter_rate, R);
+  halloc(p.gauge_slot, R); halloc(p.gauge_value, R);
+  halloc(p.histo_slot, R); halloc(p.histo_value, R); halloc(p.histo_rate, R);
+  halloc(p.set_slot, R); halloc(p.set_member_off, R + 1); halloc(p.set_member_bytes, e->max_member_bytes);
 }
 
 void destroy_impl(vn_engine* e) {
@@ -275,6 +287,7 @@ void ingest_host(vn_engine* e, const vn_batch* b) {
     if (!(b->counter_rate[i] > 0.0f && b->counter_rate[i] <= 1.0f))
       throw std::invalid_argument("sample rate must be >0 and <=1");
   hipStream_t st = e->st;
+  ensure_device_stage(e);
   DeviceBatch& d = e->dstage;
   vn_batch db{};
   db.n_counter = b->n_counter;
@@ -367,8 +380,10 @@ const char* vn_last_error(const vn_engine* e) { return e ? e->err.c_str() : "nul
 
 int vn_stage_acquire(vn_engine* e, vn_stage* out) {
   if (!e || !out) return VN_EINVAL;
-  *out = e->pstage;
-  return VN_OK;
+  return guarded(e, [&] {
+    ensure_pinned_stage(e);
+    *out = e->pstage;
+  });
 }
 
 int vn_submit(vn_engine* e, const vn_batch_counts* c) {
@@ -399,6 +414,7 @@ int vn_import_counters(vn_engine* e, const uint32_t* slot, const int64_t* value,
   return guarded(e, [&] {
     if (n > e->max_records) throw std::invalid_argument("import batch too large");
     check_slots_host(slot, n, e->cap[VN_COUNTER], "counter");
+    ensure_device_stage(e);
     h2d(e->dstage.c_slot, slot, n, e->st);
     h2d(reinterpret_cast<int64_t*>(e->dstage.c_val), value, n, e->st);
     import_counters(e, n, e->dstage.c_slot, reinterpret_cast<const int64_t*>(e->dstage.c_val));
@@ -411,6 +427,7 @@ int vn_import_gauges(vn_engine* e, const uint32_t* slot, const double* value, ui
   return guarded(e, [&] {
     if (n > e->max_records) throw std::invalid_argument("import batch too large");
     check_slots_host(slot, n, e->cap[VN_GAUGE], "gauge");
+    ensure_device_stage(e);
     h2d(e->dstage.g_slot, slot, n, e->st);
     h2d(e->dstage.g_val, value, n, e->st);
     ingest_gauges(e, n, e->dstage.g_slot, e->dstage.g_val);
@@ -561,5 +578,9 @@ int vn_copy_to_device(int device, void* dst, const void* src, uint64_t bytes) {
   return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? VN_OK : VN_EHIP;
 }
 int vn_device_count(int* n) { return hipGetDeviceCount(n) == hipSuccess ? VN_OK : VN_EHIP; }
+int vn_device_synchronize(int device) {
+  if (hipSetDevice(device) != hipSuccess) return VN_EHIP;
+  return hipDeviceSynchronize() == hipSuccess ? VN_OK : VN_EHIP;
+}
 
 }  // extern "C"
