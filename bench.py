@@ -84,19 +84,12 @@ def main():
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof runs)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        dist = tdist
-
     import veneur_amd as V
     import veneur_amd._abi as A
+    from veneur_amd.dist import Group, env_world
+
+    world, rank, local_rank = env_world()
+    group = Group(backend="nccl", local_rank=local_rank)  # world 1: no process group
 
     # ---- synthetic C3 shard stream (host), then resident in HBM
     t0 = time.time()
@@ -143,15 +136,10 @@ def main():
         return eng.flush_raw()
 
     def sync():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-        else:
-            A.lib.vn_device_synchronize(local_rank)
+        A.lib.vn_device_synchronize(local_rank)
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        group.barrier()
 
     for _ in range(args.warmup):
         step()
@@ -169,16 +157,8 @@ def main():
     elapsed = time.perf_counter() - t0
     for _ in range(args.profile_steps):
         step()
-    if dist is not None:
-        import torch
-        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        tot = torch.tensor([float(args.samples)], dtype=torch.float64, device="cuda")
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        total_samples = float(tot.item()) * args.steps
-    else:
-        total_samples = float(args.samples) * args.steps
+    elapsed = group.max(elapsed)                                  # max over ranks
+    total_samples = group.sum(float(args.samples)) * args.steps  # every rank's shard stream
     ms_per_step = elapsed * 1e3 / args.steps
     value = total_samples / elapsed
 
@@ -268,8 +248,7 @@ def main():
     eng.close()
     for b in bufs:
         b.free()
-    if dist is not None:
-        dist.destroy_process_group()
+    group.close()
 
 
 if __name__ == "__main__":

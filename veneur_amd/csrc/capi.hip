@@ -80,6 +80,8 @@ void create_impl(vn_engine* e) {
   dalloc(e->gseq, cg); dzero(e->gseq, cg, st);
   dalloc(e->gval, cg); dzero(e->gval, cg, st);
   dalloc(e->gtouch, cg); dzero(e->gtouch, cg, st);
+  dalloc(e->pk, (cc || cg) ? R : 0);
+  dalloc(e->pp, (cc || cg) ? R : 0);
 
   dalloc(e->hst, (size_t)ch * VN_HISTO_STATS);
   dalloc(e->hncent, ch); dzero(e->hncent, ch, st);
@@ -167,7 +169,7 @@ void create_impl(vn_engine* e) {
                               hipMemcpyHostToDevice, st));
   halloc(e->hf_cnt, 16);
 
-  radix_scratch_reserve(e->rs, std::max<uint64_t>(e->h_sort_cap, cs ? R : 0));
+  radix_scratch_reserve(e->rs, std::max<uint64_t>(e->h_sort_cap, (cs || cc || cg) ? R : 0));
   init_state(e);
   VN_HIP_CHECK(hipStreamSynchronize(st));
 }
@@ -198,7 +200,7 @@ void ensure_pinned_stage(vn_engine* e) {
 
 void destroy_impl(vn_engine* e) {
   if (e->st) (void)hipStreamSynchronize(e->st);
-  dfree(e->cval); dfree(e->ctouch); dfree(e->gseq); dfree(e->gval); dfree(e->gtouch);
+  dfree(e->cval); dfree(e->ctouch); dfree(e->gseq); dfree(e->gval); dfree(e->gtouch); dfree(e->pk); dfree(e->pp);
   dfree(e->hst); dfree(e->hncent); dfree(e->hcur); dfree(e->htouch);
   for (int b = 0; b < 2; b++) { dfree(e->cmean[b]); dfree(e->cw[b]); }
   dfree(e->h_bt); dfree(e->h_pos); dfree(e->h_tl); dfree(e->h_cnt); dfree(e->h_oldcnt); dfree(e->h_oldoff);
@@ -249,6 +251,7 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
   const bool tm = e->timing;
   if (tm) {
     e->pool.used = 0;
+    e->rstat_c = RadixStats{&e->pool, 0, 0};
     e->rstat_h = RadixStats{&e->pool, 0, 0};
     e->rstat_s = RadixStats{&e->pool, 0, 0};
     VN_HIP_CHECK(hipEventRecord(e->ev[0], st));
@@ -460,8 +463,8 @@ int vn_flush(vn_engine* e, vn_flush_result* out) {
         tot += ms;
       }
       t.ms_radix_scatter_total = tot;
-      t.radix_scatter_launches = e->rstat_h.launches + e->rstat_s.launches;
-      t.radix_scatter_bytes = e->rstat_h.bytes + e->rstat_s.bytes;
+      t.radix_scatter_launches = e->rstat_c.launches + e->rstat_h.launches + e->rstat_s.launches;
+      t.radix_scatter_bytes = e->rstat_c.bytes + e->rstat_h.bytes + e->rstat_s.bytes;
     }
   });
 }

@@ -47,6 +47,9 @@ struct vn_engine {
   double* gval = nullptr;
   uint32_t* gtouch = nullptr;
   uint64_t seq_base = 0;
+  // counter / gauge partition scratch (slot, payload) [max_records]
+  uint32_t* pk = nullptr;
+  uint64_t* pp = nullptr;
   // ---- histos
   double* hst = nullptr;
   uint32_t* hncent = nullptr;
@@ -149,5 +152,5 @@ struct vn_engine {
   vn::EventPool pool;
   std::vector<hipEvent_t> pool_storage;
   vn_timing last{};
-  vn::RadixStats rstat_h, rstat_s;
+  vn::RadixStats rstat_c, rstat_h, rstat_s;
 };

@@ -1,5 +1,7 @@
 // histo.h -- shared declarations of the t-digest (Histo) kernels.
 #pragma once
+#include <stdexcept>
+
 #include "kernels.h"
 
 namespace vn {

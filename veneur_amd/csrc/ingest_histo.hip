@@ -500,20 +500,41 @@ __global__ void k_histo_hot_keys(const uint32_t* __restrict__ cnt, const uint32_
   }
 }
 
-// copy the hot remainder of each hot key into the batch-merge sort input
-__global__ void k_histo_gather_hot(const uint32_t* __restrict__ hotlist, const uint32_t* __restrict__ tl,
-                                   const uint32_t* __restrict__ start, const uint32_t* __restrict__ ex,
-                                   const uint32_t* __restrict__ hotcnt, const uint32_t* __restrict__ hotoff,
-                                   const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
-                                   uint64_t* __restrict__ A2, uint64_t* __restrict__ B2) {
-  uint32_t k = hotlist[blockIdx.x];
-  uint32_t s = tl[k];
-  uint64_t src = (uint64_t)start[s] + ex[k];
-  uint64_t dst = hotoff[k];
-  uint32_t cnt = hotcnt[k];
-  for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-    A2[dst + i] = ordered_bits(bitsd(A[src + i]));
-    B2[dst + i] = B[src + i];
+// copy the hot remainder of each hot key into the batch-merge sort input: output record o
+// belongs to the touched key k with hotoff[k] <= o < hotoff[k + 1] (a block of 4096 outputs
+// spans few keys, so each thread searches only between the block's first and last key)
+__device__ __forceinline__ uint32_t last_le(const uint32_t* off, uint32_t lo, uint32_t hi, uint32_t o) {
+  while (hi - lo > 1) {  // last k in [lo, hi) with off[k] <= o
+    uint32_t m = (lo + hi) >> 1;
+    if (off[m] <= o) lo = m;
+    else hi = m;
+  }
+  return lo;
+}
+__global__ __launch_bounds__(kBlock) void k_histo_gather_hot(uint32_t ntouched, uint64_t nhotrec,
+                                                             const uint32_t* __restrict__ tl,
+                                                             const uint32_t* __restrict__ start,
+                                                             const uint32_t* __restrict__ ex,
+                                                             const uint32_t* __restrict__ hotoff,
+                                                             const uint64_t* __restrict__ A,
+                                                             const uint64_t* __restrict__ B,
+                                                             uint64_t* __restrict__ A2, uint64_t* __restrict__ B2) {
+  __shared__ uint32_t s_k[2];
+  const uint64_t base = (uint64_t)blockIdx.x * kTile;
+  if (threadIdx.x < 2) {
+    uint64_t o = base + (threadIdx.x ? (uint64_t)kTile - 1 : 0);
+    if (o >= nhotrec) o = nhotrec - 1;
+    s_k[threadIdx.x] = last_le(hotoff, 0, ntouched, (uint32_t)o);
+  }
+  __syncthreads();
+  const uint32_t k0 = s_k[0], k1 = s_k[1] + 1;
+  for (uint32_t j = threadIdx.x; j < (uint32_t)kTile; j += kBlock) {
+    const uint64_t o = base + j;
+    if (o >= nhotrec) break;
+    const uint32_t k = last_le(hotoff, k0, k1, (uint32_t)o);
+    const uint64_t src = (uint64_t)start[tl[k]] + ex[k] + (o - hotoff[k]);
+    A2[o] = ordered_bits(bitsd(A[src]));
+    B2[o] = B[src];
   }
 }
 
@@ -586,8 +607,9 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   }
   const uint64_t n2 = nhotrec + nold;
   if (n2 > e->h_sort_cap) throw std::runtime_error("histo batch exceeds sort capacity");
-  hipLaunchKernelGGL(k_histo_gather_hot, dim3(nhot), dim3(256), 0, st, e->h_hotlist, e->h_tl, e->h_start, e->h_ex,
-                     e->h_hotcnt, e->h_hotoff, As, Bs, Ao, Bo);
+  if (nhotrec)
+    hipLaunchKernelGGL(k_histo_gather_hot, dim3(blocks_for(nhotrec, kTile)), dim3(kBlock), 0, st, ntouched, nhotrec,
+                       e->h_tl, e->h_start, e->h_ex, e->h_hotoff, As, Bs, Ao, Bo);
   hipLaunchKernelGGL(k_histo_append_old, dim3(nhot), dim3(256), 0, st, e->h_tl2, e->h_oldoff, e->hncent, e->hcur,
                      e->cmean[0], e->cmean[1], e->cap_cent, nhotrec, Ao, Bo);
   RadixPass passes[16];

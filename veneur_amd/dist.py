@@ -1,0 +1,101 @@
+"""Multi-GPU plumbing for the key-sharded flush window (one process per GPU).
+
+Keys are partitioned the way veneur routes them to workers -- FNV-1a-32 digest of
+(name, type, joined tags) modulo the number of consumers (server.go:655,
+samplers/parser.go:213-304) -- so every rank aggregates a disjoint key set and the data
+path needs no collective.  The only collectives are the bench's control plane: a barrier
+around the timed region, the max of the per-rank elapsed times and the sum of samples.
+They run over RCCL ("nccl") on GPUs and over gloo on CPU (the multi-process tests).
+"""
+import os
+
+import numpy as np
+
+
+def env_world():
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def shard_of(digest, n_shards):
+    """Owner rank of each key: digest % n (veneur's worker routing applied to GPUs)."""
+    return (np.asarray(digest, dtype=np.uint32) % np.uint32(n_shards)).astype(np.int64)
+
+
+class Group:
+    """torch.distributed process group wrapper; world_size 1 means no group at all."""
+
+    def __init__(self, backend=None, local_rank=0):
+        self.world, self.rank, _ = env_world()
+        self.dist = None
+        self.device = None
+        if self.world <= 1:
+            return
+        import torch
+        import torch.distributed as td
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local_rank)
+            self.device = torch.device("cuda", local_rank)
+            td.init_process_group("nccl", device_id=self.device)
+        else:
+            self.device = torch.device("cpu")
+            td.init_process_group("gloo")
+        self.dist = td
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def _reduce(self, x, op):
+        if self.dist is None:
+            return float(x)
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64, device=self.device)
+        self.dist.all_reduce(t, op=op)
+        return float(t.item())
+
+    def max(self, x):
+        return self._reduce(x, self.dist.ReduceOp.MAX if self.dist else None)
+
+    def sum(self, x):
+        return self._reduce(x, self.dist.ReduceOp.SUM if self.dist else None)
+
+    def gather_object(self, obj):
+        """All ranks' objects on every rank (small control data only)."""
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+            self.dist = None
+
+
+def route_stream(d, rank, n_shards):
+    """The records of a synthetic stream (engine.synth output) whose key this rank owns,
+    in arrival order, keeping the stream's slot numbering: what veneur's per-worker
+    channel would deliver to consumer `rank` of `n_shards`."""
+    own = [shard_of(d["digest_of_slot"][c], n_shards) == rank for c in range(4)]
+    out = dict(d)
+    for c, (sk, cols) in enumerate((("c_slot", ("c_val", "c_rate")), ("g_slot", ("g_val",)),
+                                    ("h_slot", ("h_val", "h_rate")))):
+        m = own[c][d[sk]] if len(d[sk]) else np.zeros(0, bool)
+        out[sk] = d[sk][m]
+        for col in cols:
+            out[col] = d[col][m]
+    m = own[3][d["s_slot"]] if len(d["s_slot"]) else np.zeros(0, bool)
+    off = d["s_off"].astype(np.int64)
+    idx = np.nonzero(m)[0]
+    lens = off[idx + 1] - off[idx]
+    new_off = np.zeros(len(idx) + 1, np.int64)
+    np.cumsum(lens, out=new_off[1:])
+    take = np.repeat(off[idx] - new_off[:-1], lens) + np.arange(new_off[-1])
+    out["s_slot"] = d["s_slot"][m]
+    out["s_off"] = new_off.astype(np.uint32)
+    out["s_bytes"] = d["s_bytes"][take]
+    return out
