@@ -77,6 +77,8 @@ _sig("or_hll_decode_hash", None, C.c_uint32, C.c_uint8, C.c_uint8, u32p, u8p)
 _sig("or_hll_get_pos_val", None, C.c_uint64, C.c_uint8, u64p, u8p)
 _sig("or_td_new", C.c_void_p, C.c_double)
 _sig("or_td_free", None, C.c_void_p)
+_sig("or_td_add_batch", C.c_int, C.c_void_p, f64p, f64p, C.c_size_t)
+_sig("or_td_add_many", C.c_long, C.c_void_p, f64p, f64p, C.c_size_t)
 _sig("or_td_add", C.c_int, C.c_void_p, C.c_double, C.c_double)
 _sig("or_td_quantile", C.c_double, C.c_void_p, C.c_double)
 _sig("or_td_cdf", C.c_double, C.c_void_p, C.c_double)
@@ -285,6 +287,19 @@ class MergingDigest:
     def add(self, v, w=1.0):
         if lib.or_td_add(self.td, v, w) != 0:
             raise ValueError("invalid value added")
+
+    def add_many(self, values, weights):
+        v = np.ascontiguousarray(values, np.float64)
+        w = np.ascontiguousarray(weights, np.float64)
+        if lib.or_td_add_many(self.td, ptr(v, f64p), ptr(w, f64p), len(v)) >= 0:
+            raise ValueError("invalid value added")
+
+    def add_batch(self, values, weights):
+        """Study helper (not a reference function): one mergeAllTemps of all samples."""
+        v = np.ascontiguousarray(values, np.float64)
+        w = np.ascontiguousarray(weights, np.float64)
+        if lib.or_td_add_batch(self.td, ptr(v, f64p), ptr(w, f64p), len(v)) != 0:
+            raise MemoryError("or_td_add_batch")
 
     def quantile(self, q):
         if q < 0 or q > 1:

@@ -925,6 +925,35 @@ static void td_merge_all_temps(or_td* td) {
   td->main_weight = total_weight;
 }
 
+/* Study helper, not a reference function: merge n samples into the digest with ONE
+ * mergeAllTemps (after merging whatever is pending), the way the engine's hot-key batch
+ * path does.  Used by tools/tdigest_study.py to size the exact-replay threshold. */
+int or_td_add_batch(or_td* td, const double* v, const double* w, size_t n) {
+  td_merge_all_temps(td);
+  if (n == 0) return 0;
+  centroid* keep = td->temp;
+  size_t keepcap = td->captemp;
+  centroid* big = (centroid*)malloc(n * sizeof(centroid));
+  if (!big) return -1;
+  double tw = 0.0;
+  for (size_t i = 0; i < n; i++) {
+    big[i].mean = v[i];
+    big[i].weight = w[i];
+    tw += w[i];
+    td->min = go_min(td->min, v[i]);
+    td->max = go_max(td->max, v[i]);
+  }
+  td->temp = big;
+  td->captemp = n;
+  td->ntemp = n;
+  td->temp_weight = tw;
+  td_merge_all_temps(td);
+  free(big);
+  td->temp = keep;
+  td->captemp = keepcap;
+  return 0;
+}
+
 int or_td_add(or_td* td, double value, double weight) { /* merging_digest.go:97-118 */
   if (isnan(value) || isinf(value) || weight <= 0) return -1; /* Go: panic */
   if (td->ntemp == td->captemp) td_merge_all_temps(td);
@@ -935,6 +964,12 @@ int or_td_add(or_td* td, double value, double weight) { /* merging_digest.go:97-
   td->ntemp++;
   td->temp_weight += weight;
   return 0;
+}
+/* convenience: Add() every sample in order; returns the index of the first rejected one, or -1 */
+long or_td_add_many(or_td* td, const double* v, const double* w, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    if (or_td_add(td, v[i], w[i]) != 0) return (long)i;
+  return -1;
 }
 double or_td_cdf(or_td* td, double value) { /* merging_digest.go:247-279 */
   td_merge_all_temps(td);

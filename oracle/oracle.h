@@ -92,6 +92,10 @@ double or_td_count(const or_td* td);
 void or_td_merge(or_td* td, or_td* other, const int64_t* perm);
 size_t or_td_centroids(or_td* td, double* means, double* weights, size_t cap); /* merges temps */
 size_t or_td_temp_len(const or_td* td);
+/* study helper (not in the reference): one mergeAllTemps of n samples, as the engine's
+ * hot-key batch merge does */
+int or_td_add_batch(or_td* td, const double* v, const double* w, size_t n);
+long or_td_add_many(or_td* td, const double* v, const double* w, size_t n); /* Add() in order */
 /* gob codec of (Centroids, compression, min, max); encode returns bytes written (0 = cap short) */
 size_t or_td_gob_encode(or_td* td, uint8_t* out, size_t cap);
 int or_td_gob_decode(or_td* td, const uint8_t* data, size_t len);

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Per-phase cycle profile of the exact t-digest replay (GPU box; profiling build).
+
+Runs one hot key (and optionally many cold keys alongside it) through the engine built
+with -DVN_EXACT_PROF (make -C veneur_amd prof) and prints the clock64 cycles block 0 spent
+per merge phase.  Usage: VN_LIB=libveneur_amd_prof.so python tools/exact_profile.py
+"""
+import ctypes as C
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("VN_LIB", "libveneur_amd_prof.so")
+import veneur_amd as V  # noqa: E402
+import veneur_amd._abi as A  # noqa: E402
+
+A.lib.vn_prof_exact_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+NAMES = ["tempW", "rank+pos", "prefix+kin", "chain", "welford", "merges", "elements", "centroids", "kernel"]
+
+
+def run(n_hot, n_cold_keys, cold_per_key, seed=1):
+    rng = np.random.default_rng(seed)
+    nk = 1 + n_cold_keys
+    slots = np.concatenate([np.zeros(n_hot, np.uint32),
+                            np.repeat(np.arange(1, nk, dtype=np.uint32), cold_per_key)])
+    rng.shuffle(slots[n_hot:])
+    vals = np.exp(rng.normal(3.9, 1.0, len(slots)))
+    rates = np.ones(len(slots), np.float32)
+    with V.Engine((1, 1, nk, 1), compression=100.0, percentiles=(0.5, 0.99),
+                  max_batch_records=len(slots) + 1) as e:
+        e.timing_enable(True)
+        buf = (C.c_ulonglong * 16)()
+        A.lib.vn_prof_exact_read(buf, 1)
+        t0 = time.perf_counter()
+        e.ingest(histos=(slots, vals, rates))
+        e.sync()
+        wall = time.perf_counter() - t0
+        A.lib.vn_prof_exact_read(buf, 1)
+        e.flush()
+        t = e.timing()
+    p = list(buf)
+    merges = max(1, p[5])
+    out = {"n_hot": n_hot, "cold_keys": n_cold_keys, "ms_ingest_histo": round(t["ms_ingest_histo"], 3), "wall_ms": round(wall * 1e3, 3),
+           "merges": p[5], "avg_elements": round(p[6] / merges, 1), "avg_centroids": round(p[7] / merges, 1),
+           "kernel_cycles_block0": p[8]}
+    for i in range(5):
+        out["cyc_per_merge_" + NAMES[i]] = round(p[i] / merges, 1)
+    out["cyc_per_merge_total"] = round(sum(p[:5]) / merges, 1)
+    print(out, flush=True)
+
+
+if __name__ == "__main__":
+    run(32768, 0, 0)
+    run(32768, 2000, 100)
+    run(32768, 100000, 150)

@@ -8,7 +8,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libveneur_amd.so")
+# VN_LIB selects a variant built from the same sources (tools only: the profiling build)
+LIB_PATH = os.path.join(HERE, os.environ.get("VN_LIB", "libveneur_amd.so"))
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

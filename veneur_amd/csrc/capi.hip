@@ -128,6 +128,9 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_hotoff, (size_t)touch_max + 1);
   dalloc(e->h_hotlist, touch_max);
   dalloc(e->h_tl2, touch_max);
+  dalloc(e->h_ccnt, touch_max);
+  dalloc(e->h_coff, (size_t)touch_max + 1);
+  dalloc(e->h_tw, e->h_sort_cap);
 
   dalloc(e->smode, cs); dzero(e->smode, cs, st);
   dalloc(e->sbase, cs); dzero(e->sbase, cs, st);
@@ -209,7 +212,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->ch_lastk); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
   dfree(e->hseen); dfree(e->hpend); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
-  dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2);
+  dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);
   dfree(e->smode); dfree(e->sbase); dfree(e->snz); dfree(e->slc); dfree(e->slb); dfree(e->slast); dfree(e->stc);
   dfree(e->stouch); dfree(e->stmp); dfree(e->sarena); dfree(e->sR0); dfree(e->sR1); dfree(e->s_bt);
   dfree(e->s_pos); dfree(e->s_tl); dfree(e->s_cnt); dfree(e->s_start); dfree(e->s_end);

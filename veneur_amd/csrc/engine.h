@@ -96,6 +96,9 @@ struct vn_engine {
   uint32_t* h_hotoff = nullptr;
   uint32_t* h_hotlist = nullptr;
   uint32_t* h_tl2 = nullptr;     // slots of hot keys
+  uint32_t* h_ccnt = nullptr;    // per touched key: pure chunks to pre-sort
+  uint32_t* h_coff = nullptr;    // scan of h_ccnt (touched + 1)
+  double* h_tw = nullptr;        // per chunk (at its first record): Add-order weight sum
 
   // ---- sets
   uint8_t* smode = nullptr;      // 0 sparse, 1 dense

@@ -243,7 +243,7 @@ void flush_all(vn_engine* e, vn_flush_result* out) {
     xc.hpw = e->hpw;
     xc.err = e->h_err;
     xc.flush_mode = 1;
-    launch_histo_exact(xc, st);
+    launch_histo_exact(xc, st, nullptr, 0);
     hipLaunchKernelGGL(k_flush_histo, dim3(blocks_for(n[2], 128)), dim3(128), 0, st, e->f_cnt + 2, e->f_list[2],
                        e->hst, e->hncent, e->hcur, e->cmean[0], e->cmean[1], e->cw[0], e->cw[1], e->cap_cent,
                        e->d_pct, e->cfg.n_percentiles, e->f_hstats, e->f_hq);

@@ -28,10 +28,18 @@ struct ExactCtx {
   double* hpw;
   uint32_t* err;
   int flush_mode;            // 1: only merge pending temps (Quantile's mergeAllTemps)
+  // pure-chunk pre-sort (ingest only): per key chunk count and scan, sorted chunk
+  // means/weights at the chunk's record positions, Add-order weight sum at its first record
+  uint32_t* ccnt;
+  uint32_t* coff;
+  double* csv;
+  double* csw;
+  double* ctw;
 };
 
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap);
-void launch_histo_exact(const ExactCtx& x, hipStream_t st);
+// max_chunks: upper bound on the pure chunks of the batch (grid of the chunk sorter)
+void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks);
 // estimateTempBuffer (merging_digest.go:87-93)
 inline uint32_t temp_buffer_cap(double compression) {
   double c = compression < 20 ? 20 : (compression > 925 ? 925 : compression);

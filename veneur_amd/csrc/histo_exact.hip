@@ -26,6 +26,17 @@
 
 namespace vn {
 
+#ifdef VN_EXACT_PROF
+// profiling build only (tools/exact_profile.py): cycles per merge phase of block 0
+__device__ unsigned long long g_exact_prof[16];
+#define PROF_T(v) const long long v = clock64()
+#define PROF_ADD(i, a, b) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_exact_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define PROF_T(v)
+#define PROF_ADD(i, a, b)
+#endif
+
 namespace {
 
 constexpr uint32_t kMaxTempPerLane = 4;  // tcap <= 256 (estimateTempBuffer <= 178)
@@ -155,14 +166,15 @@ struct GoSortCent {
 
 struct Lds {
   double *mm, *mw;       // main centroids [capc]
-  double *tv, *tw;       // temps in Add order [TP]
-  double *sv, *sw;       // Go-sorted temps (tie fallback) [TP]
-  double *gm, *gw, *kin; // merged elements [capc + TP]
-  uint32_t* starts;      // [capc + TP + 1]
-  uint32_t* flag;        // [4]
+  double *tv, *tw;       // pending temps in Add order [TP]
+  double *sv, *sw;       // sorted temps of the merge being done [TP]
+  double *gm, *gw, *kin; // merged elements [JW]
+  uint16_t* jump;        // next-start tables, levels x [JW]
+  uint32_t* starts;      // [JW]
+  uint32_t JW, levels;
 };
 
-// #main centroids with mean < v
+// #main centroids with mean < v (main is sorted by mean)
 __device__ __forceinline__ uint32_t main_below(const double* mm, uint32_t nm, double v) {
   uint32_t l = 0, h = nm;
   while (l < h) {
@@ -172,15 +184,25 @@ __device__ __forceinline__ uint32_t main_below(const double* mm, uint32_t nm, do
   }
   return l;
 }
+// #sorted temps with mean <= v
+__device__ __forceinline__ uint32_t temps_le(const double* sv, uint32_t np, double v) {
+  uint32_t l = 0, h = np;
+  while (l < h) {
+    uint32_t md = (l + h) >> 1;
+    if (sv[md] <= v) l = md + 1;
+    else h = md;
+  }
+  return l;
+}
 
-// One mergeAllTemps of the np pending temps into main.
-__device__ void exact_merge(const ExactCtx& x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np) {
-  const uint32_t lane = threadIdx.x;
-  // ---- td.tempWeight (sequential sum in Add order)
+// td.tempWeight of np temps in Add order: the sequential fold, computed as a wave sum when
+// every weight is an integer and the total stays below 2^53 (then every order is exact).
+__device__ double temp_weight(const double* tw, uint32_t np) {
+  const uint32_t lane = threadIdx.x & 63;
   bool tint = true;
   double part = 0.0;
   for (uint32_t t = lane; t < np; t += 64) {
-    double w = L.tw[t];
+    double w = tw[t];
     tint &= is_int_weight(w);
     part = dadd(part, w);
   }
@@ -190,80 +212,91 @@ __device__ void exact_merge(const ExactCtx& x, const Lds& L, uint32_t& nm, doubl
   if (!tint || !(tempW <= 9007199254740992.0)) {
     tempW = 0.0;
     for (uint32_t b = 0; b < np; b += 64) {
-      double w = (b + lane < np) ? L.tw[b + lane] : 0.0;
+      double w = (b + lane < np) ? tw[b + lane] : 0.0;
       const uint32_t c = min(64u, np - b);
       for (uint32_t i = 0; i < c; i++) tempW = dadd(tempW, rl_d(w, (int)i));
     }
   }
-  const double T = dadd(mainW, tempW);  // totalWeight := td.mainWeight + td.tempWeight
+  return tempW;
+}
 
-  // ---- temp ranks by (mean, Add index); detect observable ties
+// Sort np temps (tv/tw, Add order) into sv/sw as sort.Sort(centroidList) orders them:
+// counting rank over (mean, Add index); when equal means make the order observable
+// (different weights or signed zeros) lane 0 runs Go's quickSort instead.  One wave.
+__device__ void sort_temps(const double* tv, const double* tw, double* sv, double* sw, uint32_t np) {
+  const uint32_t lane = threadIdx.x & 63;
   uint32_t rank[kMaxTempPerLane];
-  double tvr[kMaxTempPerLane], twr[kMaxTempPerLane];
+  double vr[kMaxTempPerLane], wr[kMaxTempPerLane];
   bool tie = false;
 #pragma unroll
   for (uint32_t q = 0; q < kMaxTempPerLane; q++) {
     const uint32_t t = q * 64 + lane;
     rank[q] = 0;
-    tvr[q] = 0.0;
-    twr[q] = 0.0;
+    vr[q] = 0.0;
+    wr[q] = 0.0;
     if (t < np) {
-      const double v = L.tv[t], w = L.tw[t];
+      const double v = tv[t], w = tw[t];
       uint32_t r = 0;
       for (uint32_t u = 0; u < np; u++) {
-        const double vu = L.tv[u];
+        const double vu = tv[u];
         r += (vu < v) || (vu == v && u < t);
         if (vu == v && u != t)
-          tie |= (__double_as_longlong(vu) != __double_as_longlong(v)) || (L.tw[u] != w);
+          tie |= (__double_as_longlong(vu) != __double_as_longlong(v)) || (tw[u] != w);
       }
       rank[q] = r;
-      tvr[q] = v;
-      twr[q] = w;
+      vr[q] = v;
+      wr[q] = w;
     }
   }
   if (__any(tie)) {
-    // Go's unstable quickSort decides the order of equal means: reproduce it
     for (uint32_t t = lane; t < np; t += 64) {
-      L.sv[t] = L.tv[t];
-      L.sw[t] = L.tw[t];
+      sv[t] = tv[t];
+      sw[t] = tw[t];
     }
     __syncthreads();
-    if (lane == 0) GoSortCent{L.sv, L.sw}.sort((int)np);
-    __syncthreads();
-    for (uint32_t r = lane; r < np; r += 64) {
-      const double v = L.sv[r];
-      const uint32_t p = r + main_below(L.mm, nm, v);
-      L.gm[p] = v;
-      L.gw[p] = L.sw[r];
-    }
+    if (lane == 0) GoSortCent{sv, sw}.sort((int)np);
   } else {
 #pragma unroll
-    for (uint32_t q = 0; q < kMaxTempPerLane; q++) {
+    for (uint32_t q = 0; q < kMaxTempPerLane; q++)
       if (q * 64 + lane < np) {
-        const uint32_t p = rank[q] + main_below(L.mm, nm, tvr[q]);
-        L.gm[p] = tvr[q];
-        L.gw[p] = twr[q];
+        sv[rank[q]] = vr[q];
+        sw[rank[q]] = wr[q];
       }
-    }
+  }
+  __syncthreads();
+}
+
+// mergeAllTemps of the sorted temps L.sv/L.sw (np of them, Add-order weight sum tempW)
+// into main L.mm/L.mw.  One wave; every step is a parallel pass of O(log) depth.
+__device__ void merge_sorted(const ExactCtx& x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
+                             double tempW) {
+  const uint32_t lane = threadIdx.x;
+  PROF_T(p0);
+  const double T = dadd(mainW, tempW);  // totalWeight := td.mainWeight + td.tempWeight
+  // ---- merged order: main first only if strictly smaller (merging_digest.go:169)
+  for (uint32_t t = lane; t < np; t += 64) {
+    const double v = L.sv[t];
+    const uint32_t p = t + main_below(L.mm, nm, v);
+    L.gm[p] = v;
+    L.gw[p] = L.sw[t];
   }
   for (uint32_t j = lane; j < nm; j += 64) {
     const double v = L.mm[j];
-    uint32_t c = 0;
-    for (uint32_t u = 0; u < np; u++) c += L.tv[u] <= v;
-    L.gm[j + c] = v;
-    L.gw[j + c] = L.mw[j];
+    const uint32_t p = j + temps_le(L.sv, np, v);
+    L.gm[p] = v;
+    L.gw[p] = L.mw[j];
   }
   __syncthreads();
-
-  // ---- mergedWeight prefix (inclusive) -> k-index, one lane per element
+  PROF_T(p1);
   const uint32_t m = nm + np;
+  // ---- mergedWeight prefix (inclusive), then the k-index of every element
   bool wint = true;
   for (uint32_t j = lane; j < m; j += 64) wint &= is_int_weight(L.gw[j]);
   wint = __all(wint) && T <= 9007199254740992.0;
   double carry = 0.0;
   for (uint32_t b = 0; b < m; b += 64) {
     const uint32_t j = b + lane;
-    double w = j < m ? L.gw[j] : 0.0;
+    const double w = j < m ? L.gw[j] : 0.0;
     double incl;
     if (wint) {
       double v = w;
@@ -283,40 +316,98 @@ __device__ void exact_merge(const ExactCtx& x, const Lds& L, uint32_t& nm, doubl
       }
     }
     carry = rl_d(incl, (int)min(63u, m - b - 1));
-    if (j < m) L.kin[j] = index_estimate(x.delta, ddiv(incl, T));
+    if (j < m) L.kin[j] = incl;
   }
-
-  // ---- greedy chain (mergeOne): ballot over 64 k values at a time
-  const double k0 = index_estimate(x.delta, 0.0);
-  uint32_t nc = 0;
-  double base = k0;
-  double kprev_carry = k0;  // k of the element before the group (k(0) before element 0)
-  bool overflow = false;
-  for (uint32_t b = 0; b < m && !overflow; b += 64) {
-    const uint32_t j = b + lane;
-    const bool valid = j < m;
-    const double kv = valid ? L.kin[j] : 0.0;  // written by this lane above
-    double kp = __shfl_up(kv, 1, 64);
-    if (lane == 0) kp = kprev_carry;
-    uint32_t from = 0;
-    for (;;) {
-      const bool c = valid && lane >= from && (nc == 0 || dsub(kv, base) > 1.0);
-      const uint64_t bal = __ballot(c);
-      if (!bal) break;
-      const uint32_t f = (uint32_t)__builtin_ctzll(bal);
-      if (nc >= x.capc) { overflow = true; break; }
-      if (lane == 0) L.starts[nc] = b + f;
-      nc++;
-      base = rl_d(kp, (int)f);  // k(W_start / T): the k of the element before the start
-      from = f + 1;
+  for (uint32_t b = 0; b < m; b += 256) {  // independent asin evaluations, four per lane
+    double q[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t j = b + 64 * u + lane;
+      q[u] = j < m ? ddiv(L.kin[j], T) : 0.0;
     }
-    kprev_carry = rl_d(kv, 63);
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t j = b + 64 * u + lane;
+      if (j < m) L.kin[j] = index_estimate(x.delta, q[u]);
+    }
+  }
+  __syncthreads();
+  PROF_T(p2);
+  // ---- greedy chain of mergeOne (210-236).  A centroid starting at element s ends before
+  // next(s) = the first j > s with k_j - k_{s-1} > 1 (k_{-1} = k(0)).  next() depends on s
+  // alone, so the starts 0, next(0), next(next(0)), ... follow by pointer doubling.  The
+  // binary search needs k monotone; a non-monotone k (ulp-level asin wiggle) takes the
+  // sequential walk instead, so the result is always the reference's.
+  const double k0 = index_estimate(x.delta, 0.0);
+  bool mono = true;
+  for (uint32_t j = lane + 1; j < m; j += 64) mono &= !(L.kin[j] < L.kin[j - 1]);
+  mono = __all(mono);
+  uint32_t nc = 0;
+  bool overflow = false;
+  const uint32_t capc = x.capc;
+  if (mono) {
+    uint16_t* J0 = L.jump;
+    for (uint32_t s = lane; s <= m; s += 64) {
+      uint32_t r = m;
+      if (s < m) {
+        const double base = s ? L.kin[s - 1] : k0;
+        uint32_t l = s + 1, h = m;
+        while (l < h) {
+          uint32_t md = (l + h) >> 1;
+          if (dsub(L.kin[md], base) > 1.0) h = md;
+          else l = md + 1;
+        }
+        r = l;
+      }
+      J0[s] = (uint16_t)r;
+    }
+    __syncthreads();
+    for (uint32_t lv = 1; lv < L.levels; lv++) {
+      const uint16_t* Jp = L.jump + (lv - 1) * L.JW;
+      uint16_t* Jl = L.jump + lv * L.JW;
+      for (uint32_t s = lane; s <= m; s += 64) Jl[s] = Jp[Jp[s]];
+      __syncthreads();
+    }
+    // start t = next^t(0), composed from the power-of-two tables; t <= capc
+    for (uint32_t t = lane; t <= capc; t += 64) {
+      uint32_t p = 0;
+      for (uint32_t lv = 0; lv < L.levels && p < m; lv++)
+        if ((t >> lv) & 1u) p = L.jump[lv * L.JW + p];
+      const bool on = p < m;
+      if (on && t < capc) L.starts[t] = p;
+      nc += (uint32_t)__popcll(__ballot(on));
+      overflow |= on && t == capc;
+    }
+    overflow = __any(overflow);
+    if (nc > capc) nc = capc;
+  } else {
+    double base = k0, kprev_carry = k0;
+    for (uint32_t b = 0; b < m && !overflow; b += 64) {
+      const uint32_t j = b + lane;
+      const bool valid = j < m;
+      const double kv = valid ? L.kin[j] : 0.0;
+      double kp = __shfl_up(kv, 1, 64);
+      if (lane == 0) kp = kprev_carry;
+      uint32_t from = 0;
+      for (;;) {
+        const bool c = valid && lane >= from && (nc == 0 || dsub(kv, base) > 1.0);
+        const uint64_t bal = __ballot(c);
+        if (!bal) break;
+        const uint32_t f = (uint32_t)__builtin_ctzll(bal);
+        if (nc >= capc) { overflow = true; break; }
+        if (lane == 0) L.starts[nc] = b + f;
+        nc++;
+        base = rl_d(kp, (int)f);
+        from = f + 1;
+      }
+      kprev_carry = rl_d(kv, 63);
+    }
   }
   if (overflow && lane == 0) atomicOr(x.err, 1u);
   if (lane == 0) L.starts[nc] = m;
   __syncthreads();
-
-  // ---- Welford per centroid, in element order
+  PROF_T(p3);
+  // ---- Welford per centroid, in element order (weight first, then mean)
   for (uint32_t c = lane; c < nc; c += 64) {
     const uint32_t a = L.starts[c], e = L.starts[c + 1];
     double mean = L.gm[a], W = L.gw[a];
@@ -329,15 +420,94 @@ __device__ void exact_merge(const ExactCtx& x, const Lds& L, uint32_t& nm, doubl
     L.mw[c] = W;
   }
   __syncthreads();
+  PROF_T(p4);
+  PROF_ADD(1, p0, p1);
+  PROF_ADD(2, p1, p2);
+  PROF_ADD(3, p2, p3);
+  PROF_ADD(4, p3, p4);
+  PROF_ADD(5, 0, 1);
+  PROF_ADD(6, 0, (long long)m);
+  PROF_ADD(7, 0, (long long)nc);
   nm = nc;
   mainW = T;
 }
 
+// sort the pending temps in LDS and merge them
+__device__ void merge_pending(const ExactCtx& x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np) {
+  PROF_T(a0);
+  const double tempW = temp_weight(L.tw, np);
+  sort_temps(L.tv, L.tw, L.sv, L.sw, np);
+  PROF_T(a1);
+  PROF_ADD(0, a0, a1);
+  merge_sorted(x, L, nm, mainW, np, tempW);
+}
+
 __device__ __forceinline__ uint32_t round64(uint32_t v) { return (v + 63u) & ~63u; }
+
+// Where a key's batch splits (shared by the chunk sorter and the replay):
+//   head  [0, off0)         tops up the pending temps (merged if the list fills and more follow)
+//   pure  npure chunks of tcap samples, each merged (a later sample always follows it)
+//   tail  the rest          stays pending (or is merged by a final merge)
+struct ExactSplit {
+  uint32_t off0, npure;
+};
+__device__ __forceinline__ ExactSplit exact_split(uint32_t np0, uint32_t nex, uint32_t tcap) {
+  const uint32_t np = (nex > 0 && np0 == tcap) ? 0u : np0;  // a full list merges before the first Add
+  ExactSplit r;
+  r.off0 = np == 0 ? 0u : min(tcap - np, nex);
+  r.npure = nex > r.off0 ? (nex - r.off0 - 1) / tcap : 0u;
+  return r;
+}
+
+__device__ __forceinline__ uint32_t last_le_u32(const uint32_t* off, uint32_t n, uint32_t o) {
+  uint32_t lo = 0, hi = n;  // last k in [0, n) with off[k] <= o
+  while (hi - lo > 1) {
+    uint32_t m = (lo + hi) >> 1;
+    if (off[m] <= o) lo = m;
+    else hi = m;
+  }
+  return lo;
+}
 
 }  // namespace
 
-// One 64-thread block (one wave) per key.
+// ---- pure-chunk sorter: the contents of every full chunk are known before the replay, so
+// all of them are sorted here in parallel (one wave per chunk), off the replay's critical path.
+__global__ void k_exact_chunk_count(ExactCtx x) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= x.nkeys) return;
+  const uint32_t nex = x.nex[k];
+  x.ccnt[k] = exact_split(x.hpend[x.keys[k]], nex, x.tcap).npure;
+}
+
+__global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t g = blockIdx.x, lane = threadIdx.x;
+  if (g >= x.coff[x.nkeys]) return;
+  const uint32_t tcap = x.tcap, TP = round64(tcap + 1);
+  double* tv = reinterpret_cast<double*>(smem);
+  double* tw = tv + TP;
+  double* sv = tw + TP;
+  double* sw = sv + TP;
+  const uint32_t k = last_le_u32(x.coff, x.nkeys, g);
+  const uint32_t s = x.keys[k];
+  const ExactSplit sp = exact_split(x.hpend[s], x.nex[k], tcap);
+  const uint64_t base = (uint64_t)x.start[s] + sp.off0 + (uint64_t)(g - x.coff[k]) * tcap;
+  for (uint32_t t = lane; t < tcap; t += 64) {
+    tv[t] = bitsd(x.A[base + t]);
+    tw[t] = (double)(1.0f / __uint_as_float((uint32_t)x.B[base + t]));  // float64(1/rate) in float32
+  }
+  __syncthreads();
+  const double tempW = temp_weight(tw, tcap);
+  sort_temps(tv, tw, sv, sw, tcap);
+  for (uint32_t t = lane; t < tcap; t += 64) {
+    x.csv[base + t] = sv[t];
+    x.csw[base + t] = sw[t];
+  }
+  if (lane == 0) x.ctw[base] = tempW;
+}
+
+// ---- the replay: one 64-thread block (one wave) per key
 __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t k = blockIdx.x, lane = threadIdx.x;
@@ -345,6 +515,9 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   const uint32_t capc = x.capc, tcap = x.tcap;
   const uint32_t TP = round64(tcap + 1);
   Lds L;
+  L.JW = capc + TP + 1;
+  L.levels = 1;
+  while ((1u << L.levels) <= capc) L.levels++;
   L.mm = reinterpret_cast<double*>(smem);
   L.mw = L.mm + capc;
   L.tv = L.mw + capc;
@@ -352,11 +525,12 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   L.sv = L.tw + TP;
   L.sw = L.sv + TP;
   L.gm = L.sw + TP;
-  L.gw = L.gm + capc + TP;
-  L.kin = L.gw + capc + TP;
-  L.starts = reinterpret_cast<uint32_t*>(L.kin + capc + TP);
-  L.flag = L.starts + capc + TP + 1;
+  L.gw = L.gm + L.JW;
+  L.kin = L.gw + L.JW;
+  L.starts = reinterpret_cast<uint32_t*>(L.kin + L.JW);
+  L.jump = reinterpret_cast<uint16_t*>(L.starts + L.JW);
 
+  PROF_T(k0);
   const uint32_t s = x.keys[k];
   const uint32_t nex = x.nex ? x.nex[k] : 0u;
   const bool final_merge = x.flush_mode || (x.hot && x.hot[k]);
@@ -369,21 +543,9 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   uint32_t nm = x.hncent[s];
   double* h = x.hst + (uint64_t)s * VN_HISTO_STATS;
   double mainW = h[7];
-  const uint32_t lo = x.start[s];
+  const uint32_t lo = nex ? x.start[s] : 0u;  // start/A/B are null in flush mode (nex == 0)
+  const ExactSplit sp = exact_split(np, nex, tcap);
 
-  // first chunk of samples into registers (overlaps the state load)
-  uint32_t r = 0;
-  if (nex) r = min(np == tcap ? tcap : tcap - np, nex);
-  double cv[kMaxTempPerLane];
-  float cr[kMaxTempPerLane];
-#pragma unroll
-  for (uint32_t q = 0; q < kMaxTempPerLane; q++) {
-    const uint32_t i = q * 64 + lane;
-    if (i < r) {
-      cv[q] = bitsd(x.A[lo + i]);
-      cr[q] = __uint_as_float((uint32_t)x.B[lo + i]);
-    }
-  }
   for (uint32_t j = lane; j < nm; j += 64) {
     L.mm[j] = cmg[j];
     L.mw[j] = cwg[j];
@@ -398,47 +560,75 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
 
   // Histo.Sample local statistics of the replayed samples (samplers.go:346-356)
   double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
-  if (nex && np == tcap) {  // Add finds the temp list full: mergeAllTemps first
-    exact_merge(x, L, nm, mainW, np);
-    np = 0;
-  }
-  uint32_t pos = 0;
-  while (r) {
-#pragma unroll
-    for (uint32_t q = 0; q < kMaxTempPerLane; q++) {
-      const uint32_t i = q * 64 + lane;
-      if (i < r) {
-        const double v = cv[q];
-        const double wt = (double)(1.0f / cr[q]);  // float64(1/sampleRate) in float32
-        L.tv[np + i] = v;
-        L.tw[np + i] = wt;
-        sw = dadd(sw, wt);
-        mn = min_go(mn, v);
-        mx = max_go(mx, v);
-        sxw = dadd(sxw, dmul(v, wt));
-        srw = dadd(srw, dmul(ddiv(1.0, v), wt));
-      }
+  auto stat = [&](double v, double wt) {
+    sw = dadd(sw, wt);
+    mn = min_go(mn, v);
+    mx = max_go(mx, v);
+    sxw = dadd(sxw, dmul(v, wt));
+    srw = dadd(srw, dmul(ddiv(1.0, v), wt));
+  };
+  // append raw samples [a, b) of the batch to the pending temps (Add order)
+  auto append = [&](uint32_t a, uint32_t b) {
+    for (uint32_t i = a + lane; i < b; i += 64) {
+      const double v = bitsd(x.A[lo + i]);
+      const double wt = (double)(1.0f / __uint_as_float((uint32_t)x.B[lo + i]));
+      L.tv[np + (i - a)] = v;
+      L.tw[np + (i - a)] = wt;
+      stat(v, wt);
     }
-    np += r;
-    pos += r;
-    if (pos >= nex) break;
-    // the temp list is full (np == tcap): prefetch the next chunk, then merge
-    r = min(tcap, nex - pos);
-#pragma unroll
-    for (uint32_t q = 0; q < kMaxTempPerLane; q++) {
-      const uint32_t i = q * 64 + lane;
-      if (i < r) {
-        cv[q] = bitsd(x.A[lo + pos + i]);
-        cr[q] = __uint_as_float((uint32_t)x.B[lo + pos + i]);
-      }
-    }
+    np += b - a;
     __syncthreads();
-    exact_merge(x, L, nm, mainW, np);
+  };
+
+  if (nex && np == tcap) {  // Add finds the temp list full: mergeAllTemps first
+    merge_pending(x, L, nm, mainW, np);
     np = 0;
   }
-  __syncthreads();
+  // head
+  if (sp.off0) {
+    append(0, sp.off0);
+    if (np == tcap && sp.off0 < nex) {
+      merge_pending(x, L, nm, mainW, np);
+      np = 0;
+    }
+  }
+  // pure chunks: pre-sorted by k_exact_chunk_sort; the next one is loaded before each merge
+  if (sp.npure) {
+    double cv[kMaxTempPerLane], cw[kMaxTempPerLane], ctw = 0.0;
+    auto load = [&](uint32_t c) {
+      const uint64_t base = (uint64_t)lo + sp.off0 + (uint64_t)c * tcap;
+#pragma unroll
+      for (uint32_t q = 0; q < kMaxTempPerLane; q++) {
+        const uint32_t t = q * 64 + lane;
+        if (t < tcap) {
+          cv[q] = x.csv[base + t];
+          cw[q] = x.csw[base + t];
+        }
+      }
+      ctw = x.ctw[base];
+    };
+    load(0);
+    for (uint32_t c = 0; c < sp.npure; c++) {
+#pragma unroll
+      for (uint32_t q = 0; q < kMaxTempPerLane; q++) {
+        const uint32_t t = q * 64 + lane;
+        if (t < tcap) {
+          L.sv[t] = cv[q];
+          L.sw[t] = cw[q];
+          stat(cv[q], cw[q]);
+        }
+      }
+      const double tempW = ctw;
+      if (c + 1 < sp.npure) load(c + 1);
+      __syncthreads();
+      merge_sorted(x, L, nm, mainW, tcap, tempW);
+    }
+  }
+  // tail
+  const uint32_t tail = sp.off0 + sp.npure * tcap;
+  if (nex > tail) append(tail, nex);
   if (final_merge && np > 0) {
-    exact_merge(x, L, nm, mainW, np);
+    merge_pending(x, L, nm, mainW, np);
     np = 0;
   }
   // ---- write back the key's digest and statistics
@@ -460,6 +650,8 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
     mn = min_go(mn, __shfl_xor(mn, d, 64));
     mx = max_go(mx, __shfl_xor(mx, d, 64));
   }
+  PROF_T(k1);
+  PROF_ADD(8, k0, k1);
   if (lane == 0) {
     x.hncent[s] = nm;
     x.hpend[s] = np;
@@ -477,13 +669,35 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
 }
 
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap) {
-  const uint32_t TP = (tcap + 1 + 63u) & ~63u;
-  return sizeof(double) * (2 * capc + 4 * TP + 3 * (capc + TP)) + sizeof(uint32_t) * (capc + TP + 1 + 4);
+  const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = capc + TP + 1;
+  uint32_t levels = 1;
+  while ((1u << levels) <= capc) levels++;
+  return sizeof(double) * (2 * capc + 4 * TP + 3 * JW) + sizeof(uint32_t) * JW + sizeof(uint16_t) * levels * JW + 16;
 }
 
-void launch_histo_exact(const ExactCtx& x, hipStream_t st) {
+#ifdef VN_EXACT_PROF
+extern "C" int vn_prof_exact_read(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_exact_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_exact_prof), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
+void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks) {
   if (!x.nkeys) return;
   if (x.tcap > 64 * kMaxTempPerLane) throw std::runtime_error("temp buffer larger than the exact kernel supports");
+  if (x.capc + x.tcap + 64 >= 65535) throw std::runtime_error("centroid capacity too large for the exact kernel");
+  if (x.nex) {
+    // sort every pure chunk in parallel first
+    hipLaunchKernelGGL(k_exact_chunk_count, dim3(blocks_for(x.nkeys, 256)), dim3(256), 0, st, x);
+    scan_exclusive_u32(x.ccnt, x.coff, x.nkeys, *ss, st);
+    if (max_chunks)
+      hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)max_chunks), dim3(64),
+                         sizeof(double) * 4 * ((x.tcap + 1 + 63u) & ~63u), st, x);
+  }
   size_t sm = exact_smem_bytes(x.capc, x.tcap);
   hipLaunchKernelGGL(k_histo_exact, dim3(x.nkeys), dim3(64), sm, st, x);
 }

@@ -586,7 +586,12 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   xc.hpw = e->hpw;
   xc.err = e->h_err;
   xc.flush_mode = 0;
-  launch_histo_exact(xc, st);
+  xc.ccnt = e->h_ccnt;
+  xc.coff = e->h_coff;
+  xc.csv = e->h_wk;  // free until the hot-key batch merge below reuses them
+  xc.csw = e->h_w;
+  xc.ctw = e->h_tw;
+  launch_histo_exact(xc, st, &e->ss, n / e->temp_cap + 1);
 
   // ---- 3. hot remainders: one-shot merge of (main centroids + samples) per key
   compact_flags(e->h_hotflag, e->h_pos, e->h_hotlist, e->h_cnt + 1, ntouched, e->ss, st);

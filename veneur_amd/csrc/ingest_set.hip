@@ -71,16 +71,22 @@ constexpr uint32_t kMark = 0x80000000u;
 
 __device__ __forceinline__ uint32_t hslot(uint32_t c) { return (c * 2654435761u) >> 23; }  // 9 bits
 
-// sequential insert (single lane); returns true if the code was new
-__device__ __forceinline__ bool hash_insert_seq(uint32_t* h, uint32_t c) {
+// lookup (read only)
+__device__ __forceinline__ bool hash_contains(const uint32_t* h, uint32_t c) {
   uint32_t i = hslot(c);
   for (;;) {
     uint32_t v = h[i];
-    if (v == c) return false;
-    if (v == kHllNoCode) {
-      h[i] = c;
-      return true;
-    }
+    if (v == c) return true;
+    if (v == kHllNoCode) return false;
+    i = (i + 1) & (kHashSlots - 1);
+  }
+}
+// parallel insert; returns the entry index holding c
+__device__ __forceinline__ uint32_t hash_claim(uint32_t* h, uint32_t c) {
+  uint32_t i = hslot(c);
+  for (;;) {
+    uint32_t prev = atomicCAS(&h[i], kHllNoCode, c);
+    if (prev == kHllNoCode || prev == c) return i;
     i = (i + 1) & (kHashSlots - 1);
   }
 }
@@ -126,6 +132,7 @@ __device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t 
 __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
   __shared__ uint32_t U[kArenaWords];   // sparse list (sorted codes) or dense registers (u32 each)
   __shared__ uint32_t s_hash[kHashSlots];
+  __shared__ uint32_t s_first[kHashSlots];  // lowest lane of the current group holding the entry
   __shared__ uint32_t s_tmp[256];       // tmpSet codes in insertion order, then sorted
   __shared__ uint32_t s_new[256];       // tmp codes not yet in the list (sorted)
   __shared__ uint32_t s_red[4];
@@ -153,7 +160,10 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
 
   if (s_mode == 0) {
     // ------------------------------------------------------------ sparse phase
-    for (uint32_t i = t; i < kHashSlots; i += kBlock) s_hash[i] = kHllNoCode;
+    for (uint32_t i = t; i < kHashSlots; i += kBlock) {
+      s_hash[i] = kHllNoCode;
+      s_first[i] = 0xffffffffu;
+    }
     __syncthreads();
     const uint32_t tc0 = s_tc;
     if (t < tc0) {
@@ -163,21 +173,45 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
     }
     __syncthreads();
     while (s_pos < n && s_mode == 0) {
-      if (t == 0) {
+      // wave 0 advances to the next mergeSparse trigger -- the record that makes the tmpSet
+      // hold kHllTmpTrigger distinct codes -- 64 records per step: a record counts if its
+      // code is neither in the tmpSet nor held by a lower lane of the same step.
+      if (t < 64) {
         uint32_t pos = s_pos, tc = s_tc, trig = 0;
+        const uint64_t below = (t == 0) ? 0ull : (~0ull >> (64 - t));
         while (pos < n) {
-          uint32_t c = (uint32_t)R[pos++];
-          if (hash_insert_seq(s_hash, c)) {
-            s_tmp[tc++] = c;
-            if (tc >= kHllTmpTrigger) {
-              trig = 1;
-              break;
-            }
+          const uint32_t p = pos + t;
+          const bool valid = p < n;
+          const uint32_t c = valid ? (uint32_t)R[p] : kHllNoCode;
+          const bool fresh = valid && !hash_contains(s_hash, c);
+          uint32_t hi = 0;
+          if (fresh) {
+            hi = hash_claim(s_hash, c);
+            atomicMin(&s_first[hi], t);
           }
+          const bool first = fresh && s_first[hi] == t;
+          const uint64_t bal = __ballot(first);
+          const uint32_t cnt = (uint32_t)__popcll(bal);
+          const uint32_t need = kHllTmpTrigger - tc;
+          uint32_t take = 64, add = cnt;
+          if (cnt >= need) {  // the need-th first occurrence triggers the merge
+            uint64_t b = bal;
+            for (uint32_t q = 1; q < need; q++) b &= b - 1;
+            const uint32_t L = (uint32_t)__builtin_ctzll(b);
+            take = L + 1;
+            add = need;
+            trig = 1;
+          }
+          if (first && t < take) s_tmp[tc + (uint32_t)__popcll(bal & below)] = c;
+          tc += add;
+          pos += take;
+          if (trig) break;
         }
-        s_pos = pos;
-        s_tc = tc;
-        s_trig = trig;
+        if (t == 0) {
+          s_pos = min(pos, n);
+          s_tc = tc;
+          s_trig = trig;
+        }
       }
       __syncthreads();
       if (!s_trig) break;
@@ -234,7 +268,10 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
         s_lc = nlc;
         s_tc = 0;
       }
-      for (uint32_t i = t; i < kHashSlots; i += kBlock) s_hash[i] = kHllNoCode;
+      for (uint32_t i = t; i < kHashSlots; i += kBlock) {
+        s_hash[i] = kHllNoCode;
+        s_first[i] = 0xffffffffu;
+      }
       __syncthreads();
       if (bytes > kHllM) {
         // toNormal: registers from the merged list (b stays; nz > 0 so no rebase can occur)
@@ -290,6 +327,15 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
   }
 
   // -------------------------------------------------------------- dense phase
+  uint32_t raw[kItems];
+  {
+    const uint32_t c0 = s_pos;
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      uint32_t p = c0 + j * kBlock + t;
+      raw[j] = p < n ? (uint32_t)R[p] : 0u;
+    }
+  }
   for (uint32_t cpos0 = s_pos; cpos0 < n; cpos0 += kTile) {
     const uint32_t cend = min(n, cpos0 + (uint32_t)kTile);
     uint32_t ri[kItems], rr[kItems];
@@ -298,13 +344,54 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
       uint32_t p = cpos0 + j * kBlock + t;
       ri[j] = 0;
       rr[j] = 0;
-      if (p < cend) decode_hash((uint32_t)R[p], &ri[j], &rr[j]);
+      if (p < cend) decode_hash(raw[j], &ri[j], &rr[j]);
+    }
+    // prefetch the next chunk; its latency hides behind this chunk's phases
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      uint32_t p = cpos0 + kTile + j * kBlock + t;
+      raw[j] = p < n ? (uint32_t)R[p] : 0u;
     }
     uint32_t cpos = cpos0;
     for (;;) {
       const uint32_t b = s_b;
       uint32_t tfull;
       if (s_nz > 0) {
+        // fast path: mark the zero registers this chunk would fill; if they do not cover
+        // all nz of them, the fill cannot complete here, so no rebase can occur in the
+        // chunk and every update is a plain max
+        if (t == 0) s_filled = 0;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == 0)
+            if (atomicOr(&U[ri[j]], kMark) == 0) atomicAdd(&s_filled, 1u);
+        }
+        __syncthreads();
+        const bool completes = s_filled >= s_nz;
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
+        }
+        __syncthreads();
+        if (!completes) {
+          if (t == 0) s_newfill = 0;
+          __syncthreads();
+#pragma unroll
+          for (int j = 0; j < kItems; j++) {
+            uint32_t p = cpos0 + j * kBlock + t;
+            if (p >= cpos && p < cend && rr[j] > b) {
+              uint32_t old = atomicMax(&U[ri[j]], min(rr[j] - b, kHllCapacity - 1));
+              if (old == 0) atomicAdd(&s_newfill, 1u);
+            }
+          }
+          __syncthreads();
+          if (t == 0) s_nz -= s_newfill;
+          __syncthreads();
+          break;
+        }
         if (t == 0) {
           s_filled = 0;
           s_tfull = 0;
