@@ -49,10 +49,10 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     for i in range(5):
         out["cyc_per_merge_" + NAMES[i]] = round(p[i] / merges, 1)
     out["cyc_per_merge_total"] = round(sum(p[:5]) / merges, 1)
+    for i, nme in zip(range(9, 13), ("chain.mono", "chain.bsearch", "chain.levels", "chain.compose")):
+        out["cyc_" + nme] = round(p[i] / merges, 1)
     print(out, flush=True)
 
 
 if __name__ == "__main__":
     run(32768, 0, 0)
-    run(32768, 2000, 100)
-    run(32768, 100000, 150)

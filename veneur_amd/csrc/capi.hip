@@ -267,6 +267,7 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
   if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[3], st));
   ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
   if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[4], st));
+  VN_HIP_CHECK(hipGetLastError());  // a launch that could not start (e.g. LDS over budget) fails loudly
   e->processed += b->n_counter + b->n_gauge + b->n_histo + b->n_set;
 }
 
@@ -446,6 +447,7 @@ int vn_flush(vn_engine* e, vn_flush_result* out) {
   return guarded(e, [&] {
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[5], e->st));
     flush_all(e, out);
+    VN_HIP_CHECK(hipGetLastError());
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[6], e->st));
     check_error_flags(e);
     if (e->timing) {

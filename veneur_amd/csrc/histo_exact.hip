@@ -7,7 +7,8 @@
 // the temp first), feeding each element to mergeOne (210-236).  Quantile (283-313)
 // merges whatever is pending first.
 //
-// One wave (a 64-thread block) owns one key.  A hot key replays ~800 merges back to back,
+// One wave (a 64-thread block) owns one key; lanes exchange data through LDS with
+// wave_lds_sync() (no workgroup barrier, so prefetched global loads stay in flight).  A hot key replays ~800 merges back to back,
 // so each merge is built for latency -- no lane-0 loops over LDS:
 //   tempWeight       arrival-order fold: wave sum when every weight is an integer (exact in
 //                    any order), otherwise a sequential fold through v_readlane
@@ -164,12 +165,21 @@ struct GoSortCent {
   }
 };
 
+// what a merge needs from ExactCtx, by value (a reference to the kernel-argument struct
+// would force a copy of it into scratch memory)
+struct MergeParams {
+  double delta;
+  uint32_t capc;
+  uint32_t* err;
+};
+
 struct Lds {
   double *mm, *mw;       // main centroids [capc]
   double *tv, *tw;       // pending temps in Add order [TP]
   double *sv, *sw;       // sorted temps of the merge being done [TP]
   double *gm, *gw, *kin; // merged elements [JW]
-  uint16_t* jump;        // next-start tables, levels x [JW]
+  uint32_t* jump;        // next-start tables, levels x [JW]: u32 in the fast merge
+  uint16_t* jump16;      // the same memory as u16 tables in the generic merge (large delta)
   uint32_t* starts;      // [JW]
   uint32_t JW, levels;
 };
@@ -223,7 +233,7 @@ __device__ double temp_weight(const double* tw, uint32_t np) {
 // Sort np temps (tv/tw, Add order) into sv/sw as sort.Sort(centroidList) orders them:
 // counting rank over (mean, Add index); when equal means make the order observable
 // (different weights or signed zeros) lane 0 runs Go's quickSort instead.  One wave.
-__device__ void sort_temps(const double* tv, const double* tw, double* sv, double* sw, uint32_t np) {
+__device__ __noinline__ void sort_temps(const double* tv, const double* tw, double* sv, double* sw, uint32_t np) {
   const uint32_t lane = threadIdx.x & 63;
   uint32_t rank[kMaxTempPerLane];
   double vr[kMaxTempPerLane], wr[kMaxTempPerLane];
@@ -253,7 +263,7 @@ __device__ void sort_temps(const double* tv, const double* tw, double* sv, doubl
       sv[t] = tv[t];
       sw[t] = tw[t];
     }
-    __syncthreads();
+    wave_lds_sync();
     if (lane == 0) GoSortCent{sv, sw}.sort((int)np);
   } else {
 #pragma unroll
@@ -263,12 +273,12 @@ __device__ void sort_temps(const double* tv, const double* tw, double* sv, doubl
         sw[rank[q]] = wr[q];
       }
   }
-  __syncthreads();
+  wave_lds_sync();
 }
 
 // mergeAllTemps of the sorted temps L.sv/L.sw (np of them, Add-order weight sum tempW)
 // into main L.mm/L.mw.  One wave; every step is a parallel pass of O(log) depth.
-__device__ void merge_sorted(const ExactCtx& x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
+__device__ __noinline__ void merge_sorted(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
                              double tempW) {
   const uint32_t lane = threadIdx.x;
   PROF_T(p0);
@@ -286,7 +296,7 @@ __device__ void merge_sorted(const ExactCtx& x, const Lds& L, uint32_t& nm, doub
     L.gm[p] = v;
     L.gw[p] = L.mw[j];
   }
-  __syncthreads();
+  wave_lds_sync();
   PROF_T(p1);
   const uint32_t m = nm + np;
   // ---- mergedWeight prefix (inclusive), then the k-index of every element
@@ -331,7 +341,7 @@ __device__ void merge_sorted(const ExactCtx& x, const Lds& L, uint32_t& nm, doub
       if (j < m) L.kin[j] = index_estimate(x.delta, q[u]);
     }
   }
-  __syncthreads();
+  wave_lds_sync();
   PROF_T(p2);
   // ---- greedy chain of mergeOne (210-236).  A centroid starting at element s ends before
   // next(s) = the first j > s with k_j - k_{s-1} > 1 (k_{-1} = k(0)).  next() depends on s
@@ -346,7 +356,7 @@ __device__ void merge_sorted(const ExactCtx& x, const Lds& L, uint32_t& nm, doub
   bool overflow = false;
   const uint32_t capc = x.capc;
   if (mono) {
-    uint16_t* J0 = L.jump;
+    uint16_t* J0 = L.jump16;
     for (uint32_t s = lane; s <= m; s += 64) {
       uint32_t r = m;
       if (s < m) {
@@ -361,18 +371,18 @@ __device__ void merge_sorted(const ExactCtx& x, const Lds& L, uint32_t& nm, doub
       }
       J0[s] = (uint16_t)r;
     }
-    __syncthreads();
+    wave_lds_sync();
     for (uint32_t lv = 1; lv < L.levels; lv++) {
-      const uint16_t* Jp = L.jump + (lv - 1) * L.JW;
-      uint16_t* Jl = L.jump + lv * L.JW;
-      for (uint32_t s = lane; s <= m; s += 64) Jl[s] = Jp[Jp[s]];
-      __syncthreads();
+      const uint16_t* Jp = L.jump16 + (lv - 1) * L.JW;
+      uint16_t* Jl = L.jump16 + lv * L.JW;
+      for (uint32_t s = lane; s <= m; s += 64) Jl[s] = (uint16_t)Jp[Jp[s]];
+      wave_lds_sync();
     }
     // start t = next^t(0), composed from the power-of-two tables; t <= capc
     for (uint32_t t = lane; t <= capc; t += 64) {
       uint32_t p = 0;
       for (uint32_t lv = 0; lv < L.levels && p < m; lv++)
-        if ((t >> lv) & 1u) p = L.jump[lv * L.JW + p];
+        if ((t >> lv) & 1u) p = L.jump16[lv * L.JW + p];
       const bool on = p < m;
       if (on && t < capc) L.starts[t] = p;
       nc += (uint32_t)__popcll(__ballot(on));
@@ -405,7 +415,7 @@ __device__ void merge_sorted(const ExactCtx& x, const Lds& L, uint32_t& nm, doub
   }
   if (overflow && lane == 0) atomicOr(x.err, 1u);
   if (lane == 0) L.starts[nc] = m;
-  __syncthreads();
+  wave_lds_sync();
   PROF_T(p3);
   // ---- Welford per centroid, in element order (weight first, then mean)
   for (uint32_t c = lane; c < nc; c += 64) {
@@ -419,7 +429,7 @@ __device__ void merge_sorted(const ExactCtx& x, const Lds& L, uint32_t& nm, doub
     L.mm[c] = mean;
     L.mw[c] = W;
   }
-  __syncthreads();
+  wave_lds_sync();
   PROF_T(p4);
   PROF_ADD(1, p0, p1);
   PROF_ADD(2, p1, p2);
@@ -432,14 +442,284 @@ __device__ void merge_sorted(const ExactCtx& x, const Lds& L, uint32_t& nm, doub
   mainW = T;
 }
 
+// Same merge, written branch-free for a lone wave: every per-lane loop is unrolled over kR
+// rounds with fixed trip counts, clamped indices and selects, so the independent LDS loads of
+// all rounds issue back to back instead of one exec-masked round at a time.
+// Requires nm + np < 64 * kR <= JW (delta <= ~150) and np <= 64.
+constexpr int kR = 5;     // largest instantiation: nm + np < 320
+constexpr int kLogM = 9;  // steps of a search over main (nm <= 256 < 2^9)
+constexpr int kLogT = 7;  // steps of a search over the temps (np <= 64 < 2^7)
+
+template <int kR>
+__device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
+                                  double tempW) {
+  constexpr int kLogR = kR <= 1 ? 7 : (kR <= 2 ? 8 : 9);  // steps of a search over the merged list
+  const uint32_t lane = threadIdx.x;
+  PROF_T(p0);
+  const double T = dadd(mainW, tempW);
+  const uint32_t m = nm + np;
+  // ---- merged positions: temp t after the mains strictly below it; main j after the temps <= it
+  {
+    const double tv = L.sv[lane < np ? lane : 0];
+    double mv[kR];
+    uint32_t ml[kR], mh[kR];
+#pragma unroll
+    for (int r = 0; r < kR; r++) {
+      const uint32_t j = 64 * r + lane;
+      mv[r] = L.mm[j < nm ? j : 0];
+      ml[r] = 0;
+      mh[r] = j < nm ? np : 0;
+    }
+    uint32_t tl = 0, th = lane < np ? nm : 0;
+#pragma unroll
+    for (int it = 0; it < kLogM; it++) {
+      const uint32_t tmd = (tl + th) >> 1;
+      const double tval = L.mm[tmd < nm ? tmd : 0];
+      const bool tgo = tl < th, tlt = tval < tv;
+      tl = (tgo && tlt) ? tmd + 1 : tl;
+      th = (tgo && !tlt) ? tmd : th;
+      if (it < kLogT) {
+        uint32_t mmd[kR];
+        double mval[kR];
+#pragma unroll
+        for (int r = 0; r < kR; r++) {
+          mmd[r] = (ml[r] + mh[r]) >> 1;
+          mval[r] = L.sv[mmd[r] < np ? mmd[r] : 0];
+        }
+#pragma unroll
+        for (int r = 0; r < kR; r++) {
+          const bool go = ml[r] < mh[r], le = mval[r] <= mv[r];
+          ml[r] = (go && le) ? mmd[r] + 1 : ml[r];
+          mh[r] = (go && !le) ? mmd[r] : mh[r];
+        }
+      }
+    }
+    if (lane < np) {
+      L.gm[lane + tl] = tv;
+      L.gw[lane + tl] = L.sw[lane];
+    }
+#pragma unroll
+    for (int r = 0; r < kR; r++) {
+      const uint32_t j = 64 * r + lane;
+      if (j < nm) {
+        L.gm[j + ml[r]] = mv[r];
+        L.gw[j + ml[r]] = L.mw[j];
+      }
+    }
+  }
+  wave_lds_sync();
+  PROF_T(p1);
+  // ---- mergedWeight prefix: per-round wave scans, then the round carries (integer weights:
+  // exact in any order); otherwise the sequential fold in Go's order.  Then k per element.
+  double kv[kR];
+  {
+    double w[kR];
+    bool wint = true;
+#pragma unroll
+    for (int r = 0; r < kR; r++) {
+      const uint32_t j = 64 * r + lane;
+      const double g = L.gw[j];
+      w[r] = j < m ? g : 0.0;
+      wint &= is_int_weight(w[r]);
+    }
+    wint = __all(wint) && T <= 9007199254740992.0;
+    if (wint) {
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+        for (int r = 0; r < kR; r++) {
+          const double o = __shfl_up(w[r], d, 64);
+          w[r] = (int)lane >= d ? dadd(w[r], o) : w[r];
+        }
+      }
+      double carry = 0.0;
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+        const double tot = rl_d(w[r], 63);
+        kv[r] = dadd(carry, w[r]);
+        carry = dadd(carry, tot);
+      }
+    } else {
+      double run = 0.0;
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+        kv[r] = 0.0;
+        const uint32_t b = 64 * r;
+        const uint32_t c = b < m ? min(64u, m - b) : 0u;
+        for (uint32_t i = 0; i < c; i++) {
+          run = dadd(run, rl_d(w[r], (int)i));
+          if (i == lane) kv[r] = run;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kR; r++) kv[r] = index_estimate(x.delta, ddiv(kv[r], T));
+#pragma unroll
+    for (int r = 0; r < kR; r++) L.kin[64 * r + lane] = kv[r];
+  }
+  wave_lds_sync();
+  PROF_T(p2);
+  // ---- chain by pointer doubling (see merge_sorted); tables are padded to 64*kR entries
+  // and every entry is <= m, so all loads below stay in range without guards
+  const double k0 = index_estimate(x.delta, 0.0);
+  bool mono = true;
+#pragma unroll
+  for (int r = 0; r < kR; r++) {
+    const uint32_t j = 64 * r + lane;
+    const double prev = L.kin[j ? j - 1 : 0];
+    mono &= !(j >= 1 && j < m && kv[r] < prev);
+  }
+  mono = __all(mono);
+  PROF_T(c1);
+  PROF_ADD(9, p2, c1);
+  uint32_t nc = 0;
+  bool overflow = false;
+  const uint32_t capc = x.capc;
+  if (mono) {
+    {
+      double base[kR];
+      uint32_t bl[kR], bh[kR];
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+        const uint32_t s = 64 * r + lane;
+        const double kb = L.kin[(s >= 1 ? s - 1 : 0)];
+        base[r] = s >= 1 ? kb : k0;
+        bl[r] = s < m ? s + 1 : m;
+        bh[r] = m;
+      }
+#pragma unroll
+      for (int it = 0; it < kLogR; it++) {
+        uint32_t md[kR];
+        double kval[kR];
+#pragma unroll
+        for (int r = 0; r < kR; r++) {
+          md[r] = (bl[r] + bh[r]) >> 1;
+          kval[r] = L.kin[md[r]];
+        }
+#pragma unroll
+        for (int r = 0; r < kR; r++) {
+          const bool go = bl[r] < bh[r], gt = dsub(kval[r], base[r]) > 1.0;
+          bh[r] = (go && gt) ? md[r] : bh[r];
+          bl[r] = (go && !gt) ? md[r] + 1 : bl[r];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kR; r++) L.jump[64 * r + lane] = bl[r];
+    }
+    wave_lds_sync();
+    PROF_T(c2);
+    PROF_ADD(10, c1, c2);
+    uint32_t levels = 1;  // t < 64 * kR needs bits 0 .. levels-1
+    while ((1u << levels) < 64u * kR) levels++;
+    for (uint32_t lv = 1; lv < levels; lv++) {
+      const uint32_t* Jp = L.jump + (lv - 1) * L.JW;
+      uint32_t* Jl = L.jump + lv * L.JW;
+      uint32_t a[kR];
+#pragma unroll
+      for (int r = 0; r < kR; r++) a[r] = Jp[64 * r + lane];
+#pragma unroll
+      for (int r = 0; r < kR; r++) a[r] = Jp[a[r]];
+#pragma unroll
+      for (int r = 0; r < kR; r++) Jl[64 * r + lane] = a[r];
+      wave_lds_sync();
+    }
+    PROF_T(c3);
+    PROF_ADD(11, c2, c3);
+    uint32_t p[kR];
+#pragma unroll
+    for (int r = 0; r < kR; r++) p[r] = 0;
+    for (uint32_t lv = 0; lv < levels; lv++) {
+      const uint32_t* J = L.jump + lv * L.JW;
+#pragma unroll
+      for (int r = 0; r < kR; r++) {
+        const uint32_t t = 64 * r + lane;
+        const uint32_t nx = J[p[r]];
+        p[r] = ((t >> lv) & 1u) ? nx : p[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kR; r++) {
+      const uint32_t t = 64 * r + lane;
+      const bool on = t <= capc && p[r] < m;
+      if (on && t < capc) L.starts[t] = p[r];
+      nc += (uint32_t)__popcll(__ballot(on));
+      overflow |= on && t == capc;
+    }
+    overflow = __any(overflow);
+    if (nc > capc) nc = capc;
+    PROF_T(c4);
+    PROF_ADD(12, c3, c4);
+  } else {
+    double base = k0, kprev_carry = k0;
+    for (uint32_t b = 0; b < m && !overflow; b += 64) {
+      const uint32_t j = b + lane;
+      const bool valid = j < m;
+      const double kj = valid ? L.kin[j] : 0.0;
+      double kp = __shfl_up(kj, 1, 64);
+      if (lane == 0) kp = kprev_carry;
+      uint32_t from = 0;
+      for (;;) {
+        const bool c = valid && lane >= from && (nc == 0 || dsub(kj, base) > 1.0);
+        const uint64_t bal = __ballot(c);
+        if (!bal) break;
+        const uint32_t f = (uint32_t)__builtin_ctzll(bal);
+        if (nc >= capc) { overflow = true; break; }
+        if (lane == 0) L.starts[nc] = b + f;
+        nc++;
+        base = rl_d(kp, (int)f);
+        from = f + 1;
+      }
+      kprev_carry = rl_d(kj, 63);
+    }
+  }
+  if (overflow && lane == 0) atomicOr(x.err, 1u);
+  if (lane == 0) L.starts[nc] = m;
+  wave_lds_sync();
+  PROF_T(p3);
+  // ---- Welford per centroid, in element order
+  for (uint32_t c = lane; c < nc; c += 64) {
+    const uint32_t a = L.starts[c], e = L.starts[c + 1];
+    double mean = L.gm[a], W = L.gw[a];
+    for (uint32_t j = a + 1; j < e; j++) {
+      const double wt = L.gw[j];
+      W = dadd(W, wt);
+      mean = dadd(mean, ddiv(dmul(dsub(L.gm[j], mean), wt), W));
+    }
+    L.mm[c] = mean;
+    L.mw[c] = W;
+  }
+  wave_lds_sync();
+  PROF_T(p4);
+  PROF_ADD(1, p0, p1);
+  PROF_ADD(2, p1, p2);
+  PROF_ADD(3, p2, p3);
+  PROF_ADD(4, p3, p4);
+  PROF_ADD(5, 0, 1);
+  PROF_ADD(6, 0, (long long)m);
+  PROF_ADD(7, 0, (long long)nc);
+  nm = nc;
+  mainW = T;
+}
+
+__device__ __forceinline__ void merge_any(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
+                                          double tempW) {
+  // nc <= m < 64 * R: the fast merge's start enumeration (t < 64 * R) covers every centroid
+  const uint32_t m = nm + np;
+  if (np > 64 || m >= 64u * kR) merge_sorted(x, L, nm, mainW, np, tempW);
+  else if (m < 128) merge_sorted_fast<2>(x, L, nm, mainW, np, tempW);
+  else if (m < 192) merge_sorted_fast<3>(x, L, nm, mainW, np, tempW);
+  else if (m < 256) merge_sorted_fast<4>(x, L, nm, mainW, np, tempW);
+  else merge_sorted_fast<5>(x, L, nm, mainW, np, tempW);
+}
+
 // sort the pending temps in LDS and merge them
-__device__ void merge_pending(const ExactCtx& x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np) {
+__device__ __noinline__ void merge_pending(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np) {
   PROF_T(a0);
   const double tempW = temp_weight(L.tw, np);
   sort_temps(L.tv, L.tw, L.sv, L.sw, np);
   PROF_T(a1);
   PROF_ADD(0, a0, a1);
-  merge_sorted(x, L, nm, mainW, np, tempW);
+  merge_any(x, L, nm, mainW, np, tempW);
 }
 
 __device__ __forceinline__ uint32_t round64(uint32_t v) { return (v + 63u) & ~63u; }
@@ -497,7 +777,7 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
     tv[t] = bitsd(x.A[base + t]);
     tw[t] = (double)(1.0f / __uint_as_float((uint32_t)x.B[base + t]));  // float64(1/rate) in float32
   }
-  __syncthreads();
+  wave_lds_sync();
   const double tempW = temp_weight(tw, tcap);
   sort_temps(tv, tw, sv, sw, tcap);
   for (uint32_t t = lane; t < tcap; t += 64) {
@@ -507,7 +787,9 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
   if (lane == 0) x.ctw[base] = tempW;
 }
 
-// ---- the replay: one 64-thread block (one wave) per key
+// ---- the replay: one 64-thread block (one wave) per key.  TPL = temps per lane of a chunk
+// (1 when estimateTempBuffer <= 64, i.e. delta <= ~150; 4 up to delta 1000).
+template <int TPL>
 __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t k = blockIdx.x, lane = threadIdx.x;
@@ -515,7 +797,7 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   const uint32_t capc = x.capc, tcap = x.tcap;
   const uint32_t TP = round64(tcap + 1);
   Lds L;
-  L.JW = capc + TP + 1;
+  L.JW = max(capc + TP + 1, 320u);  // >= 64 * kR: the fast merge pads its tables
   L.levels = 1;
   while ((1u << L.levels) <= capc) L.levels++;
   L.mm = reinterpret_cast<double*>(smem);
@@ -528,9 +810,17 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   L.gw = L.gm + L.JW;
   L.kin = L.gw + L.JW;
   L.starts = reinterpret_cast<uint32_t*>(L.kin + L.JW);
-  L.jump = reinterpret_cast<uint16_t*>(L.starts + L.JW);
+  L.jump = L.starts + L.JW;
+  L.jump16 = reinterpret_cast<uint16_t*>(L.jump);
 
   PROF_T(k0);
+  // kernel arguments into registers: nothing below may take the address of x
+  const MergeParams mp{x.delta, x.capc, x.err};
+  const uint64_t* const xA = x.A;
+  const uint64_t* const xB = x.B;
+  const double* const xcsv = x.csv;
+  const double* const xcsw = x.csw;
+  const double* const xctw = x.ctw;
   const uint32_t s = x.keys[k];
   const uint32_t nex = x.nex ? x.nex[k] : 0u;
   const bool final_merge = x.flush_mode || (x.hot && x.hot[k]);
@@ -556,7 +846,7 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
     L.tv[j] = pv[j];
     L.tw[j] = pw[j];
   }
-  __syncthreads();
+  wave_lds_sync();
 
   // Histo.Sample local statistics of the replayed samples (samplers.go:346-356)
   double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
@@ -570,47 +860,47 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   // append raw samples [a, b) of the batch to the pending temps (Add order)
   auto append = [&](uint32_t a, uint32_t b) {
     for (uint32_t i = a + lane; i < b; i += 64) {
-      const double v = bitsd(x.A[lo + i]);
-      const double wt = (double)(1.0f / __uint_as_float((uint32_t)x.B[lo + i]));
+      const double v = bitsd(xA[lo + i]);
+      const double wt = (double)(1.0f / __uint_as_float((uint32_t)xB[lo + i]));
       L.tv[np + (i - a)] = v;
       L.tw[np + (i - a)] = wt;
       stat(v, wt);
     }
     np += b - a;
-    __syncthreads();
+    wave_lds_sync();
   };
 
   if (nex && np == tcap) {  // Add finds the temp list full: mergeAllTemps first
-    merge_pending(x, L, nm, mainW, np);
+    merge_pending(mp, L, nm, mainW, np);
     np = 0;
   }
   // head
   if (sp.off0) {
     append(0, sp.off0);
     if (np == tcap && sp.off0 < nex) {
-      merge_pending(x, L, nm, mainW, np);
+      merge_pending(mp, L, nm, mainW, np);
       np = 0;
     }
   }
   // pure chunks: pre-sorted by k_exact_chunk_sort; the next one is loaded before each merge
   if (sp.npure) {
-    double cv[kMaxTempPerLane], cw[kMaxTempPerLane], ctw = 0.0;
+    double cv[TPL], cw[TPL], ctw = 0.0;
     auto load = [&](uint32_t c) {
       const uint64_t base = (uint64_t)lo + sp.off0 + (uint64_t)c * tcap;
 #pragma unroll
-      for (uint32_t q = 0; q < kMaxTempPerLane; q++) {
+      for (uint32_t q = 0; q < (uint32_t)TPL; q++) {
         const uint32_t t = q * 64 + lane;
         if (t < tcap) {
-          cv[q] = x.csv[base + t];
-          cw[q] = x.csw[base + t];
+          cv[q] = xcsv[base + t];
+          cw[q] = xcsw[base + t];
         }
       }
-      ctw = x.ctw[base];
+      ctw = xctw[base];
     };
     load(0);
     for (uint32_t c = 0; c < sp.npure; c++) {
 #pragma unroll
-      for (uint32_t q = 0; q < kMaxTempPerLane; q++) {
+      for (uint32_t q = 0; q < (uint32_t)TPL; q++) {
         const uint32_t t = q * 64 + lane;
         if (t < tcap) {
           L.sv[t] = cv[q];
@@ -620,15 +910,15 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
       }
       const double tempW = ctw;
       if (c + 1 < sp.npure) load(c + 1);
-      __syncthreads();
-      merge_sorted(x, L, nm, mainW, tcap, tempW);
+      wave_lds_sync();
+      merge_any(mp, L, nm, mainW, tcap, tempW);
     }
   }
   // tail
   const uint32_t tail = sp.off0 + sp.npure * tcap;
   if (nex > tail) append(tail, nex);
   if (final_merge && np > 0) {
-    merge_pending(x, L, nm, mainW, np);
+    merge_pending(mp, L, nm, mainW, np);
     np = 0;
   }
   // ---- write back the key's digest and statistics
@@ -669,10 +959,10 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
 }
 
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap) {
-  const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = capc + TP + 1;
+  const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = std::max(capc + TP + 1, 320u);
   uint32_t levels = 1;
   while ((1u << levels) <= capc) levels++;
-  return sizeof(double) * (2 * capc + 4 * TP + 3 * JW) + sizeof(uint32_t) * JW + sizeof(uint16_t) * levels * JW + 16;
+  return sizeof(double) * (2 * capc + 4 * TP + 3 * JW) + sizeof(uint32_t) * JW + std::max<size_t>(sizeof(uint16_t) * levels * JW, tcap <= 64 ? sizeof(uint32_t) * 9 * JW : 0) + 16;
 }
 
 #ifdef VN_EXACT_PROF
@@ -689,7 +979,6 @@ extern "C" int vn_prof_exact_read(unsigned long long* out16, int reset) {
 void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks) {
   if (!x.nkeys) return;
   if (x.tcap > 64 * kMaxTempPerLane) throw std::runtime_error("temp buffer larger than the exact kernel supports");
-  if (x.capc + x.tcap + 64 >= 65535) throw std::runtime_error("centroid capacity too large for the exact kernel");
   if (x.nex) {
     // sort every pure chunk in parallel first
     hipLaunchKernelGGL(k_exact_chunk_count, dim3(blocks_for(x.nkeys, 256)), dim3(256), 0, st, x);
@@ -699,7 +988,9 @@ void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint
                          sizeof(double) * 4 * ((x.tcap + 1 + 63u) & ~63u), st, x);
   }
   size_t sm = exact_smem_bytes(x.capc, x.tcap);
-  hipLaunchKernelGGL(k_histo_exact, dim3(x.nkeys), dim3(64), sm, st, x);
+  if (sm > 160 * 1024) throw std::runtime_error("compression too large for the exact replay's LDS budget");
+  if (x.tcap <= 64) hipLaunchKernelGGL(k_histo_exact<1>, dim3(x.nkeys), dim3(64), sm, st, x);
+  else hipLaunchKernelGGL(k_histo_exact<kMaxTempPerLane>, dim3(x.nkeys), dim3(64), sm, st, x);
 }
 
 }  // namespace vn

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
     s_lc = x.lc[slot];
     s_pos = 0;
   }
-  __syncthreads();
+  lds_barrier();
   bool list_in_lds = false, list_dirty = false;
   uint32_t lbytes = x.lb[slot];
 
@@ -164,14 +164,14 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
       s_hash[i] = kHllNoCode;
       s_first[i] = 0xffffffffu;
     }
-    __syncthreads();
+    lds_barrier();
     const uint32_t tc0 = s_tc;
     if (t < tc0) {
       uint32_t c = x.tmp[(uint64_t)slot * kTmpCap + t];
       s_tmp[t] = c;
       hash_insert_par(s_hash, c);
     }
-    __syncthreads();
+    lds_barrier();
     while (s_pos < n && s_mode == 0) {
       // wave 0 advances to the next mergeSparse trigger -- the record that makes the tmpSet
       // hold kHllTmpTrigger distinct codes -- 64 records per step: a record counts if its
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
           s_trig = trig;
         }
       }
-      __syncthreads();
+      lds_barrier();
       if (!s_trig) break;
       // mergeSparse: sorted union of the list and the tmpSet
       if (!list_in_lds) {
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
         list_in_lds = true;
       }
       if (t >= kHllTmpTrigger) s_tmp[t] = kHllNoCode;
-      __syncthreads();
+      lds_barrier();
       bitonic256(s_tmp);
       const uint32_t lc = s_lc;
       uint32_t isnew = 0, lb = 0, code = 0;
@@ -234,13 +234,13 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
       uint64_t bal = __ballot(isnew);
       const int lane = t & 63, w = t >> 6;
       if (lane == 0) s_red[w] = (uint32_t)__popcll(bal);
-      __syncthreads();
+      lds_barrier();
       uint32_t before = 0;
       for (int i = 0; i < w; i++) before += s_red[i];
       const uint32_t nnew = s_red[0] + s_red[1] + s_red[2] + s_red[3];
       uint32_t rank = before + (uint32_t)__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
       if (isnew) s_new[rank] = code;
-      __syncthreads();
+      lds_barrier();
       // move list elements up by the number of new codes below them
       constexpr int kPer = (kArenaWords + kBlock - 1) / kBlock;
       uint32_t keep[kPer];
@@ -249,14 +249,14 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
         uint32_t i = t + j * kBlock;
         keep[j] = i < lc ? U[i] : 0u;
       }
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int j = 0; j < kPer; j++) {
         uint32_t i = t + j * kBlock;
         if (i < lc) U[i + lower_bound_u32(s_new, nnew, keep[j])] = keep[j];
       }
       if (isnew) U[lb + rank] = code;
-      __syncthreads();
+      lds_barrier();
       const uint32_t nlc = lc + nnew;
       // varint byte length of the delta-encoded list
       uint32_t bytes = 0;
@@ -272,7 +272,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
         s_hash[i] = kHllNoCode;
         s_first[i] = 0xffffffffu;
       }
-      __syncthreads();
+      lds_barrier();
       if (bytes > kHllM) {
         // toNormal: registers from the merged list (b stays; nz > 0 so no rebase can occur)
 #pragma unroll
@@ -280,9 +280,9 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
           uint32_t i = t + j * kBlock;
           keep[j] = i < nlc ? U[i] : kHllNoCode;
         }
-        __syncthreads();
+        lds_barrier();
         for (uint32_t i = t; i < kHllM; i += kBlock) U[i] = 0;
-        __syncthreads();
+        lds_barrier();
         const uint32_t b = s_b;
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
@@ -292,7 +292,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
             if (r > b) atomicMax(&U[ri], min(r - b, kHllCapacity - 1));
           }
         }
-        __syncthreads();
+        lds_barrier();
         uint32_t z = 0;
         for (uint32_t i = t; i < kHllM; i += kBlock) z += U[i] == 0;
         z = block_allreduce_u32_sum(z, s_red);
@@ -302,10 +302,10 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
         }
         list_in_lds = false;
         list_dirty = false;
-        __syncthreads();
+        lds_barrier();
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (s_mode == 0) {
       // write back the sparse state
       const uint32_t tc = s_tc;
@@ -323,7 +323,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
   } else {
     // ------------------------------------------------------------ dense: registers to LDS
     for (uint32_t i = t; i < kHllM; i += kBlock) U[i] = regs8[i];
-    __syncthreads();
+    lds_barrier();
   }
 
   // -------------------------------------------------------------- dense phase
@@ -361,24 +361,24 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
         // all nz of them, the fill cannot complete here, so no rebase can occur in the
         // chunk and every update is a plain max
         if (t == 0) s_filled = 0;
-        __syncthreads();
+        lds_barrier();
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
           uint32_t p = cpos0 + j * kBlock + t;
           if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == 0)
             if (atomicOr(&U[ri[j]], kMark) == 0) atomicAdd(&s_filled, 1u);
         }
-        __syncthreads();
+        lds_barrier();
         const bool completes = s_filled >= s_nz;
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
           uint32_t p = cpos0 + j * kBlock + t;
           if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
         }
-        __syncthreads();
+        lds_barrier();
         if (!completes) {
           if (t == 0) s_newfill = 0;
-          __syncthreads();
+          lds_barrier();
 #pragma unroll
           for (int j = 0; j < kItems; j++) {
             uint32_t p = cpos0 + j * kBlock + t;
@@ -387,9 +387,9 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
               if (old == 0) atomicAdd(&s_newfill, 1u);
             }
           }
-          __syncthreads();
+          lds_barrier();
           if (t == 0) s_nz -= s_newfill;
-          __syncthreads();
+          lds_barrier();
           break;
         }
         if (t == 0) {
@@ -405,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
             if (v == 0 || (v & kMark)) atomicMax(&U[ri[j]], kMark | (0x7fffffffu - p));
           }
         }
-        __syncthreads();
+        lds_barrier();
         // phase B: count first fillers, latest fill position
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
@@ -415,14 +415,14 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
             atomicMax(&s_tfull, p);
           }
         }
-        __syncthreads();
+        lds_barrier();
         tfull = (s_filled == s_nz) ? s_tfull : 0xffffffffu;
 #pragma unroll
         for (int j = 0; j < kItems; j++) {
           uint32_t p = cpos0 + j * kBlock + t;
           if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
         }
-        __syncthreads();
+        lds_barrier();
       } else {
         tfull = cpos - 1;  // already full (cpos >= 1 whenever nz == 0 inside a key's stream)
         if (cpos == 0) tfull = 0xfffffffeu;
@@ -431,7 +431,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
         s_pstar = 0xffffffffu;
         s_newfill = 0;
       }
-      __syncthreads();
+      lds_barrier();
       // phase C: first rebase candidate strictly after T_full
       if (tfull != 0xffffffffu) {
 #pragma unroll
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
           if (p >= cpos && p < cend && after && ((rr[j] - b) & 0xffu) >= kHllCapacity) atomicMin(&s_pstar, p);
         }
       }
-      __syncthreads();
+      lds_barrier();
       const uint32_t pstar = s_pstar;
       // phase D: plain max updates before the rebase point
 #pragma unroll
@@ -452,19 +452,19 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
           if (old == 0) atomicAdd(&s_newfill, 1u);
         }
       }
-      __syncthreads();
+      lds_barrier();
       if (t == 0) s_nz -= s_newfill;
-      __syncthreads();
+      lds_barrier();
       if (pstar == 0xffffffffu) break;
       // rebase at pstar (nz == 0 here): b += min(regs); regs -= min
       if (t == 0) s_min = 0xffffffffu;
-      __syncthreads();
+      lds_barrier();
       {
         uint32_t mn = 0xffffffffu;
         for (uint32_t i = t; i < kHllM; i += kBlock) mn = min(mn, U[i]);
         atomicMin(&s_min, mn);
       }
-      __syncthreads();
+      lds_barrier();
       const uint32_t db = s_min;
       uint32_t z = 0;
       for (uint32_t i = t; i < kHllM; i += kBlock) {
@@ -489,12 +489,12 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
       cpos = pstar + 1;
       if (cpos >= cend) break;
     }
   }
-  __syncthreads();
+  lds_barrier();
   for (uint32_t i = t; i < kHllM; i += kBlock) regs8[i] = (uint8_t)U[i];
   if (t == 0) {
     x.mode[slot] = 1;

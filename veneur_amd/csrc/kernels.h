@@ -25,6 +25,14 @@ void metro64_batch(const uint8_t* bytes, const uint32_t* off, uint64_t n, uint64
                    hipStream_t st);
 
 // ---------------------------------------------------------------- device helpers
+// Workgroup barrier for LDS traffic only.  __syncthreads() also waits for every outstanding
+// global load (s_waitcnt vmcnt(0)), which would stall register prefetches issued ahead of
+// it; these kernels exchange data between threads through LDS only.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// Single-wave workgroups: LDS ordering between the lanes of the wave (DS instructions of a
+// wave execute in order; the clobber stops the compiler from moving memory accesses).
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 
