@@ -95,8 +95,6 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_pos, (size_t)ch + 1);
   dalloc(e->h_tl, ch);
   dalloc(e->h_cnt, 8);
-  dalloc(e->h_oldcnt, (size_t)ch + 1);
-  dalloc(e->h_oldoff, (size_t)ch + 2);
   const uint64_t touch_max = ch ? std::min<uint64_t>(ch, R) : 0;
   e->h_sort_cap = ch ? R + touch_max * capc : 0;
   dalloc(e->hA0, e->h_sort_cap); dalloc(e->hB0, e->h_sort_cap);
@@ -131,6 +129,27 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_ccnt, touch_max);
   dalloc(e->h_coff, (size_t)touch_max + 1);
   dalloc(e->h_tw, e->h_sort_cap);
+  dalloc(e->h_seen0, touch_max);
+  dalloc(e->h_pcnt, touch_max);
+  dalloc(e->h_pi0, touch_max);
+  dalloc(e->h_pbase, (size_t)touch_max + 1);
+  dalloc(e->p_start, ch ? R + 1 : 0);
+  dalloc(e->p_end, ch ? R + 1 : 0);
+  dalloc(e->r_flag, touch_max);
+  dalloc(e->r_len, touch_max);
+  dalloc(e->r_list, touch_max);
+  dalloc(e->r_off, (size_t)touch_max + 1);
+  dalloc(e->r_pos, (size_t)touch_max + 1);
+  {
+    // piece boundaries of the geometric remainder (see ingest_histo.hip)
+    std::vector<uint64_t> geo;
+    for (uint64_t b = e->exact_threshold; geo.size() < 255 && b < (1ull << 40); b += std::max<uint64_t>(1, b / 10))
+      geo.push_back(b);
+    e->n_geo = (uint32_t)geo.size();
+    dalloc(e->h_geo, geo.size());
+    VN_HIP_CHECK(hipMemcpyAsync(e->h_geo, geo.data(), geo.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    VN_HIP_CHECK(hipStreamSynchronize(st));
+  }
 
   dalloc(e->smode, cs); dzero(e->smode, cs, st);
   dalloc(e->sbase, cs); dzero(e->sbase, cs, st);
@@ -206,13 +225,15 @@ void destroy_impl(vn_engine* e) {
   dfree(e->cval); dfree(e->ctouch); dfree(e->gseq); dfree(e->gval); dfree(e->gtouch); dfree(e->pk); dfree(e->pp);
   dfree(e->hst); dfree(e->hncent); dfree(e->hcur); dfree(e->htouch);
   for (int b = 0; b < 2; b++) { dfree(e->cmean[b]); dfree(e->cw[b]); }
-  dfree(e->h_bt); dfree(e->h_pos); dfree(e->h_tl); dfree(e->h_cnt); dfree(e->h_oldcnt); dfree(e->h_oldoff);
+  dfree(e->h_bt); dfree(e->h_pos); dfree(e->h_tl); dfree(e->h_cnt);
   dfree(e->hA0); dfree(e->hB0); dfree(e->hA1); dfree(e->hB1); dfree(e->h_w); dfree(e->h_wk);
   dfree(e->h_start); dfree(e->h_end); dfree(e->h_nch); dfree(e->h_chb);
   dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->ch_lastk); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
   dfree(e->hseen); dfree(e->hpend); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);
+  dfree(e->h_geo); dfree(e->h_seen0); dfree(e->h_pcnt); dfree(e->h_pi0); dfree(e->h_pbase); dfree(e->p_start);
+  dfree(e->p_end); dfree(e->r_flag); dfree(e->r_len); dfree(e->r_list); dfree(e->r_off); dfree(e->r_pos);
   dfree(e->smode); dfree(e->sbase); dfree(e->snz); dfree(e->slc); dfree(e->slb); dfree(e->slast); dfree(e->stc);
   dfree(e->stouch); dfree(e->stmp); dfree(e->sarena); dfree(e->sR0); dfree(e->sR1); dfree(e->s_bt);
   dfree(e->s_pos); dfree(e->s_tl); dfree(e->s_cnt); dfree(e->s_start); dfree(e->s_end);

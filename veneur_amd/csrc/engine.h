@@ -62,8 +62,6 @@ struct vn_engine {
   uint32_t* h_pos = nullptr;     // scan of flags (cap+1)
   uint32_t* h_tl = nullptr;      // touched list
   uint32_t* h_cnt = nullptr;     // device counters [8]
-  uint32_t* h_oldcnt = nullptr;  // per touched slot: existing centroids (cap)
-  uint32_t* h_oldoff = nullptr;  // scan (cap+1)
   uint64_t *hA0 = nullptr, *hB0 = nullptr, *hA1 = nullptr, *hB1 = nullptr;
   uint64_t h_sort_cap = 0;
   double* h_w = nullptr;         // per record weight
@@ -99,6 +97,16 @@ struct vn_engine {
   uint32_t* h_ccnt = nullptr;    // per touched key: pure chunks to pre-sort
   uint32_t* h_coff = nullptr;    // scan of h_ccnt (touched + 1)
   double* h_tw = nullptr;        // per chunk (at its first record): Add-order weight sum
+  // geometric remainder of hot keys (ingest_histo.hip)
+  uint64_t* h_geo = nullptr;     // piece boundaries b_0 = E, b_{i+1} = b_i + max(1, b_i / 10)
+  uint32_t n_geo = 0;
+  uint32_t* h_seen0 = nullptr;   // per touched key: window samples before this batch
+  uint32_t* h_pcnt = nullptr;    // per touched key: remainder pieces in this batch
+  uint32_t* h_pi0 = nullptr;     // per touched key: first boundary index after its remainder start
+  uint32_t* h_pbase = nullptr;   // scan of h_pcnt: piece ids
+  uint32_t* p_start = nullptr;   // per piece: range in the (piece, value)-sorted remainder
+  uint32_t* p_end = nullptr;
+  uint32_t *r_flag = nullptr, *r_len = nullptr, *r_off = nullptr, *r_pos = nullptr, *r_list = nullptr;
 
   // ---- sets
   uint8_t* smode = nullptr;      // 0 sparse, 1 dense
