@@ -1,12 +1,17 @@
 #!/bin/bash
 # GPU-box check: parity tests, bench, rocprof kernel stats.  Stops at the first step that
 # fails, faults, aborts or times out.
+#   tools/gpu_check.sh TAG [skip-tests]
 export TMPDIR=/tmp
 TAG=${1:-run}
 mkdir -p gpurun_out
-timeout -k 10 700 python -m pytest tests -m gpu -x -q > gpurun_out/${TAG}_tests.log 2>&1
-rc=$?; echo "tests_rc=$rc" >> gpurun_out/${TAG}_tests.log
-if [ $rc -ne 0 ]; then exit $rc; fi  # a failed test may be a device fault: stop here
-timeout -k 10 400 python bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.log || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
-exit $rc
+if [ "$2" != "skip-tests" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
+    > gpurun_out/${TAG}_tests.log 2>&1
+  rc=$?; echo "tests_rc=$rc" >> gpurun_out/${TAG}_tests.log
+  if [ $rc -ne 0 ]; then exit $rc; fi  # a failed test may be a device fault: stop here
+fi
+timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.log || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- \
+  python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
+exit 0
