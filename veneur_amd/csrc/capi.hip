@@ -109,7 +109,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->ch_sum, e->h_max_chunks);
   dalloc(e->ch_pre, e->h_max_chunks);
   dalloc(e->ch_stats, e->h_max_chunks * 5);
-  dalloc(e->ch_lastk, e->h_max_chunks);
+  dalloc(e->h_glk, e->h_max_chunks * (kTile / 64));
   dalloc(e->seg_T, touch_max);
   dalloc(e->starts, (size_t)touch_max * capc);
   dalloc(e->nc_new, touch_max);
@@ -228,7 +228,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->h_bt); dfree(e->h_pos); dfree(e->h_tl); dfree(e->h_cnt);
   dfree(e->hA0); dfree(e->hB0); dfree(e->hA1); dfree(e->hB1); dfree(e->h_w); dfree(e->h_wk);
   dfree(e->h_start); dfree(e->h_end); dfree(e->h_nch); dfree(e->h_chb);
-  dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->ch_lastk); dfree(e->seg_T);
+  dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->h_glk); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
   dfree(e->hseen); dfree(e->hpend); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);

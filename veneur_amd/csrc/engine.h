@@ -74,7 +74,7 @@ struct vn_engine {
   double* ch_sum = nullptr;
   double* ch_pre = nullptr;
   double* ch_stats = nullptr;    // [chunk][5]
-  double* ch_lastk = nullptr;
+  double* h_glk = nullptr;       // last k per 64-element group (hot-round chain index)
   double* seg_T = nullptr;       // per touched seg
   uint32_t* starts = nullptr;    // [touched][cap_cent]
   uint32_t* nc_new = nullptr;

@@ -26,6 +26,7 @@
 namespace vn {
 
 constexpr uint32_t kMaxCent = 2048;  // supports compression <= ~1000
+constexpr uint32_t kGroupsPerTile = kTile / 64;  // 64-element groups per 4096-element chunk
 
 struct HistoCtx {
   uint32_t ntouched;         // grid bound on segments
@@ -43,7 +44,7 @@ struct HistoCtx {
   double* ch_sum;
   double* ch_pre;
   double* ch_stats;
-  double* ch_lastk;
+  double* glk;               // last k of every 64-element group (chunk-major, kGroupsPerTile per chunk)
   double* seg_T;
   uint32_t* starts;
   uint32_t* nc_new;
@@ -210,7 +211,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(HistoCtx x) {
   }
 }
 
-// 5. k-index of every element
+// 5. k-index of every element; the last k of every 64-element group goes to glk (the chain's
+// LDS index: group q of segment k is glk[chb[k] * 64 + q])
 __global__ __launch_bounds__(kBlock) void k_chunk_kin(HistoCtx x) {
   __shared__ uint32_t s_k;
   ChunkRange r;
@@ -218,58 +220,95 @@ __global__ __launch_bounds__(kBlock) void k_chunk_kin(HistoCtx x) {
   const uint32_t c = blockIdx.x;
   const double pre = x.ch_pre[c];
   const double T = x.seg_T[r.k];
+  double* glk = x.glk + (uint64_t)x.chb[r.k] * kGroupsPerTile;
   for (uint32_t i = r.lo + threadIdx.x; i < r.hi; i += kBlock) {
     double W = dadd(pre, x.wk[i]);
     double kv = index_estimate(x.delta, ddiv(W, T));
     x.wk[i] = kv;
-    if (i == r.hi - 1) x.ch_lastk[c] = kv;
+    const uint32_t rel = i - r.seg_lo;
+    if ((rel & 63u) == 63u || i == r.seg_hi - 1) glk[rel >> 6] = kv;
   }
 }
 
-// 6 (+7 for one-chunk segments). Greedy centroid chain of mergeOne.
-__global__ __launch_bounds__(kBlock) void k_chain(HistoCtx x) {
-  __shared__ double s_kv[kTile];
+// 6. Greedy centroid chain of mergeOne, one wave per segment.  Each step finds the next
+// start = the first element j > pos with k_j - k_{pos'-1} > 1 (k monotone): one coalesced
+// 64-element load of the group holding pos+1, and if the start lies further on, a 64-ary
+// probe of the group-last index (LDS) to the group holding it, then one more load.  The
+// new base k_{next-1} is a lane of the loaded group or the previous group's last k.
+constexpr uint32_t kChainLdsGroups = 12288;  // 96 KiB of group-last k in LDS (segments <= 786k elements)
+__global__ __launch_bounds__(64) void k_chain(HistoCtx x) {
+  __shared__ double s_g[kChainLdsGroups];
   __shared__ uint32_t s_st[kMaxCent + 1];
-  __shared__ uint32_t s_nc, s_pos, s_q, s_g, s_next, s_done;
-  __shared__ double s_base;
-  const uint32_t k = blockIdx.x, t = threadIdx.x;
+  const uint32_t k = blockIdx.x, lane = threadIdx.x;
   if (x.count && k >= *x.count) return;
   const uint32_t s = x.tl[k];
   const uint32_t lo = x.start[s], n = x.end[s] - lo;
-  const uint32_t cb = x.chb[k], nch = x.chb[k + 1] - cb;
-  const double base0 = index_estimate(x.delta, 0.0);
+  const uint32_t nch = x.chb[k + 1] - x.chb[k];
   const double* kin = x.wk + lo;
+  const double* glk = x.glk + (uint64_t)x.chb[k] * kGroupsPerTile;
   const uint32_t capc = x.capc;
+  const uint32_t ng = (n + 63) >> 6;
+  const bool lds = ng <= kChainLdsGroups;
+  if (lds)
+    for (uint32_t q = lane; q < ng; q += 64) s_g[q] = glk[q];
+  wave_lds_sync();
+  auto G = [&](uint32_t q) -> double { return lds ? s_g[q] : glk[q]; };
 
-  if (nch == 1) {
-    for (uint32_t j = t; j < n; j += kBlock) s_kv[j] = kin[j];
-    __syncthreads();
-    if (t == 0) {
-      uint32_t nc = 0, pos = 0;
-      double base = base0;
-      for (;;) {
-        if (nc >= capc) { atomicOr(x.err, 1u); break; }
-        s_st[nc++] = pos;
-        uint32_t l = pos + 1, h = n;
-        while (l < h) {
-          uint32_t m = (l + h) >> 1;
-          if (dsub(s_kv[m], base) > 1.0) h = m;
-          else l = m + 1;
-        }
-        if (l >= n) break;
-        base = s_kv[l - 1];
-        pos = l;
-      }
-      s_nc = nc;
-      s_st[nc] = n;
+  uint32_t nc = 0, pos = 0;
+  double base = index_estimate(x.delta, 0.0);
+  for (;;) {
+    if (nc >= capc) {
+      if (lane == 0) atomicOr(x.err, 1u);
+      break;
     }
-    __syncthreads();
+    if (lane == 0) s_st[nc] = pos;
+    nc++;
+    const uint32_t from = pos + 1;
+    if (from >= n) break;
+    uint32_t g = from >> 6;
+    uint32_t idx = (g << 6) + lane;
+    double kv = idx < n ? kin[idx] : 0.0;
+    uint64_t m = __ballot(idx >= from && idx < n && dsub(kv, base) > 1.0);
+    if (m == 0) {
+      // the start lies beyond group g: find the first group q > g whose last k qualifies
+      uint32_t qlo = g + 1, qhi = ng;  // search [qlo, qhi)
+      bool found = false;
+      while (qlo < qhi) {
+        const uint32_t span = qhi - qlo;
+        const uint32_t step = span <= 64 ? 1u : (span + 63) / 64;
+        uint32_t q = qlo + (lane + 1) * step - 1;
+        if (q >= qhi) q = qhi - 1;
+        const uint64_t mq = __ballot(qlo + lane * step < qhi && dsub(G(q), base) > 1.0);
+        if (mq == 0) break;
+        const uint32_t f = (uint32_t)__ffsll((unsigned long long)mq) - 1;
+        const uint32_t qf = min(qlo + (f + 1) * step - 1, qhi - 1);
+        if (step == 1) {
+          g = qf;
+          found = true;
+          break;
+        }
+        qlo = qlo + f * step;  // the first qualifying group is in (previous probe, qf]
+        qhi = qf + 1;
+      }
+      if (!found) break;
+      idx = (g << 6) + lane;
+      kv = idx < n ? kin[idx] : 0.0;
+      m = __ballot(idx < n && dsub(kv, base) > 1.0);
+      if (m == 0) break;  // not reachable for a monotone k array; stop safely
+    }
+    const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
+    const uint32_t nxt = (g << 6) + f;
+    base = (f != 0) ? __shfl(kv, (int)f - 1, 64) : G(g - 1);
+    pos = nxt;
+  }
+  if (lane == 0) s_st[nc] = n;
+  wave_lds_sync();
+  if (nch == 1) {
     // Welford per centroid, in element order, exactly as mergeOne does
-    const uint32_t nc = s_nc;
     const uint8_t nb = x.hcur[s] ^ 1;
     double* cm = nb ? x.cm1 : x.cm0;
     double* cwn = nb ? x.cw1 : x.cw0;
-    for (uint32_t ci = t; ci < nc; ci += kBlock) {
+    for (uint32_t ci = lane; ci < nc; ci += 64) {
       uint32_t a = s_st[ci], b = s_st[ci + 1];
       double mean = from_ordered_bits(x.A[lo + a]);
       double W = x.w[lo + a];
@@ -282,90 +321,21 @@ __global__ __launch_bounds__(kBlock) void k_chain(HistoCtx x) {
       cm[(uint64_t)s * capc + ci] = mean;
       cwn[(uint64_t)s * capc + ci] = W;
     }
-    if (t == 0) {
+    if (lane == 0) {
       x.hncent[s] = nc;
       x.hcur[s] = nb;
       x.nc_new[k] = nc;
     }
     return;
   }
-
-  // multi-chunk segment: coarse index of chunk-last k values in LDS
-  const double* lastk = x.ch_lastk + cb;
-  const bool coarse_lds = nch <= (uint32_t)kTile;
-  if (coarse_lds)
-    for (uint32_t q = t; q < nch; q += kBlock) s_kv[q] = lastk[q];
-  if (t == 0) {
-    s_nc = 0;
-    s_pos = 0;
-    s_base = base0;
-    s_done = 0;
-  }
-  __syncthreads();
-  for (;;) {
-    // thread 0: record the start, locate the chunk holding the next start
-    if (t == 0) {
-      if (s_nc >= capc) {
-        atomicOr(x.err, 1u);
-        s_done = 1;
-      } else {
-        s_st[s_nc++] = s_pos;
-        uint32_t from = s_pos + 1;
-        if (from >= n) s_done = 1;
-        else {
-          uint32_t l = from / kTile, h = nch;
-          const double base = s_base;
-          while (l < h) {
-            uint32_t m = (l + h) >> 1;
-            double v = coarse_lds ? s_kv[m] : lastk[m];
-            if (dsub(v, base) > 1.0) h = m;
-            else l = m + 1;
-          }
-          if (l >= nch) s_done = 1;
-          else s_q = l;
-        }
-      }
-      s_g = 0xffffffffu;
-      s_next = 0xffffffffu;
-    }
-    __syncthreads();
-    if (s_done) break;
-    const uint32_t pos = s_pos, q = s_q;
-    const double base = s_base;
-    const uint32_t qlo = q * kTile, qhi = min(n, qlo + (uint32_t)kTile);
-    {  // 256-ary probe of 16-element groups
-      uint32_t gl = qlo + t * kItems;
-      if (gl < qhi) {
-        uint32_t ge = min(qhi, gl + (uint32_t)kItems) - 1;
-        if (ge > pos && dsub(kin[ge], base) > 1.0) atomicMin(&s_g, t);
-      }
-    }
-    __syncthreads();
-    if (s_g != 0xffffffffu && t < (uint32_t)kItems) {
-      uint32_t p = qlo + s_g * kItems + t;
-      if (p < qhi && p > pos && dsub(kin[p], base) > 1.0) atomicMin(&s_next, p);
-    }
-    __syncthreads();
-    if (t == 0) {
-      if (s_next == 0xffffffffu) {
-        s_done = 1;  // not reachable for a monotone k array; stop safely
-      } else {
-        s_base = kin[s_next - 1];
-        s_pos = s_next;
-      }
-    }
-    __syncthreads();
-    if (s_done) break;
-  }
-  __syncthreads();
-  const uint32_t nc = s_nc;
-  for (uint32_t ci = t; ci < nc; ci += kBlock) {
+  for (uint32_t ci = lane; ci < nc; ci += 64) {
     x.starts[(uint64_t)k * capc + ci] = s_st[ci];
     x.acc_xw[(uint64_t)k * capc + ci] = 0.0;
     x.acc_w[(uint64_t)k * capc + ci] = 0.0;
   }
-  if (t == 0) x.nc_new[k] = nc;
+  if (lane == 0) x.nc_new[k] = nc;
 }
+
 
 // 7. centroid sums of multi-chunk segments
 __global__ __launch_bounds__(kBlock) void k_chunk_cent(HistoCtx x) {
@@ -561,72 +531,132 @@ __global__ __launch_bounds__(kBlock) void k_histo_gather_hot(uint32_t ntouched, 
   }
 }
 
-// round j: which hot keys merge a piece, and how long their merged segment is
-__global__ void k_round_setup(uint32_t nhot, uint32_t j, const uint32_t* __restrict__ hotlist,
-                              const uint32_t* __restrict__ tl, const uint32_t* __restrict__ pcnt,
-                              const uint32_t* __restrict__ pbase, const uint32_t* __restrict__ pstart,
-                              const uint32_t* __restrict__ pend, const uint32_t* __restrict__ hncent,
-                              uint32_t* __restrict__ rflag, uint32_t* __restrict__ rlen) {
-  const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
-  if (h >= nhot) return;
-  const uint32_t k = hotlist[h];
-  const bool act = pcnt[k] > j;
-  uint32_t len = 0;
-  if (act) {
-    const uint32_t g = pbase[k] + j;
-    len = hncent[tl[k]] + (pend[g] - pstart[g]);
+// round j, planned by one workgroup: which hot keys merge a piece (pcnt > j), in hot-list
+// order, and for each active key a its slot (tl2), piece (rg), current centroid count (rnc),
+// merged segment [roff[a], roff[a+1]) (also start/end by slot) and chunk base chb[a];
+// count = number of active keys, roff/chb[count] = totals.
+__global__ __launch_bounds__(1024) void k_round_plan(uint32_t nhot, uint32_t j, const uint32_t* __restrict__ hotlist,
+                                                     const uint32_t* __restrict__ tl, const uint32_t* __restrict__ pcnt,
+                                                     const uint32_t* __restrict__ pbase,
+                                                     const uint32_t* __restrict__ pstart,
+                                                     const uint32_t* __restrict__ pend,
+                                                     const uint32_t* __restrict__ hncent, uint32_t* __restrict__ tl2,
+                                                     uint32_t* __restrict__ rg, uint32_t* __restrict__ rnc,
+                                                     uint32_t* __restrict__ roff, uint32_t* __restrict__ chb,
+                                                     uint32_t* __restrict__ start, uint32_t* __restrict__ end,
+                                                     uint32_t* __restrict__ count) {
+  __shared__ uint32_t s_w[3][16];
+  __shared__ uint32_t s_carry[3];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t < 3) s_carry[t] = 0;
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < nhot; b0 += 1024) {
+    const uint32_t h = b0 + t;
+    uint32_t act = 0, len = 0, nch = 0, s = 0, g = 0, nc = 0;
+    if (h < nhot) {
+      const uint32_t k = hotlist[h];
+      if (pcnt[k] > j) {
+        act = 1;
+        s = tl[k];
+        g = pbase[k] + j;
+        nc = hncent[s];
+        len = nc + (pend[g] - pstart[g]);
+        nch = (len + kTile - 1) / kTile;
+      }
+    }
+    uint32_t v[3] = {act, len, nch}, inc[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      uint32_t x = v[q];
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        uint32_t o = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += o;
+      }
+      inc[q] = x;
+      if (lane == 63) s_w[q][w] = x;
+    }
+    __syncthreads();
+    uint32_t ex[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+      uint32_t base = s_carry[q];
+      for (uint32_t i = 0; i < w; i++) base += s_w[q][i];
+      ex[q] = base + inc[q] - v[q];
+    }
+    if (act) {
+      const uint32_t a = ex[0];
+      tl2[a] = s;
+      rg[a] = g;
+      rnc[a] = nc;
+      roff[a] = ex[1];
+      chb[a] = ex[2];
+      start[s] = ex[1];
+      end[s] = ex[1] + len;
+    }
+    __syncthreads();
+    if (t < 3) {
+      uint32_t tot = 0;
+      for (uint32_t i = 0; i < 16; i++) tot += s_w[t][i];
+      s_carry[t] += tot;
+    }
+    __syncthreads();
   }
-  rflag[h] = act;
-  rlen[h] = len;
+  if (t == 0) {
+    count[0] = s_carry[0];
+    roff[s_carry[0]] = s_carry[1];
+  }
+  for (uint32_t i = s_carry[0] + t; i <= nhot; i += 1024) chb[i] = s_carry[2];  // chunk_range reads chb[nhot]
 }
 
 // round j: lay out (current centroids + piece j) of every active key in merged order -- a
 // centroid goes before a sample only if strictly smaller (merging_digest.go:169) -- in the
-// pipeline's element format (A = ordered value bits, B = slot << 32 | tag)
-__global__ __launch_bounds__(kBlock) void k_round_materialize(
-    uint32_t j, uint32_t capc, const uint32_t* __restrict__ hotlist, const uint32_t* __restrict__ tl,
-    const uint32_t* __restrict__ pbase, const uint32_t* __restrict__ pstart, const uint32_t* __restrict__ pend,
-    const uint32_t* __restrict__ rflag, const uint32_t* __restrict__ roff, const uint32_t* __restrict__ rpos,
-    const uint32_t* __restrict__ hncent, const uint8_t* __restrict__ hcur, const double* __restrict__ cm0,
-    const double* __restrict__ cm1, const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
-    uint64_t* __restrict__ Ao, uint64_t* __restrict__ Bo, uint32_t* __restrict__ tl2, uint32_t* __restrict__ start,
-    uint32_t* __restrict__ end) {
-  const uint32_t h = blockIdx.x;
-  if (!rflag[h]) return;
-  const uint32_t k = hotlist[h], s = tl[k], g = pbase[k] + j;
-  const uint32_t ps = pstart[g], np = pend[g] - ps, nc = hncent[s];
-  const uint64_t off = roff[h];
-  const double* cm = (hcur[s] ? cm1 : cm0) + (uint64_t)s * capc;
-  if (threadIdx.x == 0) {
-    tl2[rpos[h]] = s;
-    start[s] = (uint32_t)off;
-    end[s] = (uint32_t)(off + nc + np);
-  }
-  for (uint32_t c = threadIdx.x; c < nc; c += kBlock) {
-    const double v = cm[c];
-    uint32_t l = 0, hh = np;  // samples <= v
-    while (l < hh) {
-      uint32_t m = (l + hh) >> 1;
-      if (from_ordered_bits(A[ps + m]) <= v) l = m + 1;
-      else hh = m;
+// pipeline's element format (A = ordered value bits, B = slot << 32 | tag).  One thread per
+// input element over all active keys (grid-stride): its output position is its own index
+// plus the count of elements of the other list that precede it.
+__global__ __launch_bounds__(kBlock) void k_round_merge(uint32_t capc, const uint32_t* __restrict__ count,
+                                                        const uint32_t* __restrict__ tl2, const uint32_t* __restrict__ rg,
+                                                        const uint32_t* __restrict__ rnc,
+                                                        const uint32_t* __restrict__ roff,
+                                                        const uint32_t* __restrict__ pstart,
+                                                        const uint32_t* __restrict__ pend,
+                                                        const uint8_t* __restrict__ hcur, const double* __restrict__ cm0,
+                                                        const double* __restrict__ cm1, const uint64_t* __restrict__ A,
+                                                        const uint64_t* __restrict__ B, uint64_t* __restrict__ Ao,
+                                                        uint64_t* __restrict__ Bo) {
+  const uint32_t nact = *count;
+  const uint32_t total = roff[nact];
+  for (uint32_t u = blockIdx.x * kBlock + threadIdx.x; u < total; u += gridDim.x * kBlock) {
+    uint32_t a = last_le(roff, 0, nact, u);
+    const uint32_t s = tl2[a], g = rg[a], nc = rnc[a], off = roff[a];
+    const uint32_t ps = pstart[g], np = pend[g] - ps;
+    const double* cm = (hcur[s] ? cm1 : cm0) + (uint64_t)s * capc;
+    const uint32_t r = u - off;
+    if (r < nc) {
+      const double v = cm[r];
+      uint32_t l = 0, hh = np;  // samples <= v
+      while (l < hh) {
+        uint32_t m = (l + hh) >> 1;
+        if (from_ordered_bits(A[ps + m]) <= v) l = m + 1;
+        else hh = m;
+      }
+      Ao[off + r + l] = ordered_bits(v);
+      Bo[off + r + l] = ((uint64_t)s << 32) | 0x80000000ull | (uint64_t)(s * capc + r);
+    } else {
+      const uint32_t i = r - nc;
+      const uint64_t av = A[ps + i];
+      const double v = from_ordered_bits(av);
+      uint32_t l = 0, hh = nc;  // centroids < v
+      while (l < hh) {
+        uint32_t m = (l + hh) >> 1;
+        if (cm[m] < v) l = m + 1;
+        else hh = m;
+      }
+      Ao[off + i + l] = av;
+      Bo[off + i + l] = ((uint64_t)s << 32) | (B[ps + i] & 0xffffffffull);
     }
-    Ao[off + c + l] = ordered_bits(v);
-    Bo[off + c + l] = ((uint64_t)s << 32) | 0x80000000ull | (uint64_t)(s * capc + c);
-  }
-  for (uint32_t i = threadIdx.x; i < np; i += kBlock) {
-    const uint64_t a = A[ps + i];
-    const double v = from_ordered_bits(a);
-    uint32_t l = 0, hh = nc;  // centroids < v
-    while (l < hh) {
-      uint32_t m = (l + hh) >> 1;
-      if (cm[m] < v) l = m + 1;
-      else hh = m;
-    }
-    Ao[off + i + l] = a;
-    Bo[off + i + l] = ((uint64_t)s << 32) | (B[ps + i] & 0xffffffffull);
   }
 }
-
 void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate) {
   if (!n) return;
   hipStream_t st = e->st;
@@ -739,7 +769,7 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   x.ch_sum = e->ch_sum;
   x.ch_pre = e->ch_pre;
   x.ch_stats = e->ch_stats;
-  x.ch_lastk = e->ch_lastk;
+  x.glk = e->h_glk;
   x.seg_T = e->seg_T;
   x.starts = e->starts;
   x.nc_new = e->nc_new;
@@ -753,21 +783,18 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   x.cw0 = e->cw[0];
   x.cw1 = e->cw[1];
   x.err = e->h_err;
+  const int merge_blocks = std::min(1024, blocks_for(nhotrec + (uint64_t)nhot * e->cap_cent, kBlock));
   for (uint32_t j = 0; j < maxp; j++) {
-    hipLaunchKernelGGL(k_round_setup, dim3(blocks_for(nhot, 256)), dim3(256), 0, st, nhot, j, e->h_hotlist, e->h_tl,
-                       e->h_pcnt, e->h_pbase, e->p_start, e->p_end, e->hncent, e->r_flag, e->r_len);
-    compact_flags(e->r_flag, e->r_pos, e->r_list, e->h_cnt + 5, nhot, e->ss, st);
-    scan_exclusive_u32(e->r_len, e->r_off, nhot, e->ss, st);
-    hipLaunchKernelGGL(k_round_materialize, dim3(nhot), dim3(kBlock), 0, st, j, e->cap_cent, e->h_hotlist, e->h_tl,
-                       e->h_pbase, e->p_start, e->p_end, e->r_flag, e->r_off, e->r_pos, e->hncent, e->hcur,
-                       e->cmean[0], e->cmean[1], PA, PB, MA, MB, e->h_tl2, e->h_start, e->h_end);
-    hipLaunchKernelGGL(k_seg_nch, dim3(blocks_for(nhot, 256)), dim3(256), 0, st, nhot, e->h_cnt + 5, e->h_tl2,
-                       e->h_start, e->h_end, e->h_nch);
-    scan_exclusive_u32(e->h_nch, e->h_chb, nhot, e->ss, st);
+    hipLaunchKernelGGL(k_round_plan, dim3(1), dim3(1024), 0, st, nhot, j, e->h_hotlist, e->h_tl, e->h_pcnt,
+                       e->h_pbase, e->p_start, e->p_end, e->hncent, e->h_tl2, e->r_flag, e->r_len, e->r_off, e->h_chb,
+                       e->h_start, e->h_end, e->h_cnt + 5);
+    hipLaunchKernelGGL(k_round_merge, dim3(merge_blocks), dim3(kBlock), 0, st, e->cap_cent, e->h_cnt + 5, e->h_tl2,
+                       e->r_flag, e->r_len, e->r_off, e->p_start, e->p_end, e->hcur, e->cmean[0], e->cmean[1], PA, PB,
+                       MA, MB);
     hipLaunchKernelGGL(k_chunk_prep, dim3(maxch), dim3(kBlock), 0, st, x);
     hipLaunchKernelGGL(k_seg_scan, dim3(nhot), dim3(kBlock), 0, st, x);
     hipLaunchKernelGGL(k_chunk_kin, dim3(maxch), dim3(kBlock), 0, st, x);
-    hipLaunchKernelGGL(k_chain, dim3(nhot), dim3(kBlock), 0, st, x);
+    hipLaunchKernelGGL(k_chain, dim3(nhot), dim3(64), 0, st, x);
     hipLaunchKernelGGL(k_chunk_cent, dim3(maxch), dim3(kBlock), 0, st, x);
     hipLaunchKernelGGL(k_finalize, dim3(nhot), dim3(kBlock), 0, st, x);
   }
