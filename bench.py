@@ -81,6 +81,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0x5EED0003)
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--timing-steps", type=int, default=2, help="untimed steps with per-kernel HIP-event timing")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof runs)")
     args = ap.parse_args()
 
@@ -143,20 +144,25 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    eng.timing_enable(True)
-    tim = []
     barrier()
     sync()
     t0 = time.perf_counter()
     last = None
     for _ in range(args.steps):
         last = step()
-        tim.append(eng.timing())
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    # per-kernel timing (HIP events on the engine's stream) from extra, untimed steps: with
+    # timing on, the side-stream classes run serialised so every launch is measured alone
+    eng.timing_enable(True)
+    tim = []
+    for _ in range(max(1, args.timing_steps)):
+        last = step()  # every step flushes the same window: parity below reads the latest result
+        tim.append(eng.timing())
+    eng.timing_enable(False)
     for _ in range(args.profile_steps):
-        step()
+        last = step()
     elapsed = group.max(elapsed)                                  # max over ranks
     total_samples = group.sum(float(args.samples)) * args.steps  # every rank's shard stream
     ms_per_step = elapsed * 1e3 / args.steps
@@ -195,7 +201,8 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "launches_per_step": sc_launch, "ms_per_step": sc_ms},
         "path": {"algorithmic_bytes_per_step": path_bytes, "effective_GBs": path_gbs,
-                 "frac_of_hbm_peak": path_gbs / HBM_PEAK_GBS, "phase_ms": phase},
+                 "frac_of_hbm_peak": path_gbs / HBM_PEAK_GBS,
+                 "phase_ms_serialised": phase, "ms_per_step_serialised": round(sum(phase.values()), 4)},
     }
 
     # ---- CPU baseline + full-scale parity (rank 0, N=1)

@@ -69,6 +69,9 @@ void check_slots_host(const uint32_t* slot, uint64_t n, uint32_t cap, const char
 void create_impl(vn_engine* e) {
   VN_HIP_CHECK(hipSetDevice(e->device));
   VN_HIP_CHECK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+  VN_HIP_CHECK(hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
   hipStream_t st = e->st;
   const uint64_t R = e->max_records;
   const uint32_t cc = e->cap[VN_COUNTER], cg = e->cap[VN_GAUGE], ch = e->cap[VN_HISTO], cs = e->cap[VN_SET];
@@ -105,11 +108,10 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_end, ch);
   dalloc(e->h_nch, (size_t)touch_max + 1);
   dalloc(e->h_chb, (size_t)touch_max + 2);
-  e->h_max_chunks = ch ? e->h_sort_cap / kTile + touch_max + 2 : 0;
+  e->h_max_chunks = ch ? e->h_sort_cap / kHTile + touch_max + 2 : 0;
   dalloc(e->ch_sum, e->h_max_chunks);
   dalloc(e->ch_pre, e->h_max_chunks);
   dalloc(e->ch_stats, e->h_max_chunks * 5);
-  dalloc(e->h_glk, e->h_max_chunks * (kTile / 64));
   dalloc(e->seg_T, touch_max);
   dalloc(e->starts, (size_t)touch_max * capc);
   dalloc(e->nc_new, touch_max);
@@ -192,6 +194,7 @@ void create_impl(vn_engine* e) {
   halloc(e->hf_cnt, 16);
 
   radix_scratch_reserve(e->rs, std::max<uint64_t>(e->h_sort_cap, (cs || cc || cg) ? R : 0));
+  radix_scratch_reserve(e->rs2, (cs || cc || cg) ? R : 1);
   init_state(e);
   VN_HIP_CHECK(hipStreamSynchronize(st));
 }
@@ -228,7 +231,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->h_bt); dfree(e->h_pos); dfree(e->h_tl); dfree(e->h_cnt);
   dfree(e->hA0); dfree(e->hB0); dfree(e->hA1); dfree(e->hB1); dfree(e->h_w); dfree(e->h_wk);
   dfree(e->h_start); dfree(e->h_end); dfree(e->h_nch); dfree(e->h_chb);
-  dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->h_glk); dfree(e->seg_T);
+  dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
   dfree(e->hseen); dfree(e->hpend); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);
@@ -250,7 +253,13 @@ void destroy_impl(vn_engine* e) {
   dfree(e->f_hstats); hfree(e->hf_hstats); dfree(e->f_hq); hfree(e->hf_hq); dfree(e->f_sest); hfree(e->hf_sest);
   dfree(e->f_ssparse); hfree(e->hf_ssparse); dfree(e->d_pct); hfree(e->hf_cnt);
   radix_scratch_free(e->rs);
+  radix_scratch_free(e->rs2);
   if (e->ss.partials) (void)hipFree(e->ss.partials);
+  if (e->ss2.partials) (void)hipFree(e->ss2.partials);
+  if (e->st2) (void)hipStreamSynchronize(e->st2);
+  if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_join) (void)hipEventDestroy(e->ev_join);
+  if (e->st2) (void)hipStreamDestroy(e->st2);
   for (auto ev : e->pool_storage) (void)hipEventDestroy(ev);
   for (auto& ev : e->ev)
     if (ev) (void)hipEventDestroy(ev);
@@ -262,6 +271,7 @@ void check_error_flags(vn_engine* e) {
   VN_HIP_CHECK(hipMemcpy(&flags, e->h_err, sizeof(uint32_t), hipMemcpyDeviceToHost));
   if (flags & 1u) throw std::runtime_error("t-digest centroid tile overflow (compression too large for cap_cent)");
   if (flags & 2u) throw std::runtime_error("HLL rebase invariant violated");
+  if (flags & 4u) throw std::runtime_error("t-digest chain window hand-off stalled");
 }
 
 void ingest_device(vn_engine* e, const vn_batch* b) {
@@ -280,6 +290,9 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
     e->rstat_s = RadixStats{&e->pool, 0, 0};
     VN_HIP_CHECK(hipEventRecord(e->ev[0], st));
   }
+  // counters and gauges go first on the side stream, then the histo path (which waits on the
+  // host for its segment counts) on the main stream, then sets on the side stream again
+  side_begin(e);
   ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
   if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[1], st));
   ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
@@ -287,6 +300,7 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
   ingest_histos(e, b->n_histo, b->histo_slot, b->histo_value, b->histo_rate);
   if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[3], st));
   ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
+  side_join(e);
   if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[4], st));
   VN_HIP_CHECK(hipGetLastError());  // a launch that could not start (e.g. LDS over budget) fails loudly
   e->processed += b->n_counter + b->n_gauge + b->n_histo + b->n_set;
@@ -356,6 +370,29 @@ void ingest_host(vn_engine* e, const vn_batch* b) {
 }
 
 }  // namespace
+
+namespace vn {
+void side_begin(vn_engine* e) {
+  if (e->timing) {  // measured kernels run alone
+    e->side = e->st;
+    e->side_rs = &e->rs;
+    e->side_ss = &e->ss;
+    return;
+  }
+  e->side = e->st2;
+  e->side_rs = &e->rs2;
+  e->side_ss = &e->ss2;
+  VN_HIP_CHECK(hipEventRecord(e->ev_fork, e->st));
+  VN_HIP_CHECK(hipStreamWaitEvent(e->st2, e->ev_fork, 0));
+}
+void side_join(vn_engine* e) {
+  if (e->side != e->st) {
+    VN_HIP_CHECK(hipEventRecord(e->ev_join, e->st2));
+    VN_HIP_CHECK(hipStreamWaitEvent(e->st, e->ev_join, 0));
+  }
+  e->side = e->st;
+}
+}  // namespace vn
 
 extern "C" {
 
@@ -445,7 +482,9 @@ int vn_import_counters(vn_engine* e, const uint32_t* slot, const int64_t* value,
     ensure_device_stage(e);
     h2d(e->dstage.c_slot, slot, n, e->st);
     h2d(reinterpret_cast<int64_t*>(e->dstage.c_val), value, n, e->st);
+    side_begin(e);
     import_counters(e, n, e->dstage.c_slot, reinterpret_cast<const int64_t*>(e->dstage.c_val));
+    side_join(e);
     e->imported += n;
   });
 }
@@ -458,7 +497,9 @@ int vn_import_gauges(vn_engine* e, const uint32_t* slot, const double* value, ui
     ensure_device_stage(e);
     h2d(e->dstage.g_slot, slot, n, e->st);
     h2d(e->dstage.g_val, value, n, e->st);
+    side_begin(e);
     ingest_gauges(e, n, e->dstage.g_slot, e->dstage.g_val);
+    side_join(e);
     e->imported += n;
   });
 }

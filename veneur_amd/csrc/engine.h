@@ -32,7 +32,12 @@ struct DeviceBatch {  // device-resident staging for one ingest call
 struct vn_engine {
   vn_config cfg{};
   int device = 0;
-  hipStream_t st = nullptr;
+  hipStream_t st = nullptr;       // main stream (histos, flush, staging copies)
+  hipStream_t st2 = nullptr;      // side stream: counters, gauges and sets overlap the histo path
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // stream + scratch the counter / gauge / set launchers use for the current call
+  // (st2 normally; st when timing is enabled, so per-kernel durations are measured alone)
+  hipStream_t side = nullptr;
   std::string err;
   uint32_t cap[VN_NCLASS] = {0, 0, 0, 0};
   uint32_t cap_cent = 256;      // centroids per histo slot (>= 2*compression + 4)
@@ -74,7 +79,6 @@ struct vn_engine {
   double* ch_sum = nullptr;
   double* ch_pre = nullptr;
   double* ch_stats = nullptr;    // [chunk][5]
-  double* h_glk = nullptr;       // last k per 64-element group (hot-round chain index)
   double* seg_T = nullptr;       // per touched seg
   uint32_t* starts = nullptr;    // [touched][cap_cent]
   uint32_t* nc_new = nullptr;
@@ -156,6 +160,10 @@ struct vn_engine {
 
   vn::RadixScratch rs;
   vn::ScanScratch ss;
+  vn::RadixScratch rs2;           // side-stream scratch
+  vn::ScanScratch ss2;
+  vn::RadixScratch* side_rs = nullptr;
+  vn::ScanScratch* side_ss = nullptr;
 
   // ---- timing
   bool timing = false;

@@ -6,6 +6,11 @@
 
 namespace vn {
 
+// chunk geometry of the hot-key batch-merge kernels (ingest_histo.hip): small chunks spread a
+// hot key's segment over many workgroups, since only a few hundred keys take that path
+constexpr uint32_t kHItems = 4;
+constexpr uint32_t kHTile = kBlock * kHItems;  // 1024 elements per chunk
+
 struct ExactCtx {
   uint32_t nkeys;
   const uint32_t* keys;      // slot of each processed key

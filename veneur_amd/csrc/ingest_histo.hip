@@ -11,12 +11,12 @@
 //      appended as elements tagged with their centroid index (they are merged exactly like
 //      temps are merged with main in the reference);
 //   2. stable LSD radix sort by (slot, value)  -> one contiguous, value-sorted segment per key;
-//   3. per 4096-element chunk: weights, local inclusive prefix, Histo local statistics;
+//   3. per 1024-element chunk: weights, local inclusive prefix, Histo local statistics;
 //   4. per segment: chunk prefix (exact for veneur's integer weights), totals;
 //   5. per element: k = indexEstimate(W_incl / T);
 //   6. per segment: the greedy centroid chain -- each next start is the first element whose
-//      k exceeds the current start's k(W_excl/T) by more than 1 (binary search on the
-//      monotone k array, chunk-coarse index in LDS);
+//      k exceeds the current start's k(W_excl/T) by more than 1 (one wave walks the
+//      monotone k array as it streams through LDS);
 //   7. centroid sums: one-chunk segments run the reference's Welford update per centroid
 //      (thread per centroid); larger segments reduce sum(x*w), sum(w) per centroid.
 // The greedy boundary rule is the reference's; the batch (rather than 42-sample chunks)
@@ -26,7 +26,6 @@
 namespace vn {
 
 constexpr uint32_t kMaxCent = 2048;  // supports compression <= ~1000
-constexpr uint32_t kGroupsPerTile = kTile / 64;  // 64-element groups per 4096-element chunk
 
 struct HistoCtx {
   uint32_t ntouched;         // grid bound on segments
@@ -44,7 +43,6 @@ struct HistoCtx {
   double* ch_sum;
   double* ch_pre;
   double* ch_stats;
-  double* glk;               // last k of every 64-element group (chunk-major, kGroupsPerTile per chunk)
   double* seg_T;
   uint32_t* starts;
   uint32_t* nc_new;
@@ -70,19 +68,6 @@ __global__ void k_seg_mark(uint64_t n, const uint64_t* __restrict__ B, uint32_t*
   if (i == n - 1 || (uint32_t)(B[i + 1] >> 32) != s) end[s] = (uint32_t)(i + 1);
 }
 
-__global__ void k_seg_nch(uint32_t ntouched, const uint32_t* __restrict__ count, const uint32_t* __restrict__ tl,
-                          const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
-                          uint32_t* __restrict__ nch) {
-  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= ntouched) return;
-  if (count && k >= *count) {
-    nch[k] = 0;
-    return;
-  }
-  uint32_t s = tl[k];
-  nch[k] = (end[s] - start[s] + kTile - 1) / kTile;
-}
-
 __device__ __forceinline__ uint32_t find_seg(const uint32_t* chb, uint32_t ntouched, uint32_t c) {
   uint32_t lo = 0, hi = ntouched;
   while (hi - lo > 1) {
@@ -105,8 +90,8 @@ __device__ __forceinline__ bool chunk_range(const HistoCtx& x, ChunkRange& r, ui
   r.s = x.tl[r.k];
   r.seg_lo = x.start[r.s];
   r.seg_hi = x.end[r.s];
-  r.lo = r.seg_lo + (c - x.chb[r.k]) * kTile;
-  r.hi = min(r.seg_hi, r.lo + (uint32_t)kTile);
+  r.lo = r.seg_lo + (c - x.chb[r.k]) * kHTile;
+  r.hi = min(r.seg_hi, r.lo + kHTile);
   r.nch = x.chb[r.k + 1] - x.chb[r.k];
   return true;
 }
@@ -119,11 +104,11 @@ __global__ __launch_bounds__(kBlock) void k_chunk_prep(HistoCtx x) {
   if (!chunk_range(x, r, &s_k)) return;
   const uint32_t c = blockIdx.x, t = threadIdx.x;
   const double* cwo = x.hcur[r.s] ? x.cw1 : x.cw0;
-  double wv[kItems];
+  double wv[kHItems];
   double run = 0.0, sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
-  const uint32_t base = r.lo + t * kItems;
+  const uint32_t base = r.lo + t * kHItems;
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
+  for (int j = 0; j < (int)kHItems; j++) {
     uint32_t i = base + j;
     wv[j] = 0.0;
     if (i < r.hi) {
@@ -149,7 +134,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_prep(HistoCtx x) {
   double tot;
   double acc = block_excl_scan_d(run, s_tmp, tot);
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
+  for (int j = 0; j < (int)kHItems; j++) {
     uint32_t i = base + j;
     if (i < r.hi) {
       acc = dadd(acc, wv[j]);
@@ -211,8 +196,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(HistoCtx x) {
   }
 }
 
-// 5. k-index of every element; the last k of every 64-element group goes to glk (the chain's
-// LDS index: group q of segment k is glk[chb[k] * 64 + q])
+// 5. k-index of every element
 __global__ __launch_bounds__(kBlock) void k_chunk_kin(HistoCtx x) {
   __shared__ uint32_t s_k;
   ChunkRange r;
@@ -220,95 +204,163 @@ __global__ __launch_bounds__(kBlock) void k_chunk_kin(HistoCtx x) {
   const uint32_t c = blockIdx.x;
   const double pre = x.ch_pre[c];
   const double T = x.seg_T[r.k];
-  double* glk = x.glk + (uint64_t)x.chb[r.k] * kGroupsPerTile;
   for (uint32_t i = r.lo + threadIdx.x; i < r.hi; i += kBlock) {
     double W = dadd(pre, x.wk[i]);
-    double kv = index_estimate(x.delta, ddiv(W, T));
-    x.wk[i] = kv;
-    const uint32_t rel = i - r.seg_lo;
-    if ((rel & 63u) == 63u || i == r.seg_hi - 1) glk[rel >> 6] = kv;
+    x.wk[i] = index_estimate(x.delta, ddiv(W, T));
   }
 }
 
-// 6. Greedy centroid chain of mergeOne, one wave per segment.  Each step finds the next
-// start = the first element j > pos with k_j - k_{pos'-1} > 1 (k monotone): one coalesced
-// 64-element load of the group holding pos+1, and if the start lies further on, a 64-ary
-// probe of the group-last index (LDS) to the group holding it, then one more load.  The
-// new base k_{next-1} is a lane of the loaded group or the previous group's last k.
-constexpr uint32_t kChainLdsGroups = 12288;  // 96 KiB of group-last k in LDS (segments <= 786k elements)
-__global__ __launch_bounds__(64) void k_chain(HistoCtx x) {
-  __shared__ double s_g[kChainLdsGroups];
+// 6. Greedy centroid chain of mergeOne, one workgroup per segment.  The walk moves forward
+// through the segment's k array, so the array streams through an LDS ring of windows of kCW
+// elements: waves 1..3 load windows (each keeps two in flight in registers) and publish them
+// into ring slots; wave 0 walks.  Each step finds the next start = the first element j > pos
+// with k_j - k_{pos-1} > 1 (k monotone) by one probe of the window's 64-element group-last
+// values and one probe of that group, both LDS reads; the new base k_{next-1} is a lane of the
+// probed group or the previous group's (window's) last k.  Loader/walker hand-offs are LDS
+// flags (workgroup scope) with bounded spins: a stalled protocol flags an error, never hangs.
+constexpr uint32_t kCW = 2048;        // elements per window
+constexpr uint32_t kCWL = kCW / 64;   // window elements per lane (registers) = groups per window
+constexpr uint32_t kRing = 6;         // LDS ring slots (96 KiB)
+constexpr uint32_t kLoaders = 3;
+constexpr uint32_t kSpinCap = 1u << 24;
+
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__global__ __launch_bounds__(256) void k_chain(HistoCtx x) {
+  __shared__ double s_win[kRing][kCW];
+  __shared__ double s_last[kRing][kCWL];
   __shared__ uint32_t s_st[kMaxCent + 1];
-  const uint32_t k = blockIdx.x, lane = threadIdx.x;
+  __shared__ uint32_t s_ready[kRing];  // window id + 1 published in the slot
+  __shared__ uint32_t s_done;          // windows [0, s_done) released by the walker
+  __shared__ uint32_t s_nc;
+  const uint32_t k = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   if (x.count && k >= *x.count) return;
   const uint32_t s = x.tl[k];
   const uint32_t lo = x.start[s], n = x.end[s] - lo;
   const uint32_t nch = x.chb[k + 1] - x.chb[k];
   const double* kin = x.wk + lo;
-  const double* glk = x.glk + (uint64_t)x.chb[k] * kGroupsPerTile;
   const uint32_t capc = x.capc;
-  const uint32_t ng = (n + 63) >> 6;
-  const bool lds = ng <= kChainLdsGroups;
-  if (lds)
-    for (uint32_t q = lane; q < ng; q += 64) s_g[q] = glk[q];
-  wave_lds_sync();
-  auto G = [&](uint32_t q) -> double { return lds ? s_g[q] : glk[q]; };
+  const uint32_t nw = (n + kCW - 1) / kCW;
+  if (t < kRing) s_ready[t] = 0;
+  if (t == 0) s_done = 0;
+  __syncthreads();
 
-  uint32_t nc = 0, pos = 0;
-  double base = index_estimate(x.delta, 0.0);
-  for (;;) {
-    if (nc >= capc) {
-      if (lane == 0) atomicOr(x.err, 1u);
-      break;
+  if (wave != 0) {
+    // ---- loader: windows w = wave-1, wave-1+3, ...; two in flight in registers
+    double ra[kCWL], rb[kCWL];
+    auto fetch = [&](double* r, uint32_t w) {
+      const uint32_t b = w * kCW;
+#pragma unroll
+      for (uint32_t j = 0; j < kCWL; j++) {
+        const uint32_t i = b + 64 * j + lane;
+        r[j] = i < n ? kin[i] : kInf;
+      }
+    };
+    auto publish = [&](const double* r, uint32_t w) -> bool {
+      uint32_t spins = 0;
+      while (w >= lds_ld(&s_done) + kRing) {  // slot still holds a window the walker needs
+        if (++spins > kSpinCap) return false;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      double* bw = s_win[w % kRing];
+#pragma unroll
+      for (uint32_t j = 0; j < kCWL; j++) bw[64 * j + lane] = r[j];
+      wave_lds_sync();
+      if (lane < kCWL) s_last[w % kRing][lane] = bw[64 * lane + 63];
+      wave_lds_sync();
+      if (lane == 0) lds_st(&s_ready[w % kRing], w + 1);
+      return true;
+    };
+    uint32_t w = wave - 1;
+    if (w < nw) fetch(ra, w);
+    if (w + kLoaders < nw) fetch(rb, w + kLoaders);
+    for (; w < nw; w += 2 * kLoaders) {
+      if (!publish(ra, w)) break;
+      if (w + 2 * kLoaders < nw) fetch(ra, w + 2 * kLoaders);
+      if (w + kLoaders >= nw) break;
+      if (!publish(rb, w + kLoaders)) break;
+      if (w + 3 * kLoaders < nw) fetch(rb, w + 3 * kLoaders);
     }
-    if (lane == 0) s_st[nc] = pos;
-    nc++;
-    const uint32_t from = pos + 1;
-    if (from >= n) break;
-    uint32_t g = from >> 6;
-    uint32_t idx = (g << 6) + lane;
-    double kv = idx < n ? kin[idx] : 0.0;
-    uint64_t m = __ballot(idx >= from && idx < n && dsub(kv, base) > 1.0);
-    if (m == 0) {
-      // the start lies beyond group g: find the first group q > g whose last k qualifies
-      uint32_t qlo = g + 1, qhi = ng;  // search [qlo, qhi)
-      bool found = false;
-      while (qlo < qhi) {
-        const uint32_t span = qhi - qlo;
-        const uint32_t step = span <= 64 ? 1u : (span + 63) / 64;
-        uint32_t q = qlo + (lane + 1) * step - 1;
-        if (q >= qhi) q = qhi - 1;
-        const uint64_t mq = __ballot(qlo + lane * step < qhi && dsub(G(q), base) > 1.0);
-        if (mq == 0) break;
-        const uint32_t f = (uint32_t)__ffsll((unsigned long long)mq) - 1;
-        const uint32_t qf = min(qlo + (f + 1) * step - 1, qhi - 1);
-        if (step == 1) {
-          g = qf;
-          found = true;
-          break;
+  } else {
+    // ---- walker
+    bool ok = true;
+    auto acquire = [&](uint32_t w) {
+      uint32_t spins = 0;
+      while (lds_ld(&s_ready[w % kRing]) != w + 1) {
+        if (++spins > kSpinCap) {
+          ok = false;
+          return;
         }
-        qlo = qlo + f * step;  // the first qualifying group is in (previous probe, qf]
-        qhi = qf + 1;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    };
+    uint32_t cw = 0;          // window the walk is in
+    double prev_last = 0.0;   // last k of window cw - 1
+    acquire(0);
+    uint32_t nc = 0, pos = 0;
+    double base = index_estimate(x.delta, 0.0);
+    while (ok) {
+      if (nc >= capc) {
+        if (lane == 0) atomicOr(x.err, 1u);
+        break;
+      }
+      if (lane == 0) s_st[nc] = pos;
+      nc++;
+      uint32_t from = pos + 1;
+      if (from >= n) break;
+      bool found = false;
+      for (;;) {
+        while (from >= (cw + 1) * kCW) {  // the start lies in a later window
+          prev_last = s_win[cw % kRing][kCW - 1];
+          cw++;
+          if (lane == 0) lds_st(&s_done, cw);  // release the window left behind
+          acquire(cw);
+          if (!ok) break;
+        }
+        if (!ok) break;
+        const uint32_t slot = cw % kRing;
+        const uint32_t wb = cw * kCW, q0 = (from - wb) >> 6;
+        const double gl = s_last[slot][lane < kCWL ? lane : 0];
+        const uint64_t mq = __ballot(lane >= q0 && lane < kCWL && dsub(gl, base) > 1.0);
+        if (mq == 0) {
+          if (wb + kCW >= n) break;  // no later element qualifies: the chain ends
+          from = wb + kCW;
+          continue;
+        }
+        const uint32_t q = (uint32_t)__ffsll((unsigned long long)mq) - 1;
+        const uint32_t idx = wb + 64 * q + lane;
+        const double kv = s_win[slot][64 * q + lane];
+        const uint64_t m = __ballot(idx >= from && idx < n && dsub(kv, base) > 1.0);
+        if (m == 0) break;  // only padding past n qualified: the chain ends
+        const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
+        const double kprev = __shfl(kv, f ? (int)f - 1 : 0, 64);
+        base = f ? kprev : (q ? s_last[slot][q - 1] : prev_last);
+        pos = wb + 64 * q + f;
+        found = true;
+        break;
       }
       if (!found) break;
-      idx = (g << 6) + lane;
-      kv = idx < n ? kin[idx] : 0.0;
-      m = __ballot(idx < n && dsub(kv, base) > 1.0);
-      if (m == 0) break;  // not reachable for a monotone k array; stop safely
     }
-    const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
-    const uint32_t nxt = (g << 6) + f;
-    base = (f != 0) ? __shfl(kv, (int)f - 1, 64) : G(g - 1);
-    pos = nxt;
+    if (!ok && lane == 0) atomicOr(x.err, 4u);
+    if (lane == 0) {
+      s_st[nc] = n;
+      s_nc = nc;
+      lds_st(&s_done, nw + kRing);  // release everything: loaders still waiting finish
+    }
   }
-  if (lane == 0) s_st[nc] = n;
-  wave_lds_sync();
+  __syncthreads();
+  const uint32_t nc = s_nc;
   if (nch == 1) {
     // Welford per centroid, in element order, exactly as mergeOne does
     const uint8_t nb = x.hcur[s] ^ 1;
     double* cm = nb ? x.cm1 : x.cm0;
     double* cwn = nb ? x.cw1 : x.cw0;
-    for (uint32_t ci = lane; ci < nc; ci += 64) {
+    for (uint32_t ci = t; ci < nc; ci += 256) {
       uint32_t a = s_st[ci], b = s_st[ci + 1];
       double mean = from_ordered_bits(x.A[lo + a]);
       double W = x.w[lo + a];
@@ -321,21 +373,21 @@ __global__ __launch_bounds__(64) void k_chain(HistoCtx x) {
       cm[(uint64_t)s * capc + ci] = mean;
       cwn[(uint64_t)s * capc + ci] = W;
     }
-    if (lane == 0) {
+    __syncthreads();
+    if (t == 0) {
       x.hncent[s] = nc;
       x.hcur[s] = nb;
       x.nc_new[k] = nc;
     }
     return;
   }
-  for (uint32_t ci = lane; ci < nc; ci += 64) {
+  for (uint32_t ci = t; ci < nc; ci += 256) {
     x.starts[(uint64_t)k * capc + ci] = s_st[ci];
     x.acc_xw[(uint64_t)k * capc + ci] = 0.0;
     x.acc_w[(uint64_t)k * capc + ci] = 0.0;
   }
-  if (lane == 0) x.nc_new[k] = nc;
+  if (t == 0) x.nc_new[k] = nc;
 }
-
 
 // 7. centroid sums of multi-chunk segments
 __global__ __launch_bounds__(kBlock) void k_chunk_cent(HistoCtx x) {
@@ -356,7 +408,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_cent(HistoCtx x) {
   }
   if (t == 0) s_st[nc] = n;
   __syncthreads();
-  const uint32_t b0 = r.lo + t * kItems;
+  const uint32_t b0 = r.lo + t * kHItems;
   if (b0 < r.hi) {
     uint32_t rel = b0 - r.seg_lo;
     uint32_t l = 0, h = nc;  // last centroid with start <= rel
@@ -367,7 +419,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_cent(HistoCtx x) {
     }
     uint32_t cid = l;
     double axw = 0.0, aw = 0.0;
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < (int)kHItems; j++) {
       uint32_t i = b0 + j;
       if (i >= r.hi) break;
       rel = i - r.seg_lo;
@@ -561,7 +613,7 @@ __global__ __launch_bounds__(1024) void k_round_plan(uint32_t nhot, uint32_t j, 
         g = pbase[k] + j;
         nc = hncent[s];
         len = nc + (pend[g] - pstart[g]);
-        nch = (len + kTile - 1) / kTile;
+        nch = (len + kHTile - 1) / kHTile;
       }
     }
     uint32_t v[3] = {act, len, nch}, inc[3];
@@ -750,7 +802,7 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(nhotrec, 256)), dim3(256), 0, st, nhotrec, PB, e->p_start,
                      e->p_end);
 
-  const uint64_t maxch = (nhotrec + (uint64_t)nhot * e->cap_cent) / kTile + nhot + 1;
+  const uint64_t maxch = (nhotrec + (uint64_t)nhot * e->cap_cent) / kHTile + nhot + 1;
   if (maxch > e->h_max_chunks || nhotrec + (uint64_t)nhot * e->cap_cent > e->h_sort_cap)
     throw std::runtime_error("histo chunk capacity exceeded");
   HistoCtx x;
@@ -769,7 +821,6 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   x.ch_sum = e->ch_sum;
   x.ch_pre = e->ch_pre;
   x.ch_stats = e->ch_stats;
-  x.glk = e->h_glk;
   x.seg_T = e->seg_T;
   x.starts = e->starts;
   x.nc_new = e->nc_new;
@@ -794,7 +845,7 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
     hipLaunchKernelGGL(k_chunk_prep, dim3(maxch), dim3(kBlock), 0, st, x);
     hipLaunchKernelGGL(k_seg_scan, dim3(nhot), dim3(kBlock), 0, st, x);
     hipLaunchKernelGGL(k_chunk_kin, dim3(maxch), dim3(kBlock), 0, st, x);
-    hipLaunchKernelGGL(k_chain, dim3(nhot), dim3(64), 0, st, x);
+    hipLaunchKernelGGL(k_chain, dim3(nhot), dim3(256), 0, st, x);
     hipLaunchKernelGGL(k_chunk_cent, dim3(maxch), dim3(kBlock), 0, st, x);
     hipLaunchKernelGGL(k_finalize, dim3(nhot), dim3(kBlock), 0, st, x);
   }

@@ -124,14 +124,14 @@ __global__ void k_counter_import(uint64_t n, const uint32_t* __restrict__ slot, 
 void ingest_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate) {
   if (!n) return;
   RadixStats* rs = e->timing ? &e->rstat_c : nullptr;
-  partition_pass(CounterSrc{slot, val, rate}, KV64Dst{e->pk, e->pp}, n, 0, e->rs, e->st, rs, 16 + 12);
-  hipLaunchKernelGGL(k_scalar_agg<false>, dim3(blocks_for(n, kAggChunk)), dim3(kAggThreads), 0, e->st, n, e->pk,
+  partition_pass(CounterSrc{slot, val, rate}, KV64Dst{e->pk, e->pp}, n, 0, *e->side_rs, e->side, rs, 16 + 12);
+  hipLaunchKernelGGL(k_scalar_agg<false>, dim3(blocks_for(n, kAggChunk)), dim3(kAggThreads), 0, e->side, n, e->pk,
                      e->pp, 0, (uint64_t*)e->cval, e->ctouch);
 }
 
 void import_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const int64_t* val) {
   if (!n) return;
-  hipLaunchKernelGGL(k_counter_import, dim3(blocks_for(n, 256)), dim3(256), 0, e->st, n, slot, val, e->cval,
+  hipLaunchKernelGGL(k_counter_import, dim3(blocks_for(n, 256)), dim3(256), 0, e->side, n, slot, val, e->cval,
                      e->ctouch);
 }
 
@@ -140,10 +140,10 @@ void ingest_gauges(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   const uint64_t base = e->seq_base;
   e->seq_base += n;
   RadixStats* rs = e->timing ? &e->rstat_c : nullptr;
-  partition_pass(GaugeSrc{slot, val}, KV64Dst{e->pk, e->pp}, n, 0, e->rs, e->st, rs, 12 + 12);
-  hipLaunchKernelGGL(k_scalar_agg<true>, dim3(blocks_for(n, kAggChunk)), dim3(kAggThreads), 0, e->st, n, e->pk,
+  partition_pass(GaugeSrc{slot, val}, KV64Dst{e->pk, e->pp}, n, 0, *e->side_rs, e->side, rs, 12 + 12);
+  hipLaunchKernelGGL(k_scalar_agg<true>, dim3(blocks_for(n, kAggChunk)), dim3(kAggThreads), 0, e->side, n, e->pk,
                      nullptr, base, e->gseq, e->gtouch);
-  hipLaunchKernelGGL(k_gauge_resolve, dim3(blocks_for(e->cap[VN_GAUGE], 256)), dim3(256), 0, e->st,
+  hipLaunchKernelGGL(k_gauge_resolve, dim3(blocks_for(e->cap[VN_GAUGE], 256)), dim3(256), 0, e->side,
                      e->cap[VN_GAUGE], base, e->gseq, e->pp, e->gval);
 }
 

@@ -514,21 +514,21 @@ __global__ void k_set_clear_flags(uint32_t n, const uint32_t* __restrict__ list,
 void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t* off, const uint8_t* bytes,
                  const uint64_t* hashes) {
   if (!n) return;
-  hipStream_t st = e->st;
+  hipStream_t st = e->side;
   const uint32_t caps = e->cap[VN_SET];
   hipLaunchKernelGGL(k_set_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, off, bytes, hashes, e->sR0,
                      e->s_bt, e->stouch);
   RadixPass passes[4];
   int np = 0;
   for (int sh = 32; sh < 32 + e->slot_bits[VN_SET]; sh += 8) passes[np++] = RadixPass{false, sh};
-  bool fl = radix_sort(e->sR0, nullptr, e->sR1, nullptr, n, passes, np, e->rs, st,
+  bool fl = radix_sort(e->sR0, nullptr, e->sR1, nullptr, n, passes, np, *e->side_rs, st,
                        e->timing ? &e->rstat_s : nullptr);
   const uint64_t* R = fl ? e->sR1 : e->sR0;
   hipLaunchKernelGGL(k_set_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, R, e->s_start, e->s_end);
-  compact_flags(e->s_bt, e->s_pos, e->s_tl, e->s_cnt, caps, e->ss, st);
-  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 2, e->s_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  compact_flags(e->s_bt, e->s_pos, e->s_tl, e->s_cnt, caps, *e->side_ss, st);
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 8, e->s_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipStreamSynchronize(st));
-  const uint32_t ntouched = e->hf_cnt[2];
+  const uint32_t ntouched = e->hf_cnt[8];
   if (!ntouched) return;
   SetCtx x;
   x.ntouched = ntouched;

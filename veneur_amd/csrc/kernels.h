@@ -6,6 +6,10 @@
 
 namespace vn {
 
+// The side stream: work issued between side_begin and side_join runs on e->side, after
+// everything already issued on the main stream; the main stream waits for it at the join.
+void side_begin(vn_engine* e);
+void side_join(vn_engine* e);
 // Counter.Sample (samplers.go:132-134) / Counter.Combine (171-183)
 void ingest_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate);
 void import_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const int64_t* val);
