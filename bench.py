@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--samples", type=int, default=100_000_000, help="samples per rank per flush window")
     ap.add_argument("--batches", type=int, default=1, help="ingest calls per flush window")
     ap.add_argument("--seed", type=int, default=0x5EED0003)
+    ap.add_argument("--exact-threshold", type=int, default=0,
+                    help="t-digest samples per key and window replayed bit-exactly (0: engine default)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timing-steps", type=int, default=2, help="untimed steps with per-kernel HIP-event timing")
@@ -104,7 +106,7 @@ def main():
     per_batch = [(c + args.batches - 1) // args.batches for c in counts]
     eng = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,
                    max_batch_records=max(per_batch) + 1, max_batch_member_bytes=int(len(d["s_bytes"])) + 64,
-                   device=local_rank)
+                   device=local_rank, exact_threshold=args.exact_threshold)
     bufs = []
 
     def dev(a):

@@ -559,9 +559,9 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
   }
   wave_lds_sync();
   PROF_T(p2);
+  const double k0 = index_estimate(x.delta, 0.0);
   // ---- chain by pointer doubling (see merge_sorted); tables are padded to 64*kR entries
   // and every entry is <= m, so all loads below stay in range without guards
-  const double k0 = index_estimate(x.delta, 0.0);
   bool mono = true;
 #pragma unroll
   for (int r = 0; r < kR; r++) {
