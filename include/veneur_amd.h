@@ -165,6 +165,14 @@ int vn_ingest(vn_engine* eng, const vn_batch* device_batch);     /* inputs alrea
 int vn_import_counters(vn_engine* eng, const uint32_t* slot, const int64_t* value, uint64_t n);
 int vn_import_gauges(vn_engine* eng, const uint32_t* slot, const double* value, uint64_t n);
 
+/* ImportMetric for histograms and timers (worker.go:253-266): Histo.Combine
+ * (samplers.go:519-526) of each payload = the forwarded MergingDigest.GobEncode() bytes
+ * (merging_digest.go:361-380), payload i = bytes[off[i], off[i+1]), into histo slot[i], in
+ * order.  Every centroid is Add()ed to the key's digest (MergingDigest.Merge, 344-356, in the
+ * stored order instead of rand.Perm); Local* statistics are untouched.  A malformed payload, or
+ * a centroid Add() would panic on, fails the whole call with VN_EDECODE and applies nothing. */
+int vn_import_histos(vn_engine* eng, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n);
+
 int vn_flush(vn_engine* eng, vn_flush_result* out);
 int vn_sync(vn_engine* eng);
 

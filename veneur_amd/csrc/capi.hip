@@ -33,6 +33,11 @@ void hfree(T*& p) {
   p = nullptr;
 }
 
+template <class T>
+void h2d(T* dst, const T* src, uint64_t n, hipStream_t st) {
+  if (n) VN_HIP_CHECK(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, st));
+}
+
 int bits_for(uint32_t cap) {
   int b = 1;
   while (b < 32 && (1u << b) < cap) b++;
@@ -52,6 +57,8 @@ int guarded(vn_engine* e, F&& f) {
   } catch (const HipError& h) {
     return fail(e, VN_EHIP, std::string(hipGetErrorString(h.err)) + " at " + h.file + ":" + std::to_string(h.line) +
                                 ": " + h.expr);
+  } catch (const DecodeError& x) {
+    return fail(e, VN_EDECODE, x.what());
   } catch (const std::invalid_argument& x) {
     return fail(e, VN_EINVAL, x.what());
   } catch (const std::bad_alloc&) {
@@ -111,7 +118,7 @@ void create_impl(vn_engine* e) {
   e->h_max_chunks = ch ? e->h_sort_cap / kHTile + touch_max + 2 : 0;
   dalloc(e->ch_sum, e->h_max_chunks);
   dalloc(e->ch_pre, e->h_max_chunks);
-  dalloc(e->ch_stats, e->h_max_chunks * 5);
+  dalloc(e->ch_stats, e->h_max_chunks * kChunkStats);
   dalloc(e->seg_T, touch_max);
   dalloc(e->starts, (size_t)touch_max * capc);
   dalloc(e->nc_new, touch_max);
@@ -223,6 +230,48 @@ void ensure_pinned_stage(vn_engine* e) {
   halloc(p.set_slot, R); halloc(p.set_member_off, R + 1); halloc(p.set_member_bytes, e->max_member_bytes);
 }
 
+// import staging, grown to the call's payload count / byte size
+void ensure_import(vn_engine* e, uint64_t n, uint64_t nbytes) {
+  ImportScratch& s = e->imp;
+  if (n > s.cap_n) {
+    dfree(s.in_slot); dfree(s.in_off); dfree(s.cnt); dfree(s.coff);
+    if (s.parts) (void)hipFree(s.parts);
+    s.cap_n = std::max<uint64_t>(n, 1024);
+    dalloc(s.in_slot, s.cap_n);
+    dalloc(s.in_off, s.cap_n + 1);
+    dalloc(s.cnt, s.cap_n + 1);
+    dalloc(s.coff, s.cap_n + 1);
+    VN_HIP_CHECK(hipMalloc(&s.parts, s.cap_n * 64));
+  }
+  if (nbytes > s.cap_bytes) {
+    dfree(s.in_bytes);
+    s.cap_bytes = std::max<uint64_t>(nbytes, 1 << 16);
+    dalloc(s.in_bytes, s.cap_bytes);
+  }
+  if (!s.cap_cent) {
+    s.cap_cent = e->max_records;
+    dalloc(s.cslot, s.cap_cent);
+    dalloc(s.cmean, s.cap_cent);
+    dalloc(s.cw, s.cap_cent);
+  }
+}
+
+// stage host payloads (slot[n], off[n+1], bytes) for an import call
+void stage_import(vn_engine* e, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n,
+                  uint32_t cap) {
+  if (n > e->max_records) throw std::invalid_argument("import batch larger than max_batch_records");
+  check_slots_host(slot, n, cap, "import");
+  for (uint64_t i = 0; i < n; i++)
+    if (off[i + 1] < off[i]) throw std::invalid_argument("import offsets must be non-decreasing");
+  const uint64_t nb = off[n];
+  ensure_import(e, n, nb);
+  ImportScratch& s = e->imp;
+  hipStream_t st = e->st;
+  h2d(s.in_slot, slot, n, st);
+  h2d(s.in_off, off, n + 1, st);
+  h2d(s.in_bytes, bytes, nb, st);
+}
+
 void destroy_impl(vn_engine* e) {
   if (e->st) (void)hipStreamSynchronize(e->st);
   dfree(e->cval); dfree(e->ctouch); dfree(e->gseq); dfree(e->gval); dfree(e->gtouch); dfree(e->pk); dfree(e->pp);
@@ -240,6 +289,10 @@ void destroy_impl(vn_engine* e) {
   dfree(e->smode); dfree(e->sbase); dfree(e->snz); dfree(e->slc); dfree(e->slb); dfree(e->slast); dfree(e->stc);
   dfree(e->stouch); dfree(e->stmp); dfree(e->sarena); dfree(e->sR0); dfree(e->sR1); dfree(e->s_bt);
   dfree(e->s_pos); dfree(e->s_tl); dfree(e->s_cnt); dfree(e->s_start); dfree(e->s_end);
+  ImportScratch& is = e->imp;
+  dfree(is.in_slot); dfree(is.in_off); dfree(is.in_bytes); dfree(is.cnt); dfree(is.coff); dfree(is.cslot);
+  dfree(is.cmean); dfree(is.cw);
+  if (is.parts) (void)hipFree(is.parts);
   DeviceBatch& d = e->dstage;
   dfree(d.c_slot); dfree(d.c_val); dfree(d.c_rate); dfree(d.g_slot); dfree(d.g_val);
   dfree(d.h_slot); dfree(d.h_val); dfree(d.h_rate); dfree(d.s_slot); dfree(d.s_off); dfree(d.s_bytes);
@@ -306,10 +359,6 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
   e->processed += b->n_counter + b->n_gauge + b->n_histo + b->n_set;
 }
 
-template <class T>
-void h2d(T* dst, const T* src, uint64_t n, hipStream_t st) {
-  if (n) VN_HIP_CHECK(hipMemcpyAsync(dst, src, n * sizeof(T), hipMemcpyHostToDevice, st));
-}
 
 void ingest_host(vn_engine* e, const vn_batch* b) {
   if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
@@ -372,6 +421,15 @@ void ingest_host(vn_engine* e, const vn_batch* b) {
 }  // namespace
 
 namespace vn {
+void take_decode_error(vn_engine* e) {
+  uint32_t flags = 0;
+  VN_HIP_CHECK(hipMemcpy(&flags, e->h_err, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (flags & kErrDecode) {
+    flags &= ~kErrDecode;
+    VN_HIP_CHECK(hipMemcpy(e->h_err, &flags, sizeof(uint32_t), hipMemcpyHostToDevice));
+    throw DecodeError("malformed import payload");
+  }
+}
 void side_begin(vn_engine* e) {
   if (e->timing) {  // measured kernels run alone
     e->side = e->st;
@@ -423,6 +481,10 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
   e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 32768u;
   e->temp_cap = temp_buffer_cap(e->cfg.compression);
   e->max_records = cfg->max_batch_records ? cfg->max_batch_records : (1u << 20);
+  if (e->max_records > kTagIndex) {  // record indices ride in 30-bit tags
+    delete e;
+    return VN_EINVAL;
+  }
   e->max_member_bytes = cfg->max_batch_member_bytes ? cfg->max_batch_member_bytes : e->max_records * 16;
   if (e->max_member_bytes < e->max_records * 8) e->max_member_bytes = e->max_records * 8;
   int rc = guarded(e, [&] { create_impl(e); });
@@ -500,6 +562,17 @@ int vn_import_gauges(vn_engine* e, const uint32_t* slot, const double* value, ui
     side_begin(e);
     ingest_gauges(e, n, e->dstage.g_slot, e->dstage.g_val);
     side_join(e);
+    e->imported += n;
+  });
+}
+
+int vn_import_histos(vn_engine* e, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n) {
+  if (!e || (n && (!slot || !off || !bytes))) return VN_EINVAL;
+  return guarded(e, [&] {
+    if (!n) return;
+    stage_import(e, slot, off, bytes, n, e->cap[VN_HISTO]);
+    import_histos(e, n, e->imp.in_slot, e->imp.in_off, e->imp.in_bytes);
+    VN_HIP_CHECK(hipGetLastError());
     e->imported += n;
   });
 }

@@ -20,6 +20,21 @@ namespace vn {
 constexpr uint32_t kArenaWords = 16640;  // == kHllListCap
 constexpr uint32_t kTmpCap = 164;
 
+// Import staging (vn_import_histos / vn_import_sets): payloads as received, per-payload
+// parse results, and the decoded centroids.  Grown on demand.
+struct ImportScratch {
+  uint64_t cap_n = 0, cap_bytes = 0, cap_cent = 0;
+  uint32_t* in_slot = nullptr;    // [cap_n]
+  uint64_t* in_off = nullptr;     // [cap_n + 1]
+  uint8_t* in_bytes = nullptr;    // [cap_bytes]
+  uint32_t* cnt = nullptr;        // [cap_n + 1] per payload: centroids
+  uint32_t* coff = nullptr;       // [cap_n + 1] scan of cnt
+  void* parts = nullptr;          // [cap_n] parsed HLL payload headers (import_set.hip)
+  uint32_t* cslot = nullptr;      // [cap_cent] decoded centroids: slot, mean, weight
+  double* cmean = nullptr;
+  double* cw = nullptr;
+};
+
 struct DeviceBatch {  // device-resident staging for one ingest call
   uint32_t *c_slot, *g_slot, *h_slot, *s_slot, *s_off;
   double *c_val, *g_val, *h_val;
@@ -134,6 +149,7 @@ struct vn_engine {
 
   // ---- staging
   vn::DeviceBatch dstage{};
+  vn::ImportScratch imp;
   vn_stage pstage{};             // pinned host views
   // ---- flush outputs
   uint32_t* f_pos = nullptr;     // scan scratch (max cap + 1)

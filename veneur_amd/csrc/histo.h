@@ -10,6 +10,22 @@ namespace vn {
 // hot key's segment over many workgroups, since only a few hundred keys take that path
 constexpr uint32_t kHItems = 4;
 constexpr uint32_t kHTile = kBlock * kHItems;  // 1024 elements per chunk
+constexpr uint32_t kChunkStats = 7;  // per chunk: Local weight/min/max/sum/rsum, digest min/max
+
+// Tags in the low 32 bits of a histo element (B word):
+//   sample            float32 bits of its sample rate: weight float64(float32(1) / rate)
+//                     (samplers.go:347); Histo's Local* statistics count it
+//   kTagImport | i    a centroid of an imported digest (Histo.Combine): weight impw[i]; it
+//                     counts for the digest (Add updates min/max) but not for Local*
+//   kTagCentroid | i  an existing centroid of the key (hot-key batch merge), weight from the
+//                     centroid tile
+constexpr uint32_t kTagCentroid = 0x80000000u;
+constexpr uint32_t kTagImport = 0x40000000u;
+constexpr uint32_t kTagIndex = 0x3fffffffu;
+__device__ __forceinline__ bool tag_is_sample(uint32_t tag) { return (tag & (kTagCentroid | kTagImport)) == 0; }
+__device__ __forceinline__ double tag_weight(uint32_t tag, const double* impw) {
+  return (tag & kTagImport) ? impw[tag & kTagIndex] : (double)(1.0f / __uint_as_float(tag));
+}
 
 struct ExactCtx {
   uint32_t nkeys;
@@ -18,7 +34,8 @@ struct ExactCtx {
   const uint32_t* nex;       // per processed key: records to replay exactly (nullptr: none)
   const uint32_t* hot;       // per processed key: 1 -> merge pending temps after the exact part
   const uint64_t* A;         // raw float64 bits of the value
-  const uint64_t* B;         // slot<<32 | float32 bits of the sample rate
+  const uint64_t* B;         // slot<<32 | tag (see above)
+  const double* impw;        // weights of imported centroids (kTagImport)
   double delta;
   uint32_t capc, tcap;
   double* hst;

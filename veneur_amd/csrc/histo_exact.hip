@@ -212,7 +212,7 @@ __device__ double temp_weight(const double* tw, uint32_t np) {
   bool tint = true;
   double part = 0.0;
   for (uint32_t t = lane; t < np; t += 64) {
-    double w = tw[t];
+    double w = __builtin_fabs(tw[t]);  // the chunk sorter marks imported centroids by a negative weight
     tint &= is_int_weight(w);
     part = dadd(part, w);
   }
@@ -224,6 +224,7 @@ __device__ double temp_weight(const double* tw, uint32_t np) {
     for (uint32_t b = 0; b < np; b += 64) {
       double w = (b + lane < np) ? tw[b + lane] : 0.0;
       const uint32_t c = min(64u, np - b);
+      w = __builtin_fabs(w);
       for (uint32_t i = 0; i < c; i++) tempW = dadd(tempW, rl_d(w, (int)i));
     }
   }
@@ -774,8 +775,10 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
   const ExactSplit sp = exact_split(x.hpend[s], x.nex[k], tcap);
   const uint64_t base = (uint64_t)x.start[s] + sp.off0 + (uint64_t)(g - x.coff[k]) * tcap;
   for (uint32_t t = lane; t < tcap; t += 64) {
+    const uint32_t tag = (uint32_t)x.B[base + t];
+    const double wt = tag_weight(tag, x.impw);
     tv[t] = bitsd(x.A[base + t]);
-    tw[t] = (double)(1.0f / __uint_as_float((uint32_t)x.B[base + t]));  // float64(1/rate) in float32
+    tw[t] = tag_is_sample(tag) ? wt : -wt;  // sign: an imported centroid (no Local* statistics)
   }
   wave_lds_sync();
   const double tempW = temp_weight(tw, tcap);
@@ -821,6 +824,7 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   const double* const xcsv = x.csv;
   const double* const xcsw = x.csw;
   const double* const xctw = x.ctw;
+  const double* const ximpw = x.impw;
   const uint32_t s = x.keys[k];
   const uint32_t nex = x.nex ? x.nex[k] : 0u;
   const bool final_merge = x.flush_mode || (x.hot && x.hot[k]);
@@ -848,9 +852,13 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   }
   wave_lds_sync();
 
-  // Histo.Sample local statistics of the replayed samples (samplers.go:346-356)
-  double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
-  auto stat = [&](double v, double wt) {
+  // Histo.Sample local statistics of the replayed samples (samplers.go:346-356); the digest's
+  // min/max (Add, merging_digest.go:106-107) also take imported centroids
+  double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf, dmn = kInf, dmx = -kInf;
+  auto stat = [&](double v, double wt, bool sample) {
+    dmn = min_go(dmn, v);
+    dmx = max_go(dmx, v);
+    if (!sample) return;
     sw = dadd(sw, wt);
     mn = min_go(mn, v);
     mx = max_go(mx, v);
@@ -861,10 +869,11 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   auto append = [&](uint32_t a, uint32_t b) {
     for (uint32_t i = a + lane; i < b; i += 64) {
       const double v = bitsd(xA[lo + i]);
-      const double wt = (double)(1.0f / __uint_as_float((uint32_t)xB[lo + i]));
+      const uint32_t tag = (uint32_t)xB[lo + i];
+      const double wt = tag_weight(tag, ximpw);
       L.tv[np + (i - a)] = v;
       L.tw[np + (i - a)] = wt;
-      stat(v, wt);
+      stat(v, wt, tag_is_sample(tag));
     }
     np += b - a;
     wave_lds_sync();
@@ -904,8 +913,8 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
         const uint32_t t = q * 64 + lane;
         if (t < tcap) {
           L.sv[t] = cv[q];
-          L.sw[t] = cw[q];
-          stat(cv[q], cw[q]);
+          L.sw[t] = __builtin_fabs(cw[q]);
+          stat(cv[q], __builtin_fabs(cw[q]), cw[q] > 0.0);
         }
       }
       const double tempW = ctw;
@@ -939,6 +948,8 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
     srw = dadd(srw, __shfl_xor(srw, d, 64));
     mn = min_go(mn, __shfl_xor(mn, d, 64));
     mx = max_go(mx, __shfl_xor(mx, d, 64));
+    dmn = min_go(dmn, __shfl_xor(dmn, d, 64));
+    dmx = max_go(dmx, __shfl_xor(dmx, d, 64));
   }
   PROF_T(k1);
   PROF_ADD(8, k0, k1);
@@ -952,8 +963,8 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
       h[2] = max_go(h[2], mx);
       h[3] = dadd(h[3], sxw);
       h[4] = dadd(h[4], srw);
-      h[5] = min_go(h[5], mn);
-      h[6] = max_go(h[6], mx);
+      h[5] = min_go(h[5], dmn);
+      h[6] = max_go(h[6], dmx);
     }
   }
 }

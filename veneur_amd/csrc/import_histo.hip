@@ -1,0 +1,308 @@
+// import_histo.hip -- Worker.ImportMetric for histograms and timers (worker.go:230-268).
+//
+// Histo.Combine (samplers/samplers.go:519-526) decodes the forwarded digest --
+// tdigest.NewMerging(100) + GobDecode (tdigest/merging_digest.go:382-412) -- and calls
+// MergingDigest.Merge (344-356), which Add()s every centroid of the other digest.  Local*
+// statistics are not touched.  Merge visits the centroids in rand.Perm order, seeded from the
+// clock (trace/trace.go:30-32), so not even the reference reproduces itself; the engine Adds
+// them in their stored order (ascending mean), which the parity tests hand the oracle as the
+// permutation.
+//
+// The payloads are the JSONMetric.Value bytes a global veneur receives (after the JSON,
+// base64 and zlib decode of handlers_global.go:110-188).  One lane per payload parses the gob
+// stream (count pass, scan, emit pass); the centroids then join the ordinary histo ingest as
+// records tagged kTagImport, so the exact replay / hot-key batch merge applies them in Add
+// order, and they count for the digest (min/max, weight) but not for Local*.
+#include "histo.h"
+
+namespace vn {
+
+namespace {
+
+// encoding/gob reader over one payload (the subset MergingDigest.GobEncode writes)
+struct GobIn {
+  const uint8_t* d;
+  uint32_t n, i;
+  bool err;
+  __device__ uint64_t u() {  // gob unsigned integer
+    if (i >= n) {
+      err = true;
+      return 0;
+    }
+    const uint32_t b = d[i++];
+    if (b < 0x80u) return b;
+    const uint32_t cnt = 256u - b;  // byte count, sent negated
+    if (cnt > 8u || cnt > n - i) {
+      err = true;
+      return 0;
+    }
+    uint64_t v = 0;
+    for (uint32_t k = 0; k < cnt; k++) v = (v << 8) | d[i++];
+    return v;
+  }
+  __device__ int64_t s() {  // gob signed integer: sign in bit 0
+    const uint64_t x = u();
+    return (x & 1) ? ~(int64_t)(x >> 1) : (int64_t)(x >> 1);
+  }
+  __device__ double f() {  // gob float64: IEEE bits byte-reversed, sent as an unsigned integer
+    uint64_t x = u(), v = 0;
+    for (int k = 0; k < 8; k++) {
+      v = (v << 8) | (x & 0xffu);
+      x >>= 8;
+    }
+    return bitsd(v);
+  }
+  __device__ void skip_string() {
+    const uint64_t l = u();
+    if (l > n - i) {
+      err = true;
+      return;
+    }
+    i += (uint32_t)l;
+  }
+  __device__ int field_name() {  // 1 = "Mean", 2 = "Weight", 0 = any other name
+    const uint64_t l = u();
+    if (l > n - i) {
+      err = true;
+      return 0;
+    }
+    const uint8_t* p = d + i;
+    int r = 0;
+    if (l == 4 && p[0] == 'M' && p[1] == 'e' && p[2] == 'a' && p[3] == 'n') r = 1;
+    if (l == 6 && p[0] == 'W' && p[1] == 'e' && p[2] == 'i' && p[3] == 'g' && p[4] == 'h' && p[5] == 't') r = 2;
+    i += (uint32_t)l;
+    return r;
+  }
+  __device__ int64_t common_type() {  // CommonType {Name string; Id typeId} -> Id
+    int64_t id = 0, f = -1;
+    for (;;) {
+      const uint64_t dl = u();
+      if (err || dl == 0) break;
+      f += (int64_t)dl;
+      if (f == 0) skip_string();
+      else if (f == 1) id = s();
+      else {
+        err = true;
+        break;
+      }
+    }
+    return id;
+  }
+};
+
+constexpr int kGobSlices = 4, kGobFields = 6;
+// the type definitions of a digest stream: slice types (id -> elem) and one struct type
+struct GobTypes {
+  int ns = 0;
+  int64_t sid[kGobSlices], selem[kGobSlices];
+  int64_t st = -1;
+  int nf = 0;
+  int fname[kGobFields];
+  int64_t fid[kGobFields];
+};
+
+// one wireType message (encoding/gob type.go: ArrayT 0, SliceT 1, StructT 2)
+__device__ void gob_wiretype(GobIn& r, GobTypes& T) {
+  int64_t f = -1;
+  for (;;) {
+    const uint64_t dl = r.u();
+    if (r.err || dl == 0) return;
+    f += (int64_t)dl;
+    if (f == 0 || f == 1) {  // {CommonType; Elem; [Len]}
+      int64_t sf = -1, id = 0, elem = 0;
+      for (;;) {
+        const uint64_t d2 = r.u();
+        if (r.err || d2 == 0) break;
+        sf += (int64_t)d2;
+        if (sf == 0) id = r.common_type();
+        else if (sf == 1) elem = r.s();
+        else if (sf == 2) (void)r.s();
+        else {
+          r.err = true;
+          return;
+        }
+      }
+      if (T.ns >= kGobSlices) {
+        r.err = true;
+        return;
+      }
+      T.sid[T.ns] = id;
+      T.selem[T.ns] = elem;
+      T.ns++;
+    } else if (f == 2) {  // {CommonType; Field []*fieldType{Name; Id}}
+      int64_t sf = -1;
+      for (;;) {
+        const uint64_t d2 = r.u();
+        if (r.err || d2 == 0) break;
+        sf += (int64_t)d2;
+        if (sf == 0) {
+          T.st = r.common_type();
+        } else if (sf == 1) {
+          const uint64_t nf = r.u();
+          if (nf > (uint64_t)kGobFields) {
+            r.err = true;
+            return;
+          }
+          T.nf = (int)nf;
+          for (int k = 0; k < (int)nf; k++) {
+            T.fname[k] = 0;
+            T.fid[k] = 0;
+            int64_t ff = -1;
+            for (;;) {
+              const uint64_t d3 = r.u();
+              if (r.err || d3 == 0) break;
+              ff += (int64_t)d3;
+              if (ff == 0) T.fname[k] = r.field_name();
+              else if (ff == 1) T.fid[k] = r.s();
+              else {
+                r.err = true;
+                return;
+              }
+            }
+          }
+        } else {
+          r.err = true;
+          return;
+        }
+      }
+    } else {
+      r.err = true;
+      return;
+    }
+  }
+}
+
+// skip one field value of type id tid: builtin scalars, strings, or a slice of scalars
+// (Centroid.Samples []float64, only sent by debug digests)
+__device__ void gob_skip(GobIn& r, const GobTypes& T, int64_t tid) {
+  if (tid >= 1 && tid <= 4) {  // bool, int, uint, float
+    (void)r.u();
+    return;
+  }
+  if (tid == 5 || tid == 6) {  // []byte, string
+    r.skip_string();
+    return;
+  }
+  for (int k = 0; k < T.ns; k++)
+    if (T.sid[k] == tid && T.selem[k] >= 1 && T.selem[k] <= 4) {
+      const uint64_t c = r.u();
+      for (uint64_t j = 0; j < c && !r.err; j++) (void)r.u();
+      return;
+    }
+  r.err = true;
+}
+
+// One GobEncode()d MergingDigest ([]Centroid, then compression, min, max as float64):
+// the number of centroids, written to mean/w when EMIT; -1 if the stream is malformed.
+template <bool EMIT>
+__device__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double* w) {
+  GobIn r{d, n, 0, false};
+  GobTypes T;
+  bool have = false;
+  int floats = 0;
+  int64_t cnt = 0;
+  while (r.i < r.n && floats < 3) {
+    const uint64_t mlen = r.u();
+    if (r.err || mlen > r.n - r.i) return -1;
+    const uint32_t end = r.i + (uint32_t)mlen;
+    const int64_t id = r.s();
+    if (id < 0) {
+      gob_wiretype(r, T);
+    } else {
+      if (r.u() != 0) return -1;  // a non-struct value starts with a zero delta
+      if (!have) {
+        int si = -1;
+        for (int k = 0; k < T.ns; k++)
+          if (T.sid[k] == id) si = k;
+        if (si < 0 || T.selem[si] != T.st) return -1;
+        const uint64_t c = r.u();
+        for (uint64_t j = 0; j < c && !r.err; j++) {
+          double m = 0.0, wt = 0.0;  // gob omits zero fields
+          int64_t f = -1;
+          for (;;) {
+            const uint64_t dl = r.u();
+            if (r.err || dl == 0) break;
+            f += (int64_t)dl;
+            if (f >= T.nf) {
+              r.err = true;
+              break;
+            }
+            if (T.fname[f] == 1 && T.fid[f] == 4) m = r.f();
+            else if (T.fname[f] == 2 && T.fid[f] == 4) wt = r.f();
+            else gob_skip(r, T, T.fid[f]);
+          }
+          if (EMIT) {
+            mean[cnt] = m;
+            w[cnt] = wt;
+          }
+          cnt++;
+        }
+        have = true;
+      } else {
+        if (id != 4) return -1;  // compression, min, max: float64
+        (void)r.f();
+        floats++;
+      }
+    }
+    if (r.err || r.i != end) return -1;
+  }
+  return (have && floats == 3) ? cnt : -1;
+}
+
+__global__ void k_gob_count(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+                            uint32_t* __restrict__ cnt, uint32_t* __restrict__ err) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t len = off[i + 1] - off[i];
+  const int64_t c = len <= 0xffffffffull ? gob_digest<false>(bytes + off[i], (uint32_t)len, nullptr, nullptr) : -1;
+  if (c < 0 || c > (int64_t)kTagIndex) {
+    atomicOr(err, kErrDecode);
+    cnt[i] = 0;
+  } else {
+    cnt[i] = (uint32_t)c;
+  }
+}
+
+__global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+                           const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff,
+                           uint32_t* __restrict__ oslot, double* __restrict__ omean, double* __restrict__ ow,
+                           uint32_t* __restrict__ err) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t o = coff[i];
+  const int64_t c = gob_digest<true>(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), omean + o, ow + o);
+  if (c < 0) {
+    atomicOr(err, kErrDecode);
+    return;
+  }
+  const uint32_t s = slot[i];
+  for (int64_t j = 0; j < c; j++) {
+    oslot[o + j] = s;
+    const double m = omean[o + j], wt = ow[o + j];
+    if (d_isnan(m) || d_isinf(m) || wt <= 0.0) atomicOr(err, kErrDecode);  // Add panics (merging_digest.go:98-100)
+  }
+}
+
+}  // namespace
+
+void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes) {
+  if (!n) return;
+  hipStream_t st = e->st;
+  ImportScratch& s = e->imp;
+  hipLaunchKernelGGL(k_gob_count, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, s.cnt, e->h_err);
+  scan_exclusive_u32(s.cnt, s.coff, n, e->ss, st);
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 9, s.coff + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  take_decode_error(e);
+  const uint64_t nc = e->hf_cnt[9];
+  if (nc > e->max_records)
+    throw std::invalid_argument("imported digests hold more centroids than max_batch_records: split the import");
+  if (!nc) return;
+  hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.cslot,
+                     s.cmean, s.cw, e->h_err);
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  take_decode_error(e);
+  ingest_histos(e, nc, s.cslot, s.cmean, nullptr, s.cw);
+}
+
+}  // namespace vn

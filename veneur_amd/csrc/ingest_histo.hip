@@ -38,6 +38,7 @@ struct HistoCtx {
   const uint32_t* chb;
   const uint64_t* A;
   const uint64_t* B;
+  const double* impw;        // weights of imported centroids (kTagImport)
   double* w;
   double* wk;
   double* ch_sum;
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(kBlock) void k_chunk_prep(HistoCtx x) {
   const uint32_t c = blockIdx.x, t = threadIdx.x;
   const double* cwo = x.hcur[r.s] ? x.cw1 : x.cw0;
   double wv[kHItems];
-  double run = 0.0, sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
+  double run = 0.0, sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf, dmn = kInf, dmx = -kInf;
   const uint32_t base = r.lo + t * kHItems;
 #pragma unroll
   for (int j = 0; j < (int)kHItems; j++) {
@@ -116,15 +117,19 @@ __global__ __launch_bounds__(kBlock) void k_chunk_prep(HistoCtx x) {
       uint32_t tag = (uint32_t)b;
       double xv = from_ordered_bits(x.A[i]);
       double wt;
-      if (tag & 0x80000000u) {
+      if (tag & kTagCentroid) {
         wt = cwo[tag & 0x7fffffffu];
       } else {
-        wt = (double)(1.0f / __uint_as_float(tag));  // float64(1/sampleRate) in float32
-        sw = dadd(sw, wt);
-        mn = min_go(mn, xv);
-        mx = max_go(mx, xv);
-        sxw = dadd(sxw, dmul(xv, wt));
-        srw = dadd(srw, dmul(ddiv(1.0, xv), wt));
+        wt = tag_weight(tag, x.impw);
+        dmn = min_go(dmn, xv);
+        dmx = max_go(dmx, xv);
+        if (tag_is_sample(tag)) {
+          sw = dadd(sw, wt);
+          mn = min_go(mn, xv);
+          mx = max_go(mx, xv);
+          sxw = dadd(sxw, dmul(xv, wt));
+          srw = dadd(srw, dmul(ddiv(1.0, xv), wt));
+        }
       }
       wv[j] = wt;
       run = dadd(run, wt);
@@ -146,10 +151,12 @@ __global__ __launch_bounds__(kBlock) void k_chunk_prep(HistoCtx x) {
   srw = block_allreduce(srw, s_tmp, SumOp());
   mn = block_allreduce(mn, s_tmp, MinGoOp());
   mx = block_allreduce(mx, s_tmp, MaxGoOp());
+  dmn = block_allreduce(dmn, s_tmp, MinGoOp());
+  dmx = block_allreduce(dmx, s_tmp, MaxGoOp());
   if (t == 0) {
     x.ch_sum[c] = tot;
-    double* st = x.ch_stats + (uint64_t)c * 5;
-    st[0] = sw; st[1] = mn; st[2] = mx; st[3] = sxw; st[4] = srw;
+    double* st = x.ch_stats + (uint64_t)c * kChunkStats;
+    st[0] = sw; st[1] = mn; st[2] = mx; st[3] = sxw; st[4] = srw; st[5] = dmn; st[6] = dmx;
   }
 }
 
@@ -160,7 +167,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(HistoCtx x) {
   if (x.count && k >= *x.count) return;
   const uint32_t s = x.tl[k];
   const uint32_t cb = x.chb[k], ce = x.chb[k + 1];
-  double carry = 0.0, sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
+  double carry = 0.0, sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf, dmn = kInf, dmx = -kInf;
   for (uint32_t base = cb; base < ce; base += kBlock) {
     uint32_t c = base + t;
     double v = c < ce ? x.ch_sum[c] : 0.0;
@@ -168,12 +175,14 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(HistoCtx x) {
     double ex = block_excl_scan_d(v, s_tmp, tot);
     if (c < ce) {
       x.ch_pre[c] = dadd(carry, ex);
-      const double* st = x.ch_stats + (uint64_t)c * 5;
+      const double* st = x.ch_stats + (uint64_t)c * kChunkStats;
       sw = dadd(sw, st[0]);
       mn = min_go(mn, st[1]);
       mx = max_go(mx, st[2]);
       sxw = dadd(sxw, st[3]);
       srw = dadd(srw, st[4]);
+      dmn = min_go(dmn, st[5]);
+      dmx = max_go(dmx, st[6]);
     }
     carry = dadd(carry, tot);
   }
@@ -182,6 +191,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(HistoCtx x) {
   srw = block_allreduce(srw, s_tmp, SumOp());
   mn = block_allreduce(mn, s_tmp, MinGoOp());
   mx = block_allreduce(mx, s_tmp, MaxGoOp());
+  dmn = block_allreduce(dmn, s_tmp, MinGoOp());
+  dmx = block_allreduce(dmx, s_tmp, MaxGoOp());
   if (t == 0) {
     double* h = x.hst + (uint64_t)s * VN_HISTO_STATS;
     h[0] = dadd(h[0], sw);
@@ -189,8 +200,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(HistoCtx x) {
     h[2] = max_go(h[2], mx);
     h[3] = dadd(h[3], sxw);
     h[4] = dadd(h[4], srw);
-    h[5] = min_go(h[5], mn);
-    h[6] = max_go(h[6], mx);
+    h[5] = min_go(h[5], dmn);
+    h[6] = max_go(h[6], dmx);
     h[7] = carry;
     x.seg_T[k] = carry;
   }
@@ -473,6 +484,7 @@ __global__ void k_clear_flags(uint32_t n, const uint32_t* __restrict__ list, uin
 }
 
 // raw (arrival-order) keys: A = float64 bits, B = slot<<32 | float32 rate bits
+// (rate == nullptr: imported centroids, weights in impw, tagged kTagImport | i)
 __global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, const double* __restrict__ val,
                                  const float* __restrict__ rate, uint64_t* __restrict__ A, uint64_t* __restrict__ B,
                                  uint32_t* __restrict__ bt, uint32_t* __restrict__ htouch) {
@@ -480,7 +492,8 @@ __global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, 
   if (i >= n) return;
   uint32_t s = slot[i];
   A[i] = dbits(val[i]);
-  B[i] = ((uint64_t)s << 32) | (uint64_t)__float_as_uint(rate[i]);
+  const uint32_t tag = rate ? __float_as_uint(rate[i]) : (kTagImport | (uint32_t)i);
+  B[i] = ((uint64_t)s << 32) | (uint64_t)tag;
   bt[s] = 1;
   htouch[s] = 1;
 }
@@ -709,7 +722,8 @@ __global__ __launch_bounds__(kBlock) void k_round_merge(uint32_t capc, const uin
     }
   }
 }
-void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate) {
+void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate,
+                   const double* impw) {
   if (!n) return;
   hipStream_t st = e->st;
   const uint32_t caph = e->cap[VN_HISTO];
@@ -742,6 +756,7 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   xc.hot = e->h_hotflag;
   xc.A = As;
   xc.B = Bs;
+  xc.impw = impw;
   xc.delta = e->cfg.compression;
   xc.capc = e->cap_cent;
   xc.tcap = e->temp_cap;
@@ -816,6 +831,7 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   x.chb = e->h_chb;
   x.A = MA;
   x.B = MB;
+  x.impw = impw;
   x.w = e->h_w;
   x.wk = e->h_wk;
   x.ch_sum = e->ch_sum;

@@ -1,10 +1,25 @@
 // kernels.h -- host launchers of the engine's HIP kernels (one stream per engine).
 #pragma once
+#include <stdexcept>
 #include "engine.h"
 #include "gomath.h"
 #include "sketch.h"
 
 namespace vn {
+
+constexpr uint32_t kErrDecode = 8u;  // device error flag: malformed import payload
+
+// A malformed import payload (where the reference's decoder errors or panics): VN_EDECODE.
+struct DecodeError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+// after a stream sync: throws DecodeError (and clears the flag) if a decode kernel raised it
+void take_decode_error(vn_engine* e);
+// Worker.ImportMetric for histograms / timers: Histo.Combine of GobEncode()d digests
+// (payload i = bytes[off[i], off[i+1]), device pointers)
+void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes);
+// Worker.ImportMetric for sets: Set.Combine of MarshalBinary()d sketches
+void import_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes);
 
 // The side stream: work issued between side_begin and side_join runs on e->side, after
 // everything already issued on the main stream; the main stream waits for it at the join.
@@ -16,7 +31,9 @@ void import_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const int64
 // Gauge.Sample (198-200) / Gauge.Combine (237-249): last write in arrival order wins
 void ingest_gauges(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val);
 // Histo.Sample (346-356) + MergingDigest.Add/mergeAllTemps (merging_digest.go:97-236)
-void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate);
+// rate == nullptr: the records are imported centroids (Histo.Combine) with weights impw
+void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate,
+                   const double* impw = nullptr);
 // Set.Sample (265-267) -> Sketch.Insert (hyperloglog.go:186-200)
 void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t* off, const uint8_t* bytes,
                  const uint64_t* hashes);

@@ -136,6 +136,23 @@ class Engine:
         s, v = _c(slot, np.uint32), _c(values, np.float64)
         self._check(A.lib.vn_import_gauges(self.h, s.ctypes.data_as(A.u32p), v.ctypes.data_as(A.f64p), len(s)))
 
+    @staticmethod
+    def _payloads(slot, payloads):
+        s = _c(slot, np.uint32)
+        if len(s) != len(payloads):
+            raise ValueError("one slot per payload")
+        off = np.zeros(len(payloads) + 1, np.uint64)
+        off[1:] = np.cumsum([len(p) for p in payloads])
+        blob = np.frombuffer(b"".join(payloads) or b"\0", np.uint8).copy()
+        return s, off, blob
+
+    def import_histos(self, slot, payloads):
+        """ImportMetric of histograms/timers: Histo.Combine of each GobEncode()d digest
+        (samplers.go:519-526) into histo slot[i], in order."""
+        s, off, blob = self._payloads(slot, payloads)
+        self._check(A.lib.vn_import_histos(self.h, s.ctypes.data_as(A.u32p), off.ctypes.data_as(A.u64p),
+                                           blob.ctypes.data_as(A.u8p), len(s)))
+
     def sync(self):
         self._check(A.lib.vn_sync(self.h))
 
