@@ -173,6 +173,14 @@ int vn_import_gauges(vn_engine* eng, const uint32_t* slot, const double* value, 
  * a centroid Add() would panic on, fails the whole call with VN_EDECODE and applies nothing. */
 int vn_import_histos(vn_engine* eng, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n);
 
+/* ImportMetric for sets (worker.go:248-252): Set.Combine (samplers.go:313-325) of each payload
+ * = the forwarded Sketch.MarshalBinary() bytes (hyperloglog.go:270-315), payload i =
+ * bytes[off[i], off[i+1]), into set slot[i], in order: UnmarshalBinary + Sketch.Merge
+ * (hyperloglog.go:92-149), bit-exact (a sparse payload's tmpSet is merged in ascending order
+ * where Go iterates a map).  A payload of another precision is skipped, as Merge's error is
+ * only logged; a truncated payload fails the whole call with VN_EDECODE and applies nothing. */
+int vn_import_sets(vn_engine* eng, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n);
+
 int vn_flush(vn_engine* eng, vn_flush_result* out);
 int vn_sync(vn_engine* eng);
 

@@ -133,3 +133,107 @@ def test_import_histos_malformed_fails_loudly():
         e.import_histos([2], [good])
         f = e.flush()
     assert f.histo_slot.tolist() == [2]
+
+
+# ------------------------------------------------------------------ sets
+def random_hashes(rng, n):
+    return rng.integers(0, 2**63, n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, n, dtype=np.uint64)
+
+
+def sketch_payload(rng, n, p=14):
+    """A local veneur's forwarded set: n random members inserted, then MarshalBinary."""
+    sk = oracle.Sketch(p)
+    for h in random_hashes(rng, n):
+        sk.insert_hash(int(h))
+    return sk.marshal()
+
+
+def _set_state_equal(e, w, slot):
+    st = e.read_set(slot)
+    sk = w.set_sketch(slot)
+    assert bool(st["sparse"]) == sk.sparse, slot
+    assert st["b"] == sk.b, slot
+    if sk.sparse:
+        assert np.array_equal(st["list"], sk.list_codes()), slot
+        assert np.array_equal(st["tmp"], sk.tmp_codes()), slot
+        assert st["list_bytes"] == sk.list_bytes(), slot
+    else:
+        assert np.array_equal(st["registers"], sk.registers()), slot
+        assert st["nz"] == sk.nz, slot
+
+
+def test_import_sets_every_merge_path_bit_exact():
+    """sparse<-sparse (with and without the mergeSparse trigger and the toNormal switch),
+    sparse<-dense, dense<-sparse, dense<-dense with either base higher, a precision-16 payload
+    (skipped, key still Upserted), keys that already hold local samples; state and Estimate
+    bit-exact against the restated axiomhq Merge."""
+    rng = np.random.default_rng(21)
+    nk = 12
+    small = [sketch_payload(rng, k) for k in (1, 30, 150)]
+    mid = [sketch_payload(rng, k) for k in (400, 3000)]
+    big = [sketch_payload(rng, k) for k in (9000, 40000)]
+    reb = sketch_payload(rng, 400_000)
+    p16 = sketch_payload(rng, 100, p=16)
+    tmp = oracle.Sketch()
+    tmp.unmarshal(reb)
+    assert not tmp.sparse and tmp.b > 0  # a based (rebased) dense payload
+    w = oracle.Worker(1, 1, 1, nk)
+    # local samples first: keys 4,5 sparse, 6,7 dense, 8 dense with b > 0
+    loc_slots, loc_h = [], []
+    for s, n in ((4, 200), (5, 200), (6, 20000), (7, 20000), (8, 400_000)):
+        loc_slots.append(np.full(n, s, np.uint32))
+        loc_h.append(random_hashes(rng, n))
+    ls, lh = np.concatenate(loc_slots), np.concatenate(loc_h)
+    w.set_hashed(ls, lh)
+    calls = [
+        ([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11],
+         [small[0], small[1], mid[0], big[0], small[2], mid[1], small[1], big[1], reb, p16, reb, mid[1]]),
+        ([0, 0, 1, 2, 3, 9, 10, 11, 11, 8, 6], [small[1], mid[1], big[0], reb, small[0], small[2], big[1], small[0],
+                                                 big[0], big[1], mid[0]]),
+        ([0, 0, 0, 0, 0, 2, 5], [mid[0], mid[1], small[2], small[1], small[0], mid[0], reb]),
+    ]
+    with make_engine((1, 1, 1, nk), max_records=1 << 19) as e:
+        e.ingest(set_hashes=(ls, lh))
+        for slots, pays in calls:
+            e.import_sets(np.array(slots, np.uint32), pays)
+            for s, p in zip(slots, pays):
+                w.import_set(s, p)
+        for s in range(nk):
+            _set_state_equal(e, w, s)
+        f = e.flush()
+    assert f.set_slot.tolist() == list(range(nk))
+    assert f.samples_imported == sum(len(c[0]) for c in calls)
+    exp = [w.set_estimate(s) for s in range(nk)]
+    assert f.set_estimate.tolist() == exp
+
+
+def test_import_sets_many_hosts_sparse_trigger_path():
+    """200 keys x 30 hosts' small sparse sketches: the tmpSet/list union and the 164-code
+    trigger across many payloads per key."""
+    rng = np.random.default_rng(22)
+    nk, hosts = 200, 30
+    pays = [sketch_payload(rng, int(n)) for n in rng.integers(1, 120, 64)]
+    w = oracle.Worker(1, 1, 1, nk)
+    with make_engine((1, 1, 1, nk)) as e:
+        for h in range(hosts):
+            slots = rng.integers(0, nk, 150).astype(np.uint32)
+            pl = [pays[i] for i in rng.integers(0, len(pays), len(slots))]
+            e.import_sets(slots, pl)
+            for s, p in zip(slots, pl):
+                w.import_set(int(s), p)
+        touched = [s for s in range(nk) if w.touched(3, s)]
+        for s in touched:
+            _set_state_equal(e, w, s)
+        f = e.flush()
+    assert f.set_estimate.tolist() == [w.set_estimate(s) for s in touched]
+
+
+def test_import_sets_malformed_fails_loudly():
+    rng = np.random.default_rng(23)
+    good = sketch_payload(rng, 50)
+    with make_engine((1, 1, 1, 4)) as e:
+        with pytest.raises(V.EngineError, match="rc=-4"):
+            e.import_sets([0, 1], [good, good[:-2]])
+        e.import_sets([2], [good])
+        f = e.flush()
+    assert f.set_slot.tolist() == [2]

@@ -116,6 +116,7 @@ _sig("vn_ingest", C.c_int, vp, C.POINTER(Batch))
 _sig("vn_import_counters", C.c_int, vp, u32p, i64p, C.c_uint64)
 _sig("vn_import_gauges", C.c_int, vp, u32p, f64p, C.c_uint64)
 _sig("vn_import_histos", C.c_int, vp, u32p, u64p, u8p, C.c_uint64)
+_sig("vn_import_sets", C.c_int, vp, u32p, u64p, u8p, C.c_uint64)
 _sig("vn_flush", C.c_int, vp, C.POINTER(FlushResult))
 _sig("vn_sync", C.c_int, vp)
 _sig("vn_read_histo", C.c_int, vp, C.c_uint32, f64p, f64p, C.c_uint32, u32p, f64p)
@@ -134,7 +135,7 @@ _sig("vn_synth_free", None, C.POINTER(SynthOut))
 # every symbol include/*.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
     "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
-    "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_flush", "vn_sync",
+    "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_flush", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
 ]

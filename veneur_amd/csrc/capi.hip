@@ -577,6 +577,17 @@ int vn_import_histos(vn_engine* e, const uint32_t* slot, const uint64_t* off, co
   });
 }
 
+int vn_import_sets(vn_engine* e, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n) {
+  if (!e || (n && (!slot || !off || !bytes))) return VN_EINVAL;
+  return guarded(e, [&] {
+    if (!n) return;
+    stage_import(e, slot, off, bytes, n, e->cap[VN_SET]);
+    import_sets(e, n, e->imp.in_slot, e->imp.in_off, e->imp.in_bytes);
+    VN_HIP_CHECK(hipGetLastError());
+    e->imported += n;
+  });
+}
+
 int vn_flush(vn_engine* e, vn_flush_result* out) {
   if (!e || !out) return VN_EINVAL;
   return guarded(e, [&] {

@@ -1,0 +1,556 @@
+// import_set.hip -- Worker.ImportMetric for sets (worker.go:248-252), bit-exact.
+//
+// Set.Combine (samplers/samplers.go:313-325) = hyperloglog.New() + UnmarshalBinary
+// (vendor/github.com/axiomhq/hyperloglog/hyperloglog.go:318-376) + Sketch.Merge (92-149):
+//   sparse <- sparse   every tmpSet code and list code of the other joins the tmpSet, then
+//                      maybeToNormal (80-87): if len(tmpSet)*100 > m, mergeSparse (229-267)
+//                      and, if the list's byte length > m, toNormal (152-166)
+//   sparse <- dense    toNormal, then dense <- dense
+//   dense  <- sparse   insert(decodeHash(code)) for the other's tmpSet codes (map order in Go;
+//                      ascending here and in the oracle) and then its list, in order
+//   dense  <- dense    align the bases: the lower side is rebase()d by the difference
+//                      (registers.go:56-74: registers below it are left alone), then a
+//                      per-register max with registers.set's nz bookkeeping
+// A payload whose precision is not 14 makes Merge return "precisions must be equal"; the
+// worker logs it and moves on (worker.go:248-252) -- the key is still Upserted, nothing merges.
+// A payload UnmarshalBinary would panic on (truncated) fails the whole call (VN_EDECODE).
+//
+// MI355X formulation: one lane per payload parses and validates it (k_hll_parse); payloads
+// are grouped by key with a stable radix sort; one 256-thread workgroup per key then applies
+// its payloads in arrival order with the key's list or registers in LDS: varint lists decode
+// in parallel (scan of terminator bytes, then a scan of the deltas), unions are merge-path
+// merges staged in registers, registers are LDS atomic maxes, and inserts into a dense key
+// run the exact insert machinery of set_dense.h (rebase epochs included).
+#include "set_dense.h"
+
+namespace vn {
+
+namespace {
+
+struct HllPart {
+  uint32_t kind;      // 0 sparse, 1 dense, 2 skipped (precision != 14)
+  uint32_t b;
+  uint32_t ntmp;      // tmpSet codes (big-endian u32) at tmp_off
+  uint32_t list_len;  // varint list bytes at list_off
+  uint32_t regs_len;  // dense: tailcut bytes at regs_off (<= 8192; missing bytes are zero registers)
+  uint32_t pad;
+  uint64_t tmp_off, list_off, regs_off;
+};
+static_assert(sizeof(HllPart) <= 64, "ImportScratch.parts holds 64 bytes per payload");
+
+constexpr uint32_t kMaxImportTmp = 256;   // tmpSet codes per payload (Go keeps < 164)
+constexpr uint32_t kPer = (kArenaWords + kBlock - 1) / kBlock;  // 65 codes per thread
+constexpr uint32_t kCWords = kArenaWords + 512;                 // payload codes + the key's tmpSet
+constexpr uint32_t kCPer = (kCWords + kBlock - 1) / kBlock;     // 67
+
+__device__ __forceinline__ uint32_t be32(const uint8_t* d) {
+  return ((uint32_t)d[0] << 24) | ((uint32_t)d[1] << 16) | ((uint32_t)d[2] << 8) | d[3];
+}
+
+// parse + validate one MarshalBinary payload (hyperloglog.go:318-376, compressed.go:83-97)
+__global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+                            HllPart* __restrict__ parts, uint32_t* __restrict__ err) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t o = off[i], len = off[i + 1] - o;
+  const uint8_t* d = bytes + o;
+  HllPart p{};
+  p.kind = 2;
+  bool bad = len < 4;
+  if (!bad && d[1] == kHllP) {
+    p.b = d[2];
+    if (d[3] == 1) {  // sparse: tmpSet, then the compressed list (count, last, byte length, bytes)
+      bad = len < 8;
+      if (!bad) {
+        const uint64_t tssz = be32(d + 4), last = 8 + 4 * tssz;
+        bad = tssz > kMaxImportTmp || len < last + 12;
+        if (!bad) {
+          const uint64_t sz = be32(d + last + 8);
+          bad = sz > kHllM || len < last + 12 + sz;
+          if (!bad) {
+            // the list must decode completely into strictly increasing codes
+            const uint8_t* lb = d + last + 12;
+            uint32_t prev = 0, x = 0, sh = 0, k = 0;
+            for (uint64_t j = 0; j < sz && !bad; j++) {
+              const uint32_t b = lb[j];
+              if (sh < 32) x |= (b & 0x7fu) << sh;
+              sh += 7;
+              if (!(b & 0x80u)) {
+                const uint32_t c = prev + x;
+                if (k > 0 && c <= prev) bad = true;
+                prev = c;
+                k++;
+                x = 0;
+                sh = 0;
+              }
+            }
+            if (sz && (lb[sz - 1] & 0x80u)) bad = true;  // a code without its last byte
+            p.kind = 0;
+            p.ntmp = (uint32_t)tssz;
+            p.tmp_off = o + 8;
+            p.list_off = o + last + 12;
+            p.list_len = (uint32_t)sz;
+          }
+        }
+      }
+    } else {  // dense: m/2 tailcut bytes
+      bad = len < 8 || be32(d + 4) != kHllM / 2 || len - 8 > kHllM / 2;
+      if (!bad) {
+        p.kind = 1;
+        p.regs_off = o + 8;
+        p.regs_len = (uint32_t)(len - 8);
+      }
+    }
+  }
+  if (bad) atomicOr(err, kErrDecode);
+  parts[i] = p;
+}
+
+__global__ void k_hll_keys(uint64_t n, const uint32_t* __restrict__ slot, uint64_t* __restrict__ keys,
+                           uint32_t* __restrict__ bt, uint32_t* __restrict__ stouch) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = slot[i];
+  keys[i] = ((uint64_t)s << 32) | (uint64_t)i;
+  bt[s] = 1;
+  stouch[s] = 1;  // Upsert happens before Combine (worker.go:241), even if the merge fails
+}
+
+// ---- block-wide helpers (256 threads)
+__device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* a, uint32_t n, uint32_t v) {
+  uint32_t l = 0, h = n;
+  while (l < h) {
+    uint32_t m = (l + h) >> 1;
+    if (a[m] <= v) l = m + 1;
+    else h = m;
+  }
+  return l;
+}
+
+// exclusive scan (sum or max) of one u32 per thread; s_red holds 4 u32
+template <bool MAX>
+__device__ __forceinline__ uint32_t block_scan_u32(uint32_t v, uint32_t* s_red, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if ((int)lane >= d) inc = MAX ? max(inc, o) : inc + o;
+  }
+  if (lane == 63) s_red[w] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t i = 0; i < w; i++) base = MAX ? max(base, s_red[i]) : base + s_red[i];
+  total = 0;
+  for (uint32_t i = 0; i < 4; i++) total = MAX ? max(total, s_red[i]) : total + s_red[i];
+  __syncthreads();
+  uint32_t ex = __shfl_up(inc, 1, 64);
+  if (lane == 0) ex = 0;
+  return MAX ? max(base, ex) : base + ex;
+}
+
+// compressedList bytes (a validated payload) -> codes in out[], ascending; returns the count
+__device__ uint32_t decode_list(const uint8_t* g, uint32_t L, uint32_t* out, uint32_t* s_red) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (L + kBlock - 1) / kBlock, lo = min(L, t * per), hi = min(L, lo + per);
+  uint32_t ends = 0, last_end = 0;  // last_end: position + 1 of my last terminator (0: none)
+  for (uint32_t k = lo; k < hi; k++)
+    if (!(g[k] & 0x80u)) {
+      ends++;
+      last_end = k + 1;
+    }
+  uint32_t total, tmax;
+  const uint32_t ci0 = block_scan_u32<false>(ends, s_red, total);
+  const uint32_t prev_end = block_scan_u32<true>(last_end, s_red, tmax);
+  for (uint32_t k = t; k < total; k += kBlock) out[k] = 0;
+  __syncthreads();
+  uint32_t ci = ci0, start = prev_end;  // first byte of the code my first byte belongs to
+  for (uint32_t k = lo; k < hi; k++) {
+    const uint32_t b = g[k], j = k - start;
+    if (7 * j < 32) atomicOr(&out[ci], (b & 0x7fu) << (7 * j));
+    if (!(b & 0x80u)) {
+      ci++;
+      start = k + 1;
+    }
+  }
+  __syncthreads();
+  // deltas -> codes: prefix sum (uint32 arithmetic, as compressedList.decode)
+  const uint32_t per2 = (total + kBlock - 1) / kBlock, lo2 = min(total, t * per2), hi2 = min(total, lo2 + per2);
+  uint32_t sum = 0;
+  for (uint32_t k = lo2; k < hi2; k++) sum += out[k];
+  uint32_t tt;
+  uint32_t run = block_scan_u32<false>(sum, s_red, tt);
+  for (uint32_t k = lo2; k < hi2; k++) {
+    run += out[k];
+    out[k] = run;
+  }
+  __syncthreads();
+  return total;
+}
+
+// Remove repeats from sorted A[0..n) in place (register-staged); returns the new length.
+template <int K>
+__device__ uint32_t unique_sorted(uint32_t* A, uint32_t n, uint32_t* s_red) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t per = (n + kBlock - 1) / kBlock, lo = min(n, t * per), hi = min(n, lo + per);
+  uint32_t v[K];
+  bool keep[K];
+  uint32_t kept = 0;
+#pragma unroll
+  for (int q = 0; q < K; q++) {
+    const uint32_t k = lo + q;
+    keep[q] = false;
+    v[q] = 0;
+    if (k < hi) {
+      v[q] = A[k];
+      keep[q] = k == 0 || A[k - 1] != v[q];
+      kept += keep[q];
+    }
+  }
+  uint32_t total;
+  uint32_t pos = block_scan_u32<false>(kept, s_red, total);  // its barriers order the reads above
+#pragma unroll
+  for (int q = 0; q < K; q++)
+    if (keep[q]) A[pos++] = v[q];
+  __syncthreads();
+  return total;
+}
+
+// OUT = sorted A[0..na) U sorted B[0..nb), both free of repeats; OUT may alias A or B (every
+// input is staged in registers before anything is written).  An element's place is its index
+// plus the elements of the other list below it, minus the common elements below it (an
+// exclusive scan of the "also in the other list" flags).  Capacity: na <= 256*KA, nb <= 256*KB.
+template <int KA, int KB>
+__device__ uint32_t union_unique(const uint32_t* A, uint32_t na, const uint32_t* B, uint32_t nb, uint32_t* OUT,
+                                 uint32_t* s_red) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t pa = (na + kBlock - 1) / kBlock, loA = min(na, t * pa), hiA = min(na, loA + pa);
+  const uint32_t pb = (nb + kBlock - 1) / kBlock, loB = min(nb, t * pb), hiB = min(nb, loB + pb);
+  uint32_t av[KA], apos[KA], bv[KB], bpos[KB];
+  bool ain[KA], bin[KB];
+  uint32_t ca = 0, cb = 0;
+#pragma unroll
+  for (int q = 0; q < KA; q++) {
+    const uint32_t i = loA + q;
+    ain[q] = false;
+    av[q] = 0;
+    apos[q] = 0;
+    if (i < hiA) {
+      av[q] = A[i];
+      const uint32_t l = lower_bound_u32(B, nb, av[q]);
+      ain[q] = l < nb && B[l] == av[q];
+      apos[q] = i + l;
+      ca += ain[q];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < KB; q++) {
+    const uint32_t j = loB + q;
+    bin[q] = false;
+    bv[q] = 0;
+    bpos[q] = 0;
+    if (j < hiB) {
+      bv[q] = B[j];
+      const uint32_t l = lower_bound_u32(A, na, bv[q]);
+      bin[q] = l < na && A[l] == bv[q];
+      bpos[q] = j + l;
+      cb += bin[q];
+    }
+  }
+  uint32_t common, common2;
+  uint32_t exa = block_scan_u32<false>(ca, s_red, common);
+  uint32_t exb = block_scan_u32<false>(cb, s_red, common2);
+#pragma unroll
+  for (int q = 0; q < KA; q++)
+    if (loA + q < hiA) {
+      OUT[apos[q] - exa] = av[q];
+      exa += ain[q];
+    }
+#pragma unroll
+  for (int q = 0; q < KB; q++)
+    if (loB + q < hiB) {
+      if (!bin[q]) OUT[bpos[q] - exb] = bv[q];
+      exb += bin[q];
+    }
+  __syncthreads();
+  return na + nb - common;
+}
+
+// varint byte length of sorted unique codes (compressedList.Append deltas from 0)
+__device__ uint32_t list_bytes(const uint32_t* U, uint32_t n, uint32_t* s_red) {
+  uint32_t bytes = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) bytes += varint_len(U[i] - (i ? U[i - 1] : 0u));
+  return block_allreduce_u32_sum(bytes, s_red);
+}
+
+// toNormal (hyperloglog.go:152-166): registers from the codes of A and B (duplicates harmless:
+// with nz > 0 every insert is a plain max of min(r - b, 15)); the registers replace U.
+// A and B may live in U.  Returns nz.
+__device__ uint32_t to_normal(uint32_t* U, const uint32_t* A, uint32_t na, const uint32_t* B, uint32_t nb, uint32_t b,
+                              uint32_t* s_red) {
+  const uint32_t t = threadIdx.x;
+  uint32_t ka[kPer], kb[kPer];
+#pragma unroll
+  for (int q = 0; q < (int)kPer; q++) {
+    const uint32_t i = t + q * kBlock;
+    ka[q] = i < na ? A[i] : kHllNoCode;
+    kb[q] = i < nb ? B[i] : kHllNoCode;
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < kHllM; i += kBlock) U[i] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < (int)kPer; q++) {
+    uint32_t ri, r;
+    if (ka[q] != kHllNoCode) {
+      decode_hash(ka[q], &ri, &r);
+      if (r > b) atomicMax(&U[ri], min(r - b, kHllCapacity - 1));
+    }
+    if (kb[q] != kHllNoCode) {
+      decode_hash(kb[q], &ri, &r);
+      if (r > b) atomicMax(&U[ri], min(r - b, kHllCapacity - 1));
+    }
+  }
+  __syncthreads();
+  uint32_t z = 0;
+  for (uint32_t i = t; i < kHllM; i += kBlock) z += U[i] == 0;
+  return block_allreduce_u32_sum(z, s_red);
+}
+
+struct MergeCtx {
+  const uint32_t* tl;
+  const uint32_t* start;
+  const uint32_t* end;
+  const uint64_t* keys;   // sorted (slot << 32 | payload index)
+  const HllPart* parts;
+  const uint8_t* bytes;
+  uint8_t* mode;
+  uint8_t* base;
+  uint32_t* nz;
+  uint32_t* lc;
+  uint32_t* lb;
+  uint32_t* last;
+  uint32_t* tc;
+  uint32_t* tmp;
+  uint32_t* arena;
+  uint32_t* err;
+};
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) void k_set_merge(MergeCtx x) {
+  __shared__ uint32_t U[kArenaWords];  // the key: sorted list codes, or registers (u32 each)
+  __shared__ uint32_t Cb[kCWords];     // the payload's list codes / unions
+  __shared__ uint32_t s_tmp[256];      // the key's tmpSet, sorted (kHllNoCode padding)
+  __shared__ uint32_t s_ptmp[256];     // the payload's tmpSet, sorted
+  __shared__ uint32_t s_red[4];
+  __shared__ uint32_t s_b, s_nz, s_filled, s_tfull, s_pstar, s_newfill, s_min;
+  const uint32_t k = blockIdx.x, t = threadIdx.x;
+  const uint32_t slot = x.tl[k];
+  const uint32_t p0 = x.start[slot], p1 = x.end[slot];
+  uint32_t* arena = x.arena + (uint64_t)slot * kArenaWords;
+  uint8_t* regs8 = reinterpret_cast<uint8_t*>(arena);
+
+  bool dense = x.mode[slot] != 0;
+  uint32_t lc = x.lc[slot], tc = x.tc[slot], lbytes = x.lb[slot];
+  bool list_dirty = false;
+  if (t == 0) {
+    s_b = x.base[slot];
+    s_nz = x.nz[slot];
+  }
+  if (dense) {
+    for (uint32_t i = t; i < kHllM; i += kBlock) U[i] = regs8[i];
+  } else {
+    for (uint32_t i = t; i < lc; i += kBlock) U[i] = arena[i];
+    s_tmp[t] = t < tc ? x.tmp[(uint64_t)slot * kTmpCap + t] : kHllNoCode;
+  }
+  __syncthreads();
+  if (!dense) bitonic256(s_tmp);
+  const DenseLds S{U, &s_b, &s_nz, &s_filled, &s_tfull, &s_pstar, &s_newfill, &s_min, s_red};
+
+  for (uint32_t q = p0; q < p1; q++) {
+    const HllPart P = x.parts[(uint32_t)x.keys[q]];
+    if (P.kind == 2) continue;
+    if (P.kind == 0) {
+      // ---- the payload's codes: tmpSet (sorted) and decoded list
+      s_ptmp[t] = t < P.ntmp ? be32(x.bytes + P.tmp_off + 4ull * t) : kHllNoCode;
+      __syncthreads();
+      bitonic256(s_ptmp);
+      const uint32_t nl = decode_list(x.bytes + P.list_off, P.list_len, Cb, s_red);
+      if (!dense) {
+        // sparse <- sparse: tmpSet gets every code, then maybeToNormal
+        const uint32_t npt = unique_sorted<1>(s_ptmp, P.ntmp, s_red);
+        const uint32_t nd = union_unique<1, kCPer>(s_ptmp, npt, Cb, nl, Cb, s_red);
+        uint32_t hit = 0;
+        if (t < tc) {
+          const uint32_t c = s_tmp[t], l = lower_bound_u32(Cb, nd, c);
+          hit = l < nd && Cb[l] == c;
+        }
+        const uint32_t inter = block_allreduce_u32_sum(hit, s_red);
+        const uint32_t total = tc + nd - inter;
+        if (total * 100u > kHllM) {
+          // mergeSparse: list = list U tmpSet; then toNormal if its byte length > m
+          const uint32_t nd2 = union_unique<1, kCPer>(s_tmp, tc, Cb, nd, Cb, s_red);
+          uint32_t hit2 = 0;
+          for (uint32_t i = t; i < nd2; i += kBlock) {
+            const uint32_t c = Cb[i], l = lower_bound_u32(U, lc, c);
+            hit2 += l < lc && U[l] == c;
+          }
+          const uint32_t cnt = lc + nd2 - block_allreduce_u32_sum(hit2, s_red);
+          s_tmp[t] = kHllNoCode;
+          tc = 0;
+          if (cnt <= kArenaWords) {
+            lc = union_unique<kPer, kCPer>(U, lc, Cb, nd2, U, s_red);
+            lbytes = list_bytes(U, lc, s_red);
+            list_dirty = true;
+            if (lbytes > kHllM) {
+              const uint32_t z = to_normal(U, U, lc, nullptr, 0, s_b, s_red);
+              if (t == 0) s_nz = z;
+              dense = true;
+            }
+          } else {  // more codes than a sparse list can hold: certainly over m bytes
+            const uint32_t z = to_normal(U, U, lc, Cb, nd2, s_b, s_red);
+            if (t == 0) s_nz = z;
+            dense = true;
+          }
+          __syncthreads();
+        } else {
+          tc = union_unique<1, kCPer>(s_tmp, tc, Cb, nd, s_tmp, s_red);
+          s_tmp[t] = t < tc ? s_tmp[t] : kHllNoCode;
+          __syncthreads();
+        }
+      } else {
+        // dense <- sparse: insert every code, tmpSet first (ascending), then the list
+        const uint32_t nt = P.ntmp;
+        const uint32_t* pt = s_ptmp;
+        const uint32_t* cl = Cb;
+        dense_insert_codes(S, [pt, cl, nt](uint32_t p) { return p < nt ? pt[p] : cl[p - nt]; }, 0, nt + nl, x.err);
+        __syncthreads();
+      }
+      continue;
+    }
+    // ---- dense payload
+    if (!dense) {  // toNormal first (mergeSparse of the tmpSet included)
+      const uint32_t z = to_normal(U, U, lc, s_tmp, tc, s_b, s_red);
+      if (t == 0) s_nz = z;
+      s_tmp[t] = kHllNoCode;
+      tc = 0;
+      dense = true;
+      __syncthreads();
+    }
+    const uint32_t kb = s_b, pb = P.b;
+    uint32_t changed = 0, fills = 0;
+    if (kb < pb) {
+      // sk.regs.rebase(pb - kb): registers >= d drop by d, nz counts those left above zero
+      const uint32_t d = pb - kb;
+      for (uint32_t i = t; i < kHllM; i += kBlock) {
+        const uint32_t v = U[i];
+        if (v >= d) {
+          U[i] = v - d;
+          changed += (v - d) > 0;
+        }
+      }
+      changed = block_allreduce_u32_sum(changed, s_red);
+      if (t == 0) {
+        s_nz = kHllM - changed;
+        s_b = pb;
+      }
+    }
+    __syncthreads();
+    const uint32_t d2 = kb > pb ? kb - pb : 0u;  // cpOther.regs.rebase(kb - pb) on the copy
+    const uint8_t* rg = x.bytes + P.regs_off;
+    for (uint32_t i = t; i < kHllM; i += kBlock) {
+      const uint32_t byte = (i >> 1) < P.regs_len ? rg[i >> 1] : 0u;
+      uint32_t v = (i & 1) ? (byte & 15u) : (byte >> 4);
+      if (v >= d2) v -= d2;
+      const uint32_t cur = U[i];
+      if (v > cur) {
+        fills += cur == 0;
+        U[i] = v;
+      }
+    }
+    fills = block_allreduce_u32_sum(fills, s_red);
+    if (t == 0) s_nz -= fills;
+    __syncthreads();
+  }
+  __syncthreads();
+  // ---- write back
+  if (dense) {
+    for (uint32_t i = t; i < kHllM; i += kBlock) regs8[i] = (uint8_t)U[i];
+    if (t == 0) {
+      x.mode[slot] = 1;
+      x.base[slot] = (uint8_t)s_b;
+      x.nz[slot] = s_nz;
+      x.tc[slot] = 0;
+      x.lc[slot] = 0;
+      x.lb[slot] = 0;
+    }
+    return;
+  }
+  if (t < tc) x.tmp[(uint64_t)slot * kTmpCap + t] = s_tmp[t];
+  if (list_dirty)
+    for (uint32_t i = t; i < lc; i += kBlock) arena[i] = U[i];
+  if (t == 0) {
+    x.tc[slot] = tc;
+    x.lc[slot] = lc;
+    x.lb[slot] = lbytes;
+    if (list_dirty && lc) x.last[slot] = U[lc - 1];
+  }
+}
+
+__global__ void k_imp_seg_mark(uint64_t n, const uint64_t* __restrict__ K, uint32_t* __restrict__ start,
+                               uint32_t* __restrict__ end) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = (uint32_t)(K[i] >> 32);
+  if (i == 0 || (uint32_t)(K[i - 1] >> 32) != s) start[s] = (uint32_t)i;
+  if (i == n - 1 || (uint32_t)(K[i + 1] >> 32) != s) end[s] = (uint32_t)(i + 1);
+}
+
+__global__ void k_set_clear_bt(uint32_t n, const uint32_t* __restrict__ list, uint32_t* __restrict__ flags) {
+  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < n) flags[list[k]] = 0;
+}
+
+}  // namespace
+
+void import_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes) {
+  if (!n) return;
+  hipStream_t st = e->st;
+  HllPart* parts = reinterpret_cast<HllPart*>(e->imp.parts);
+  hipLaunchKernelGGL(k_hll_parse, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, parts, e->h_err);
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  take_decode_error(e);  // a truncated payload: nothing is applied
+  // group the payloads by key, arrival order kept
+  hipLaunchKernelGGL(k_hll_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, e->sR0, e->s_bt, e->stouch);
+  RadixPass passes[4];
+  int np = 0;
+  for (int sh = 32; sh < 32 + e->slot_bits[VN_SET]; sh += 8) passes[np++] = RadixPass{false, sh};
+  const bool fl = radix_sort(e->sR0, nullptr, e->sR1, nullptr, n, passes, np, e->rs, st, nullptr);
+  const uint64_t* keys = fl ? e->sR1 : e->sR0;
+  hipLaunchKernelGGL(k_imp_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, keys, e->s_start, e->s_end);
+  compact_flags(e->s_bt, e->s_pos, e->s_tl, e->s_cnt, e->cap[VN_SET], e->ss, st);
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 10, e->s_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  const uint32_t ntouched = e->hf_cnt[10];
+  if (!ntouched) return;
+  MergeCtx x;
+  x.tl = e->s_tl;
+  x.start = e->s_start;
+  x.end = e->s_end;
+  x.keys = keys;
+  x.parts = parts;
+  x.bytes = bytes;
+  x.mode = e->smode;
+  x.base = e->sbase;
+  x.nz = e->snz;
+  x.lc = e->slc;
+  x.lb = e->slb;
+  x.last = e->slast;
+  x.tc = e->stc;
+  x.tmp = e->stmp;
+  x.arena = e->sarena;
+  x.err = e->h_err;
+  hipLaunchKernelGGL(k_set_merge, dim3(ntouched), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_set_clear_bt, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->s_tl, e->s_bt);
+}
+
+}  // namespace vn

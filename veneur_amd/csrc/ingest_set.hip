@@ -23,7 +23,7 @@
 //         after it; records before that point are plain commutative max updates (LDS atomic
 //         max), the rebase itself is a parallel min + subtract.  Identical to the
 //         sequential semantics, rebase epochs included.
-#include "kernels.h"
+#include "set_dense.h"
 
 namespace vn {
 
@@ -67,7 +67,6 @@ __global__ void k_set_seg_mark(uint64_t n, const uint64_t* __restrict__ R, uint3
 }
 
 constexpr uint32_t kHashSlots = 512;  // LDS open-addressing table for the tmpSet (<= 163 codes)
-constexpr uint32_t kMark = 0x80000000u;
 
 __device__ __forceinline__ uint32_t hslot(uint32_t c) { return (c * 2654435761u) >> 23; }  // 9 bits
 
@@ -98,35 +97,6 @@ __device__ __forceinline__ void hash_insert_par(uint32_t* h, uint32_t c) {
     if (prev == kHllNoCode || prev == c) return;
     i = (i + 1) & (kHashSlots - 1);
   }
-}
-
-// bitonic sort of 256 u32 in LDS, ascending (all 256 threads)
-__device__ __forceinline__ void bitonic256(uint32_t* a) {
-  const uint32_t t = threadIdx.x;
-  for (uint32_t k = 2; k <= 256; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      uint32_t ixj = t ^ j;
-      if (ixj > t) {
-        uint32_t x = a[t], y = a[ixj];
-        bool up = (t & k) == 0;
-        if ((x > y) == up) {
-          a[t] = y;
-          a[ixj] = x;
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t v) {
-  uint32_t l = 0, h = n;
-  while (l < h) {
-    uint32_t m = (l + h) >> 1;
-    if (a[m] < v) l = m + 1;
-    else h = m;
-  }
-  return l;
 }
 
 __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
@@ -327,172 +297,9 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
   }
 
   // -------------------------------------------------------------- dense phase
-  uint32_t raw[kItems];
   {
-    const uint32_t c0 = s_pos;
-#pragma unroll
-    for (int j = 0; j < kItems; j++) {
-      uint32_t p = c0 + j * kBlock + t;
-      raw[j] = p < n ? (uint32_t)R[p] : 0u;
-    }
-  }
-  for (uint32_t cpos0 = s_pos; cpos0 < n; cpos0 += kTile) {
-    const uint32_t cend = min(n, cpos0 + (uint32_t)kTile);
-    uint32_t ri[kItems], rr[kItems];
-#pragma unroll
-    for (int j = 0; j < kItems; j++) {
-      uint32_t p = cpos0 + j * kBlock + t;
-      ri[j] = 0;
-      rr[j] = 0;
-      if (p < cend) decode_hash(raw[j], &ri[j], &rr[j]);
-    }
-    // prefetch the next chunk; its latency hides behind this chunk's phases
-#pragma unroll
-    for (int j = 0; j < kItems; j++) {
-      uint32_t p = cpos0 + kTile + j * kBlock + t;
-      raw[j] = p < n ? (uint32_t)R[p] : 0u;
-    }
-    uint32_t cpos = cpos0;
-    for (;;) {
-      const uint32_t b = s_b;
-      uint32_t tfull;
-      if (s_nz > 0) {
-        // fast path: mark the zero registers this chunk would fill; if they do not cover
-        // all nz of them, the fill cannot complete here, so no rebase can occur in the
-        // chunk and every update is a plain max
-        if (t == 0) s_filled = 0;
-        lds_barrier();
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-          uint32_t p = cpos0 + j * kBlock + t;
-          if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == 0)
-            if (atomicOr(&U[ri[j]], kMark) == 0) atomicAdd(&s_filled, 1u);
-        }
-        lds_barrier();
-        const bool completes = s_filled >= s_nz;
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-          uint32_t p = cpos0 + j * kBlock + t;
-          if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
-        }
-        lds_barrier();
-        if (!completes) {
-          if (t == 0) s_newfill = 0;
-          lds_barrier();
-#pragma unroll
-          for (int j = 0; j < kItems; j++) {
-            uint32_t p = cpos0 + j * kBlock + t;
-            if (p >= cpos && p < cend && rr[j] > b) {
-              uint32_t old = atomicMax(&U[ri[j]], min(rr[j] - b, kHllCapacity - 1));
-              if (old == 0) atomicAdd(&s_newfill, 1u);
-            }
-          }
-          lds_barrier();
-          if (t == 0) s_nz -= s_newfill;
-          lds_barrier();
-          break;
-        }
-        if (t == 0) {
-          s_filled = 0;
-          s_tfull = 0;
-        }
-        // phase A: mark the first filler of every zero register
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-          uint32_t p = cpos0 + j * kBlock + t;
-          if (p >= cpos && p < cend && rr[j] > b) {
-            uint32_t v = U[ri[j]];
-            if (v == 0 || (v & kMark)) atomicMax(&U[ri[j]], kMark | (0x7fffffffu - p));
-          }
-        }
-        lds_barrier();
-        // phase B: count first fillers, latest fill position
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-          uint32_t p = cpos0 + j * kBlock + t;
-          if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == (kMark | (0x7fffffffu - p))) {
-            atomicAdd(&s_filled, 1u);
-            atomicMax(&s_tfull, p);
-          }
-        }
-        lds_barrier();
-        tfull = (s_filled == s_nz) ? s_tfull : 0xffffffffu;
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-          uint32_t p = cpos0 + j * kBlock + t;
-          if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
-        }
-        lds_barrier();
-      } else {
-        tfull = cpos - 1;  // already full (cpos >= 1 whenever nz == 0 inside a key's stream)
-        if (cpos == 0) tfull = 0xfffffffeu;
-      }
-      if (t == 0) {
-        s_pstar = 0xffffffffu;
-        s_newfill = 0;
-      }
-      lds_barrier();
-      // phase C: first rebase candidate strictly after T_full
-      if (tfull != 0xffffffffu) {
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-          uint32_t p = cpos0 + j * kBlock + t;
-          bool after = (tfull == 0xfffffffeu) ? true : (p > tfull);
-          if (p >= cpos && p < cend && after && ((rr[j] - b) & 0xffu) >= kHllCapacity) atomicMin(&s_pstar, p);
-        }
-      }
-      lds_barrier();
-      const uint32_t pstar = s_pstar;
-      // phase D: plain max updates before the rebase point
-#pragma unroll
-      for (int j = 0; j < kItems; j++) {
-        uint32_t p = cpos0 + j * kBlock + t;
-        if (p >= cpos && p < cend && p < pstar && rr[j] > b) {
-          uint32_t old = atomicMax(&U[ri[j]], min(rr[j] - b, kHllCapacity - 1));
-          if (old == 0) atomicAdd(&s_newfill, 1u);
-        }
-      }
-      lds_barrier();
-      if (t == 0) s_nz -= s_newfill;
-      lds_barrier();
-      if (pstar == 0xffffffffu) break;
-      // rebase at pstar (nz == 0 here): b += min(regs); regs -= min
-      if (t == 0) s_min = 0xffffffffu;
-      lds_barrier();
-      {
-        uint32_t mn = 0xffffffffu;
-        for (uint32_t i = t; i < kHllM; i += kBlock) mn = min(mn, U[i]);
-        atomicMin(&s_min, mn);
-      }
-      lds_barrier();
-      const uint32_t db = s_min;
-      uint32_t z = 0;
-      for (uint32_t i = t; i < kHllM; i += kBlock) {
-        uint32_t v = U[i] - db;
-        U[i] = v;
-        z += v == 0;
-      }
-      z = block_allreduce_u32_sum(z, s_red);
-      if (t == 0) {
-        if (db == 0 || db == 0xffffffffu) atomicOr(x.err, 2u);
-        uint32_t nb = b + db;
-        s_b = nb;
-        s_nz = z;
-        // the candidate record itself, after the rebase
-        uint32_t pi, pr;
-        decode_hash((uint32_t)R[pstar], &pi, &pr);
-        if (pr > nb) {
-          uint32_t v = min(pr - nb, kHllCapacity - 1);
-          if (v > U[pi]) {
-            if (U[pi] == 0) s_nz -= 1;
-            U[pi] = v;
-          }
-        }
-      }
-      lds_barrier();
-      cpos = pstar + 1;
-      if (cpos >= cend) break;
-    }
+    const DenseLds S{U, &s_b, &s_nz, &s_filled, &s_tfull, &s_pstar, &s_newfill, &s_min, s_red};
+    dense_insert_codes(S, [R](uint32_t p) { return (uint32_t)R[p]; }, s_pos, n, x.err);
   }
   lds_barrier();
   for (uint32_t i = t; i < kHllM; i += kBlock) regs8[i] = (uint8_t)U[i];

@@ -1,0 +1,231 @@
+// set_dense.h -- axiomhq Sketch.insert over a stream of sparse codes for one key whose dense
+// registers sit in LDS, run by one 256-thread workgroup.  Shared by Set.Sample ingest
+// (ingest_set.hip) and Set.Combine of a sparse sketch into a dense one (import_set.hip).
+//
+// Reference: vendor/github.com/axiomhq/hyperloglog/hyperloglog.go:168-183 (insert) with
+// registers.go:56-123 (rebase, set, min).  Per chunk of kTile codes the workgroup finds T_full
+// (the code that fills the last zero register -- first filler per register via an LDS atomic
+// max on a marker) and the first rebase candidate after it; codes before that point are plain
+// commutative max updates (LDS atomic max), the rebase itself is a parallel min + subtract.
+// Identical to the sequential semantics, rebase epochs included.
+#pragma once
+#include "kernels.h"
+
+namespace vn {
+
+constexpr uint32_t kMark = 0x80000000u;
+
+// bitonic sort of 256 u32 in LDS, ascending (all 256 threads)
+__device__ __forceinline__ void bitonic256(uint32_t* a) {
+  const uint32_t t = threadIdx.x;
+  for (uint32_t k = 2; k <= 256; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      uint32_t ixj = t ^ j;
+      if (ixj > t) {
+        uint32_t x = a[t], y = a[ixj];
+        bool up = (t & k) == 0;
+        if ((x > y) == up) {
+          a[t] = y;
+          a[ixj] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t lower_bound_u32(const uint32_t* a, uint32_t n, uint32_t v) {
+  uint32_t l = 0, h = n;
+  while (l < h) {
+    uint32_t m = (l + h) >> 1;
+    if (a[m] < v) l = m + 1;
+    else h = m;
+  }
+  return l;
+}
+
+
+// LDS state of the key (all pointers into __shared__ memory of the calling kernel)
+struct DenseLds {
+  uint32_t* U;  // kHllM registers, one u32 each
+  uint32_t *b, *nz;
+  uint32_t *filled, *tfull, *pstar, *newfill, *mn;
+  uint32_t* red;  // 4
+};
+
+// insert(decode(src(p))) for p in [pos0, n), in order; src(p) -> sparse code (u32)
+template <class Src>
+__device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src& src, uint32_t pos0, uint32_t n,
+                                                   uint32_t* err) {
+  const uint32_t t = threadIdx.x;
+  uint32_t* U = S.U;
+  uint32_t raw[kItems];
+  {
+    const uint32_t c0 = pos0;
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      uint32_t p = c0 + j * kBlock + t;
+      raw[j] = p < n ? src(p) : 0u;
+    }
+  }
+  for (uint32_t cpos0 = pos0; cpos0 < n; cpos0 += kTile) {
+    const uint32_t cend = min(n, cpos0 + (uint32_t)kTile);
+    uint32_t ri[kItems], rr[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      uint32_t p = cpos0 + j * kBlock + t;
+      ri[j] = 0;
+      rr[j] = 0;
+      if (p < cend) decode_hash(raw[j], &ri[j], &rr[j]);
+    }
+    // prefetch the next chunk; its latency hides behind this chunk's phases
+#pragma unroll
+    for (int j = 0; j < kItems; j++) {
+      uint32_t p = cpos0 + kTile + j * kBlock + t;
+      raw[j] = p < n ? src(p) : 0u;
+    }
+    uint32_t cpos = cpos0;
+    for (;;) {
+      const uint32_t b = (*S.b);
+      uint32_t tfull;
+      if ((*S.nz) > 0) {
+        // fast path: mark the zero registers this chunk would fill; if they do not cover
+        // all nz of them, the fill cannot complete here, so no rebase can occur in the
+        // chunk and every update is a plain max
+        if (t == 0) (*S.filled) = 0;
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == 0)
+            if (atomicOr(&U[ri[j]], kMark) == 0) atomicAdd(&(*S.filled), 1u);
+        }
+        lds_barrier();
+        const bool completes = (*S.filled) >= (*S.nz);
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
+        }
+        lds_barrier();
+        if (!completes) {
+          if (t == 0) (*S.newfill) = 0;
+          lds_barrier();
+#pragma unroll
+          for (int j = 0; j < kItems; j++) {
+            uint32_t p = cpos0 + j * kBlock + t;
+            if (p >= cpos && p < cend && rr[j] > b) {
+              uint32_t old = atomicMax(&U[ri[j]], min(rr[j] - b, kHllCapacity - 1));
+              if (old == 0) atomicAdd(&(*S.newfill), 1u);
+            }
+          }
+          lds_barrier();
+          if (t == 0) (*S.nz) -= (*S.newfill);
+          lds_barrier();
+          break;
+        }
+        if (t == 0) {
+          (*S.filled) = 0;
+          (*S.tfull) = 0;
+        }
+        // phase A: mark the first filler of every zero register
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && rr[j] > b) {
+            uint32_t v = U[ri[j]];
+            if (v == 0 || (v & kMark)) atomicMax(&U[ri[j]], kMark | (0x7fffffffu - p));
+          }
+        }
+        lds_barrier();
+        // phase B: count first fillers, latest fill position
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == (kMark | (0x7fffffffu - p))) {
+            atomicAdd(&(*S.filled), 1u);
+            atomicMax(&(*S.tfull), p);
+          }
+        }
+        lds_barrier();
+        tfull = ((*S.filled) == (*S.nz)) ? (*S.tfull) : 0xffffffffu;
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
+        }
+        lds_barrier();
+      } else {
+        tfull = cpos - 1;  // already full (cpos >= 1 whenever nz == 0 inside a key's stream)
+        if (cpos == 0) tfull = 0xfffffffeu;
+      }
+      if (t == 0) {
+        (*S.pstar) = 0xffffffffu;
+        (*S.newfill) = 0;
+      }
+      lds_barrier();
+      // phase C: first rebase candidate strictly after T_full
+      if (tfull != 0xffffffffu) {
+#pragma unroll
+        for (int j = 0; j < kItems; j++) {
+          uint32_t p = cpos0 + j * kBlock + t;
+          bool after = (tfull == 0xfffffffeu) ? true : (p > tfull);
+          if (p >= cpos && p < cend && after && ((rr[j] - b) & 0xffu) >= kHllCapacity) atomicMin(&(*S.pstar), p);
+        }
+      }
+      lds_barrier();
+      const uint32_t pstar = (*S.pstar);
+      // phase D: plain max updates before the rebase point
+#pragma unroll
+      for (int j = 0; j < kItems; j++) {
+        uint32_t p = cpos0 + j * kBlock + t;
+        if (p >= cpos && p < cend && p < pstar && rr[j] > b) {
+          uint32_t old = atomicMax(&U[ri[j]], min(rr[j] - b, kHllCapacity - 1));
+          if (old == 0) atomicAdd(&(*S.newfill), 1u);
+        }
+      }
+      lds_barrier();
+      if (t == 0) (*S.nz) -= (*S.newfill);
+      lds_barrier();
+      if (pstar == 0xffffffffu) break;
+      // rebase at pstar (nz == 0 here): b += min(regs); regs -= min
+      if (t == 0) (*S.mn) = 0xffffffffu;
+      lds_barrier();
+      {
+        uint32_t mn = 0xffffffffu;
+        for (uint32_t i = t; i < kHllM; i += kBlock) mn = min(mn, U[i]);
+        atomicMin(&(*S.mn), mn);
+      }
+      lds_barrier();
+      const uint32_t db = (*S.mn);
+      uint32_t z = 0;
+      for (uint32_t i = t; i < kHllM; i += kBlock) {
+        uint32_t v = U[i] - db;
+        U[i] = v;
+        z += v == 0;
+      }
+      z = block_allreduce_u32_sum(z, S.red);
+      if (t == 0) {
+        if (db == 0 || db == 0xffffffffu) atomicOr(err, 2u);
+        uint32_t nb = b + db;
+        (*S.b) = nb;
+        (*S.nz) = z;
+        // the candidate record itself, after the rebase
+        uint32_t pi, pr;
+        decode_hash(src(pstar), &pi, &pr);
+        if (pr > nb) {
+          uint32_t v = min(pr - nb, kHllCapacity - 1);
+          if (v > U[pi]) {
+            if (U[pi] == 0) (*S.nz) -= 1;
+            U[pi] = v;
+          }
+        }
+      }
+      lds_barrier();
+      cpos = pstar + 1;
+      if (cpos >= cend) break;
+    }
+  }
+}
+
+}  // namespace vn

@@ -153,6 +153,13 @@ class Engine:
         self._check(A.lib.vn_import_histos(self.h, s.ctypes.data_as(A.u32p), off.ctypes.data_as(A.u64p),
                                            blob.ctypes.data_as(A.u8p), len(s)))
 
+    def import_sets(self, slot, payloads):
+        """ImportMetric of sets: Set.Combine of each MarshalBinary()d sketch
+        (samplers.go:313-325) into set slot[i], in order."""
+        s, off, blob = self._payloads(slot, payloads)
+        self._check(A.lib.vn_import_sets(self.h, s.ctypes.data_as(A.u32p), off.ctypes.data_as(A.u64p),
+                                         blob.ctypes.data_as(A.u8p), len(s)))
+
     def sync(self):
         self._check(A.lib.vn_sync(self.h))
 
