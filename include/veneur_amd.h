@@ -181,6 +181,31 @@ int vn_import_histos(vn_engine* eng, const uint32_t* slot, const uint64_t* off, 
  * only logged; a truncated payload fails the whole call with VN_EDECODE and applies nothing. */
 int vn_import_sets(vn_engine* eng, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n);
 
+/* MergingDigest.Quantile (kind 0, merging_digest.go:283-313) or CDF (kind 1, 247-279) of
+ * histo slot[i]'s digest in the current window at arg[i], into out[i] (host arrays).  As in
+ * the reference the pending temps are merged first (mergeAllTemps mutates the digest).
+ * Quantile arguments outside [0, 1] are rejected (the reference panics). */
+int vn_histo_query(vn_engine* eng, int kind, const uint32_t* slot, const double* arg, uint64_t n, double* out);
+
+/* Forward encoders (flushForward, flusher.go:264-353): one payload per requested slot, in
+ * request order, as the JSONMetric.Value a local veneur POSTs to its global.
+ *   vn_export_histos  Histo.Export (samplers.go:501-514) = MergingDigest.GobEncode
+ *                     (merging_digest.go:361-380); merges the key's pending temps first, as
+ *                     GobEncode does
+ *   vn_export_sets    Set.Export (samplers.go:296-310) = Sketch.MarshalBinary
+ *                     (hyperloglog.go:270-315), tmpSet in ascending order (Go: map order)
+ * The result (host and device views) is engine-owned and valid until the next export call;
+ * the device view feeds a GPU-to-GPU exchange (RCCL all-gather) of hot keys directly. */
+typedef struct {
+  uint64_t n;
+  const uint64_t* off;        /* n + 1 offsets into bytes (pinned host memory) */
+  const uint8_t* bytes;
+  const uint64_t* dev_off;    /* the same in device memory */
+  const uint8_t* dev_bytes;
+} vn_export;
+int vn_export_histos(vn_engine* eng, const uint32_t* slot, uint64_t n, vn_export* out);
+int vn_export_sets(vn_engine* eng, const uint32_t* slot, uint64_t n, vn_export* out);
+
 int vn_flush(vn_engine* eng, vn_flush_result* out);
 int vn_sync(vn_engine* eng);
 

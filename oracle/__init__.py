@@ -416,6 +416,10 @@ class Worker:
     def histo_quantile(self, slot, q):
         return lib.or_worker_histo_quantile(self.w, slot, q)
 
+    def histo_cdf(self, slot, x):
+        """MergingDigest.CDF of the slot's digest (merges its pending temps, as Go does)."""
+        return lib.or_td_cdf(lib.or_worker_histo_digest(self.w, slot), x)
+
     def histo_centroids(self, slot):
         n = lib.or_worker_histo_centroids(self.w, slot, None, None, 0)
         m = np.zeros(max(n, 1))
@@ -425,6 +429,13 @@ class Worker:
 
     def set_estimate(self, slot):
         return lib.or_worker_set_estimate(self.w, slot)
+
+    def histo_gob(self, slot) -> bytes:
+        """Histo.Export of the slot: GobEncode of its digest (merges its pending temps)."""
+        td = lib.or_worker_histo_digest(self.w, slot)
+        buf = np.zeros(1 << 20, np.uint8)
+        k = lib.or_td_gob_encode(td, ptr(buf, u8p), len(buf))
+        return buf[:k].tobytes()
 
     def set_sketch(self, slot):
         """Borrowed view of the slot's sketch (do not outlive the worker)."""

@@ -15,7 +15,7 @@ import pytest
 
 import oracle
 import veneur_amd as V
-from tests.util import PCT
+from tests.util import PCT, run_oracle
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -237,3 +237,53 @@ def test_import_sets_malformed_fails_loudly():
         e.import_sets([2], [good])
         f = e.flush()
     assert f.set_slot.tolist() == [2]
+
+
+# ------------------------------------------------------------------ export (forward encoders)
+def test_export_histos_byte_identical_and_roundtrip():
+    """Histo.Export = GobEncode (merging_digest.go:361-380): the engine's bytes equal the
+    restated Go encoder's (which reproduces fixtures/import.uncompressed), and a global that
+    imports them holds the local's digest."""
+    d = V.synth(seed=61, n_keys=80, zipf_s=1.0, mix=(0, 0, 1, 0), n_samples=30_000)
+    w = run_oracle(d, d["n_slots"])
+    slots = np.array([s for s in range(d["n_slots"][2]) if w.touched(2, s)], np.uint32)
+    with make_engine(d["n_slots"]) as e:
+        e.ingest(histos=(d["h_slot"], d["h_val"], d["h_rate"]))
+        pays = e.export_histos(slots)
+        again = e.export_histos(slots[::-1])  # pending temps merged once; repeats are stable
+    exp = [w.histo_gob(int(s)) for s in slots]
+    assert pays == exp
+    assert again == exp[::-1]
+    with make_engine(d["n_slots"]) as g:  # the global
+        g.import_histos(slots, pays)
+        f = g.flush()
+    w2 = oracle.Worker(*d["n_slots"])
+    for s, p in zip(slots, pays):
+        t = oracle.MergingDigest(100.0)
+        t.gob_decode(p)
+        w2.import_histo(int(s), p, identity(len(t.centroids()[0])))
+    oq = np.array([[w2.histo_quantile(int(s), p) for p in PCT] for s in f.histo_slot])
+    np.testing.assert_array_equal(f.histo_quantiles, oq)
+
+
+def test_export_sets_byte_identical_and_roundtrip():
+    """Set.Export = MarshalBinary (hyperloglog.go:270-315), sparse and dense (b > 0 too)."""
+    rng = np.random.default_rng(62)
+    sizes = [0, 1, 50, 163, 164, 900, 6000, 30000, 400_000]
+    slots = np.concatenate([np.full(n, i, np.uint32) for i, n in enumerate(sizes)])
+    hashes = random_hashes(rng, len(slots))
+    perm = rng.permutation(len(slots))
+    slots, hashes = slots[perm], hashes[perm]
+    nk = len(sizes)
+    w = oracle.Worker(1, 1, 1, nk)
+    w.set_hashed(slots, hashes)
+    with make_engine((1, 1, 1, nk), max_records=1 << 19) as e:
+        e.ingest(set_hashes=(slots, hashes))
+        touched = [s for s in range(nk) if w.touched(3, s)]
+        pays = e.export_sets(touched)
+    exp = [w.set_sketch(s).marshal() for s in touched]
+    assert pays == exp
+    with make_engine((1, 1, 1, nk), max_records=1 << 19) as g:
+        g.import_sets(touched, pays)
+        f = g.flush()
+    assert f.set_estimate.tolist() == [w.set_estimate(s) for s in touched]

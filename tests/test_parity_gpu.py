@@ -327,3 +327,25 @@ def test_invalid_inputs_fail_loudly():  # merging_digest.go:98-100 panics; parse
             e.ingest(histos=([0], [1.0], [0.0]))
         with pytest.raises(V.EngineError):
             e.ingest(counters=([5], [1.0], [1.0]))  # slot out of range
+
+
+def test_histo_quantile_cdf_queries():  # merging_digest.go:247-313 (Quantile, CDF mid-window)
+    d = V.synth(seed=25, n_keys=60, zipf_s=1.0, mix=(0, 0, 1, 0), n_samples=40_000)
+    w = run_oracle(d, d["n_slots"])
+    rng = np.random.default_rng(3)
+    with make_engine(d["n_slots"]) as e:
+        engine_ingest(e, d)
+        slots = np.array([s for s in range(d["n_slots"][2]) if w.touched(2, s)], np.uint32)
+        xs = np.exp(rng.normal(3.9, 1.2, len(slots)))
+        qs = rng.random(len(slots))
+        got_c = e.cdf(slots, xs)
+        got_q = e.quantile(slots, qs)
+        with pytest.raises(V.EngineError):
+            e.quantile(slots[:1], [1.5])  # Quantile panics outside [0, 1] (284-286)
+        f = e.flush()  # the queries merged pending temps: flush quantiles are unchanged by them
+    exp_c = np.array([w.histo_cdf(int(s), float(x)) for s, x in zip(slots, xs)])
+    exp_q = np.array([w.histo_quantile(int(s), float(q)) for s, q in zip(slots, qs)])
+    np.testing.assert_array_equal(got_c, exp_c)
+    np.testing.assert_array_equal(got_q, exp_q)
+    oq = np.array([[w.histo_quantile(int(s), p) for p in PCT] for s in f.histo_slot])
+    np.testing.assert_array_equal(f.histo_quantiles, oq)

@@ -73,6 +73,10 @@ class SetState(C.Structure):
                 ("list_last", C.c_uint32), ("tmp_count", C.c_uint32)]
 
 
+class Export(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("off", u64p), ("bytes", u8p), ("dev_off", C.c_void_p), ("dev_bytes", C.c_void_p)]
+
+
 class Timing(C.Structure):
     _fields_ = [("ms_ingest_counter", C.c_float), ("ms_ingest_gauge", C.c_float), ("ms_ingest_histo", C.c_float),
                 ("ms_ingest_set", C.c_float), ("ms_flush", C.c_float), ("ms_sort_histo", C.c_float),
@@ -117,6 +121,9 @@ _sig("vn_import_counters", C.c_int, vp, u32p, i64p, C.c_uint64)
 _sig("vn_import_gauges", C.c_int, vp, u32p, f64p, C.c_uint64)
 _sig("vn_import_histos", C.c_int, vp, u32p, u64p, u8p, C.c_uint64)
 _sig("vn_import_sets", C.c_int, vp, u32p, u64p, u8p, C.c_uint64)
+_sig("vn_histo_query", C.c_int, vp, C.c_int, u32p, f64p, C.c_uint64, f64p)
+_sig("vn_export_histos", C.c_int, vp, u32p, C.c_uint64, C.POINTER(Export))
+_sig("vn_export_sets", C.c_int, vp, u32p, C.c_uint64, C.POINTER(Export))
 _sig("vn_flush", C.c_int, vp, C.POINTER(FlushResult))
 _sig("vn_sync", C.c_int, vp)
 _sig("vn_read_histo", C.c_int, vp, C.c_uint32, f64p, f64p, C.c_uint32, u32p, f64p)
@@ -135,7 +142,7 @@ _sig("vn_synth_free", None, C.POINTER(SynthOut))
 # every symbol include/*.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
     "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
-    "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_flush", "vn_sync",
+    "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
 ]

@@ -1,5 +1,7 @@
 // capi.hip -- engine lifetime and the C-ABI of include/veneur_amd.h.
+#include <algorithm>
 #include <cstring>
+#include <vector>
 #include <stdexcept>
 
 #include "histo.h"
@@ -272,6 +274,40 @@ void stage_import(vn_engine* e, const uint32_t* slot, const uint64_t* off, const
   h2d(s.in_bytes, bytes, nb, st);
 }
 
+void ensure_export(vn_engine* e, uint64_t n) {
+  ExportBuffers& x = e->exp;
+  if (n <= x.cap_n) return;
+  dfree(x.d_slot); dfree(x.d_keys); dfree(x.d_size); dfree(x.d_off); hfree(x.h_off);
+  x.cap_n = std::max<uint64_t>(n, 1024);
+  dalloc(x.d_slot, x.cap_n);
+  dalloc(x.d_keys, x.cap_n);
+  dalloc(x.d_size, x.cap_n);
+  dalloc(x.d_off, x.cap_n + 1);
+  halloc(x.h_off, x.cap_n + 1);
+}
+
+void export_impl(vn_engine* e, int cls, const uint32_t* slot, uint64_t n, vn_export* out) {
+  check_slots_host(slot, n, e->cap[cls], cls == VN_HISTO ? "histo" : "set");
+  ensure_export(e, n);
+  ExportBuffers& x = e->exp;
+  h2d(x.d_slot, slot, n, e->st);
+  if (cls == VN_HISTO) {  // GobEncode merges the pending temps first (merging_digest.go:362)
+    std::vector<uint32_t> keys(slot, slot + n);
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    h2d(x.d_keys, keys.data(), keys.size(), e->st);
+    histo_merge_pending(e, x.d_keys, (uint32_t)keys.size());
+    export_histos(e, x.d_slot, n, x);
+  } else {
+    export_sets(e, x.d_slot, n, x);
+  }
+  out->n = n;
+  out->off = x.h_off;
+  out->bytes = x.h_bytes;
+  out->dev_off = x.d_off;
+  out->dev_bytes = x.d_bytes;
+}
+
 void destroy_impl(vn_engine* e) {
   if (e->st) (void)hipStreamSynchronize(e->st);
   dfree(e->cval); dfree(e->ctouch); dfree(e->gseq); dfree(e->gval); dfree(e->gtouch); dfree(e->pk); dfree(e->pp);
@@ -289,6 +325,9 @@ void destroy_impl(vn_engine* e) {
   dfree(e->smode); dfree(e->sbase); dfree(e->snz); dfree(e->slc); dfree(e->slb); dfree(e->slast); dfree(e->stc);
   dfree(e->stouch); dfree(e->stmp); dfree(e->sarena); dfree(e->sR0); dfree(e->sR1); dfree(e->s_bt);
   dfree(e->s_pos); dfree(e->s_tl); dfree(e->s_cnt); dfree(e->s_start); dfree(e->s_end);
+  ExportBuffers& xb = e->exp;
+  dfree(xb.d_slot); dfree(xb.d_keys); dfree(xb.d_size); dfree(xb.d_off); hfree(xb.h_off); dfree(xb.d_bytes);
+  hfree(xb.h_bytes);
   ImportScratch& is = e->imp;
   dfree(is.in_slot); dfree(is.in_off); dfree(is.in_bytes); dfree(is.cnt); dfree(is.coff); dfree(is.cslot);
   dfree(is.cmean); dfree(is.cw);
@@ -421,6 +460,15 @@ void ingest_host(vn_engine* e, const vn_batch* b) {
 }  // namespace
 
 namespace vn {
+void ensure_export_bytes(vn_engine* e, ExportBuffers& x, uint64_t nbytes) {
+  (void)e;
+  if (nbytes <= x.cap_bytes && x.d_bytes) return;
+  dfree(x.d_bytes);
+  hfree(x.h_bytes);
+  x.cap_bytes = std::max<uint64_t>(nbytes, 1 << 16);
+  dalloc(x.d_bytes, x.cap_bytes);
+  halloc(x.h_bytes, x.cap_bytes);
+}
 void take_decode_error(vn_engine* e) {
   uint32_t flags = 0;
   VN_HIP_CHECK(hipMemcpy(&flags, e->h_err, sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -586,6 +634,49 @@ int vn_import_sets(vn_engine* e, const uint32_t* slot, const uint64_t* off, cons
     VN_HIP_CHECK(hipGetLastError());
     e->imported += n;
   });
+}
+
+int vn_histo_query(vn_engine* e, int kind, const uint32_t* slot, const double* arg, uint64_t n, double* out) {
+  if (!e || (kind != 0 && kind != 1) || (n && (!slot || !arg || !out))) return VN_EINVAL;
+  return guarded(e, [&] {
+    if (!n) return;
+    check_slots_host(slot, n, e->cap[VN_HISTO], "histo");
+    if (kind == 0)
+      for (uint64_t i = 0; i < n; i++)
+        if (!(arg[i] >= 0.0 && arg[i] <= 1.0)) throw std::invalid_argument("quantile out of bounds");  // 284-286
+    std::vector<uint32_t> keys(slot, slot + n);
+    std::sort(keys.begin(), keys.end());
+    keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
+    uint32_t *dk = nullptr, *ds = nullptr;
+    double *da = nullptr, *dout = nullptr;
+    dalloc(dk, keys.size());
+    dalloc(ds, n);
+    dalloc(da, n);
+    dalloc(dout, n);
+    try {
+      h2d(dk, keys.data(), keys.size(), e->st);
+      h2d(ds, slot, n, e->st);
+      h2d(da, arg, n, e->st);
+      histo_merge_pending(e, dk, (uint32_t)keys.size());
+      histo_query(e, kind, ds, da, n, dout);
+      VN_HIP_CHECK(hipMemcpyAsync(out, dout, n * sizeof(double), hipMemcpyDeviceToHost, e->st));
+      VN_HIP_CHECK(hipStreamSynchronize(e->st));
+    } catch (...) {
+      dfree(dk); dfree(ds); dfree(da); dfree(dout);
+      throw;
+    }
+    dfree(dk); dfree(ds); dfree(da); dfree(dout);
+  });
+}
+
+int vn_export_histos(vn_engine* e, const uint32_t* slot, uint64_t n, vn_export* out) {
+  if (!e || !out || (n && !slot)) return VN_EINVAL;
+  return guarded(e, [&] { export_impl(e, VN_HISTO, slot, n, out); });
+}
+
+int vn_export_sets(vn_engine* e, const uint32_t* slot, uint64_t n, vn_export* out) {
+  if (!e || !out || (n && !slot)) return VN_EINVAL;
+  return guarded(e, [&] { export_impl(e, VN_SET, slot, n, out); });
 }
 
 int vn_flush(vn_engine* e, vn_flush_result* out) {

@@ -35,6 +35,18 @@ struct ImportScratch {
   double* cw = nullptr;
 };
 
+// Export results (vn_export_histos / vn_export_sets): engine-owned, valid until the next export.
+struct ExportBuffers {
+  uint64_t cap_n = 0, cap_bytes = 0;
+  uint32_t* d_slot = nullptr;     // [cap_n] requested slots
+  uint32_t* d_keys = nullptr;     // [cap_n] distinct slots (pending-temp merge)
+  uint32_t* d_size = nullptr;     // [cap_n]
+  uint64_t* d_off = nullptr;      // [cap_n + 1]
+  uint64_t* h_off = nullptr;      // pinned copy
+  uint8_t* d_bytes = nullptr;     // [cap_bytes]
+  uint8_t* h_bytes = nullptr;     // pinned copy
+};
+
 struct DeviceBatch {  // device-resident staging for one ingest call
   uint32_t *c_slot, *g_slot, *h_slot, *s_slot, *s_off;
   double *c_val, *g_val, *h_val;
@@ -150,6 +162,7 @@ struct vn_engine {
   // ---- staging
   vn::DeviceBatch dstage{};
   vn::ImportScratch imp;
+  vn::ExportBuffers exp;
   vn_stage pstage{};             // pinned host views
   // ---- flush outputs
   uint32_t* f_pos = nullptr;     // scan scratch (max cap + 1)

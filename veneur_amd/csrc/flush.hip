@@ -40,6 +40,71 @@ __device__ double td_quantile(const double* m, const double* w, uint32_t nc, dou
   return __builtin_nan("");
 }
 
+// MergingDigest.CDF (merging_digest.go:247-279)
+__device__ double td_cdf(const double* m, const double* w, uint32_t nc, double main_weight, double dmin, double dmax,
+                         double value) {
+  if (nc == 0) return __builtin_nan("");
+  if (value <= dmin) return 0.0;
+  if (value >= dmax) return 1.0;
+  double wsf = 0.0, lower = dmin;
+  for (uint32_t i = 0; i < nc; i++) {
+    const double upper = (i != nc - 1) ? ddiv(dadd(m[i + 1], m[i]), 2.0) : dmax;
+    if (value < upper) {
+      wsf = dadd(wsf, ddiv(dmul(w[i], dsub(value, lower)), dsub(upper, lower)));
+      return ddiv(wsf, main_weight);
+    }
+    wsf = dadd(wsf, w[i]);
+    lower = upper;
+  }
+  return __builtin_nan("");
+}
+
+// Quantile (kind 0) / CDF (kind 1) of slot[i]'s digest at arg[i] (pending temps already merged)
+__global__ void k_histo_query(uint64_t n, int kind, const uint32_t* __restrict__ slot, const double* __restrict__ arg,
+                              const double* __restrict__ hst, const uint32_t* __restrict__ hncent,
+                              const uint8_t* __restrict__ hcur, const double* __restrict__ cm0,
+                              const double* __restrict__ cm1, const double* __restrict__ cw0,
+                              const double* __restrict__ cw1, uint32_t capc, double* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t s = slot[i];
+  const double* h = hst + (uint64_t)s * VN_HISTO_STATS;
+  const uint8_t c = hcur[s];
+  const double* m = (c ? cm1 : cm0) + (uint64_t)s * capc;
+  const double* w = (c ? cw1 : cw0) + (uint64_t)s * capc;
+  out[i] = kind == 0 ? td_quantile(m, w, hncent[s], h[7], h[5], h[6], arg[i])
+                     : td_cdf(m, w, hncent[s], h[7], h[5], h[6], arg[i]);
+}
+
+// mergeAllTemps of the given keys (Quantile / CDF / GobEncode merge pending temps first)
+void histo_merge_pending(vn_engine* e, const uint32_t* dev_keys, uint32_t nkeys) {
+  if (!nkeys) return;
+  ExactCtx xc{};
+  xc.nkeys = nkeys;
+  xc.keys = dev_keys;
+  xc.delta = e->cfg.compression;
+  xc.capc = e->cap_cent;
+  xc.tcap = e->temp_cap;
+  xc.hst = e->hst;
+  xc.hncent = e->hncent;
+  xc.hcur = e->hcur;
+  xc.cm0 = e->cmean[0];
+  xc.cm1 = e->cmean[1];
+  xc.cw0 = e->cw[0];
+  xc.cw1 = e->cw[1];
+  xc.hpend = e->hpend;
+  xc.hpv = e->hpv;
+  xc.hpw = e->hpw;
+  xc.err = e->h_err;
+  xc.flush_mode = 1;
+  launch_histo_exact(xc, e->st, nullptr, 0);
+}
+
+void histo_query(vn_engine* e, int kind, const uint32_t* dev_slot, const double* dev_arg, uint64_t n, double* dev_out) {
+  hipLaunchKernelGGL(k_histo_query, dim3(blocks_for(n, 256)), dim3(256), 0, e->st, n, kind, dev_slot, dev_arg, e->hst,
+                     e->hncent, e->hcur, e->cmean[0], e->cmean[1], e->cw[0], e->cw[1], e->cap_cent, dev_out);
+}
+
 __global__ void k_flush_histo(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ list,
                               const double* __restrict__ hst, const uint32_t* __restrict__ hncent,
                               const uint8_t* __restrict__ hcur, const double* __restrict__ cm0,
@@ -225,25 +290,7 @@ void flush_all(vn_engine* e, vn_flush_result* out) {
   const uint32_t n[4] = {e->hf_cnt[4], e->hf_cnt[5], e->hf_cnt[6], e->hf_cnt[7]};
   if (ch && n[2]) {
     // Quantile() first merges the pending temps (merging_digest.go:287)
-    ExactCtx xc{};
-    xc.nkeys = n[2];
-    xc.keys = e->f_list[2];
-    xc.delta = e->cfg.compression;
-    xc.capc = e->cap_cent;
-    xc.tcap = e->temp_cap;
-    xc.hst = e->hst;
-    xc.hncent = e->hncent;
-    xc.hcur = e->hcur;
-    xc.cm0 = e->cmean[0];
-    xc.cm1 = e->cmean[1];
-    xc.cw0 = e->cw[0];
-    xc.cw1 = e->cw[1];
-    xc.hpend = e->hpend;
-    xc.hpv = e->hpv;
-    xc.hpw = e->hpw;
-    xc.err = e->h_err;
-    xc.flush_mode = 1;
-    launch_histo_exact(xc, st, nullptr, 0);
+    histo_merge_pending(e, e->f_list[2], n[2]);
     hipLaunchKernelGGL(k_flush_histo, dim3(blocks_for(n[2], 128)), dim3(128), 0, st, e->f_cnt + 2, e->f_list[2],
                        e->hst, e->hncent, e->hcur, e->cmean[0], e->cmean[1], e->cw[0], e->cw[1], e->cap_cent,
                        e->d_pct, e->cfg.n_percentiles, e->f_hstats, e->f_hq);

@@ -37,6 +37,17 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
 // Set.Sample (265-267) -> Sketch.Insert (hyperloglog.go:186-200)
 void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t* off, const uint8_t* bytes,
                  const uint64_t* hashes);
+// mergeAllTemps for the given (distinct) histo slots, device list
+void histo_merge_pending(vn_engine* e, const uint32_t* dev_keys, uint32_t nkeys);
+// MergingDigest.Quantile (kind 0) / CDF (kind 1) per (slot, arg); call histo_merge_pending first
+void histo_query(vn_engine* e, int kind, const uint32_t* dev_slot, const double* dev_arg, uint64_t n, double* dev_out);
+// exclusive scan of n u32 sizes into n+1 u64 offsets (device arrays)
+void scan_sizes_u64(const uint32_t* size, uint64_t* off, uint64_t n, hipStream_t st);
+// Histo.Export (GobEncode) / Set.Export (MarshalBinary) of the given slots (device list);
+// histo slots must have had their pending temps merged (histo_merge_pending)
+void export_histos(vn_engine* e, const uint32_t* dev_slot, uint64_t n, ExportBuffers& x);
+void export_sets(vn_engine* e, const uint32_t* dev_slot, uint64_t n, ExportBuffers& x);
+void ensure_export_bytes(vn_engine* e, ExportBuffers& x, uint64_t nbytes);
 // Worker.Flush + Counter/Gauge/Histo/Set.Flush math; resets the window
 void flush_all(vn_engine* e, vn_flush_result* out);
 // initial (empty-window) state of every slot
@@ -66,6 +77,24 @@ struct MinGoOp {
 struct MaxGoOp {
   __device__ double operator()(double a, double b) const { return max_go(a, b); }
 };
+
+// exclusive prefix sum of one u32 per thread across a 256-thread block; total = block sum
+__device__ __forceinline__ uint32_t block_scan_sum_u32(uint32_t v, uint32_t* s_wave, uint32_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) s_wave[w] = inc;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int i = 0; i < w; i++) base += s_wave[i];
+  total = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+  __syncthreads();
+  return base + inc - v;
+}
 
 // all-reduce across a 256-thread block (4 waves); s_tmp holds 4 doubles
 template <class Op>

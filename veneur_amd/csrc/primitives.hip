@@ -284,4 +284,54 @@ bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t
   return flipped;
 }
 
+// ---------------------------------------------------------------- u32 sizes -> u64 offsets
+// (export payload offsets may pass 4 GiB): per-tile sums, one-workgroup scan of the tile sums,
+// then each tile writes its running offsets
+__global__ __launch_bounds__(kBlock) void k_size_tiles(const uint32_t* __restrict__ size, uint64_t n,
+                                                       uint64_t* __restrict__ tile) {
+  __shared__ uint64_t s_w[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kTile;
+  uint64_t sum = 0;
+  for (uint32_t j = threadIdx.x; j < (uint32_t)kTile; j += kBlock)
+    if (base + j < n) sum += size[base + j];
+  for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) tile[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+__global__ void k_size_tiles_scan(uint64_t* __restrict__ tile, uint32_t ntiles) {
+  if (threadIdx.x != 0) return;
+  uint64_t run = 0;
+  for (uint32_t i = 0; i < ntiles; i++) {
+    const uint64_t v = tile[i];
+    tile[i] = run;
+    run += v;
+  }
+  tile[ntiles] = run;
+}
+__global__ void k_size_offsets(const uint32_t* __restrict__ size, uint64_t n, const uint64_t* __restrict__ tile,
+                               uint32_t ntiles, uint64_t* __restrict__ off) {
+  if (threadIdx.x != 0) return;  // one lane walks its tile (export sizes: latency, not bandwidth)
+  const uint64_t base = (uint64_t)blockIdx.x * kTile;
+  uint64_t run = tile[blockIdx.x];
+  for (uint32_t j = 0; j < (uint32_t)kTile && base + j < n; j++) {
+    off[base + j] = run;
+    run += size[base + j];
+  }
+  if (blockIdx.x == ntiles - 1) off[n] = tile[ntiles];
+}
+void scan_sizes_u64(const uint32_t* size, uint64_t* off, uint64_t n, hipStream_t st) {
+  if (n == 0) {
+    VN_HIP_CHECK(hipMemsetAsync(off, 0, sizeof(uint64_t), st));
+    return;
+  }
+  const uint32_t ntiles = (uint32_t)blocks_for(n, kTile);
+  uint64_t* tile = nullptr;
+  VN_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&tile), (ntiles + 1) * sizeof(uint64_t), st));
+  hipLaunchKernelGGL(k_size_tiles, dim3(ntiles), dim3(kBlock), 0, st, size, n, tile);
+  hipLaunchKernelGGL(k_size_tiles_scan, dim3(1), dim3(64), 0, st, tile, ntiles);
+  hipLaunchKernelGGL(k_size_offsets, dim3(ntiles), dim3(64), 0, st, size, n, tile, ntiles, off);
+  VN_HIP_CHECK(hipFreeAsync(tile, st));
+}
+
 }  // namespace vn

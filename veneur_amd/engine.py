@@ -160,6 +160,41 @@ class Engine:
         self._check(A.lib.vn_import_sets(self.h, s.ctypes.data_as(A.u32p), off.ctypes.data_as(A.u64p),
                                          blob.ctypes.data_as(A.u8p), len(s)))
 
+    def _query(self, kind, slot, arg):
+        s, a = _c(np.atleast_1d(slot), np.uint32), _c(np.atleast_1d(arg), np.float64)
+        s, a = np.broadcast_arrays(s, a)
+        s, a = np.ascontiguousarray(s), np.ascontiguousarray(a)
+        out = np.zeros(len(s))
+        self._check(A.lib.vn_histo_query(self.h, kind, s.ctypes.data_as(A.u32p), a.ctypes.data_as(A.f64p), len(s),
+                                         out.ctypes.data_as(A.f64p)))
+        return out
+
+    def quantile(self, slot, q):
+        """MergingDigest.Quantile of histo slot(s) in the current window (merging_digest.go:283-313)."""
+        return self._query(0, slot, q)
+
+    def cdf(self, slot, x):
+        """MergingDigest.CDF of histo slot(s) in the current window (merging_digest.go:247-279)."""
+        return self._query(1, slot, x)
+
+    def _export(self, fn, slot):
+        s = _c(np.atleast_1d(slot), np.uint32)
+        x = A.Export()
+        self._check(fn(self.h, s.ctypes.data_as(A.u32p), len(s), C.byref(x)))
+        if x.n == 0:
+            return []
+        off = np.ctypeslib.as_array(x.off, shape=(x.n + 1,)).copy()
+        blob = np.ctypeslib.as_array(x.bytes, shape=(max(1, int(off[-1])),)).tobytes()
+        return [blob[off[i]:off[i + 1]] for i in range(x.n)]
+
+    def export_histos(self, slot):
+        """Histo.Export: GobEncode()d digest of each histo slot (merges its pending temps)."""
+        return self._export(A.lib.vn_export_histos, slot)
+
+    def export_sets(self, slot):
+        """Set.Export: MarshalBinary()d sketch of each set slot."""
+        return self._export(A.lib.vn_export_sets, slot)
+
     def sync(self):
         self._check(A.lib.vn_sync(self.h))
 
