@@ -185,6 +185,12 @@ int vn_import_sets(vn_engine* eng, const uint32_t* slot, const uint64_t* off, co
  * histo slot[i]'s digest in the current window at arg[i], into out[i] (host arrays).  As in
  * the reference the pending temps are merged first (mergeAllTemps mutates the digest).
  * Quantile arguments outside [0, 1] are rejected (the reference panics). */
+/* The same two imports with slot/off/bytes already in device memory (HBM), e.g. payloads
+ * another GPU's export sent by an RCCL all-gather (veneur_amd/dist.py hot-key exchange). */
+int vn_import_histos_device(vn_engine* eng, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes,
+                            uint64_t n);
+int vn_import_sets_device(vn_engine* eng, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n);
+
 int vn_histo_query(vn_engine* eng, int kind, const uint32_t* slot, const double* arg, uint64_t n, double* out);
 
 /* Forward encoders (flushForward, flusher.go:264-353): one payload per requested slot, in
@@ -223,6 +229,7 @@ int vn_metro64(int device, const uint8_t* bytes, const uint32_t* off, uint64_t n
 int vn_device_alloc(int device, uint64_t bytes, void** out);
 int vn_device_free(void* p);
 int vn_copy_to_device(int device, void* dst, const void* src, uint64_t bytes);
+int vn_device_copy(int device, void* dst, const void* src, uint64_t bytes);  /* device to device */
 int vn_device_count(int* n);
 int vn_device_synchronize(int device);
 

@@ -121,6 +121,8 @@ _sig("vn_import_counters", C.c_int, vp, u32p, i64p, C.c_uint64)
 _sig("vn_import_gauges", C.c_int, vp, u32p, f64p, C.c_uint64)
 _sig("vn_import_histos", C.c_int, vp, u32p, u64p, u8p, C.c_uint64)
 _sig("vn_import_sets", C.c_int, vp, u32p, u64p, u8p, C.c_uint64)
+_sig("vn_import_histos_device", C.c_int, vp, vp, vp, vp, C.c_uint64)
+_sig("vn_import_sets_device", C.c_int, vp, vp, vp, vp, C.c_uint64)
 _sig("vn_histo_query", C.c_int, vp, C.c_int, u32p, f64p, C.c_uint64, f64p)
 _sig("vn_export_histos", C.c_int, vp, u32p, C.c_uint64, C.POINTER(Export))
 _sig("vn_export_sets", C.c_int, vp, u32p, C.c_uint64, C.POINTER(Export))
@@ -132,6 +134,7 @@ _sig("vn_metro64", C.c_int, C.c_int, u8p, u32p, C.c_uint64, C.c_uint64, u64p)
 _sig("vn_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(vp))
 _sig("vn_device_free", C.c_int, vp)
 _sig("vn_copy_to_device", C.c_int, C.c_int, vp, vp, C.c_uint64)
+_sig("vn_device_copy", C.c_int, C.c_int, vp, vp, C.c_uint64)
 _sig("vn_device_count", C.c_int, C.POINTER(C.c_int))
 _sig("vn_device_synchronize", C.c_int, C.c_int)
 _sig("vn_timing_enable", C.c_int, vp, C.c_int)
@@ -142,7 +145,7 @@ _sig("vn_synth_free", None, C.POINTER(SynthOut))
 # every symbol include/*.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
     "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
-    "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_sync",
+    "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
-    "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
+    "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
 ]

@@ -625,6 +625,36 @@ int vn_import_histos(vn_engine* e, const uint32_t* slot, const uint64_t* off, co
   });
 }
 
+// device-resident payloads: validate slots and offsets on the device
+__global__ void k_check_payloads(uint64_t n, const uint32_t* __restrict__ slot, const uint64_t* __restrict__ off,
+                                 uint32_t cap, uint32_t* __restrict__ err) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (slot[i] >= cap || off[i + 1] < off[i]) atomicOr(err, kErrDecode);
+}
+void import_device(vn_engine* e, int cls, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n) {
+  if (n > e->max_records) throw std::invalid_argument("import batch larger than max_batch_records");
+  ensure_import(e, n, 0);
+  hipLaunchKernelGGL(k_check_payloads, dim3(blocks_for(n, 256)), dim3(256), 0, e->st, n, slot, off, e->cap[cls],
+                     e->h_err);
+  VN_HIP_CHECK(hipStreamSynchronize(e->st));
+  take_decode_error(e);
+  if (cls == VN_HISTO) import_histos(e, n, slot, off, bytes);
+  else import_sets(e, n, slot, off, bytes);
+  VN_HIP_CHECK(hipGetLastError());
+  e->imported += n;
+}
+
+int vn_import_histos_device(vn_engine* e, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n) {
+  if (!e || (n && (!slot || !off || !bytes))) return VN_EINVAL;
+  return guarded(e, [&] { if (n) import_device(e, VN_HISTO, slot, off, bytes, n); });
+}
+
+int vn_import_sets_device(vn_engine* e, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n) {
+  if (!e || (n && (!slot || !off || !bytes))) return VN_EINVAL;
+  return guarded(e, [&] { if (n) import_device(e, VN_SET, slot, off, bytes, n); });
+}
+
 int vn_import_sets(vn_engine* e, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n) {
   if (!e || (n && (!slot || !off || !bytes))) return VN_EINVAL;
   return guarded(e, [&] {
@@ -821,6 +851,10 @@ int vn_device_free(void* p) { return hipFree(p) == hipSuccess ? VN_OK : VN_EHIP;
 int vn_copy_to_device(int device, void* dst, const void* src, uint64_t bytes) {
   if (hipSetDevice(device) != hipSuccess) return VN_EHIP;
   return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? VN_OK : VN_EHIP;
+}
+int vn_device_copy(int device, void* dst, const void* src, uint64_t bytes) {
+  if (hipSetDevice(device) != hipSuccess) return VN_EHIP;
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice) == hipSuccess ? VN_OK : VN_EHIP;
 }
 int vn_device_count(int* n) { return hipGetDeviceCount(n) == hipSuccess ? VN_OK : VN_EHIP; }
 int vn_device_synchronize(int device) {
