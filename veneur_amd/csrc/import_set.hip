@@ -523,7 +523,7 @@ void import_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t*
   hipLaunchKernelGGL(k_hll_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, e->sR0, e->s_bt, e->stouch);
   RadixPass passes[4];
   int np = 0;
-  for (int sh = 32; sh < 32 + e->slot_bits[VN_SET]; sh += 8) passes[np++] = RadixPass{false, sh};
+  np = make_passes(passes, false, 32, e->slot_bits[VN_SET]);
   const bool fl = radix_sort(e->sR0, nullptr, e->sR1, nullptr, n, passes, np, e->rs, st, nullptr);
   const uint64_t* keys = fl ? e->sR1 : e->sR0;
   hipLaunchKernelGGL(k_imp_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, keys, e->s_start, e->s_end);

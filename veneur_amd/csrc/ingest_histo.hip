@@ -732,7 +732,7 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
                      e->h_bt, e->htouch);
   RadixPass spass[4];
   int nsp = 0;
-  for (int sh = 32; sh < 32 + e->slot_bits[VN_HISTO]; sh += 8) spass[nsp++] = RadixPass{true, sh};
+  nsp = make_passes(spass, true, 32, e->slot_bits[VN_HISTO]);
   bool fl = radix_sort(e->hA0, e->hB0, e->hA1, e->hB1, n, spass, nsp, e->rs, st, e->timing ? &e->rstat_h : nullptr);
   uint64_t* As = fl ? e->hA1 : e->hA0;
   uint64_t* Bs = fl ? e->hB1 : e->hB0;
@@ -805,10 +805,10 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
                      e->n_geo, As, Bs, Ao, Bo);
   RadixPass passes[16];
   int np = 0;
-  for (int sh = 0; sh < 64; sh += 8) passes[np++] = RadixPass{false, sh};
+  np = make_passes(passes, false, 0, 64);
   int pbits = 1;
   while (pbits < 32 && (1ull << pbits) < npieces) pbits++;
-  for (int sh = 32; sh < 32 + pbits; sh += 8) passes[np++] = RadixPass{true, sh};
+  np += make_passes(passes + np, true, 32, pbits);
   const bool fl2 = radix_sort(Ao, Bo, As, Bs, nhotrec, passes, np, e->rs, st, e->timing ? &e->rstat_h : nullptr);
   const uint64_t* PA = fl2 ? As : Ao;  // sorted pieces
   const uint64_t* PB = fl2 ? Bs : Bo;

@@ -327,7 +327,7 @@ void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t*
                      e->s_bt, e->stouch);
   RadixPass passes[4];
   int np = 0;
-  for (int sh = 32; sh < 32 + e->slot_bits[VN_SET]; sh += 8) passes[np++] = RadixPass{false, sh};
+  np = make_passes(passes, false, 32, e->slot_bits[VN_SET]);
   bool fl = radix_sort(e->sR0, nullptr, e->sR1, nullptr, n, passes, np, *e->side_rs, st,
                        e->timing ? &e->rstat_s : nullptr);
   const uint64_t* R = fl ? e->sR1 : e->sR0;

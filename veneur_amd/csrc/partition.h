@@ -37,6 +37,9 @@ __device__ __forceinline__ uint64_t part_match8(uint32_t d, bool active) {
   return m;
 }
 
+// Each wave owns a contiguous quarter of the tile: its records are loaded up front (all loads
+// in flight together) and ranked with wave ballots against a per-wave running count per digit
+// in LDS (a wave's DS operations execute in order: no workgroup barrier while ranking).
 template <class Src, class Dst>
 __global__ __launch_bounds__(kBlock) void k_part_scatter(Src src, Dst dst, uint64_t n, int shift,
                                                          const uint32_t* __restrict__ counts,
@@ -44,14 +47,24 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(Src src, Dst dst, uint6
   using P = typename Src::P;
   __shared__ uint32_t s_key[kTile];
   __shared__ P s_pay[kTile];
-  __shared__ uint32_t s_wcnt[4][256];
-  __shared__ uint32_t s_run[256];
+  __shared__ uint32_t s_run[4][256];
   __shared__ uint32_t s_loc[256];
   __shared__ uint32_t s_glob[256];
   __shared__ uint32_t s_wave[4];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * kTile;
   const uint32_t tile_n = (uint32_t)((n - base) < (uint64_t)kTile ? (n - base) : kTile);
+  constexpr uint32_t kWaveTile = kTile / 4;
+  const uint32_t wbase = (uint32_t)w * kWaveTile;
+  uint32_t key[kItems];
+  P pay[kItems];
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    const uint32_t li = wbase + (uint32_t)j * 64 + lane;
+    key[j] = 0;
+    pay[j] = P{};
+    if (li < tile_n) src.load(base + li, key[j], pay[j]);
+  }
   {
     uint32_t c = counts[(uint64_t)t * nblocks + blockIdx.x];
     // exclusive scan of the tile's digit counts (4 waves)
@@ -67,40 +80,46 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(Src src, Dst dst, uint6
     for (int i = 0; i < w; i++) b0 += s_wave[i];
     s_loc[t] = b0 + inc - c;
     s_glob[t] = offsets[(uint64_t)t * nblocks + blockIdx.x];
-    s_run[t] = 0;
-    s_wcnt[0][t] = s_wcnt[1][t] = s_wcnt[2][t] = s_wcnt[3][t] = 0;
+    s_run[0][t] = s_run[1][t] = s_run[2][t] = s_run[3][t] = 0;
   }
   __syncthreads();
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t rank[kItems];
+#pragma unroll
   for (int j = 0; j < kItems; j++) {
-    const uint32_t li = (uint32_t)j * kBlock + t;
+    const uint32_t li = wbase + (uint32_t)j * 64 + lane;
     const bool active = li < tile_n;
-    uint32_t key = 0, d = 0;
-    P p{};
-    if (active) {
-      src.load(base + li, key, p);
-      d = (key >> shift) & 0xffu;
-    }
-    uint64_t peers = part_match8(d, active);
-    uint32_t rank = __popcll(peers & lt);
-    if (active && rank == 0) s_wcnt[w][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    if (active) {
-      uint32_t before = s_run[d];
-      for (int ww = 0; ww < w; ww++) before += s_wcnt[ww][d];
-      uint32_t pos = s_loc[d] + before + rank;
-      s_key[pos] = key;
-      s_pay[pos] = p;
-    }
-    __syncthreads();
-    s_run[t] += s_wcnt[0][t] + s_wcnt[1][t] + s_wcnt[2][t] + s_wcnt[3][t];
-    s_wcnt[0][t] = s_wcnt[1][t] = s_wcnt[2][t] = s_wcnt[3][t] = 0;
-    __syncthreads();
+    const uint32_t d = active ? (key[j] >> shift) & 0xffu : 0u;
+    const uint64_t peers = part_match8(d, active);
+    const uint32_t before = active ? s_run[w][d] : 0u;
+    rank[j] = before + (uint32_t)__popcll(peers & lt);
+    asm volatile("" ::: "memory");  // the wave's reads of s_run precede its leaders' update
+    if (active && (peers & lt) == 0) s_run[w][d] = before + (uint32_t)__popcll(peers);
+    asm volatile("" ::: "memory");
   }
+  __syncthreads();
+  {
+    const uint32_t c0 = s_run[0][t], c1 = s_run[1][t], c2 = s_run[2][t], l = s_loc[t];
+    s_run[0][t] = l;
+    s_run[1][t] = l + c0;
+    s_run[2][t] = l + c0 + c1;
+    s_run[3][t] = l + c0 + c1 + c2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    const uint32_t li = wbase + (uint32_t)j * 64 + lane;
+    if (li < tile_n) {
+      const uint32_t pos = s_run[w][(key[j] >> shift) & 0xffu] + rank[j];
+      s_key[pos] = key[j];
+      s_pay[pos] = pay[j];
+    }
+  }
+  __syncthreads();
   for (uint32_t li = t; li < tile_n; li += kBlock) {
-    uint32_t key = s_key[li];
-    uint32_t d = (key >> shift) & 0xffu;
-    dst.store((uint64_t)s_glob[d] + (li - s_loc[d]), key, s_pay[li]);
+    uint32_t k = s_key[li];
+    uint32_t d = (k >> shift) & 0xffu;
+    dst.store((uint64_t)s_glob[d] + (li - s_loc[d]), k, s_pay[li]);
   }
 }
 

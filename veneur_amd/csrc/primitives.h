@@ -22,7 +22,16 @@ void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, ScanScrat
 struct RadixPass {
   bool from_b;
   int shift;
+  int bits = 8;  // digit width (<= 8): fewer buckets give longer contiguous write runs
 };
+// Split the key field [lo, lo + nbits) of A (from_b false) or B into the fewest passes of
+// <= 8 bits, all of the same width (e.g. 18 slot bits -> 3 passes of 6 bits); returns the count.
+inline int make_passes(RadixPass* out, bool from_b, int lo, int nbits) {
+  if (nbits <= 0) return 0;
+  const int np = (nbits + 7) / 8, w = (nbits + np - 1) / np;
+  for (int p = 0; p < np; p++) out[p] = RadixPass{from_b, lo + p * w, w};
+  return np;
+}
 struct RadixScratch {
   uint32_t* counts = nullptr;    // 256 * blocks
   uint32_t* offsets = nullptr;   // 256 * blocks + 1

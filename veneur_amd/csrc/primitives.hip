@@ -127,14 +127,14 @@ void compact_flags(const uint32_t* flag, uint32_t* pos, uint32_t* list, uint32_t
 
 // ---------------------------------------------------------------- radix sort
 template <bool HASB>
-__device__ __forceinline__ uint32_t digit_of(uint64_t a, uint64_t b, bool from_b, int shift) {
+__device__ __forceinline__ uint32_t digit_of(uint64_t a, uint64_t b, bool from_b, int shift, uint32_t mask) {
   uint64_t w = (HASB && from_b) ? b : a;
-  return (uint32_t)(w >> shift) & 0xffu;
+  return (uint32_t)(w >> shift) & mask;
 }
 
 template <bool HASB>
 __global__ __launch_bounds__(kBlock) void k_radix_count(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
-                                                        uint64_t n, bool from_b, int shift,
+                                                        uint64_t n, bool from_b, int shift, uint32_t mask,
                                                         uint32_t* __restrict__ counts, uint32_t nblocks) {
   __shared__ uint32_t s_hist[4][256];
   const int w = threadIdx.x >> 6;
@@ -145,87 +145,111 @@ __global__ __launch_bounds__(kBlock) void k_radix_count(const uint64_t* __restri
 #pragma unroll 4
   for (int j = 0; j < kItems; j++) {
     uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
-    if (i < n) atomicAdd(&s_hist[w][(uint32_t)(src[i] >> shift) & 0xffu], 1u);
+    if (i < n) atomicAdd(&s_hist[w][(uint32_t)(src[i] >> shift) & mask], 1u);
   }
   __syncthreads();
   uint32_t d = threadIdx.x;
-  counts[(uint64_t)d * nblocks + blockIdx.x] = s_hist[0][d] + s_hist[1][d] + s_hist[2][d] + s_hist[3][d];
+  if (d <= mask) counts[(uint64_t)d * nblocks + blockIdx.x] = s_hist[0][d] + s_hist[1][d] + s_hist[2][d] + s_hist[3][d];
 }
 
-// lanes of the wave holding the same 8-bit digit as this lane (among `active` lanes)
-__device__ __forceinline__ uint64_t match_digit8(uint32_t d, bool active) {
+// lanes of the wave holding the same digit (of `bits` bits) as this lane (among `active` lanes)
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, bool active, int bits) {
   uint64_t m = __ballot(active);
-#pragma unroll
-  for (int bit = 0; bit < 8; bit++) {
+  for (int bit = 0; bit < bits; bit++) {
     uint64_t bb = __ballot(active && ((d >> bit) & 1u));
     m &= ((d >> bit) & 1u) ? bb : ~bb;
   }
   return m;
 }
 
+// Stable scatter of one tile (kTile records) by an 8-bit digit.  Each wave owns a contiguous
+// quarter of the tile (kItems records per lane, loaded up front so all global loads are in
+// flight together); it ranks its records with wave ballots and a per-wave running count per
+// digit in LDS -- DS operations of one wave execute in order, so no workgroup barrier is needed
+// while ranking.  Then the per-(wave, digit) starts are a scan over the four waves, the tile is
+// reordered in LDS, and written out with consecutive lanes on consecutive records of a digit.
 template <bool HASB>
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
                                                           uint64_t* __restrict__ A2, uint64_t* __restrict__ B2,
-                                                          uint64_t n, bool from_b, int shift,
+                                                          uint64_t n, bool from_b, int shift, int bits,
                                                           const uint32_t* __restrict__ counts,
                                                           const uint32_t* __restrict__ offsets, uint32_t nblocks) {
   __shared__ uint64_t s_a[kTile];
   __shared__ uint64_t s_b[HASB ? kTile : 1];
-  __shared__ uint32_t s_wcnt[4][256];
-  __shared__ uint32_t s_run[256];
-  __shared__ uint32_t s_loc[256];   // tile-local start of each digit
-  __shared__ uint32_t s_glob[256];  // global start of each digit for this tile
+  __shared__ uint32_t s_run[4][256];  // per wave: records of each digit ranked so far
+  __shared__ uint32_t s_loc[256];     // tile-local start of each digit
+  __shared__ uint32_t s_glob[256];    // global start of each digit for this tile
   __shared__ uint32_t s_wave[4];
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * kTile;
   const uint32_t tile_n = (uint32_t)((n - base) < (uint64_t)kTile ? (n - base) : kTile);
+  constexpr uint32_t kWaveTile = kTile / 4;
 
+  // all of this lane's records first: 16 coalesced loads in flight per array
+  uint64_t a[kItems], b[kItems];
+  const uint32_t wbase = (uint32_t)w * kWaveTile;
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    const uint32_t li = wbase + (uint32_t)j * 64 + lane;
+    a[j] = li < tile_n ? A[base + li] : 0;
+    if (HASB) b[j] = li < tile_n ? B[base + li] : 0;
+  }
+  const uint32_t mask = (1u << bits) - 1u;
   {
-    uint32_t c = counts[(uint64_t)t * nblocks + blockIdx.x];
+    const bool dig = (uint32_t)t <= mask;
+    uint32_t c = dig ? counts[(uint64_t)t * nblocks + blockIdx.x] : 0u;
     uint32_t total;
     s_loc[t] = block_excl_scan_u32(c, s_wave, total);
-    s_glob[t] = offsets[(uint64_t)t * nblocks + blockIdx.x];
-    s_run[t] = 0;
-    s_wcnt[0][t] = s_wcnt[1][t] = s_wcnt[2][t] = s_wcnt[3][t] = 0;
+    s_glob[t] = dig ? offsets[(uint64_t)t * nblocks + blockIdx.x] : 0u;
+    s_run[0][t] = s_run[1][t] = s_run[2][t] = s_run[3][t] = 0;
   }
   __syncthreads();
-
+  // rank inside the wave's quarter, in record order
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t rank[kItems];
+#pragma unroll
   for (int j = 0; j < kItems; j++) {
-    const uint32_t li = (uint32_t)j * kBlock + t;
+    const uint32_t li = wbase + (uint32_t)j * 64 + lane;
     const bool active = li < tile_n;
-    uint64_t a = 0, b = 0;
-    uint32_t d = 0;
-    if (active) {
-      a = A[base + li];
-      if (HASB) b = B[base + li];
-      d = digit_of<HASB>(a, b, from_b, shift);
-    }
-    uint64_t peers = match_digit8(d, active);
-    uint32_t rank = __popcll(peers & lt);
-    if (active && rank == 0) s_wcnt[w][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    if (active) {
-      uint32_t before = s_run[d];
-      for (int ww = 0; ww < w; ww++) before += s_wcnt[ww][d];
-      uint32_t pos = s_loc[d] + before + rank;
-      s_a[pos] = a;
-      if (HASB) s_b[pos] = b;
-    }
-    __syncthreads();
-    s_run[t] += s_wcnt[0][t] + s_wcnt[1][t] + s_wcnt[2][t] + s_wcnt[3][t];
-    s_wcnt[0][t] = s_wcnt[1][t] = s_wcnt[2][t] = s_wcnt[3][t] = 0;
-    __syncthreads();
+    const uint32_t d = active ? digit_of<HASB>(a[j], HASB ? b[j] : 0, from_b, shift, mask) : 0u;
+    const uint64_t peers = match_digit(d, active, bits);
+    const uint32_t before = active ? s_run[w][d] : 0u;
+    rank[j] = before + (uint32_t)__popcll(peers & lt);
+    asm volatile("" ::: "memory");  // the wave's reads of s_run precede its leaders' update
+    if (active && (peers & lt) == 0) s_run[w][d] = before + (uint32_t)__popcll(peers);
+    asm volatile("" ::: "memory");
   }
-
+  __syncthreads();
+  // per (wave, digit) start inside the tile: digit start + the earlier waves' counts
+  {
+    const uint32_t c0 = s_run[0][t], c1 = s_run[1][t], c2 = s_run[2][t];
+    const uint32_t l = s_loc[t];
+    __syncthreads();
+    s_run[0][t] = l;
+    s_run[1][t] = l + c0;
+    s_run[2][t] = l + c0 + c1;
+    s_run[3][t] = l + c0 + c1 + c2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    const uint32_t li = wbase + (uint32_t)j * 64 + lane;
+    if (li < tile_n) {
+      const uint32_t d = digit_of<HASB>(a[j], HASB ? b[j] : 0, from_b, shift, mask);
+      const uint32_t pos = s_run[w][d] + rank[j];
+      s_a[pos] = a[j];
+      if (HASB) s_b[pos] = b[j];
+    }
+  }
+  __syncthreads();
   for (uint32_t li = t; li < tile_n; li += kBlock) {
-    uint64_t a = s_a[li];
-    uint64_t b = HASB ? s_b[li] : 0;
-    uint32_t d = digit_of<HASB>(a, b, from_b, shift);
-    uint64_t pos = (uint64_t)s_glob[d] + (li - s_loc[d]);
-    A2[pos] = a;
-    if (HASB) B2[pos] = b;
+    const uint64_t av = s_a[li];
+    const uint64_t bv = HASB ? s_b[li] : 0;
+    const uint32_t d = digit_of<HASB>(av, bv, from_b, shift, mask);
+    const uint64_t pos = (uint64_t)s_glob[d] + (li - s_loc[d]);
+    A2[pos] = av;
+    if (HASB) B2[pos] = bv;
   }
 }
 
@@ -258,22 +282,23 @@ bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t
     uint64_t* sb = flipped ? b1 : b0;
     uint64_t* da = flipped ? a0 : a1;
     uint64_t* db = flipped ? b0 : b1;
+    const uint32_t mask = (1u << ps.bits) - 1u;
     if (hasb)
-      hipLaunchKernelGGL(k_radix_count<true>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, n, ps.from_b, ps.shift,
+      hipLaunchKernelGGL(k_radix_count<true>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, n, ps.from_b, ps.shift, mask,
                          s.counts, nblocks);
     else
       hipLaunchKernelGGL(k_radix_count<false>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, n, ps.from_b, ps.shift,
-                         s.counts, nblocks);
-    scan_exclusive_u32(s.counts, s.offsets, (uint64_t)256 * nblocks, s.scan, st);
+                         mask, s.counts, nblocks);
+    scan_exclusive_u32(s.counts, s.offsets, (uint64_t)(mask + 1) * nblocks, s.scan, st);
     hipEvent_t e0 = (stats && stats->pool) ? stats->pool->next() : nullptr;
     hipEvent_t e1 = (stats && stats->pool) ? stats->pool->next() : nullptr;
     if (e0 && e1) VN_HIP_CHECK(hipEventRecord(e0, st));
     if (hasb)
       hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, da, db, n, ps.from_b,
-                         ps.shift, s.counts, s.offsets, nblocks);
+                         ps.shift, ps.bits, s.counts, s.offsets, nblocks);
     else
       hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, da, db, n, ps.from_b,
-                         ps.shift, s.counts, s.offsets, nblocks);
+                         ps.shift, ps.bits, s.counts, s.offsets, nblocks);
     if (e0 && e1) VN_HIP_CHECK(hipEventRecord(e1, st));
     if (stats) {
       stats->launches += 1;
