@@ -65,6 +65,10 @@ typedef struct {
    * MergingDigest's 42-sample incremental merge bit-for-bit; samples beyond it are merged
    * in one batch per ingest (rank-error parity).  0 -> 32768; UINT32_MAX -> always exact. */
   uint32_t histo_exact_threshold;
+  /* a key that passes the threshold is not bit-exact anyway: only its first
+   * `histo_hot_prefix` samples are replayed exactly, the rest merge in geometric pieces
+   * (each 10% of the samples seen so far).  0 -> 4096; clamped to the threshold. */
+  uint32_t histo_hot_prefix;
 } vn_config;
 
 /* One ingest batch: per-class SoA streams in arrival order (the order ProcessMetric saw

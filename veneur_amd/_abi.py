@@ -32,7 +32,8 @@ class Config(C.Structure):
     _fields_ = [("device", C.c_int32), ("capacity", C.c_uint32 * 4), ("compression", C.c_double),
                 ("n_percentiles", C.c_uint32), ("percentiles", C.c_double * VN_MAX_PERCENTILES),
                 ("max_batch_records", C.c_uint64), ("max_batch_member_bytes", C.c_uint64),
-                ("histo_exact_threshold", C.c_uint32)]
+                ("histo_exact_threshold", C.c_uint32),
+                ("histo_hot_prefix", C.c_uint32)]
 
 
 class Batch(C.Structure):

@@ -1,6 +1,7 @@
 // capi.hip -- engine lifetime and the C-ABI of include/veneur_amd.h.
 #include <algorithm>
 #include <cstring>
+#include <cstdlib>
 #include <vector>
 #include <stdexcept>
 
@@ -77,10 +78,41 @@ void check_slots_host(const uint32_t* slot, uint64_t n, uint32_t cap, const char
 
 void create_impl(vn_engine* e) {
   VN_HIP_CHECK(hipSetDevice(e->device));
-  VN_HIP_CHECK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
-  VN_HIP_CHECK(hipStreamCreateWithFlags(&e->st2, hipStreamNonBlocking));
+  // the histo path (main and replay streams) is the critical path: it gets the high queue
+  // priority, the side stream's counters / gauges / sets fill whatever CUs it leaves
+  int prio_lo = 0, prio_hi = 0;
+  VN_HIP_CHECK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+  VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st, hipStreamNonBlocking, prio_hi));
+  // Queue priority does not preempt: once the long set merge and the replay of the keys under
+  // the threshold (100k+ workgroups, some running for milliseconds) fill the CUs, the
+  // remainder rounds' chain workgroups (~100 KiB of LDS each) wait for a CU to drain -- and a
+  // workgroup waits inside the shader engine it was dealt to.  Those two streams therefore
+  // leave the last quarter of the CU mask to the main stream.  Measured on gfx950
+  // (tools/probe/cumask_probe.hip): mask bit i is XCC i % 8, shader engine (i / 8) % 4, CU
+  // i / 32 within it, so bits [3/4 ncu, ncu) are 2 CUs in every shader engine of every XCC.
+  {
+    hipDeviceProp_t prop;
+    VN_HIP_CHECK(hipGetDeviceProperties(&prop, e->device));
+    const uint32_t ncu = (uint32_t)prop.multiProcessorCount;
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (uint32_t i = 0; i < ncu - ncu / 4; i++) mask[i / 32] |= 1u << (i % 32);
+    e->side_cus = ncu - ncu / 4;
+    if (ncu < 64 || hipExtStreamCreateWithCUMask(&e->st2, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&e->st3, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+      (void)hipGetLastError();
+      if (e->st2) (void)hipStreamDestroy(e->st2);
+      e->st2 = nullptr;
+      VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st2, hipStreamNonBlocking, prio_lo));
+      VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st3, hipStreamNonBlocking, prio_hi));
+      e->side_cus = ncu;
+    }
+  }
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
+  VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st4, hipStreamNonBlocking, prio_hi));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join4, hipEventDisableTiming));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork3, hipEventDisableTiming));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join3, hipEventDisableTiming));
   hipStream_t st = e->st;
   const uint64_t R = e->max_records;
   const uint32_t cc = e->cap[VN_COUNTER], cg = e->cap[VN_GAUGE], ch = e->cap[VN_HISTO], cs = e->cap[VN_SET];
@@ -136,6 +168,11 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_hotcnt, touch_max);
   dalloc(e->h_hotoff, (size_t)touch_max + 1);
   dalloc(e->h_hotlist, touch_max);
+  dalloc(e->h_coldflag, touch_max);
+  dalloc(e->h_coldlist, touch_max);
+  dalloc(e->hA2, e->h_sort_cap); dalloc(e->hB2, e->h_sort_cap);
+  dalloc(e->h_csv, ch ? R : 0); dalloc(e->h_csw, ch ? R : 0);
+  dalloc(e->h_lpt0, touch_max); dalloc(e->h_lpt1, touch_max);
   dalloc(e->h_tl2, touch_max);
   dalloc(e->h_ccnt, touch_max);
   dalloc(e->h_coff, (size_t)touch_max + 1);
@@ -154,7 +191,7 @@ void create_impl(vn_engine* e) {
   {
     // piece boundaries of the geometric remainder (see ingest_histo.hip)
     std::vector<uint64_t> geo;
-    for (uint64_t b = e->exact_threshold; geo.size() < 255 && b < (1ull << 40); b += std::max<uint64_t>(1, b / 10))
+    for (uint64_t b = e->hot_prefix; geo.size() < 255 && b < (1ull << 40); b += std::max<uint64_t>(1, b / 10))
       geo.push_back(b);
     e->n_geo = (uint32_t)geo.size();
     dalloc(e->h_geo, geo.size());
@@ -178,6 +215,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->s_pos, (size_t)cs + 1);
   dalloc(e->s_tl, cs);
   dalloc(e->s_cnt, 4);
+  dalloc(e->s_lpt0, cs); dalloc(e->s_lpt1, cs);
   dalloc(e->s_start, cs);
   dalloc(e->s_end, cs);
 
@@ -204,6 +242,7 @@ void create_impl(vn_engine* e) {
 
   radix_scratch_reserve(e->rs, std::max<uint64_t>(e->h_sort_cap, (cs || cc || cg) ? R : 0));
   radix_scratch_reserve(e->rs2, (cs || cc || cg) ? R : 1);
+  radix_scratch_reserve(e->rs3, std::max<uint64_t>(touch_max, 1));
   init_state(e);
   VN_HIP_CHECK(hipStreamSynchronize(st));
 }
@@ -319,6 +358,8 @@ void destroy_impl(vn_engine* e) {
   dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
   dfree(e->hseen); dfree(e->hpend); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
+  dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw);
+  dfree(e->h_lpt0); dfree(e->h_lpt1); dfree(e->s_lpt0); dfree(e->s_lpt1);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);
   dfree(e->h_geo); dfree(e->h_seen0); dfree(e->h_pcnt); dfree(e->h_pi0); dfree(e->h_pbase); dfree(e->p_start);
   dfree(e->p_end); dfree(e->r_flag); dfree(e->r_len); dfree(e->r_list); dfree(e->r_off); dfree(e->r_pos);
@@ -346,9 +387,17 @@ void destroy_impl(vn_engine* e) {
   dfree(e->f_ssparse); hfree(e->hf_ssparse); dfree(e->d_pct); hfree(e->hf_cnt);
   radix_scratch_free(e->rs);
   radix_scratch_free(e->rs2);
+  radix_scratch_free(e->rs3);
   if (e->ss.partials) (void)hipFree(e->ss.partials);
   if (e->ss2.partials) (void)hipFree(e->ss2.partials);
   if (e->st2) (void)hipStreamSynchronize(e->st2);
+  if (e->st3) (void)hipStreamSynchronize(e->st3);
+  if (e->ev_fork3) (void)hipEventDestroy(e->ev_fork3);
+  if (e->ev_join3) (void)hipEventDestroy(e->ev_join3);
+  if (e->st3) (void)hipStreamDestroy(e->st3);
+  if (e->st4) (void)hipStreamSynchronize(e->st4);
+  if (e->ev_join4) (void)hipEventDestroy(e->ev_join4);
+  if (e->st4) (void)hipStreamDestroy(e->st4);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->st2) (void)hipStreamDestroy(e->st2);
@@ -382,17 +431,33 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
     e->rstat_s = RadixStats{&e->pool, 0, 0};
     VN_HIP_CHECK(hipEventRecord(e->ev[0], st));
   }
-  // counters and gauges go first on the side stream, then the histo path (which waits on the
-  // host for its segment counts) on the main stream, then sets on the side stream again
-  side_begin(e);
-  ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
-  if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[1], st));
-  ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
-  if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[2], st));
-  ingest_histos(e, b->n_histo, b->histo_slot, b->histo_value, b->histo_rate);
-  if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[3], st));
-  ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
-  side_join(e);
+  if (tm) {
+    // measured: one phase at a time on the main stream
+    side_begin(e);
+    ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
+    VN_HIP_CHECK(hipEventRecord(e->ev[1], st));
+    ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
+    VN_HIP_CHECK(hipEventRecord(e->ev[2], st));
+    ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
+    VN_HIP_CHECK(hipEventRecord(e->ev[3], st));
+    ingest_histos(e, b->n_histo, b->histo_slot, b->histo_value, b->histo_rate);
+    side_join(e);
+  } else {
+    // the histo grouping sort (critical path) is queued first on the main stream; then
+    // counters, gauges and sets on the low-priority side stream (none of them waits on the
+    // host); then the rest of the histo path, whose host round trips no longer hold back
+    // the side work -- it fills the GPU while the replays and remainder rounds run
+    side_begin(e);  // the side stream waits for what the main stream held before this call
+    const HistoGroups g = histo_group(e, b->n_histo, b->histo_slot, b->histo_value, b->histo_rate);
+    ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
+    ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
+    e->set_defer = true;  // histo_process queues the set merge after the remainder sort
+    ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
+    e->set_defer = false;
+    histo_process(e, b->n_histo, g);
+    set_finish(e);
+    side_join(e);
+  }
   if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[4], st));
   VN_HIP_CHECK(hipGetLastError());  // a launch that could not start (e.g. LDS over budget) fails loudly
   e->processed += b->n_counter + b->n_gauge + b->n_histo + b->n_set;
@@ -527,6 +592,8 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
     return VN_EINVAL;
   }
   e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 32768u;
+  if (const char* v = std::getenv("VN_LPT")) e->lpt = (uint32_t)std::atoi(v);
+  e->hot_prefix = std::min(e->exact_threshold, cfg->histo_hot_prefix ? cfg->histo_hot_prefix : 4096u);
   e->temp_cap = temp_buffer_cap(e->cfg.compression);
   e->max_records = cfg->max_batch_records ? cfg->max_batch_records : (1u << 20);
   if (e->max_records > kTagIndex) {  // record indices ride in 30-bit tags
@@ -723,8 +790,8 @@ int vn_flush(vn_engine* e, vn_flush_result* out) {
       t = vn_timing{};
       VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_counter, e->ev[0], e->ev[1]));
       VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_gauge, e->ev[1], e->ev[2]));
-      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_histo, e->ev[2], e->ev[3]));
-      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_set, e->ev[3], e->ev[4]));
+      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_set, e->ev[2], e->ev[3]));
+      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_histo, e->ev[3], e->ev[4]));
       VN_HIP_CHECK(hipEventElapsedTime(&t.ms_flush, e->ev[5], e->ev[6]));
       t.sort_passes_histo = e->rstat_h.launches;
       t.sort_passes_set = e->rstat_s.launches;

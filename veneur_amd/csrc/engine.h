@@ -62,6 +62,20 @@ struct vn_engine {
   hipStream_t st = nullptr;       // main stream (histos, flush, staging copies)
   hipStream_t st2 = nullptr;      // side stream: counters, gauges and sets overlap the histo path
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // replay stream: the exact replay of the keys under the threshold runs here while the hot
+  // keys' short prefix and remainder rounds run on st (st itself when timing is enabled)
+  hipStream_t st3 = nullptr;
+  hipEvent_t ev_fork3 = nullptr, ev_join3 = nullptr;
+  // hot-prefix stream: the hot keys' short replays run here while st gathers and sorts their
+  // remainders
+  hipStream_t st4 = nullptr;
+  hipEvent_t ev_join4 = nullptr;
+  // set segment merge held back (ingest_device): the grouped set records are merged once the
+  // histo path's remainder sort is done, so the long set kernel does not crowd it out
+  bool set_defer = false, set_pending = false;
+  uint32_t lpt = 3;              // longest-first order: bit 0 set merge, bit 1 replay (VN_LPT overrides)
+  uint64_t set_pending_n = 0;
+  const uint64_t* set_pending_R = nullptr;
   // stream + scratch the counter / gauge / set launchers use for the current call
   // (st2 normally; st when timing is enabled, so per-kernel durations are measured alone)
   hipStream_t side = nullptr;
@@ -114,6 +128,7 @@ struct vn_engine {
   uint32_t* h_err = nullptr;     // device error flags
   // exact (Go-incremental) replay state and batch split
   uint32_t exact_threshold = 32768;
+  uint32_t hot_prefix = 4096;    // a key past the threshold replays this many samples exactly
   uint32_t temp_cap = 42;        // estimateTempBuffer(compression)
   uint32_t* hseen = nullptr;     // samples seen this window per slot
   uint32_t* hpend = nullptr;     // pending temps per slot
@@ -124,12 +139,20 @@ struct vn_engine {
   uint32_t* h_hotcnt = nullptr;
   uint32_t* h_hotoff = nullptr;
   uint32_t* h_hotlist = nullptr;
+  uint32_t* h_coldflag = nullptr;  // per touched key: whole batch replayed exactly
+  uint32_t* h_coldlist = nullptr;
+  uint64_t* hA2 = nullptr;       // hot remainder sort ping-pong (As/Bs stay with the replay)
+  uint64_t* hB2 = nullptr;
+  uint64_t* h_lpt0 = nullptr;    // replay order of the keys under the threshold, longest first
+  uint64_t* h_lpt1 = nullptr;
+  double* h_csv = nullptr;       // pre-sorted pure chunks: means, weights (per record)
+  double* h_csw = nullptr;
   uint32_t* h_tl2 = nullptr;     // slots of hot keys
   uint32_t* h_ccnt = nullptr;    // per touched key: pure chunks to pre-sort
   uint32_t* h_coff = nullptr;    // scan of h_ccnt (touched + 1)
   double* h_tw = nullptr;        // per chunk (at its first record): Add-order weight sum
   // geometric remainder of hot keys (ingest_histo.hip)
-  uint64_t* h_geo = nullptr;     // piece boundaries b_0 = E, b_{i+1} = b_i + max(1, b_i / 10)
+  uint64_t* h_geo = nullptr;     // piece boundaries b_0 = hot_prefix, b_{i+1} = b_i + max(1, b_i / 10)
   uint32_t n_geo = 0;
   uint32_t* h_seen0 = nullptr;   // per touched key: window samples before this batch
   uint32_t* h_pcnt = nullptr;    // per touched key: remainder pieces in this batch
@@ -155,7 +178,9 @@ struct vn_engine {
   uint32_t* s_bt = nullptr;
   uint32_t* s_pos = nullptr;
   uint32_t* s_tl = nullptr;
-  uint32_t* s_cnt = nullptr;
+  uint32_t* s_cnt = nullptr;     // [0] touched set keys, [1] merge work counter
+  uint64_t* s_lpt0 = nullptr;    // set merge order, most records first
+  uint64_t* s_lpt1 = nullptr;
   uint32_t* s_start = nullptr;
   uint32_t* s_end = nullptr;
 
@@ -191,6 +216,8 @@ struct vn_engine {
   vn::ScanScratch ss;
   vn::RadixScratch rs2;           // side-stream scratch
   vn::ScanScratch ss2;
+  vn::RadixScratch rs3;           // replay-stream scratch (longest-first key order)
+  uint32_t side_cus = 0;          // CUs the side and replay streams may use (CU mask)
   vn::RadixScratch* side_rs = nullptr;
   vn::ScanScratch* side_ss = nullptr;
 

@@ -30,6 +30,9 @@ __device__ __forceinline__ double tag_weight(uint32_t tag, const double* impw) {
 struct ExactCtx {
   uint32_t nkeys;
   const uint32_t* keys;      // slot of each processed key
+  const uint32_t* order;     // replay only: key indices of this launch (nullptr: 0..nkeys-1)
+  uint32_t norder;           // replay grid when order is set
+  const uint64_t* order64;   // replay only: key index in the low 32 bits, longest first (norder)
   const uint32_t* start;     // per slot: first record of its segment (arrival order)
   const uint32_t* nex;       // per processed key: records to replay exactly (nullptr: none)
   const uint32_t* hot;       // per processed key: 1 -> merge pending temps after the exact part
@@ -62,6 +65,13 @@ struct ExactCtx {
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap);
 // max_chunks: upper bound on the pure chunks of the batch (grid of the chunk sorter)
 void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks);
+// the pure-chunk pre-sort alone, and the replay alone (over x.order when set)
+void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks);
+void histo_exact_replay(const ExactCtx& x, hipStream_t st);
+// replay list[0..n) longest first: sorts the order into buf0/buf1 (n each) on st and sets x
+// up for histo_exact_replay
+void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* buf0, uint64_t* buf1,
+                       RadixScratch& rs, hipStream_t st);
 // estimateTempBuffer (merging_digest.go:87-93)
 inline uint32_t temp_buffer_cap(double compression) {
   double c = compression < 20 ? 20 : (compression > 925 ? 925 : compression);

@@ -793,10 +793,9 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
 // ---- the replay: one 64-thread block (one wave) per key.  TPL = temps per lane of a chunk
 // (1 when estimateTempBuffer <= 64, i.e. delta <= ~150; 4 up to delta 1000).
 template <int TPL>
-__global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
+__device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const uint32_t k = blockIdx.x, lane = threadIdx.x;
-  if (k >= x.nkeys) return;
+  const uint32_t lane = threadIdx.x;
   const uint32_t capc = x.capc, tcap = x.tcap;
   const uint32_t TP = round64(tcap + 1);
   Lds L;
@@ -969,6 +968,35 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   }
 }
 
+// One wave per key: key index blockIdx.x, or the blockIdx.x-th of x.order / x.order64 (the
+// latter longest first, so the longest replays do not start last).
+template <int TPL>
+__global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
+  const uint32_t i = blockIdx.x;
+  const uint32_t k = x.order64 ? (uint32_t)x.order64[i] : x.order ? x.order[i] : i;
+  if (k < x.nkeys) replay_key<TPL>(x, k);
+}
+
+// longest-first order of the listed keys: (0xFFFFF - min(nex, 0xFFFFF)) << 32 | key index
+__global__ void k_exact_lpt_keys(uint32_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ nex,
+                                 uint64_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = list[i], c = min(nex[k], 0xFFFFFu);
+  out[i] = ((uint64_t)(0xFFFFFu - c) << 32) | k;
+}
+
+void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* buf0, uint64_t* buf1,
+                       RadixScratch& rs, hipStream_t st) {
+  x.order = list;
+  x.norder = n;
+  if (!n) return;
+  hipLaunchKernelGGL(k_exact_lpt_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, list, x.nex, buf0);
+  RadixPass passes[4];
+  const int np = make_passes(passes, false, 32, 20);
+  x.order64 = radix_sort(buf0, nullptr, buf1, nullptr, n, passes, np, rs, st, nullptr) ? buf1 : buf0;
+}
+
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap) {
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = std::max(capc + TP + 1, 320u);
   uint32_t levels = 1;
@@ -987,21 +1015,31 @@ extern "C" int vn_prof_exact_read(unsigned long long* out16, int reset) {
 }
 #endif
 
+void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks) {
+  if (!x.nkeys || !x.nex) return;
+  // sort every pure chunk in parallel first
+  hipLaunchKernelGGL(k_exact_chunk_count, dim3(blocks_for(x.nkeys, 256)), dim3(256), 0, st, x);
+  scan_exclusive_u32(x.ccnt, x.coff, x.nkeys, *ss, st);
+  if (max_chunks)
+    hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)max_chunks), dim3(64),
+                       sizeof(double) * 4 * ((x.tcap + 1 + 63u) & ~63u), st, x);
+}
+
+void histo_exact_replay(const ExactCtx& x, hipStream_t st) {
+  const uint32_t grid = (x.order || x.order64) ? x.norder : x.nkeys;
+  if (!grid) return;
+  if (x.tcap > 64 * kMaxTempPerLane) throw std::runtime_error("temp buffer larger than the exact kernel supports");
+  size_t sm = exact_smem_bytes(x.capc, x.tcap);
+  if (sm > 160 * 1024) throw std::runtime_error("compression too large for the exact replay's LDS budget");
+  if (x.tcap <= 64) hipLaunchKernelGGL(k_histo_exact<1>, dim3(grid), dim3(64), sm, st, x);
+  else hipLaunchKernelGGL(k_histo_exact<kMaxTempPerLane>, dim3(grid), dim3(64), sm, st, x);
+}
+
 void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks) {
   if (!x.nkeys) return;
   if (x.tcap > 64 * kMaxTempPerLane) throw std::runtime_error("temp buffer larger than the exact kernel supports");
-  if (x.nex) {
-    // sort every pure chunk in parallel first
-    hipLaunchKernelGGL(k_exact_chunk_count, dim3(blocks_for(x.nkeys, 256)), dim3(256), 0, st, x);
-    scan_exclusive_u32(x.ccnt, x.coff, x.nkeys, *ss, st);
-    if (max_chunks)
-      hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)max_chunks), dim3(64),
-                         sizeof(double) * 4 * ((x.tcap + 1 + 63u) & ~63u), st, x);
-  }
-  size_t sm = exact_smem_bytes(x.capc, x.tcap);
-  if (sm > 160 * 1024) throw std::runtime_error("compression too large for the exact replay's LDS budget");
-  if (x.tcap <= 64) hipLaunchKernelGGL(k_histo_exact<1>, dim3(x.nkeys), dim3(64), sm, st, x);
-  else hipLaunchKernelGGL(k_histo_exact<kMaxTempPerLane>, dim3(x.nkeys), dim3(64), sm, st, x);
+  histo_exact_presort(x, st, ss, max_chunks);
+  histo_exact_replay(x, st);
 }
 
 }  // namespace vn

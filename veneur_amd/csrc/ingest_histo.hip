@@ -232,9 +232,15 @@ __global__ __launch_bounds__(kBlock) void k_chunk_kin(HistoCtx x) {
 constexpr uint32_t kCW = 2048;        // elements per window
 constexpr uint32_t kCWL = kCW / 64;   // window elements per lane (registers) = groups per window
 constexpr uint32_t kRing = 6;         // LDS ring slots (96 KiB)
-constexpr uint32_t kLoaders = 3;
+constexpr uint32_t kLoaders = 7;      // one CU streams the k array: 7 loader waves x 2 windows in flight
+constexpr uint32_t kChainThreads = 64 * (kLoaders + 1);
 constexpr uint32_t kSpinCap = 1u << 24;
 
+__device__ __forceinline__ double readlane_d(double v, uint32_t i) {  // i wave-uniform
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, i), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), i);
+  return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -242,7 +248,7 @@ __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__global__ __launch_bounds__(256) void k_chain(HistoCtx x) {
+__global__ __launch_bounds__(kChainThreads) void k_chain(HistoCtx x) {
   __shared__ double s_win[kRing][kCW];
   __shared__ double s_last[kRing][kCWL];
   __shared__ uint32_t s_st[kMaxCent + 1];
@@ -313,6 +319,9 @@ __global__ __launch_bounds__(256) void k_chain(HistoCtx x) {
     uint32_t cw = 0;          // window the walk is in
     double prev_last = 0.0;   // last k of window cw - 1
     acquire(0);
+    // the window's group-last k values stay in a register (lane q < kCWL holds group q), so a
+    // step costs one LDS probe (the group) plus ballots and readlanes
+    double gl = s_last[0][lane < kCWL ? lane : 0];
     uint32_t nc = 0, pos = 0;
     double base = index_estimate(x.delta, 0.0);
     while (ok) {
@@ -327,16 +336,16 @@ __global__ __launch_bounds__(256) void k_chain(HistoCtx x) {
       bool found = false;
       for (;;) {
         while (from >= (cw + 1) * kCW) {  // the start lies in a later window
-          prev_last = s_win[cw % kRing][kCW - 1];
+          prev_last = readlane_d(gl, kCWL - 1);
           cw++;
           if (lane == 0) lds_st(&s_done, cw);  // release the window left behind
           acquire(cw);
           if (!ok) break;
+          gl = s_last[cw % kRing][lane < kCWL ? lane : 0];
         }
         if (!ok) break;
         const uint32_t slot = cw % kRing;
         const uint32_t wb = cw * kCW, q0 = (from - wb) >> 6;
-        const double gl = s_last[slot][lane < kCWL ? lane : 0];
         const uint64_t mq = __ballot(lane >= q0 && lane < kCWL && dsub(gl, base) > 1.0);
         if (mq == 0) {
           if (wb + kCW >= n) break;  // no later element qualifies: the chain ends
@@ -349,8 +358,7 @@ __global__ __launch_bounds__(256) void k_chain(HistoCtx x) {
         const uint64_t m = __ballot(idx >= from && idx < n && dsub(kv, base) > 1.0);
         if (m == 0) break;  // only padding past n qualified: the chain ends
         const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;
-        const double kprev = __shfl(kv, f ? (int)f - 1 : 0, 64);
-        base = f ? kprev : (q ? s_last[slot][q - 1] : prev_last);
+        base = f ? readlane_d(kv, f - 1) : (q ? readlane_d(gl, q - 1) : prev_last);
         pos = wb + 64 * q + f;
         found = true;
         break;
@@ -371,7 +379,7 @@ __global__ __launch_bounds__(256) void k_chain(HistoCtx x) {
     const uint8_t nb = x.hcur[s] ^ 1;
     double* cm = nb ? x.cm1 : x.cm0;
     double* cwn = nb ? x.cw1 : x.cw0;
-    for (uint32_t ci = t; ci < nc; ci += 256) {
+    for (uint32_t ci = t; ci < nc; ci += kChainThreads) {
       uint32_t a = s_st[ci], b = s_st[ci + 1];
       double mean = from_ordered_bits(x.A[lo + a]);
       double W = x.w[lo + a];
@@ -392,7 +400,7 @@ __global__ __launch_bounds__(256) void k_chain(HistoCtx x) {
     }
     return;
   }
-  for (uint32_t ci = t; ci < nc; ci += 256) {
+  for (uint32_t ci = t; ci < nc; ci += kChainThreads) {
     x.starts[(uint64_t)k * capc + ci] = s_st[ci];
     x.acc_xw[(uint64_t)k * capc + ci] = 0.0;
     x.acc_w[(uint64_t)k * capc + ci] = 0.0;
@@ -499,25 +507,32 @@ __global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, 
 }
 
 // how much of each key's batch is replayed exactly, and how much goes to the batch merge
+// Per touched key: how many of its batch samples the exact replay takes.  A key whose window
+// stays within E samples is replayed whole (bit-exact); a key that passes E is not bit-exact
+// anyway, so only its first P (hot_prefix) window samples replay exactly and the rest joins the
+// geometric remainder -- the replay of a hot key is short and its remainder rounds can start
+// while the long replays of the keys under E still run.
 __global__ void k_histo_plan(uint32_t ntouched, const uint32_t* __restrict__ tl, const uint32_t* __restrict__ start,
-                             const uint32_t* __restrict__ end, uint32_t* __restrict__ hseen, uint32_t E,
-                             uint32_t* __restrict__ ex, uint32_t* __restrict__ hotflag, uint32_t* __restrict__ hotcnt,
-                             uint32_t* __restrict__ seen0) {
+                             const uint32_t* __restrict__ end, uint32_t* __restrict__ hseen, uint32_t E, uint32_t P,
+                             uint32_t* __restrict__ ex, uint32_t* __restrict__ hotflag, uint32_t* __restrict__ coldflag,
+                             uint32_t* __restrict__ hotcnt, uint32_t* __restrict__ seen0) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= ntouched) return;
   uint32_t s = tl[k];
   uint32_t nk = end[s] - start[s];
   uint32_t seen = hseen[s];
-  uint32_t e = seen >= E ? 0u : min(nk, E - seen);
+  const bool hot = (uint64_t)seen + nk > E;
+  uint32_t e = !hot ? nk : (seen >= P ? 0u : min(nk, P - seen));
   ex[k] = e;
   hotcnt[k] = nk - e;
-  hotflag[k] = nk > e;
+  hotflag[k] = hot;
+  coldflag[k] = !hot;
   seen0[k] = seen;
   hseen[s] = seen + nk;
 }
 
-// ---- geometric remainder: a hot key's samples beyond the exact threshold are merged in
-// pieces cut at window positions b_0 = E, b_{i+1} = b_i + max(1, b_i / 10) (and at batch
+// ---- geometric remainder: a hot key's samples beyond its exact prefix are merged in
+// pieces cut at window positions b_0 = P, b_{i+1} = b_i + max(1, b_i / 10) (and at batch
 // edges): each piece is one mergeAllTemps of (current centroids + the piece's samples).
 // tools/tdigest_study.py measured this schedule at <= 4.2e-4 rank error against the
 // reference's 42-sample incremental merge for keys of 40k..4M samples (one merge of the
@@ -722,32 +737,71 @@ __global__ __launch_bounds__(kBlock) void k_round_merge(uint32_t capc, const uin
     }
   }
 }
-void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate,
-                   const double* impw) {
-  if (!n) return;
+HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate) {
+  HistoGroups g{};
+  if (!n) return g;
   hipStream_t st = e->st;
   const uint32_t caph = e->cap[VN_HISTO];
-  // ---- 1. group by key, arrival order kept (stable radix by slot)
+  // ---- 1. group by key, arrival order kept (stable radix by slot); nothing here waits on
+  // the host, so the caller can queue other streams' work before histo_process syncs
   hipLaunchKernelGGL(k_histo_keys_raw, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, val, rate, e->hA0, e->hB0,
                      e->h_bt, e->htouch);
   RadixPass spass[4];
   int nsp = 0;
   nsp = make_passes(spass, true, 32, e->slot_bits[VN_HISTO]);
   bool fl = radix_sort(e->hA0, e->hB0, e->hA1, e->hB1, n, spass, nsp, e->rs, st, e->timing ? &e->rstat_h : nullptr);
-  uint64_t* As = fl ? e->hA1 : e->hA0;
-  uint64_t* Bs = fl ? e->hB1 : e->hB0;
-  uint64_t* Ao = fl ? e->hA0 : e->hA1;
-  uint64_t* Bo = fl ? e->hB0 : e->hB1;
-  hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, Bs, e->h_start, e->h_end);
+  g.As = fl ? e->hA1 : e->hA0;
+  g.Bs = fl ? e->hB1 : e->hB0;
+  g.Ao = fl ? e->hA0 : e->hA1;
+  g.Bo = fl ? e->hB0 : e->hB1;
+  hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, g.Bs, e->h_start, e->h_end);
   compact_flags(e->h_bt, e->h_pos, e->h_tl, e->h_cnt, caph, e->ss, st);
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt, e->h_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  return g;
+}
+
+void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate,
+                   const double* impw) {
+  const HistoGroups g = histo_group(e, n, slot, val, rate);
+  histo_process(e, n, g, impw);
+}
+
+void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double* impw) {
+  if (!n) return;
+  hipStream_t st = e->st;
+  uint64_t* const As = g.As;
+  uint64_t* const Bs = g.Bs;
+  uint64_t* const Ao = g.Ao;
+  uint64_t* const Bo = g.Bo;
   VN_HIP_CHECK(hipStreamSynchronize(st));
   const uint32_t ntouched = e->hf_cnt[0];
   if (!ntouched) return;
 
-  // ---- 2. exact replay of MergingDigest.Add for keys under the threshold
+  // ---- 2. plan: exact part of every key; hot remainders cut into geometric pieces
   hipLaunchKernelGGL(k_histo_plan, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_start,
-                     e->h_end, e->hseen, e->exact_threshold, e->h_ex, e->h_hotflag, e->h_hotcnt, e->h_seen0);
+                     e->h_end, e->hseen, e->exact_threshold, e->hot_prefix, e->h_ex, e->h_hotflag, e->h_coldflag,
+                     e->h_hotcnt, e->h_seen0);
+  compact_flags(e->h_hotflag, e->h_pos, e->h_hotlist, e->h_cnt + 1, ntouched, e->ss, st);
+  compact_flags(e->h_coldflag, e->h_pos, e->h_coldlist, e->h_cnt + 6, ntouched, e->ss, st);
+  scan_exclusive_u32(e->h_hotcnt, e->h_hotoff, ntouched, e->ss, st);
+  VN_HIP_CHECK(hipMemsetAsync(e->h_cnt + 4, 0, sizeof(uint32_t), st));
+  hipLaunchKernelGGL(k_histo_pieces, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_ex,
+                     e->h_hotcnt, e->h_seen0, e->h_geo, e->n_geo, e->h_pcnt, e->h_pi0, e->h_cnt + 4);
+  scan_exclusive_u32(e->h_pcnt, e->h_pbase, ntouched, e->ss, st);
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 1, e->h_cnt + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 2, e->h_hotoff + ntouched, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 3, e->h_pbase + ntouched, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 4, e->h_cnt + 4, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 5, e->h_cnt + 6, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  const uint32_t nhot = e->hf_cnt[1];
+  const uint64_t nhotrec = e->hf_cnt[2];
+  const uint32_t npieces = e->hf_cnt[3];
+  const uint32_t maxp = e->hf_cnt[4];
+  const uint32_t ncold = e->hf_cnt[5];
+
+  // ---- 3. exact replay of MergingDigest.Add (histo_exact.hip): every pure chunk pre-sorted,
+  // then the keys under the threshold on the replay stream, the hot keys' prefixes here
   ExactCtx xc{};
   xc.nkeys = ntouched;
   xc.keys = e->h_tl;
@@ -774,28 +828,31 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   xc.flush_mode = 0;
   xc.ccnt = e->h_ccnt;
   xc.coff = e->h_coff;
-  xc.csv = e->h_wk;  // free until the hot-key batch merge below reuses them
-  xc.csw = e->h_w;
+  xc.csv = e->h_csv;
+  xc.csw = e->h_csw;
   xc.ctw = e->h_tw;
-  launch_histo_exact(xc, st, &e->ss, n / e->temp_cap + 1);
+  histo_exact_presort(xc, st, &e->ss, n / e->temp_cap + 1);
+  // replays on their own streams: the hot keys' prefixes on st4 (short) while st gathers and
+  // sorts the hot remainders; then the keys under the threshold on st3 (long) -- started after
+  // the sort, whose passes would otherwise wait for CUs behind 100k+ replay workgroups -- and
+  // the held-back set merge on the side stream
+  const bool fork = nhot && !e->timing;
+  if (fork) {
+    VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
+    VN_HIP_CHECK(hipStreamWaitEvent(e->st4, e->ev_fork3, 0));
+  } else {
+    xc.order = e->h_coldlist;
+    xc.norder = ncold;
+    histo_exact_replay(xc, st);
+  }
+  xc.order = e->h_hotlist;
+  xc.norder = nhot;
+  histo_exact_replay(xc, fork ? e->st4 : st);
+  if (fork) VN_HIP_CHECK(hipEventRecord(e->ev_join4, e->st4));
 
-  // ---- 3. hot remainders: geometric pieces, merged round by round
-  compact_flags(e->h_hotflag, e->h_pos, e->h_hotlist, e->h_cnt + 1, ntouched, e->ss, st);
-  scan_exclusive_u32(e->h_hotcnt, e->h_hotoff, ntouched, e->ss, st);
-  VN_HIP_CHECK(hipMemsetAsync(e->h_cnt + 4, 0, sizeof(uint32_t), st));
-  hipLaunchKernelGGL(k_histo_pieces, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_ex,
-                     e->h_hotcnt, e->h_seen0, e->h_geo, e->n_geo, e->h_pcnt, e->h_pi0, e->h_cnt + 4);
-  scan_exclusive_u32(e->h_pcnt, e->h_pbase, ntouched, e->ss, st);
-  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 1, e->h_cnt + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 2, e->h_hotoff + ntouched, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 3, e->h_pbase + ntouched, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 4, e->h_cnt + 4, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipStreamSynchronize(st));
-  const uint32_t nhot = e->hf_cnt[1];
-  const uint64_t nhotrec = e->hf_cnt[2];
-  const uint32_t npieces = e->hf_cnt[3];
-  const uint32_t maxp = e->hf_cnt[4];
+  // ---- 4. hot remainders: geometric pieces, merged round by round (As/Bs stay with the replay)
   if (nhot == 0 || nhotrec == 0) {
+    set_finish(e);
     hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
     return;
   }
@@ -809,13 +866,28 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   int pbits = 1;
   while (pbits < 32 && (1ull << pbits) < npieces) pbits++;
   np += make_passes(passes + np, true, 32, pbits);
-  const bool fl2 = radix_sort(Ao, Bo, As, Bs, nhotrec, passes, np, e->rs, st, e->timing ? &e->rstat_h : nullptr);
-  const uint64_t* PA = fl2 ? As : Ao;  // sorted pieces
-  const uint64_t* PB = fl2 ? Bs : Bo;
-  uint64_t* MA = fl2 ? Ao : As;        // per-round merged segments
-  uint64_t* MB = fl2 ? Bo : Bs;
+  const bool fl2 = radix_sort(Ao, Bo, e->hA2, e->hB2, nhotrec, passes, np, e->rs, st,
+                              e->timing ? &e->rstat_h : nullptr);
+  const uint64_t* PA = fl2 ? e->hA2 : Ao;  // sorted pieces
+  const uint64_t* PB = fl2 ? e->hB2 : Bo;
+  uint64_t* MA = fl2 ? Ao : e->hA2;        // per-round merged segments
+  uint64_t* MB = fl2 ? Bo : e->hB2;
   hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(nhotrec, 256)), dim3(256), 0, st, nhotrec, PB, e->p_start,
                      e->p_end);
+  if (fork) {
+    VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
+    VN_HIP_CHECK(hipStreamWaitEvent(e->st3, e->ev_fork3, 0));
+    // keys longest first
+    histo_exact_order(xc, e->h_coldlist, ncold, e->h_lpt0, e->h_lpt1, e->rs3, e->st3);
+    if (!(e->lpt & 2)) xc.order64 = nullptr;
+    histo_exact_replay(xc, e->st3);
+    VN_HIP_CHECK(hipEventRecord(e->ev_join3, e->st3));
+    if (e->set_pending) {
+      VN_HIP_CHECK(hipStreamWaitEvent(e->side, e->ev_fork3, 0));
+      set_finish(e);
+    }
+    VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_join4, 0));  // the rounds start from the prefixes' state
+  }
 
   const uint64_t maxch = (nhotrec + (uint64_t)nhot * e->cap_cent) / kHTile + nhot + 1;
   if (maxch > e->h_max_chunks || nhotrec + (uint64_t)nhot * e->cap_cent > e->h_sort_cap)
@@ -861,10 +933,11 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
     hipLaunchKernelGGL(k_chunk_prep, dim3(maxch), dim3(kBlock), 0, st, x);
     hipLaunchKernelGGL(k_seg_scan, dim3(nhot), dim3(kBlock), 0, st, x);
     hipLaunchKernelGGL(k_chunk_kin, dim3(maxch), dim3(kBlock), 0, st, x);
-    hipLaunchKernelGGL(k_chain, dim3(nhot), dim3(256), 0, st, x);
+    hipLaunchKernelGGL(k_chain, dim3(nhot), dim3(kChainThreads), 0, st, x);
     hipLaunchKernelGGL(k_chunk_cent, dim3(maxch), dim3(kBlock), 0, st, x);
     hipLaunchKernelGGL(k_finalize, dim3(nhot), dim3(kBlock), 0, st, x);
   }
+  if (fork) VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_join3, 0));
   hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
 }
 

@@ -28,7 +28,8 @@
 namespace vn {
 
 struct SetCtx {
-  uint32_t ntouched;
+  const uint32_t* cnt;  // touched keys (device count)
+  const uint64_t* order;  // slot of the i-th key to merge (low 32 bits), most records first
   const uint32_t* tl;
   const uint32_t* start;
   const uint32_t* end;
@@ -99,7 +100,7 @@ __device__ __forceinline__ void hash_insert_par(uint32_t* h, uint32_t c) {
   }
 }
 
-__global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
+__device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot) {
   __shared__ uint32_t U[kArenaWords];   // sparse list (sorted codes) or dense registers (u32 each)
   __shared__ uint32_t s_hash[kHashSlots];
   __shared__ uint32_t s_first[kHashSlots];  // lowest lane of the current group holding the entry
@@ -109,8 +110,7 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
   __shared__ uint32_t s_pos, s_trig, s_tc, s_lc, s_mode, s_b, s_nz;
   __shared__ uint32_t s_filled, s_tfull, s_pstar, s_newfill, s_min;
 
-  const uint32_t k = blockIdx.x, t = threadIdx.x;
-  const uint32_t slot = x.tl[k];
+  const uint32_t t = threadIdx.x;
   const uint32_t lo = x.start[slot], n = x.end[slot] - lo;
   const uint64_t* R = x.R + lo;
   uint32_t* arena = x.arena + (uint64_t)slot * kArenaWords;
@@ -313,9 +313,32 @@ __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
   }
 }
 
-__global__ void k_set_clear_flags(uint32_t n, const uint32_t* __restrict__ list, uint32_t* __restrict__ flags) {
+// One workgroup per touched key; with an order, workgroup i takes the key with the i-th most
+// records (longest-processing-time first: the biggest keys do not start last).
+__global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
+  const uint32_t i = blockIdx.x;
+  if (i >= *x.cnt) return;
+  set_segment(x, x.order ? (uint32_t)x.order[i] : x.tl[i]);
+}
+
+// longest-first order: key = (0xFFFFF - min(records, 0xFFFFF)) << 32 | slot; untouched -> ~0
+__global__ void k_set_lpt_keys(uint32_t n, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ tl,
+                               const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
+                               uint64_t* __restrict__ out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  if (k >= *cnt) {
+    out[k] = ~0ull;
+    return;
+  }
+  const uint32_t s = tl[k], c = min(end[s] - start[s], 0xFFFFFu);
+  out[k] = ((uint64_t)(0xFFFFFu - c) << 32) | s;
+}
+
+__global__ void k_set_clear_flags(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ list,
+                                  uint32_t* __restrict__ flags) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n) flags[list[k]] = 0;
+  if (k < *cnt) flags[list[k]] = 0;
 }
 
 void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t* off, const uint8_t* bytes,
@@ -333,16 +356,38 @@ void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t*
   const uint64_t* R = fl ? e->sR1 : e->sR0;
   hipLaunchKernelGGL(k_set_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, R, e->s_start, e->s_end);
   compact_flags(e->s_bt, e->s_pos, e->s_tl, e->s_cnt, caps, *e->side_ss, st);
-  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 8, e->s_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipStreamSynchronize(st));
-  const uint32_t ntouched = e->hf_cnt[8];
-  if (!ntouched) return;
+  if (e->set_defer) {
+    e->set_pending = true;
+    e->set_pending_n = n;
+    e->set_pending_R = R;
+    return;
+  }
+  e->set_pending_n = n;
+  e->set_pending_R = R;
+  e->set_pending = true;
+  set_finish(e);
+}
+
+void set_finish(vn_engine* e) {
+  if (!e->set_pending) return;
+  e->set_pending = false;
+  hipStream_t st = e->side;
+  // no host round trip: the touched-key count stays on the device and the grid is its upper
+  // bound, so the whole set path is queued before the histogram path blocks the host
+  const uint32_t nk = (uint32_t)std::min<uint64_t>(e->cap[VN_SET], e->set_pending_n);  // >= touched keys
+  hipLaunchKernelGGL(k_set_lpt_keys, dim3(blocks_for(nk, 256)), dim3(256), 0, st, nk, e->s_cnt, e->s_tl, e->s_start,
+                     e->s_end, e->s_lpt0);
+  RadixPass passes[4];
+  const int np = make_passes(passes, false, 32, 20);
+  const bool fl = radix_sort(e->s_lpt0, nullptr, e->s_lpt1, nullptr, nk, passes, np, *e->side_rs, st, nullptr);
+  const uint32_t grid = nk;  // >= touched keys
   SetCtx x;
-  x.ntouched = ntouched;
+  x.cnt = e->s_cnt;
+  x.order = (e->lpt & 1) ? (fl ? e->s_lpt1 : e->s_lpt0) : nullptr;
   x.tl = e->s_tl;
   x.start = e->s_start;
   x.end = e->s_end;
-  x.R = R;
+  x.R = e->set_pending_R;
   x.mode = e->smode;
   x.base = e->sbase;
   x.nz = e->snz;
@@ -353,8 +398,8 @@ void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t*
   x.tmp = e->stmp;
   x.arena = e->sarena;
   x.err = e->h_err;
-  hipLaunchKernelGGL(k_set_segments, dim3(ntouched), dim3(kBlock), 0, st, x);
-  hipLaunchKernelGGL(k_set_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->s_tl, e->s_bt);
+  hipLaunchKernelGGL(k_set_segments, dim3(grid), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_set_clear_flags, dim3(blocks_for(nk, 256)), dim3(256), 0, st, e->s_cnt, e->s_tl, e->s_bt);
 }
 
 }  // namespace vn

@@ -32,9 +32,19 @@ void import_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const int64
 void ingest_gauges(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val);
 // Histo.Sample (346-356) + MergingDigest.Add/mergeAllTemps (merging_digest.go:97-236)
 // rate == nullptr: the records are imported centroids (Histo.Combine) with weights impw
+// the histo ingest in two halves: group (sort by key, queue the segment-count read-back) and
+// process (wait for the count, replay, remainder rounds); ingest_histos runs both
+struct HistoGroups {
+  uint64_t *As, *Bs, *Ao, *Bo;  // key-grouped records and the spare pair
+};
+HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate);
+void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double* impw = nullptr);
 void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate,
                    const double* impw = nullptr);
 // Set.Sample (265-267) -> Sketch.Insert (hyperloglog.go:186-200)
+// queue the set segment merge held back by ingest_sets while e->set_defer is on (no-op
+// otherwise); runs on e->side
+void set_finish(vn_engine* e);
 void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t* off, const uint8_t* bytes,
                  const uint64_t* hashes);
 // mergeAllTemps for the given (distinct) histo slots, device list
