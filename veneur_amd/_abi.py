@@ -33,7 +33,7 @@ class Config(C.Structure):
                 ("n_percentiles", C.c_uint32), ("percentiles", C.c_double * VN_MAX_PERCENTILES),
                 ("max_batch_records", C.c_uint64), ("max_batch_member_bytes", C.c_uint64),
                 ("histo_exact_threshold", C.c_uint32),
-                ("histo_hot_prefix", C.c_uint32)]
+                ("histo_hot_prefix", C.c_uint32), ("histo_piece_growth", C.c_uint32)]
 
 
 class Batch(C.Structure):

@@ -138,7 +138,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_bt, ch); dzero(e->h_bt, ch, st);
   dalloc(e->h_pos, (size_t)ch + 1);
   dalloc(e->h_tl, ch);
-  dalloc(e->h_cnt, 8);
+  dalloc(e->h_cnt, 16);
   const uint64_t touch_max = ch ? std::min<uint64_t>(ch, R) : 0;
   e->h_sort_cap = ch ? R + touch_max * capc : 0;
   dalloc(e->hA0, e->h_sort_cap); dalloc(e->hB0, e->h_sort_cap);
@@ -170,6 +170,9 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_hotlist, touch_max);
   dalloc(e->h_coldflag, touch_max);
   dalloc(e->h_coldlist, touch_max);
+  dalloc(e->h_vhflag, touch_max);
+  dalloc(e->h_warmflag, touch_max);
+  dalloc(e->h_warmlist, touch_max);
   dalloc(e->hA2, e->h_sort_cap); dalloc(e->hB2, e->h_sort_cap);
   dalloc(e->h_csv, ch ? R : 0); dalloc(e->h_csw, ch ? R : 0);
   dalloc(e->h_lpt0, touch_max); dalloc(e->h_lpt1, touch_max);
@@ -191,7 +194,8 @@ void create_impl(vn_engine* e) {
   {
     // piece boundaries of the geometric remainder (see ingest_histo.hip)
     std::vector<uint64_t> geo;
-    for (uint64_t b = e->hot_prefix; geo.size() < 255 && b < (1ull << 40); b += std::max<uint64_t>(1, b / 10))
+    for (uint64_t b = e->hot_prefix; geo.size() < 255 && b < (1ull << 40);
+         b += std::max<uint64_t>(1, b * e->piece_growth / 100))
       geo.push_back(b);
     e->n_geo = (uint32_t)geo.size();
     dalloc(e->h_geo, geo.size());
@@ -358,7 +362,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
   dfree(e->hseen); dfree(e->hpend); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
-  dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw);
+  dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw);
   dfree(e->h_lpt0); dfree(e->h_lpt1); dfree(e->s_lpt0); dfree(e->s_lpt1);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);
   dfree(e->h_geo); dfree(e->h_seen0); dfree(e->h_pcnt); dfree(e->h_pi0); dfree(e->h_pbase); dfree(e->p_start);
@@ -594,6 +598,7 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
   e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 32768u;
   if (const char* v = std::getenv("VN_LPT")) e->lpt = (uint32_t)std::atoi(v);
   e->hot_prefix = std::min(e->exact_threshold, cfg->histo_hot_prefix ? cfg->histo_hot_prefix : 4096u);
+  e->piece_growth = cfg->histo_piece_growth ? std::min(cfg->histo_piece_growth, 1000u) : 25u;
   e->temp_cap = temp_buffer_cap(e->cfg.compression);
   e->max_records = cfg->max_batch_records ? cfg->max_batch_records : (1u << 20);
   if (e->max_records > kTagIndex) {  // record indices ride in 30-bit tags

@@ -107,7 +107,7 @@ struct vn_engine {
   uint32_t* h_bt = nullptr;      // batch-touched flags
   uint32_t* h_pos = nullptr;     // scan of flags (cap+1)
   uint32_t* h_tl = nullptr;      // touched list
-  uint32_t* h_cnt = nullptr;     // device counters [8]
+  uint32_t* h_cnt = nullptr;     // device counters [16]
   uint64_t *hA0 = nullptr, *hB0 = nullptr, *hA1 = nullptr, *hB1 = nullptr;
   uint64_t h_sort_cap = 0;
   double* h_w = nullptr;         // per record weight
@@ -129,6 +129,7 @@ struct vn_engine {
   // exact (Go-incremental) replay state and batch split
   uint32_t exact_threshold = 32768;
   uint32_t hot_prefix = 4096;    // a key past the threshold replays this many samples exactly
+  uint32_t piece_growth = 25;    // remainder piece size, percent of the window samples before it
   uint32_t temp_cap = 42;        // estimateTempBuffer(compression)
   uint32_t* hseen = nullptr;     // samples seen this window per slot
   uint32_t* hpend = nullptr;     // pending temps per slot
@@ -139,8 +140,11 @@ struct vn_engine {
   uint32_t* h_hotcnt = nullptr;
   uint32_t* h_hotoff = nullptr;
   uint32_t* h_hotlist = nullptr;
-  uint32_t* h_coldflag = nullptr;  // per touched key: whole batch replayed exactly
+  uint32_t* h_coldflag = nullptr;  // per touched key: replayed on the replay stream (cold / warm)
   uint32_t* h_coldlist = nullptr;
+  uint32_t* h_vhflag = nullptr;    // hot: short exact prefix, rounds beside the replay (-> h_hotlist)
+  uint32_t* h_warmflag = nullptr;  // warm: exact prefix of E, rounds after the replay
+  uint32_t* h_warmlist = nullptr;
   uint64_t* hA2 = nullptr;       // hot remainder sort ping-pong (As/Bs stay with the replay)
   uint64_t* hB2 = nullptr;
   uint64_t* h_lpt0 = nullptr;    // replay order of the keys under the threshold, longest first

@@ -571,6 +571,9 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
     mono &= !(j >= 1 && j < m && kv[r] < prev);
   }
   mono = __all(mono);
+#ifdef VN_CHAIN_WALK
+  mono = false;
+#endif
   PROF_T(c1);
   PROF_ADD(9, p2, c1);
   uint32_t nc = 0;

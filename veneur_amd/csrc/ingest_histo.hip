@@ -506,37 +506,51 @@ __global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, 
   htouch[s] = 1;
 }
 
-// how much of each key's batch is replayed exactly, and how much goes to the batch merge
-// Per touched key: how many of its batch samples the exact replay takes.  A key whose window
-// stays within E samples is replayed whole (bit-exact); a key that passes E is not bit-exact
-// anyway, so only its first P (hot_prefix) window samples replay exactly and the rest joins the
-// geometric remainder -- the replay of a hot key is short and its remainder rounds can start
-// while the long replays of the keys under E still run.
+// Per touched key: how many of its batch samples the exact replay takes, by the key's window
+// count after this batch, tot:
+//   cold  tot <= E            the whole batch replays exactly (bit-exact);
+//   warm  E < tot <= W*E      the first E window samples replay exactly (with the cold keys),
+//                             the rest joins the geometric remainder after that replay;
+//   hot   tot > W*E           not bit-exact anyway and long: only the first P (hot_prefix)
+//                             window samples replay exactly, on their own stream, so the hot
+//                             remainder rounds run beside the long replays of the cold keys.
+// (A key past E in an earlier batch has nothing left to replay: it joins the hot rounds.)
+// Warm keys keep the long exact prefix because a remainder that is small next to it changes
+// the quantiles least: keys just above E showed up to 5e-3 rank error at p50 with P = 4096
+// and none with P = E (tools/tdigest_study.py, 8 seeds); above W*E = 4E both stay <= 7e-4.
+constexpr uint32_t kWarmFactor = 4;
 __global__ void k_histo_plan(uint32_t ntouched, const uint32_t* __restrict__ tl, const uint32_t* __restrict__ start,
                              const uint32_t* __restrict__ end, uint32_t* __restrict__ hseen, uint32_t E, uint32_t P,
-                             uint32_t* __restrict__ ex, uint32_t* __restrict__ hotflag, uint32_t* __restrict__ coldflag,
-                             uint32_t* __restrict__ hotcnt, uint32_t* __restrict__ seen0) {
+                             uint32_t* __restrict__ ex, uint32_t* __restrict__ remflag,
+                             uint32_t* __restrict__ replayflag, uint32_t* __restrict__ hotflag,
+                             uint32_t* __restrict__ warmflag, uint32_t* __restrict__ hotcnt,
+                             uint32_t* __restrict__ seen0) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= ntouched) return;
   uint32_t s = tl[k];
   uint32_t nk = end[s] - start[s];
   uint32_t seen = hseen[s];
-  const bool hot = (uint64_t)seen + nk > E;
-  uint32_t e = !hot ? nk : (seen >= P ? 0u : min(nk, P - seen));
+  const uint64_t tot = (uint64_t)seen + nk;
+  const bool cold = tot <= E;
+  const bool warm = !cold && seen < E && tot <= (uint64_t)kWarmFactor * E;
+  const uint32_t e = cold ? nk : warm ? E - seen : (seen >= P ? 0u : min(nk, P - seen));
   ex[k] = e;
   hotcnt[k] = nk - e;
-  hotflag[k] = hot;
-  coldflag[k] = !hot;
+  remflag[k] = !cold;              // merge the pending temps after the exact part
+  replayflag[k] = cold || warm;    // replayed on the replay stream
+  hotflag[k] = !cold && !warm;     // prefix on the hot-prefix stream, rounds beside the replay
+  warmflag[k] = warm;              // rounds after the replay
   seen0[k] = seen;
   hseen[s] = seen + nk;
 }
 
 // ---- geometric remainder: a hot key's samples beyond its exact prefix are merged in
-// pieces cut at window positions b_0 = P, b_{i+1} = b_i + max(1, b_i / 10) (and at batch
+// pieces cut at window positions b_0 = P, b_{i+1} = b_i + max(1, b_i * g / 100) (and at batch
 // edges): each piece is one mergeAllTemps of (current centroids + the piece's samples).
-// tools/tdigest_study.py measured this schedule at <= 4.2e-4 rank error against the
-// reference's 42-sample incremental merge for keys of 40k..4M samples (one merge of the
-// whole remainder: up to 1.9e-3).
+// tools/tdigest_study.py measured P = 4096 with g = 10, 15, 20, 25 at <= 8e-4 rank error
+// against the reference's 42-sample incremental merge for keys of 40k..3M samples, g making
+// no systematic difference (one merge of the whole remainder: up to 1.9e-3); g = 25 needs
+// 30 rounds for a 3M-sample key where g = 10 needs 71.
 __device__ __forceinline__ uint32_t geo_upper(const uint64_t* geo, uint32_t ngeo, uint64_t p) {
   uint32_t l = 0, h = ngeo;  // first index with geo[i] > p
   while (l < h) {
@@ -547,9 +561,11 @@ __device__ __forceinline__ uint32_t geo_upper(const uint64_t* geo, uint32_t ngeo
   return l;
 }
 
+// maxp[0]: most pieces of a hot key, maxp[1]: of a warm key (the two round loops)
 __global__ void k_histo_pieces(uint32_t ntouched, const uint32_t* __restrict__ ex, const uint32_t* __restrict__ hotcnt,
-                               const uint32_t* __restrict__ seen0, const uint64_t* __restrict__ geo, uint32_t ngeo,
-                               uint32_t* __restrict__ pcnt, uint32_t* __restrict__ pi0, uint32_t* __restrict__ maxp) {
+                               const uint32_t* __restrict__ seen0, const uint32_t* __restrict__ warmflag,
+                               const uint64_t* __restrict__ geo, uint32_t ngeo, uint32_t* __restrict__ pcnt,
+                               uint32_t* __restrict__ pi0, uint32_t* __restrict__ maxp) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= ntouched) return;
   const uint32_t n = hotcnt[k];
@@ -562,7 +578,7 @@ __global__ void k_histo_pieces(uint32_t ntouched, const uint32_t* __restrict__ e
   const uint32_t i1 = geo_upper(geo, ngeo, P1 - 1);  // first boundary after its last sample
   pi0[k] = i0;
   pcnt[k] = 1 + (i1 - i0);
-  atomicMax(maxp, 1 + (i1 - i0));
+  atomicMax(maxp + (warmflag[k] ? 1 : 0), 1 + (i1 - i0));
 }
 
 // copy the hot remainder into the piece-sort input: A = ordered value bits, B = piece id << 32 |
@@ -777,37 +793,43 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   const uint32_t ntouched = e->hf_cnt[0];
   if (!ntouched) return;
 
-  // ---- 2. plan: exact part of every key; hot remainders cut into geometric pieces
+  // ---- 2. plan: exact part of every key (cold / warm / hot, k_histo_plan); the remainders
+  // of warm and hot keys cut into geometric pieces
+  uint32_t* const remflag = e->h_hotflag;
   hipLaunchKernelGGL(k_histo_plan, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_start,
-                     e->h_end, e->hseen, e->exact_threshold, e->hot_prefix, e->h_ex, e->h_hotflag, e->h_coldflag,
-                     e->h_hotcnt, e->h_seen0);
-  compact_flags(e->h_hotflag, e->h_pos, e->h_hotlist, e->h_cnt + 1, ntouched, e->ss, st);
+                     e->h_end, e->hseen, e->exact_threshold, e->hot_prefix, e->h_ex, remflag, e->h_coldflag,
+                     e->h_vhflag, e->h_warmflag, e->h_hotcnt, e->h_seen0);
+  compact_flags(e->h_vhflag, e->h_pos, e->h_hotlist, e->h_cnt + 1, ntouched, e->ss, st);
+  compact_flags(e->h_warmflag, e->h_pos, e->h_warmlist, e->h_cnt + 8, ntouched, e->ss, st);
   compact_flags(e->h_coldflag, e->h_pos, e->h_coldlist, e->h_cnt + 6, ntouched, e->ss, st);
   scan_exclusive_u32(e->h_hotcnt, e->h_hotoff, ntouched, e->ss, st);
-  VN_HIP_CHECK(hipMemsetAsync(e->h_cnt + 4, 0, sizeof(uint32_t), st));
+  VN_HIP_CHECK(hipMemsetAsync(e->h_cnt + 9, 0, 2 * sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_histo_pieces, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_ex,
-                     e->h_hotcnt, e->h_seen0, e->h_geo, e->n_geo, e->h_pcnt, e->h_pi0, e->h_cnt + 4);
+                     e->h_hotcnt, e->h_seen0, e->h_warmflag, e->h_geo, e->n_geo, e->h_pcnt, e->h_pi0, e->h_cnt + 9);
   scan_exclusive_u32(e->h_pcnt, e->h_pbase, ntouched, e->ss, st);
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 1, e->h_cnt + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 2, e->h_hotoff + ntouched, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 3, e->h_pbase + ntouched, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 4, e->h_cnt + 4, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 5, e->h_cnt + 6, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 4, e->h_cnt + 9, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 6, e->h_cnt + 6, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 7, e->h_cnt + 8, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipStreamSynchronize(st));
   const uint32_t nhot = e->hf_cnt[1];
-  const uint64_t nhotrec = e->hf_cnt[2];
+  const uint64_t nremrec = e->hf_cnt[2];  // remainder records of warm and hot keys
   const uint32_t npieces = e->hf_cnt[3];
-  const uint32_t maxp = e->hf_cnt[4];
-  const uint32_t ncold = e->hf_cnt[5];
+  const uint32_t maxp_hot = e->hf_cnt[4];
+  const uint32_t maxp_warm = e->hf_cnt[5];
+  const uint32_t nreplay = e->hf_cnt[6];  // cold + warm keys
+  const uint32_t nwarm = e->hf_cnt[7];
 
   // ---- 3. exact replay of MergingDigest.Add (histo_exact.hip): every pure chunk pre-sorted,
-  // then the keys under the threshold on the replay stream, the hot keys' prefixes here
+  // then the cold and warm keys on the replay stream, the hot keys' prefixes on their own
   ExactCtx xc{};
   xc.nkeys = ntouched;
   xc.keys = e->h_tl;
   xc.start = e->h_start;
   xc.nex = e->h_ex;
-  xc.hot = e->h_hotflag;
+  xc.hot = remflag;
   xc.A = As;
   xc.B = Bs;
   xc.impw = impw;
@@ -832,32 +854,41 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.csw = e->h_csw;
   xc.ctw = e->h_tw;
   histo_exact_presort(xc, st, &e->ss, n / e->temp_cap + 1);
-  // replays on their own streams: the hot keys' prefixes on st4 (short) while st gathers and
-  // sorts the hot remainders; then the keys under the threshold on st3 (long) -- started after
-  // the sort, whose passes would otherwise wait for CUs behind 100k+ replay workgroups -- and
-  // the held-back set merge on the side stream
+  // The hot keys' prefixes run on st4 (short) while st gathers and sorts the remainders; the
+  // cold and warm keys (long) on st3 after the sort, whose passes would otherwise wait for CUs
+  // behind 100k+ replay workgroups -- then the held-back set merge on the side stream.  With
+  // no hot key (or when timing) everything runs in order on st.
   const bool fork = nhot && !e->timing;
+  auto replay_cold = [&](hipStream_t s, RadixScratch& rs) {
+    if (e->lpt & 2) histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
+    else {
+      xc.order64 = nullptr;
+      xc.order = e->h_coldlist;
+      xc.norder = nreplay;
+    }
+    histo_exact_replay(xc, s);
+  };
   if (fork) {
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
     VN_HIP_CHECK(hipStreamWaitEvent(e->st4, e->ev_fork3, 0));
   } else {
-    xc.order = e->h_coldlist;
-    xc.norder = ncold;
-    histo_exact_replay(xc, st);
+    replay_cold(st, e->rs);
   }
+  xc.order64 = nullptr;
   xc.order = e->h_hotlist;
   xc.norder = nhot;
   histo_exact_replay(xc, fork ? e->st4 : st);
   if (fork) VN_HIP_CHECK(hipEventRecord(e->ev_join4, e->st4));
 
-  // ---- 4. hot remainders: geometric pieces, merged round by round (As/Bs stay with the replay)
-  if (nhot == 0 || nhotrec == 0) {
+  // ---- 4. remainders of warm and hot keys: geometric pieces, merged round by round (As/Bs
+  // stay with the replay)
+  if (nremrec == 0) {
     set_finish(e);
     hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
     return;
   }
-  // sort the remainder by (piece, value): every piece contiguous and value-sorted
-  hipLaunchKernelGGL(k_histo_gather_hot, dim3(blocks_for(nhotrec, kTile)), dim3(kBlock), 0, st, ntouched, nhotrec,
+  // sort the remainders by (piece, value): every piece contiguous and value-sorted
+  hipLaunchKernelGGL(k_histo_gather_hot, dim3(blocks_for(nremrec, kTile)), dim3(kBlock), 0, st, ntouched, nremrec,
                      e->h_tl, e->h_start, e->h_ex, e->h_hotoff, e->h_seen0, e->h_pbase, e->h_pi0, e->h_geo,
                      e->n_geo, As, Bs, Ao, Bo);
   RadixPass passes[16];
@@ -866,34 +897,31 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   int pbits = 1;
   while (pbits < 32 && (1ull << pbits) < npieces) pbits++;
   np += make_passes(passes + np, true, 32, pbits);
-  const bool fl2 = radix_sort(Ao, Bo, e->hA2, e->hB2, nhotrec, passes, np, e->rs, st,
+  const bool fl2 = radix_sort(Ao, Bo, e->hA2, e->hB2, nremrec, passes, np, e->rs, st,
                               e->timing ? &e->rstat_h : nullptr);
   const uint64_t* PA = fl2 ? e->hA2 : Ao;  // sorted pieces
   const uint64_t* PB = fl2 ? e->hB2 : Bo;
   uint64_t* MA = fl2 ? Ao : e->hA2;        // per-round merged segments
   uint64_t* MB = fl2 ? Bo : e->hB2;
-  hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(nhotrec, 256)), dim3(256), 0, st, nhotrec, PB, e->p_start,
+  hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, nremrec, PB, e->p_start,
                      e->p_end);
   if (fork) {
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
     VN_HIP_CHECK(hipStreamWaitEvent(e->st3, e->ev_fork3, 0));
-    // keys longest first
-    histo_exact_order(xc, e->h_coldlist, ncold, e->h_lpt0, e->h_lpt1, e->rs3, e->st3);
-    if (!(e->lpt & 2)) xc.order64 = nullptr;
-    histo_exact_replay(xc, e->st3);
+    replay_cold(e->st3, e->rs3);
     VN_HIP_CHECK(hipEventRecord(e->ev_join3, e->st3));
     if (e->set_pending) {
       VN_HIP_CHECK(hipStreamWaitEvent(e->side, e->ev_fork3, 0));
       set_finish(e);
     }
-    VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_join4, 0));  // the rounds start from the prefixes' state
+    VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_join4, 0));  // the hot rounds start from the prefixes' state
   }
 
-  const uint64_t maxch = (nhotrec + (uint64_t)nhot * e->cap_cent) / kHTile + nhot + 1;
-  if (maxch > e->h_max_chunks || nhotrec + (uint64_t)nhot * e->cap_cent > e->h_sort_cap)
+  const uint32_t nrem = nhot + nwarm;
+  const uint64_t maxch = (nremrec + (uint64_t)nrem * e->cap_cent) / kHTile + nrem + 1;
+  if (maxch > e->h_max_chunks || nremrec + (uint64_t)nrem * e->cap_cent > e->h_sort_cap)
     throw std::runtime_error("histo chunk capacity exceeded");
   HistoCtx x;
-  x.ntouched = nhot;
   x.count = e->h_cnt + 5;
   x.capc = e->cap_cent;
   x.delta = e->cfg.compression;
@@ -922,22 +950,29 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   x.cw0 = e->cw[0];
   x.cw1 = e->cw[1];
   x.err = e->h_err;
-  const int merge_blocks = std::min(1024, blocks_for(nhotrec + (uint64_t)nhot * e->cap_cent, kBlock));
-  for (uint32_t j = 0; j < maxp; j++) {
-    hipLaunchKernelGGL(k_round_plan, dim3(1), dim3(1024), 0, st, nhot, j, e->h_hotlist, e->h_tl, e->h_pcnt,
-                       e->h_pbase, e->p_start, e->p_end, e->hncent, e->h_tl2, e->r_flag, e->r_len, e->r_off, e->h_chb,
-                       e->h_start, e->h_end, e->h_cnt + 5);
-    hipLaunchKernelGGL(k_round_merge, dim3(merge_blocks), dim3(kBlock), 0, st, e->cap_cent, e->h_cnt + 5, e->h_tl2,
-                       e->r_flag, e->r_len, e->r_off, e->p_start, e->p_end, e->hcur, e->cmean[0], e->cmean[1], PA, PB,
-                       MA, MB);
-    hipLaunchKernelGGL(k_chunk_prep, dim3(maxch), dim3(kBlock), 0, st, x);
-    hipLaunchKernelGGL(k_seg_scan, dim3(nhot), dim3(kBlock), 0, st, x);
-    hipLaunchKernelGGL(k_chunk_kin, dim3(maxch), dim3(kBlock), 0, st, x);
-    hipLaunchKernelGGL(k_chain, dim3(nhot), dim3(kChainThreads), 0, st, x);
-    hipLaunchKernelGGL(k_chunk_cent, dim3(maxch), dim3(kBlock), 0, st, x);
-    hipLaunchKernelGGL(k_finalize, dim3(nhot), dim3(kBlock), 0, st, x);
-  }
+  const int merge_blocks = std::min(1024, blocks_for(nremrec + (uint64_t)nrem * e->cap_cent, kBlock));
+  // round j merges piece j of every key of the list that has one
+  auto rounds = [&](const uint32_t* list, uint32_t nkeys, uint32_t maxp) {
+    x.ntouched = nkeys;
+    for (uint32_t j = 0; j < maxp; j++) {
+      hipLaunchKernelGGL(k_round_plan, dim3(1), dim3(1024), 0, st, nkeys, j, list, e->h_tl, e->h_pcnt, e->h_pbase,
+                         e->p_start, e->p_end, e->hncent, e->h_tl2, e->r_flag, e->r_len, e->r_off, e->h_chb,
+                         e->h_start, e->h_end, e->h_cnt + 5);
+      hipLaunchKernelGGL(k_round_merge, dim3(merge_blocks), dim3(kBlock), 0, st, e->cap_cent, e->h_cnt + 5, e->h_tl2,
+                         e->r_flag, e->r_len, e->r_off, e->p_start, e->p_end, e->hcur, e->cmean[0], e->cmean[1], PA,
+                         PB, MA, MB);
+      hipLaunchKernelGGL(k_chunk_prep, dim3(maxch), dim3(kBlock), 0, st, x);
+      hipLaunchKernelGGL(k_seg_scan, dim3(nkeys), dim3(kBlock), 0, st, x);
+      hipLaunchKernelGGL(k_chunk_kin, dim3(maxch), dim3(kBlock), 0, st, x);
+      hipLaunchKernelGGL(k_chain, dim3(nkeys), dim3(kChainThreads), 0, st, x);
+      hipLaunchKernelGGL(k_chunk_cent, dim3(maxch), dim3(kBlock), 0, st, x);
+      hipLaunchKernelGGL(k_finalize, dim3(nkeys), dim3(kBlock), 0, st, x);
+    }
+  };
+  if (nhot) rounds(e->h_hotlist, nhot, maxp_hot);
+  // the warm keys' rounds start from their exact prefixes: after the replay stream
   if (fork) VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_join3, 0));
+  if (nwarm) rounds(e->h_warmlist, nwarm, maxp_warm);
   hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
 }
 

@@ -375,15 +375,19 @@ void set_finish(vn_engine* e) {
   // no host round trip: the touched-key count stays on the device and the grid is its upper
   // bound, so the whole set path is queued before the histogram path blocks the host
   const uint32_t nk = (uint32_t)std::min<uint64_t>(e->cap[VN_SET], e->set_pending_n);  // >= touched keys
-  hipLaunchKernelGGL(k_set_lpt_keys, dim3(blocks_for(nk, 256)), dim3(256), 0, st, nk, e->s_cnt, e->s_tl, e->s_start,
-                     e->s_end, e->s_lpt0);
-  RadixPass passes[4];
-  const int np = make_passes(passes, false, 32, 20);
-  const bool fl = radix_sort(e->s_lpt0, nullptr, e->s_lpt1, nullptr, nk, passes, np, *e->side_rs, st, nullptr);
+  const uint64_t* order = nullptr;  // most records first (longest-processing-time order)
+  if (e->lpt & 1) {
+    hipLaunchKernelGGL(k_set_lpt_keys, dim3(blocks_for(nk, 256)), dim3(256), 0, st, nk, e->s_cnt, e->s_tl, e->s_start,
+                       e->s_end, e->s_lpt0);
+    RadixPass passes[4];
+    const int np = make_passes(passes, false, 32, 20);
+    order = radix_sort(e->s_lpt0, nullptr, e->s_lpt1, nullptr, nk, passes, np, *e->side_rs, st, nullptr) ? e->s_lpt1
+                                                                                                          : e->s_lpt0;
+  }
   const uint32_t grid = nk;  // >= touched keys
   SetCtx x;
   x.cnt = e->s_cnt;
-  x.order = (e->lpt & 1) ? (fl ? e->s_lpt1 : e->s_lpt0) : nullptr;
+  x.order = order;
   x.tl = e->s_tl;
   x.start = e->s_start;
   x.end = e->s_end;

@@ -50,10 +50,11 @@ def _arr(ptr, n, dt, shape=None):
 
 class Engine:
     def __init__(self, capacity, compression=100.0, percentiles=(0.5, 0.9, 0.99, 0.999), max_batch_records=1 << 20,
-                 max_batch_member_bytes=0, device=0, exact_threshold=0, hot_prefix=0):
+                 max_batch_member_bytes=0, device=0, exact_threshold=0, hot_prefix=0, piece_growth=0):
         cfg = A.Config()
         cfg.histo_exact_threshold = int(exact_threshold)
         cfg.histo_hot_prefix = int(hot_prefix)
+        cfg.histo_piece_growth = int(piece_growth)
         cfg.device = device
         for i, c in enumerate(capacity):
             cfg.capacity[i] = int(c)
