@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box check: parity tests, bench, rocprof kernel stats.  Stops at the first step that
 # fails, faults, aborts or times out.
-#   tools/gpu_check.sh TAG [skip-tests]
+#   tools/gpu_check.sh TAG [skip-tests|tests] [pmc]
 export TMPDIR=/tmp
 TAG=${1:-run}
 mkdir -p gpurun_out
@@ -14,4 +14,11 @@ fi
 timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.log || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
   python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
+if [ "$3" = "pmc" ]; then
+  # HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots), counters only
+  timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch -o run -- \
+    python3 bench.py --steps 1 --warmup 1 --timing-steps 1 --no-cpu-baseline > gpurun_out/${TAG}_pmc_fetch.log 2>&1 || exit $?
+  timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_write -o run -- \
+    python3 bench.py --steps 1 --warmup 1 --timing-steps 1 --no-cpu-baseline > gpurun_out/${TAG}_pmc_write.log 2>&1 || exit $?
+fi
 exit 0

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""HBM traffic of the roofline kernel from two rocprofv3 --pmc passes.
+
+    python tools/pmc_traffic.py gpurun_out/TAG_pmc_fetch gpurun_out/TAG_pmc_write TAG
+
+Each pass is its own `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` run of the same bench
+command (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2: they cannot share a pass).  Both counters
+are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the
+bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is taken as is.
+
+Algorithmic bytes of a k_radix_scatter launch = n records x (8 B key [+ 8 B value]) read +
+the same written; n is recovered from the grid (4096-record tiles, 256 threads per tile), the
+last tile's padding (< 4096 records) being the only approximation.
+
+Writes roofline_traffic.json (read by bench.py for `roofline.traffic`) and a copy under
+profiles/TAG_pmc_traffic.json.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNEL = "k_radix_scatter"
+TILE, BLOCK = 4096, 256
+
+
+def read_pass(path, counter):
+    """dispatch id -> (kernel name, grid size, value) for one counter."""
+    out = {}
+    files = glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit("no counter_collection.csv under %s" % path)
+    for f in files:
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r.get("Counter_Name") != counter:
+                    continue
+                key = (f, r["Dispatch_Id"])
+                name = r["Kernel_Name"]
+                grid = int(r.get("Grid_Size") or r.get("Grid_Size_X") or 0)
+                v = float(r["Counter_Value"])
+                if key in out:  # one row per (dispatch, counter) normally; sum instances otherwise
+                    out[key] = (name, grid, out[key][2] + v)
+                else:
+                    out[key] = (name, grid, v)
+    return out
+
+
+def main():
+    fetch_dir, write_dir, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    fetch = read_pass(fetch_dir, "FETCH_SIZE")
+    write = read_pass(write_dir, "WRITE_SIZE")
+
+    def scatter(rows):
+        per = defaultdict(list)
+        for (_, _), (name, grid, v) in sorted(rows.items(), key=lambda kv: int(kv[0][1])):
+            if KERNEL in name:
+                hasb = "<true>" in name
+                n = (grid // BLOCK) * TILE
+                per["bytes"].append(v * 1024.0)
+                per["alg"].append(n * (32.0 if hasb else 16.0))
+        return per
+
+    f, w = scatter(fetch), scatter(write)
+    if not f["bytes"] or len(f["bytes"]) != len(w["bytes"]):
+        raise SystemExit("dispatch mismatch: %d fetch vs %d write rows" % (len(f["bytes"]), len(w["bytes"])))
+    n = len(f["bytes"])
+    fetch_b = 2.0 * sum(f["bytes"])  # gfx950: FETCH_SIZE counts half of a wide streaming read
+    write_b = sum(w["bytes"])
+    alg_b = sum(f["alg"])
+    res = {
+        "kernel": KERNEL,
+        "dispatches": n,
+        "traffic_per_launch": (fetch_b + write_b) / n,
+        "fetch_per_launch": fetch_b / n,
+        "write_per_launch": write_b / n,
+        "algorithmic_per_launch": alg_b / n,
+        "traffic_over_algorithmic": (fetch_b + write_b) / alg_b,
+        "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), WRITE_SIZE x1; KiB -> bytes",
+        "source": "profiles/%s_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes)"
+                  % tag,
+    }
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (os.path.join(root, "roofline_traffic.json"), os.path.join(root, "profiles", "%s_pmc_traffic.json" % tag)):
+        with open(p, "w") as fh:
+            json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
