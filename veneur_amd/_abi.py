@@ -16,6 +16,26 @@ if not os.path.exists(LIB_PATH):
         "veneur_amd: %s is missing -- build the HIP engine first (make -C veneur_amd, or "
         "python -c 'import __graft_entry__; __graft_entry__.build()')" % LIB_PATH)
 
+
+
+def _share_torch_hip_runtime():
+    """One HIP runtime per process.  PyTorch-ROCm wheels bundle their own libamdhip64 and
+    libhsa-runtime64 under the same sonames as /opt/rocm's.  Whichever copy loads first wins
+    the soname; if the engine loads /opt/rocm's first, torch later loads its bundled copy as a
+    second runtime, whose KFD open fails ("No HIP GPUs are available").  When torch is
+    installed (dist.py uses it for RCCL), bind the engine to torch's runtime by loading that
+    copy first -- without importing torch.  A Go host has no torch and links
+    /opt/rocm's runtime as usual."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    hip = os.path.join(list(spec.submodule_search_locations)[0], "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        C.CDLL(hip, mode=C.RTLD_GLOBAL)
+
+
+_share_torch_hip_runtime()
 lib = C.CDLL(LIB_PATH)
 
 VN_OK, VN_EINVAL, VN_EHIP, VN_ENOMEM, VN_EDECODE = 0, -1, -2, -3, -4
