@@ -161,6 +161,8 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_err, 4); dzero(e->h_err, 4, st);
   dalloc(e->hseen, ch); dzero(e->hseen, ch, st);
   dalloc(e->hpend, ch); dzero(e->hpend, ch, st);
+  dalloc(e->hspn, ch); dzero(e->hspn, ch, st);
+  dalloc(e->hspw, ch);
   dalloc(e->hpv, (size_t)ch * e->temp_cap);
   dalloc(e->hpw, (size_t)ch * e->temp_cap);
   dalloc(e->h_ex, touch_max);
@@ -361,7 +363,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->h_start); dfree(e->h_end); dfree(e->h_nch); dfree(e->h_chb);
   dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
-  dfree(e->hseen); dfree(e->hpend); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
+  dfree(e->hseen); dfree(e->hpend); dfree(e->hspn); dfree(e->hspw); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
   dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw);
   dfree(e->h_lpt0); dfree(e->h_lpt1); dfree(e->s_lpt0); dfree(e->s_lpt1);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);

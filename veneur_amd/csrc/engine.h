@@ -133,6 +133,8 @@ struct vn_engine {
   uint32_t temp_cap = 42;        // estimateTempBuffer(compression)
   uint32_t* hseen = nullptr;     // samples seen this window per slot
   uint32_t* hpend = nullptr;     // pending temps per slot
+  uint32_t* hspn = nullptr;      // centroids of the flush-ready digest in the other buffer (0: none)
+  double* hspw = nullptr;        // its mainWeight
   double* hpv = nullptr;         // [slot][temp_cap] pending temp means
   double* hpw = nullptr;         // [slot][temp_cap] pending temp weights
   uint32_t* h_ex = nullptr;      // per touched key: samples replayed exactly

@@ -93,6 +93,8 @@ void histo_merge_pending(vn_engine* e, const uint32_t* dev_keys, uint32_t nkeys)
   xc.cw0 = e->cw[0];
   xc.cw1 = e->cw[1];
   xc.hpend = e->hpend;
+  xc.hspn = e->hspn;
+  xc.hspw = e->hspw;
   xc.hpv = e->hpv;
   xc.hpw = e->hpw;
   xc.err = e->h_err;
@@ -226,7 +228,8 @@ __device__ __forceinline__ void histo_empty(double* h) {
   h[7] = 0.0;       // digest weight
 }
 __global__ void k_reset_histo(const uint32_t* cnt, const uint32_t* list, double* hst, uint32_t* hncent,
-                              uint32_t* touch, uint32_t* hseen, uint32_t* hpend) {
+                              uint32_t* touch, uint32_t* hseen, uint32_t* hpend,
+                              uint32_t* hspn) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= cnt[0]) return;
   uint32_t s = list[k];
@@ -235,6 +238,7 @@ __global__ void k_reset_histo(const uint32_t* cnt, const uint32_t* list, double*
   touch[s] = 0;
   hseen[s] = 0;
   hpend[s] = 0;
+  hspn[s] = 0;
 }
 __global__ void k_reset_set(const uint32_t* cnt, const uint32_t* list, uint8_t* mode, uint8_t* base, uint32_t* nz,
                             uint32_t* lc, uint32_t* lb, uint32_t* last, uint32_t* tc, uint32_t* touch) {
@@ -323,7 +327,7 @@ void flush_all(vn_engine* e, vn_flush_result* out) {
                        e->gseq, e->gval, e->gtouch);
   if (ch)
     hipLaunchKernelGGL(k_reset_histo, dim3(blocks_for(ch, 256)), dim3(256), 0, st, e->f_cnt + 2, e->f_list[2], e->hst,
-                       e->hncent, e->htouch, e->hseen, e->hpend);
+                       e->hncent, e->htouch, e->hseen, e->hpend, e->hspn);
   if (cs)
     hipLaunchKernelGGL(k_reset_set, dim3(blocks_for(cs, 256)), dim3(256), 0, st, e->f_cnt + 3, e->f_list[3], e->smode,
                        e->sbase, e->snz, e->slc, e->slb, e->slast, e->stc, e->stouch);

@@ -43,7 +43,7 @@ struct ExactCtx {
   uint32_t capc, tcap;
   double* hst;
   uint32_t* hncent;
-  const uint8_t* hcur;
+  uint8_t* hcur;
   double* cm0;
   double* cm1;
   double* cw0;
@@ -53,6 +53,11 @@ struct ExactCtx {
   double* hpw;
   uint32_t* err;
   int flush_mode;            // 1: only merge pending temps (Quantile's mergeAllTemps)
+  // flush-ready digest: with spec set, a replay that leaves temps pending also merges them
+  // into the other centroid buffer (hspn/hspw); the flush adopts it unless the key changed
+  int spec;
+  uint32_t* hspn;
+  double* hspw;
   // pure-chunk pre-sort (ingest only): per key chunk count and scan, sorted chunk
   // means/weights at the chunk's record positions, Add-order weight sum at its first record
   uint32_t* ccnt;

@@ -178,8 +178,8 @@ struct Lds {
   double *tv, *tw;       // pending temps in Add order [TP]
   double *sv, *sw;       // sorted temps of the merge being done [TP]
   double *gm, *gw, *kin; // merged elements [JW]
-  uint32_t* jump;        // next-start tables, levels x [JW]: u32 in the fast merge
-  uint16_t* jump16;      // the same memory as u16 tables in the generic merge (large delta)
+  uint32_t* jump;        // start of the table memory (jump16 aliases it)
+  uint16_t* jump16;      // next-start tables, levels x [JW] u16 (entries <= JW < 65536)
   uint32_t* starts;      // [JW]
   uint32_t JW, levels;
 };
@@ -608,7 +608,7 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
         }
       }
 #pragma unroll
-      for (int r = 0; r < kR; r++) L.jump[64 * r + lane] = bl[r];
+      for (int r = 0; r < kR; r++) L.jump16[64 * r + lane] = (uint16_t)bl[r];
     }
     wave_lds_sync();
     PROF_T(c2);
@@ -616,15 +616,15 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
     uint32_t levels = 1;  // t < 64 * kR needs bits 0 .. levels-1
     while ((1u << levels) < 64u * kR) levels++;
     for (uint32_t lv = 1; lv < levels; lv++) {
-      const uint32_t* Jp = L.jump + (lv - 1) * L.JW;
-      uint32_t* Jl = L.jump + lv * L.JW;
+      const uint16_t* Jp = L.jump16 + (lv - 1) * L.JW;
+      uint16_t* Jl = L.jump16 + lv * L.JW;
       uint32_t a[kR];
 #pragma unroll
       for (int r = 0; r < kR; r++) a[r] = Jp[64 * r + lane];
 #pragma unroll
       for (int r = 0; r < kR; r++) a[r] = Jp[a[r]];
 #pragma unroll
-      for (int r = 0; r < kR; r++) Jl[64 * r + lane] = a[r];
+      for (int r = 0; r < kR; r++) Jl[64 * r + lane] = (uint16_t)a[r];
       wave_lds_sync();
     }
     PROF_T(c3);
@@ -633,7 +633,7 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
 #pragma unroll
     for (int r = 0; r < kR; r++) p[r] = 0;
     for (uint32_t lv = 0; lv < levels; lv++) {
-      const uint32_t* J = L.jump + lv * L.JW;
+      const uint16_t* J = L.jump16 + lv * L.JW;
 #pragma unroll
       for (int r = 0; r < kR; r++) {
         const uint32_t t = 64 * r + lane;
@@ -831,6 +831,20 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
   const uint32_t nex = x.nex ? x.nex[k] : 0u;
   const bool final_merge = x.flush_mode || (x.hot && x.hot[k]);
   uint32_t np = x.hpend[s];
+  if (x.flush_mode && x.hspn) {
+    // the last replay of this key already merged its pending temps into the other buffer
+    const uint32_t fn = x.hspn[s];
+    if (fn) {
+      if (lane == 0) {
+        x.hcur[s] ^= 1;
+        x.hncent[s] = fn;
+        x.hst[(uint64_t)s * VN_HISTO_STATS + 7] = x.hspw[s];
+        x.hpend[s] = 0;
+        x.hspn[s] = 0;
+      }
+      return;
+    }
+  }
   if (nex == 0 && !(final_merge && np > 0)) return;
 
   const uint8_t cur = x.hcur[s];
@@ -969,6 +983,26 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
       h[6] = max_go(h[6], dmx);
     }
   }
+  // flush-ready digest: Quantile's mergeAllTemps (merging_digest.go:288) done now, into the
+  // other buffer, while this wave still holds the key in LDS.  A later replay, a hot-path
+  // merge or the window reset invalidates it; the flush then merges as usual.
+  if (x.hspn) {
+    uint32_t fn = 0;
+    if (x.spec && !final_merge && np > 0) {
+      merge_pending(mp, L, nm, mainW, np);
+      double* fmg = (cur ? x.cm0 : x.cm1) + (uint64_t)s * capc;
+      double* fwg = (cur ? x.cw0 : x.cw1) + (uint64_t)s * capc;
+      for (uint32_t j = lane; j < nm; j += 64) {
+        fmg[j] = L.mm[j];
+        fwg[j] = L.mw[j];
+      }
+      fn = nm;
+    }
+    if (lane == 0) {
+      x.hspn[s] = fn;
+      if (fn) x.hspw[s] = mainW;
+    }
+  }
 }
 
 // One wave per key: key index blockIdx.x, or the blockIdx.x-th of x.order / x.order64 (the
@@ -1004,7 +1038,7 @@ size_t exact_smem_bytes(uint32_t capc, uint32_t tcap) {
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = std::max(capc + TP + 1, 320u);
   uint32_t levels = 1;
   while ((1u << levels) <= capc) levels++;
-  return sizeof(double) * (2 * capc + 4 * TP + 3 * JW) + sizeof(uint32_t) * JW + std::max<size_t>(sizeof(uint16_t) * levels * JW, tcap <= 64 ? sizeof(uint32_t) * 9 * JW : 0) + 16;
+  return sizeof(double) * (2 * capc + 4 * TP + 3 * JW) + sizeof(uint32_t) * JW + sizeof(uint16_t) * std::max(levels, 9u) * JW + 16;
 }
 
 #ifdef VN_EXACT_PROF

@@ -52,6 +52,7 @@ struct HistoCtx {
   double* hst;
   uint32_t* hncent;
   uint8_t* hcur;
+  uint32_t* hspn;  // cleared when the hot path rewrites a key (its flush-ready digest is stale)
   double* cm0;
   double* cm1;
   double* cw0;
@@ -396,6 +397,7 @@ __global__ __launch_bounds__(kChainThreads) void k_chain(HistoCtx x) {
     if (t == 0) {
       x.hncent[s] = nc;
       x.hcur[s] = nb;
+      x.hspn[s] = 0;
       x.nc_new[k] = nc;
     }
     return;
@@ -483,6 +485,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize(HistoCtx x) {
   if (t == 0) {
     x.hncent[s] = nc;
     x.hcur[s] = nb;
+    x.hspn[s] = 0;
   }
 }
 
@@ -844,6 +847,9 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.cw0 = e->cw[0];
   xc.cw1 = e->cw[1];
   xc.hpend = e->hpend;
+  xc.spec = 1;
+  xc.hspn = e->hspn;
+  xc.hspw = e->hspw;
   xc.hpv = e->hpv;
   xc.hpw = e->hpw;
   xc.err = e->h_err;
@@ -945,6 +951,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   x.hst = e->hst;
   x.hncent = e->hncent;
   x.hcur = e->hcur;
+  x.hspn = e->hspn;
   x.cm0 = e->cmean[0];
   x.cm1 = e->cmean[1];
   x.cw0 = e->cw[0];

@@ -162,35 +162,39 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, bool active, int bit
   return m;
 }
 
-// Stable scatter of one tile (kTile records) by an 8-bit digit.  Each wave owns a contiguous
-// quarter of the tile (kItems records per lane, loaded up front so all global loads are in
-// flight together); it ranks its records with wave ballots and a per-wave running count per
-// digit in LDS -- DS operations of one wave execute in order, so no workgroup barrier is needed
-// while ranking.  Then the per-(wave, digit) starts are a scan over the four waves, the tile is
-// reordered in LDS, and written out with consecutive lanes on consecutive records of a digit.
-template <bool HASB>
-__global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
-                                                          uint64_t* __restrict__ A2, uint64_t* __restrict__ B2,
-                                                          uint64_t n, bool from_b, int shift, int bits,
-                                                          const uint32_t* __restrict__ counts,
-                                                          const uint32_t* __restrict__ offsets, uint32_t nblocks) {
-  __shared__ uint64_t s_a[kTile];
-  __shared__ uint64_t s_b[HASB ? kTile : 1];
-  __shared__ uint32_t s_run[4][256];  // per wave: records of each digit ranked so far
-  __shared__ uint32_t s_loc[256];     // tile-local start of each digit
-  __shared__ uint32_t s_glob[256];    // global start of each digit for this tile
-  __shared__ uint32_t s_wave[4];
+// Stable scatter of one tile (kTile records) by a digit of <= 8 bits.  NW waves per workgroup;
+// each wave owns a contiguous 1/NW of the tile (kTile / (64 NW) records per lane, loaded up
+// front so all global loads are in flight together) and ranks its records with wave ballots and
+// a per-wave running count per digit in LDS -- DS operations of one wave execute in order, so no
+// workgroup barrier is needed while ranking.  The per-(wave, digit) starts are a scan over the
+// waves.  The tile is then reordered through one LDS word array -- for 16-byte records A words
+// first, then B words, with each position's digit kept beside them -- and written out with
+// consecutive lanes on consecutive records of a digit.  16-byte records use 8 waves and stage
+// one word array at a time (~46 KiB of LDS, VGPR-bound at 6 waves/SIMD); 8-byte records use 4
+// waves (~38 KiB, 4 workgroups per CU).
+template <bool HASB, int NW>
+__global__ __launch_bounds__(NW * 64) void k_radix_scatter(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
+                                                           uint64_t* __restrict__ A2, uint64_t* __restrict__ B2,
+                                                           uint64_t n, bool from_b, int shift, int bits,
+                                                           const uint32_t* __restrict__ counts,
+                                                           const uint32_t* __restrict__ offsets, uint32_t nblocks) {
+  constexpr int kRWaves = NW, kRBlock = NW * 64, kRItems = kTile / kRBlock;
+  __shared__ uint64_t s_x[kTile];
+  __shared__ uint8_t s_dig[HASB ? kTile : 1];
+  __shared__ uint32_t s_run[kRWaves][256];  // per wave: records of each digit ranked so far
+  __shared__ uint32_t s_loc[256];           // tile-local start of each digit
+  __shared__ uint32_t s_glob[256];          // global start of each digit for this tile
+  __shared__ uint32_t s_wave[kRWaves];
 
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * kTile;
   const uint32_t tile_n = (uint32_t)((n - base) < (uint64_t)kTile ? (n - base) : kTile);
-  constexpr uint32_t kWaveTile = kTile / 4;
+  constexpr uint32_t kWaveTile = kTile / kRWaves;
 
-  // all of this lane's records first: 16 coalesced loads in flight per array
-  uint64_t a[kItems], b[kItems];
+  uint64_t a[kRItems], b[kRItems];
   const uint32_t wbase = (uint32_t)w * kWaveTile;
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
+  for (int j = 0; j < kRItems; j++) {
     const uint32_t li = wbase + (uint32_t)j * 64 + lane;
     a[j] = li < tile_n ? A[base + li] : 0;
     if (HASB) b[j] = li < tile_n ? B[base + li] : 0;
@@ -200,19 +204,24 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
     const bool dig = (uint32_t)t <= mask;
     uint32_t c = dig ? counts[(uint64_t)t * nblocks + blockIdx.x] : 0u;
     uint32_t total;
-    s_loc[t] = block_excl_scan_u32(c, s_wave, total);
-    s_glob[t] = dig ? offsets[(uint64_t)t * nblocks + blockIdx.x] : 0u;
-    s_run[0][t] = s_run[1][t] = s_run[2][t] = s_run[3][t] = 0;
+    const uint32_t loc = block_excl_scan_u32(c, s_wave, total);  // digits live in waves 0..3
+    if (t < 256) {  // (NW = 4: every thread)
+      s_loc[t] = loc;
+      s_glob[t] = dig ? offsets[(uint64_t)t * nblocks + blockIdx.x] : 0u;
+#pragma unroll
+      for (int v = 0; v < kRWaves; v++) s_run[v][t] = 0;
+    }
   }
   __syncthreads();
-  // rank inside the wave's quarter, in record order
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  uint32_t rank[kItems];
+  uint32_t rank[kRItems];
+  uint8_t dg[kRItems];
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
+  for (int j = 0; j < kRItems; j++) {
     const uint32_t li = wbase + (uint32_t)j * 64 + lane;
     const bool active = li < tile_n;
     const uint32_t d = active ? digit_of<HASB>(a[j], HASB ? b[j] : 0, from_b, shift, mask) : 0u;
+    dg[j] = (uint8_t)d;
     const uint64_t peers = match_digit(d, active, bits);
     const uint32_t before = active ? s_run[w][d] : 0u;
     rank[j] = before + (uint32_t)__popcll(peers & lt);
@@ -221,35 +230,43 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(const uint64_t* __rest
     asm volatile("" ::: "memory");
   }
   __syncthreads();
-  // per (wave, digit) start inside the tile: digit start + the earlier waves' counts
-  {
-    const uint32_t c0 = s_run[0][t], c1 = s_run[1][t], c2 = s_run[2][t];
-    const uint32_t l = s_loc[t];
-    __syncthreads();
-    s_run[0][t] = l;
-    s_run[1][t] = l + c0;
-    s_run[2][t] = l + c0 + c1;
-    s_run[3][t] = l + c0 + c1 + c2;
-  }
-  __syncthreads();
+  if (t < 256) {  // per (wave, digit) start inside the tile: digit start + the earlier waves' counts
+    uint32_t run = s_loc[t];
 #pragma unroll
-  for (int j = 0; j < kItems; j++) {
-    const uint32_t li = wbase + (uint32_t)j * 64 + lane;
-    if (li < tile_n) {
-      const uint32_t d = digit_of<HASB>(a[j], HASB ? b[j] : 0, from_b, shift, mask);
-      const uint32_t pos = s_run[w][d] + rank[j];
-      s_a[pos] = a[j];
-      if (HASB) s_b[pos] = b[j];
+    for (int v = 0; v < kRWaves; v++) {
+      const uint32_t c = s_run[v][t];
+      s_run[v][t] = run;
+      run += c;
     }
   }
   __syncthreads();
-  for (uint32_t li = t; li < tile_n; li += kBlock) {
-    const uint64_t av = s_a[li];
-    const uint64_t bv = HASB ? s_b[li] : 0;
-    const uint32_t d = digit_of<HASB>(av, bv, from_b, shift, mask);
-    const uint64_t pos = (uint64_t)s_glob[d] + (li - s_loc[d]);
-    A2[pos] = av;
-    if (HASB) B2[pos] = bv;
+#pragma unroll
+  for (int j = 0; j < kRItems; j++) {
+    const uint32_t li = wbase + (uint32_t)j * 64 + lane;
+    if (li < tile_n) {
+      rank[j] += s_run[w][dg[j]];
+      s_x[rank[j]] = a[j];
+      if (HASB) s_dig[rank[j]] = dg[j];
+    }
+  }
+  __syncthreads();
+  for (uint32_t li = t; li < tile_n; li += kRBlock) {
+    const uint64_t av = s_x[li];
+    const uint32_t d = HASB ? (uint32_t)s_dig[li] : digit_of<false>(av, 0, false, shift, mask);
+    A2[(uint64_t)s_glob[d] + (li - s_loc[d])] = av;
+  }
+  if (HASB) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kRItems; j++) {
+      const uint32_t li = wbase + (uint32_t)j * 64 + lane;
+      if (li < tile_n) s_x[rank[j]] = b[j];
+    }
+    __syncthreads();
+    for (uint32_t li = t; li < tile_n; li += kRBlock) {
+      const uint32_t d = s_dig[li];
+      B2[(uint64_t)s_glob[d] + (li - s_loc[d])] = s_x[li];
+    }
   }
 }
 
@@ -294,10 +311,10 @@ bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t
     hipEvent_t e1 = (stats && stats->pool) ? stats->pool->next() : nullptr;
     if (e0 && e1) VN_HIP_CHECK(hipEventRecord(e0, st));
     if (hasb)
-      hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, da, db, n, ps.from_b,
+      hipLaunchKernelGGL((k_radix_scatter<true, 8>), dim3(nblocks), dim3(512), 0, st, sa, sb, da, db, n, ps.from_b,
                          ps.shift, ps.bits, s.counts, s.offsets, nblocks);
     else
-      hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, da, db, n, ps.from_b,
+      hipLaunchKernelGGL((k_radix_scatter<false, 4>), dim3(nblocks), dim3(256), 0, st, sa, sb, da, db, n, ps.from_b,
                          ps.shift, ps.bits, s.counts, s.offsets, nblocks);
     if (e0 && e1) VN_HIP_CHECK(hipEventRecord(e1, st));
     if (stats) {
