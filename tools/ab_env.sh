@@ -1,0 +1,6 @@
+# A/B of an engine environment switch on the C3 bench: tools/ab_env.sh VAR "v1 v2 ..."
+export TMPDIR=/tmp; mkdir -p gpurun_out
+for v in $2; do
+  env $1=$v timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 10 > gpurun_out/ab_$1_$v.json 2>gpurun_out/ab_$1_$v.log || exit $?
+  python -c "import json; d=json.load(open('gpurun_out/ab_$1_$v.json')); print('$1=$v', round(d['value']/1e9,3), round(d['ms_per_step'],3), round(d['roofline']['achieved']), round(d['roofline']['frac'],3))"
+done

@@ -163,6 +163,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->hpend, ch); dzero(e->hpend, ch, st);
   dalloc(e->hspn, ch); dzero(e->hspn, ch, st);
   dalloc(e->hspw, ch);
+  dalloc(e->hm_flag, ch); dalloc(e->hm_pos, (size_t)ch + 1); dalloc(e->hm_idx, ch); dalloc(e->hm_list, ch); dalloc(e->hm_cnt, 1);
   dalloc(e->hpv, (size_t)ch * e->temp_cap);
   dalloc(e->hpw, (size_t)ch * e->temp_cap);
   dalloc(e->h_ex, touch_max);
@@ -363,7 +364,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->h_start); dfree(e->h_end); dfree(e->h_nch); dfree(e->h_chb);
   dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
-  dfree(e->hseen); dfree(e->hpend); dfree(e->hspn); dfree(e->hspw); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
+  dfree(e->hseen); dfree(e->hpend); dfree(e->hspn); dfree(e->hspw); dfree(e->hm_flag); dfree(e->hm_pos); dfree(e->hm_idx); dfree(e->hm_list); dfree(e->hm_cnt); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
   dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw);
   dfree(e->h_lpt0); dfree(e->h_lpt1); dfree(e->s_lpt0); dfree(e->s_lpt1);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);
@@ -599,6 +600,7 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
   }
   e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 32768u;
   if (const char* v = std::getenv("VN_LPT")) e->lpt = (uint32_t)std::atoi(v);
+  if (const char* v = std::getenv("VN_EARLY_REPLAY")) e->early_replay = std::atoi(v) != 0;
   e->hot_prefix = std::min(e->exact_threshold, cfg->histo_hot_prefix ? cfg->histo_hot_prefix : 4096u);
   e->piece_growth = cfg->histo_piece_growth ? std::min(cfg->histo_piece_growth, 1000u) : 25u;
   e->temp_cap = temp_buffer_cap(e->cfg.compression);

@@ -74,6 +74,8 @@ struct vn_engine {
   // histo path's remainder sort is done, so the long set kernel does not crowd it out
   bool set_defer = false, set_pending = false;
   uint32_t lpt = 3;              // longest-first order: bit 0 set merge, bit 1 replay (VN_LPT overrides)
+  bool early_replay = true;      // replay of the keys under the threshold starts beside the remainder sort
+                                 // (VN_EARLY_REPLAY=0: after it)
   uint64_t set_pending_n = 0;
   const uint64_t* set_pending_R = nullptr;
   // stream + scratch the counter / gauge / set launchers use for the current call
@@ -135,6 +137,11 @@ struct vn_engine {
   uint32_t* hpend = nullptr;     // pending temps per slot
   uint32_t* hspn = nullptr;      // centroids of the flush-ready digest in the other buffer (0: none)
   double* hspw = nullptr;        // its mainWeight
+  uint32_t* hm_flag = nullptr;   // merge-pending scratch: keys still needing a final merge
+  uint32_t* hm_pos = nullptr;
+  uint32_t* hm_idx = nullptr;
+  uint32_t* hm_list = nullptr;
+  uint32_t* hm_cnt = nullptr;
   double* hpv = nullptr;         // [slot][temp_cap] pending temp means
   double* hpw = nullptr;         // [slot][temp_cap] pending temp weights
   uint32_t* h_ex = nullptr;      // per touched key: samples replayed exactly

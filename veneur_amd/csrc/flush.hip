@@ -76,12 +76,42 @@ __global__ void k_histo_query(uint64_t n, int kind, const uint32_t* __restrict__
                      : td_cdf(m, w, hncent[s], h[7], h[5], h[6], arg[i]);
 }
 
+// Keys whose last replay left a flush-ready digest adopt it (one lane per key); the others
+// with pending temps are listed for a real mergeAllTemps.
+__global__ void k_histo_adopt(uint32_t n, const uint32_t* __restrict__ keys, uint32_t* __restrict__ hspn,
+                              const double* __restrict__ hspw, uint8_t* __restrict__ hcur,
+                              uint32_t* __restrict__ hncent, double* __restrict__ hst, uint32_t* __restrict__ hpend,
+                              uint32_t* __restrict__ flag) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t s = keys[k];
+  const uint32_t fn = hspn[s];
+  if (fn) {
+    hcur[s] ^= 1;
+    hncent[s] = fn;
+    hst[(uint64_t)s * VN_HISTO_STATS + 7] = hspw[s];
+    hpend[s] = 0;
+    hspn[s] = 0;
+  }
+  flag[k] = !fn && hpend[s] > 0;
+}
+__global__ void k_gather_u32(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ idx,
+                             const uint32_t* __restrict__ src, uint32_t* __restrict__ dst) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < cnt[0]) dst[i] = src[idx[i]];
+}
+
 // mergeAllTemps of the given keys (Quantile / CDF / GobEncode merge pending temps first)
 void histo_merge_pending(vn_engine* e, const uint32_t* dev_keys, uint32_t nkeys) {
   if (!nkeys) return;
+  hipLaunchKernelGGL(k_histo_adopt, dim3(blocks_for(nkeys, 256)), dim3(256), 0, e->st, nkeys, dev_keys, e->hspn,
+                     e->hspw, e->hcur, e->hncent, e->hst, e->hpend, e->hm_flag);
+  compact_flags(e->hm_flag, e->hm_pos, e->hm_idx, e->hm_cnt, nkeys, e->ss, e->st);
+  hipLaunchKernelGGL(k_gather_u32, dim3(blocks_for(nkeys, 256)), dim3(256), 0, e->st, e->hm_cnt, e->hm_idx, dev_keys,
+                     e->hm_list);
   ExactCtx xc{};
   xc.nkeys = nkeys;
-  xc.keys = dev_keys;
+  xc.keys = e->hm_list;
   xc.delta = e->cfg.compression;
   xc.capc = e->cap_cent;
   xc.tcap = e->temp_cap;
@@ -99,7 +129,7 @@ void histo_merge_pending(vn_engine* e, const uint32_t* dev_keys, uint32_t nkeys)
   xc.hpw = e->hpw;
   xc.err = e->h_err;
   xc.flush_mode = 1;
-  launch_histo_exact(xc, e->st, nullptr, 0);
+  histo_exact_replay_list(xc, e->hm_cnt, nkeys, e->st);
 }
 
 void histo_query(vn_engine* e, int kind, const uint32_t* dev_slot, const double* dev_arg, uint64_t n, double* dev_out) {
@@ -107,23 +137,78 @@ void histo_query(vn_engine* e, int kind, const uint32_t* dev_slot, const double*
                      e->hncent, e->hcur, e->cmean[0], e->cmean[1], e->cw[0], e->cw[1], e->cap_cent, dev_out);
 }
 
-__global__ void k_flush_histo(const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ list,
-                              const double* __restrict__ hst, const uint32_t* __restrict__ hncent,
-                              const uint8_t* __restrict__ hcur, const double* __restrict__ cm0,
-                              const double* __restrict__ cm1, const double* __restrict__ cw0,
-                              const double* __restrict__ cw1, uint32_t capc, const double* __restrict__ pct,
-                              uint32_t npct, double* __restrict__ out_stats, double* __restrict__ out_q) {
-  uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+// Histo.Flush statistics and Quantile per percentile (merging_digest.go:283-313): one wave
+// per key.  Quantile's walk compares q against the running weight sum P_i = P_(i-1) + w_i and
+// stops at the first i with q <= P_i; the engine forms the same P_i (a wave scan when every
+// weight is an integer and the total stays below 2^53 -- every partial sum is then exact, so
+// the association does not matter; otherwise lane 0 folds them in order), then each
+// percentile's lane binary-searches P and interpolates exactly as the walk would.
+constexpr uint32_t kQWaves = 4;
+__global__ __launch_bounds__(64 * kQWaves) void k_flush_histo(
+    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ list, const double* __restrict__ hst,
+    const uint32_t* __restrict__ hncent, const uint8_t* __restrict__ hcur, const double* __restrict__ cm0,
+    const double* __restrict__ cm1, const double* __restrict__ cw0, const double* __restrict__ cw1, uint32_t capc,
+    const double* __restrict__ pct, uint32_t npct, double* __restrict__ out_stats, double* __restrict__ out_q) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t k = blockIdx.x * kQWaves + wv;
   if (k >= cnt[0]) return;
-  uint32_t s = list[k];
+  double* P = reinterpret_cast<double*>(smem) + (uint64_t)wv * capc;
+  const uint32_t s = list[k];
   const double* h = hst + (uint64_t)s * VN_HISTO_STATS;
-  for (int j = 0; j < VN_HISTO_STATS; j++) out_stats[(uint64_t)k * VN_HISTO_STATS + j] = h[j];
+  if (lane < VN_HISTO_STATS) out_stats[(uint64_t)k * VN_HISTO_STATS + lane] = h[lane];
   const uint8_t c = hcur[s];
   const double* m = (c ? cm1 : cm0) + (uint64_t)s * capc;
   const double* w = (c ? cw1 : cw0) + (uint64_t)s * capc;
   const uint32_t nc = hncent[s];
-  for (uint32_t j = 0; j < npct; j++)
-    out_q[(uint64_t)k * npct + j] = td_quantile(m, w, nc, h[7], h[5], h[6], pct[j]);
+  const double mainW = h[7];
+  bool wint = mainW <= 9007199254740992.0;
+  for (uint32_t j = lane; j < nc; j += 64) {
+    const double x = w[j];
+    P[j] = x;
+    wint &= x == __builtin_trunc(x);
+  }
+  wint = __all(wint);
+  wave_lds_sync();
+  if (wint) {
+    double carry = 0.0;
+    for (uint32_t b = 0; b < nc; b += 64) {
+      double v = b + lane < nc ? P[b + lane] : 0.0;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const double o = __shfl_up(v, d, 64);
+        v = (int)lane >= d ? dadd(v, o) : v;
+      }
+      if (b + lane < nc) P[b + lane] = dadd(carry, v);
+      carry = dadd(carry, __shfl(v, 63, 64));
+    }
+  } else if (lane == 0) {
+    double run = 0.0;
+    for (uint32_t j = 0; j < nc; j++) {
+      run = dadd(run, P[j]);
+      P[j] = run;
+    }
+  }
+  wave_lds_sync();
+  if (lane < npct) {
+    const double q = dmul(pct[lane], mainW);
+    uint32_t lo = 0, hi = nc;  // first i with q <= P[i]
+    while (lo < hi) {
+      const uint32_t md = (lo + hi) >> 1;
+      if (q <= P[md]) hi = md;
+      else lo = md + 1;
+    }
+    double r = __builtin_nan("");
+    if (lo < nc) {
+      const uint32_t i = lo;
+      const double wsf = i ? P[i - 1] : 0.0;
+      const double lower = i ? ddiv(dadd(m[i], m[i - 1]), 2.0) : h[5];
+      const double upper = (i != nc - 1) ? ddiv(dadd(m[i + 1], m[i]), 2.0) : h[6];
+      const double prop = ddiv(dsub(q, wsf), w[i]);
+      r = dadd(lower, dmul(prop, dsub(upper, lower)));
+    }
+    out_q[(uint64_t)k * npct + lane] = r;
+  }
 }
 
 // Sketch.Estimate: one workgroup per touched set slot
@@ -292,31 +377,43 @@ void flush_all(vn_engine* e, vn_flush_result* out) {
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 4, e->f_cnt, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipStreamSynchronize(st));
   const uint32_t n[4] = {e->hf_cnt[4], e->hf_cnt[5], e->hf_cnt[6], e->hf_cnt[7]};
+  // Results to pinned host memory.  Counter and gauge results are final after the sync: their
+  // copies run on the side stream at once.  The sets' estimates run first on the main stream
+  // (all CUs, ~0.15 ms), their copies then follow on the side stream while the main stream
+  // flushes the histograms and copies their (larger) results.
+  hipStream_t s2 = e->timing ? st : e->st2;
+  for (int c : {0, 1})
+    if (n[c])
+      VN_HIP_CHECK(hipMemcpyAsync(e->hf_list[c], e->f_list[c], n[c] * sizeof(uint32_t), hipMemcpyDeviceToHost, s2));
+  if (n[0]) VN_HIP_CHECK(hipMemcpyAsync(e->hf_cval, e->f_cval, n[0] * 8, hipMemcpyDeviceToHost, s2));
+  if (n[1]) VN_HIP_CHECK(hipMemcpyAsync(e->hf_gval, e->f_gval, n[1] * 8, hipMemcpyDeviceToHost, s2));
+  if (cs && n[3]) {
+    hipLaunchKernelGGL(k_flush_set, dim3(n[3]), dim3(kBlock), 0, st, e->f_cnt + 3, e->f_list[3], e->smode, e->sbase,
+                       e->slc, e->stc, e->stmp, e->sarena, e->f_sest, e->f_ssparse);
+    if (s2 != st) {
+      VN_HIP_CHECK(hipEventRecord(e->ev_fork, st));
+      VN_HIP_CHECK(hipStreamWaitEvent(s2, e->ev_fork, 0));
+    }
+    VN_HIP_CHECK(hipMemcpyAsync(e->hf_list[3], e->f_list[3], n[3] * sizeof(uint32_t), hipMemcpyDeviceToHost, s2));
+    VN_HIP_CHECK(hipMemcpyAsync(e->hf_sest, e->f_sest, n[3] * 8, hipMemcpyDeviceToHost, s2));
+    VN_HIP_CHECK(hipMemcpyAsync(e->hf_ssparse, e->f_ssparse, n[3], hipMemcpyDeviceToHost, s2));
+  }
   if (ch && n[2]) {
     // Quantile() first merges the pending temps (merging_digest.go:287)
     histo_merge_pending(e, e->f_list[2], n[2]);
-    hipLaunchKernelGGL(k_flush_histo, dim3(blocks_for(n[2], 128)), dim3(128), 0, st, e->f_cnt + 2, e->f_list[2],
+    hipLaunchKernelGGL(k_flush_histo, dim3(blocks_for(n[2], kQWaves)), dim3(64 * kQWaves),
+                       sizeof(double) * kQWaves * e->cap_cent, st, e->f_cnt + 2, e->f_list[2],
                        e->hst, e->hncent, e->hcur, e->cmean[0], e->cmean[1], e->cw[0], e->cw[1], e->cap_cent,
                        e->d_pct, e->cfg.n_percentiles, e->f_hstats, e->f_hq);
-  }
-  if (cs && n[3])
-    hipLaunchKernelGGL(k_flush_set, dim3(n[3]), dim3(kBlock), 0, st, e->f_cnt + 3, e->f_list[3], e->smode, e->sbase,
-                       e->slc, e->stc, e->stmp, e->sarena, e->f_sest, e->f_ssparse);
-  // results to pinned host memory
-  for (int c = 0; c < VN_NCLASS; c++)
-    if (n[c])
-      VN_HIP_CHECK(hipMemcpyAsync(e->hf_list[c], e->f_list[c], n[c] * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  if (n[0]) VN_HIP_CHECK(hipMemcpyAsync(e->hf_cval, e->f_cval, n[0] * 8, hipMemcpyDeviceToHost, st));
-  if (n[1]) VN_HIP_CHECK(hipMemcpyAsync(e->hf_gval, e->f_gval, n[1] * 8, hipMemcpyDeviceToHost, st));
-  if (n[2]) {
+    VN_HIP_CHECK(hipMemcpyAsync(e->hf_list[2], e->f_list[2], n[2] * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     VN_HIP_CHECK(hipMemcpyAsync(e->hf_hstats, e->f_hstats, (size_t)n[2] * VN_HISTO_STATS * 8, hipMemcpyDeviceToHost, st));
     if (e->cfg.n_percentiles)
       VN_HIP_CHECK(
           hipMemcpyAsync(e->hf_hq, e->f_hq, (size_t)n[2] * e->cfg.n_percentiles * 8, hipMemcpyDeviceToHost, st));
   }
-  if (n[3]) {
-    VN_HIP_CHECK(hipMemcpyAsync(e->hf_sest, e->f_sest, n[3] * 8, hipMemcpyDeviceToHost, st));
-    VN_HIP_CHECK(hipMemcpyAsync(e->hf_ssparse, e->f_ssparse, n[3], hipMemcpyDeviceToHost, st));
+  if (s2 != st) {  // the resets below follow the side stream's reads
+    VN_HIP_CHECK(hipEventRecord(e->ev_join, s2));
+    VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_join, 0));
   }
   // new window: reset the touched slots
   if (cc)

@@ -73,6 +73,8 @@ void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint
 // the pure-chunk pre-sort alone, and the replay alone (over x.order when set)
 void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks);
 void histo_exact_replay(const ExactCtx& x, hipStream_t st);
+// the replay over x.keys[0, *dev_count) (count known on the device only; <= max_keys)
+void histo_exact_replay_list(const ExactCtx& x, const uint32_t* dev_count, uint32_t max_keys, hipStream_t st);
 // replay list[0..n) longest first: sorts the order into buf0/buf1 (n each) on st and sets x
 // up for histo_exact_replay
 void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* buf0, uint64_t* buf1,

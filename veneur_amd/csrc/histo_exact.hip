@@ -1014,6 +1014,23 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   if (k < x.nkeys) replay_key<TPL>(x, k);
 }
 
+// keys [0, *cnt) of x.keys, grid-stride: a bounded grid when only the device knows the count
+template <int TPL>
+__global__ __launch_bounds__(64) void k_histo_exact_list(ExactCtx x, const uint32_t* __restrict__ cnt) {
+  const uint32_t n = *cnt;
+  for (uint32_t k = blockIdx.x; k < n; k += gridDim.x) replay_key<TPL>(x, k);
+}
+
+void histo_exact_replay_list(const ExactCtx& x, const uint32_t* dev_count, uint32_t max_keys, hipStream_t st) {
+  if (!max_keys) return;
+  if (x.tcap > 64 * kMaxTempPerLane) throw std::runtime_error("temp buffer larger than the exact kernel supports");
+  const size_t sm = exact_smem_bytes(x.capc, x.tcap);
+  if (sm > 160 * 1024) throw std::runtime_error("compression too large for the exact replay's LDS budget");
+  const uint32_t grid = std::min<uint32_t>(max_keys, 4096);
+  if (x.tcap <= 64) hipLaunchKernelGGL(k_histo_exact_list<1>, dim3(grid), dim3(64), sm, st, x, dev_count);
+  else hipLaunchKernelGGL(k_histo_exact_list<kMaxTempPerLane>, dim3(grid), dim3(64), sm, st, x, dev_count);
+}
+
 // longest-first order of the listed keys: (0xFFFFF - min(nex, 0xFFFFF)) << 32 | key index
 __global__ void k_exact_lpt_keys(uint32_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ nex,
                                  uint64_t* __restrict__ out) {

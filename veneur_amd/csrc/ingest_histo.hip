@@ -877,6 +877,11 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   if (fork) {
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
     VN_HIP_CHECK(hipStreamWaitEvent(e->st4, e->ev_fork3, 0));
+    if (e->early_replay) {
+      VN_HIP_CHECK(hipStreamWaitEvent(e->st3, e->ev_fork3, 0));
+      replay_cold(e->st3, e->rs3);
+      VN_HIP_CHECK(hipEventRecord(e->ev_join3, e->st3));
+    }
   } else {
     replay_cold(st, e->rs);
   }
@@ -913,9 +918,11 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
                      e->p_end);
   if (fork) {
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
-    VN_HIP_CHECK(hipStreamWaitEvent(e->st3, e->ev_fork3, 0));
-    replay_cold(e->st3, e->rs3);
-    VN_HIP_CHECK(hipEventRecord(e->ev_join3, e->st3));
+    if (!e->early_replay) {
+      VN_HIP_CHECK(hipStreamWaitEvent(e->st3, e->ev_fork3, 0));
+      replay_cold(e->st3, e->rs3);
+      VN_HIP_CHECK(hipEventRecord(e->ev_join3, e->st3));
+    }
     if (e->set_pending) {
       VN_HIP_CHECK(hipStreamWaitEvent(e->side, e->ev_fork3, 0));
       set_finish(e);
