@@ -1,0 +1,269 @@
+"""veneur_amd.Worker: veneur's Worker / samplers API over the HIP engine.
+
+The CPU tests check the host logic with a recording stand-in engine (scope routing of Upsert,
+staging order around imports, the panics and logged errors, Histo.Flush's InterMetrics); the
+GPU tests run the reference's worker_test.go / samplers_test.go cases through the real engine
+and compare a random DogStatsD-shaped stream's InterMetrics with the restated Go worker.
+"""
+import math
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+from veneur_amd import worker as W
+from veneur_amd.engine import EngineError, FlushOutput
+
+K = W.MetricKey
+
+
+class RecordingEngine:
+    """Stands in for veneur_amd.Engine: records the calls, flushes counters as sums."""
+
+    def __init__(self, capacity=(8, 8, 8, 8), percentiles=(0.5, 0.9)):
+        self.capacity, self.percentiles, self.calls = capacity, percentiles, []
+        self.cval = {}
+
+    def ingest(self, **kw):
+        self.calls.append(("ingest", {k: [a.tolist() for a in v] for k, v in kw.items()}))
+        if "counters" in kw:
+            for s, v, r in zip(*kw["counters"]):
+                self.cval[int(s)] = self.cval.get(int(s), 0) + int(v) * int(np.float32(1) / r)
+
+    def import_counters(self, slot, v):
+        self.calls.append(("import_counters", slot.tolist(), v.tolist()))
+        self.cval[int(slot[0])] = self.cval.get(int(slot[0]), 0) + int(v[0])
+
+    def import_gauges(self, slot, v):
+        self.calls.append(("import_gauges", slot.tolist(), v.tolist()))
+
+    def import_histos(self, slot, p):
+        if p[0] == b"bad":
+            raise EngineError("malformed (rc=-4)")
+        self.calls.append(("import_histos", slot.tolist()))
+
+    def import_sets(self, slot, p):
+        self.calls.append(("import_sets", slot.tolist()))
+
+    def flush(self):
+        self.calls.append(("flush",))
+        cs = sorted(self.cval)
+        z = np.zeros(0, np.uint32)
+        out = FlushOutput(np.array(cs, np.uint32), np.array([self.cval[s] for s in cs], np.int64), z, np.zeros(0),
+                          z, np.zeros((0, 8)), np.zeros((0, len(self.percentiles))), z, np.zeros(0, np.uint64),
+                          np.zeros(0, np.uint8), 0, 0)
+        self.cval = {}
+        return out
+
+
+def cpu_worker(**kw):
+    return W.Worker(engine=RecordingEngine(**kw), batch_records=1000)
+
+
+def test_worker_counter_flush_and_empty_window():  # worker_test.go:11-30
+    w = cpu_worker()
+    w.ProcessMetric(W.UDPMetric(K("a.b.c", "counter"), 1.0, 1.0, digest=12345))
+    wm = w.Flush()
+    assert len(wm.counters) == 1 and wm.counters[K("a.b.c", "counter")].value == 1
+    assert len(w.Flush().counters) == 0
+
+
+def test_worker_local_and_global_maps():  # worker_test.go:32-83
+    w = cpu_worker()
+    w.ProcessMetric(W.UDPMetric(K("a.b.c", "histogram"), 1.0, scope=W.MetricScope.LocalOnly))
+    w.ProcessMetric(W.UDPMetric(K("a.b.c", "counter"), 1.0, scope=W.MetricScope.GlobalOnly))
+    w.ProcessMetric(W.UDPMetric(K("b.c.a", "gauge"), 1.0, scope=W.MetricScope.GlobalOnly))
+    w.ProcessMetric(W.UDPMetric(K("t", "timer"), 2.0, scope=W.MetricScope.LocalOnly))
+    w.ProcessMetric(W.UDPMetric(K("s", "set"), "x", scope=W.MetricScope.LocalOnly))
+    wm = w.Flush()
+    assert (len(wm.local_histograms), len(wm.histograms)) == (1, 0)
+    assert (len(wm.global_gauges), len(wm.gauges)) == (1, 0)
+    assert (len(wm.global_counters), len(wm.counters)) == (1, 0)
+    assert (len(wm.local_timers), len(wm.local_sets)) == (1, 1)
+
+
+def test_worker_same_key_different_maps_get_different_slots():
+    w = cpu_worker()
+    w.ProcessMetric(W.UDPMetric(K("a", "counter"), 3.0))
+    w.ProcessMetric(W.UDPMetric(K("a", "counter"), 4.0, scope=W.MetricScope.GlobalOnly))
+    w.ProcessMetric(W.UDPMetric(K("a", "counter"), 5.0, 0.5))
+    wm = w.Flush()
+    assert wm.counters[K("a", "counter")].value == 13 and wm.global_counters[K("a", "counter")].value == 4
+
+
+def test_worker_import_drains_staged_samples_first():  # arrival order across ProcessMetric / ImportMetric
+    w = cpu_worker()
+    w.ProcessMetric(W.UDPMetric(K("g", "gauge"), 1.0, scope=W.MetricScope.GlobalOnly))
+    w.ImportMetric(W.JSONMetric(K("g", "gauge"), [], struct.pack("<d", 7.0)))
+    w.ImportMetric(W.JSONMetric(K("c", "counter"), [], struct.pack("<q", 9)))
+    names = [c[0] for c in w.engine.calls]
+    assert names == ["ingest", "import_gauges", "import_counters"]
+    assert w.engine.calls[1][1:] == ([0], [7.0])
+    assert w.imported == 2 and w.processed == 1
+    wm = w.Flush()
+    assert wm.global_counters[K("c", "counter")].value == 9 and len(wm.global_gauges) == 1
+
+
+def test_worker_errors_like_the_reference(caplog):
+    w = cpu_worker()
+    with pytest.raises(ValueError, match="invalid value added"):  # merging_digest.go:98-100 panic
+        w.ProcessMetric(W.UDPMetric(K("h", "histogram"), float("nan")))
+    w.ProcessMetric(W.UDPMetric(K("x", "distribution"), 1.0))  # logged, counted
+    w.ImportMetric(W.JSONMetric(K("h", "histogram"), [], b"bad"))  # Combine error: logged, skipped
+    w.ImportMetric(W.JSONMetric(K("c", "counter"), [], b"\x01"))
+    assert "Unknown metric type" in caplog.text and "Could not merge" in caplog.text
+    assert w.processed == 2 and w.imported == 2
+    with pytest.raises(OverflowError):
+        for i in range(20):
+            w.ProcessMetric(W.UDPMetric(K("k%d" % i, "counter"), 1.0))
+
+
+def _histo_view(vals, tags=("a:b",)):
+    """The Histo a window of samples flushes to (statistics from the restated Go sampler)."""
+    w = oracle.Worker(1, 1, 1, 1)
+    w.histo(np.zeros(len(vals), np.uint32), np.array(vals, float), np.ones(len(vals), np.float32))
+    st = w.histo_stats(0)
+    q = {p: w.histo_quantile(0, p) for p in (0.5, 0.9, 0.99, 0.999)}
+    return W.Histo("a.b.c", list(tags), st[0], st[1], st[2], st[3], st[4], q)
+
+
+def test_histo_flush_intermetrics():  # samplers_test.go:192-283
+    h = _histo_view([5, 10, 15, 20, 25])
+    A = W.Aggregate
+    agg = W.HistogramAggregates(A.AggregateMin | A.AggregateMax | A.AggregateMedian | A.AggregateAverage |
+                                A.AggregateCount | A.AggregateSum | A.AggregateHarmonicMean, 7)
+    m = h.flush(10, [0.90], agg)
+    assert len(m) == agg.count + 1
+    assert [x.name for x in m] == ["a.b.c.max", "a.b.c.min", "a.b.c.sum", "a.b.c.avg", "a.b.c.count",
+                                   "a.b.c.median", "a.b.c.hmean", "a.b.c.90percentile"]
+    assert [x.value for x in m[:6]] == [25, 5, 75, 15, 5, 15]
+    assert m[6].value == 5 / (1 / 5 + 1 / 10 + 1 / 15 + 1 / 20 + 1 / 25)
+    assert m[7].value == 23.75
+    assert m[4].type == W.MetricType.CounterMetric and all(x.type == W.MetricType.GaugeMetric for x in m if
+                                                           x.name != "a.b.c.count")
+    assert all(x.tags == ["a:b"] for x in m)
+
+
+def test_histo_flush_single_aggregates_and_guards():  # samplers_test.go:285-352; samplers.go:380-452 guards
+    h = _histo_view([5, 10, 15, 20, 25])
+    assert [(x.name, x.value) for x in h.flush(10, [], W.HistogramAggregates(W.Aggregate.AggregateAverage, 1))] == \
+        [("a.b.c.avg", 15.0)]
+    hm = h.flush(10, [], W.HistogramAggregates(W.Aggregate.AggregateHarmonicMean, 1))
+    assert len(hm) == 1 and hm[0].name == "a.b.c.hmean"
+    empty = W.Histo("e", [], 0.0, math.inf, -math.inf, 0.0, 0.0, {0.5: float("nan")})
+    assert [x.name for x in empty.flush(10, [], W.DEFAULT_AGGREGATES)] == []
+    assert h.flush(10, [0.999], W.HistogramAggregates())[0].name == "a.b.c.99percentile"  # Go's int(p*100)
+    with pytest.raises(ValueError):
+        h.flush(10, [0.75], W.HistogramAggregates())
+
+
+def test_route_info_and_exports():  # samplers.go:104-122, 150-234
+    assert W.route_info(["a:b", "veneursinkonly:datadog", "veneursinkonly:kafka"]) == {"datadog", "kafka"}
+    assert W.route_info(["a:b"]) is None
+    c = W.Counter("c", ["x:y"], -5)
+    assert c.export().value == struct.pack("<q", -5) and c.flush(10)[0].type == W.MetricType.CounterMetric
+    g = W.Gauge("g", [], 2.5)
+    assert g.export().value == struct.pack("<d", 2.5)
+    with pytest.raises(ValueError):
+        W.Set("s", [], 3, True).export()
+
+
+# ------------------------------------------------------------------ through the engine (GPU)
+def gpu_worker(**kw):
+    return W.Worker(capacity=(64, 64, 64, 64), percentiles=(0.5, 0.9, 0.99), batch_records=4096, **kw)
+
+
+@pytest.mark.gpu
+def test_gpu_worker_reference_cases():  # worker_test.go:11-117, samplers_test.go:73-80, 144-168, 192-283
+    w = gpu_worker()
+    try:
+        w.ProcessMetric(W.UDPMetric(K("a.b.c", "counter"), 1.0, 1.0, digest=12345))
+        w.ProcessMetric(W.UDPMetric(K("rate", "counter"), 5.0, 0.5))
+        for v in (5, 10, 15, 20, 25):
+            w.ProcessMetric(W.UDPMetric(K("a.b.c", "histogram", "a:b"), float(v), tags=["a:b"]))
+        for m in ("5", "5", "123", "2147483647", "-2147483648"):
+            w.ProcessMetric(W.UDPMetric(K("s", "set", "a:b"), m, tags=["a:b"]))
+        # a forwarded set and histogram (Set.Export / Histo.Export of local samplers)
+        sk = oracle.Sketch()
+        sk.insert(b"foo"), sk.insert(b"bar")
+        w.ImportMetric(W.JSONMetric(K("imp", "set"), [], sk.marshal()))
+        td = oracle.MergingDigest(100.0)
+        td.add(1.0), td.add(2.0)
+        w.ImportMetric(W.JSONMetric(K("imp", "histogram"), [], td.gob_encode()))
+        wm = w.Flush()
+        assert wm.counters[K("a.b.c", "counter")].value == 1 and wm.counters[K("rate", "counter")].value == 10
+        h = wm.histograms[K("a.b.c", "histogram", "a:b")]
+        A = W.Aggregate
+        m = h.flush(10, [0.9], W.HistogramAggregates(A.AggregateMin | A.AggregateMax | A.AggregateMedian |
+                                                      A.AggregateAverage | A.AggregateCount | A.AggregateSum |
+                                                      A.AggregateHarmonicMean, 7))
+        assert [x.value for x in m[:6]] + [m[7].value] == [25, 5, 75, 15, 5, 15, 23.75]
+        assert wm.sets[K("s", "set", "a:b")].flush()[0].value == 4
+        assert len(wm.sets) == 2 and len(wm.histograms) == 2
+        assert wm.sets[K("imp", "set")].estimate == 2
+        assert wm.histograms[K("imp", "histogram")].quantile(0.5) == td.quantile(0.5)
+        assert len(w.Flush()) == 0
+    finally:
+        w.close()
+
+
+@pytest.mark.gpu
+def test_gpu_worker_random_stream_matches_restated_go():
+    rng = np.random.default_rng(7)
+    keys = [K("m%d" % i, t, "env:%d" % (i % 3)) for i, t in
+            enumerate(["counter", "gauge", "histogram", "timer", "set"] * 8)]
+    scopes = [W.MetricScope(int(x)) for x in rng.integers(0, 3, len(keys))]
+    w = gpu_worker()
+    o = oracle.Worker(64, 64, 64, 64)
+    slots, nxt = {}, [0, 0, 0, 0]
+    cls_of = {"counter": 0, "gauge": 1, "histogram": 2, "timer": 2, "set": 3}
+    try:
+        for _ in range(3000):
+            i = int(rng.integers(0, len(keys)))
+            k, sc = keys[i], scopes[i]
+            rate = float(rng.choice([1.0, 0.5, 0.1]))
+            v = ("u%d" % rng.integers(0, 500)) if k.type == "set" else float(np.round(rng.lognormal(3, 1), 3))
+            w.ProcessMetric(W.UDPMetric(k, v, rate, tags=[k.joined_tags], scope=sc))
+            mp = W._map_for(k.type, sc)
+            cls = cls_of[k.type]
+            if (mp, k) not in slots:  # slots are dense per class in order of first Upsert
+                slots[(mp, k)] = nxt[cls]
+                nxt[cls] += 1
+            s = slots[(mp, k)]
+            feed(o, cls, s, v, rate)
+        wm = w.Flush(forward=True)
+        for k, sc in zip(keys, scopes):
+            mp = W._map_for(k.type, sc)
+            smp = getattr(wm, mp)[k]
+            s = slots[(mp, k)]
+            cls = cls_of[k.type]
+            if cls == 0:
+                assert smp.value == o.counter_value(s)
+            elif cls == 1:
+                assert smp.value == o.gauge_value(s)
+            elif cls == 2:
+                st = o.histo_stats(s)
+                assert (smp.local_weight, smp.local_min, smp.local_max) == tuple(st[:3])
+                assert smp.quantile(0.99) == o.histo_quantile(s, 0.99)  # few samples: exact replay
+                if mp in ("histograms", "timers"):
+                    assert smp.export().value == o.histo_gob(s)
+            else:  # Set.Export before Estimate: the restated Estimate merges the tmpSet (hyperloglog.go:204)
+                if mp == "sets":
+                    assert smp.export().value == o.set_sketch(s).marshal()
+                assert smp.estimate == o.set_estimate(s)
+    finally:
+        w.close()
+
+
+def feed(o, cls, s, v, rate):
+    one = np.array([s], np.uint32)
+    if cls == 0:
+        o.counter(one, np.array([v]), np.array([rate], np.float32))
+    elif cls == 1:
+        o.gauge(one, np.array([v]))
+    elif cls == 2:
+        o.histo(one, np.array([v]), np.array([rate], np.float32))
+    else:
+        b = v.encode()
+        o.set(one, np.array([0, len(b)], np.uint32), np.frombuffer(b, np.uint8))

@@ -1,0 +1,456 @@
+"""veneur's Worker and samplers API over the HIP engine (host side of the drop-in boundary).
+
+This mirrors the reference's operator interface for the aggregation path -- the same names,
+argument meaning and error behaviour -- so that code written against veneur's Worker reads the
+same here:
+
+  worker.go:22-138   Worker, WorkerMetrics (10 maps by type x scope), Upsert
+  worker.go:187-227  Worker.ProcessMetric(UDPMetric)
+  worker.go:230-268  Worker.ImportMetric(JSONMetric)
+  worker.go:271-298  Worker.Flush() -> WorkerMetrics (swap, processed/imported reset)
+  samplers/samplers.go:45-122   InterMetric, MetricType, Aggregate, HistogramAggregates, routeInfo
+  samplers/samplers.go:136-526  Counter/Gauge/Set/Histo .Flush and .Export
+  samplers/parser.go:21-43      UDPMetric, MetricKey, MetricScope
+
+What differs is where the work happens: ProcessMetric interns the MetricKey to a class-local
+slot of the window (the map lookup of Upsert) and appends (slot, value, rate) to a staging
+batch; the batch is aggregated on the GPU when it fills, before an import (so arrival order
+across ProcessMetric and ImportMetric is kept) and at Flush.  Flush returns WorkerMetrics whose
+samplers are views of the engine's flush results: their .Flush() builds the InterMetrics exactly
+as samplers.go does, and .Export() returns the forwarded JSONMetric (the engine's device
+GobEncode / MarshalBinary when Flush(forward=True) asked for it).
+"""
+import enum
+import logging
+import struct
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, NamedTuple, Optional, Union
+
+import numpy as np
+
+COUNTER_TYPE, GAUGE_TYPE, HISTOGRAM_TYPE, SET_TYPE, TIMER_TYPE = "counter", "gauge", "histogram", "set", "timer"
+SINK_PREFIX = "veneursinkonly:"  # samplers.go:104
+log = logging.getLogger("veneur_amd.worker")
+
+
+class MetricScope(enum.IntEnum):  # parser.go:30-36
+    MixedScope = 0
+    LocalOnly = 1
+    GlobalOnly = 2
+
+
+class MetricType(enum.IntEnum):  # samplers.go:17-26
+    CounterMetric = 0
+    GaugeMetric = 1
+
+
+class Aggregate(enum.IntFlag):  # samplers.go:60-68
+    AggregateMin = 1 << 0
+    AggregateMax = 1 << 1
+    AggregateMedian = 1 << 2
+    AggregateAverage = 1 << 3
+    AggregateCount = 1 << 4
+    AggregateSum = 1 << 5
+    AggregateHarmonicMean = 1 << 6
+
+
+AGGREGATES_LOOKUP = {"min": Aggregate.AggregateMin, "max": Aggregate.AggregateMax,
+                     "median": Aggregate.AggregateMedian, "avg": Aggregate.AggregateAverage,
+                     "count": Aggregate.AggregateCount, "sum": Aggregate.AggregateSum,
+                     "hmean": Aggregate.AggregateHarmonicMean}
+
+
+@dataclass
+class HistogramAggregates:  # samplers.go:80-83
+    value: Aggregate = Aggregate(0)
+    count: int = 0
+
+
+# veneur's default (server.go:144-146): min, max, count
+DEFAULT_AGGREGATES = HistogramAggregates(Aggregate.AggregateMin | Aggregate.AggregateMax | Aggregate.AggregateCount, 3)
+
+
+class MetricKey(NamedTuple):  # parser.go:39-43 (comparable: the worker's map key)
+    name: str
+    type: str
+    joined_tags: str = ""
+
+
+@dataclass
+class UDPMetric:  # parser.go:21-28
+    key: MetricKey
+    value: Union[float, str]
+    sample_rate: float = 1.0
+    digest: int = 0
+    tags: List[str] = field(default_factory=list)
+    scope: MetricScope = MetricScope.MixedScope
+
+
+@dataclass
+class JSONMetric:  # samplers.go:97-102
+    key: MetricKey
+    tags: List[str]
+    value: bytes
+
+
+@dataclass
+class InterMetric:  # samplers.go:45-56
+    name: str
+    timestamp: int
+    value: float
+    tags: List[str]
+    type: MetricType
+    sinks: Optional[set] = None
+
+
+def route_info(tags):
+    """routeInfo (samplers.go:106-122): sinks named by veneursinkonly: tags, or None (all)."""
+    info = None
+    for t in tags:
+        if t.startswith(SINK_PREFIX):
+            info = info if info is not None else set()
+            info.add(t[len(SINK_PREFIX):])
+    return info
+
+
+def _im(name, now, value, tags, typ, sinks):
+    return InterMetric(name, now, float(value), list(tags), typ, sinks)
+
+
+# ---------------------------------------------------------------- flushed samplers
+@dataclass
+class Counter:
+    name: str
+    tags: List[str]
+    value: int  # int64 (samplers.go:125-129)
+    key: MetricKey = None
+
+    def flush(self, interval=None):  # samplers.go:136-147
+        return [_im(self.name, int(time.time()), float(self.value), self.tags, MetricType.CounterMetric,
+                    route_info(self.tags))]
+
+    def export(self):  # samplers.go:150-165: 8-byte little-endian int64
+        return JSONMetric(MetricKey(self.name, COUNTER_TYPE, ",".join(self.tags)), list(self.tags),
+                          struct.pack("<q", self.value))
+
+
+@dataclass
+class Gauge:
+    name: str
+    tags: List[str]
+    value: float
+    key: MetricKey = None
+
+    def flush(self):  # samplers.go:203-215
+        return [_im(self.name, int(time.time()), self.value, self.tags, MetricType.GaugeMetric,
+                    route_info(self.tags))]
+
+    def export(self):  # samplers.go:218-234: 8-byte little-endian float64
+        return JSONMetric(MetricKey(self.name, GAUGE_TYPE, ",".join(self.tags)), list(self.tags),
+                          struct.pack("<d", self.value))
+
+
+@dataclass
+class Set:
+    name: str
+    tags: List[str]
+    estimate: int      # Hll.Estimate()
+    sparse: bool
+    payload: Optional[bytes] = None  # MarshalBinary, when the flush forwarded it
+    key: MetricKey = None
+
+    def flush(self):  # samplers.go:282-294: the estimate as a GaugeMetric
+        return [_im(self.name, int(time.time()), float(self.estimate), self.tags, MetricType.GaugeMetric,
+                    route_info(self.tags))]
+
+    def export(self):  # samplers.go:296-310
+        if self.payload is None:
+            raise ValueError("set %r was not exported: flush(forward=True)" % self.name)
+        return JSONMetric(MetricKey(self.name, SET_TYPE, ",".join(self.tags)), list(self.tags), self.payload)
+
+
+@dataclass
+class Histo:
+    name: str
+    tags: List[str]
+    local_weight: float
+    local_min: float
+    local_max: float
+    local_sum: float
+    local_reciprocal_sum: float
+    quantiles: Dict[float, float]     # Value.Quantile(p) for the engine's percentiles
+    payload: Optional[bytes] = None   # GobEncode, when the flush forwarded it
+    type_name: str = HISTOGRAM_TYPE
+    key: MetricKey = None
+
+    def quantile(self, p):
+        try:
+            return self.quantiles[float(p)]
+        except KeyError:
+            raise ValueError("percentile %r was not computed at flush: add it to the Worker's percentiles" % p)
+
+    def flush(self, interval, percentiles, aggregates: HistogramAggregates):  # samplers.go:373-498
+        now = int(time.time())
+        sinks = route_info(self.tags)
+        a = Aggregate(aggregates.value)
+        out = []
+        G, Cm = MetricType.GaugeMetric, MetricType.CounterMetric
+        inf = float("inf")
+        if a & Aggregate.AggregateMax and abs(self.local_max) != inf:
+            out.append(_im(self.name + ".max", now, self.local_max, self.tags, G, sinks))
+        if a & Aggregate.AggregateMin and abs(self.local_min) != inf:
+            out.append(_im(self.name + ".min", now, self.local_min, self.tags, G, sinks))
+        if a & Aggregate.AggregateSum and self.local_sum != 0:
+            out.append(_im(self.name + ".sum", now, self.local_sum, self.tags, G, sinks))
+        if a & Aggregate.AggregateAverage and self.local_sum != 0 and self.local_weight != 0:
+            out.append(_im(self.name + ".avg", now, self.local_sum / self.local_weight, self.tags, G, sinks))
+        if a & Aggregate.AggregateCount and self.local_weight != 0:
+            out.append(_im(self.name + ".count", now, self.local_weight, self.tags, Cm, sinks))
+        if a & Aggregate.AggregateMedian:
+            out.append(_im(self.name + ".median", now, self.quantile(0.5), self.tags, G, sinks))
+        if a & Aggregate.AggregateHarmonicMean and self.local_reciprocal_sum != 0 and self.local_weight != 0:
+            out.append(_im(self.name + ".hmean", now, self.local_weight / self.local_reciprocal_sum, self.tags, G,
+                           sinks))
+        for p in percentiles:  # "%s.%dpercentile" with int(p*100): p99.9 is named 99percentile, as in Go
+            out.append(_im("%s.%dpercentile" % (self.name, int(p * 100)), now, self.quantile(p), self.tags, G, sinks))
+        return out
+
+    def export(self):  # samplers.go:501-510
+        if self.payload is None:
+            raise ValueError("histogram %r was not exported: flush(forward=True)" % self.name)
+        return JSONMetric(MetricKey(self.name, self.type_name, ",".join(self.tags)), list(self.tags), self.payload)
+
+
+# map name -> (engine class, type name); worker.go:40-58
+_MAPS = {
+    "counters": (0, COUNTER_TYPE), "global_counters": (0, COUNTER_TYPE),
+    "gauges": (1, GAUGE_TYPE), "global_gauges": (1, GAUGE_TYPE),
+    "histograms": (2, HISTOGRAM_TYPE), "local_histograms": (2, HISTOGRAM_TYPE),
+    "timers": (2, TIMER_TYPE), "local_timers": (2, TIMER_TYPE),
+    "sets": (3, SET_TYPE), "local_sets": (3, SET_TYPE),
+}
+
+
+def _map_for(typ, scope):
+    """Upsert's map choice (worker.go:81-138)."""
+    if typ == COUNTER_TYPE:
+        return "global_counters" if scope == MetricScope.GlobalOnly else "counters"
+    if typ == GAUGE_TYPE:
+        return "global_gauges" if scope == MetricScope.GlobalOnly else "gauges"
+    if typ == HISTOGRAM_TYPE:
+        return "local_histograms" if scope == MetricScope.LocalOnly else "histograms"
+    if typ == SET_TYPE:
+        return "local_sets" if scope == MetricScope.LocalOnly else "sets"
+    if typ == TIMER_TYPE:
+        return "local_timers" if scope == MetricScope.LocalOnly else "timers"
+    return None
+
+
+class WorkerMetrics:
+    """The flushed window: one dict MetricKey -> sampler per reference map (worker.go:40-58)."""
+
+    def __init__(self):
+        for m in _MAPS:
+            setattr(self, m, {})
+
+    def __len__(self):
+        return sum(len(getattr(self, m)) for m in _MAPS)
+
+
+class _Window:
+    """Interned keys of one flush window: per map MetricKey -> (slot, tags); slots are dense per
+    engine class (the engine resets the touched slots at flush, so every window restarts at 0)."""
+
+    def __init__(self):
+        self.maps = {m: {} for m in _MAPS}
+        self.next_slot = [0, 0, 0, 0]
+
+    def upsert(self, map_name, key, tags, cap):
+        d = self.maps[map_name]
+        hit = d.get(key)
+        if hit is not None:
+            return hit[0]
+        cls = _MAPS[map_name][0]
+        s = self.next_slot[cls]
+        if s >= cap[cls]:
+            raise OverflowError("more %s keys in one window than the engine's capacity (%d)" %
+                                (("counter", "gauge", "histo", "set")[cls], cap[cls]))
+        self.next_slot[cls] = s + 1
+        d[key] = (s, list(tags))
+        return s
+
+
+class Worker:
+    """veneur Worker (worker.go) whose samplers live in HBM.
+
+    engine: a veneur_amd.Engine (or anything with its ingest/import/export/flush methods);
+    created from `capacity`/`percentiles` when omitted.  percentiles: the quantiles Flush
+    computes (0.5 is always added for the median aggregate)."""
+
+    def __init__(self, id=0, capacity=(1 << 16, 1 << 16, 1 << 16, 1 << 16), percentiles=(0.5, 0.9, 0.99),
+                 batch_records=1 << 16, engine=None, **engine_kw):
+        self.id = id
+        pct = tuple(sorted(set(float(p) for p in percentiles) | {0.5}))
+        if engine is None:
+            from .engine import Engine
+            engine = Engine(capacity, percentiles=pct, max_batch_records=max(batch_records, 1),
+                            max_batch_member_bytes=max(batch_records, 1) * 64, **engine_kw)
+        self.engine = engine
+        self.capacity = tuple(int(c) for c in getattr(engine, "capacity", capacity))
+        self.percentiles = tuple(float(p) for p in getattr(engine, "percentiles", pct))
+        self.batch_records = int(batch_records)
+        self.processed = 0
+        self.imported = 0
+        self._win = _Window()
+        self._reset_stage()
+
+    # ------------------------------------------------------------ staging
+    def _reset_stage(self):
+        self._c = ([], [], [])
+        self._g = ([], [])
+        self._h = ([], [], [])
+        self._s = ([], [])
+        self._staged = 0
+
+    def _drain(self):
+        """Aggregate the staged ProcessMetric records on the GPU (arrival order per class)."""
+        if not self._staged:
+            return
+        kw = {}
+        if self._c[0]:
+            kw["counters"] = (np.array(self._c[0], np.uint32), np.array(self._c[1], np.float64),
+                              np.array(self._c[2], np.float32))
+        if self._g[0]:
+            kw["gauges"] = (np.array(self._g[0], np.uint32), np.array(self._g[1], np.float64))
+        if self._h[0]:
+            kw["histos"] = (np.array(self._h[0], np.uint32), np.array(self._h[1], np.float64),
+                            np.array(self._h[2], np.float32))
+        if self._s[0]:
+            mem = self._s[1]
+            off = np.zeros(len(mem) + 1, np.uint32)
+            off[1:] = np.cumsum([len(m) for m in mem])
+            kw["sets"] = (np.array(self._s[0], np.uint32), off, np.frombuffer(b"".join(mem) or b"\0", np.uint8))
+        self._reset_stage()
+        self.engine.ingest(**kw)
+
+    # ------------------------------------------------------------ the reference's operations
+    def process_metric(self, m: UDPMetric):
+        """Worker.ProcessMetric (worker.go:187-227)."""
+        self.processed += 1
+        map_name = _map_for(m.key.type, m.scope)
+        if map_name is None:
+            log.error("Unknown metric type for processing: %s", m.key.type)
+            return
+        cls = _MAPS[map_name][0]
+        if cls == 3:
+            if not isinstance(m.value, str):
+                raise TypeError("set sample value must be a string (samplers.go:265)")
+        else:
+            v = float(m.value)
+            if cls == 2 and (v != v or v in (float("inf"), float("-inf"))):
+                raise ValueError("invalid value added")  # MergingDigest.Add panics (merging_digest.go:98-100)
+        slot = self._win.upsert(map_name, m.key, m.tags, self.capacity)
+        rate = np.float32(m.sample_rate)
+        if cls == 0:
+            self._c[0].append(slot), self._c[1].append(v), self._c[2].append(rate)
+        elif cls == 1:
+            self._g[0].append(slot), self._g[1].append(v)
+        elif cls == 2:
+            self._h[0].append(slot), self._h[1].append(v), self._h[2].append(rate)
+        else:
+            self._s[0].append(slot), self._s[1].append(m.value.encode())
+        self._staged += 1
+        if self._staged >= self.batch_records:
+            self._drain()
+
+    ProcessMetric = process_metric
+
+    def ingest_udp(self, m: UDPMetric):
+        """IngestUDP (worker.go:36-38): the channel hand-off is a direct call here."""
+        self.process_metric(m)
+
+    def import_metric(self, other: JSONMetric):
+        """Worker.ImportMetric (worker.go:230-268): counters/gauges go to the global maps, sets and
+        histograms/timers to the mixed-scope maps; a payload that fails to decode is logged and
+        skipped, as Combine's error is."""
+        self.imported += 1
+        typ = other.key.type
+        scope = MetricScope.GlobalOnly if typ in (COUNTER_TYPE, GAUGE_TYPE) else MetricScope.MixedScope
+        map_name = _map_for(typ, scope)
+        if map_name is None:
+            log.error("Unknown metric type for importing: %s", typ)
+            return
+        slot = self._win.upsert(map_name, other.key, other.tags, self.capacity)
+        self._drain()  # samples staged before this import are aggregated first
+        cls = _MAPS[map_name][0]
+        from .engine import EngineError
+        try:
+            if cls == 0:
+                if len(other.value) != 8:
+                    raise EngineError("counter payload is %d bytes, not 8" % len(other.value))
+                self.engine.import_counters(np.array([slot], np.uint32), np.array(struct.unpack("<q", other.value)))
+            elif cls == 1:
+                if len(other.value) != 8:
+                    raise EngineError("gauge payload is %d bytes, not 8" % len(other.value))
+                self.engine.import_gauges(np.array([slot], np.uint32), np.array(struct.unpack("<d", other.value)))
+            elif cls == 2:
+                self.engine.import_histos(np.array([slot], np.uint32), [bytes(other.value)])
+            else:
+                self.engine.import_sets(np.array([slot], np.uint32), [bytes(other.value)])
+        except EngineError as err:
+            log.error("Could not merge %s: %s", map_name.replace("global_", ""), err)
+
+    ImportMetric = import_metric
+
+    def flush(self, forward=False) -> WorkerMetrics:
+        """Worker.Flush (worker.go:271-298): the window's samplers, and a fresh window.  With
+        forward=True the mixed-scope histograms/timers and sets are also exported (GobEncode /
+        MarshalBinary on the GPU) for flushForward (flusher.go:264-353)."""
+        self._drain()
+        win, self._win = self._win, _Window()
+        payload = {}
+        if forward:
+            for cls, names, fn in ((2, ("histograms", "timers"), self.engine.export_histos),
+                                   (3, ("sets",), self.engine.export_sets)):
+                slots = [s for n in names for (s, _) in win.maps[n].values()]
+                if slots:
+                    for s, p in zip(slots, fn(np.array(slots, np.uint32))):
+                        payload[(cls, s)] = p
+        f = self.engine.flush()
+        self.processed = 0
+        self.imported = 0
+        by_cls = [dict(zip(f.counter_slot.tolist(), f.counter_value.tolist())),
+                  dict(zip(f.gauge_slot.tolist(), f.gauge_value.tolist())),
+                  {int(s): i for i, s in enumerate(f.histo_slot)},
+                  {int(s): i for i, s in enumerate(f.set_slot)}]
+        wm = WorkerMetrics()
+        for map_name, (cls, typ) in _MAPS.items():
+            out = getattr(wm, map_name)
+            for key, (s, tags) in win.maps[map_name].items():
+                if cls == 0:
+                    out[key] = Counter(key.name, tags, int(by_cls[0].get(s, 0)), key)
+                elif cls == 1:
+                    out[key] = Gauge(key.name, tags, float(by_cls[1].get(s, 0.0)), key)
+                elif cls == 2:
+                    i = by_cls[2].get(s)
+                    if i is None:  # upserted by an import that failed to decode: an empty Histo
+                        st = [0.0, float("inf"), float("-inf"), 0.0, 0.0]
+                        q = {p: float("nan") for p in self.percentiles}
+                    else:
+                        st = f.histo_stats[i].tolist()
+                        q = dict(zip(self.percentiles, f.histo_quantiles[i].tolist()))
+                    out[key] = Histo(key.name, tags, st[0], st[1], st[2], st[3], st[4], q, payload.get((2, s)), typ,
+                                     key)
+                else:
+                    i = by_cls[3].get(s)
+                    est = int(f.set_estimate[i]) if i is not None else 0
+                    sparse = bool(f.set_sparse[i]) if i is not None else True
+                    out[key] = Set(key.name, tags, est, sparse, payload.get((3, s)), key)
+        return wm
+
+    Flush = flush
+
+    def close(self):
+        if hasattr(self.engine, "close"):
+            self.engine.close()
