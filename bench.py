@@ -178,12 +178,15 @@ def main():
     achieved = (sc_bytes / (sc_ms * 1e-3)) / 1e9 if sc_ms > 0 else 0.0
     phase = {k: round(float(np.mean([t[k] for t in tim])), 4) for k in
              ("ms_ingest_counter", "ms_ingest_gauge", "ms_ingest_histo", "ms_ingest_set", "ms_flush")}
-    traffic, traffic_src = None, None
+    traffic, traffic_src, traffic_ratio = None, None, None
     tf = os.path.join(ROOT, "roofline_traffic.json")  # tools/pmc_traffic.py, PMC passes of this same command
-    if os.path.exists(tf):
+    if os.path.exists(tf) and sc_launch:
         with open(tf) as fh:
             tj = json.load(fh)
-        traffic, traffic_src = tj["traffic_per_launch"], tj["source"]
+        # the PMC passes measure HBM bytes / algorithmic bytes over every scatter dispatch of their
+        # run; scaled to this step's launches (whose mix of record counts it shares)
+        traffic_ratio = tj["traffic_over_algorithmic"]
+        traffic, traffic_src = traffic_ratio * sc_bytes / sc_launch, tj["source"]
     path_bytes = algorithmic_bytes(d)
     path_gbs = path_bytes / (ms_per_step * 1e-3) / 1e9
 
@@ -208,7 +211,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_radix_scatter", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_unit": "bytes per launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                     "traffic_source": traffic_src,
+                     "traffic_over_algorithmic": traffic_ratio, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": sc_bytes / sc_launch if sc_launch else None,
                      "launches_per_step": sc_launch, "ms_per_step": sc_ms},
         "path": {"algorithmic_bytes_per_step": path_bytes, "effective_GBs": path_gbs,

@@ -23,7 +23,7 @@ import sys
 from collections import defaultdict
 
 KERNEL = "k_radix_scatter"
-TILE, BLOCK = 4096, 256
+TILE, BLOCK = 4096, 512  # k_radix_scatter: 8 waves per 4096-record tile
 
 
 def read_pass(path, counter):
@@ -57,7 +57,7 @@ def main():
         per = defaultdict(list)
         for (_, _), (name, grid, v) in sorted(rows.items(), key=lambda kv: int(kv[0][1])):
             if KERNEL in name:
-                hasb = "<true>" in name
+                hasb = "<true" in name  # k_radix_scatter<true, NW>: 16-byte records
                 n = (grid // BLOCK) * TILE
                 per["bytes"].append(v * 1024.0)
                 per["alg"].append(n * (32.0 if hasb else 16.0))
