@@ -1,5 +1,7 @@
 // capi.hip -- engine lifetime and the C-ABI of include/veneur_amd.h.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <cstdlib>
 #include <vector>
@@ -454,16 +456,26 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
     // counters, gauges and sets on the low-priority side stream (none of them waits on the
     // host); then the rest of the histo path, whose host round trips no longer hold back
     // the side work -- it fills the GPU while the replays and remainder rounds run
+    static const bool host_timing = std::getenv("VN_HOST_TIMING") != nullptr;  // enqueue-cost probe
+    auto now = [] { return std::chrono::duration<double, std::micro>(
+                        std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t0 = host_timing ? now() : 0.0;
     side_begin(e);  // the side stream waits for what the main stream held before this call
     const HistoGroups g = histo_group(e, b->n_histo, b->histo_slot, b->histo_value, b->histo_rate);
+    const double t1 = host_timing ? now() : 0.0;
     ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
     ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
     e->set_defer = true;  // histo_process queues the set merge after the remainder sort
     ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
     e->set_defer = false;
+    const double t2 = host_timing ? now() : 0.0;
     histo_process(e, b->n_histo, g);
+    const double t3 = host_timing ? now() : 0.0;
     set_finish(e);
     side_join(e);
+    if (host_timing)
+      std::fprintf(stderr, "[vn host] histo_group %.0f us, side enqueue %.0f us, histo_process %.0f us\n", t1 - t0,
+                   t2 - t1, t3 - t2);
   }
   if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[4], st));
   VN_HIP_CHECK(hipGetLastError());  // a launch that could not start (e.g. LDS over budget) fails loudly
