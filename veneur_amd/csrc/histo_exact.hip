@@ -448,13 +448,14 @@ __device__ __noinline__ void merge_sorted(const MergeParams x, const Lds& L, uin
 // all rounds issue back to back instead of one exec-masked round at a time.
 // Requires nm + np < 64 * kR <= JW (delta <= ~150) and np <= 64.
 constexpr int kR = 5;     // largest instantiation: nm + np < 320
-constexpr int kLogM = 9;  // steps of a search over main (nm <= 256 < 2^9)
 constexpr int kLogT = 7;  // steps of a search over the temps (np <= 64 < 2^7)
 
 template <int kR>
 __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
                                   double tempW) {
-  constexpr int kLogR = kR <= 1 ? 7 : (kR <= 2 ? 8 : 9);  // steps of a search over the merged list
+  // steps of a lower-bound search over at most 64 kR - 1 entries: ceil(log2(64 kR))
+  constexpr int kLogR = kR <= 1 ? 6 : (kR <= 2 ? 7 : (kR <= 4 ? 8 : 9));
+  constexpr int kLogMT = kLogR > kLogT ? kLogR : kLogT;  // main (nm < 64 kR) and temps (np <= 64)
   const uint32_t lane = threadIdx.x;
   PROF_T(p0);
   const double T = dadd(mainW, tempW);
@@ -473,7 +474,7 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
     }
     uint32_t tl = 0, th = lane < np ? nm : 0;
 #pragma unroll
-    for (int it = 0; it < kLogM; it++) {
+    for (int it = 0; it < kLogMT; it++) {
       const uint32_t tmd = (tl + th) >> 1;
       const double tval = L.mm[tmd < nm ? tmd : 0];
       const bool tgo = tl < th, tlt = tval < tv;
@@ -580,6 +581,7 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
   bool overflow = false;
   const uint32_t capc = x.capc;
   if (mono) {
+    uint32_t cur[kR];  // this lane's entries of the newest jump table, kept in registers
     {
       double base[kR];
       uint32_t bl[kR], bh[kR];
@@ -608,7 +610,10 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
         }
       }
 #pragma unroll
-      for (int r = 0; r < kR; r++) L.jump16[64 * r + lane] = (uint16_t)bl[r];
+      for (int r = 0; r < kR; r++) {
+        L.jump16[64 * r + lane] = (uint16_t)bl[r];
+        cur[r] = bl[r];
+      }
     }
     wave_lds_sync();
     PROF_T(c2);
@@ -620,11 +625,12 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
       uint16_t* Jl = L.jump16 + lv * L.JW;
       uint32_t a[kR];
 #pragma unroll
-      for (int r = 0; r < kR; r++) a[r] = Jp[64 * r + lane];
+      for (int r = 0; r < kR; r++) a[r] = Jp[cur[r]];  // J_lv[s] = J_(lv-1)[J_(lv-1)[s]]
 #pragma unroll
-      for (int r = 0; r < kR; r++) a[r] = Jp[a[r]];
-#pragma unroll
-      for (int r = 0; r < kR; r++) Jl[64 * r + lane] = (uint16_t)a[r];
+      for (int r = 0; r < kR; r++) {
+        Jl[64 * r + lane] = (uint16_t)a[r];
+        cur[r] = a[r];
+      }
       wave_lds_sync();
     }
     PROF_T(c3);
