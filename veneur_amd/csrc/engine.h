@@ -78,6 +78,7 @@ struct vn_engine {
                                  // (VN_EARLY_REPLAY=0: after it)
   uint64_t set_pending_n = 0;
   const uint64_t* set_pending_R = nullptr;
+  const uint64_t* set_pending_order = nullptr;  // LPT order of the pending set merge (or null)
   // stream + scratch the counter / gauge / set launchers use for the current call
   // (st2 normally; st when timing is enabled, so per-kernel durations are measured alone)
   hipStream_t side = nullptr;

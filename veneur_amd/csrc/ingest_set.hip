@@ -356,34 +356,31 @@ void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t*
   const uint64_t* R = fl ? e->sR1 : e->sR0;
   hipLaunchKernelGGL(k_set_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, R, e->s_start, e->s_end);
   compact_flags(e->s_bt, e->s_pos, e->s_tl, e->s_cnt, caps, *e->side_ss, st);
-  if (e->set_defer) {
-    e->set_pending = true;
-    e->set_pending_n = n;
-    e->set_pending_R = R;
-    return;
+  // no host round trip: the touched-key count stays on the device and the grid is its upper
+  // bound, so the whole set path is queued before the histogram path blocks the host
+  const uint32_t nk = (uint32_t)std::min<uint64_t>(caps, n);  // >= touched keys
+  const uint64_t* order = nullptr;  // most records first (longest-processing-time order)
+  if (e->lpt & 1) {  // ordered now, before the replays fill the CUs; only the merge is deferred
+    hipLaunchKernelGGL(k_set_lpt_keys, dim3(blocks_for(nk, 256)), dim3(256), 0, st, nk, e->s_cnt, e->s_tl, e->s_start,
+                       e->s_end, e->s_lpt0);
+    RadixPass lp[4];
+    const int nlp = make_passes(lp, false, 32, 20);
+    order = radix_sort(e->s_lpt0, nullptr, e->s_lpt1, nullptr, nk, lp, nlp, *e->side_rs, st, nullptr) ? e->s_lpt1
+                                                                                                     : e->s_lpt0;
   }
+  e->set_pending = true;
   e->set_pending_n = n;
   e->set_pending_R = R;
-  e->set_pending = true;
-  set_finish(e);
+  e->set_pending_order = order;
+  if (!e->set_defer) set_finish(e);
 }
 
 void set_finish(vn_engine* e) {
   if (!e->set_pending) return;
   e->set_pending = false;
   hipStream_t st = e->side;
-  // no host round trip: the touched-key count stays on the device and the grid is its upper
-  // bound, so the whole set path is queued before the histogram path blocks the host
   const uint32_t nk = (uint32_t)std::min<uint64_t>(e->cap[VN_SET], e->set_pending_n);  // >= touched keys
-  const uint64_t* order = nullptr;  // most records first (longest-processing-time order)
-  if (e->lpt & 1) {
-    hipLaunchKernelGGL(k_set_lpt_keys, dim3(blocks_for(nk, 256)), dim3(256), 0, st, nk, e->s_cnt, e->s_tl, e->s_start,
-                       e->s_end, e->s_lpt0);
-    RadixPass passes[4];
-    const int np = make_passes(passes, false, 32, 20);
-    order = radix_sort(e->s_lpt0, nullptr, e->s_lpt1, nullptr, nk, passes, np, *e->side_rs, st, nullptr) ? e->s_lpt1
-                                                                                                          : e->s_lpt0;
-  }
+  const uint64_t* order = e->set_pending_order;
   const uint32_t grid = nk;  // >= touched keys
   SetCtx x;
   x.cnt = e->s_cnt;
