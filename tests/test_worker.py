@@ -169,6 +169,29 @@ def test_route_info_and_exports():  # samplers.go:104-122, 150-234
         W.Set("s", [], 3, True).export()
 
 
+def test_import_routing_kats():  # http_test.go:23-57
+    ms = [W.JSONMetric(K(n, t), [], b"") for n, t in (("foo", "histogram"), ("bar", "set"), ("baz", "counter"),
+                                                      ("qux", "gauge"))]
+    assert [W.metric_digest(m.key) % 96 for m in ms] == [0x4F, 0x3A, 0x2, 0x3C]
+    chunks = list(W.json_metrics_by_worker(ms, 96))
+    assert [(c[0].key.name, w) for c, w in chunks] == [("baz", 2), ("bar", 0x3A), ("qux", 0x3C), ("foo", 0x4F)]
+    # the import hash equals the parser's digest of "foo:1|h|#bar" (restated in the oracle)
+    assert W.metric_digest(K("foo", "histogram", "bar")) == oracle.metric_digest("foo", "histogram", "bar")
+
+
+def test_import_metrics_and_udp_routing_reach_the_right_workers():
+    ws = [cpu_worker() for _ in range(3)]
+    ms = [W.JSONMetric(K("c%d" % i, "counter"), [], struct.pack("<q", i)) for i in range(12)]
+    W.import_metrics(ws, ms)
+    for w in ws:
+        got = w.Flush().global_counters
+        assert all(W.metric_digest(k) % 3 == ws.index(w) for k in got)
+        assert all(got[k].value == int(k.name[1:]) for k in got)
+    u = W.UDPMetric(K("x", "counter"), 2.0)
+    W.route_udp(ws, u)
+    assert len(ws[W.metric_digest(u.key) % 3].Flush().counters) == 1
+
+
 # ------------------------------------------------------------------ through the engine (GPU)
 def gpu_worker(**kw):
     return W.Worker(capacity=(64, 64, 64, 64), percentiles=(0.5, 0.9, 0.99), batch_records=4096, **kw)

@@ -11,6 +11,7 @@ same here:
   samplers/samplers.go:45-122   InterMetric, MetricType, Aggregate, HistogramAggregates, routeInfo
   samplers/samplers.go:136-526  Counter/Gauge/Set/Histo .Flush and .Export
   samplers/parser.go:21-43      UDPMetric, MetricKey, MetricScope
+  parser.go:213-304, server.go:655, http.go:52-139   Digest routing and ImportMetrics chunking
 
 What differs is where the work happens: ProcessMetric interns the MetricKey to a class-local
 slot of the window (the map lookup of Upsert) and appends (slot, value, rate) to a staging
@@ -220,6 +221,45 @@ class Histo:
         if self.payload is None:
             raise ValueError("histogram %r was not exported: flush(forward=True)" % self.name)
         return JSONMetric(MetricKey(self.name, self.type_name, ",".join(self.tags)), list(self.tags), self.payload)
+
+
+# ---------------------------------------------------------------- routing (host side)
+def metric_digest(key: MetricKey) -> int:
+    """FNV-1a 32 of name, type and joined tags: UDPMetric.Digest (parser.go:213-304) and the
+    import worker hash (http.go:77-90).  Keys route to worker Digest % len(workers)."""
+    h = 0x811C9DC5
+    for part in (key.name, key.type, key.joined_tags):
+        for b in part.encode():
+            h = ((h ^ b) * 0x01000193) & 0xFFFFFFFF
+    return h
+
+
+def route_udp(workers, m: UDPMetric):
+    """Server.HandleMetricPacket's hand-off (server.go:655): workers[Digest % n].IngestUDP."""
+    d = m.digest if m.digest else metric_digest(m.key)
+    workers[d % len(workers)].ingest_udp(m)
+
+
+def json_metrics_by_worker(metrics, num_workers):
+    """newJSONMetricsByWorker (http.go:71-139): the imported metrics ordered by worker index,
+    yielded as contiguous (chunk, worker index) runs.  Go's sort.Sort leaves the order inside
+    a worker's run unspecified; this keeps arrival order there (one of the orders it allows)."""
+    idx = [metric_digest(m.key) % num_workers for m in metrics]
+    order = sorted(range(len(metrics)), key=lambda i: idx[i])
+    i = 0
+    while i < len(order):
+        j = i
+        while j < len(order) and idx[order[j]] == idx[order[i]]:
+            j += 1
+        yield [metrics[k] for k in order[i:j]], idx[order[i]]
+        i = j
+
+
+def import_metrics(workers, metrics):
+    """Server.ImportMetrics (http.go:52-67): each worker's chunk to its ImportMetric, in order."""
+    for chunk, w in json_metrics_by_worker(metrics, len(workers)):
+        for m in chunk:
+            workers[w].import_metric(m)
 
 
 # map name -> (engine class, type name); worker.go:40-58
