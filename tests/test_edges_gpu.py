@@ -1,0 +1,132 @@
+"""Edge cases of the engine's boundary and of the per-key state machines, against the oracle:
+empty batches and windows, batches of exactly max_batch_records, slots at the capacity edge,
+t-digest keys around the 42-entry temp buffer (estimateTempBuffer(100), merging_digest.go:87-93),
+empty and long set members, a key touched only by imports."""
+import numpy as np
+import pytest
+
+import oracle
+import veneur_amd as V
+from tests.util import PCT, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+Z32, ZF, ZF32 = np.zeros(0, np.uint32), np.zeros(0), np.zeros(0, np.float32)
+
+
+def make_engine(n_slots, max_records=1 << 14):
+    return V.Engine(tuple(n_slots), percentiles=PCT, max_batch_records=max_records,
+                    max_batch_member_bytes=max_records * 64)
+
+
+def stream(**kw):
+    d = {"c_slot": Z32, "c_val": ZF, "c_rate": ZF32, "g_slot": Z32, "g_val": ZF, "h_slot": Z32, "h_val": ZF,
+         "h_rate": ZF32, "s_slot": Z32, "s_off": np.zeros(1, np.uint32), "s_bytes": np.zeros(0, np.uint8)}
+    d.update(kw)
+    return d
+
+
+def test_empty_batches_and_empty_window():
+    with make_engine((4, 4, 4, 4)) as e:
+        e.ingest()
+        e.ingest(counters=(Z32, ZF, ZF32), gauges=(Z32, ZF), histos=(Z32, ZF, ZF32), set_hashes=(Z32, Z32.astype(np.uint64)))
+        f = e.flush()
+        assert (len(f.counter_slot), len(f.gauge_slot), len(f.histo_slot), len(f.set_slot)) == (0, 0, 0, 0)
+        assert f.samples_processed == 0 and f.samples_imported == 0
+        f = e.flush()  # a second empty window
+        assert len(f.histo_slot) == 0
+
+
+def test_batch_of_exactly_max_records_and_capacity_edges():
+    n, cap = 1 << 14, 1000
+    rng = np.random.default_rng(5)
+    slots = rng.integers(0, cap, n).astype(np.uint32)
+    slots[:4] = cap - 1  # the last slot of every class
+    vals = np.round(rng.lognormal(3, 1, n), 3)
+    rates = np.where(rng.random(n) < 0.2, np.float32(0.1), np.float32(1.0)).astype(np.float32)
+    members = [("m%d" % i).encode() for i in rng.integers(0, 5000, n)]
+    off = np.zeros(n + 1, np.uint32)
+    off[1:] = np.cumsum([len(m) for m in members])
+    mb = np.frombuffer(b"".join(members), np.uint8)
+    d = stream(c_slot=slots, c_val=vals, c_rate=rates, g_slot=slots, g_val=vals, h_slot=slots, h_val=vals,
+               h_rate=rates, s_slot=slots, s_off=off, s_bytes=mb)
+    w = run_oracle(d, (cap,) * 4)
+    with make_engine((cap,) * 4, max_records=n) as e:
+        e.ingest(counters=(slots, vals, rates), gauges=(slots, vals), histos=(slots, vals, rates), sets=(slots, off, mb))
+        with pytest.raises(V.EngineError):  # one record over max_batch_records fails loudly
+            e.ingest(counters=(np.zeros(n + 1, np.uint32), np.ones(n + 1), np.ones(n + 1, np.float32)))
+        with pytest.raises(V.EngineError):  # slot == capacity
+            e.ingest(gauges=(np.array([cap], np.uint32), np.ones(1)))
+        f = e.flush()
+    assert f.samples_processed == 4 * n
+    assert cap - 1 in f.counter_slot.tolist()
+    assert dict(zip(f.counter_slot.tolist(), f.counter_value.tolist())) == \
+        {s: w.counter_value(s) for s in range(cap) if w.touched(0, s)}
+    assert dict(zip(f.gauge_slot.tolist(), f.gauge_value.tolist())) == \
+        {s: w.gauge_value(s) for s in range(cap) if w.touched(1, s)}
+    assert f.set_estimate.tolist() == [w.set_estimate(int(s)) for s in f.set_slot]
+    oq = np.array([[w.histo_quantile(int(s), p) for p in PCT] for s in f.histo_slot])
+    np.testing.assert_array_equal(f.histo_quantiles, oq)
+
+
+@pytest.mark.parametrize("batches", [1, 3])
+def test_digest_sizes_around_the_temp_buffer(batches):
+    """Keys with 1, 41, 42, 43, 84, 85, 126, 127 and 1000 samples: every merge boundary of the
+    42-entry temp buffer, within one batch and split across batches."""
+    sizes = [1, 41, 42, 43, 84, 85, 126, 127, 1000]
+    rng = np.random.default_rng(9)
+    slots = np.concatenate([np.full(n, i, np.uint32) for i, n in enumerate(sizes)])
+    perm = rng.permutation(len(slots))
+    slots = slots[perm]
+    vals = np.round(rng.lognormal(2, 1, len(slots)), 2)  # repeated values: ties in the temp sort
+    rates = np.ones(len(slots), np.float32)
+    w = oracle.Worker(1, 1, len(sizes), 1)
+    w.histo(slots, vals, rates)
+    with make_engine((1, 1, len(sizes), 1)) as e:
+        for part in np.array_split(np.arange(len(slots)), batches):
+            e.ingest(histos=(slots[part], vals[part], rates[part]))
+        f = e.flush()
+    assert f.histo_slot.tolist() == list(range(len(sizes)))
+    ost = np.array([w.histo_stats(s) for s in range(len(sizes))])
+    np.testing.assert_array_equal(f.histo_stats[:, [0, 1, 2, 5, 6, 7]], ost[:, [0, 1, 2, 5, 6, 7]])
+    np.testing.assert_array_equal(f.histo_quantiles, [[w.histo_quantile(s, p) for p in PCT] for s in range(len(sizes))])
+
+
+def test_set_members_empty_and_long():
+    members = [b"", b"", b"x", b"a" * 4097, b"a" * 4097, bytes(range(256)) * 3, b"\x00"]
+    slots = np.array([0, 0, 0, 0, 1, 1, 1], np.uint32)
+    off = np.zeros(len(members) + 1, np.uint32)
+    off[1:] = np.cumsum([len(m) for m in members])
+    mb = np.frombuffer(b"".join(members), np.uint8)
+    w = oracle.Worker(1, 1, 1, 2)
+    w.set(slots, off, mb)
+    with make_engine((1, 1, 1, 2)) as e:
+        e.ingest(sets=(slots, off, mb))
+        for s in (0, 1):
+            assert np.array_equal(e.read_set(s)["tmp"], w.set_sketch(s).tmp_codes())
+        f = e.flush()
+    assert f.set_estimate.tolist() == [w.set_estimate(0), w.set_estimate(1)] == [3, 3]
+
+
+def test_key_touched_only_by_imports():  # worker.go:237-242: imports Upsert the key too
+    td = oracle.MergingDigest(100.0)
+    td.add_many(np.arange(1.0, 50.0), np.ones(49))
+    sk = oracle.Sketch()
+    for h in range(1, 30):
+        sk.insert_hash(h * 0x9E3779B97F4A7C15 % (1 << 64))
+    hp, sp = td.gob_encode(), sk.marshal()
+    w = oracle.Worker(2, 2, 2, 2)
+    assert w.import_histo(1, hp) == 0
+    w.import_set(1, sp)
+    with make_engine((2, 2, 2, 2)) as e:
+        e.import_counters(np.array([1], np.uint32), np.array([-7], np.int64))
+        e.import_gauges(np.array([1], np.uint32), np.array([2.5]))
+        e.import_histos(np.array([1], np.uint32), [hp])
+        e.import_sets(np.array([1], np.uint32), [sp])
+        f = e.flush()
+    assert f.counter_slot.tolist() == [1] and f.counter_value.tolist() == [-7]
+    assert f.gauge_value.tolist() == [2.5]
+    assert f.histo_stats[0][0] == 0.0  # no local samples: LocalWeight stays 0 (samplers.go:519-526)
+    assert f.histo_quantiles[0].tolist() == [w.histo_quantile(1, p) for p in PCT]
+    assert f.set_estimate.tolist() == [w.set_estimate(1)]
+    assert f.samples_imported == 4 and f.samples_processed == 0
