@@ -85,6 +85,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timing-steps", type=int, default=2, help="untimed steps with per-kernel HIP-event timing")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof runs)")
+    ap.add_argument("--pcie-steps", type=int, default=2,
+                    help="extra steps from host arrays (vn_ingest_host), reported as pcie_inclusive; 0: off")
     args = ap.parse_args()
 
     import veneur_amd as V
@@ -165,6 +167,23 @@ def main():
     eng.timing_enable(False)
     for _ in range(args.profile_steps):
         last = step()
+    # PCIe-inclusive rate (never `value`): the same window handed over as pageable host arrays
+    # through vn_ingest_host (host-side checks, pinned staging, H2D copies, then the same kernels)
+    pcie = None
+    if args.pcie_steps > 0 and world == 1 and args.batches == 1:
+        hkw = dict(counters=(d["c_slot"], d["c_val"], d["c_rate"]), gauges=(d["g_slot"], d["g_val"]),
+                   histos=(d["h_slot"], d["h_val"], d["h_rate"]), sets=(d["s_slot"], d["s_off"], d["s_bytes"]))
+        eng.ingest(**hkw)
+        eng.flush_raw()
+        sync()
+        tp = time.perf_counter()
+        for _ in range(args.pcie_steps):
+            eng.ingest(**hkw)
+            last = eng.flush_raw()
+        sync()
+        pms = (time.perf_counter() - tp) * 1e3 / args.pcie_steps
+        pcie = {"value": args.samples / (pms * 1e-3), "unit": "samples/s", "ms_per_step": pms,
+                "path": "vn_ingest_host from pageable host arrays: host checks + pinned staging + H2D + kernels"}
     elapsed = group.max(elapsed)                                  # max over ranks
     total_samples = group.sum(float(args.samples)) * args.steps  # every rank's shard stream
     ms_per_step = elapsed * 1e3 / args.steps
@@ -217,6 +236,7 @@ def main():
         "path": {"algorithmic_bytes_per_step": path_bytes, "effective_GBs": path_gbs,
                  "frac_of_hbm_peak": path_gbs / HBM_PEAK_GBS,
                  "phase_ms_serialised": phase, "ms_per_step_serialised": round(sum(phase.values()), 4)},
+        "pcie_inclusive": pcie,
     }
 
     # ---- CPU baseline + full-scale parity (rank 0, N=1)
