@@ -157,16 +157,6 @@ def main():
     sync()
     barrier()
     elapsed = time.perf_counter() - t0
-    # per-kernel timing (HIP events on the engine's stream) from extra, untimed steps: with
-    # timing on, the side-stream classes run serialised so every launch is measured alone
-    eng.timing_enable(True)
-    tim = []
-    for _ in range(max(1, args.timing_steps)):
-        last = step()  # every step flushes the same window: parity below reads the latest result
-        tim.append(eng.timing())
-    eng.timing_enable(False)
-    for _ in range(args.profile_steps):
-        last = step()
     # PCIe-inclusive rate (never `value`): the same window handed over as pageable host arrays
     # through vn_ingest_host (host-side checks, pinned staging, H2D copies, then the same kernels)
     pcie = None
@@ -184,6 +174,16 @@ def main():
         pms = (time.perf_counter() - tp) * 1e3 / args.pcie_steps
         pcie = {"value": args.samples / (pms * 1e-3), "unit": "samples/s", "ms_per_step": pms,
                 "path": "vn_ingest_host from pageable host arrays: host checks + pinned staging + H2D + kernels"}
+    # per-kernel timing (HIP events on the engine's stream) from extra, untimed steps: with
+    # timing on, the side-stream classes run serialised so every launch is measured alone
+    eng.timing_enable(True)
+    tim = []
+    for _ in range(max(1, args.timing_steps)):
+        last = step()  # every step flushes the same window: parity below reads the latest result
+        tim.append(eng.timing())
+    eng.timing_enable(False)
+    for _ in range(args.profile_steps):
+        last = step()
     elapsed = group.max(elapsed)                                  # max over ranks
     total_samples = group.sum(float(args.samples)) * args.steps  # every rank's shard stream
     ms_per_step = elapsed * 1e3 / args.steps
