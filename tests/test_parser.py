@@ -102,3 +102,56 @@ def test_datagram_to_workers():  # server.go:612-722
             assert W.metric_digest(k) % 3 == i and k.joined_tags == "env:a"
             got[k.name] = c.value
     assert got == {"c%d" % j: sum(2 * i for i in range(40) if i % 5 == j) for j in range(5)}
+
+
+@pytest.mark.gpu
+def test_gpu_dogstatsd_text_through_worker_matches_oracle():
+    """DogStatsD datagrams -> read_metric_datagram -> Worker on the engine, against the restated
+    Go worker fed with the generator's own values (not the parser's)."""
+    import oracle
+    from tests.test_worker import feed
+    rng = np.random.default_rng(5)
+    types = {"counter": b"c", "gauge": b"g", "histogram": b"h", "timer": b"ms", "set": b"s"}
+    scope_tag = {W.MetricScope.MixedScope: b"", W.MetricScope.LocalOnly: b",veneurlocalonly",
+                 W.MetricScope.GlobalOnly: b",veneurglobalonly"}
+    keys = [("m%d" % i, t, W.MetricScope(int(rng.integers(0, 3)))) for i, t in enumerate(list(types) * 6)]
+    cls_of = {"counter": 0, "gauge": 1, "histogram": 2, "timer": 2, "set": 3}
+    w = W.Worker(capacity=(64, 64, 64, 64), percentiles=(0.5, 0.9, 0.99), batch_records=4096)
+    o = oracle.Worker(64, 64, 64, 64)
+    slots, nxt = {}, [0, 0, 0, 0]
+    try:
+        lines = []
+        for _ in range(3000):
+            name, typ, sc = keys[int(rng.integers(0, len(keys)))]
+            rtxt = [b"1", b"0.5", b"0.1"][int(rng.integers(0, 3))]
+            if typ == "set":
+                v = "u%d" % rng.integers(0, 500)
+                vtxt = v.encode()
+            else:
+                vtxt = b"%.3f" % rng.lognormal(3, 1)
+                v = float(vtxt)
+            lines.append(b"%s:%s|%s|@%s|#zone:b,env:a%s" % (name.encode(), vtxt, types[typ], rtxt, scope_tag[sc]))
+            k = K(name, typ, "env:a,zone:b")
+            mp = W._map_for(typ, sc)
+            if (mp, k) not in slots:
+                slots[(mp, k)] = nxt[cls_of[typ]]
+                nxt[cls_of[typ]] += 1
+            feed(o, cls_of[typ], slots[(mp, k)], v, float(np.float32(float(rtxt))))
+        for i in range(0, len(lines), 25):  # datagrams of 25 lines
+            assert P.read_metric_datagram([w], b"\n".join(lines[i:i + 25])) == []
+        wm = w.Flush()
+        for (mp, k), s in slots.items():
+            smp = getattr(wm, mp)[k]
+            cls = cls_of[k.type]
+            if cls == 0:
+                assert smp.value == o.counter_value(s)
+            elif cls == 1:
+                assert smp.value == o.gauge_value(s)
+            elif cls == 2:
+                assert (smp.local_weight, smp.local_min, smp.local_max) == tuple(o.histo_stats(s)[:3])
+                assert smp.quantile(0.99) == o.histo_quantile(s, 0.99)
+            else:
+                assert smp.estimate == o.set_estimate(s)
+            assert smp.tags == ["env:a", "zone:b"]
+    finally:
+        w.close()
