@@ -254,6 +254,27 @@ typedef struct {
 int vn_timing_enable(vn_engine* eng, int enable);
 int vn_get_timing(vn_engine* eng, vn_timing* out);
 
+/* DogStatsD metric lines (host code, no GPU): samplers/parser.go:186-307 ParseMetric over a
+ * datagram split on '\n' (server.go:706-714), empty packets skipped (server.go:612-616).
+ * Returns the number of non-empty lines written to out (<0 on error); joined sorted tags go to
+ * tags_out. Replaces the Go parse in front of vn_stage_acquire/vn_submit. */
+enum {
+  VN_PARSE_OK = 0, VN_PARSE_NO_COLON, VN_PARSE_EMPTY_NAME, VN_PARSE_NO_PIPE, VN_PARSE_NO_TYPE,
+  VN_PARSE_BAD_TYPE, VN_PARSE_BAD_VALUE, VN_PARSE_EMPTY_SECTION, VN_PARSE_MULTI_RATE,
+  VN_PARSE_BAD_RATE, VN_PARSE_RATE_RANGE, VN_PARSE_MULTI_TAGS, VN_PARSE_UNKNOWN_SECTION,
+  VN_PARSE_NOT_METRIC, VN_PARSE_TAGS_FULL
+};
+typedef struct {
+  uint64_t line_off, name_off, value_off, tags_off; /* name/value into buf, tags into tags_out */
+  double value;                                     /* non-set types */
+  uint32_t line_len, name_len, value_len, tags_len, n_tags, digest;
+  float rate;
+  int32_t status;                                   /* VN_PARSE_* */
+  uint8_t type, scope, has_tags, pad;               /* type: counter gauge histogram timer set */
+} vn_parsed_line;
+int64_t vn_parse_dogstatsd(const char* buf, uint64_t len, vn_parsed_line* out, uint64_t max_lines,
+                           char* tags_out, uint64_t tags_cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -155,3 +155,42 @@ def test_gpu_dogstatsd_text_through_worker_matches_oracle():
             assert smp.tags == ["env:a", "zone:b"]
     finally:
         w.close()
+
+
+def _mutations(rng, n):
+    base = [b"a.b.c:1|c", b"x:2.5|g|@0.25|#b:1,a:2", b"t:3e2|ms|#veneurlocalonly,z", b"s:m1|s|#veneurglobalonly",
+            b"h:-0.5|h|@1|#", b"q:1.00000005960464477539062500000000001|c|@1.00000005960464477539062500000000001"]
+    alphabet = b"|:@#,.e+-0123456789abcghmsnaif\n"
+    out = list(INVALID) + base
+    for _ in range(n):
+        b = bytearray(base[int(rng.integers(0, len(base)))])
+        for _ in range(int(rng.integers(1, 4))):
+            i = int(rng.integers(0, len(b) + 1))
+            op = int(rng.integers(0, 3))
+            if op == 0:
+                b.insert(i, alphabet[int(rng.integers(0, len(alphabet)))])
+            elif op == 1 and i < len(b):
+                del b[i]
+            elif i < len(b):
+                b[i] = alphabet[int(rng.integers(0, len(alphabet)))]
+        out.append(bytes(b))
+    return out
+
+
+def test_native_parse_matches_python_mirror():  # vn_parse_dogstatsd vs parse_metric, line by line
+    rng = np.random.default_rng(3)
+    lines = [l for l in _mutations(rng, 4000) if b"\n" not in l and l]
+    got = P.parse_datagram_native(b"\n".join(lines))
+    assert len(got) == len(lines)
+    for line, g in zip(lines, got):
+        try:
+            m = P.parse_metric(line) if not line.startswith((b"_e{", b"_sc")) else None
+        except P.ParseError:
+            m = None
+        if m is None:
+            assert isinstance(g, int) and g > 0, line
+        else:
+            assert not isinstance(g, int), (line, g)
+            assert (g.key, g.digest, g.scope, g.tags) == (m.key, m.digest, m.scope, m.tags), line
+            assert g.sample_rate == m.sample_rate or (np.isnan(g.sample_rate) and np.isnan(m.sample_rate)), line
+            assert g.value == m.value or (isinstance(m.value, float) and np.signbit(g.value) == np.signbit(m.value)), line

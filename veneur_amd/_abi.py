@@ -152,6 +152,18 @@ _sig("vn_sync", C.c_int, vp)
 _sig("vn_read_histo", C.c_int, vp, C.c_uint32, f64p, f64p, C.c_uint32, u32p, f64p)
 _sig("vn_read_set", C.c_int, vp, C.c_uint32, C.POINTER(SetState), u32p, C.c_uint32, u32p, C.c_uint32, u8p)
 _sig("vn_metro64", C.c_int, C.c_int, u8p, u32p, C.c_uint64, C.c_uint64, u64p)
+
+
+class ParsedLine(C.Structure):  # vn_parsed_line
+    _fields_ = [("line_off", C.c_uint64), ("name_off", C.c_uint64), ("value_off", C.c_uint64),
+                ("tags_off", C.c_uint64), ("value", C.c_double), ("line_len", C.c_uint32),
+                ("name_len", C.c_uint32), ("value_len", C.c_uint32), ("tags_len", C.c_uint32),
+                ("n_tags", C.c_uint32), ("digest", C.c_uint32), ("rate", C.c_float), ("status", C.c_int32),
+                ("type", C.c_uint8), ("scope", C.c_uint8), ("has_tags", C.c_uint8), ("pad", C.c_uint8)]
+
+
+_sig("vn_parse_dogstatsd", C.c_int64, C.c_char_p, C.c_uint64, C.POINTER(ParsedLine), C.c_uint64, C.c_char_p,
+     C.c_uint64)
 _sig("vn_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(vp))
 _sig("vn_device_free", C.c_int, vp)
 _sig("vn_copy_to_device", C.c_int, C.c_int, vp, vp, C.c_uint64)
@@ -167,6 +179,6 @@ _sig("vn_synth_free", None, C.POINTER(SynthOut))
 EXPORTED = [
     "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
     "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_sync",
-    "vn_read_histo", "vn_read_set", "vn_metro64", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
+    "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
 ]

@@ -198,3 +198,34 @@ def read_metric_datagram(workers, datagram: bytes) -> List[Exception]:
         except ParseError as e:
             errs.append(e)
     return errs
+
+
+_NTYPES = ("counter", "gauge", "histogram", "timer", "set")
+
+
+def parse_datagram_native(datagram: bytes):
+    """vn_parse_dogstatsd (veneur_amd/csrc/parse.cpp): the C-ABI parse of a whole datagram.
+    Returns one entry per non-empty line: a UDPMetric, or the VN_PARSE_* error code (int)."""
+    import ctypes as C
+
+    from . import _abi as A
+    n_max = datagram.count(b"\n") + 1
+    out = (A.ParsedLine * n_max)()
+    tags = C.create_string_buffer(len(datagram) + 1)
+    n = A.lib.vn_parse_dogstatsd(datagram, len(datagram), out, n_max, tags, len(datagram) + 1)
+    if n < 0:
+        raise ParseError("vn_parse_dogstatsd failed (%d)" % n)
+    res, tb = [], tags.raw
+    dec = lambda b: b.decode("utf-8", "surrogateescape")  # noqa: E731
+    for o in out[:n]:
+        if o.status:
+            res.append(int(o.status))
+            continue
+        typ = _NTYPES[o.type]
+        name = datagram[o.name_off:o.name_off + o.name_len]
+        joined = tb[o.tags_off:o.tags_off + o.tags_len]
+        val = dec(datagram[o.value_off:o.value_off + o.value_len]) if typ == "set" else o.value
+        tl = [dec(t) for t in joined.split(b",")] if o.has_tags and o.n_tags else []
+        res.append(UDPMetric(MetricKey(dec(name), typ, dec(joined)), val, np.float32(o.rate), digest=o.digest,
+                             tags=tl, scope=MetricScope(o.scope)))
+    return res
