@@ -164,9 +164,14 @@ const char* vn_last_error(const vn_engine* eng);
 int vn_abi_version(void);
 
 int vn_stage_acquire(vn_engine* eng, vn_stage* out);
-int vn_submit(vn_engine* eng, const vn_batch_counts* counts);  /* stage -> HBM -> ingest */
+/* stage -> HBM -> ingest; returns once the stage has been copied (it may be refilled at once) */
+int vn_submit(vn_engine* eng, const vn_batch_counts* counts);
 int vn_ingest_host(vn_engine* eng, const vn_batch* host_batch);  /* copies through the stage */
-int vn_ingest(vn_engine* eng, const vn_batch* device_batch);     /* inputs already in HBM */
+/* Inputs already in HBM.  The batch is validated on the device before anything is applied --
+ * slots within capacity, histo values finite (merging_digest.go:98-100), counter / histo rates
+ * in (0, 1], set member offsets non-decreasing -- and a faulty batch fails with VN_EINVAL and
+ * leaves the window unchanged (vn_ingest_host checks the same on the host). */
+int vn_ingest(vn_engine* eng, const vn_batch* device_batch);
 
 /* ImportMetric for decoded values (Counter.Combine adds int64, Gauge.Combine overwrites in
  * arrival order); they target the GlobalOnly slot tables the host chose. */
@@ -221,6 +226,14 @@ int vn_export_histos(vn_engine* eng, const uint32_t* slot, uint64_t n, vn_export
 int vn_export_sets(vn_engine* eng, const uint32_t* slot, uint64_t n, vn_export* out);
 
 int vn_flush(vn_engine* eng, vn_flush_result* out);
+/* vn_flush for a local veneur (flusher.go:41-48,168-230): the percentiles of a histogram are
+ * evaluated only where histo_quantile_mask[slot] != 0 (the others come back NaN: Server.Flush
+ * passes percentiles=nil for mixed-scope histograms and timers, whose digests are forwarded
+ * instead), and a set is estimated only where set_estimate_mask[slot] != 0 (mixed-scope sets
+ * are forwarded, not flushed; their estimate comes back 0).  Either mask may be NULL (= all);
+ * otherwise it holds capacity[VN_HISTO] / capacity[VN_SET] bytes. */
+int vn_flush_masked(vn_engine* eng, const uint8_t* histo_quantile_mask, const uint8_t* set_estimate_mask,
+                    vn_flush_result* out);
 int vn_sync(vn_engine* eng);
 
 /* Introspection of the current (unflushed) window. */

@@ -130,3 +130,98 @@ def test_key_touched_only_by_imports():  # worker.go:237-242: imports Upsert the
     assert f.histo_quantiles[0].tolist() == [w.histo_quantile(1, p) for p in PCT]
     assert f.set_estimate.tolist() == [w.set_estimate(1)]
     assert f.samples_imported == 4 and f.samples_processed == 0
+
+
+def _device_batch(bufs, **cls):
+    """An A.Batch whose arrays are copied to device memory (kept alive in bufs)."""
+    import veneur_amd._abi as A
+
+    def dev(a):
+        b = V.DeviceBuffer(a)
+        bufs.append(b)
+        return b.ptr.value
+
+    b = A.Batch()
+    if "counters" in cls:
+        s, v, r = cls["counters"]
+        b.n_counter, b.counter_slot, b.counter_value, b.counter_rate = len(s), dev(s), dev(v), dev(r)
+    if "gauges" in cls:
+        s, v = cls["gauges"]
+        b.n_gauge, b.gauge_slot, b.gauge_value = len(s), dev(s), dev(v)
+    if "histos" in cls:
+        s, v, r = cls["histos"]
+        b.n_histo, b.histo_slot, b.histo_value, b.histo_rate = len(s), dev(s), dev(v), dev(r)
+    if "sets" in cls:
+        s, o, m = cls["sets"]
+        b.n_set, b.set_slot, b.set_member_off, b.set_member_bytes = len(s), dev(s), dev(o), dev(m)
+    return b
+
+
+@pytest.mark.parametrize("fault", ["counter_slot", "gauge_slot", "histo_slot", "set_slot", "histo_nan",
+                                   "histo_inf", "histo_rate_zero", "counter_rate_big", "counter_rate_nan",
+                                   "set_offsets"])
+def test_device_batch_validation_rejects_and_leaves_state(fault):
+    """vn_ingest validates a device-resident batch before applying anything (VN_EINVAL)."""
+    n, cap = 4096, 64
+    rng = np.random.default_rng(3)
+    slots = rng.integers(0, cap, n).astype(np.uint32)
+    vals = np.round(rng.lognormal(3, 1, n), 3)
+    rates = np.ones(n, np.float32)
+    members = [("m%d" % i).encode() for i in rng.integers(0, 500, n)]
+    off = np.zeros(n + 1, np.uint32)
+    off[1:] = np.cumsum([len(m) for m in members])
+    mb = np.frombuffer(b"".join(members), np.uint8).copy()
+    good = dict(counters=(slots, vals, rates), gauges=(slots, vals), histos=(slots, vals, rates),
+                sets=(slots, off, mb))
+    bad = {k: tuple(a.copy() for a in v) for k, v in good.items()}
+    i = n // 2
+    if fault.endswith("_slot"):
+        bad[{"counter": "counters", "gauge": "gauges", "histo": "histos", "set": "sets"}[fault[:-5]]][0][i] = cap
+    elif fault == "histo_nan":
+        bad["histos"][1][i] = np.nan
+    elif fault == "histo_inf":
+        bad["histos"][1][i] = -np.inf
+    elif fault == "histo_rate_zero":
+        bad["histos"][2][i] = 0.0
+    elif fault == "counter_rate_big":
+        bad["counters"][2][i] = 1.5
+    elif fault == "counter_rate_nan":
+        bad["counters"][2][i] = np.nan
+    elif fault == "set_offsets":
+        bad["sets"][1][i] = bad["sets"][1][i + 1] + 1
+    bufs = []
+    with make_engine((cap,) * 4) as e, make_engine((cap,) * 4) as ref:
+        e.ingest_device(_device_batch(bufs, **good))
+        with pytest.raises(V.EngineError, match="out of range|invalid value|sample rate|offsets"):
+            e.ingest_device(_device_batch(bufs, **bad))
+        ref.ingest(**good)
+        fe, fr = e.flush(), ref.flush()
+    for b in bufs:
+        b.free()
+    assert fe.samples_processed == fr.samples_processed == 4 * n
+    np.testing.assert_array_equal(fe.counter_value, fr.counter_value)
+    np.testing.assert_array_equal(fe.gauge_value, fr.gauge_value)
+    np.testing.assert_array_equal(fe.histo_quantiles, fr.histo_quantiles)
+    np.testing.assert_array_equal(fe.histo_stats, fr.histo_stats)
+    np.testing.assert_array_equal(fe.set_estimate, fr.set_estimate)
+
+
+def test_submit_counter_only_batch_then_refill_stage():
+    """vn_submit returns once the pinned stage has been copied: refilling it at once for the next
+    batch (as the cgo binding in INTEGRATION.md does) cannot change what the first one ingested."""
+    rng = np.random.default_rng(11)
+    batches = [(rng.integers(0, 100, 50000).astype(np.uint32), rng.integers(1, 10, 50000).astype(np.float64))
+               for _ in range(4)]
+    with make_engine((100, 1, 1, 1), max_records=1 << 16) as e:
+        st = e.stage()
+        for s, v in batches:
+            st["counter_slot"][:len(s)] = s
+            st["counter_value"][:len(s)] = v
+            st["counter_rate"][:len(s)] = 1.0
+            e.submit(n_counter=len(s))
+        f = e.flush()
+    exp = np.zeros(100, np.int64)
+    for s, v in batches:
+        np.add.at(exp, s, v.astype(np.int64))
+    assert f.counter_slot.tolist() == np.nonzero(exp)[0].tolist()
+    np.testing.assert_array_equal(f.counter_value, exp[f.counter_slot])

@@ -24,9 +24,13 @@ class RecordingEngine:
     def __init__(self, capacity=(8, 8, 8, 8), percentiles=(0.5, 0.9)):
         self.capacity, self.percentiles, self.calls = capacity, percentiles, []
         self.cval = {}
+        self.hvals = {}
 
     def ingest(self, **kw):
         self.calls.append(("ingest", {k: [a.tolist() for a in v] for k, v in kw.items()}))
+        if "histos" in kw:
+            for s, v, r in zip(*kw["histos"]):
+                self.hvals.setdefault(int(s), []).append(float(v))
         if "counters" in kw:
             for s, v, r in zip(*kw["counters"]):
                 self.cval[int(s)] = self.cval.get(int(s), 0) + int(v) * int(np.float32(1) / r)
@@ -46,14 +50,25 @@ class RecordingEngine:
     def import_sets(self, slot, p):
         self.calls.append(("import_sets", slot.tolist()))
 
-    def flush(self):
+    def export_histos(self, slots):
+        return [b"gob%d" % s for s in slots]
+
+    def export_sets(self, slots):
+        return [b"hll%d" % s for s in slots]
+
+    def flush(self, histo_quantile_mask=None, set_estimate_mask=None):
         self.calls.append(("flush",))
+        self.masks = (histo_quantile_mask, set_estimate_mask)
         cs = sorted(self.cval)
+        hs = sorted(self.hvals)
         z = np.zeros(0, np.uint32)
+        hst = np.array([[len(v), min(v), max(v), sum(v), sum(1 / x for x in v), min(v), max(v), len(v)]
+                        for v in (self.hvals[s] for s in hs)]).reshape(-1, 8)
         out = FlushOutput(np.array(cs, np.uint32), np.array([self.cval[s] for s in cs], np.int64), z, np.zeros(0),
-                          z, np.zeros((0, 8)), np.zeros((0, len(self.percentiles))), z, np.zeros(0, np.uint64),
-                          np.zeros(0, np.uint8), 0, 0)
+                          np.array(hs, np.uint32), hst, np.full((len(hs), len(self.percentiles)), 1.0), z,
+                          np.zeros(0, np.uint64), np.zeros(0, np.uint8), 0, 0)
         self.cval = {}
+        self.hvals = {}
         return out
 
 
@@ -290,3 +305,152 @@ def feed(o, cls, s, v, rate):
     else:
         b = v.encode()
         o.set(one, np.array([0, len(b)], np.uint32), np.frombuffer(b, np.uint8))
+
+
+def _names(ims):
+    return sorted(m.name for m in ims)
+
+
+def test_generate_inter_metrics_local_and_global_rules():
+    """generateInterMetrics (flusher.go:168-230): a local veneur flushes no percentiles of mixed
+    histograms/timers, no mixed sets, global counters or global gauges -- those are forwarded --
+    while local-only histograms keep their percentiles; a global veneur flushes everything."""
+    def feed(w):
+        for v in (1.0, 2.0, 7.0, 8.0, 100.0):
+            w.ProcessMetric(W.UDPMetric(K("a.b.c", "histogram"), v))                              # mixed
+            w.ProcessMetric(W.UDPMetric(K("l.h", "histogram"), v, scope=W.MetricScope.LocalOnly))
+            w.ProcessMetric(W.UDPMetric(K("t.m", "timer"), v))
+        for _ in range(40):
+            w.ProcessMetric(W.UDPMetric(K("x.y.z", "counter"), 1.0, scope=W.MetricScope.LocalOnly))
+        w.ProcessMetric(W.UDPMetric(K("g.c", "counter"), 3.0, scope=W.MetricScope.GlobalOnly))
+        w.ProcessMetric(W.UDPMetric(K("g.g", "gauge"), 3.0, scope=W.MetricScope.GlobalOnly))
+        w.ProcessMetric(W.UDPMetric(K("s", "set"), "a"))
+        w.ProcessMetric(W.UDPMetric(K("ls", "set"), "a", scope=W.MetricScope.LocalOnly))
+
+    pct = (0.5, 0.75, 0.99)
+    w = W.Worker(engine=RecordingEngine(percentiles=pct), batch_records=1000, percentiles=pct)
+    feed(w)
+    final, fwd = W.server_flush([w], True, pct)
+    assert _names(final) == sorted(["x.y.z", "a.b.c.max", "a.b.c.min", "a.b.c.count", "t.m.max", "t.m.min",
+                                    "t.m.count", "l.h.max", "l.h.min", "l.h.count", "l.h.50percentile",
+                                    "l.h.75percentile", "l.h.99percentile", "ls"])
+    assert sorted((m.key.name, m.key.type) for m in fwd) == [("a.b.c", "histogram"), ("g.c", "counter"),
+                                                              ("g.g", "gauge"), ("s", "set"), ("t.m", "timer")]
+    qmask, emask = w.engine.masks
+    win_slots = {"a.b.c": 0, "l.h": 1, "t.m": 2}  # histo slots in upsert order
+    assert qmask[win_slots["l.h"]] == 1 and qmask[win_slots["a.b.c"]] == 0 and qmask[win_slots["t.m"]] == 0
+    assert emask[0] == 0 and emask[1] == 1  # sets: "s" (mixed) then "ls" (local-only)
+
+    g = W.Worker(engine=RecordingEngine(percentiles=pct), batch_records=1000, percentiles=pct)
+    feed(g)
+    final, fwd = W.server_flush([g], False, pct)
+    assert fwd == [] and g.engine.masks == (None, None)
+    names = _names(final)
+    for n in ("a.b.c.50percentile", "t.m.99percentile", "s", "g.c", "g.g", "ls", "l.h.75percentile"):
+        assert n in names
+
+
+def test_nan_sample_rate_drops_one_record_not_the_batch():
+    """A NaN rate passes the parser (parser.go:262-272, both comparisons false); the Worker
+    drops that one record and keeps the rest of the staged batch."""
+    from veneur_amd import parser as P
+    w = W.Worker(engine=RecordingEngine(capacity=(8, 8, 8, 8)), batch_records=4)
+    lines = [b"a:1|c", b"a:2|c|@nan", b"b:5|h|@nan", b"a:3|c", b"a:4|c", b"a:5|c"]
+    for ln in lines:
+        m = P.parse_metric(ln)
+        w.ProcessMetric(m)
+    assert w.dropped == 2
+    wm = w.Flush()
+    assert wm.counters[K("a", "counter")].value == 1 + 3 + 4 + 5
+    assert K("b", "histogram") not in wm.histograms
+
+
+def test_non_utf8_set_member_and_name_bytes():
+    """Invalid UTF-8 in a set member or name reaches the engine as the raw bytes (Go inserts the
+    bytes into the HLL and hashes them into the digest)."""
+    from veneur_amd import parser as P
+    w = W.Worker(engine=RecordingEngine(), batch_records=1000)
+    m = P.parse_metric(b"s\xfe:\xff\x80|s")
+    w.ProcessMetric(m)
+    assert W.metric_digest(m.key) == oracle.fnv1a32(b"s\xfe", b"set", b"")
+    w._drain()
+    call = [c for c in w.engine.calls if c[0] == "ingest"][-1][1]
+    assert bytes(call["sets"][2]) == b"\xff\x80"
+
+
+def test_set_member_bytes_drain_before_engine_limit():
+    """Long members: the staged member bytes never pass the engine's max_batch_member_bytes."""
+    eng = RecordingEngine()
+    eng.max_batch_member_bytes = 1000
+    w = W.Worker(engine=eng, batch_records=10000)
+    for i in range(200):
+        w.ProcessMetric(W.UDPMetric(K("s", "set"), ("%03d" % i) * 30))  # 90-byte members
+    w.Flush()
+    sizes = [len(c[1]["sets"][2]) for c in eng.calls if c[0] == "ingest" and "sets" in c[1]]
+    assert sum(sizes) == 200 * 90 and max(sizes) <= 1000
+
+
+def test_import_lone_surrogate_name_is_replaced():
+    """encoding/json decodes an escaped lone surrogate as U+FFFD (the digest must not crash)."""
+    from veneur_amd import http_import as H
+    body = b'[{"name":"a\\ud800b","type":"counter","tagstring":"","tags":null,"value":"AQAAAAAAAAA="}]'
+    ms = H.unmarshal_metrics_from_http(body, "")
+    assert ms[0].key.name == "a\ufffdb"
+    W.metric_digest(ms[0].key)
+
+
+@pytest.mark.gpu
+def test_gpu_local_and_global_server_flush():
+    """server_test.go TestLocalServerMixedMetrics (303-416), TestLocalServerUnaggregatedMetrics
+    (239-270) and TestGlobalServerFlush (272-301) through the engine: percentiles [.5 .75 .99],
+    aggregates min/max/count."""
+    from veneur_amd import http_import as H
+    pct = (0.5, 0.75, 0.99)
+    vals = (1.0, 2.0, 7.0, 8.0, 100.0)
+    # local veneur: mixed histogram forwarded (no percentiles on the engine), local counter flushed
+    w = W.Worker(capacity=(64, 64, 64, 64), percentiles=pct, batch_records=4096)
+    try:
+        for v in vals:
+            w.ProcessMetric(W.UDPMetric(K("a.b.c", "histogram"), v, 1.0, digest=12345))
+        for _ in range(40):
+            w.ProcessMetric(W.UDPMetric(K("x.y.z", "counter"), 1.0, 1.0, digest=12345, scope=W.MetricScope.LocalOnly))
+        w.ProcessMetric(W.UDPMetric(K("s", "set"), "m"))
+        final, fwd = W.server_flush([w], True, pct)
+        byname = {m.name: m.value for m in final}
+        assert byname == {"x.y.z": 40.0, "a.b.c.max": 100.0, "a.b.c.min": 1.0, "a.b.c.count": 5.0}
+        assert [(m.key.name, m.key.type) for m in fwd] == [("a.b.c", "histogram"), ("s", "set")]
+        # the global receives the histogram's digest: centroids {1,2,7,8,100}, min 1, max 100
+        exp = oracle.MergingDigest(100.0)
+        with open("tests/golden/tdigest_1_2_7_8_100.gob", "rb") as fh:
+            exp.gob_decode(fh.read())
+        got = oracle.MergingDigest(100.0)
+        got.gob_decode(fwd[0].value)
+        for a, b in zip(got.centroids(), exp.centroids()):
+            np.testing.assert_array_equal(a, b)
+        assert (got.min(), got.max(), got.count()) == (1.0, 100.0, 5.0)
+        # the global veneur: import the forward, flush everything
+        g = W.Worker(capacity=(64, 64, 64, 64), percentiles=pct, batch_records=4096)
+        try:
+            H.import_metrics([g], fwd)
+            final, fwd2 = W.server_flush([g], False, pct)
+            byname = {m.name: m.value for m in final}
+            assert fwd2 == []
+            assert (byname["a.b.c.50percentile"], byname["a.b.c.75percentile"], byname["a.b.c.99percentile"]) == \
+                (6.0, 42.375, 97.7)
+            assert byname["s"] == 1.0
+            assert "a.b.c.count" not in byname  # imported digests carry no Local* weight
+        finally:
+            g.close()
+        # local-only histogram on a local veneur: 3 aggregates + 3 percentiles
+        for v in vals:
+            w.ProcessMetric(W.UDPMetric(K("a.b.c", "histogram"), v, scope=W.MetricScope.LocalOnly))
+        final, fwd = W.server_flush([w], True, pct)
+        assert len(final) == 6 and fwd == []
+        # global veneur flush of the same samples
+        for v in vals:
+            w.ProcessMetric(W.UDPMetric(K("a.b.c", "histogram"), v, scope=W.MetricScope.LocalOnly))
+        final, _ = W.server_flush([w], False, pct)
+        byname = {m.name: m.value for m in final}
+        assert len(final) == 6 and byname["a.b.c.max"] == 100.0 and byname["a.b.c.50percentile"] == 6.0
+    finally:
+        w.close()

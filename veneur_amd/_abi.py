@@ -148,6 +148,7 @@ _sig("vn_histo_query", C.c_int, vp, C.c_int, u32p, f64p, C.c_uint64, f64p)
 _sig("vn_export_histos", C.c_int, vp, u32p, C.c_uint64, C.POINTER(Export))
 _sig("vn_export_sets", C.c_int, vp, u32p, C.c_uint64, C.POINTER(Export))
 _sig("vn_flush", C.c_int, vp, C.POINTER(FlushResult))
+_sig("vn_flush_masked", C.c_int, vp, u8p, u8p, C.POINTER(FlushResult))
 _sig("vn_sync", C.c_int, vp)
 _sig("vn_read_histo", C.c_int, vp, C.c_uint32, f64p, f64p, C.c_uint32, u32p, f64p)
 _sig("vn_read_set", C.c_int, vp, C.c_uint32, C.POINTER(SetState), u32p, C.c_uint32, u32p, C.c_uint32, u8p)
@@ -178,7 +179,7 @@ _sig("vn_synth_free", None, C.POINTER(SynthOut))
 # every symbol include/*.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
     "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
-    "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_sync",
+    "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_flush_masked", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
 ]

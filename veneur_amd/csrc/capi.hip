@@ -1,6 +1,5 @@
 // capi.hip -- engine lifetime and the C-ABI of include/veneur_amd.h.
 #include <algorithm>
-#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -114,6 +113,7 @@ void create_impl(vn_engine* e) {
   VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st4, hipStreamNonBlocking, prio_hi));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join4, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork3, hipEventDisableTiming));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_h2d, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join3, hipEventDisableTiming));
   hipStream_t st = e->st;
   const uint64_t R = e->max_records;
@@ -245,6 +245,8 @@ void create_impl(vn_engine* e) {
   dalloc(e->f_sest, cs); halloc(e->hf_sest, cs);
   dalloc(e->f_ssparse, cs); halloc(e->hf_ssparse, cs);
   dalloc(e->d_pct, VN_MAX_PERCENTILES);
+  dalloc(e->f_hmask, ch);
+  dalloc(e->f_smask, cs);
   VN_HIP_CHECK(hipMemcpyAsync(e->d_pct, e->cfg.percentiles, sizeof(double) * VN_MAX_PERCENTILES,
                               hipMemcpyHostToDevice, st));
   halloc(e->hf_cnt, 16);
@@ -394,6 +396,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->f_cnt); dfree(e->f_cval); hfree(e->hf_cval); dfree(e->f_gval); hfree(e->hf_gval);
   dfree(e->f_hstats); hfree(e->hf_hstats); dfree(e->f_hq); hfree(e->hf_hq); dfree(e->f_sest); hfree(e->hf_sest);
   dfree(e->f_ssparse); hfree(e->hf_ssparse); dfree(e->d_pct); hfree(e->hf_cnt);
+  dfree(e->f_hmask); dfree(e->f_smask);
   radix_scratch_free(e->rs);
   radix_scratch_free(e->rs2);
   radix_scratch_free(e->rs3);
@@ -408,6 +411,7 @@ void destroy_impl(vn_engine* e) {
   if (e->ev_join4) (void)hipEventDestroy(e->ev_join4);
   if (e->st4) (void)hipStreamDestroy(e->st4);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);
+  if (e->ev_h2d) (void)hipEventDestroy(e->ev_h2d);
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->st2) (void)hipStreamDestroy(e->st2);
   for (auto ev : e->pool_storage) (void)hipEventDestroy(ev);
@@ -422,6 +426,63 @@ void check_error_flags(vn_engine* e) {
   if (flags & 1u) throw std::runtime_error("t-digest centroid tile overflow (compression too large for cap_cent)");
   if (flags & 2u) throw std::runtime_error("HLL rebase invariant violated");
   if (flags & 4u) throw std::runtime_error("t-digest chain window hand-off stalled");
+}
+
+// Validation of a device-resident batch (vn_ingest), where the reference would panic or the
+// parser would have rejected the line: slots within capacity (an interned key), histo values
+// neither NaN nor +-Inf (MergingDigest.Add panics, merging_digest.go:98-100), sample rates in
+// (0, 1] (parser.go:262-272; Counter.Sample / Histo.Sample divide by them), set member offsets
+// non-decreasing.  One pass over the batch, flags in h_err[1]; the host reads them before any
+// state-mutating kernel is queued, so a rejected batch leaves the window untouched.
+constexpr uint32_t kBadSlot = 1u, kBadValue = 2u, kBadRate = 4u, kBadOffsets = 8u;
+__global__ void k_validate_batch(vn_batch b, uint32_t cc, uint32_t cg, uint32_t ch, uint32_t cs,
+                                 uint32_t* __restrict__ err) {
+  const uint64_t nmax = max(max(b.n_counter, b.n_gauge), max(b.n_histo, b.n_set));
+  uint32_t f = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nmax; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (i < b.n_counter) {
+      const float r = b.counter_rate[i];
+      if (b.counter_slot[i] >= cc) f |= kBadSlot;
+      if (!(r > 0.0f && r <= 1.0f)) f |= kBadRate;
+    }
+    if (i < b.n_gauge && b.gauge_slot[i] >= cg) f |= kBadSlot;
+    if (i < b.n_histo) {
+      const double v = b.histo_value[i];
+      const float r = b.histo_rate[i];
+      if (b.histo_slot[i] >= ch) f |= kBadSlot;
+      if (v != v || v - v != 0.0) f |= kBadValue;
+      if (!(r > 0.0f && r <= 1.0f)) f |= kBadRate;
+    }
+    if (i < b.n_set) {
+      if (b.set_slot[i] >= cs) f |= kBadSlot;
+      if (!b.set_hash && b.set_member_off[i + 1] < b.set_member_off[i]) f |= kBadOffsets;
+    }
+  }
+  // one atomic per wave that saw a fault
+  for (int d = 32; d >= 1; d >>= 1) f |= __shfl_xor(f, d, 64);
+  if (f && (threadIdx.x & 63) == 0) atomicOr(err, f);
+}
+
+void validate_device_batch(vn_engine* e, const vn_batch* b) {
+  const uint64_t nmax = std::max(std::max(b->n_counter, b->n_gauge), std::max(b->n_histo, b->n_set));
+  if (!nmax) return;
+  if ((b->n_counter && (!b->counter_slot || !b->counter_value || !b->counter_rate)) ||
+      (b->n_gauge && (!b->gauge_slot || !b->gauge_value)) ||
+      (b->n_histo && (!b->histo_slot || !b->histo_value || !b->histo_rate)) ||
+      (b->n_set && (!b->set_slot || (!b->set_hash && (!b->set_member_off || !b->set_member_bytes)))))
+    throw std::invalid_argument("batch class with records but a null array");
+  hipStream_t st = e->st;
+  VN_HIP_CHECK(hipMemsetAsync(e->h_err + 1, 0, sizeof(uint32_t), st));
+  const int grid = (int)std::min<uint64_t>(blocks_for(nmax, 256), 4096);
+  hipLaunchKernelGGL(k_validate_batch, dim3(grid), dim3(256), 0, st, *b, e->cap[VN_COUNTER], e->cap[VN_GAUGE],
+                     e->cap[VN_HISTO], e->cap[VN_SET], e->h_err + 1);
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 15, e->h_err + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  const uint32_t f = e->hf_cnt[15];
+  if (f & kBadSlot) throw std::invalid_argument("slot out of range");
+  if (f & kBadValue) throw std::invalid_argument("invalid value added");  // merging_digest.go:98-100
+  if (f & kBadRate) throw std::invalid_argument("sample rate must be >0 and <=1");
+  if (f & kBadOffsets) throw std::invalid_argument("set member offsets must be non-decreasing");
 }
 
 void ingest_device(vn_engine* e, const vn_batch* b) {
@@ -456,26 +517,16 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
     // counters, gauges and sets on the low-priority side stream (none of them waits on the
     // host); then the rest of the histo path, whose host round trips no longer hold back
     // the side work -- it fills the GPU while the replays and remainder rounds run
-    static const bool host_timing = std::getenv("VN_HOST_TIMING") != nullptr;  // enqueue-cost probe
-    auto now = [] { return std::chrono::duration<double, std::micro>(
-                        std::chrono::steady_clock::now().time_since_epoch()).count(); };
-    const double t0 = host_timing ? now() : 0.0;
     side_begin(e);  // the side stream waits for what the main stream held before this call
     const HistoGroups g = histo_group(e, b->n_histo, b->histo_slot, b->histo_value, b->histo_rate);
-    const double t1 = host_timing ? now() : 0.0;
     ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
     ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
     e->set_defer = true;  // histo_process queues the set merge after the remainder sort
     ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
     e->set_defer = false;
-    const double t2 = host_timing ? now() : 0.0;
     histo_process(e, b->n_histo, g);
-    const double t3 = host_timing ? now() : 0.0;
     set_finish(e);
     side_join(e);
-    if (host_timing)
-      std::fprintf(stderr, "[vn host] histo_group %.0f us, side enqueue %.0f us, histo_process %.0f us\n", t1 - t0,
-                   t2 - t1, t3 - t2);
   }
   if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[4], st));
   VN_HIP_CHECK(hipGetLastError());  // a launch that could not start (e.g. LDS over budget) fails loudly
@@ -538,6 +589,8 @@ void ingest_host(vn_engine* e, const vn_batch* b) {
       db.set_member_bytes = d.s_bytes;
     }
   }
+  // the pinned stage may be refilled as soon as its copies have been read (vn_submit waits)
+  VN_HIP_CHECK(hipEventRecord(e->ev_h2d, st));
   ingest_device(e, &db);
 }
 
@@ -611,8 +664,6 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
     return VN_EINVAL;
   }
   e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 32768u;
-  if (const char* v = std::getenv("VN_LPT")) e->lpt = (uint32_t)std::atoi(v);
-  if (const char* v = std::getenv("VN_EARLY_REPLAY")) e->early_replay = std::atoi(v) != 0;
   e->hot_prefix = std::min(e->exact_threshold, cfg->histo_hot_prefix ? cfg->histo_hot_prefix : 4096u);
   e->piece_growth = cfg->histo_piece_growth ? std::min(cfg->histo_piece_growth, 1000u) : 25u;
   e->temp_cap = temp_buffer_cap(e->cfg.compression);
@@ -659,7 +710,12 @@ int vn_submit(vn_engine* e, const vn_batch_counts* c) {
   b.n_histo = c->n_histo; b.histo_slot = p.histo_slot; b.histo_value = p.histo_value; b.histo_rate = p.histo_rate;
   b.n_set = c->n_set; b.set_slot = p.set_slot; b.set_member_off = p.set_member_off;
   b.set_member_bytes = p.set_member_bytes;
-  return guarded(e, [&] { ingest_host(e, &b); });
+  return guarded(e, [&] {
+    ingest_host(e, &b);
+    // the caller refills the engine-owned pinned stage right after this returns: wait until the
+    // DMA engine has read it (the kernels keep running)
+    VN_HIP_CHECK(hipEventSynchronize(e->ev_h2d));
+  });
 }
 
 int vn_ingest_host(vn_engine* e, const vn_batch* b) {
@@ -669,7 +725,13 @@ int vn_ingest_host(vn_engine* e, const vn_batch* b) {
 
 int vn_ingest(vn_engine* e, const vn_batch* b) {
   if (!e || !b) return VN_EINVAL;
-  return guarded(e, [&] { ingest_device(e, b); });
+  return guarded(e, [&] {
+    if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
+        b->n_set > e->max_records)
+      throw std::invalid_argument("batch larger than max_batch_records");
+    validate_device_batch(e, b);
+    ingest_device(e, b);
+  });
 }
 
 int vn_import_counters(vn_engine* e, const uint32_t* slot, const int64_t* value, uint64_t n) {
@@ -797,11 +859,14 @@ int vn_export_sets(vn_engine* e, const uint32_t* slot, uint64_t n, vn_export* ou
   return guarded(e, [&] { export_impl(e, VN_SET, slot, n, out); });
 }
 
-int vn_flush(vn_engine* e, vn_flush_result* out) {
+int vn_flush(vn_engine* e, vn_flush_result* out) { return vn_flush_masked(e, nullptr, nullptr, out); }
+
+int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint8_t* set_estimate_mask,
+                    vn_flush_result* out) {
   if (!e || !out) return VN_EINVAL;
   return guarded(e, [&] {
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[5], e->st));
-    flush_all(e, out);
+    flush_all(e, out, histo_quantile_mask, set_estimate_mask);
     VN_HIP_CHECK(hipGetLastError());
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[6], e->st));
     check_error_flags(e);

@@ -62,6 +62,7 @@ struct vn_engine {
   hipStream_t st = nullptr;       // main stream (histos, flush, staging copies)
   hipStream_t st2 = nullptr;      // side stream: counters, gauges and sets overlap the histo path
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_h2d = nullptr;    // recorded after a host batch's copies into HBM (vn_submit waits on it)
   // replay stream: the exact replay of the keys under the threshold runs here while the hot
   // keys' short prefix and remainder rounds run on st (st itself when timing is enabled)
   hipStream_t st3 = nullptr;
@@ -73,9 +74,6 @@ struct vn_engine {
   // set segment merge held back (ingest_device): the grouped set records are merged once the
   // histo path's remainder sort is done, so the long set kernel does not crowd it out
   bool set_defer = false, set_pending = false;
-  uint32_t lpt = 3;              // longest-first order: bit 0 set merge, bit 1 replay (VN_LPT overrides)
-  bool early_replay = true;      // replay of the keys under the threshold starts beside the remainder sort
-                                 // (VN_EARLY_REPLAY=0: after it)
   uint64_t set_pending_n = 0;
   const uint64_t* set_pending_R = nullptr;
   const uint64_t* set_pending_order = nullptr;  // LPT order of the pending set merge (or null)
@@ -214,6 +212,8 @@ struct vn_engine {
   uint64_t* f_sest = nullptr;
   uint8_t* f_ssparse = nullptr;
   double* d_pct = nullptr;
+  uint8_t* f_hmask = nullptr;    // flush masks (vn_flush_masked), cap[VN_HISTO] / cap[VN_SET] bytes
+  uint8_t* f_smask = nullptr;
   // pinned host copies of the flush result
   uint32_t* hf_list[VN_NCLASS] = {nullptr, nullptr, nullptr, nullptr};
   int64_t* hf_cval = nullptr;

@@ -148,7 +148,8 @@ __global__ __launch_bounds__(64 * kQWaves) void k_flush_histo(
     const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ list, const double* __restrict__ hst,
     const uint32_t* __restrict__ hncent, const uint8_t* __restrict__ hcur, const double* __restrict__ cm0,
     const double* __restrict__ cm1, const double* __restrict__ cw0, const double* __restrict__ cw1, uint32_t capc,
-    const double* __restrict__ pct, uint32_t npct, double* __restrict__ out_stats, double* __restrict__ out_q) {
+    const double* __restrict__ pct, uint32_t npct, const uint8_t* __restrict__ qmask, double* __restrict__ out_stats,
+    double* __restrict__ out_q) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t k = blockIdx.x * kQWaves + wv;
@@ -157,6 +158,10 @@ __global__ __launch_bounds__(64 * kQWaves) void k_flush_histo(
   const uint32_t s = list[k];
   const double* h = hst + (uint64_t)s * VN_HISTO_STATS;
   if (lane < VN_HISTO_STATS) out_stats[(uint64_t)k * VN_HISTO_STATS + lane] = h[lane];
+  if (qmask && !qmask[s]) {  // percentiles=nil for this histogram (flusher.go:41-48,181-188)
+    if (lane < npct) out_q[(uint64_t)k * npct + lane] = __builtin_nan("");
+    return;
+  }
   const uint8_t c = hcur[s];
   const double* m = (c ? cm1 : cm0) + (uint64_t)s * capc;
   const double* w = (c ? cw1 : cw0) + (uint64_t)s * capc;
@@ -219,12 +224,20 @@ __global__ __launch_bounds__(kBlock) void k_flush_set(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ lc, const uint32_t* __restrict__ tc,
                                                       const uint32_t* __restrict__ tmp,
                                                       const uint32_t* __restrict__ arena,
+                                                      const uint8_t* __restrict__ emask,
                                                       uint64_t* __restrict__ out_est, uint8_t* __restrict__ out_sparse) {
   __shared__ double s_tmp[4];
   __shared__ uint32_t s_red[4];
   const uint32_t k = blockIdx.x, t = threadIdx.x;
   if (k >= cnt[0]) return;
   const uint32_t s = list[k];
+  if (emask && !emask[s]) {  // a set a local veneur only forwards (flusher.go:206-211)
+    if (t == 0) {
+      out_est[k] = 0;
+      out_sparse[k] = mode[s] == 0;
+    }
+    return;
+  }
   const uint32_t* ar = arena + (uint64_t)s * kArenaWords;
   if (mode[s] == 0) {
     // mergeSparse then linearCount(2^25, 2^25 - count)   (hyperloglog.go:204-207, utils.go:53-56)
@@ -357,8 +370,20 @@ void init_state(vn_engine* e) {
     hipLaunchKernelGGL(k_init_set, dim3(blocks_for(e->cap[VN_SET], 256)), dim3(256), 0, st, e->cap[VN_SET], e->snz);
 }
 
-void flush_all(vn_engine* e, vn_flush_result* out) {
+void flush_all(vn_engine* e, vn_flush_result* out, const uint8_t* histo_qmask, const uint8_t* set_emask) {
   hipStream_t st = e->st;
+  // per-slot masks of the flush (vn_flush_masked): which histograms get percentiles, which sets
+  // an estimate; null = all
+  const uint8_t* qmask = nullptr;
+  const uint8_t* emask = nullptr;
+  if (histo_qmask && e->cap[VN_HISTO]) {
+    VN_HIP_CHECK(hipMemcpyAsync(e->f_hmask, histo_qmask, e->cap[VN_HISTO], hipMemcpyHostToDevice, st));
+    qmask = e->f_hmask;
+  }
+  if (set_emask && e->cap[VN_SET]) {
+    VN_HIP_CHECK(hipMemcpyAsync(e->f_smask, set_emask, e->cap[VN_SET], hipMemcpyHostToDevice, st));
+    emask = e->f_smask;
+  }
   uint32_t* touch[VN_NCLASS] = {e->ctouch, e->gtouch, e->htouch, e->stouch};
   for (int c = 0; c < VN_NCLASS; c++) {
     if (!e->cap[c]) {
@@ -389,7 +414,7 @@ void flush_all(vn_engine* e, vn_flush_result* out) {
   if (n[1]) VN_HIP_CHECK(hipMemcpyAsync(e->hf_gval, e->f_gval, n[1] * 8, hipMemcpyDeviceToHost, s2));
   if (cs && n[3]) {
     hipLaunchKernelGGL(k_flush_set, dim3(n[3]), dim3(kBlock), 0, st, e->f_cnt + 3, e->f_list[3], e->smode, e->sbase,
-                       e->slc, e->stc, e->stmp, e->sarena, e->f_sest, e->f_ssparse);
+                       e->slc, e->stc, e->stmp, e->sarena, emask, e->f_sest, e->f_ssparse);
     if (s2 != st) {
       VN_HIP_CHECK(hipEventRecord(e->ev_fork, st));
       VN_HIP_CHECK(hipStreamWaitEvent(s2, e->ev_fork, 0));
@@ -404,7 +429,7 @@ void flush_all(vn_engine* e, vn_flush_result* out) {
     hipLaunchKernelGGL(k_flush_histo, dim3(blocks_for(n[2], kQWaves)), dim3(64 * kQWaves),
                        sizeof(double) * kQWaves * e->cap_cent, st, e->f_cnt + 2, e->f_list[2],
                        e->hst, e->hncent, e->hcur, e->cmean[0], e->cmean[1], e->cw[0], e->cw[1], e->cap_cent,
-                       e->d_pct, e->cfg.n_percentiles, e->f_hstats, e->f_hq);
+                       e->d_pct, e->cfg.n_percentiles, qmask, e->f_hstats, e->f_hq);
     VN_HIP_CHECK(hipMemcpyAsync(e->hf_list[2], e->f_list[2], n[2] * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     VN_HIP_CHECK(hipMemcpyAsync(e->hf_hstats, e->f_hstats, (size_t)n[2] * VN_HISTO_STATS * 8, hipMemcpyDeviceToHost, st));
     if (e->cfg.n_percentiles)

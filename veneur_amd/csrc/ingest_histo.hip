@@ -866,22 +866,15 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   // no hot key (or when timing) everything runs in order on st.
   const bool fork = nhot && !e->timing;
   auto replay_cold = [&](hipStream_t s, RadixScratch& rs) {
-    if (e->lpt & 2) histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
-    else {
-      xc.order64 = nullptr;
-      xc.order = e->h_coldlist;
-      xc.norder = nreplay;
-    }
+    histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
     histo_exact_replay(xc, s);
   };
   if (fork) {
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
     VN_HIP_CHECK(hipStreamWaitEvent(e->st4, e->ev_fork3, 0));
-    if (e->early_replay) {
-      VN_HIP_CHECK(hipStreamWaitEvent(e->st3, e->ev_fork3, 0));
-      replay_cold(e->st3, e->rs3);
-      VN_HIP_CHECK(hipEventRecord(e->ev_join3, e->st3));
-    }
+    VN_HIP_CHECK(hipStreamWaitEvent(e->st3, e->ev_fork3, 0));
+    replay_cold(e->st3, e->rs3);
+    VN_HIP_CHECK(hipEventRecord(e->ev_join3, e->st3));
   } else {
     replay_cold(st, e->rs);
   }
@@ -918,11 +911,6 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
                      e->p_end);
   if (fork) {
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
-    if (!e->early_replay) {
-      VN_HIP_CHECK(hipStreamWaitEvent(e->st3, e->ev_fork3, 0));
-      replay_cold(e->st3, e->rs3);
-      VN_HIP_CHECK(hipEventRecord(e->ev_join3, e->st3));
-    }
     if (e->set_pending) {
       VN_HIP_CHECK(hipStreamWaitEvent(e->side, e->ev_fork3, 0));
       set_finish(e);

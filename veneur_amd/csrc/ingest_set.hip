@@ -360,7 +360,7 @@ void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t*
   // bound, so the whole set path is queued before the histogram path blocks the host
   const uint32_t nk = (uint32_t)std::min<uint64_t>(caps, n);  // >= touched keys
   const uint64_t* order = nullptr;  // most records first (longest-processing-time order)
-  if (e->lpt & 1) {  // ordered now, before the replays fill the CUs; only the merge is deferred
+  {  // ordered now, before the replays fill the CUs; only the merge is deferred
     hipLaunchKernelGGL(k_set_lpt_keys, dim3(blocks_for(nk, 256)), dim3(256), 0, st, nk, e->s_cnt, e->s_tl, e->s_start,
                        e->s_end, e->s_lpt0);
     RadixPass lp[4];

@@ -59,7 +59,9 @@ void export_histos(vn_engine* e, const uint32_t* dev_slot, uint64_t n, ExportBuf
 void export_sets(vn_engine* e, const uint32_t* dev_slot, uint64_t n, ExportBuffers& x);
 void ensure_export_bytes(vn_engine* e, ExportBuffers& x, uint64_t nbytes);
 // Worker.Flush + Counter/Gauge/Histo/Set.Flush math; resets the window
-void flush_all(vn_engine* e, vn_flush_result* out);
+// histo_qmask / set_emask: host arrays of cap[class] bytes (1 = percentiles / estimate), or null
+void flush_all(vn_engine* e, vn_flush_result* out, const uint8_t* histo_qmask = nullptr,
+               const uint8_t* set_emask = nullptr);
 // initial (empty-window) state of every slot
 void init_state(vn_engine* e);
 // metro64 over a batch (KAT entry point)

@@ -287,8 +287,6 @@ void radix_scratch_free(RadixScratch& s) {
   s = RadixScratch{};
 }
 
-// 8-byte records also scatter with 8 waves (measured ~1% faster on C3); VN_SCATTER8W=0: 4 waves
-static const bool g_scatter8w = [] { const char* v = std::getenv("VN_SCATTER8W"); return !(v && *v == '0'); }();
 
 bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t n, const RadixPass* passes,
                 int npasses, RadixScratch& s, hipStream_t st, RadixStats* stats) {
@@ -317,11 +315,8 @@ bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t
     if (hasb)
       hipLaunchKernelGGL((k_radix_scatter<true, 8>), dim3(nblocks), dim3(512), 0, st, sa, sb, da, db, n, ps.from_b,
                          ps.shift, ps.bits, s.counts, s.offsets, nblocks);
-    else if (g_scatter8w)
+    else  // 8-byte records also scatter with 8 waves (measured ~1% faster on C3 than 4)
       hipLaunchKernelGGL((k_radix_scatter<false, 8>), dim3(nblocks), dim3(512), 0, st, sa, sb, da, db, n, ps.from_b,
-                         ps.shift, ps.bits, s.counts, s.offsets, nblocks);
-    else
-      hipLaunchKernelGGL((k_radix_scatter<false, 4>), dim3(nblocks), dim3(256), 0, st, sa, sb, da, db, n, ps.from_b,
                          ps.shift, ps.bits, s.counts, s.offsets, nblocks);
     if (e0 && e1) VN_HIP_CHECK(hipEventRecord(e1, st));
     if (stats) {

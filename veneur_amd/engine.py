@@ -67,6 +67,10 @@ class Engine:
         self.percentiles = tuple(float(p) for p in percentiles)
         self.capacity = tuple(int(c) for c in capacity)
         self.device = device
+        # the engine's effective limits (capi.hip vn_engine_create)
+        self.max_batch_records = int(max_batch_records) or (1 << 20)
+        self.max_batch_member_bytes = max(int(max_batch_member_bytes) or self.max_batch_records * 16,
+                                          self.max_batch_records * 8)
         h = C.c_void_p()
         rc = A.lib.vn_engine_create(C.byref(cfg), C.byref(h))
         self.h = h
@@ -125,6 +129,24 @@ class Engine:
             keep += [s, hs]
             b.n_set, b.set_slot, b.set_hash = len(s), _p(s), _p(hs)
         self._check(A.lib.vn_ingest_host(self.h, C.byref(b)))
+
+    def stage(self):
+        """vn_stage_acquire: numpy views of the engine-owned pinned staging buffers."""
+        st = A.Stage()
+        self._check(A.lib.vn_stage_acquire(self.h, C.byref(st)))
+        n, nb = int(st.capacity), int(st.member_bytes_capacity)
+        v = lambda p, k: np.ctypeslib.as_array(p, shape=(k,))
+        return {"counter_slot": v(st.counter_slot, n), "counter_value": v(st.counter_value, n),
+                "counter_rate": v(st.counter_rate, n), "gauge_slot": v(st.gauge_slot, n),
+                "gauge_value": v(st.gauge_value, n), "histo_slot": v(st.histo_slot, n),
+                "histo_value": v(st.histo_value, n), "histo_rate": v(st.histo_rate, n),
+                "set_slot": v(st.set_slot, n), "set_member_off": v(st.set_member_off, n + 1),
+                "set_member_bytes": v(st.set_member_bytes, nb)}
+
+    def submit(self, n_counter=0, n_gauge=0, n_histo=0, n_set=0, n_set_member_bytes=0):
+        """vn_submit: ingest the records the caller wrote into the pinned stage."""
+        c = A.BatchCounts(n_counter, n_gauge, n_histo, n_set, n_set_member_bytes)
+        self._check(A.lib.vn_submit(self.h, C.byref(c)))
 
     def ingest_device(self, batch):
         """Ingest a batch whose arrays are already resident in device memory (A.Batch)."""
@@ -201,13 +223,28 @@ class Engine:
         self._check(A.lib.vn_sync(self.h))
 
     # ---------------------------------------------------------------- flush
-    def flush_raw(self):
+    def flush_raw(self, histo_quantile_mask=None, set_estimate_mask=None):
         out = A.FlushResult()
-        self._check(A.lib.vn_flush(self.h, C.byref(out)))
+        if histo_quantile_mask is None and set_estimate_mask is None:
+            self._check(A.lib.vn_flush(self.h, C.byref(out)))
+            return out
+        masks = []
+        for m, cap in ((histo_quantile_mask, self.capacity[2]), (set_estimate_mask, self.capacity[3])):
+            if m is None:
+                masks.append(None)
+            else:
+                a = np.zeros(max(cap, 1), np.uint8)
+                m = np.asarray(m, np.uint8)
+                a[:len(m)] = m[:cap]
+                masks.append(a)
+        self._check(A.lib.vn_flush_masked(self.h, *(None if a is None else a.ctypes.data_as(A.u8p) for a in masks),
+                                          C.byref(out)))
         return out
 
-    def flush(self) -> FlushOutput:
-        o = self.flush_raw()
+    def flush(self, histo_quantile_mask=None, set_estimate_mask=None) -> FlushOutput:
+        """Worker.Flush + sampler flush math; the masks (per slot, 1 = compute) select which
+        histograms get percentiles and which sets an estimate (a local veneur, vn_flush_masked)."""
+        o = self.flush_raw(histo_quantile_mask, set_estimate_mask)
         npct = len(self.percentiles)
         return FlushOutput(
             counter_slot=_arr(o.counter_slot, o.n_counter, np.uint32),

@@ -32,6 +32,7 @@ Go decoding rules kept here:
 import base64
 import binascii
 import json
+import re
 import logging
 import zlib
 from typing import List, Optional, Tuple
@@ -124,6 +125,15 @@ def _go_bytes(v):
         raise ValueError("illegal base64 data: %s" % e)
 
 
+_LONE_SURROGATE = re.compile("[\ud800-\udfff]")
+
+
+def _go_str(v: str) -> str:
+    """Go's JSON decoder turns an escaped lone surrogate (\\ud800 not followed by its pair) into
+    U+FFFD; Python's keeps it, and it cannot be encoded as UTF-8 (pairs arrive combined)."""
+    return _LONE_SURROGATE.sub("\ufffd", v)
+
+
 def _decode_metric(obj) -> Optional[dict]:
     """One element of []samplers.JSONMetric; None stands for Go's zero value fields."""
     m = {"name": "", "type": "", "tagstring": "", "tags": None, "value": None}
@@ -139,12 +149,12 @@ def _decode_metric(obj) -> Optional[dict]:
             continue
         if f in ("name", "type", "tagstring"):
             if isinstance(v, str):
-                m[f] = v
+                m[f] = _go_str(v)
             else:
                 err = err or "json: cannot unmarshal into Go struct field .%s of type string" % f
         elif f == "tags":
             if isinstance(v, list) and all(t is None or isinstance(t, str) for t in v):
-                m[f] = ["" if t is None else t for t in v]
+                m[f] = ["" if t is None else _go_str(t) for t in v]
             else:
                 err = err or "json: cannot unmarshal into Go struct field .tags of type []string"
         else:
