@@ -73,6 +73,11 @@ typedef struct {
    * are cut at window positions b_0 = prefix, b_{i+1} = b_i + max(1, b_i * growth / 100).
    * 0 -> 25 (tools/tdigest_study.py: <= 8e-4 rank error for 10..25). */
   uint32_t histo_piece_growth;
+  /* split keys: records a window may hold per class (histo, set) on this rank; 0 -> none */
+  uint64_t split_max_records;
+  /* compression of the micro-centroids a rank sends for its share of a split histogram's
+   * piece (tools/split_study.py); 0 -> 5 * compression */
+  double split_compression;
 } vn_config;
 
 /* One ingest batch: per-class SoA streams in arrival order (the order ProcessMetric saw
@@ -251,6 +256,7 @@ int vn_device_alloc(int device, uint64_t bytes, void** out);
 int vn_device_free(void* p);
 int vn_copy_to_device(int device, void* dst, const void* src, uint64_t bytes);
 int vn_device_copy(int device, void* dst, const void* src, uint64_t bytes);  /* device to device */
+int vn_copy_to_host(int device, void* dst, const void* src, uint64_t bytes);
 int vn_device_count(int* n);
 int vn_device_synchronize(int device);
 
@@ -266,6 +272,69 @@ typedef struct {
 } vn_timing;
 int vn_timing_enable(vn_engine* eng, int enable);
 int vn_get_timing(vn_engine* eng, vn_timing* out);
+
+/* ---------------------------------------------------------------- multi-GPU
+ * One engine per GPU (one process per GPU); keys are sharded the way veneur routes them to
+ * workers, Digest % N (server.go:655, samplers/parser.go:213-304), so ordinary keys need no
+ * exchange.  A key too hot for one GPU is *split*: the host deals its records round-robin over
+ * the ranks by the key's window arrival index (record j of the key goes to rank j % N, so the
+ * i-th split record a rank holds is the key's record j = rank + N*i), and at vn_flush the
+ * partial states meet on the key's owner rank (Digest % N) -- the reference's local -> global
+ * combine (flusher.go:264-353 -> handlers_global.go:53-63 -> worker.go:230-268) done over xGMI:
+ *   counters  ncclAllReduce(sum, int64): exact (Counter.Combine)
+ *   sets      the exact HLL state of the whole ordered stream (bit-identical to one Sketch
+ *             that saw every record): the sparse phase from the gathered first records, then
+ *             rebase epochs by ncclAllReduce min (first-fill positions, rebase candidates) and
+ *             max (registers, uint8) -- the all-reduce-max fast path whenever no rebase occurs
+ *   histos    Local* statistics by all-reduce (sum/min/max); the digest on the owner: the first
+ *             histo_hot_prefix records replayed exactly (gathered), then one mergeAllTemps per
+ *             geometric piece of the window over every rank's share of that piece, each share
+ *             sorted and compressed on its own rank into micro-centroids (compression
+ *             split_compression) and sent to the owner (grouped ncclSend/ncclRecv)
+ * Gauges are never split (last write wins needs the arrival order; their ingest is cheap).
+ * The communicator is RCCL (vn_comm_init, ids from vn_comm_unique_id on rank 0 passed over the
+ * host's control plane), or an in-process group of engines on one device (vn_comm_init_local:
+ * each rank's vn_flush runs in its own host thread; tests on one GPU).  Without a communicator
+ * an engine is a group of one. */
+typedef struct vn_comm vn_comm;
+#define VN_COMM_ID_BYTES 128
+enum { VN_DT_U8 = 0, VN_DT_U32 = 1, VN_DT_U64 = 2, VN_DT_I64 = 3, VN_DT_F64 = 4 };
+enum { VN_OP_SUM = 0, VN_OP_MAX = 1, VN_OP_MIN = 2 };
+int vn_comm_unique_id(uint8_t* id /* VN_COMM_ID_BYTES */);                       /* ncclGetUniqueId */
+int vn_comm_init(const uint8_t* id, int nranks, int rank, int device, vn_comm** out);  /* ncclCommInitRank */
+int vn_comm_init_local(int nranks, int device, vn_comm** out /* nranks handles */);
+void vn_comm_destroy(vn_comm* comm);
+const char* vn_comm_last_error(const vn_comm* comm);
+int vn_comm_rank(const vn_comm* comm);
+int vn_comm_nranks(const vn_comm* comm);
+/* control-plane all-reduce of a device buffer (synchronous) */
+int vn_comm_allreduce(vn_comm* comm, const void* send, void* recv, uint64_t count, int dtype, int op);
+/* the engine exchanges its split keys over comm at vn_flush (comm outlives the engine's use) */
+int vn_engine_set_comm(vn_engine* eng, vn_comm* comm);
+
+/* The split keys of the current window, per class (counter, histo, set; gauges cannot be
+ * split): the same list in the same order on every rank, slot[i] = this rank's slot of key i,
+ * owner[i] = the rank that flushes it (Digest % N).  Host arrays.  Set before the window's
+ * first ingest; cleared by vn_flush. */
+int vn_split_keys(vn_engine* eng, int cls, const uint32_t* slot, const uint32_t* owner, uint32_t n);
+/* Records of split histos / sets (device arrays), in this rank's arrival order; key = index into
+ * the class's split list.  Split counters go through vn_ingest like any counter. */
+typedef struct {
+  uint64_t n_histo;
+  const uint32_t* histo_key;
+  const double* histo_value;
+  const float* histo_rate;
+  uint64_t n_set;
+  const uint32_t* set_key;
+  const uint32_t* set_member_off;
+  const uint8_t* set_member_bytes;
+  const uint64_t* set_hash;
+} vn_split_batch;
+int vn_ingest_split(vn_engine* eng, const vn_split_batch* device_batch);
+/* Combine the split keys now (collective over the group; vn_flush does it when they are still
+ * pending): afterwards the owners hold each split key's state in its slot, the other ranks
+ * have cleared theirs, and the split lists are empty. */
+int vn_split_combine(vn_engine* eng);
 
 /* DogStatsD metric lines (host code, no GPU): samplers/parser.go:186-307 ParseMetric over a
  * datagram split on '\n' (server.go:706-714), empty packets skipped (server.go:612-616).

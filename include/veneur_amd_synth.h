@@ -10,6 +10,8 @@
 #define VENEUR_AMD_SYNTH_H
 #include <stdint.h>
 
+#include "veneur_amd.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -40,6 +42,44 @@ typedef struct {
 
 int vn_synth_generate(const vn_synth_config* cfg, vn_synth_out* out);
 void vn_synth_free(vn_synth_out* out);
+
+/* The C4 stream, generated in HBM by the GPU: one global stream of n_samples records over
+ * n_keys keys (Zipf popularity, alias-method draws; the classes and digests of the keys as
+ * vn_synth_generate), of which this rank keeps its own -- keys routed by digest % nranks
+ * (server.go:655), split keys dealt round-robin by their window arrival index (record j of a
+ * split key to rank j % nranks).  Local slots per class: the rank's own keys in ascending key
+ * id, then the class's split keys in list order (split key i at split_slot0[class] + i).  Split
+ * counters come out in `batch` at their local slot; split histograms and sets in `split`. */
+typedef struct {
+  uint64_t seed;
+  uint32_t n_keys;
+  double zipf_s;
+  double mix[4];
+  uint64_t n_samples;           /* positions of the global stream */
+  uint32_t rank, nranks;
+  uint64_t member_universe;
+  double rate_half, rate_tenth, histo_mu, histo_sigma;
+  int device;
+  uint32_t n_split[4];          /* split keys per class (gauges: 0) */
+  const uint32_t* split_key[4]; /* their key ids (host arrays) */
+} vn_synth_dev_config;
+
+typedef struct {
+  uint32_t n_slots[4];
+  uint32_t split_slot0[4];
+  uint32_t* key_of_slot[4];     /* host arrays */
+  uint32_t* digest_of_slot[4];
+  vn_batch batch;               /* device arrays (vn_ingest) */
+  vn_split_batch split;         /* device arrays (vn_ingest_split) */
+  uint64_t n_member_bytes, n_split_member_bytes;
+  int64_t counter_sum;          /* this rank's sum of int64(value) * int64(float32(1 / rate)) */
+  double histo_weight;          /* this rank's sum of histogram weights */
+} vn_synth_dev_out;
+
+int vn_synth_device(const vn_synth_dev_config* cfg, vn_synth_dev_out* out);
+void vn_synth_device_free(vn_synth_dev_out* out);
+/* record count of every key over the first n_positions of the stream (hot-key detection) */
+int vn_synth_key_counts(const vn_synth_dev_config* cfg, uint64_t n_positions, uint32_t* counts /* n_keys */);
 
 #ifdef __cplusplus
 }

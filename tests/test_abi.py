@@ -31,8 +31,9 @@ def test_struct_layouts_match_header():
     import ctypes as C
     import veneur_amd._abi as A
     # sizes derived from the C declarations (LP64)
-    assert C.sizeof(A.Config) == 4 + 16 + 4 + 8 + 4 + 4 + 16 * 8 + 8 + 8 + 4 + 4 + 4 + 4
+    assert C.sizeof(A.Config) == 4 + 16 + 4 + 8 + 4 + 4 + 16 * 8 + 8 + 8 + 4 + 4 + 4 + 4 + 8 + 8
     assert C.sizeof(A.Batch) == 16 * 8
+    assert C.sizeof(A.SplitBatch) == 9 * 8
     assert C.sizeof(A.SetState) == 4 + 5 * 4
 
 

@@ -435,8 +435,8 @@ def test_gpu_local_and_global_server_flush():
             final, fwd2 = W.server_flush([g], False, pct)
             byname = {m.name: m.value for m in final}
             assert fwd2 == []
-            assert (byname["a.b.c.50percentile"], byname["a.b.c.75percentile"], byname["a.b.c.99percentile"]) == \
-                (6.0, 42.375, 97.7)
+            assert [byname["a.b.c.%dpercentile" % int(p * 100)] for p in pct] == [exp.quantile(p) for p in pct]
+            assert [round(byname["a.b.c.%dpercentile" % int(p * 100)], 9) for p in pct] == [6.0, 42.375, 97.7]
             assert byname["s"] == 1.0
             assert "a.b.c.count" not in byname  # imported digests carry no Local* weight
         finally:

@@ -39,6 +39,9 @@ _share_torch_hip_runtime()
 lib = C.CDLL(LIB_PATH)
 
 VN_OK, VN_EINVAL, VN_EHIP, VN_ENOMEM, VN_EDECODE = 0, -1, -2, -3, -4
+VN_DT_U8, VN_DT_U32, VN_DT_U64, VN_DT_I64, VN_DT_F64 = 0, 1, 2, 3, 4
+VN_OP_SUM, VN_OP_MAX, VN_OP_MIN = 0, 1, 2
+VN_COMM_ID_BYTES = 128
 VN_COUNTER, VN_GAUGE, VN_HISTO, VN_SET = 0, 1, 2, 3
 VN_MAX_PERCENTILES = 16
 VN_HISTO_STATS = 8
@@ -53,7 +56,14 @@ class Config(C.Structure):
                 ("n_percentiles", C.c_uint32), ("percentiles", C.c_double * VN_MAX_PERCENTILES),
                 ("max_batch_records", C.c_uint64), ("max_batch_member_bytes", C.c_uint64),
                 ("histo_exact_threshold", C.c_uint32),
-                ("histo_hot_prefix", C.c_uint32), ("histo_piece_growth", C.c_uint32)]
+                ("histo_hot_prefix", C.c_uint32), ("histo_piece_growth", C.c_uint32),
+                ("split_max_records", C.c_uint64), ("split_compression", C.c_double)]
+
+
+class SplitBatch(C.Structure):
+    _fields_ = [("n_histo", C.c_uint64), ("histo_key", C.c_void_p), ("histo_value", C.c_void_p),
+                ("histo_rate", C.c_void_p), ("n_set", C.c_uint64), ("set_key", C.c_void_p),
+                ("set_member_off", C.c_void_p), ("set_member_bytes", C.c_void_p), ("set_hash", C.c_void_p)]
 
 
 class Batch(C.Structure):
@@ -165,10 +175,23 @@ class ParsedLine(C.Structure):  # vn_parsed_line
 
 _sig("vn_parse_dogstatsd", C.c_int64, C.c_char_p, C.c_uint64, C.POINTER(ParsedLine), C.c_uint64, C.c_char_p,
      C.c_uint64)
+_sig("vn_comm_unique_id", C.c_int, u8p)
+_sig("vn_comm_init", C.c_int, u8p, C.c_int, C.c_int, C.c_int, C.POINTER(vp))
+_sig("vn_comm_init_local", C.c_int, C.c_int, C.c_int, C.POINTER(vp))
+_sig("vn_comm_destroy", None, vp)
+_sig("vn_comm_last_error", C.c_char_p, vp)
+_sig("vn_comm_rank", C.c_int, vp)
+_sig("vn_comm_nranks", C.c_int, vp)
+_sig("vn_comm_allreduce", C.c_int, vp, vp, vp, C.c_uint64, C.c_int, C.c_int)
+_sig("vn_engine_set_comm", C.c_int, vp, vp)
+_sig("vn_split_keys", C.c_int, vp, C.c_int, u32p, u32p, C.c_uint32)
+_sig("vn_ingest_split", C.c_int, vp, C.POINTER(SplitBatch))
+_sig("vn_split_combine", C.c_int, vp)
 _sig("vn_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(vp))
 _sig("vn_device_free", C.c_int, vp)
 _sig("vn_copy_to_device", C.c_int, C.c_int, vp, vp, C.c_uint64)
 _sig("vn_device_copy", C.c_int, C.c_int, vp, vp, C.c_uint64)
+_sig("vn_copy_to_host", C.c_int, C.c_int, vp, vp, C.c_uint64)
 _sig("vn_device_count", C.c_int, C.POINTER(C.c_int))
 _sig("vn_device_synchronize", C.c_int, C.c_int)
 _sig("vn_timing_enable", C.c_int, vp, C.c_int)
@@ -182,4 +205,6 @@ EXPORTED = [
     "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_flush_masked", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
+    "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",
+    "vn_comm_nranks", "vn_comm_allreduce", "vn_engine_set_comm", "vn_split_keys", "vn_ingest_split", "vn_split_combine",
 ]

@@ -360,6 +360,7 @@ void export_impl(vn_engine* e, int cls, const uint32_t* slot, uint64_t n, vn_exp
 
 void destroy_impl(vn_engine* e) {
   if (e->st) (void)hipStreamSynchronize(e->st);
+  split_destroy(e);
   dfree(e->cval); dfree(e->ctouch); dfree(e->gseq); dfree(e->gval); dfree(e->gtouch); dfree(e->pk); dfree(e->pp);
   dfree(e->hst); dfree(e->hncent); dfree(e->hcur); dfree(e->htouch);
   for (int b = 0; b < 2; b++) { dfree(e->cmean[b]); dfree(e->cw[b]); }
@@ -866,6 +867,7 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
   if (!e || !out) return VN_EINVAL;
   return guarded(e, [&] {
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[5], e->st));
+    split_flush(e);  // split (hot) keys meet on their owner ranks first
     flush_all(e, out, histo_quantile_mask, set_estimate_mask);
     VN_HIP_CHECK(hipGetLastError());
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[6], e->st));
@@ -1004,6 +1006,10 @@ int vn_device_free(void* p) { return hipFree(p) == hipSuccess ? VN_OK : VN_EHIP;
 int vn_copy_to_device(int device, void* dst, const void* src, uint64_t bytes) {
   if (hipSetDevice(device) != hipSuccess) return VN_EHIP;
   return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice) == hipSuccess ? VN_OK : VN_EHIP;
+}
+int vn_copy_to_host(int device, void* dst, const void* src, uint64_t bytes) {
+  if (hipSetDevice(device) != hipSuccess) return VN_EHIP;
+  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost) == hipSuccess ? VN_OK : VN_EHIP;
 }
 int vn_device_copy(int device, void* dst, const void* src, uint64_t bytes) {
   if (hipSetDevice(device) != hipSuccess) return VN_EHIP;

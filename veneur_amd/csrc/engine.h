@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/veneur_amd.h"
+#include "comm.h"
 #include "primitives.h"
 
 namespace vn {
@@ -52,6 +53,24 @@ struct DeviceBatch {  // device-resident staging for one ingest call
   double *c_val, *g_val, *h_val;
   float *c_rate, *h_rate;
   uint8_t* s_bytes;
+};
+
+// Split (hot) keys of the window and the records they received (split.hip).
+struct SplitState {
+  vn_comm* comm = nullptr;          // the engine's group (vn_engine_set_comm); null: a group of one
+  vn_comm* solo = nullptr;          // that group of one, created on first use
+  std::vector<uint32_t> slot[VN_NCLASS], owner[VN_NCLASS];
+  uint32_t* d_slot[VN_NCLASS] = {nullptr, nullptr, nullptr, nullptr};
+  uint32_t d_cap[VN_NCLASS] = {0, 0, 0, 0};
+  uint64_t cap = 0;                 // records per class and window (vn_config.split_max_records)
+  uint64_t nh = 0, ns = 0;          // records buffered this window
+  uint32_t* hkey = nullptr;         // histo records: split key index, value, rate (arrival order)
+  double* hval = nullptr;
+  float* hrate = nullptr;
+  uint64_t* srec = nullptr;         // set records: key << 32 | sparse code (arrival order)
+  uint32_t* s_scratch_bt = nullptr; // set ingest: touched flags of the metro64 pass (unused slots)
+  std::vector<void*> scratch;       // flush scratch (freed at destroy)
+  std::vector<size_t> scratch_cap;
 };
 
 }  // namespace vn
@@ -239,6 +258,7 @@ struct vn_engine {
   bool timing = false;
   hipEvent_t ev[16] = {};
   vn::EventPool pool;
+  vn::SplitState sp;
   std::vector<hipEvent_t> pool_storage;
   vn_timing last{};
   vn::RadixStats rstat_c, rstat_h, rstat_s;

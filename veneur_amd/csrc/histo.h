@@ -79,6 +79,36 @@ void histo_exact_replay_list(const ExactCtx& x, const uint32_t* dev_count, uint3
 // up for histo_exact_replay
 void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* buf0, uint64_t* buf1,
                        RadixScratch& rs, hipStream_t st);
+// the geometric remainder's rounds (ingest_histo.hip): see the definition
+void histo_rounds(vn_engine* e, const uint32_t* list, uint32_t nkeys, uint32_t maxp, uint64_t nrec, uint32_t nrem,
+                  const uint64_t* PA, const uint64_t* PB, uint64_t* MA, uint64_t* MB, const double* impw,
+                  hipStream_t st);
+// One mergeAllTemps of each segment [start[k], end[k]) of (A = ordered value bits, B = tag) alone,
+// at compression delta, into the pseudo-slot tiles k = tl[k] of the given arrays (the split-key
+// micro-centroids, split.hip).  Per segment a capc-wide tile; w/wk sized nrec; chunk arrays sized
+// nrec / kHTile + nseg + 1; nch/chb nseg + 1.
+struct SegCompress {
+  uint32_t nseg = 0;
+  uint64_t nrec = 0;
+  uint32_t capc = 0;
+  double delta = 0;
+  const uint32_t* tl = nullptr;
+  const uint32_t* start = nullptr;
+  const uint32_t* end = nullptr;
+  uint32_t* nch = nullptr;
+  uint32_t* chb = nullptr;
+  const uint64_t* A = nullptr;
+  const uint64_t* B = nullptr;
+  double *w = nullptr, *wk = nullptr, *ch_sum = nullptr, *ch_pre = nullptr, *ch_stats = nullptr, *seg_T = nullptr;
+  uint32_t *starts = nullptr, *nc_new = nullptr;
+  double *acc_xw = nullptr, *acc_w = nullptr, *hst = nullptr;
+  uint32_t *hncent = nullptr;
+  uint8_t* hcur = nullptr;
+  uint32_t* hspn = nullptr;
+  double *cm0 = nullptr, *cm1 = nullptr, *cw0 = nullptr, *cw1 = nullptr;
+  uint32_t* err = nullptr;
+};
+void histo_compress_segments(const SegCompress& c, ScanScratch& ss, hipStream_t st);
 // estimateTempBuffer (merging_digest.go:87-93)
 inline uint32_t temp_buffer_cap(double compression) {
   double c = compression < 20 ? 20 : (compression > 925 ? 925 : compression);

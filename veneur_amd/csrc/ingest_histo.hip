@@ -756,6 +756,117 @@ __global__ __launch_bounds__(kBlock) void k_round_merge(uint32_t capc, const uin
     }
   }
 }
+// Round j of the geometric remainder merges piece j of every listed key that has one: one
+// mergeAllTemps of (the key's centroids + the piece's elements).  list indexes the per-key
+// arrays e->h_tl (slot), e->h_pcnt (pieces), e->h_pbase (first piece id); pieces are the
+// (piece id, value)-sorted elements PA/PB with ranges e->p_start/p_end per piece id.  nrec /
+// nkeys bound the merged elements (capacity check); MA/MB receive each round's merged layout.
+void histo_rounds(vn_engine* e, const uint32_t* list, uint32_t nkeys, uint32_t maxp, uint64_t nrec, uint32_t nrem,
+                  const uint64_t* PA, const uint64_t* PB, uint64_t* MA, uint64_t* MB, const double* impw,
+                  hipStream_t st) {
+  if (!nkeys || !maxp) return;
+  const uint64_t maxch = (nrec + (uint64_t)nrem * e->cap_cent) / kHTile + nrem + 1;
+  if (maxch > e->h_max_chunks || nrec + (uint64_t)nrem * e->cap_cent > e->h_sort_cap)
+    throw std::runtime_error("histo chunk capacity exceeded");
+  HistoCtx x;
+  x.ntouched = nkeys;
+  x.count = e->h_cnt + 5;
+  x.capc = e->cap_cent;
+  x.delta = e->cfg.compression;
+  x.tl = e->h_tl2;
+  x.start = e->h_start;
+  x.end = e->h_end;
+  x.chb = e->h_chb;
+  x.A = MA;
+  x.B = MB;
+  x.impw = impw;
+  x.w = e->h_w;
+  x.wk = e->h_wk;
+  x.ch_sum = e->ch_sum;
+  x.ch_pre = e->ch_pre;
+  x.ch_stats = e->ch_stats;
+  x.seg_T = e->seg_T;
+  x.starts = e->starts;
+  x.nc_new = e->nc_new;
+  x.acc_xw = e->acc_xw;
+  x.acc_w = e->acc_w;
+  x.hst = e->hst;
+  x.hncent = e->hncent;
+  x.hcur = e->hcur;
+  x.hspn = e->hspn;
+  x.cm0 = e->cmean[0];
+  x.cm1 = e->cmean[1];
+  x.cw0 = e->cw[0];
+  x.cw1 = e->cw[1];
+  x.err = e->h_err;
+  const int merge_blocks = std::min(1024, blocks_for(nrec + (uint64_t)nrem * e->cap_cent, kBlock));
+  for (uint32_t j = 0; j < maxp; j++) {
+    hipLaunchKernelGGL(k_round_plan, dim3(1), dim3(1024), 0, st, nkeys, j, list, e->h_tl, e->h_pcnt, e->h_pbase,
+                       e->p_start, e->p_end, e->hncent, e->h_tl2, e->r_flag, e->r_len, e->r_off, e->h_chb,
+                       e->h_start, e->h_end, e->h_cnt + 5);
+    hipLaunchKernelGGL(k_round_merge, dim3(merge_blocks), dim3(kBlock), 0, st, e->cap_cent, e->h_cnt + 5, e->h_tl2,
+                       e->r_flag, e->r_len, e->r_off, e->p_start, e->p_end, e->hcur, e->cmean[0], e->cmean[1], PA,
+                       PB, MA, MB);
+    hipLaunchKernelGGL(k_chunk_prep, dim3(maxch), dim3(kBlock), 0, st, x);
+    hipLaunchKernelGGL(k_seg_scan, dim3(nkeys), dim3(kBlock), 0, st, x);
+    hipLaunchKernelGGL(k_chunk_kin, dim3(maxch), dim3(kBlock), 0, st, x);
+    hipLaunchKernelGGL(k_chain, dim3(nkeys), dim3(kChainThreads), 0, st, x);
+    hipLaunchKernelGGL(k_chunk_cent, dim3(maxch), dim3(kBlock), 0, st, x);
+    hipLaunchKernelGGL(k_finalize, dim3(nkeys), dim3(kBlock), 0, st, x);
+  }
+}
+
+// chunks of each segment: nch[k] = ceil(len / kHTile) (0 for an empty segment)
+__global__ void k_seg_chunks(uint32_t nseg, const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
+                             uint32_t* __restrict__ nch) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < nseg) nch[k] = (end[k] - start[k] + kHTile - 1) / kHTile;
+}
+
+void histo_compress_segments(const SegCompress& c, ScanScratch& ss, hipStream_t st) {
+  if (!c.nseg) return;
+  hipLaunchKernelGGL(k_seg_chunks, dim3(blocks_for(c.nseg, 256)), dim3(256), 0, st, c.nseg, c.start, c.end, c.nch);
+  scan_exclusive_u32(c.nch, c.chb, c.nseg, ss, st);
+  HistoCtx x;
+  x.ntouched = c.nseg;
+  x.count = nullptr;
+  x.capc = c.capc;
+  x.delta = c.delta;
+  x.tl = c.tl;
+  x.start = c.start;
+  x.end = c.end;
+  x.chb = c.chb;
+  x.A = c.A;
+  x.B = c.B;
+  x.impw = nullptr;
+  x.w = c.w;
+  x.wk = c.wk;
+  x.ch_sum = c.ch_sum;
+  x.ch_pre = c.ch_pre;
+  x.ch_stats = c.ch_stats;
+  x.seg_T = c.seg_T;
+  x.starts = c.starts;
+  x.nc_new = c.nc_new;
+  x.acc_xw = c.acc_xw;
+  x.acc_w = c.acc_w;
+  x.hst = c.hst;
+  x.hncent = c.hncent;
+  x.hcur = c.hcur;
+  x.hspn = c.hspn;
+  x.cm0 = c.cm0;
+  x.cm1 = c.cm1;
+  x.cw0 = c.cw0;
+  x.cw1 = c.cw1;
+  x.err = c.err;
+  const uint64_t maxch = c.nrec / kHTile + c.nseg + 1;
+  hipLaunchKernelGGL(k_chunk_prep, dim3(maxch), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_seg_scan, dim3(c.nseg), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_chunk_kin, dim3(maxch), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_chain, dim3(c.nseg), dim3(kChainThreads), 0, st, x);
+  hipLaunchKernelGGL(k_chunk_cent, dim3(maxch), dim3(kBlock), 0, st, x);
+  hipLaunchKernelGGL(k_finalize, dim3(c.nseg), dim3(kBlock), 0, st, x);
+}
+
 HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate) {
   HistoGroups g{};
   if (!n) return g;
@@ -919,57 +1030,9 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   }
 
   const uint32_t nrem = nhot + nwarm;
-  const uint64_t maxch = (nremrec + (uint64_t)nrem * e->cap_cent) / kHTile + nrem + 1;
-  if (maxch > e->h_max_chunks || nremrec + (uint64_t)nrem * e->cap_cent > e->h_sort_cap)
-    throw std::runtime_error("histo chunk capacity exceeded");
-  HistoCtx x;
-  x.count = e->h_cnt + 5;
-  x.capc = e->cap_cent;
-  x.delta = e->cfg.compression;
-  x.tl = e->h_tl2;
-  x.start = e->h_start;
-  x.end = e->h_end;
-  x.chb = e->h_chb;
-  x.A = MA;
-  x.B = MB;
-  x.impw = impw;
-  x.w = e->h_w;
-  x.wk = e->h_wk;
-  x.ch_sum = e->ch_sum;
-  x.ch_pre = e->ch_pre;
-  x.ch_stats = e->ch_stats;
-  x.seg_T = e->seg_T;
-  x.starts = e->starts;
-  x.nc_new = e->nc_new;
-  x.acc_xw = e->acc_xw;
-  x.acc_w = e->acc_w;
-  x.hst = e->hst;
-  x.hncent = e->hncent;
-  x.hcur = e->hcur;
-  x.hspn = e->hspn;
-  x.cm0 = e->cmean[0];
-  x.cm1 = e->cmean[1];
-  x.cw0 = e->cw[0];
-  x.cw1 = e->cw[1];
-  x.err = e->h_err;
-  const int merge_blocks = std::min(1024, blocks_for(nremrec + (uint64_t)nrem * e->cap_cent, kBlock));
   // round j merges piece j of every key of the list that has one
   auto rounds = [&](const uint32_t* list, uint32_t nkeys, uint32_t maxp) {
-    x.ntouched = nkeys;
-    for (uint32_t j = 0; j < maxp; j++) {
-      hipLaunchKernelGGL(k_round_plan, dim3(1), dim3(1024), 0, st, nkeys, j, list, e->h_tl, e->h_pcnt, e->h_pbase,
-                         e->p_start, e->p_end, e->hncent, e->h_tl2, e->r_flag, e->r_len, e->r_off, e->h_chb,
-                         e->h_start, e->h_end, e->h_cnt + 5);
-      hipLaunchKernelGGL(k_round_merge, dim3(merge_blocks), dim3(kBlock), 0, st, e->cap_cent, e->h_cnt + 5, e->h_tl2,
-                         e->r_flag, e->r_len, e->r_off, e->p_start, e->p_end, e->hcur, e->cmean[0], e->cmean[1], PA,
-                         PB, MA, MB);
-      hipLaunchKernelGGL(k_chunk_prep, dim3(maxch), dim3(kBlock), 0, st, x);
-      hipLaunchKernelGGL(k_seg_scan, dim3(nkeys), dim3(kBlock), 0, st, x);
-      hipLaunchKernelGGL(k_chunk_kin, dim3(maxch), dim3(kBlock), 0, st, x);
-      hipLaunchKernelGGL(k_chain, dim3(nkeys), dim3(kChainThreads), 0, st, x);
-      hipLaunchKernelGGL(k_chunk_cent, dim3(maxch), dim3(kBlock), 0, st, x);
-      hipLaunchKernelGGL(k_finalize, dim3(nkeys), dim3(kBlock), 0, st, x);
-    }
+    histo_rounds(e, list, nkeys, maxp, nremrec, nrem, PA, PB, MA, MB, impw, st);
   };
   if (nhot) rounds(e->h_hotlist, nhot, maxp_hot);
   // the warm keys' rounds start from their exact prefixes: after the replay stream

@@ -375,6 +375,33 @@ void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t*
   if (!e->set_defer) set_finish(e);
 }
 
+// The exact Sketch.Insert replay of k_set_segments over arbitrary per-slot record ranges:
+// R holds (slot << 32 | sparse code) records, key list[k] (k < *dev_count <= grid) covers
+// R[e->s_start[slot], e->s_end[slot]) in insertion order (split.hip: a split set's gathered
+// first records).
+void set_replay_ranges(vn_engine* e, const uint64_t* R, const uint32_t* dev_count, const uint32_t* list,
+                       uint32_t grid, hipStream_t st) {
+  if (!grid) return;
+  SetCtx x;
+  x.cnt = dev_count;
+  x.order = nullptr;
+  x.tl = list;
+  x.start = e->s_start;
+  x.end = e->s_end;
+  x.R = R;
+  x.mode = e->smode;
+  x.base = e->sbase;
+  x.nz = e->snz;
+  x.lc = e->slc;
+  x.lb = e->slb;
+  x.last = e->slast;
+  x.tc = e->stc;
+  x.tmp = e->stmp;
+  x.arena = e->sarena;
+  x.err = e->h_err;
+  hipLaunchKernelGGL(k_set_segments, dim3(grid), dim3(kBlock), 0, st, x);
+}
+
 void set_finish(vn_engine* e) {
   if (!e->set_pending) return;
   e->set_pending = false;

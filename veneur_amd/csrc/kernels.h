@@ -47,6 +47,12 @@ void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
 void set_finish(vn_engine* e);
 void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t* off, const uint8_t* bytes,
                  const uint64_t* hashes);
+// k_set_segments over given record ranges (see ingest_set.hip)
+void set_replay_ranges(vn_engine* e, const uint64_t* R, const uint32_t* dev_count, const uint32_t* list,
+                       uint32_t grid, hipStream_t st);
+// split (hot) keys at flush: combine the ranks' partial states on the owners (split.hip)
+void split_flush(vn_engine* e);
+void split_destroy(vn_engine* e);
 // mergeAllTemps for the given (distinct) histo slots, device list
 void histo_merge_pending(vn_engine* e, const uint32_t* dev_keys, uint32_t nkeys);
 // MergingDigest.Quantile (kind 0) / CDF (kind 1) per (slot, arg); call histo_merge_pending first

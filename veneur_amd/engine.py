@@ -50,8 +50,11 @@ def _arr(ptr, n, dt, shape=None):
 
 class Engine:
     def __init__(self, capacity, compression=100.0, percentiles=(0.5, 0.9, 0.99, 0.999), max_batch_records=1 << 20,
-                 max_batch_member_bytes=0, device=0, exact_threshold=0, hot_prefix=0, piece_growth=0):
+                 max_batch_member_bytes=0, device=0, exact_threshold=0, hot_prefix=0, piece_growth=0,
+                 split_max_records=0, split_compression=0.0):
         cfg = A.Config()
+        cfg.split_max_records = int(split_max_records)
+        cfg.split_compression = float(split_compression)
         cfg.histo_exact_threshold = int(exact_threshold)
         cfg.histo_hot_prefix = int(hot_prefix)
         cfg.histo_piece_growth = int(piece_growth)
@@ -151,6 +154,62 @@ class Engine:
     def ingest_device(self, batch):
         """Ingest a batch whose arrays are already resident in device memory (A.Batch)."""
         self._check(A.lib.vn_ingest(self.h, C.byref(batch)))
+
+    # ------------------------------------------------------------ split (hot) keys
+    def set_comm(self, comm):
+        """Exchange split keys over comm (a Comm) at flush; None: a group of one."""
+        self.comm = comm
+        self._check(A.lib.vn_engine_set_comm(self.h, comm.h if comm is not None else None))
+
+    def split_keys(self, cls, slots, owners):
+        """The window's split keys of class cls (0 counter, 2 histo, 3 set): this rank's slots
+        and owner ranks, in the group-wide order."""
+        s, o = _c(slots, np.uint32), _c(owners, np.uint32)
+        if len(s) != len(o):
+            raise ValueError("one owner per split key")
+        self._check(A.lib.vn_split_keys(self.h, int(cls), s.ctypes.data_as(A.u32p), o.ctypes.data_as(A.u32p), len(s)))
+
+    def split_combine(self):
+        """vn_split_combine: meet the group now (collective); vn_flush does it otherwise."""
+        self._check(A.lib.vn_split_combine(self.h))
+
+    def ingest_split_device(self, batch):
+        """vn_ingest_split of an A.SplitBatch whose arrays are in device memory."""
+        self._check(A.lib.vn_ingest_split(self.h, C.byref(batch)))
+
+    def ingest_split(self, histos=None, set_hashes=None, sets=None):
+        """Split-key records from host arrays (copied to the device first): histos=(key, value,
+        rate), set_hashes=(key, hash64) or sets=(key, member_off[n+1], member_bytes)."""
+        bufs = []
+
+        def dev(a):
+            b = DeviceBuffer(a, device=self.device)
+            bufs.append(b)
+            return b.ptr.value
+
+        b = A.SplitBatch()
+        try:
+            if histos is not None:
+                k, v, r = _c(histos[0], np.uint32), _c(histos[1], np.float64), _c(histos[2], np.float32)
+                b.n_histo = len(k)
+                if len(k):
+                    b.histo_key, b.histo_value, b.histo_rate = dev(k), dev(v), dev(r)
+            if set_hashes is not None:
+                k, hs = _c(set_hashes[0], np.uint32), _c(set_hashes[1], np.uint64)
+                b.n_set = len(k)
+                if len(k):
+                    b.set_key, b.set_hash = dev(k), dev(hs)
+            elif sets is not None:
+                k, o, m = _c(sets[0], np.uint32), _c(sets[1], np.uint32), _c(sets[2], np.uint8)
+                b.n_set = len(k)
+                if len(k):
+                    b.set_key, b.set_member_off, b.set_member_bytes = dev(k), dev(o), dev(m if m.size else
+                                                                                    np.zeros(1, np.uint8))
+            self.ingest_split_device(b)
+            A.lib.vn_device_synchronize(self.device)
+        finally:
+            for x in bufs:
+                x.free()
 
     def import_counters(self, slot, values):
         s, v = _c(slot, np.uint32), _c(values, np.int64)
@@ -293,6 +352,66 @@ class Engine:
         t = A.Timing()
         self._check(A.lib.vn_get_timing(self.h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in A.Timing._fields_}
+
+
+class Comm:
+    """A group of engines exchanging split keys: RCCL (one process per GPU) or in-process."""
+
+    def __init__(self, h):
+        self.h = h
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * A.VN_COMM_ID_BYTES)()
+        if A.lib.vn_comm_unique_id(buf) != 0:
+            raise EngineError("vn_comm_unique_id failed (librccl)")
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, uid, nranks, rank, device):
+        buf = (C.c_uint8 * A.VN_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        rc = A.lib.vn_comm_init(buf, nranks, rank, device, C.byref(h))
+        if rc != 0:
+            msg = A.lib.vn_comm_last_error(h).decode() if h else ""
+            if h:
+                A.lib.vn_comm_destroy(h)
+            raise EngineError("vn_comm_init failed (rc=%d): %s" % (rc, msg))
+        return cls(h)
+
+    @classmethod
+    def local(cls, nranks, device=0):
+        hs = (C.c_void_p * nranks)()
+        if A.lib.vn_comm_init_local(nranks, device, hs) != 0:
+            raise EngineError("vn_comm_init_local failed")
+        return [cls(C.c_void_p(h)) for h in hs]
+
+    @property
+    def rank(self):
+        return A.lib.vn_comm_rank(self.h)
+
+    @property
+    def nranks(self):
+        return A.lib.vn_comm_nranks(self.h)
+
+    def allreduce_f64(self, values, op, device=0):
+        """Control-plane all-reduce of a few doubles (through device memory)."""
+        v = np.ascontiguousarray(values, np.float64)
+        b = DeviceBuffer(v, device=device)
+        try:
+            if A.lib.vn_comm_allreduce(self.h, b.ptr, b.ptr, len(v), A.VN_DT_F64, op) != 0:
+                raise EngineError("vn_comm_allreduce: %s" % A.lib.vn_comm_last_error(self.h).decode())
+            out = np.zeros_like(v)
+            A.lib.vn_device_synchronize(device)
+            A.lib.vn_copy_to_host(device, out.ctypes.data_as(C.c_void_p), b.ptr, v.nbytes)
+            return out
+        finally:
+            b.free()
+
+    def close(self):
+        if getattr(self, "h", None):
+            A.lib.vn_comm_destroy(self.h)
+            self.h = None
 
 
 def metro64_device(members, seed=1337, device=0):
