@@ -1,18 +1,24 @@
 #!/usr/bin/env python3
-"""Benchmark: samples aggregated/sec per flush at 1M keys (BASELINE.json), C3 workload.
+"""Benchmark: samples aggregated/sec per flush at 1M keys (BASELINE.json), workload C4.
 
-One step = one flush window on this GPU: ingest a 100M-sample mixed DogStatsD-shaped batch
-(counters / gauges / timers / sets over 1M keys, Zipf(1.0) popularity, already parsed and
-resident in HBM) through the engine's C-ABI, then flush it (Counter/Gauge values, Histo
-local stats + p50/p90/p99/p99.9, Set estimates copied back to pinned host memory).
+C4: ONE global DogStatsD-shaped stream of 1e9 samples per flush window
+(counters / gauges / timers / sets over 1M keys, Zipf(1.0) popularity, already parsed),
+key-sharded over the N GPUs of one node by veneur's worker routing, FNV-1a digest % N
+(server.go:655), with the hot keys split: the counter / timer / set keys whose window count
+passes a share of the per-GPU load are dealt round-robin over every GPU by their window arrival
+index and combined on their owner at flush over RCCL (include/veneur_amd.h "multi-GPU").  Every
+rank generates the whole stream on its GPU and keeps its own records, so the N ranks together
+hold exactly the one stream (strong scaling: the total work is fixed, N = 1 processes all 1e9).
 
-Multi-GPU: one process per GPU; keys are sharded by veneur's FNV-1a digest % N (the worker
-routing of server.go:655), every rank aggregates its own 100M-sample shard stream (weak
-scaling, no data-path collective).  value = samples of all ranks / max-over-ranks time.
+One step = one flush window per rank: the split-key lists, vn_ingest of the rank's batch
+(resident in HBM), vn_ingest_split of its split-key records, vn_flush (the split-key exchange,
+then Counter/Gauge values, Histo local stats + p50/p90/p99/p99.9, Set estimates to pinned host
+memory).  value = 1e9 samples x steps / the max over ranks of the timed region.
 
-The CPU baseline (rank 0, N=1) times the oracle -- a C restatement of the Go worker path
-(samplers + tdigest + axiomhq HLL), multi-threaded with veneur's key routing -- on the same
-stream; its flushed values also give the full-scale parity check and the p99 rank error.
+Rank 0 at N = 1 also times the CPU baseline -- the oracle, a C restatement of the Go Worker path
+(samplers + tdigest + axiomhq HLL) on 16 host threads with veneur's key routing -- on the same
+window, and checks the flush against it (counters / gauges / sets bit-exact, histo stats, p99
+rank error).  At N > 1 the ranks check stream invariants instead (counter total, histo weight).
 """
 import argparse
 import json
@@ -27,6 +33,7 @@ sys.path.insert(0, ROOT)
 
 PCT = (0.5, 0.9, 0.99, 0.999)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "samples aggregated/sec per flush at 1M keys (1/2/4/8 GPU); p99 rank error"
 
 
 def log(rank, *a):
@@ -34,22 +41,39 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def algorithmic_bytes(d):
-    """16 B per counter/gauge/histo record (slot u32 + value f64 + rate f32),
-    8 B + member bytes per set record, plus per-key state read+written once per flush
-    (counter 8 B, gauge 16 B, histo 40 B of local stats; centroids and HLL state excluded
-    here -- a lower bound)."""
-    n_scalar = len(d["c_slot"]) + len(d["g_slot"]) + len(d["h_slot"])
-    b = 16 * n_scalar + 8 * len(d["s_slot"]) + int(len(d["s_bytes"]))
-    nc, ng, nh, ns = d["n_slots"]
-    b += 2 * (8 * nc + 16 * ng + 40 * nh)
-    return b
+def hot_keys(counts, scale, classes, thr_cs, thr_set, max_split):
+    """Top keys by window count above the class threshold (counters and timers: a share of the
+    per-GPU load; sets: also any key that would keep one workgroup busy for long)."""
+    split = {}
+    est = counts.astype(np.float64) * scale
+    for c, thr in ((0, thr_cs), (2, thr_cs), (3, thr_set)):
+        ks = np.nonzero((classes == c) & (est > thr))[0]
+        ks = ks[np.argsort(-est[ks], kind="stable")][:max_split]
+        split[c] = np.sort(ks).astype(np.uint32)
+    return split
+
+
+def key_classes(seed, n_keys, mix=(0.4, 0.2, 0.25, 0.15)):
+    """Class of every key (the generators' draw: splitmix64 of the key id)."""
+    k = np.arange(n_keys, dtype=np.uint64)
+    x = np.uint64(seed) ^ (np.uint64(0xA5A5A5A5) + k * np.uint64(0x9E3779B97F4A7C15))
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        x = x ^ (x >> np.uint64(31))
+    u = (x >> np.uint64(11)).astype(np.float64) * (1.0 / 9007199254740992.0)
+    cum = np.cumsum(np.asarray(mix) / sum(mix))
+    return np.minimum(np.searchsorted(cum, u, side="right"), 3).astype(np.int64)
 
 
 def rank_error_stats(d, slots, eng_q, ref_q):
     """|F(q_engine) - F(q_ref)| with F the exact weighted empirical CDF of the key's samples."""
-    hs, hv = d["h_slot"], d["h_val"]
-    hw = (1.0 / d["h_rate"].astype(np.float32)).astype(np.float64)
+    want = np.zeros(int(d["h_slot"].max()) + 1 if len(d["h_slot"]) else 1, bool)
+    want[slots] = True
+    m = want[d["h_slot"]]
+    hs, hv = d["h_slot"][m], d["h_val"][m]
+    hw = (np.float32(1.0) / d["h_rate"][m]).astype(np.float64)
     o = np.lexsort((hv, hs))
     sv, ss, sw = hv[o], hs[o], hw[o]
     cw = np.cumsum(sw)
@@ -76,16 +100,20 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--keys", type=int, default=1_000_000)
-    ap.add_argument("--samples", type=int, default=100_000_000, help="samples per rank per flush window")
-    ap.add_argument("--batches", type=int, default=1, help="ingest calls per flush window")
-    ap.add_argument("--seed", type=int, default=0x5EED0003)
-    ap.add_argument("--exact-threshold", type=int, default=0,
-                    help="t-digest samples per key and window replayed bit-exactly (0: engine default)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
+    ap.add_argument("--samples", type=int, default=1_000_000_000, help="samples per flush window, all ranks")
+    ap.add_argument("--seed", type=int, default=0x5EED0004)
+    ap.add_argument("--hot-div", type=int, default=32,
+                    help="split a counter/timer key above samples / (N * hot_div) per window")
+    ap.add_argument("--set-hot", type=int, default=1 << 18, help="split a set key above this many records")
+    ap.add_argument("--max-split", type=int, default=64, help="split keys per class at most")
+    ap.add_argument("--no-split", action="store_true", help="route every key by digest % N (no hot keys)")
+    ap.add_argument("--exact-threshold", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--timing-steps", type=int, default=2, help="untimed steps with per-kernel HIP-event timing")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
+    ap.add_argument("--parity-keys", type=int, default=3000, help="histo keys sampled for the rank-error check")
+    ap.add_argument("--timing-steps", type=int, default=1, help="untimed steps with per-kernel HIP-event timing")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof runs)")
-    ap.add_argument("--pcie-steps", type=int, default=2,
+    ap.add_argument("--pcie-steps", type=int, default=1,
                     help="extra steps from host arrays (vn_ingest_host), reported as pcie_inclusive; 0: off")
     args = ap.parse_args()
 
@@ -94,123 +122,127 @@ def main():
     from veneur_amd.dist import Group, env_world
 
     world, rank, local_rank = env_world()
-    group = Group(backend="nccl", local_rank=local_rank)  # world 1: no process group
+    ctrl = Group(backend="gloo")  # host control plane: barrier, max / sum of scalars, the RCCL id
+    comm = None
+    if world > 1:
+        uid = V.Comm.unique_id() if rank == 0 else None
+        uid = ctrl.broadcast_object(uid)
+        comm = V.Comm.rccl(uid, world, rank, local_rank)
 
-    # ---- synthetic C3 shard stream (host), then resident in HBM
+    # ---- hot keys: top keys by count in the first 2^24 records of the window (every rank alike)
     t0 = time.time()
-    d = V.synth(seed=args.seed, n_keys=args.keys, zipf_s=1.0, mix=(0.4, 0.2, 0.25, 0.15), n_samples=args.samples,
-                shard=rank, n_shards=world, member_universe=50_000_000, rate_half=0.05, rate_tenth=0.05)
-    n_slots = d["n_slots"]
-    counts = [len(d["c_slot"]), len(d["g_slot"]), len(d["h_slot"]), len(d["s_slot"])]
-    log(rank, "[bench] shard %d/%d: %d samples over %s keys (c/g/h/s=%s), generated in %.1fs" %
-        (rank, world, args.samples, n_slots, counts, time.time() - t0))
+    split = {0: np.zeros(0, np.uint32), 2: np.zeros(0, np.uint32), 3: np.zeros(0, np.uint32)}
+    if not args.no_split:
+        sample = min(args.samples, 1 << 24)
+        counts = V.synth_key_counts(args.seed, args.keys, args.samples, sample, device=local_rank)
+        classes = key_classes(args.seed, args.keys)
+        thr = args.samples / (world * args.hot_div)
+        split = hot_keys(counts, args.samples / sample, classes, thr, min(thr, args.set_hot), args.max_split)
+    stream = V.DeviceStream(args.seed, args.keys, args.samples, rank, world, device=local_rank, split=split)
+    n_slots = stream.n_slots
+    log(rank, "[bench] rank %d/%d: %d of %d samples (c/g/h/s=%s, split h/s=%s), %s slots, split keys c/h/s=%s, "
+        "generated in %.1fs" % (rank, world, stream.n_records, args.samples, list(stream.counts),
+                                list(stream.split_counts), n_slots, [len(split[c]) for c in (0, 2, 3)],
+                                time.time() - t0))
 
-    per_batch = [(c + args.batches - 1) // args.batches for c in counts]
     eng = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,
-                   max_batch_records=max(per_batch) + 1, max_batch_member_bytes=int(len(d["s_bytes"])) + 64,
-                   device=local_rank, exact_threshold=args.exact_threshold)
-    bufs = []
-
-    def dev(a):
-        b = V.DeviceBuffer(a, device=local_rank)
-        bufs.append(b)
-        return b.ptr.value
-
-    batches = []
-    for bi in range(args.batches):
-        b = A.Batch()
-        sl = [slice(counts[c] * bi // args.batches, counts[c] * (bi + 1) // args.batches) for c in range(4)]
-        b.n_counter = sl[0].stop - sl[0].start
-        b.counter_slot, b.counter_value, b.counter_rate = dev(d["c_slot"][sl[0]]), dev(d["c_val"][sl[0]]), \
-            dev(d["c_rate"][sl[0]])
-        b.n_gauge = sl[1].stop - sl[1].start
-        b.gauge_slot, b.gauge_value = dev(d["g_slot"][sl[1]]), dev(d["g_val"][sl[1]])
-        b.n_histo = sl[2].stop - sl[2].start
-        b.histo_slot, b.histo_value, b.histo_rate = dev(d["h_slot"][sl[2]]), dev(d["h_val"][sl[2]]), \
-            dev(d["h_rate"][sl[2]])
-        b.n_set = sl[3].stop - sl[3].start
-        off = d["s_off"][sl[3].start:sl[3].stop + 1].astype(np.int64)
-        b.set_slot = dev(d["s_slot"][sl[3]])
-        b.set_member_off = dev((off - off[0]).astype(np.uint32))
-        b.set_member_bytes = dev(d["s_bytes"][off[0]:off[-1]])
-        batches.append(b)
+                   max_batch_records=max(stream.counts) + 1,
+                   max_batch_member_bytes=stream.counts[3] * 11 + 64, device=local_rank,
+                   exact_threshold=args.exact_threshold, split_max_records=max(stream.split_counts) + 1)
+    if comm is not None:
+        eng.set_comm(comm)
+    split_lists = []
+    for c in (0, 2, 3):
+        slots = (stream.split_slot0[c] + np.arange(len(split[c]))).astype(np.uint32)
+        owners = (stream.digest_of_slot[c][slots] % np.uint32(world)).astype(np.uint32)
+        split_lists.append((c, slots, owners))
 
     def step():
-        for b in batches:
-            eng.ingest_device(b)
+        for c, slots, owners in split_lists:
+            if len(slots):
+                eng.split_keys(c, slots, owners)
+        eng.ingest_device(stream.batch)
+        if sum(stream.split_counts):
+            eng.ingest_split_device(stream.split)
         return eng.flush_raw()
 
     def sync():
         A.lib.vn_device_synchronize(local_rank)
 
-    def barrier():
-        group.barrier()
-
     for _ in range(args.warmup):
         step()
-    barrier()
     sync()
+    ctrl.barrier()
     t0 = time.perf_counter()
     last = None
     for _ in range(args.steps):
         last = step()
     sync()
-    barrier()
+    t_rank = time.perf_counter() - t0
+    ctrl.barrier()
     elapsed = time.perf_counter() - t0
-    # PCIe-inclusive rate (never `value`): the same window handed over as pageable host arrays
-    # through vn_ingest_host (host-side checks, pinned staging, H2D copies, then the same kernels)
-    pcie = None
-    if args.pcie_steps > 0 and world == 1 and args.batches == 1:
-        hkw = dict(counters=(d["c_slot"], d["c_val"], d["c_rate"]), gauges=(d["g_slot"], d["g_val"]),
-                   histos=(d["h_slot"], d["h_val"], d["h_rate"]), sets=(d["s_slot"], d["s_off"], d["s_bytes"]))
-        eng.ingest(**hkw)
-        eng.flush_raw()
-        sync()
-        tp = time.perf_counter()
-        for _ in range(args.pcie_steps):
-            eng.ingest(**hkw)
-            last = eng.flush_raw()
-        sync()
-        pms = (time.perf_counter() - tp) * 1e3 / args.pcie_steps
-        pcie = {"value": args.samples / (pms * 1e-3), "unit": "samples/s", "ms_per_step": pms,
-                "path": "vn_ingest_host from pageable host arrays: host checks + pinned staging + H2D + kernels"}
+    elapsed = ctrl.max(elapsed)
+    rank_ms = ctrl.gather_object(t_rank * 1e3 / args.steps)
+    rank_records = ctrl.gather_object(stream.n_records)
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = float(args.samples) * args.steps / elapsed
+
+    # stream invariants of the flushed window (all ranks): counter total, histo weight
+    fc = np.ctypeslib.as_array(last.counter_value, shape=(last.n_counter,)).astype(np.int64) if last.n_counter \
+        else np.zeros(0, np.int64)
+    hst = np.ctypeslib.as_array(last.histo_stats, shape=(last.n_histo * 8,)).reshape(-1, 8) if last.n_histo \
+        else np.zeros((0, 8))
+    with np.errstate(over="ignore"):
+        csum_flushed = int(fc.sum(dtype=np.int64))
+    inv = ctrl.gather_object((csum_flushed, stream.counter_sum, float(hst[:, 0].sum()), stream.histo_weight))
+    wrap = lambda v: (v + (1 << 63)) % (1 << 64) - (1 << 63)
+    checks = {"counter_total_exact": wrap(sum(i[0] for i in inv)) == wrap(sum(i[1] for i in inv)),
+              "histo_weight_rel_err": abs(sum(i[2] for i in inv) - sum(i[3] for i in inv)) /
+              max(1.0, sum(i[3] for i in inv))}
+
     # per-kernel timing (HIP events on the engine's stream) from extra, untimed steps: with
-    # timing on, the side-stream classes run serialised so every launch is measured alone
+    # timing on, the phases run one after another so every launch is measured alone
     eng.timing_enable(True)
     tim = []
     for _ in range(max(1, args.timing_steps)):
-        last = step()  # every step flushes the same window: parity below reads the latest result
+        last = step()
         tim.append(eng.timing())
     eng.timing_enable(False)
     for _ in range(args.profile_steps):
         last = step()
-    elapsed = group.max(elapsed)                                  # max over ranks
-    total_samples = group.sum(float(args.samples)) * args.steps  # every rank's shard stream
-    ms_per_step = elapsed * 1e3 / args.steps
-    value = total_samples / elapsed
-
-    # ---- roofline of the dominant kernel: the LSD radix scatter (histo key grouping + hot-key
-    # value sort, set key grouping), algorithmic bytes = read + write of every record per pass
-    sc_ms = float(np.mean([t["ms_radix_scatter_total"] for t in tim]))
-    sc_bytes = float(np.mean([t["radix_scatter_bytes"] for t in tim]))
-    sc_launch = float(np.mean([t["radix_scatter_launches"] for t in tim]))
-    achieved = (sc_bytes / (sc_ms * 1e-3)) / 1e9 if sc_ms > 0 else 0.0
-    phase = {k: round(float(np.mean([t[k] for t in tim])), 4) for k in
+    mean = lambda k: float(np.mean([t[k] for t in tim]))
+    kern = []
+    for name, ms_k, by_k, n_k in (("k_histo_exact", "ms_histo_replay", "histo_replay_bytes", "histo_replay_launches"),
+                                  ("k_set_segments", "ms_set_segments", "set_segment_bytes", "set_segment_launches"),
+                                  ("k_radix_scatter", "ms_radix_scatter_total", "radix_scatter_bytes",
+                                   "radix_scatter_launches")):
+        ms, by, nl = mean(ms_k), mean(by_k), mean(n_k)
+        if ms > 0 and nl > 0:
+            ach = by / (ms * 1e-3) / 1e9
+            kern.append({"kernel": name, "ms_per_step": ms, "launches_per_step": nl,
+                         "algorithmic_bytes_per_launch": by / nl, "achieved": ach, "frac": ach / HBM_PEAK_GBS})
+    kern.sort(key=lambda k: -k["ms_per_step"])
+    phase = {k: round(mean(k), 4) for k in
              ("ms_ingest_counter", "ms_ingest_gauge", "ms_ingest_histo", "ms_ingest_set", "ms_flush")}
+    top = kern[0] if kern else {}
     traffic, traffic_src, traffic_ratio = None, None, None
-    tf = os.path.join(ROOT, "roofline_traffic.json")  # tools/pmc_traffic.py, PMC passes of this same command
-    if os.path.exists(tf) and sc_launch:
+    tf = os.path.join(ROOT, "roofline_traffic.json")  # tools/pmc_traffic.py, PMC passes of this command
+    if os.path.exists(tf) and top:
         with open(tf) as fh:
             tj = json.load(fh)
-        # the PMC passes measure HBM bytes / algorithmic bytes over every scatter dispatch of their
-        # run; scaled to this step's launches (whose mix of record counts it shares)
-        traffic_ratio = tj["traffic_over_algorithmic"]
-        traffic, traffic_src = traffic_ratio * sc_bytes / sc_launch, tj["source"]
-    path_bytes = algorithmic_bytes(d)
-    path_gbs = path_bytes / (ms_per_step * 1e-3) / 1e9
+        if tj.get("kernel") == top["kernel"]:
+            traffic_ratio = tj["traffic_over_algorithmic"]
+            traffic, traffic_src = traffic_ratio * top["algorithmic_bytes_per_launch"], tj["source"]
+    # whole path: SURVEY §8(d) algorithmic bytes of the window (16 B per scalar record, 8 B +
+    # member bytes per set record, per-key state once) over the window's time
+    n_sc = stream.counts[0] + stream.counts[1] + stream.counts[2] + stream.split_counts[0]
+    n_set = stream.counts[3] + stream.split_counts[1]
+    path_bytes = 16 * n_sc + 19 * n_set + 2 * (8 * n_slots[0] + 16 * n_slots[1] + 40 * n_slots[2])
+    path_bytes = ctrl.sum(float(path_bytes))
+    path_gbs = path_bytes / (ms_per_step * 1e-3) / 1e9 / world
 
     result = {
-        "metric": "samples aggregated/sec per flush at 1M keys (1/2/4/8 GPU); p99 rank error",
+        "metric": METRIC,
         "value": value,
         "unit": "samples/s",
         "n_gpus": world,
@@ -218,29 +250,63 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64/u64",
-        "data": "synthetic (DogStatsD-shaped C3 stream, seeded, resident in HBM)",
-        "config": {"workload": "C3 mixed counters/gauges/timers/sets, %d keys, %d samples/flush/GPU, Zipf(1.0)"
-                               % (args.keys, args.samples),
-                   "keys": args.keys, "samples_per_gpu": args.samples, "batches_per_flush": args.batches,
-                   "percentiles": list(PCT), "compression": 100, "hll_precision": 14,
-                   "parallelism": "key-sharded FNV %% %d" % world},
-        "roofline": {"bound": "hbm", "kernel": "k_radix_scatter", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+        "data": "synthetic (one global DogStatsD-shaped C4 stream generated in HBM, seeded)",
+        "config": {"workload": "C4 mixed counters/gauges/timers/sets, %d keys, %d samples per flush window over %d "
+                               "GPU(s), Zipf(1.0), hot keys split" % (args.keys, args.samples, world),
+                   "keys": args.keys, "samples_per_window": args.samples, "percentiles": list(PCT),
+                   "compression": 100, "hll_precision": 14,
+                   "parallelism": "key-sharded FNV %% %d + %d split hot keys (RCCL)" %
+                                  (world, sum(len(split[c]) for c in split)),
+                   "split_keys": {"counter": len(split[0]), "histo": len(split[2]), "set": len(split[3])}},
+        "roofline": {"bound": "hbm", "kernel": top.get("kernel"), "achieved": top.get("achieved"),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": top.get("frac"), "traffic": traffic,
                      "traffic_unit": "bytes per launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)",
                      "traffic_over_algorithmic": traffic_ratio, "traffic_source": traffic_src,
-                     "algorithmic_bytes_per_launch": sc_bytes / sc_launch if sc_launch else None,
-                     "launches_per_step": sc_launch, "ms_per_step": sc_ms},
-        "path": {"algorithmic_bytes_per_step": path_bytes, "effective_GBs": path_gbs,
-                 "frac_of_hbm_peak": path_gbs / HBM_PEAK_GBS,
-                 "phase_ms_serialised": phase, "ms_per_step_serialised": round(sum(phase.values()), 4)},
-        "pcie_inclusive": pcie,
+                     "algorithmic_bytes_per_launch": top.get("algorithmic_bytes_per_launch"),
+                     "launches_per_step": top.get("launches_per_step"), "ms_per_step": top.get("ms_per_step"),
+                     "kernels": kern},
+        "path": {"algorithmic_bytes_per_step": path_bytes, "effective_GBs_per_gpu": path_gbs,
+                 "frac_of_hbm_peak": path_gbs / HBM_PEAK_GBS, "phase_ms_serialised_rank0": phase},
+        "ranks": {"ms_per_step": rank_ms, "records": rank_records,
+                  "imbalance_records_max_over_mean": max(rank_records) / (sum(rank_records) / len(rank_records)),
+                  "imbalance_ms_max_over_mean": max(rank_ms) / (sum(rank_ms) / len(rank_ms))},
+        "checks": checks,
     }
 
-    # ---- CPU baseline + full-scale parity (rank 0, N=1)
+    # ---- PCIe-inclusive rate, CPU baseline and full-window parity (rank 0, N=1)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        t1 = time.time()
+        d = stream.to_host()
+        log(rank, "[bench] stream copied to the host in %.1fs" % (time.time() - t1))
+        if args.pcie_steps > 0:
+            hkw = dict(counters=(d["c_slot"][:stream.counts[0]], d["c_val"], d["c_rate"]),
+                       gauges=(d["g_slot"], d["g_val"]),
+                       histos=(d["h_slot"][:stream.counts[2]], d["h_val"][:stream.counts[2]],
+                               d["h_rate"][:stream.counts[2]]),
+                       sets=(d["s_slot"][:stream.counts[3]], d["s_off"][:stream.counts[3] + 1],
+                             d["s_bytes"][:stream.counts[3] * 11]))
+
+            def host_step():
+                for c, slots, owners in split_lists:
+                    if len(slots):
+                        eng.split_keys(c, slots, owners)
+                eng.ingest(**hkw)
+                if sum(stream.split_counts):
+                    eng.ingest_split_device(stream.split)
+                return eng.flush_raw()
+            host_step()
+            sync()
+            tp = time.perf_counter()
+            for _ in range(args.pcie_steps):
+                last = host_step()
+            sync()
+            pms = (time.perf_counter() - tp) * 1e3 / args.pcie_steps
+            result["pcie_inclusive"] = {"value": args.samples / (pms * 1e-3), "unit": "samples/s", "ms_per_step": pms,
+                                        "path": "vn_ingest_host from pageable host arrays (host checks + pinned "
+                                                "staging + H2D + kernels); split-key records from HBM"}
         import oracle
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         streams = {k: d[k] for k in ("c_slot", "c_val", "c_rate", "g_slot", "g_val", "h_slot", "h_val", "h_rate",
@@ -248,21 +314,18 @@ def main():
         secs, _, ref = oracle.baseline_run_full(threads, n_slots, streams, PCT)
         result["cpu_baseline"] = {"value": args.samples / secs, "unit": "samples/s", "cores": threads,
                                   "kind": "port", "seconds": secs,
-                                  "sample": "the full C3 flush window above (%d samples); C restatement of the Go "
+                                  "sample": "the full C4 flush window above (%d samples); C restatement of the Go "
                                             "Worker.ProcessMetric + flush path, %d worker threads routed by key"
                                             % (args.samples, threads)}
-        # parity of the last timed step's flush with the restated reference
         o = last
         npct = len(PCT)
-        c_slot = np.ctypeslib.as_array(o.counter_slot, shape=(o.n_counter,)).copy()
-        c_val = np.ctypeslib.as_array(o.counter_value, shape=(o.n_counter,)).copy()
-        g_slot = np.ctypeslib.as_array(o.gauge_slot, shape=(o.n_gauge,)).copy()
-        g_val = np.ctypeslib.as_array(o.gauge_value, shape=(o.n_gauge,)).copy()
-        h_slot = np.ctypeslib.as_array(o.histo_slot, shape=(o.n_histo,)).copy()
-        h_q = np.ctypeslib.as_array(o.histo_quantiles, shape=(o.n_histo * npct,)).copy().reshape(-1, npct)
-        h_st = np.ctypeslib.as_array(o.histo_stats, shape=(o.n_histo * 8,)).copy().reshape(-1, 8)
-        s_slot = np.ctypeslib.as_array(o.set_slot, shape=(o.n_set,)).copy()
-        s_est = np.ctypeslib.as_array(o.set_estimate, shape=(o.n_set,)).copy()
+        arr = lambda p, n, dt: np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, dt)
+        c_slot, c_val = arr(o.counter_slot, o.n_counter, np.uint32), arr(o.counter_value, o.n_counter, np.int64)
+        g_slot, g_val = arr(o.gauge_slot, o.n_gauge, np.uint32), arr(o.gauge_value, o.n_gauge, np.float64)
+        h_slot = arr(o.histo_slot, o.n_histo, np.uint32)
+        h_q = arr(o.histo_quantiles, o.n_histo * npct, np.float64).reshape(-1, npct)
+        h_st = arr(o.histo_stats, o.n_histo * 8, np.float64).reshape(-1, 8)
+        s_slot, s_est = arr(o.set_slot, o.n_set, np.uint32), arr(o.set_estimate, o.n_set, np.uint64)
         par = {
             "counters_bit_exact": bool(np.array_equal(c_slot, np.nonzero(ref["touched"][0])[0]) and
                                        np.array_equal(c_val, ref["counter"][c_slot])),
@@ -277,9 +340,29 @@ def main():
             rel = np.abs(h_st[:, 3:5] - rs[:, 3:5]) / np.abs(rs[:, 3:5])
         par["histo_sum_max_rel_err"] = float(np.nanmax(rel))
         t1 = time.time()
-        errs = rank_error_stats(d, h_slot, h_q, ref["histo_q"][h_slot])
+        # rank error: every key past the exact-replay threshold (split or hot remainder: the
+        # approximated ones) plus a seeded sample of the others
+        rng = np.random.default_rng(7)
+        split_h = set((stream.split_slot0[2] + np.arange(len(split[2]))).tolist())
+        cnt = np.bincount(d["h_slot"], minlength=n_slots[2])
+        big = set(np.nonzero(cnt > (args.exact_threshold or 32768))[0].tolist())
+        pick = np.array(sorted(split_h | big | set(rng.choice(h_slot, min(args.parity_keys, len(h_slot)),
+                                                              replace=False).tolist())), np.uint32)
+        idx = np.searchsorted(h_slot, pick)
+        errs = rank_error_stats(d, pick, h_q[idx], ref["histo_q"][pick])
+        par["rank_error_keys"] = int(len(pick))
         par["rank_error_max"] = {("p%g" % (100 * p)): float(errs[:, k].max()) for k, p in enumerate(PCT)}
         par["rank_error_mean"] = {("p%g" % (100 * p)): float(errs[:, k].mean()) for k, p in enumerate(PCT)}
+        for name, sel in (("split", split_h), ("past_exact_threshold", big)):
+            m = np.isin(pick, list(sel))
+            if m.any():
+                par["rank_error_max_%s_keys" % name] = {("p%g" % (100 * p)): float(errs[m, k].max())
+                                                        for k, p in enumerate(PCT)}
+                par["%s_keys" % name] = int(m.sum())
+        worst = np.argsort(-errs.max(axis=1))[:8]
+        par["rank_error_worst_keys"] = [{"slot": int(pick[i]), "samples": int(cnt[pick[i]]),
+                                         "split": int(pick[i]) in split_h,
+                                         "err": [round(float(x), 7) for x in errs[i]]} for i in worst]
         par["quantiles_bit_exact_frac"] = float(np.mean(np.all(h_q == ref["histo_q"][h_slot], axis=1)))
         result["p99_rank_error"] = par["rank_error_max"]["p99"]
         result["parity"] = par
@@ -287,9 +370,10 @@ def main():
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
-    for b in bufs:
-        b.free()
-    group.close()
+    stream.free()
+    if comm is not None:
+        comm.close()
+    ctrl.close()
 
 
 if __name__ == "__main__":

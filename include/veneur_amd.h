@@ -269,6 +269,17 @@ typedef struct {
   float ms_radix_scatter_total;   /* sum over radix scatter launches */
   uint64_t radix_scatter_launches;
   uint64_t radix_scatter_bytes;   /* algorithmic bytes moved by those launches */
+  /* the exact t-digest replay (k_histo_exact): launches, time, algorithmic bytes = 16 B per
+   * replayed sample + per replayed key 40 B of local statistics and 16 B per centroid written
+   * (min(samples, 160) at delta 100) -- SURVEY.md §8(d) */
+  float ms_histo_replay;
+  uint64_t histo_replay_launches;
+  uint64_t histo_replay_bytes;
+  /* the HLL state machine (k_set_segments): 8 B per grouped record it reads (its per-key
+   * state traffic is left out: a lower bound) */
+  float ms_set_segments;
+  uint64_t set_segment_launches;
+  uint64_t set_segment_bytes;
 } vn_timing;
 int vn_timing_enable(vn_engine* eng, int enable);
 int vn_get_timing(vn_engine* eng, vn_timing* out);

@@ -113,7 +113,10 @@ class Timing(C.Structure):
                 ("ms_ingest_set", C.c_float), ("ms_flush", C.c_float), ("ms_sort_histo", C.c_float),
                 ("ms_sort_set", C.c_float), ("sort_passes_histo", C.c_uint64), ("sort_passes_set", C.c_uint64),
                 ("ms_radix_scatter_total", C.c_float), ("radix_scatter_launches", C.c_uint64),
-                ("radix_scatter_bytes", C.c_uint64)]
+                ("radix_scatter_bytes", C.c_uint64), ("ms_histo_replay", C.c_float),
+                ("histo_replay_launches", C.c_uint64), ("histo_replay_bytes", C.c_uint64),
+                ("ms_set_segments", C.c_float), ("set_segment_launches", C.c_uint64),
+                ("set_segment_bytes", C.c_uint64)]
 
 
 class SynthConfig(C.Structure):
@@ -130,6 +133,21 @@ class SynthOut(C.Structure):
                 ("h_slot", u32p), ("h_val", f64p), ("h_rate", f32p),
                 ("s_slot", u32p), ("s_off", u32p), ("s_bytes", u8p), ("s_nbytes", C.c_uint64),
                 ("key_of_slot", u32p * 4), ("digest_of_slot", u32p * 4)]
+
+
+class SynthDevConfig(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_keys", C.c_uint32), ("zipf_s", C.c_double), ("mix", C.c_double * 4),
+                ("n_samples", C.c_uint64), ("rank", C.c_uint32), ("nranks", C.c_uint32),
+                ("member_universe", C.c_uint64), ("rate_half", C.c_double), ("rate_tenth", C.c_double),
+                ("histo_mu", C.c_double), ("histo_sigma", C.c_double), ("device", C.c_int),
+                ("n_split", C.c_uint32 * 4), ("split_key", u32p * 4)]
+
+
+class SynthDevOut(C.Structure):
+    _fields_ = [("n_slots", C.c_uint32 * 4), ("split_slot0", C.c_uint32 * 4), ("key_of_slot", u32p * 4),
+                ("digest_of_slot", u32p * 4), ("batch", Batch), ("split", SplitBatch),
+                ("n_member_bytes", C.c_uint64), ("n_split_member_bytes", C.c_uint64),
+                ("counter_sum", C.c_int64), ("histo_weight", C.c_double)]
 
 
 def _sig(name, res, *args):
@@ -198,6 +216,9 @@ _sig("vn_timing_enable", C.c_int, vp, C.c_int)
 _sig("vn_get_timing", C.c_int, vp, C.POINTER(Timing))
 _sig("vn_synth_generate", C.c_int, C.POINTER(SynthConfig), C.POINTER(SynthOut))
 _sig("vn_synth_free", None, C.POINTER(SynthOut))
+_sig("vn_synth_device", C.c_int, C.POINTER(SynthDevConfig), C.POINTER(SynthDevOut))
+_sig("vn_synth_device_free", None, C.POINTER(SynthDevOut))
+_sig("vn_synth_key_counts", C.c_int, C.POINTER(SynthDevConfig), C.c_uint64, u32p)
 
 # every symbol include/*.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
@@ -205,6 +226,7 @@ EXPORTED = [
     "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_flush_masked", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
+    "vn_synth_device", "vn_synth_device_free", "vn_synth_key_counts",
     "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",
     "vn_comm_nranks", "vn_comm_allreduce", "vn_engine_set_comm", "vn_split_keys", "vn_ingest_split", "vn_split_combine",
 ]

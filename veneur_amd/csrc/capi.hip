@@ -416,6 +416,8 @@ void destroy_impl(vn_engine* e) {
   if (e->ev_join) (void)hipEventDestroy(e->ev_join);
   if (e->st2) (void)hipStreamDestroy(e->st2);
   for (auto ev : e->pool_storage) (void)hipEventDestroy(ev);
+  for (auto ev : e->pool_rp_storage) (void)hipEventDestroy(ev);
+  for (auto ev : e->pool_ss_storage) (void)hipEventDestroy(ev);
   for (auto& ev : e->ev)
     if (ev) (void)hipEventDestroy(ev);
   if (e->st) (void)hipStreamDestroy(e->st);
@@ -497,6 +499,10 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
   const bool tm = e->timing;
   if (tm) {
     e->pool.used = 0;
+    e->pool_rp.used = 0;
+    e->pool_ss.used = 0;
+    e->kstat_rp = RadixStats{&e->pool_rp, 0, 0};
+    e->kstat_ss = RadixStats{&e->pool_ss, 0, 0};
     e->rstat_c = RadixStats{&e->pool, 0, 0};
     e->rstat_h = RadixStats{&e->pool, 0, 0};
     e->rstat_s = RadixStats{&e->pool, 0, 0};
@@ -892,6 +898,21 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
       t.ms_radix_scatter_total = tot;
       t.radix_scatter_launches = e->rstat_c.launches + e->rstat_h.launches + e->rstat_s.launches;
       t.radix_scatter_bytes = e->rstat_c.bytes + e->rstat_h.bytes + e->rstat_s.bytes;
+      auto pool_ms = [](EventPool& p) {
+        float tot = 0;
+        for (int i = 0; i + 1 < p.used; i += 2) {
+          float ms = 0;
+          VN_HIP_CHECK(hipEventElapsedTime(&ms, p.ev[i], p.ev[i + 1]));
+          tot += ms;
+        }
+        return tot;
+      };
+      t.ms_histo_replay = pool_ms(e->pool_rp);
+      t.histo_replay_launches = e->kstat_rp.launches;
+      t.histo_replay_bytes = e->kstat_rp.bytes;
+      t.ms_set_segments = pool_ms(e->pool_ss);
+      t.set_segment_launches = e->kstat_ss.launches;
+      t.set_segment_bytes = e->kstat_ss.bytes;
     }
   });
 }
@@ -914,6 +935,14 @@ int vn_timing_enable(vn_engine* e, int enable) {
       for (auto& ev : e->pool_storage) VN_HIP_CHECK(hipEventCreate(&ev));
       e->pool.ev = e->pool_storage.data();
       e->pool.cap = (int)e->pool_storage.size();
+      for (auto* ps : {&e->pool_rp_storage, &e->pool_ss_storage}) {
+        ps->resize(64);
+        for (auto& ev : *ps) VN_HIP_CHECK(hipEventCreate(&ev));
+      }
+      e->pool_rp.ev = e->pool_rp_storage.data();
+      e->pool_rp.cap = (int)e->pool_rp_storage.size();
+      e->pool_ss.ev = e->pool_ss_storage.data();
+      e->pool_ss.cap = (int)e->pool_ss_storage.size();
     }
   });
 }

@@ -262,4 +262,8 @@ struct vn_engine {
   std::vector<hipEvent_t> pool_storage;
   vn_timing last{};
   vn::RadixStats rstat_c, rstat_h, rstat_s;
+  // timed launches of the exact replay and of the set state machine (timing mode)
+  vn::EventPool pool_rp, pool_ss;
+  std::vector<hipEvent_t> pool_rp_storage, pool_ss_storage;
+  vn::RadixStats kstat_rp, kstat_ss;
 };

@@ -867,6 +867,14 @@ void histo_compress_segments(const SegCompress& c, ScanScratch& ss, hipStream_t 
   hipLaunchKernelGGL(k_finalize, dim3(c.nseg), dim3(kBlock), 0, st, x);
 }
 
+// timing mode: sum over the replayed keys of min(replayed samples, 160) (centroids written)
+__global__ void k_replay_state(uint32_t n, const uint32_t* __restrict__ ex, unsigned long long* __restrict__ out) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long v = k < n ? (unsigned long long)min(ex[k], 160u) : 0ull;
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, v);
+}
+
 HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate) {
   HistoGroups g{};
   if (!n) return g;
@@ -976,10 +984,29 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   // behind 100k+ replay workgroups -- then the held-back set merge on the side stream.  With
   // no hot key (or when timing) everything runs in order on st.
   const bool fork = nhot && !e->timing;
+  // timing mode: each replay launch bracketed by events (kernel-level roofline of k_histo_exact)
+  auto clocked_replay = [&](hipStream_t s) {
+    hipEvent_t a = e->timing ? e->pool_rp.next() : nullptr, b = e->timing ? e->pool_rp.next() : nullptr;
+    if (a && b) VN_HIP_CHECK(hipEventRecord(a, s));
+    histo_exact_replay(xc, s);
+    if (a && b) VN_HIP_CHECK(hipEventRecord(b, s));
+    if (e->timing) e->kstat_rp.launches++;
+  };
   auto replay_cold = [&](hipStream_t s, RadixScratch& rs) {
     histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
-    histo_exact_replay(xc, s);
+    clocked_replay(s);
   };
+  if (e->timing) {
+    // 16 B per replayed sample, 40 B of local statistics and 16 B per centroid
+    // written per replayed key (<= 160 centroids at delta 100; a key's sample count bounds it)
+    VN_HIP_CHECK(hipMemsetAsync(e->h_cnt + 12, 0, 8, st));
+    hipLaunchKernelGGL(k_replay_state, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_ex,
+                       reinterpret_cast<unsigned long long*>(e->h_cnt + 12));
+    uint64_t cent = 0;
+    VN_HIP_CHECK(hipMemcpyAsync(&cent, e->h_cnt + 12, 8, hipMemcpyDeviceToHost, st));
+    VN_HIP_CHECK(hipStreamSynchronize(st));
+    e->kstat_rp.bytes += 16ull * (n - nremrec) + 40ull * (nreplay + nhot) + 16ull * cent;
+  }
   if (fork) {
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
     VN_HIP_CHECK(hipStreamWaitEvent(e->st4, e->ev_fork3, 0));
@@ -992,7 +1019,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.order64 = nullptr;
   xc.order = e->h_hotlist;
   xc.norder = nhot;
-  histo_exact_replay(xc, fork ? e->st4 : st);
+  clocked_replay(fork ? e->st4 : st);
   if (fork) VN_HIP_CHECK(hipEventRecord(e->ev_join4, e->st4));
 
   // ---- 4. remainders of warm and hot keys: geometric pieces, merged round by round (As/Bs

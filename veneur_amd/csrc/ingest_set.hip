@@ -426,7 +426,14 @@ void set_finish(vn_engine* e) {
   x.tmp = e->stmp;
   x.arena = e->sarena;
   x.err = e->h_err;
+  hipEvent_t ea = e->timing ? e->pool_ss.next() : nullptr, eb = e->timing ? e->pool_ss.next() : nullptr;
+  if (ea && eb) VN_HIP_CHECK(hipEventRecord(ea, st));
   hipLaunchKernelGGL(k_set_segments, dim3(grid), dim3(kBlock), 0, st, x);
+  if (ea && eb) VN_HIP_CHECK(hipEventRecord(eb, st));
+  if (e->timing) {
+    e->kstat_ss.launches++;
+    e->kstat_ss.bytes += 8ull * e->set_pending_n;
+  }
   hipLaunchKernelGGL(k_set_clear_flags, dim3(blocks_for(nk, 256)), dim3(256), 0, st, e->s_cnt, e->s_tl, e->s_bt);
 }
 

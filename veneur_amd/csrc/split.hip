@@ -795,15 +795,33 @@ __global__ __launch_bounds__(kBlock) void k_ep_tfull(EpochCtx x, const uint32_t*
     tfull[k] = t;
   }
 }
-// (c) first rebase candidate strictly after T_full: uint8(r - b) >= 16 (hyperloglog.go:170)
+// (c) first rebase candidate strictly after T_full: uint8(r - b) >= 16 (hyperloglog.go:170).
+// Once b >= 2 most records are candidates (r < b), so the minimum is taken in the wave first:
+// the records are key-sorted, a wave's items nearly always share one key -- one atomic per wave
+// and item, the stragglers of another key go straight to memory.
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+  for (int d = 32; d >= 1; d >>= 1) {
+    const unsigned long long o = (unsigned long long)__shfl_xor((long long)v, d, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
 __global__ void k_ep_cand(EpochCtx x, uint64_t n, unsigned long long* __restrict__ cand) {
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t k, j, idx, r, code;
-    if (!epoch_rec(x, i, k, j, idx, r, code)) continue;
-    const uint32_t t = x.tfull[k];
-    if (t == 0xffffffffu || j <= t) continue;
-    const uint32_t s = x.kslot[k];
-    if (((r - x.base[s]) & 0xffu) >= kHllCapacity) atomicMin(&cand[k], ((unsigned long long)j << 32) | code);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {  // wave-uniform trip count
+    const uint64_t i = i0 + threadIdx.x;
+    uint32_t k = 0xffffffffu, j, idx, r, code;
+    unsigned long long v = ~0ull;
+    if (i < n && epoch_rec(x, i, k, j, idx, r, code)) {
+      const uint32_t t = x.tfull[k];
+      if (t != 0xffffffffu && j > t && ((r - x.base[x.kslot[k]]) & 0xffu) >= kHllCapacity)
+        v = ((unsigned long long)j << 32) | code;
+    }
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(k);
+    const bool same = k == k0;
+    if (!same && v != ~0ull) atomicMin(&cand[k], v);
+    const unsigned long long m = wave_min_u64(same ? v : ~0ull);
+    if ((threadIdx.x & 63) == 0 && m != ~0ull && k0 != 0xffffffffu) atomicMin(&cand[k0], m);
   }
 }
 // (d) registers after the plain max updates of every record before the candidate
@@ -820,7 +838,10 @@ __global__ void k_ep_apply(EpochCtx x, uint64_t n, uint32_t* __restrict__ W) {
     if (!epoch_rec(x, i, k, j, idx, r, code)) continue;
     if ((uint64_t)j >= (x.cand[k] >> 32)) continue;
     const uint32_t b = x.base[x.kslot[k]];
-    if (r > b) atomicMax(&W[(uint64_t)k * kHllM + idx], min(r - b, kHllCapacity - 1));
+    if (r <= b) continue;
+    const uint32_t v = min(r - b, kHllCapacity - 1);
+    uint32_t* w = &W[(uint64_t)k * kHllM + idx];
+    if (v > *w) atomicMax(w, v);  // registers only grow: a stale read only costs an atomic
   }
 }
 // (e) every rank alike: registers <- W; at the candidate the rebase (b += min, registers -= min)

@@ -62,6 +62,14 @@ class Group:
     def sum(self, x):
         return self._reduce(x, self.dist.ReduceOp.SUM if self.dist else None)
 
+    def broadcast_object(self, obj, src=0):
+        """src's object on every rank (small control data only)."""
+        if self.dist is None:
+            return obj
+        box = [obj]
+        self.dist.broadcast_object_list(box, src=src)
+        return box[0]
+
     def gather_object(self, obj):
         """All ranks' objects on every rank (small control data only)."""
         if self.dist is None:

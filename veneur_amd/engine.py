@@ -481,3 +481,94 @@ def synth(seed=1, n_keys=1000, zipf_s=1.0, mix=(0.4, 0.2, 0.25, 0.15), n_samples
     finally:
         A.lib.vn_synth_free(C.byref(out))
     return d
+
+
+# ---------------------------------------------------------------- the C4 stream in HBM
+C3_MIX = (0.4, 0.2, 0.25, 0.15)
+
+
+def _dev_config(seed, n_keys, n_samples, rank, nranks, device, zipf_s=1.0, mix=C3_MIX, member_universe=50_000_000,
+                rate_half=0.05, rate_tenth=0.05, histo_mu=3.912023005428146, histo_sigma=1.0, split=None):
+    cfg = A.SynthDevConfig()
+    cfg.seed, cfg.n_keys, cfg.zipf_s, cfg.n_samples = seed, n_keys, zipf_s, n_samples
+    for i in range(4):
+        cfg.mix[i] = mix[i]
+    cfg.rank, cfg.nranks, cfg.member_universe = rank, nranks, member_universe
+    cfg.rate_half, cfg.rate_tenth, cfg.histo_mu, cfg.histo_sigma = rate_half, rate_tenth, histo_mu, histo_sigma
+    cfg.device = device
+    keep = []
+    for c in range(4):
+        ks = np.ascontiguousarray((split or {}).get(c, np.zeros(0, np.uint32)), np.uint32)
+        keep.append(ks)
+        cfg.n_split[c] = len(ks)
+        cfg.split_key[c] = ks.ctypes.data_as(A.u32p) if len(ks) else None
+    return cfg, keep
+
+
+def synth_key_counts(seed, n_keys, n_samples, n_positions, device=0, **kw):
+    """Record count of every key over the first n_positions of the C4 stream (on the GPU)."""
+    cfg, _ = _dev_config(seed, n_keys, n_samples, 0, 1, device, **kw)
+    out = np.zeros(n_keys, np.uint32)
+    if A.lib.vn_synth_key_counts(C.byref(cfg), n_positions, out.ctypes.data_as(A.u32p)) != 0:
+        raise EngineError("vn_synth_key_counts failed")
+    return out
+
+
+class DeviceStream:
+    """vn_synth_device: this rank's share of the C4 stream, resident in HBM."""
+
+    def __init__(self, seed, n_keys, n_samples, rank, nranks, device=0, split=None, **kw):
+        cfg, self._keep = _dev_config(seed, n_keys, n_samples, rank, nranks, device, split=split, **kw)
+        self.out = A.SynthDevOut()
+        self.device = device
+        rc = A.lib.vn_synth_device(C.byref(cfg), C.byref(self.out))
+        if rc != 0:
+            raise EngineError("vn_synth_device failed (rc=%d)" % rc)
+        o = self.out
+        self.n_slots = tuple(int(o.n_slots[c]) for c in range(4))
+        self.split_slot0 = tuple(int(o.split_slot0[c]) for c in range(4))
+        self.n_split = tuple(int(cfg.n_split[c]) for c in range(4))
+        cp = lambda p, k: np.ctypeslib.as_array(p, shape=(k,)).copy() if k else np.zeros(0, np.uint32)
+        self.key_of_slot = [cp(o.key_of_slot[c], self.n_slots[c]) for c in range(4)]
+        self.digest_of_slot = [cp(o.digest_of_slot[c], self.n_slots[c]) for c in range(4)]
+        self.batch, self.split = o.batch, o.split
+        self.counts = (int(o.batch.n_counter), int(o.batch.n_gauge), int(o.batch.n_histo), int(o.batch.n_set))
+        self.split_counts = (int(o.split.n_histo), int(o.split.n_set))
+        self.n_records = sum(self.counts) + sum(self.split_counts)
+        self.counter_sum = int(o.counter_sum)
+        self.histo_weight = float(o.histo_weight)
+
+    def _host(self, ptr, n, dt):
+        a = np.zeros(max(n, 0), dt)
+        if n:
+            A.lib.vn_copy_to_host(self.device, a.ctypes.data_as(C.c_void_p), C.c_void_p(ptr), a.nbytes)
+        return a
+
+    def to_host(self):
+        """The rank's records as host arrays, split records mapped to their local slots (one
+        consumer's view of the same stream: per-key arrival order is kept)."""
+        b, s = self.batch, self.split
+        h = self._host
+        d = {"c_slot": h(b.counter_slot, b.n_counter, np.uint32), "c_val": h(b.counter_value, b.n_counter, np.float64),
+             "c_rate": h(b.counter_rate, b.n_counter, np.float32),
+             "g_slot": h(b.gauge_slot, b.n_gauge, np.uint32), "g_val": h(b.gauge_value, b.n_gauge, np.float64)}
+        hs = np.concatenate([h(b.histo_slot, b.n_histo, np.uint32),
+                             h(s.histo_key, s.n_histo, np.uint32) + np.uint32(self.split_slot0[2])])
+        d["h_slot"] = hs
+        d["h_val"] = np.concatenate([h(b.histo_value, b.n_histo, np.float64), h(s.histo_value, s.n_histo, np.float64)])
+        d["h_rate"] = np.concatenate([h(b.histo_rate, b.n_histo, np.float32), h(s.histo_rate, s.n_histo, np.float32)])
+        d["s_slot"] = np.concatenate([h(b.set_slot, b.n_set, np.uint32),
+                                      h(s.set_key, s.n_set, np.uint32) + np.uint32(self.split_slot0[3])])
+        mb = np.concatenate([h(b.set_member_bytes, b.n_set * 11, np.uint8),
+                             h(s.set_member_bytes, s.n_set * 11, np.uint8)])
+        d["s_bytes"] = mb
+        d["s_off"] = (np.arange(len(d["s_slot"]) + 1, dtype=np.uint64) * 11).astype(np.uint32)
+        d["n_slots"] = self.n_slots
+        return d
+
+    def free(self):
+        if getattr(self, "out", None) is not None:
+            A.lib.vn_synth_device_free(C.byref(self.out))
+            self.out = None
+
+    __del__ = free
