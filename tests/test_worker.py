@@ -37,13 +37,14 @@ class RecordingEngine:
 
     def import_counters(self, slot, v):
         self.calls.append(("import_counters", slot.tolist(), v.tolist()))
-        self.cval[int(slot[0])] = self.cval.get(int(slot[0]), 0) + int(v[0])
+        for s_, x in zip(slot.tolist(), v.tolist()):
+            self.cval[int(s_)] = self.cval.get(int(s_), 0) + int(x)
 
     def import_gauges(self, slot, v):
         self.calls.append(("import_gauges", slot.tolist(), v.tolist()))
 
     def import_histos(self, slot, p):
-        if p[0] == b"bad":
+        if any(x == b"bad" for x in p):  # the engine applies nothing of a failing batch
             raise EngineError("malformed (rc=-4)")
         self.calls.append(("import_histos", slot.tolist()))
 
@@ -454,3 +455,24 @@ def test_gpu_local_and_global_server_flush():
         assert len(final) == 6 and byname["a.b.c.max"] == 100.0 and byname["a.b.c.50percentile"] == 6.0
     finally:
         w.close()
+
+
+def test_import_chunk_batches_per_class_and_skips_bad_payloads(caplog):
+    """Server.ImportMetrics' chunk (http.go:52-67) reaches the engine as one call per class; a
+    payload that fails to decode is skipped alone (worker.go:246-266 logs and continues)."""
+    w = cpu_worker()
+    ms = [W.JSONMetric(K("h%d" % i, "histogram"), [], b"gob%d" % i) for i in range(5)]
+    ms += [W.JSONMetric(K("c%d" % i, "counter"), [], struct.pack("<q", i)) for i in range(3)]
+    ms += [W.JSONMetric(K("bad", "counter"), [], b"xx")]
+    W.import_metrics([w], ms)
+    names = [c[0] for c in w.engine.calls]
+    assert names.count("import_histos") == 1 and names.count("import_counters") == 1
+    assert [c for c in w.engine.calls if c[0] == "import_histos"][0][1] == [0, 1, 2, 3, 4]
+    assert "payload is 2 bytes" in caplog.text
+    w2 = cpu_worker()
+    ms2 = [W.JSONMetric(K("h%d" % i, "histogram"), [], b"bad" if i == 2 else b"ok") for i in range(4)]
+    W.import_metrics([w2], ms2)
+    ok = [c[1] for c in w2.engine.calls if c[0] == "import_histos"]
+    assert ok == [[0], [1], [3]]  # the failing batch retried one by one, the bad one skipped
+    assert "Could not merge histograms" in caplog.text
+    assert w2.imported == 4

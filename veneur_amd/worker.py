@@ -262,10 +262,11 @@ def json_metrics_by_worker(metrics, num_workers):
 
 
 def import_metrics(workers, metrics):
-    """Server.ImportMetrics (http.go:52-67): each worker's chunk to its ImportMetric, in order."""
+    """Server.ImportMetrics (http.go:52-67): each worker's chunk to its worker, in order -- one
+    batched engine call per sampler class (Worker.import_chunk) where Go sends the chunk down the
+    worker's ImportChan and ImportMetric()s it metric by metric."""
     for chunk, w in json_metrics_by_worker(metrics, len(workers)):
-        for m in chunk:
-            workers[w].import_metric(m)
+        workers[w].import_chunk(chunk)
 
 
 # map name -> (engine class, type name); worker.go:40-58
@@ -468,6 +469,48 @@ class Worker:
             log.error("Could not merge %s: %s", map_name.replace("global_", ""), err)
 
     ImportMetric = import_metric
+
+    def import_chunk(self, metrics):
+        """ImportMetric for every metric of a chunk (worker.go:230-268), with one engine call per
+        sampler class: same Upsert, same arrival order within a class (the only order that can
+        matter: a key belongs to one class), and a payload that fails to decode is logged and
+        skipped alone -- a failing batch is retried metric by metric."""
+        from .engine import EngineError
+        groups = {0: [], 1: [], 2: [], 3: []}
+        for m in metrics:
+            self.imported += 1
+            typ = m.key.type
+            scope = MetricScope.GlobalOnly if typ in (COUNTER_TYPE, GAUGE_TYPE) else MetricScope.MixedScope
+            map_name = _map_for(typ, scope)
+            if map_name is None:
+                log.error("Unknown metric type for importing: %s", typ)
+                continue
+            slot = self._win.upsert(map_name, m.key, m.tags, self.capacity)
+            cls = _MAPS[map_name][0]
+            if cls in (0, 1) and len(m.value) != 8:
+                log.error("Could not merge %s: payload is %d bytes, not 8", map_name.replace("global_", ""),
+                          len(m.value))
+                continue
+            groups[cls].append((slot, m, map_name))
+        self._drain()  # samples staged before the chunk are aggregated first
+        if groups[0]:
+            self.engine.import_counters(np.array([g[0] for g in groups[0]], np.uint32),
+                                        np.array([struct.unpack("<q", g[1].value)[0] for g in groups[0]], np.int64))
+        if groups[1]:
+            self.engine.import_gauges(np.array([g[0] for g in groups[1]], np.uint32),
+                                      np.array([struct.unpack("<d", g[1].value)[0] for g in groups[1]], np.float64))
+        for cls, fn in ((2, self.engine.import_histos), (3, self.engine.import_sets)):
+            items = groups[cls]
+            if not items:
+                continue
+            try:
+                fn(np.array([g[0] for g in items], np.uint32), [bytes(g[1].value) for g in items])
+            except EngineError:  # find the bad payload(s): the engine applied nothing of the batch
+                for slot, m, map_name in items:
+                    try:
+                        fn(np.array([slot], np.uint32), [bytes(m.value)])
+                    except EngineError as err:
+                        log.error("Could not merge %s: %s", map_name, err)
 
     def flush(self, forward=False, is_local=False, need_median=False) -> WorkerMetrics:
         """Worker.Flush (worker.go:271-298): the window's samplers, and a fresh window.  With
