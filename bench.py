@@ -44,13 +44,8 @@ def log(rank, *a):
 def hot_keys(counts, scale, classes, thr_cs, thr_set, max_split):
     """Top keys by window count above the class threshold (counters and timers: a share of the
     per-GPU load; sets: also any key that would keep one workgroup busy for long)."""
-    split = {}
-    est = counts.astype(np.float64) * scale
-    for c, thr in ((0, thr_cs), (2, thr_cs), (3, thr_set)):
-        ks = np.nonzero((classes == c) & (est > thr))[0]
-        ks = ks[np.argsort(-est[ks], kind="stable")][:max_split]
-        split[c] = np.sort(ks).astype(np.uint32)
-    return split
+    from veneur_amd.dist import hot_keys as pick
+    return pick(counts.astype(np.float64) * scale, classes, {0: thr_cs, 2: thr_cs, 3: thr_set}, max_split)
 
 
 def key_classes(seed, n_keys, mix=(0.4, 0.2, 0.25, 0.15)):
@@ -119,15 +114,11 @@ def main():
 
     import veneur_amd as V
     import veneur_amd._abi as A
-    from veneur_amd.dist import Group, env_world
+    from veneur_amd.dist import Group, env_world, make_comm
 
     world, rank, local_rank = env_world()
     ctrl = Group(backend="gloo")  # host control plane: barrier, max / sum of scalars, the RCCL id
-    comm = None
-    if world > 1:
-        uid = V.Comm.unique_id() if rank == 0 else None
-        uid = ctrl.broadcast_object(uid)
-        comm = V.Comm.rccl(uid, world, rank, local_rank)
+    comm = make_comm(ctrl, local_rank)  # the engines' RCCL group (None at N = 1)
 
     # ---- hot keys: top keys by count in the first 2^24 records of the window (every rank alike)
     t0 = time.time()

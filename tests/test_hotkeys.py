@@ -1,22 +1,20 @@
-"""Hot keys spanning GPUs (veneur_amd.dist.exchange_hot): a hot key's samples are spread over
-every rank, and at flush the partial states meet on the owner rank -- every rank exports its
-partial (Histo.Export / Set.Export), one all-gather moves the payloads, the owner imports them
-(Histo.Combine / Set.Combine, worker.go:230-268), counters are summed by an all-reduce.
+"""Hot keys spanning ranks: the split-key combine of split.hip restated on CPU (tests/split_protocol.py)
+and run by world-size 2 and 3 gloo process groups -- the same protocol the engines run over RCCL.
 
-CPU: world-size-2 gloo ranks, each holding its share in the restated Go worker (oracle/) as
-the store; the owner's result must equal (a) the reference's global-merge of the two partials
-and (b) for sets the single-consumer sketch, for histograms the single-consumer quantiles within
-rank-error tolerance.  GPU: the device-resident store (EngineStore) on one GPU, export of one
-engine imported into another straight from HBM."""
+A hot key's records are dealt round-robin by the key's window arrival index (record j to rank
+j % N, veneur_amd.dist.deal).  The owner's combined state is compared with ONE consumer of the
+whole ordered stream (the reference: server.go:655 never splits a key):
+  counters  exact;  sets  bit-identical registers / b / sparse state;
+  histos    within 1e-3 rank error, bit-identical when the key fits the exact prefix.
+The GPU counterpart (the engines themselves) is tests/test_split_gpu.py."""
 import os
 import socket
 
 import numpy as np
-import pytest
-import torch
 import torch.multiprocessing as mp
 
 import oracle
+from tests import split_protocol as SP
 from veneur_amd import dist as D
 
 PCT = (0.5, 0.9, 0.99, 0.999)
@@ -30,52 +28,22 @@ def _free_port():
     return p
 
 
-def _identity(payload):
-    t = oracle.MergingDigest(100.0)
-    t.gob_decode(payload)
-    return np.arange(len(t.centroids()[0]), dtype=np.int64)
-
-
-class OracleStore:
-    """exchange_hot's store backed by the restated Go worker (host payload tensors)."""
-
-    def __init__(self, w):
-        self.w = w
-
-    def export(self, cls, slots):
-        pays = [self.w.histo_gob(int(s)) if cls == "histo" else self.w.set_sketch(int(s)).marshal() for s in slots]
-        off = np.zeros(len(pays) + 1, np.int64)
-        off[1:] = np.cumsum([len(p) for p in pays])
-        buf = torch.from_numpy(np.frombuffer(b"".join(pays) or b"\0", np.uint8).copy())
-        return buf[:int(off[-1])], off
-
-    def import_(self, cls, slots, data, off):
-        b = data.cpu().numpy().tobytes()
-        for s, a, z in zip(slots, off[:-1], off[1:]):
-            p = b[int(a):int(z)]
-            if cls == "histo":
-                assert self.w.import_histo(int(s), p, _identity(p)) == 0
-            else:
-                assert self.w.import_set(int(s), p) == 0
-
-
-def _stream(seed=5):
-    """4 hot histo keys, 3 hot set keys, 2 hot counters; samples dealt round-robin to 2 ranks."""
-    rng = np.random.default_rng(seed)
-    nh, ns, nc = 4, 3, 2
-    h_slot = rng.integers(0, nh, 60000).astype(np.uint32)
-    h_val = np.exp(rng.normal(3.9, 1.0, len(h_slot)))
-    h_rate = np.ones(len(h_slot), np.float32)
-    s_slot = rng.integers(0, ns, 90000).astype(np.uint32)
-    s_hash = rng.integers(0, 2**63, len(s_slot), dtype=np.uint64) * np.uint64(2)
-    c_slot = rng.integers(0, nc, 5000).astype(np.uint32)
-    c_val = rng.integers(1, 10, len(c_slot)).astype(np.float64)
-    c_rate = np.ones(len(c_slot), np.float32)
-    return (nh, ns, nc), (h_slot, h_val, h_rate), (s_slot, s_hash), (c_slot, c_val, c_rate)
-
-
-def _share(arrs, rank, world):
-    return tuple(a[rank::world] for a in arrs)
+def _stream():
+    rng = np.random.default_rng(21)
+    hs = {}
+    hs["h_small"] = np.exp(rng.normal(3.9, 1.0, 3000))        # fits the exact prefix
+    hs["h_warm"] = np.exp(rng.normal(3.9, 1.0, 60000))
+    hs["h_hot"] = np.exp(rng.normal(3.9, 1.0, 400000))
+    rate = {k: np.where(rng.random(len(v)) < 0.1, np.float32(0.5), np.float32(1.0)).astype(np.float32)
+            for k, v in hs.items()}
+    sets = {}
+    sets["s_dense"] = rng.integers(0, 2**64 - 1, 600000, dtype=np.uint64)   # rebases
+    u = rng.integers(0, 2**64 - 1, 8300, dtype=np.uint64)
+    sets["s_late"] = u[rng.integers(0, 8300, 200000)]                       # switches past J0
+    u = rng.integers(0, 2**64 - 1, 50, dtype=np.uint64)
+    sets["s_sparse"] = u[rng.integers(0, 50, 90000)]                        # sparse to the end
+    ctr = rng.integers(-3, 40, (3, 5000)).astype(np.int64)
+    return hs, rate, sets, ctr
 
 
 def _worker(rank, world, port, q):
@@ -83,36 +51,34 @@ def _worker(rank, world, port, q):
                       LOCAL_RANK=str(rank))
     try:
         g = D.Group(backend="gloo")
-        (nh, ns, nc), H, S, Cn = _stream()
-        w = oracle.Worker(nc, 1, nh, ns)
-        hs = _share(H, rank, world)
-        ss = _share(S, rank, world)
-        cs = _share(Cn, rank, world)
-        w.histo(*hs)
-        w.set_hashed(*ss)
-        w.counter(*cs)
-        store = OracleStore(w)
-        h_own = np.arange(nh) % world
-        s_own = (np.arange(ns) + 1) % world
-        D.exchange_hot(g, store, "histo", np.arange(nh, dtype=np.uint32), h_own)
-        D.exchange_hot(g, store, "set", np.arange(ns, dtype=np.uint32), s_own)
-        csum = D.allreduce_counters(g, [w.counter_value(s) for s in range(nc)])
-        res = {"rank": rank,
-               "histo_q": {int(s): [w.histo_quantile(int(s), p) for p in PCT] for s in range(nh) if h_own[s] == rank},
-               "set_est": {int(s): int(w.set_estimate(int(s))) for s in range(ns) if s_own[s] == rank},
-               "counters": csum.tolist()}
-        allres = g.gather_object(res)
+        hs, rate, sets, ctr = _stream()
+        out = {"rank": rank}
+        # counters: each rank's partial sum of its dealt records
+        part = np.array([c[D.deal(len(c), world) == rank].sum() for c in ctr], np.int64)
+        out["counters"] = SP.counters(g, part).tolist()
+        for i, (name, v) in enumerate(sorted(hs.items())):
+            mine = D.deal(len(v), world) == rank
+            w = (np.float32(1.0) / rate[name][mine]).astype(np.float64)
+            td = SP.histo(g, v[mine], w, len(v), owner=i % world)
+            if td is not None:
+                out[name] = [td.quantile(p) for p in PCT]
+        for i, (name, h) in enumerate(sorted(sets.items())):
+            mine = D.deal(len(h), world) == rank
+            sk = SP.sets(g, h[mine], len(h))
+            if i % world == rank:
+                out[name] = (sk.sparse, sk.b, sk.registers().tolist() if not sk.sparse else sorted(
+                    sk.list_codes().tolist()) + ["tmp"] + sorted(sk.tmp_codes().tolist()), sk.estimate())
+        allres = g.gather_object(out)
         g.barrier()
         g.close()
         if rank == 0:
             q.put(allres)
-    except Exception as ex:
+    except Exception as ex:  # surface the failure in the parent
         q.put(repr(ex))
         raise
 
 
-def test_two_rank_hot_key_exchange_gloo():
-    world = 2
+def _run(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -120,76 +86,42 @@ def test_two_rank_hot_key_exchange_gloo():
     for p in procs:
         p.start()
     try:
-        allres = q.get(timeout=300)
+        allres = q.get(timeout=600)
     finally:
         for p in procs:
             p.join(timeout=60)
     assert not isinstance(allres, str), allres
     assert all(p.exitcode == 0 for p in procs)
-    (nh, ns, nc), H, S, Cn = _stream()
-    # (a) the reference's global merge of the partials: owner's partial, then the other's
-    parts = []
-    for r in range(world):
-        w = oracle.Worker(nc, 1, nh, ns)
-        w.histo(*_share(H, r, world))
-        w.set_hashed(*_share(S, r, world))
-        parts.append(w)
-    single = oracle.Worker(nc, 1, nh, ns)
-    single.histo(*H)
-    single.set_hashed(*S)
-    single.counter(*Cn)
-    got_q, got_s = {}, {}
+    got = {}
     for r in allres:
-        got_q.update({int(k): v for k, v in r["histo_q"].items()})
-        got_s.update({int(k): v for k, v in r["set_est"].items()})
-        assert r["counters"] == [single.counter_value(s) for s in range(nc)]
-    for s in range(nh):
-        own = s % world
-        exp = oracle.Worker(nc, 1, nh, ns)
-        exp.histo(*_share(H, own, world))
-        for r in range(world):
-            if r != own:
-                p = parts[r].histo_gob(s)
-                exp.import_histo(s, p, _identity(p))
-        assert got_q[s] == [exp.histo_quantile(s, p) for p in PCT]
-        # (b) against one consumer of every sample: merging two half digests costs what a
-        # reference global pays for merging its locals' digests (a few 1e-3 of rank); that is
-        # the price of splitting a key, which is why only hot keys are split
-        vals = np.sort(H[1][H[0] == s])
-        F = lambda x: np.searchsorted(vals, x, side="right") / len(vals)
-        err = max(abs(F(a) - F(single.histo_quantile(s, p))) for a, p in zip(got_q[s], PCT))
-        assert err <= 5e-3, (s, err)
-    for s in range(ns):
-        own = (s + 1) % world
-        exp = oracle.Worker(nc, 1, nh, ns)
-        exp.set_hashed(*_share(S, own, world))
-        for r in range(world):
-            if r != own:
-                exp.import_set(s, parts[r].set_sketch(s).marshal())
-        assert got_s[s] == exp.set_estimate(s)
-        assert got_s[s] == single.set_estimate(s)  # dense, no rebase: the union is exact
+        got.update(r)
+    hs, rate, sets, ctr = _stream()
+    assert got["counters"] == ctr.sum(axis=1).tolist()
+    for name, v in hs.items():
+        w = (np.float32(1.0) / rate[name]).astype(np.float64)
+        ref = oracle.MergingDigest(100.0)
+        ref.add_many(v, w)
+        rq = [ref.quantile(p) for p in PCT]
+        o = np.argsort(v, kind="stable")
+        cw = np.cumsum(w[o])
+        F = lambda x: cw[np.searchsorted(v[o], x, side="right") - 1] / cw[-1]
+        err = max(abs(F(a) - F(b)) for a, b in zip(got[name], rq))
+        assert err <= 1e-3, (name, err)
+        if len(v) <= SP.P_HOT:
+            assert got[name] == rq, name
+    for name, h in sets.items():
+        sk = oracle.Sketch()
+        for x in h.tolist():
+            sk.insert_hash(int(x))
+        exp = (sk.sparse, sk.b, sk.registers().tolist() if not sk.sparse else sorted(
+            sk.list_codes().tolist()) + ["tmp"] + sorted(sk.tmp_codes().tolist()), sk.estimate())
+        assert tuple(got[name]) == exp, name
+    assert not got["s_dense"][0] and got["s_dense"][1] >= 1 and got["s_sparse"][0]
 
 
-@pytest.mark.gpu
-def test_engine_store_device_resident_roundtrip():
-    """EngineStore on one GPU: export from engine A into a device tensor, import into engine B
-    from HBM (vn_import_*_device); B equals the host-path import."""
-    import veneur_amd as V
-    (nh, ns, nc), H, S, Cn = _stream(7)
-    with V.Engine((1, 1, nh, ns), max_batch_records=1 << 17) as a, \
-            V.Engine((1, 1, nh, ns), max_batch_records=1 << 17) as b, \
-            V.Engine((1, 1, nh, ns), max_batch_records=1 << 17) as c:
-        a.ingest(histos=H, set_hashes=S)
-        sa = D.EngineStore(a)
-        for cls, n in (("histo", nh), ("set", ns)):
-            slots = np.arange(n, dtype=np.uint32)
-            buf, off = sa.export(cls, slots)
-            assert buf.is_cuda
-            D.EngineStore(b).import_(cls, slots, buf, off)
-            host = bytes(buf.cpu().numpy().tobytes())
-            pays = [host[int(off[i]):int(off[i + 1])] for i in range(n)]
-            (c.import_histos if cls == "histo" else c.import_sets)(slots, pays)
-        fb, fc = b.flush(), c.flush()
-    np.testing.assert_array_equal(fb.histo_quantiles, fc.histo_quantiles)
-    np.testing.assert_array_equal(fb.set_estimate, fc.set_estimate)
-    assert fb.samples_imported == nh + ns
+def test_split_protocol_two_ranks_gloo():
+    _run(2)
+
+
+def test_split_protocol_three_ranks_gloo():
+    _run(3)

@@ -2,10 +2,11 @@
 
 Keys are partitioned the way veneur routes them to workers -- FNV-1a-32 digest of
 (name, type, joined tags) modulo the number of consumers (server.go:655,
-samplers/parser.go:213-304) -- so every rank aggregates a disjoint key set and the data
-path needs no collective.  The only collectives are the bench's control plane: a barrier
-around the timed region, the max of the per-rank elapsed times and the sum of samples.
-They run over RCCL ("nccl") on GPUs and over gloo on CPU (the multi-process tests).
+samplers/parser.go:213-304) -- so every rank aggregates a disjoint key set and ordinary keys
+need no collective.  Hot keys are split over the ranks and combined by the engines over RCCL
+(make_comm, deal, hot_keys below; the exchange itself is in libveneur_amd.so).  The host control
+plane -- barrier around the timed region, max of the per-rank times, the RCCL id -- is a
+torch.distributed group, gloo on the host.
 """
 import os
 
@@ -110,126 +111,36 @@ def route_stream(d, rank, n_shards):
 
 
 # ---------------------------------------------------------------- hot keys spanning GPUs
-# One very hot key would pin one GPU under key routing, so its samples may instead be spread
-# over every rank (each rank holds the key in the same slot).  At flush the partial states
-# meet on the key's owner rank (digest % N), the way a global veneur combines what its locals
-# forward (flusher.go:264-353 -> handlers_global.go:53-63 -> worker.go:230-268):
-#   histograms / timers  every rank exports its partial digest (Histo.Export = GobEncode), one
-#                        all-gather moves the payloads, the owner imports them
-#                        (Histo.Combine = MergingDigest.Merge): the all-gather + re-merge
-#   sets                 the same with MarshalBinary / Sketch.Merge: an exact union
-#   counters             all-reduce(sum) of the int64 values
-# On GPUs the payloads stay in HBM end to end: export writes device bytes, RCCL (backend
-# "nccl" = RCCL over xGMI) all-gathers them, import reads them in place.  On CPU (gloo) the
-# same protocol runs over host tensors for the multi-process tests.
+# A key too hot for one GPU is split: its records are dealt round-robin over the ranks by the
+# key's window arrival index, and at flush the engines combine the partial states on the key's
+# owner over RCCL (include/veneur_amd.h "multi-GPU", csrc/split.hip).  The data path lives in
+# libveneur_amd.so; this module only supplies the host-side pieces around it.
 
-def _allgather_payloads(group, payload, off):
-    """All ranks' (bytes, offsets) of one export: payload is a 1-D uint8 tensor on the group's
-    device, off its payload offsets (numpy int64, n+1; n may differ between ranks)."""
-    import torch
-    td = group.dist
-    dev = group.device
-    meta = torch.tensor([payload.numel(), len(off)], dtype=torch.int64, device=dev)
-    metas = [torch.zeros_like(meta) for _ in range(group.world)]
-    td.all_gather(metas, meta)
-    sizes = [int(m[0].item()) for m in metas]
-    noffs = [int(m[1].item()) for m in metas]
-    mx = max(1, max(sizes))
-    pad = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    pad[:payload.numel()] = payload
-    bufs = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(group.world)]
-    td.all_gather(bufs, pad)
-    mo = max(noffs)
-    offt = torch.zeros(mo, dtype=torch.int64, device=dev)
-    offt[:len(off)] = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(dev)
-    offs = [torch.empty_like(offt) for _ in range(group.world)]
-    td.all_gather(offs, offt)
-    return [(bufs[r][:sizes[r]], offs[r][:noffs[r]].cpu().numpy()) for r in range(group.world)]
+def deal(n_records, n_ranks):
+    """Rank of each of a split key's n_records window records: its arrival index j, j % N."""
+    return np.arange(n_records, dtype=np.int64) % int(n_ranks)
 
 
-def _select(buf, off, idx):
-    """The payloads idx of (buf, off), concatenated: (bytes tensor, offsets)."""
-    import torch
-    lens = off[np.asarray(idx) + 1] - off[np.asarray(idx)]
-    new_off = np.zeros(len(idx) + 1, np.int64)
-    np.cumsum(lens, out=new_off[1:])
-    if len(idx) == 0 or new_off[-1] == 0:
-        return torch.zeros(1, dtype=torch.uint8, device=buf.device), new_off
-    return torch.cat([buf[int(off[i]):int(off[i + 1])] for i in idx]), new_off
+def hot_keys(counts, classes, thresholds, max_split=64):
+    """Top keys by window count above their class threshold: {class: sorted key ids}.
+    counts: records per key (e.g. the previous window's), classes: class of every key,
+    thresholds: {class: count} for the classes that may split (counter 0, histo 2, set 3)."""
+    counts = np.asarray(counts, np.float64)
+    out = {}
+    for c, thr in thresholds.items():
+        ks = np.nonzero((classes == c) & (counts > thr))[0]
+        ks = ks[np.argsort(-counts[ks], kind="stable")][:max_split]
+        out[c] = np.sort(ks).astype(np.uint32)
+    return out
 
 
-def exchange_hot(group, store, cls, slots, owners):
-    """Move every rank's partial state of the hot keys `slots` (class "histo" or "set") to the
-    owner rank owners[i] and merge it there, other ranks in rank order.  A rank exports only
-    the keys it does not own (export mutates: GobEncode merges pending temps, as in Go), so
-    the owner's own partial is the first contribution.  store: an EngineStore (GPU) or any
-    object with export(cls, slots) -> (uint8 tensor, offsets) and
-    import_(cls, slots, bytes tensor, offsets)."""
-    slots = np.ascontiguousarray(slots, dtype=np.uint32)
-    owners = np.asarray(owners, dtype=np.int64)
-    if group.dist is None or len(slots) == 0:
-        return
-    payload, off = store.export(cls, slots[owners != group.rank])
-    gathered = _allgather_payloads(group, payload, off)
-    if not np.any(owners == group.rank):
-        return
-    for r in range(group.world):
-        if r == group.rank:
-            continue
-        sent = owners != r                         # what rank r exported, in slot order
-        pick = np.nonzero(owners[sent] == group.rank)[0]
-        if len(pick) == 0:
-            continue
-        buf, off_r = gathered[r]
-        sel, sel_off = _select(buf, off_r, pick)
-        store.import_(cls, slots[sent][pick], sel, sel_off)
-
-
-def allreduce_counters(group, values):
-    """Sum of every rank's int64 counter values of the hot counters (Counter.Combine)."""
-    v = np.ascontiguousarray(values, dtype=np.int64)
+def make_comm(group, device):
+    """The engines' RCCL group: rank 0 draws the unique id, the host control plane (gloo)
+    broadcasts it, every rank joins (vn_comm_init).  None for a group of one."""
+    from .engine import Comm
     if group.dist is None:
-        return v
-    import torch
-    t = torch.from_numpy(v.copy()).to(group.device)
-    group.dist.all_reduce(t, op=group.dist.ReduceOp.SUM)
-    return t.cpu().numpy()
-
-
-class EngineStore:
-    """exchange_hot's view of a GPU engine: device-resident export / import (no host copy)."""
-
-    def __init__(self, engine):
-        self.e = engine
-
-    def export(self, cls, slots):
-        import ctypes as C
-
-        import torch
-
-        from . import _abi as A
-        fn = A.lib.vn_export_histos if cls == "histo" else A.lib.vn_export_sets
-        s = np.ascontiguousarray(slots, dtype=np.uint32)
-        x = A.Export()
-        self.e._check(fn(self.e.h, s.ctypes.data_as(A.u32p), len(s), C.byref(x)))
-        off = np.ctypeslib.as_array(x.off, shape=(x.n + 1,)).astype(np.int64)
-        buf = torch.empty(max(1, int(off[-1])), dtype=torch.uint8, device="cuda:%d" % self.e.device)
-        if off[-1]:
-            rc = A.lib.vn_device_copy(self.e.device, C.c_void_p(buf.data_ptr()), C.c_void_p(x.dev_bytes), int(off[-1]))
-            if rc != 0:
-                raise RuntimeError("vn_device_copy failed")
-        return buf[:int(off[-1])], off
-
-    def import_(self, cls, slots, data, off):
-        import ctypes as C
-
-        import torch
-
-        from . import _abi as A
-        dev = data.device
-        st = torch.from_numpy(np.ascontiguousarray(slots, dtype=np.uint32).view(np.int32)).to(dev)
-        ot = torch.from_numpy(np.ascontiguousarray(off, dtype=np.int64)).to(dev)
-        fn = A.lib.vn_import_histos_device if cls == "histo" else A.lib.vn_import_sets_device
-        torch.cuda.synchronize(dev)
-        self.e._check(fn(self.e.h, C.c_void_p(st.data_ptr()), C.c_void_p(ot.data_ptr()),
-                         C.c_void_p(data.data_ptr()), len(slots)))
+        return None
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")  # one node: the bootstrap stays on loopback
+    uid = Comm.unique_id() if group.rank == 0 else None
+    uid = group.broadcast_object(uid)
+    return Comm.rccl(uid, group.world, group.rank, device)
