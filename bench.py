@@ -106,8 +106,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
     ap.add_argument("--parity-keys", type=int, default=3000, help="histo keys sampled for the rank-error check")
-    ap.add_argument("--timing-steps", type=int, default=1, help="untimed steps with per-kernel HIP-event timing")
+    ap.add_argument("--timing-steps", type=int, default=1,
+                    help="untimed steps with per-kernel HIP-event timing (0: none)")
     ap.add_argument("--profile-steps", type=int, default=0, help="extra untimed steps (for rocprof runs)")
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="development only: run rank --sim-rank's share of an N-GPU split on this one GPU "
+                         "(no exchange partners; not a bench result)")
+    ap.add_argument("--sim-rank", type=int, default=0)
     ap.add_argument("--pcie-steps", type=int, default=1,
                     help="extra steps from host arrays (vn_ingest_host), reported as pcie_inclusive; 0: off")
     args = ap.parse_args()
@@ -117,6 +122,7 @@ def main():
     from veneur_amd.dist import Group, env_world, make_comm
 
     world, rank, local_rank = env_world()
+    sim = args.sim_world > 1 and world == 1
     ctrl = Group(backend="gloo")  # host control plane: barrier, max / sum of scalars, the RCCL id
     comm = make_comm(ctrl, local_rank)  # the engines' RCCL group (None at N = 1)
 
@@ -127,9 +133,10 @@ def main():
         sample = min(args.samples, 1 << 24)
         counts = V.synth_key_counts(args.seed, args.keys, args.samples, sample, device=local_rank)
         classes = key_classes(args.seed, args.keys)
-        thr = args.samples / (world * args.hot_div)
+        thr = args.samples / ((args.sim_world if sim else world) * args.hot_div)
         split = hot_keys(counts, args.samples / sample, classes, thr, min(thr, args.set_hot), args.max_split)
-    stream = V.DeviceStream(args.seed, args.keys, args.samples, rank, world, device=local_rank, split=split)
+    stream = V.DeviceStream(args.seed, args.keys, args.samples, args.sim_rank if sim else rank,
+                            args.sim_world if sim else world, device=local_rank, split=split)
     n_slots = stream.n_slots
     log(rank, "[bench] rank %d/%d: %d of %d samples (c/g/h/s=%s, split h/s=%s), %s slots, split keys c/h/s=%s, "
         "generated in %.1fs" % (rank, world, stream.n_records, args.samples, list(stream.counts),
@@ -195,10 +202,12 @@ def main():
     # timing on, the phases run one after another so every launch is measured alone
     eng.timing_enable(True)
     tim = []
-    for _ in range(max(1, args.timing_steps)):
+    for _ in range(args.timing_steps):
         last = step()
         tim.append(eng.timing())
     eng.timing_enable(False)
+    if not tim:
+        tim = [{k: 0.0 for k, _ in A.Timing._fields_}]
     for _ in range(args.profile_steps):
         last = step()
     mean = lambda k: float(np.mean([t[k] for t in tim]))
@@ -268,7 +277,10 @@ def main():
     }
 
     # ---- PCIe-inclusive rate, CPU baseline and full-window parity (rank 0, N=1)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if sim:
+        result["simulated"] = "rank %d of %d on one GPU, no exchange partners: not a bench result" % (
+            args.sim_rank, args.sim_world)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not sim:
         t1 = time.time()
         d = stream.to_host()
         log(rank, "[bench] stream copied to the host in %.1fs" % (time.time() - t1))

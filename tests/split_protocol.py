@@ -20,7 +20,7 @@ import torch
 
 import oracle
 
-P_HOT, GROWTH, DELTA_HI, J0 = 4096, 25, 500.0, 32768
+P_HOT, GROWTH, DELTA_HI, J0 = 4096, 25, 500.0, 12288
 INF = np.iinfo(np.int64).max
 
 

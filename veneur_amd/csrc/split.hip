@@ -175,17 +175,17 @@ __global__ void k_sh_keys(uint64_t n, const uint32_t* __restrict__ key, const do
 }
 
 // per key, over its run of the key-sorted records: record count and Histo.Sample's Local*
-// statistics (samplers.go:346-356): weight, min, max, sum(x*w), sum(w/x)
+// statistics (samplers.go:346-356): weight, min, max, sum(x*w), sum(w/x).  Blocks of kStatChunks
+// per key (grid y = key) reduce slices of the run into partials; k_sh_stats_fold combines them.
+constexpr uint32_t kStatChunks = 64;
 __global__ __launch_bounds__(kBlock) void k_sh_stats(const uint32_t* __restrict__ start,
                                                      const uint32_t* __restrict__ end, const uint64_t* __restrict__ A,
-                                                     const uint64_t* __restrict__ B, uint64_t* __restrict__ cnt,
-                                                     double* __restrict__ sums, double* __restrict__ mins,
-                                                     double* __restrict__ maxs) {
+                                                     const uint64_t* __restrict__ B, double* __restrict__ part) {
   __shared__ double s_tmp[4];
-  const uint32_t k = blockIdx.x;
+  const uint32_t k = blockIdx.y, c = blockIdx.x;
   const uint32_t lo = start[k], hi = end[k];
   double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
-  for (uint32_t i = lo + threadIdx.x; i < hi; i += kBlock) {
+  for (uint32_t i = lo + c * kBlock + threadIdx.x; i < hi; i += kStatChunks * kBlock) {
     const double x = bitsd(A[i]);
     const double w = (double)(1.0f / __uint_as_float((uint32_t)B[i]));
     sw = dadd(sw, w);
@@ -200,13 +200,30 @@ __global__ __launch_bounds__(kBlock) void k_sh_stats(const uint32_t* __restrict_
   mn = block_allreduce(mn, s_tmp, MinGoOp());
   mx = block_allreduce(mx, s_tmp, MaxGoOp());
   if (threadIdx.x == 0) {
-    cnt[k] = hi - lo;
-    sums[3 * k + 0] = sw;
-    sums[3 * k + 1] = sxw;
-    sums[3 * k + 2] = srw;
-    mins[k] = mn;
-    maxs[k] = mx;
+    double* p = part + ((uint64_t)k * kStatChunks + c) * 5;
+    p[0] = sw; p[1] = sxw; p[2] = srw; p[3] = mn; p[4] = mx;
   }
+}
+__global__ void k_sh_stats_fold(uint32_t H, const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
+                                const double* __restrict__ part, uint64_t* __restrict__ cnt, double* __restrict__ sums,
+                                double* __restrict__ mins, double* __restrict__ maxs) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= H) return;
+  double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf;
+  for (uint32_t c = 0; c < kStatChunks; c++) {
+    const double* p = part + ((uint64_t)k * kStatChunks + c) * 5;
+    sw = dadd(sw, p[0]);
+    sxw = dadd(sxw, p[1]);
+    srw = dadd(srw, p[2]);
+    mn = min_go(mn, p[3]);
+    mx = max_go(mx, p[4]);
+  }
+  cnt[k] = end[k] - start[k];
+  sums[3 * k + 0] = sw;
+  sums[3 * k + 1] = sxw;
+  sums[3 * k + 2] = srw;
+  mins[k] = mn;
+  maxs[k] = mx;
 }
 
 // one element of a split histogram on its way to the owner
@@ -445,7 +462,10 @@ void split_histos(vn_engine* e, vn_comm* c, hipStream_t st) {
   double* sums = sbuf<double>(e, kSStat, 3 * (size_t)H);
   double* mins = sbuf<double>(e, kSMin, H);
   double* maxs = sbuf<double>(e, kSMax, H);
-  hipLaunchKernelGGL(k_sh_stats, dim3(H), dim3(kBlock), 0, st, kst, ken, As, Bs, tot, sums, mins, maxs);
+  double* spart = sbuf<double>(e, kSLocalStats, (size_t)H * kStatChunks * 5);
+  hipLaunchKernelGGL(k_sh_stats, dim3(kStatChunks, H), dim3(kBlock), 0, st, kst, ken, As, Bs, spart);
+  hipLaunchKernelGGL(k_sh_stats_fold, dim3(blocks_for(H, 64)), dim3(64), 0, st, H, kst, ken, spart, tot, sums, mins,
+                     maxs);
   comm_allreduce(c, tot, tot, H, kU64, kSum, st);
   comm_allreduce(c, sums, sums, 3 * (size_t)H, kF64, kSum, st);
   comm_allreduce(c, mins, mins, H, kF64, kMin, st);
@@ -956,7 +976,9 @@ void split_sets(vn_engine* e, vn_comm* c, hipStream_t st) {
   to_dev(downer, S.owner[VN_SET].data(), H, st);
 
   // 2. the first J records of every key, gathered and replayed exactly (sparse phase, switch)
-  uint64_t J = std::min<uint64_t>(32768, std::max<uint64_t>(maxtot, 1));
+  // the sparse phase ends by ~8-9k distinct codes (the list passes 16 KiB); a key still sparse
+  // at J with more records to come gathers 4x more (its trigger sequence goes on)
+  uint64_t J = std::min<uint64_t>(12288, std::max<uint64_t>(maxtot, 1));
   for (;;) {
     const uint32_t M = (uint32_t)((J + N - 1) / N);
     uint32_t* gsend = sbuf<uint32_t>(e, kSW32, (size_t)H * M);
