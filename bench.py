@@ -113,6 +113,8 @@ def main():
                     help="development only: run rank --sim-rank's share of an N-GPU split on this one GPU "
                          "(no exchange partners; not a bench result)")
     ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--host-trace", action="store_true",
+                    help="development only: report host ms in split_keys+ingest_split / ingest / flush")
     ap.add_argument("--pcie-steps", type=int, default=1,
                     help="extra steps from host arrays (vn_ingest_host), reported as pcie_inclusive; 0: off")
     args = ap.parse_args()
@@ -155,14 +157,28 @@ def main():
         owners = (stream.digest_of_slot[c][slots] % np.uint32(world)).astype(np.uint32)
         split_lists.append((c, slots, owners))
 
+    host_marks = []  # --host-trace: host clock at each call's return (development)
+
     def step():
+        t = [time.perf_counter()] if args.host_trace else None
         for c, slots, owners in split_lists:
             if len(slots):
                 eng.split_keys(c, slots, owners)
-        eng.ingest_device(stream.batch)
+        # split records first: they are buffered on the split engine's stream, so the split
+        # combine at flush does not wait behind this engine's ingest
         if sum(stream.split_counts):
             eng.ingest_split_device(stream.split)
-        return eng.flush_raw()
+        if t:
+            t.append(time.perf_counter())
+        eng.ingest_device(stream.batch)
+        if t:
+            t.append(time.perf_counter())
+        r = eng.flush_raw()
+        if t:
+            t.append(time.perf_counter())
+            tm = eng.timing()
+            host_marks.append(np.concatenate([np.diff(t) * 1e3, [tm["ms_split_host"]]]))
+        return r
 
     def sync():
         A.lib.vn_device_synchronize(local_rank)
@@ -181,6 +197,9 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = ctrl.max(elapsed)
     rank_ms = ctrl.gather_object(t_rank * 1e3 / args.steps)
+    if host_marks:
+        log(rank, "[bench] host ms per call (split+ingest_split, ingest, flush; split combine in flush): %s" %
+            np.round(np.mean(host_marks[args.warmup:] or host_marks, axis=0), 3).tolist())
     rank_records = ctrl.gather_object(stream.n_records)
     ms_per_step = elapsed * 1e3 / args.steps
     value = float(args.samples) * args.steps / elapsed

@@ -280,6 +280,10 @@ typedef struct {
   float ms_set_segments;
   uint64_t set_segment_launches;
   uint64_t set_segment_bytes;
+  /* host wall clock of the last vn_flush (filled with timing on or off): the whole call, and
+   * the split combine inside it (its waits are for the split engine's stream only) */
+  float ms_flush_host;
+  float ms_split_host;
 } vn_timing;
 int vn_timing_enable(vn_engine* eng, int enable);
 int vn_get_timing(vn_engine* eng, vn_timing* out);

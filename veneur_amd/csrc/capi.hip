@@ -1,4 +1,5 @@
 // capi.hip -- engine lifetime and the C-ABI of include/veneur_amd.h.
+#include <chrono>
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
@@ -872,8 +873,10 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
                     vn_flush_result* out) {
   if (!e || !out) return VN_EINVAL;
   return guarded(e, [&] {
+    const auto h0 = std::chrono::steady_clock::now();
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[5], e->st));
     split_flush(e);  // split (hot) keys meet on their owner ranks first
+    const auto h1 = std::chrono::steady_clock::now();
     flush_all(e, out, histo_quantile_mask, set_estimate_mask);
     VN_HIP_CHECK(hipGetLastError());
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[6], e->st));
@@ -914,6 +917,9 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
       t.set_segment_launches = e->kstat_ss.launches;
       t.set_segment_bytes = e->kstat_ss.bytes;
     }
+    const auto h2 = std::chrono::steady_clock::now();
+    e->last.ms_flush_host = std::chrono::duration<float, std::milli>(h2 - h0).count();
+    e->last.ms_split_host = std::chrono::duration<float, std::milli>(h1 - h0).count();
   });
 }
 

@@ -69,6 +69,8 @@ struct SplitState {
   float* hrate = nullptr;
   uint64_t* srec = nullptr;         // set records: key << 32 | sparse code (arrival order)
   uint32_t* s_scratch_bt = nullptr; // set ingest: touched flags of the metro64 pass (unused slots)
+  vn_engine* aux = nullptr;         // the split engine (split.hip): split histos / sets combine there
+  hipEvent_t ev_done = nullptr;     // its combine done (this engine's stream waits on it)
   std::vector<void*> scratch;       // flush scratch (freed at destroy)
   std::vector<size_t> scratch_cap;
 };

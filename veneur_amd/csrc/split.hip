@@ -40,7 +40,7 @@ enum ScratchId {
   kSSegT, kSStarts, kSNcNew, kSAccXw, kSAccW, kSHst, kSHnc, kSHcur, kSHspn, kSCm0, kSCm1, kSCw0, kSCw1, kSElem,
   kSSend, kSRecv, kSKeyOff, kSCntMat, kSCntAll, kSOwnList, kSImpA, kSImpB, kSImpA1, kSImpB1, kSImpSlot, kSImpVal,
   kSImpW, kSMicW, kSCP, kSCM, kSPcnt, kSFF, kSW32, kSCand, kSTfull, kSP0, kSDone, kSR2, kSPre, kSDev1,
-  kSLocalStats, kSCtr, kSTouch, kSCount
+  kSLocalStats, kSCtr, kSTouch, kSIota, kSCount
 };
 
 template <class T>
@@ -70,6 +70,43 @@ vn_comm* group_of(vn_engine* e) {
     S.solo = c;
   }
   return S.solo;
+}
+
+// The split engine: a second engine on the same device holding the split histograms and sets
+// while they combine (slot k = split key k).  Its own streams and scratch let the whole combine
+// -- local preparation, exchange, the owner's replay and rounds -- run beside this engine's
+// replay of the ordinary keys; its host waits only wait for its own stream.  The finished
+// states move into this engine's slots (k_split_move_*), before this engine's flush reads them.
+constexpr uint32_t kMaxSplitKeys = 256;  // per class
+
+vn_engine* split_engine(vn_engine* e, uint64_t records) {
+  SplitState& S = e->sp;
+  if (S.aux && S.aux->max_records >= records) return S.aux;
+  if (S.aux) {
+    vn_engine_destroy(S.aux);
+    S.aux = nullptr;
+  }
+  vn_config c = e->cfg;
+  c.capacity[VN_COUNTER] = 0;
+  c.capacity[VN_GAUGE] = 0;
+  c.capacity[VN_HISTO] = kMaxSplitKeys;
+  c.capacity[VN_SET] = kMaxSplitKeys;
+  c.max_batch_records = std::max<uint64_t>(records, 1u << 21);
+  c.max_batch_member_bytes = 0;
+  vn_engine* a = nullptr;
+  if (vn_engine_create(&c, &a) != VN_OK) {
+    const std::string m = a ? a->err : std::string("no engine");
+    if (a) vn_engine_destroy(a);
+    throw std::runtime_error("cannot create the split engine: " + m);
+  }
+  S.aux = a;
+  radix_scratch_reserve(a->rs, std::max<uint64_t>(e->cfg.split_max_records, a->max_records));
+  uint32_t* iota = sbuf<uint32_t>(e, kSIota, kMaxSplitKeys);
+  std::vector<uint32_t> h(kMaxSplitKeys);
+  std::iota(h.begin(), h.end(), 0u);
+  VN_HIP_CHECK(hipMemcpy(iota, h.data(), kMaxSplitKeys * 4, hipMemcpyHostToDevice));
+  if (!S.ev_done) VN_HIP_CHECK(hipEventCreateWithFlags(&S.ev_done, hipEventDisableTiming));
+  return a;
 }
 
 int bits_for_n(uint64_t n) {
@@ -129,6 +166,14 @@ __global__ void k_split_set_codes(uint64_t n, const uint32_t* __restrict__ key, 
   if (i >= n) return;
   const uint64_t x = hashes ? hashes[i] : metro64(bytes + off[i], off[i + 1] - off[i], kMetroSeed);
   out[i] = ((uint64_t)key[i] << 32) | (uint64_t)encode_hash(x);
+}
+
+// the split engine's error flags join this engine's (read at its flush)
+__global__ void k_split_errors(uint32_t* __restrict__ from, uint32_t* __restrict__ to) {
+  if (threadIdx.x == 0 && from[0]) {
+    atomicOr(to, from[0]);
+    from[0] = 0;
+  }
 }
 
 // ---------------------------------------------------------------- counters
@@ -394,40 +439,86 @@ __global__ void k_sh_pre_gather(uint64_t n, const uint64_t* __restrict__ PreA, c
   val[i] = e.x;
   w[i] = e.w;
 }
-// owned keys: piece count from the window total, slot list
-__global__ void k_sh_owned(uint32_t K, const uint32_t* __restrict__ okeys, const uint64_t* __restrict__ tot,
-                           const uint32_t* __restrict__ kslot_all, uint32_t P, const uint64_t* __restrict__ geo,
-                           uint32_t ngeo, uint32_t* __restrict__ tl, uint32_t* __restrict__ pcnt,
-                           uint32_t* __restrict__ list) {
+// owned keys: piece count from the window total; owned key k lives in the split engine's slot k
+__global__ void k_sh_owned(uint32_t K, const uint32_t* __restrict__ okeys, const uint64_t* __restrict__ tot, uint32_t P,
+                           const uint64_t* __restrict__ geo, uint32_t ngeo, uint32_t* __restrict__ tl,
+                           uint32_t* __restrict__ pcnt) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
-  const uint32_t h = okeys[k];
-  const uint64_t t = tot[h];
-  tl[k] = kslot_all[h];
+  const uint64_t t = tot[okeys[k]];
+  tl[k] = k;
   pcnt[k] = t > P ? geo_piece(geo, ngeo, t - 1) + 1 : 0u;
-  list[k] = k;
-}
-// owner: Local* statistics from the all-reduced partials; digest min/max over all samples
-__global__ void k_sh_owner_stats(uint32_t K, const uint32_t* __restrict__ okeys, const uint32_t* __restrict__ kslot,
-                                 const uint64_t* __restrict__ tot, const double* __restrict__ sums,
-                                 const double* __restrict__ mins, const double* __restrict__ maxs,
-                                 double* __restrict__ hst, uint32_t* __restrict__ htouch) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K) return;
-  const uint32_t h = okeys[k], s = kslot[h];
-  if (!tot[h]) return;
-  double* st = hst + (uint64_t)s * VN_HISTO_STATS;
-  st[0] = dadd(st[0], sums[3 * h + 0]);
-  st[1] = min_go(st[1], mins[h]);
-  st[2] = max_go(st[2], maxs[h]);
-  st[3] = dadd(st[3], sums[3 * h + 1]);
-  st[4] = dadd(st[4], sums[3 * h + 2]);
-  st[5] = min_go(st[5], mins[h]);
-  st[6] = max_go(st[6], maxs[h]);
-  htouch[s] = 1;
 }
 
-void split_histos(vn_engine* e, vn_comm* c, hipStream_t st) {
+// per-slot histogram state of an engine (engine.h), for moving a digest between engines
+struct HistoSlots {
+  double* hst;
+  uint32_t *hncent, *htouch, *hseen, *hpend, *hspn;
+  uint8_t* hcur;
+  double *cm0, *cm1, *cw0, *cw1, *hspw, *hpv, *hpw;
+};
+HistoSlots histo_slots(vn_engine* e) {
+  return HistoSlots{e->hst,      e->hncent,   e->htouch,   e->hseen, e->hpend, e->hspn, e->hcur, e->cmean[0],
+                    e->cmean[1], e->cw[0],    e->cw[1],    e->hspw,  e->hpv,   e->hpw};
+}
+// owner: the split engine's digest of owned key k moves into this engine's slot of the key, the
+// Local* statistics from the all-reduced partials, the digest min/max over all samples (the
+// prefix replay was import-tagged); the split engine's slot is left empty for the next window
+__global__ __launch_bounds__(256) void k_split_move_histo(const uint32_t* __restrict__ okeys,
+                                                          const uint32_t* __restrict__ kslot,
+                                                          const uint64_t* __restrict__ tot,
+                                                          const double* __restrict__ sums,
+                                                          const double* __restrict__ mins,
+                                                          const double* __restrict__ maxs, HistoSlots src,
+                                                          HistoSlots dst, uint32_t capc, uint32_t tcap) {
+  const uint32_t k = blockIdx.x, h = okeys[k];
+  if (tot[h]) {
+    const uint32_t s = kslot[h];
+    const uint64_t fo = (uint64_t)k * capc, to = (uint64_t)s * capc;
+    for (uint32_t i = threadIdx.x; i < capc; i += blockDim.x) {
+      dst.cm0[to + i] = src.cm0[fo + i];
+      dst.cm1[to + i] = src.cm1[fo + i];
+      dst.cw0[to + i] = src.cw0[fo + i];
+      dst.cw1[to + i] = src.cw1[fo + i];
+    }
+    for (uint32_t i = threadIdx.x; i < tcap; i += blockDim.x) {
+      dst.hpv[(uint64_t)s * tcap + i] = src.hpv[(uint64_t)k * tcap + i];
+      dst.hpw[(uint64_t)s * tcap + i] = src.hpw[(uint64_t)k * tcap + i];
+    }
+    if (threadIdx.x == 0) {
+      const double* a = src.hst + (uint64_t)k * VN_HISTO_STATS;
+      double* d = dst.hst + (uint64_t)s * VN_HISTO_STATS;
+      d[0] = dadd(a[0], sums[3 * h + 0]);
+      d[1] = min_go(a[1], mins[h]);
+      d[2] = max_go(a[2], maxs[h]);
+      d[3] = dadd(a[3], sums[3 * h + 1]);
+      d[4] = dadd(a[4], sums[3 * h + 2]);
+      d[5] = min_go(a[5], mins[h]);
+      d[6] = max_go(a[6], maxs[h]);
+      d[7] = a[7];
+      dst.hncent[s] = src.hncent[k];
+      dst.hcur[s] = src.hcur[k];
+      dst.hseen[s] = src.hseen[k];
+      dst.hpend[s] = src.hpend[k];
+      dst.hspn[s] = src.hspn[k];
+      dst.hspw[s] = src.hspw[k];
+      dst.htouch[s] = 1;
+    }
+  }
+  if (threadIdx.x == 0) {  // (thread 0 alone read the scalars it clears)
+    double* a = src.hst + (uint64_t)k * VN_HISTO_STATS;
+    a[0] = 0.0; a[1] = kInf; a[2] = -kInf; a[3] = 0.0; a[4] = 0.0; a[5] = kInf; a[6] = -kInf; a[7] = 0.0;
+    src.hncent[k] = 0;
+    src.htouch[k] = 0;
+    src.hseen[k] = 0;
+    src.hpend[k] = 0;
+    src.hspn[k] = 0;
+  }
+}
+
+void split_histos(vn_engine* e, vn_comm* c) {
+  vn_engine* a = e->sp.aux;
+  hipStream_t st = a->st;
   SplitState& S = e->sp;
   const uint32_t H = (uint32_t)S.slot[VN_HISTO].size();
   if (!H) return;
@@ -452,7 +543,7 @@ void split_histos(vn_engine* e, vn_comm* c, hipStream_t st) {
     hipLaunchKernelGGL(k_sh_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, S.hkey, S.hval, S.hrate, A0, B0);
     RadixPass kp[5];
     const int nkp = make_passes(kp, true, 32, kb);
-    const bool fl = radix_sort(A0, B0, A1, B1, n, kp, nkp, e->rs, st, nullptr);
+    const bool fl = radix_sort(A0, B0, A1, B1, n, kp, nkp, a->rs, st, nullptr);
     As = fl ? A1 : A0;
     Bs = fl ? B1 : B0;
     hipLaunchKernelGGL(k_key_runs, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, Bs, kst, ken);
@@ -482,7 +573,7 @@ void split_histos(vn_engine* e, vn_comm* c, hipStream_t st) {
   uint32_t npre = 0;
   if (n) {
     hipLaunchKernelGGL(k_sh_prefix_flags, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, Bs, kst, me, N, P, flag);
-    scan_exclusive_u32(flag, ppos, n, e->ss, st);
+    scan_exclusive_u32(flag, ppos, n, a->ss, st);
     hipLaunchKernelGGL(k_sh_route, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, As, Bs, kst, me, N, P, ppos,
                        e->h_geo, e->n_geo, G, pre, PA, PB);
     to_host(&npre, ppos + n, 1, st);
@@ -500,7 +591,7 @@ void split_histos(vn_engine* e, vn_comm* c, hipStream_t st) {
     RadixPass pp[16];
     int np = make_passes(pp, false, 0, 64);
     np += make_passes(pp + np, true, 32, bits_for_n(nid));
-    const bool fl = radix_sort(PA, PB, PA1, PB1, nrest, pp, np, e->rs, st, nullptr);
+    const bool fl = radix_sort(PA, PB, PA1, PB1, nrest, pp, np, a->rs, st, nullptr);
     SA = fl ? PA1 : PA;
     SB = fl ? PB1 : PB;
     hipLaunchKernelGGL(k_key_runs, dim3(blocks_for(nrest, 256)), dim3(256), 0, st, nrest, SB, ps, pe);
@@ -511,7 +602,7 @@ void split_histos(vn_engine* e, vn_comm* c, hipStream_t st) {
   uint32_t* ids = sbuf<uint32_t>(e, kSIdList, nid);
   uint32_t* idcnt = sbuf<uint32_t>(e, kSIdCnt, 1);
   hipLaunchKernelGGL(k_sh_id_flags, dim3(blocks_for(nid, 256)), dim3(256), 0, st, nid, ps, pe, idflag);
-  compact_flags(idflag, idpos, ids, idcnt, nid, e->ss, st);
+  compact_flags(idflag, idpos, ids, idcnt, nid, a->ss, st);
   uint32_t nseg = 0;
   to_host(&nseg, idcnt, 1, st);
   const double dhi = e->cfg.split_compression > 0 ? e->cfg.split_compression : 5.0 * e->cfg.compression;
@@ -553,18 +644,18 @@ void split_histos(vn_engine* e, vn_comm* c, hipStream_t st) {
   sc.cm1 = sbuf<double>(e, kSCm1, (size_t)nseg * capc);
   sc.cw0 = sbuf<double>(e, kSCw0, (size_t)nseg * capc);
   sc.cw1 = sbuf<double>(e, kSCw1, (size_t)nseg * capc);
-  sc.err = e->h_err;
+  sc.err = a->h_err;
   if (nseg) {
     hipLaunchKernelGGL(k_sh_seg_ranges, dim3(blocks_for(nseg, 256)), dim3(256), 0, st, nseg, ids, ps, pe, ss, se, tl,
                        hcur, sc.hst);
-    histo_compress_segments(sc, e->ss, st);
+    histo_compress_segments(sc, a->ss, st);
   }
   // 5. per key element counts -> send layout grouped by owner
   uint32_t* cP = sbuf<uint32_t>(e, kSCP, H);
   uint32_t* cM = sbuf<uint32_t>(e, kSCM, H);
   uint32_t* moff = sbuf<uint32_t>(e, kSNcNew, nseg + 1);  // (nc_new is free again)
   uint32_t* segbase = sbuf<uint32_t>(e, kSPcnt, H);
-  if (nseg) scan_exclusive_u32(hnc, moff, nseg, e->ss, st);
+  if (nseg) scan_exclusive_u32(hnc, moff, nseg, a->ss, st);
   else VN_HIP_CHECK(hipMemsetAsync(moff, 0, sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_sh_counts, dim3(blocks_for(H, 256)), dim3(256), 0, st, H, kst, ken, ppos, n, hnc, ids, nseg, G,
                      cP, cM);
@@ -612,7 +703,9 @@ void split_histos(vn_engine* e, vn_comm* c, hipStream_t st) {
   SplitElem* recvb = sbuf<SplitElem>(e, kSRecv, nrecv);
   comm_alltoallv(c, sendb, sb.data(), recvb, rb.data(), st);
 
-  // 7. owner: exact replay of the gathered prefixes, pending temps merged, then the pieces
+  // 7. owner: exact replay of the gathered prefixes, pending temps merged, then the pieces --
+  // on the split engine (owned key k in its slot k), whose stream runs beside this engine's
+  // replay; the finished digests move into this engine's slots (k_split_move_histo)
   std::vector<uint32_t> okeys, local(H, 0xffffffffu);
   for (uint32_t h = 0; h < H; h++)
     if (owner[h] == (uint32_t)me) {
@@ -620,85 +713,83 @@ void split_histos(vn_engine* e, vn_comm* c, hipStream_t st) {
       okeys.push_back(h);
     }
   const uint32_t K = (uint32_t)okeys.size();
-  if (K) {
-    uint32_t* dok = sbuf<uint32_t>(e, kSIdCnt, K);
-    uint32_t* dlocal = sbuf<uint32_t>(e, kSSt, H);  // (key runs no longer needed)
-    to_dev(dok, okeys.data(), K, st);
-    to_dev(dlocal, local.data(), H, st);
-    // owned keys: slot, piece counts (from the window totals), list; piece ids = scan of counts
-    // (in scratch: the prefix ingest below reuses the engine's per-key arrays)
-    uint32_t* otl = sbuf<uint32_t>(e, kSTouch, K);
-    uint32_t* opcnt = sbuf<uint32_t>(e, kSPcnt, K + 1);
-    uint32_t* opbase = sbuf<uint32_t>(e, kSCntMat, K + 1);
-    uint32_t* olist = sbuf<uint32_t>(e, kSCtr, K);
-    hipLaunchKernelGGL(k_sh_owned, dim3(blocks_for(K, 256)), dim3(256), 0, st, K, dok, tot, S.d_slot[VN_HISTO], P,
-                       e->h_geo, e->n_geo, otl, opcnt, olist);
-    scan_exclusive_u32(opcnt, opbase, K, e->ss, st);
-    uint32_t* rflag = sbuf<uint32_t>(e, kSFlag, nrecv + 1);
-    uint32_t* rpos = sbuf<uint32_t>(e, kSPos, nrecv + 1);
-    uint32_t nrpre = 0;
-    uint64_t* PreA = sbuf<uint64_t>(e, kSImpA, nrecv);
-    uint64_t* PreB = sbuf<uint64_t>(e, kSImpB, nrecv);
-    uint64_t* PreA1 = sbuf<uint64_t>(e, kSImpA1, nrecv);
-    uint64_t* PreB1 = sbuf<uint64_t>(e, kSImpB1, nrecv);
-    uint64_t* MicA = sbuf<uint64_t>(e, kSA0, nrecv);
-    uint64_t* MicB = sbuf<uint64_t>(e, kSB0, nrecv);
-    uint64_t* MicA1 = sbuf<uint64_t>(e, kSA1, nrecv);
-    uint64_t* MicB1 = sbuf<uint64_t>(e, kSB1, nrecv);
-    double* micw = sbuf<double>(e, kSMicW, nrecv);
-    if (nrecv) {
-      hipLaunchKernelGGL(k_sh_recv_flags, dim3(blocks_for(nrecv, 256)), dim3(256), 0, st, nrecv, recvb, rflag);
-      scan_exclusive_u32(rflag, rpos, nrecv, e->ss, st);
-      hipLaunchKernelGGL(k_sh_recv_split, dim3(blocks_for(nrecv, 256)), dim3(256), 0, st, nrecv, recvb, rpos, dlocal,
-                         opbase, PreA, PreB, MicA, MicB, micw);
-      to_host(&nrpre, rpos + nrecv, 1, st);
-    }
-    if (nrpre) {
-      if (nrpre > e->max_records) throw std::runtime_error("split histogram prefixes exceed max_batch_records");
-      RadixPass rp[6];
-      const int nrp = make_passes(rp, false, 0, 32 + bits_for_n(K));
-      const bool fl = radix_sort(PreA, PreB, PreA1, PreB1, nrpre, rp, nrp, e->rs, st, nullptr);
-      uint32_t* islot = sbuf<uint32_t>(e, kSImpSlot, nrpre);
-      double* ival = sbuf<double>(e, kSImpVal, nrpre);
-      double* iw = sbuf<double>(e, kSImpW, nrpre);
-      hipLaunchKernelGGL(k_sh_pre_gather, dim3(blocks_for(nrpre, 256)), dim3(256), 0, st, (uint64_t)nrpre,
-                         fl ? PreA1 : PreA, fl ? PreB1 : PreB, recvb, otl, islot, ival, iw);
-      // MergingDigest.Add of each prefix record in window order (import-tagged: the Local*
-      // statistics come from the all-reduce; the digest min/max from the samples)
-      ingest_histos(e, nrpre, islot, ival, nullptr, iw);
-    }
-    // merge the pending temps (the single-GPU hot path does the same after the prefix)
-    uint32_t* oslots = sbuf<uint32_t>(e, kSIdList, K);
-    std::vector<uint32_t> hos(K);
-    for (uint32_t k = 0; k < K; k++) hos[k] = S.slot[VN_HISTO][okeys[k]];
-    to_dev(oslots, hos.data(), K, st);
-    histo_merge_pending(e, oslots, K);
-    const uint64_t nmic = nrecv - nrpre;
-    if (nmic) {
-      // pieces: (piece id, mean)-sorted micro-centroids, one mergeAllTemps per piece and round
-      VN_HIP_CHECK(hipMemcpyAsync(e->h_tl, otl, K * 4, hipMemcpyDeviceToDevice, st));
-      VN_HIP_CHECK(hipMemcpyAsync(e->h_pcnt, opcnt, K * 4, hipMemcpyDeviceToDevice, st));
-      VN_HIP_CHECK(hipMemcpyAsync(e->h_pbase, opbase, (K + 1) * 4, hipMemcpyDeviceToDevice, st));
-      VN_HIP_CHECK(hipMemcpyAsync(e->h_hotlist, olist, K * 4, hipMemcpyDeviceToDevice, st));
-      std::vector<uint32_t> hpc(K);
-      to_host(hpc.data(), opcnt, K, st);
-      const uint32_t maxp = *std::max_element(hpc.begin(), hpc.end());
-      uint32_t npid = 0;
-      to_host(&npid, opbase + K, 1, st);
-      RadixPass mp[16];
-      int nmp = make_passes(mp, false, 0, 64);
-      nmp += make_passes(mp + nmp, true, 32, bits_for_n(npid + 1));
-      const bool fl = radix_sort(MicA, MicB, MicA1, MicB1, nmic, mp, nmp, e->rs, st, nullptr);
-      const uint64_t* MA_ = fl ? MicA1 : MicA;
-      const uint64_t* MB_ = fl ? MicB1 : MicB;
-      VN_HIP_CHECK(hipMemsetAsync(e->p_start, 0, (size_t)(npid + 1) * 4, st));
-      VN_HIP_CHECK(hipMemsetAsync(e->p_end, 0, (size_t)(npid + 1) * 4, st));
-      hipLaunchKernelGGL(k_key_runs, dim3(blocks_for(nmic, 256)), dim3(256), 0, st, nmic, MB_, e->p_start, e->p_end);
-      histo_rounds(e, e->h_hotlist, K, maxp, nmic, K, MA_, MB_, e->hA2, e->hB2, micw, st);
-    }
-    hipLaunchKernelGGL(k_sh_owner_stats, dim3(blocks_for(K, 256)), dim3(256), 0, st, K, dok, S.d_slot[VN_HISTO], tot,
-                       sums, mins, maxs, e->hst, e->htouch);
+  if (!K) return;
+  uint32_t* dok = sbuf<uint32_t>(e, kSIdCnt, K);
+  uint32_t* dlocal = sbuf<uint32_t>(e, kSSt, H);  // (key runs no longer needed)
+  to_dev(dok, okeys.data(), K, st);
+  to_dev(dlocal, local.data(), H, st);
+  // owned keys: piece counts (from the window totals); piece ids = scan of counts
+  uint32_t* otl = sbuf<uint32_t>(e, kSTouch, K);
+  uint32_t* opcnt = sbuf<uint32_t>(e, kSPcnt, K + 1);
+  uint32_t* opbase = sbuf<uint32_t>(e, kSCntMat, K + 1);
+  hipLaunchKernelGGL(k_sh_owned, dim3(blocks_for(K, 256)), dim3(256), 0, st, K, dok, tot, P, e->h_geo, e->n_geo, otl,
+                     opcnt);
+  scan_exclusive_u32(opcnt, opbase, K, a->ss, st);
+  uint32_t* rflag = sbuf<uint32_t>(e, kSFlag, nrecv + 1);
+  uint32_t* rpos = sbuf<uint32_t>(e, kSPos, nrecv + 1);
+  uint32_t nrpre = 0;
+  uint64_t* PreA = sbuf<uint64_t>(e, kSImpA, nrecv);
+  uint64_t* PreB = sbuf<uint64_t>(e, kSImpB, nrecv);
+  uint64_t* PreA1 = sbuf<uint64_t>(e, kSImpA1, nrecv);
+  uint64_t* PreB1 = sbuf<uint64_t>(e, kSImpB1, nrecv);
+  uint64_t* MicA = sbuf<uint64_t>(e, kSA0, nrecv);
+  uint64_t* MicB = sbuf<uint64_t>(e, kSB0, nrecv);
+  uint64_t* MicA1 = sbuf<uint64_t>(e, kSA1, nrecv);
+  uint64_t* MicB1 = sbuf<uint64_t>(e, kSB1, nrecv);
+  double* micw = sbuf<double>(e, kSMicW, nrecv);
+  if (nrecv) {
+    hipLaunchKernelGGL(k_sh_recv_flags, dim3(blocks_for(nrecv, 256)), dim3(256), 0, st, nrecv, recvb, rflag);
+    scan_exclusive_u32(rflag, rpos, nrecv, a->ss, st);
+    hipLaunchKernelGGL(k_sh_recv_split, dim3(blocks_for(nrecv, 256)), dim3(256), 0, st, nrecv, recvb, rpos, dlocal,
+                       opbase, PreA, PreB, MicA, MicB, micw);
+    to_host(&nrpre, rpos + nrecv, 1, st);
   }
+  const uint64_t nmic = nrecv - nrpre;
+  if (std::max<uint64_t>(nrpre, nmic) > a->max_records) {  // a larger split engine (rare: grows once)
+    a = split_engine(e, std::max<uint64_t>(nrpre, nmic) + std::max<uint64_t>(nrpre, nmic) / 4);
+    st = a->st;
+  }
+  uint32_t* olist = sbuf<uint32_t>(e, kSIota, kMaxSplitKeys);  // owned key k -> split-engine slot k
+  if (nrpre) {
+    RadixPass rp[6];
+    const int nrp = make_passes(rp, false, 0, 32 + bits_for_n(K));
+    const bool fl = radix_sort(PreA, PreB, PreA1, PreB1, nrpre, rp, nrp, a->rs, st, nullptr);
+    uint32_t* islot = sbuf<uint32_t>(e, kSImpSlot, nrpre);
+    double* ival = sbuf<double>(e, kSImpVal, nrpre);
+    double* iw = sbuf<double>(e, kSImpW, nrpre);
+    hipLaunchKernelGGL(k_sh_pre_gather, dim3(blocks_for(nrpre, 256)), dim3(256), 0, st, (uint64_t)nrpre,
+                       fl ? PreA1 : PreA, fl ? PreB1 : PreB, recvb, otl, islot, ival, iw);
+    // MergingDigest.Add of each prefix record in window order (import-tagged: the Local*
+    // statistics come from the all-reduce; the digest min/max from the samples)
+    ingest_histos(a, nrpre, islot, ival, nullptr, iw);
+  }
+  // merge the pending temps (the single-GPU hot path does the same after the prefix)
+  histo_merge_pending(a, olist, K);
+  if (nmic) {
+    // pieces: (piece id, mean)-sorted micro-centroids, one mergeAllTemps per piece and round
+    VN_HIP_CHECK(hipMemcpyAsync(a->h_tl, otl, K * 4, hipMemcpyDeviceToDevice, st));
+    VN_HIP_CHECK(hipMemcpyAsync(a->h_pcnt, opcnt, K * 4, hipMemcpyDeviceToDevice, st));
+    VN_HIP_CHECK(hipMemcpyAsync(a->h_pbase, opbase, (K + 1) * 4, hipMemcpyDeviceToDevice, st));
+    VN_HIP_CHECK(hipMemcpyAsync(a->h_hotlist, olist, K * 4, hipMemcpyDeviceToDevice, st));
+    std::vector<uint32_t> hpc(K);
+    to_host(hpc.data(), opcnt, K, st);
+    const uint32_t maxp = *std::max_element(hpc.begin(), hpc.end());
+    uint32_t npid = 0;
+    to_host(&npid, opbase + K, 1, st);
+    RadixPass mp[16];
+    int nmp = make_passes(mp, false, 0, 64);
+    nmp += make_passes(mp + nmp, true, 32, bits_for_n(npid + 1));
+    const bool fl = radix_sort(MicA, MicB, MicA1, MicB1, nmic, mp, nmp, a->rs, st, nullptr);
+    const uint64_t* MA_ = fl ? MicA1 : MicA;
+    const uint64_t* MB_ = fl ? MicB1 : MicB;
+    VN_HIP_CHECK(hipMemsetAsync(a->p_start, 0, (size_t)(npid + 1) * 4, st));
+    VN_HIP_CHECK(hipMemsetAsync(a->p_end, 0, (size_t)(npid + 1) * 4, st));
+    hipLaunchKernelGGL(k_key_runs, dim3(blocks_for(nmic, 256)), dim3(256), 0, st, nmic, MB_, a->p_start, a->p_end);
+    histo_rounds(a, a->h_hotlist, K, maxp, nmic, K, MA_, MB_, a->hA2, a->hB2, micw, st);
+  }
+  HistoSlots src = histo_slots(a), dst = histo_slots(e);
+  hipLaunchKernelGGL(k_split_move_histo, dim3(K), dim3(256), 0, st, dok, S.d_slot[VN_HISTO], tot, sums, mins, maxs,
+                     src, dst, e->cap_cent, e->temp_cap);
 }
 
 // ---------------------------------------------------------------- sets
@@ -916,28 +1007,53 @@ __global__ __launch_bounds__(kBlock) void k_ep_finish(uint32_t H, const uint32_t
     }
   }
 }
-// owner keeps the key (touched), the other ranks clear their copy of it
-__global__ void k_ss_final(uint32_t H, const uint32_t* __restrict__ kslot, const uint32_t* __restrict__ owner, int me,
-                           const uint64_t* __restrict__ tot, uint8_t* mode, uint8_t* base, uint32_t* nz, uint32_t* lc,
-                           uint32_t* lb, uint32_t* last, uint32_t* tc, uint32_t* touch) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= H) return;
-  const uint32_t s = kslot[k];
-  if (owner[k] == (uint32_t)me) {
-    touch[s] = tot[k] ? 1u : 0u;
-    if (tot[k]) return;
+// per-slot set state of an engine (engine.h)
+struct SetSlots {
+  uint8_t *mode, *base;
+  uint32_t *nz, *lc, *lb, *last, *tc, *touch, *tmp, *arena;
+};
+SetSlots set_slots(vn_engine* e) {
+  return SetSlots{e->smode, e->sbase, e->snz, e->slc, e->slb, e->slast, e->stc, e->stouch, e->stmp, e->sarena};
+}
+// the owner's sketch moves from the split engine's slot k into this engine's slot of the key;
+// every rank leaves the split engine's slot empty for the next window
+__global__ __launch_bounds__(256) void k_split_move_set(const uint32_t* __restrict__ kslot,
+                                                        const uint32_t* __restrict__ owner, int me,
+                                                        const uint64_t* __restrict__ tot, SetSlots src,
+                                                        SetSlots dst) {
+  const uint32_t k = blockIdx.x;
+  if (owner[k] == (uint32_t)me && tot[k]) {
+    const uint32_t s = kslot[k];
+    for (uint32_t i = threadIdx.x; i < kArenaWords; i += blockDim.x)
+      dst.arena[(uint64_t)s * kArenaWords + i] = src.arena[(uint64_t)k * kArenaWords + i];
+    for (uint32_t i = threadIdx.x; i < kTmpCap; i += blockDim.x)
+      dst.tmp[(uint64_t)s * kTmpCap + i] = src.tmp[(uint64_t)k * kTmpCap + i];
+    if (threadIdx.x == 0) {
+      dst.mode[s] = src.mode[k];
+      dst.base[s] = src.base[k];
+      dst.nz[s] = src.nz[k];
+      dst.lc[s] = src.lc[k];
+      dst.lb[s] = src.lb[k];
+      dst.last[s] = src.last[k];
+      dst.tc[s] = src.tc[k];
+      dst.touch[s] = 1;
+    }
   }
-  touch[s] = 0;
-  mode[s] = 0;
-  base[s] = 0;
-  nz[s] = kHllM;
-  lc[s] = 0;
-  lb[s] = 0;
-  last[s] = 0;
-  tc[s] = 0;
+  if (threadIdx.x == 0) {
+    src.mode[k] = 0;
+    src.base[k] = 0;
+    src.nz[k] = kHllM;
+    src.lc[k] = 0;
+    src.lb[k] = 0;
+    src.last[k] = 0;
+    src.tc[k] = 0;
+    src.touch[k] = 0;
+  }
 }
 
-void split_sets(vn_engine* e, vn_comm* c, hipStream_t st) {
+void split_sets(vn_engine* e, vn_comm* c) {
+  vn_engine* a = e->sp.aux;
+  hipStream_t st = a->st;
   SplitState& S = e->sp;
   const uint32_t H = (uint32_t)S.slot[VN_SET].size();
   if (!H) return;
@@ -955,7 +1071,7 @@ void split_sets(vn_engine* e, vn_comm* c, hipStream_t st) {
     VN_HIP_CHECK(hipMemcpyAsync(R0, S.srec, n * 8, hipMemcpyDeviceToDevice, st));
     RadixPass kp[5];
     const int nkp = make_passes(kp, false, 32, bits_for_n(H));
-    R = radix_sort(R0, nullptr, R1, nullptr, n, kp, nkp, e->rs, st, nullptr) ? R1 : R0;
+    R = radix_sort(R0, nullptr, R1, nullptr, n, kp, nkp, a->rs, st, nullptr) ? R1 : R0;
     hipLaunchKernelGGL(k_key_runs, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, R, kst, ken);
   }
   uint64_t* tot = sbuf<uint64_t>(e, kSTot, H);
@@ -971,7 +1087,7 @@ void split_sets(vn_engine* e, vn_comm* c, hipStream_t st) {
   std::vector<uint64_t> htot(H);
   to_host(htot.data(), tot, H, st);
   const uint64_t maxtot = *std::max_element(htot.begin(), htot.end());
-  uint32_t* kslot = S.d_slot[VN_SET];
+  uint32_t* kslot = sbuf<uint32_t>(e, kSIota, kMaxSplitKeys);  // key k -> split-engine slot k
   uint32_t* downer = sbuf<uint32_t>(e, kSOwnList, H);
   to_dev(downer, S.owner[VN_SET].data(), H, st);
 
@@ -987,15 +1103,15 @@ void split_sets(vn_engine* e, vn_comm* c, hipStream_t st) {
                        kst, ken, R, gsend);
     comm_allgather(c, gsend, grecv, (size_t)H * M * sizeof(uint32_t), st);
     uint64_t* R2 = sbuf<uint64_t>(e, kSR2, (size_t)H * J);
-    hipLaunchKernelGGL(k_ss_reset, dim3(blocks_for(H, 256)), dim3(256), 0, st, H, kslot, e->smode, e->sbase, e->snz,
-                       e->slc, e->slb, e->slast, e->stc);
+    hipLaunchKernelGGL(k_ss_reset, dim3(blocks_for(H, 256)), dim3(256), 0, st, H, kslot, a->smode, a->sbase, a->snz,
+                       a->slc, a->slb, a->slast, a->stc);
     hipLaunchKernelGGL(k_ss_prefix_stream, dim3(std::min<uint64_t>(blocks_for(J, 256), 64), H), dim3(256), 0, st, H, M,
-                       (uint32_t)N, (uint32_t)J, tot, grecv, kslot, R2, e->s_start, e->s_end);
+                       (uint32_t)N, (uint32_t)J, tot, grecv, kslot, R2, a->s_start, a->s_end);
     uint32_t* dH = sbuf<uint32_t>(e, kSDev1, 1);
     to_dev(dH, &H, 1, st);
-    set_replay_ranges(e, R2, dH, kslot, H, st);
+    set_replay_ranges(a, R2, dH, kslot, H, st);
     uint32_t* modes = sbuf<uint32_t>(e, kSIdFlag, H);
-    hipLaunchKernelGGL(k_ss_mode, dim3(blocks_for(H, 256)), dim3(256), 0, st, H, kslot, e->smode, modes);
+    hipLaunchKernelGGL(k_ss_mode, dim3(blocks_for(H, 256)), dim3(256), 0, st, H, kslot, a->smode, modes);
     std::vector<uint32_t> hm(H);
     to_host(hm.data(), modes, H, st);
     bool more = false;  // a key still sparse with records beyond J: its trigger sequence goes on
@@ -1025,9 +1141,9 @@ void split_sets(vn_engine* e, vn_comm* c, hipStream_t st) {
   x.R = R;
   x.kst = kst;
   x.kslot = kslot;
-  x.arena8 = reinterpret_cast<const uint8_t*>(e->sarena);
-  x.base = e->sbase;
-  x.nz = e->snz;
+  x.arena8 = reinterpret_cast<const uint8_t*>(a->sarena);
+  x.base = a->sbase;
+  x.nz = a->snz;
   x.p0 = p0;
   x.done = done;
   x.tfull = tfull;
@@ -1050,10 +1166,10 @@ void split_sets(vn_engine* e, vn_comm* c, hipStream_t st) {
     if (n) hipLaunchKernelGGL(k_ep_apply, dim3(grid), dim3(256), 0, st, x, n, W);
     comm_allreduce(c, W, W, (size_t)H * kHllM, kU32, kMax, st);
     hipLaunchKernelGGL(k_ep_finish, dim3(H), dim3(kBlock), 0, st, H, kslot, W, cand,
-                       reinterpret_cast<uint8_t*>(e->sarena), e->sbase, e->snz, p0, done, e->h_err);
+                       reinterpret_cast<uint8_t*>(a->sarena), a->sbase, a->snz, p0, done, a->h_err);
   }
-  hipLaunchKernelGGL(k_ss_final, dim3(blocks_for(H, 256)), dim3(256), 0, st, H, kslot, downer, me, tot, e->smode,
-                     e->sbase, e->snz, e->slc, e->slb, e->slast, e->stc, e->stouch);
+  hipLaunchKernelGGL(k_split_move_set, dim3(H), dim3(256), 0, st, S.d_slot[VN_SET], downer, me, tot, set_slots(a),
+                     set_slots(e));
 }
 
 }  // namespace
@@ -1065,10 +1181,17 @@ void split_flush(vn_engine* e) {
     return;
   }
   vn_comm* c = group_of(e);
-  hipStream_t st = e->st;
-  split_counters(e, c, st);
-  split_histos(e, c, st);
-  split_sets(e, c, st);
+  if (S.aux) {
+    // histos and sets on the split engine's stream, beside this engine's work; this engine's
+    // stream waits for the moved states (and the group's collectives stay in one order)
+    split_histos(e, c);
+    split_sets(e, c);
+    vn_engine* a = S.aux;
+    hipLaunchKernelGGL(k_split_errors, dim3(1), dim3(64), 0, a->st, a->h_err, e->h_err);
+    VN_HIP_CHECK(hipEventRecord(S.ev_done, a->st));
+    VN_HIP_CHECK(hipStreamWaitEvent(e->st, S.ev_done, 0));
+  }
+  split_counters(e, c, e->st);
   for (int k = 0; k < VN_NCLASS; k++) {
     S.slot[k].clear();
     S.owner[k].clear();
@@ -1078,6 +1201,7 @@ void split_flush(vn_engine* e) {
 
 void split_destroy(vn_engine* e) {
   SplitState& S = e->sp;
+  if (S.aux) (void)hipStreamSynchronize(S.aux->st);
   for (void* p : S.scratch)
     if (p) (void)hipFree(p);
   S.scratch.clear();
@@ -1089,6 +1213,8 @@ void split_destroy(vn_engine* e) {
   if (S.hrate) (void)hipFree(S.hrate);
   if (S.srec) (void)hipFree(S.srec);
   if (S.solo) vn_comm_destroy(S.solo);
+  if (S.aux) vn_engine_destroy(S.aux);
+  if (S.ev_done) (void)hipEventDestroy(S.ev_done);
   S = SplitState{};
 }
 
@@ -1143,6 +1269,8 @@ int vn_split_keys(vn_engine* e, int cls, const uint32_t* slot, const uint32_t* o
       if (owner[i] >= (uint32_t)N) throw std::invalid_argument("split key owner out of range");
       if (seen[slot[i]]++) throw std::invalid_argument("split key slot listed twice");
     }
+    if (cls != VN_COUNTER && n > kMaxSplitKeys) throw std::invalid_argument("more than 256 split keys in a class");
+    if (cls != VN_COUNTER && n) split_engine(e, 0);
     S.slot[cls].assign(slot, slot + n);
     S.owner[cls].assign(owner, owner + n);
     if (n > S.d_cap[cls]) {
@@ -1176,7 +1304,8 @@ int vn_ingest_split(vn_engine* e, const vn_split_batch* b) {
     if ((b->n_histo && (!b->histo_key || !b->histo_value || !b->histo_rate)) ||
         (b->n_set && (!b->set_key || (!b->set_hash && (!b->set_member_off || !b->set_member_bytes)))))
       throw std::invalid_argument("split batch class with records but a null array");
-    hipStream_t st = e->st;
+    vn_engine* a = S.aux;  // exists: this class has split keys
+    hipStream_t st = a->st;
     if (!S.cap) {
       S.cap = e->cfg.split_max_records;
       VN_HIP_CHECK(hipMalloc(&S.hkey, S.cap * 4));
@@ -1186,12 +1315,12 @@ int vn_ingest_split(vn_engine* e, const vn_split_batch* b) {
     }
     const uint64_t nmax = std::max(b->n_histo, b->n_set);
     if (!nmax) return;
-    VN_HIP_CHECK(hipMemsetAsync(e->h_err + 1, 0, sizeof(uint32_t), st));
+    VN_HIP_CHECK(hipMemsetAsync(a->h_err + 1, 0, sizeof(uint32_t), st));
     hipLaunchKernelGGL(k_split_validate, dim3((int)std::min<uint64_t>(blocks_for(nmax, 256), 4096)), dim3(256), 0, st,
-                       *b, nh, ns, e->h_err + 1);
-    VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 15, e->h_err + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+                       *b, nh, ns, a->h_err + 1);
+    VN_HIP_CHECK(hipMemcpyAsync(a->hf_cnt + 15, a->h_err + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     VN_HIP_CHECK(hipStreamSynchronize(st));
-    const uint32_t f = e->hf_cnt[15];
+    const uint32_t f = a->hf_cnt[15];
     if (f & 1u) throw std::invalid_argument("split key index out of range");
     if (f & 2u) throw std::invalid_argument("invalid value added");
     if (f & 4u) throw std::invalid_argument("sample rate must be >0 and <=1");
