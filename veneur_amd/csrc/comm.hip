@@ -153,9 +153,12 @@ void comm_allreduce(vn_comm* c, const void* send, void* recv, size_t count, DTyp
   VN_HIP_CHECK(hipStreamSynchronize(st));
   g.send[c->rank] = send;
   g.barrier();
+  // copies on the caller's stream, complete before the barrier (a device-to-device hipMemcpy
+  // may return before its copy is done)
   for (int r = 0; r < g.n; r++)
-    VN_HIP_CHECK(hipMemcpy(static_cast<char*>(c->scratch) + (size_t)r * bytes, g.send[r], bytes,
-                           hipMemcpyDeviceToDevice));
+    VN_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(c->scratch) + (size_t)r * bytes, g.send[r], bytes,
+                                hipMemcpyDeviceToDevice, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
   g.barrier();  // every rank holds every operand: recv (which may be send) can be written
   const int grid = (int)std::min<size_t>((count + 255) / 256, 4096);
   switch (t) {
@@ -188,7 +191,9 @@ void comm_allgather(vn_comm* c, const void* send, void* recv, size_t bytes, hipS
   g.send[c->rank] = send;
   g.barrier();
   for (int r = 0; r < g.n; r++)
-    VN_HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + (size_t)r * bytes, g.send[r], bytes, hipMemcpyDeviceToDevice));
+    VN_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(recv) + (size_t)r * bytes, g.send[r], bytes,
+                                hipMemcpyDeviceToDevice, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
   g.barrier();
 }
 
@@ -220,9 +225,10 @@ void comm_alltoallv(vn_comm* c, const void* send, const uint64_t* soff, void* re
     const uint64_t a = g.soff[p][me], b = g.soff[p][me + 1];
     if (b - a != roff[p + 1] - roff[p]) throw std::runtime_error("alltoallv: send and receive sizes disagree");
     if (b > a)
-      VN_HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + roff[p], static_cast<const char*>(g.send[p]) + a, b - a,
-                             hipMemcpyDeviceToDevice));
+      VN_HIP_CHECK(hipMemcpyAsync(static_cast<char*>(recv) + roff[p], static_cast<const char*>(g.send[p]) + a, b - a,
+                                  hipMemcpyDeviceToDevice, st));
   }
+  VN_HIP_CHECK(hipStreamSynchronize(st));
   g.barrier();
 }
 

@@ -816,6 +816,210 @@ void histo_rounds(vn_engine* e, const uint32_t* list, uint32_t nkeys, uint32_t m
   }
 }
 
+// The rounds of a few keys with small pieces in one launch (split.hip's owner: every piece is
+// the ranks' micro-centroids, <= N x 1024 of them).  One workgroup per key walks its pieces in
+// order; per piece the same steps as the round pipeline above -- (centroids + piece) in merged
+// order (a centroid before an element only if strictly smaller, merging_digest.go:169), the
+// inclusive weight prefix, k = indexEstimate(W / T) in LDS, the greedy chain (a new centroid
+// where k - k(start) > 1, mergeOne 210-236) walked by one wave, and each centroid's Welford
+// update in element order (thread per centroid) -- with no host round trip and no launch per
+// step.  The merged elements live in the caller's scratch (kFuseMaxL values and weights per key).
+struct FusedRounds {
+  const uint32_t* list;  // key indices (into tl / pcnt / pbase)
+  const uint32_t* tl;
+  const uint32_t* pcnt;
+  const uint32_t* pbase;
+  const uint32_t* pstart;
+  const uint32_t* pend;
+  const uint64_t* PA;    // pieces: ordered value bits, (piece << 32 | tag), sorted by (piece, value)
+  const uint64_t* PB;
+  const double* impw;
+  uint32_t capc;
+  double delta;
+  double* hst;
+  uint32_t* hncent;
+  uint8_t* hcur;
+  uint32_t* hspn;
+  double *cm0, *cm1, *cw0, *cw1;
+  double* val;           // [key][kFuseMaxL]
+  double* w;
+  uint32_t* err;
+};
+__global__ __launch_bounds__(kBlock) void k_rounds_fused(FusedRounds x) {
+  __shared__ double s_k[kFuseMaxL];
+  __shared__ uint32_t s_st[kMaxCent + 1];
+  __shared__ double s_tmp[4];
+  __shared__ uint32_t s_nc;
+  const uint32_t t = threadIdx.x, lane = t & 63;
+  const uint32_t key = x.list[blockIdx.x];
+  const uint32_t s = x.tl[key], npieces = x.pcnt[key], capc = x.capc;
+  double* val = x.val + (uint64_t)blockIdx.x * kFuseMaxL;
+  double* wgt = x.w + (uint64_t)blockIdx.x * kFuseMaxL;
+  uint32_t nc = x.hncent[s];
+  uint8_t cur = x.hcur[s];
+  double* h = x.hst + (uint64_t)s * VN_HISTO_STATS;
+  for (uint32_t j = 0; j < npieces; j++) {
+    const uint32_t g = x.pbase[key] + j;
+    const uint32_t ps = x.pstart[g], np = x.pend[g] - ps;
+    const double* cm = (cur ? x.cm1 : x.cm0) + (uint64_t)s * capc;
+    const double* cw = (cur ? x.cw1 : x.cw0) + (uint64_t)s * capc;
+    const uint32_t L = nc + np;
+    if (np == 0) continue;  // (block-uniform) nothing to merge
+    if (L > kFuseMaxL) {  // the host sizes pieces below this
+      if (t == 0) atomicOr(x.err, 1u);
+      return;
+    }
+    // merged order, weights, the statistics of the piece's elements
+    double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf, dmn = kInf, dmx = -kInf;
+    for (uint32_t u = t; u < L; u += kBlock) {
+      if (u < nc) {
+        const double v = cm[u];
+        uint32_t l = 0, hh = np;  // piece elements <= v
+        while (l < hh) {
+          const uint32_t m = (l + hh) >> 1;
+          if (from_ordered_bits(x.PA[ps + m]) <= v) l = m + 1;
+          else hh = m;
+        }
+        val[u + l] = v;
+        wgt[u + l] = cw[u];
+      } else {
+        const uint32_t i = u - nc;
+        const double v = from_ordered_bits(x.PA[ps + i]);
+        uint32_t l = 0, hh = nc;  // centroids < v
+        while (l < hh) {
+          const uint32_t m = (l + hh) >> 1;
+          if (cm[m] < v) l = m + 1;
+          else hh = m;
+        }
+        const uint32_t tag = (uint32_t)x.PB[ps + i];
+        const double wt = tag_weight(tag, x.impw);
+        dmn = min_go(dmn, v);
+        dmx = max_go(dmx, v);
+        if (tag_is_sample(tag)) {
+          sw = dadd(sw, wt);
+          mn = min_go(mn, v);
+          mx = max_go(mx, v);
+          sxw = dadd(sxw, dmul(v, wt));
+          srw = dadd(srw, dmul(ddiv(1.0, v), wt));
+        }
+        val[i + l] = v;
+        wgt[i + l] = wt;
+      }
+    }
+    __syncthreads();
+    // inclusive weight prefix (thread t: elements [t*q, t*q + q)), k of every element
+    const uint32_t q = (L + kBlock - 1) / kBlock;
+    const uint32_t i0 = min(L, t * q), i1 = min(L, i0 + q);
+    double run = 0.0;
+    for (uint32_t i = i0; i < i1; i++) run = dadd(run, wgt[i]);
+    double T;
+    double acc = block_excl_scan_d(run, s_tmp, T);
+    for (uint32_t i = i0; i < i1; i++) {
+      acc = dadd(acc, wgt[i]);
+      s_k[i] = index_estimate(x.delta, ddiv(acc, T));
+    }
+    __syncthreads();
+    // the chain: next start = first element after pos with k - k(before start) > 1
+    if (t < 64) {
+      uint32_t n2 = 0, pos = 0;
+      double base = index_estimate(x.delta, 0.0);
+      for (;;) {
+        if (n2 >= capc) {
+          if (lane == 0) atomicOr(x.err, 1u);
+          break;
+        }
+        if (lane == 0) s_st[n2] = pos;
+        n2++;
+        bool found = false;
+        for (uint32_t from = pos + 1; from < L; from += 64) {
+          const uint32_t idx = from + lane;
+          const uint64_t m = __ballot(idx < L && dsub(s_k[idx < L ? idx : 0], base) > 1.0);
+          if (m) {
+            pos = from + (uint32_t)__ffsll((unsigned long long)m) - 1;
+            base = s_k[pos - 1];
+            found = true;
+            break;
+          }
+        }
+        if (!found) break;
+      }
+      if (lane == 0) {
+        s_st[n2] = L;
+        s_nc = n2;
+      }
+    }
+    sw = block_allreduce(sw, s_tmp, SumOp());  // (its barrier publishes the chain)
+    sxw = block_allreduce(sxw, s_tmp, SumOp());
+    srw = block_allreduce(srw, s_tmp, SumOp());
+    mn = block_allreduce(mn, s_tmp, MinGoOp());
+    mx = block_allreduce(mx, s_tmp, MaxGoOp());
+    dmn = block_allreduce(dmn, s_tmp, MinGoOp());
+    dmx = block_allreduce(dmx, s_tmp, MaxGoOp());
+    const uint32_t ncn = s_nc;
+    const uint8_t nb = cur ^ 1;
+    double* cmn = (nb ? x.cm1 : x.cm0) + (uint64_t)s * capc;
+    double* cwn = (nb ? x.cw1 : x.cw0) + (uint64_t)s * capc;
+    for (uint32_t ci = t; ci < ncn; ci += kBlock) {
+      const uint32_t a = s_st[ci], b = s_st[ci + 1];
+      double mean = val[a], W = wgt[a];
+      for (uint32_t i = a + 1; i < b; i++) {
+        const double wt = wgt[i];
+        W = dadd(W, wt);
+        mean = dadd(mean, ddiv(dmul(dsub(val[i], mean), wt), W));
+      }
+      cmn[ci] = mean;
+      cwn[ci] = W;
+    }
+    if (t == 0) {
+      h[0] = dadd(h[0], sw);
+      h[1] = min_go(h[1], mn);
+      h[2] = max_go(h[2], mx);
+      h[3] = dadd(h[3], sxw);
+      h[4] = dadd(h[4], srw);
+      h[5] = min_go(h[5], dmn);
+      h[6] = max_go(h[6], dmx);
+      h[7] = T;
+    }
+    nc = ncn;
+    cur = nb;
+    __syncthreads();  // the new centroids are the next piece's merge input
+  }
+  if (t == 0 && npieces) {
+    x.hncent[s] = nc;
+    x.hcur[s] = cur;
+    x.hspn[s] = 0;
+  }
+}
+
+void histo_rounds_fused(vn_engine* e, const uint32_t* list, uint32_t nkeys, const uint64_t* PA, const uint64_t* PB,
+                        const double* impw, double* val, double* w, hipStream_t st) {
+  if (!nkeys) return;
+  FusedRounds x;
+  x.list = list;
+  x.tl = e->h_tl;
+  x.pcnt = e->h_pcnt;
+  x.pbase = e->h_pbase;
+  x.pstart = e->p_start;
+  x.pend = e->p_end;
+  x.PA = PA;
+  x.PB = PB;
+  x.impw = impw;
+  x.capc = e->cap_cent;
+  x.delta = e->cfg.compression;
+  x.hst = e->hst;
+  x.hncent = e->hncent;
+  x.hcur = e->hcur;
+  x.hspn = e->hspn;
+  x.cm0 = e->cmean[0];
+  x.cm1 = e->cmean[1];
+  x.cw0 = e->cw[0];
+  x.cw1 = e->cw[1];
+  x.val = val;
+  x.w = w;
+  x.err = e->h_err;
+  hipLaunchKernelGGL(k_rounds_fused, dim3(nkeys), dim3(kBlock), 0, st, x);
+}
+
 // chunks of each segment: nch[k] = ceil(len / kHTile) (0 for an empty segment)
 __global__ void k_seg_chunks(uint32_t nseg, const uint32_t* __restrict__ start, const uint32_t* __restrict__ end,
                              uint32_t* __restrict__ nch) {

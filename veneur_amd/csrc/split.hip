@@ -40,7 +40,7 @@ enum ScratchId {
   kSSegT, kSStarts, kSNcNew, kSAccXw, kSAccW, kSHst, kSHnc, kSHcur, kSHspn, kSCm0, kSCm1, kSCw0, kSCw1, kSElem,
   kSSend, kSRecv, kSKeyOff, kSCntMat, kSCntAll, kSOwnList, kSImpA, kSImpB, kSImpA1, kSImpB1, kSImpSlot, kSImpVal,
   kSImpW, kSMicW, kSCP, kSCM, kSPcnt, kSFF, kSW32, kSCand, kSTfull, kSP0, kSDone, kSR2, kSPre, kSDev1,
-  kSLocalStats, kSCtr, kSTouch, kSIota, kSCount
+  kSLocalStats, kSCtr, kSTouch, kSIota, kSFuseV, kSFuseW, kSCount
 };
 
 template <class T>
@@ -770,10 +770,6 @@ void split_histos(vn_engine* e, vn_comm* c) {
     VN_HIP_CHECK(hipMemcpyAsync(a->h_tl, otl, K * 4, hipMemcpyDeviceToDevice, st));
     VN_HIP_CHECK(hipMemcpyAsync(a->h_pcnt, opcnt, K * 4, hipMemcpyDeviceToDevice, st));
     VN_HIP_CHECK(hipMemcpyAsync(a->h_pbase, opbase, (K + 1) * 4, hipMemcpyDeviceToDevice, st));
-    VN_HIP_CHECK(hipMemcpyAsync(a->h_hotlist, olist, K * 4, hipMemcpyDeviceToDevice, st));
-    std::vector<uint32_t> hpc(K);
-    to_host(hpc.data(), opcnt, K, st);
-    const uint32_t maxp = *std::max_element(hpc.begin(), hpc.end());
     uint32_t npid = 0;
     to_host(&npid, opbase + K, 1, st);
     RadixPass mp[16];
@@ -785,7 +781,18 @@ void split_histos(vn_engine* e, vn_comm* c) {
     VN_HIP_CHECK(hipMemsetAsync(a->p_start, 0, (size_t)(npid + 1) * 4, st));
     VN_HIP_CHECK(hipMemsetAsync(a->p_end, 0, (size_t)(npid + 1) * 4, st));
     hipLaunchKernelGGL(k_key_runs, dim3(blocks_for(nmic, 256)), dim3(256), 0, st, nmic, MB_, a->p_start, a->p_end);
-    histo_rounds(a, a->h_hotlist, K, maxp, nmic, K, MA_, MB_, a->hA2, a->hB2, micw, st);
+    if ((uint64_t)N * capc + a->cap_cent <= kFuseMaxL) {
+      // every piece is at most N ranks' micro-centroids: all rounds in one launch
+      double* fv = sbuf<double>(e, kSFuseV, (size_t)K * kFuseMaxL);
+      double* fw = sbuf<double>(e, kSFuseW, (size_t)K * kFuseMaxL);
+      histo_rounds_fused(a, olist, K, MA_, MB_, micw, fv, fw, st);
+    } else {
+      VN_HIP_CHECK(hipMemcpyAsync(a->h_hotlist, olist, K * 4, hipMemcpyDeviceToDevice, st));
+      std::vector<uint32_t> hpc(K);
+      to_host(hpc.data(), opcnt, K, st);
+      const uint32_t maxp = *std::max_element(hpc.begin(), hpc.end());
+      histo_rounds(a, a->h_hotlist, K, maxp, nmic, K, MA_, MB_, a->hA2, a->hB2, micw, st);
+    }
   }
   HistoSlots src = histo_slots(a), dst = histo_slots(e);
   hipLaunchKernelGGL(k_split_move_histo, dim3(K), dim3(256), 0, st, dok, S.d_slot[VN_HISTO], tot, sums, mins, maxs,
