@@ -177,7 +177,8 @@ def main():
         if t:
             t.append(time.perf_counter())
             tm = eng.timing()
-            host_marks.append(np.concatenate([np.diff(t) * 1e3, [tm["ms_split_host"]]]))
+            host_marks.append(np.concatenate([np.diff(t) * 1e3, [tm["ms_split_host"], tm["ms_main_ready"],
+                                                                 tm["ms_split_ready"]]]))
         return r
 
     def sync():
@@ -198,7 +199,7 @@ def main():
     elapsed = ctrl.max(elapsed)
     rank_ms = ctrl.gather_object(t_rank * 1e3 / args.steps)
     if host_marks:
-        log(rank, "[bench] host ms per call (split+ingest_split, ingest, flush; split combine in flush): %s" %
+        log(rank, "[bench] host ms per call (split+ingest_split, ingest, flush; split combine in flush); device ms to main / split ready: %s" %
             np.round(np.mean(host_marks[args.warmup:] or host_marks, axis=0), 3).tolist())
     rank_records = ctrl.gather_object(stream.n_records)
     ms_per_step = elapsed * 1e3 / args.steps

@@ -284,6 +284,10 @@ typedef struct {
    * the split combine inside it (its waits are for the split engine's stream only) */
   float ms_flush_host;
   float ms_split_host;
+  /* device clock from the window's first ingest call to: this engine's ingest work done (all
+   * of it queued before vn_flush), and the split combine done (0 without split keys) */
+  float ms_main_ready;
+  float ms_split_ready;
 } vn_timing;
 int vn_timing_enable(vn_engine* eng, int enable);
 int vn_get_timing(vn_engine* eng, vn_timing* out);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """HBM traffic of the roofline kernel from two rocprofv3 --pmc passes.
 
-    python tools/pmc_traffic.py gpurun_out/TAG_pmc_fetch gpurun_out/TAG_pmc_write TAG
+    python tools/pmc_traffic.py gpurun_out/TAG_pmc_fetch gpurun_out/TAG_pmc_write TAG [KERNEL BENCH_JSON]
 
 Each pass is its own `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` run of the same bench
 command (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2: they cannot share a pass).  Both counters
@@ -11,6 +11,11 @@ bytes of a wide coalesced streaming read, so it is doubled; WRITE_SIZE is taken 
 Algorithmic bytes of a k_radix_scatter launch = n records x (8 B key [+ 8 B value]) read +
 the same written; n is recovered from the grid (4096-record tiles, 256 threads per tile), the
 last tile's padding (< 4096 records) being the only approximation.
+
+Any other KERNEL (e.g. k_histo_exact, the bench's dominant kernel): its algorithmic bytes per
+launch are taken from the bench line of the same command (BENCH_JSON, roofline.kernels), which
+counts them from the launch's own work; the PMC traffic is averaged over every
+dispatch of that kernel.
 
 Writes roofline_traffic.json (read by bench.py for `roofline.traffic`) and a copy under
 profiles/TAG_pmc_traffic.json.
@@ -48,10 +53,44 @@ def read_pass(path, counter):
     return out
 
 
+def other_kernel(fetch, write, kernel, bench_json, tag):
+    with open(bench_json) as fh:
+        line = [ln for ln in fh.read().splitlines() if ln.startswith("{")][-1]
+    kern = {k["kernel"]: k for k in json.loads(line)["roofline"]["kernels"]}[kernel]
+    fb = [v * 1024.0 for (name, _, v) in fetch.values() if kernel in name]
+    wb = [v * 1024.0 for (name, _, v) in write.values() if kernel in name]
+    if not fb or len(fb) != len(wb):
+        raise SystemExit("dispatch mismatch: %d fetch vs %d write rows" % (len(fb), len(wb)))
+    n = len(fb)
+    fetch_b, write_b = 2.0 * sum(fb), sum(wb)
+    alg = kern["algorithmic_bytes_per_launch"]
+    return {
+        "kernel": kernel,
+        "dispatches": n,
+        "traffic_per_launch": (fetch_b + write_b) / n,
+        "fetch_per_launch": fetch_b / n,
+        "write_per_launch": write_b / n,
+        "algorithmic_per_launch": alg,
+        "traffic_over_algorithmic": (fetch_b + write_b) / n / alg,
+        "correction": "FETCH_SIZE x2 (gfx950 streaming-read undercount), WRITE_SIZE x1; KiB -> bytes",
+        "source": "profiles/%s_pmc_traffic.json (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; "
+                  "algorithmic bytes per launch from the bench line of the same command)" % tag,
+    }
+
+
 def main():
     fetch_dir, write_dir, tag = sys.argv[1], sys.argv[2], sys.argv[3]
     fetch = read_pass(fetch_dir, "FETCH_SIZE")
     write = read_pass(write_dir, "WRITE_SIZE")
+    if len(sys.argv) > 5 and sys.argv[4] != KERNEL:
+        res = other_kernel(fetch, write, sys.argv[4], sys.argv[5], tag)
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        for p in (os.path.join(root, "roofline_traffic.json"),
+                  os.path.join(root, "profiles", "%s_pmc_traffic.json" % tag)):
+            with open(p, "w") as fh:
+                json.dump(res, fh, indent=1)
+        print(json.dumps(res, indent=1))
+        return
 
     def scatter(rows):
         per = defaultdict(list)

@@ -116,7 +116,8 @@ class Timing(C.Structure):
                 ("radix_scatter_bytes", C.c_uint64), ("ms_histo_replay", C.c_float),
                 ("histo_replay_launches", C.c_uint64), ("histo_replay_bytes", C.c_uint64),
                 ("ms_set_segments", C.c_float), ("set_segment_launches", C.c_uint64),
-                ("set_segment_bytes", C.c_uint64), ("ms_flush_host", C.c_float), ("ms_split_host", C.c_float)]
+                ("set_segment_bytes", C.c_uint64), ("ms_flush_host", C.c_float), ("ms_split_host", C.c_float),
+                ("ms_main_ready", C.c_float), ("ms_split_ready", C.c_float)]
 
 
 class SynthConfig(C.Structure):

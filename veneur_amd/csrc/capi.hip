@@ -73,6 +73,15 @@ int guarded(vn_engine* e, F&& f) {
   }
 }
 
+}  // namespace
+namespace vn {
+void window_open(vn_engine* e, hipStream_t st) {
+  if (e->w_open) return;
+  VN_HIP_CHECK(hipEventRecord(e->ev_w0, st));
+  e->w_open = true;
+}
+}  // namespace vn
+namespace {
 void check_slots_host(const uint32_t* slot, uint64_t n, uint32_t cap, const char* what) {
   for (uint64_t i = 0; i < n; i++)
     if (slot[i] >= cap) throw std::invalid_argument(std::string(what) + " slot out of range");
@@ -115,6 +124,8 @@ void create_impl(vn_engine* e) {
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join4, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork3, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_h2d, hipEventDisableTiming));
+  VN_HIP_CHECK(hipEventCreate(&e->ev_w0));
+  VN_HIP_CHECK(hipEventCreate(&e->ev_wmain));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join3, hipEventDisableTiming));
   hipStream_t st = e->st;
   const uint64_t R = e->max_records;
@@ -343,6 +354,7 @@ void export_impl(vn_engine* e, int cls, const uint32_t* slot, uint64_t n, vn_exp
   ExportBuffers& x = e->exp;
   h2d(x.d_slot, slot, n, e->st);
   if (cls == VN_HISTO) {  // GobEncode merges the pending temps first (merging_digest.go:362)
+    histo_imports_drain(e);
     std::vector<uint32_t> keys(slot, slot + n);
     std::sort(keys.begin(), keys.end());
     keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
@@ -360,6 +372,11 @@ void export_impl(vn_engine* e, int cls, const uint32_t* slot, uint64_t n, vn_exp
 }
 
 void destroy_impl(vn_engine* e) {
+  for (hipEvent_t* ev : {&e->ev_w0, &e->ev_wmain})
+    if (*ev) {
+      (void)hipEventDestroy(*ev);
+      *ev = nullptr;
+    }
   if (e->st) (void)hipStreamSynchronize(e->st);
   split_destroy(e);
   dfree(e->cval); dfree(e->ctouch); dfree(e->gseq); dfree(e->gval); dfree(e->gtouch); dfree(e->pk); dfree(e->pp);
@@ -490,6 +507,7 @@ void validate_device_batch(vn_engine* e, const vn_batch* b) {
 }
 
 void ingest_device(vn_engine* e, const vn_batch* b) {
+  histo_imports_drain(e);  // imports that came first merge first
   if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
       b->n_set > e->max_records)
     throw std::invalid_argument("batch larger than max_batch_records");
@@ -543,6 +561,7 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
 
 
 void ingest_host(vn_engine* e, const vn_batch* b) {
+  histo_imports_drain(e);
   if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
       b->n_set > e->max_records)
     throw std::invalid_argument("batch larger than max_batch_records");
@@ -719,6 +738,7 @@ int vn_submit(vn_engine* e, const vn_batch_counts* c) {
   b.n_set = c->n_set; b.set_slot = p.set_slot; b.set_member_off = p.set_member_off;
   b.set_member_bytes = p.set_member_bytes;
   return guarded(e, [&] {
+    window_open(e, e->st);
     ingest_host(e, &b);
     // the caller refills the engine-owned pinned stage right after this returns: wait until the
     // DMA engine has read it (the kernels keep running)
@@ -728,7 +748,10 @@ int vn_submit(vn_engine* e, const vn_batch_counts* c) {
 
 int vn_ingest_host(vn_engine* e, const vn_batch* b) {
   if (!e || !b) return VN_EINVAL;
-  return guarded(e, [&] { ingest_host(e, b); });
+  return guarded(e, [&] {
+    window_open(e, e->st);
+    ingest_host(e, b);
+  });
 }
 
 int vn_ingest(vn_engine* e, const vn_batch* b) {
@@ -738,6 +761,7 @@ int vn_ingest(vn_engine* e, const vn_batch* b) {
         b->n_set > e->max_records)
       throw std::invalid_argument("batch larger than max_batch_records");
     validate_device_batch(e, b);
+    window_open(e, e->st);
     ingest_device(e, b);
   });
 }
@@ -793,12 +817,16 @@ __global__ void k_check_payloads(uint64_t n, const uint32_t* __restrict__ slot, 
 void import_device(vn_engine* e, int cls, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n) {
   if (n > e->max_records) throw std::invalid_argument("import batch larger than max_batch_records");
   ensure_import(e, n, 0);
-  hipLaunchKernelGGL(k_check_payloads, dim3(blocks_for(n, 256)), dim3(256), 0, e->st, n, slot, off, e->cap[cls],
-                     e->h_err);
-  VN_HIP_CHECK(hipStreamSynchronize(e->st));
-  take_decode_error(e);
-  if (cls == VN_HISTO) import_histos(e, n, slot, off, bytes);
-  else import_sets(e, n, slot, off, bytes);
+  if (cls == VN_HISTO) {
+    import_histos(e, n, slot, off, bytes);  // (its count pass validates slots and offsets)
+    VN_HIP_CHECK(hipStreamSynchronize(e->st));  // the caller's payload arrays are read when this returns
+  } else {
+    hipLaunchKernelGGL(k_check_payloads, dim3(blocks_for(n, 256)), dim3(256), 0, e->st, n, slot, off, e->cap[cls],
+                       e->h_err);
+    VN_HIP_CHECK(hipStreamSynchronize(e->st));
+    take_decode_error(e);
+    import_sets(e, n, slot, off, bytes);
+  }
   VN_HIP_CHECK(hipGetLastError());
   e->imported += n;
 }
@@ -832,6 +860,7 @@ int vn_histo_query(vn_engine* e, int kind, const uint32_t* slot, const double* a
     if (kind == 0)
       for (uint64_t i = 0; i < n; i++)
         if (!(arg[i] >= 0.0 && arg[i] <= 1.0)) throw std::invalid_argument("quantile out of bounds");  // 284-286
+    histo_imports_drain(e);
     std::vector<uint32_t> keys(slot, slot + n);
     std::sort(keys.begin(), keys.end());
     keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
@@ -874,6 +903,8 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
   if (!e || !out) return VN_EINVAL;
   return guarded(e, [&] {
     const auto h0 = std::chrono::steady_clock::now();
+    histo_imports_drain(e);
+    if (e->w_open) VN_HIP_CHECK(hipEventRecord(e->ev_wmain, e->st));
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[5], e->st));
     split_flush(e);  // split (hot) keys meet on their owner ranks first
     const auto h1 = std::chrono::steady_clock::now();
@@ -920,12 +951,20 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
     const auto h2 = std::chrono::steady_clock::now();
     e->last.ms_flush_host = std::chrono::duration<float, std::milli>(h2 - h0).count();
     e->last.ms_split_host = std::chrono::duration<float, std::milli>(h1 - h0).count();
+    e->last.ms_main_ready = e->last.ms_split_ready = 0.0f;
+    if (e->w_open) {  // (flush_all synchronised both streams)
+      VN_HIP_CHECK(hipEventElapsedTime(&e->last.ms_main_ready, e->ev_w0, e->ev_wmain));
+      if (e->sp.ran) VN_HIP_CHECK(hipEventElapsedTime(&e->last.ms_split_ready, e->ev_w0, e->sp.ev_done));
+      e->w_open = false;
+    }
+    e->sp.ran = false;
   });
 }
 
 int vn_sync(vn_engine* e) {
   if (!e) return VN_EINVAL;
   return guarded(e, [&] {
+    histo_imports_drain(e);
     VN_HIP_CHECK(hipStreamSynchronize(e->st));
     check_error_flags(e);
   });
@@ -963,6 +1002,7 @@ int vn_read_histo(vn_engine* e, uint32_t slot, double* means, double* weights, u
                   double* stats) {
   if (!e || slot >= e->cap[VN_HISTO]) return VN_EINVAL;
   return guarded(e, [&] {
+    histo_imports_drain(e);
     VN_HIP_CHECK(hipStreamSynchronize(e->st));
     uint32_t nc = 0;
     uint8_t cur = 0;

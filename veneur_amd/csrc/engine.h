@@ -34,6 +34,7 @@ struct ImportScratch {
   uint32_t* cslot = nullptr;      // [cap_cent] decoded centroids: slot, mean, weight
   double* cmean = nullptr;
   double* cw = nullptr;
+  uint64_t acc = 0;               // imported histo centroids appended, not yet merged (import_histo.hip)
 };
 
 // Export results (vn_export_histos / vn_export_sets): engine-owned, valid until the next export.
@@ -71,6 +72,7 @@ struct SplitState {
   uint32_t* s_scratch_bt = nullptr; // set ingest: touched flags of the metro64 pass (unused slots)
   vn_engine* aux = nullptr;         // the split engine (split.hip): split histos / sets combine there
   hipEvent_t ev_done = nullptr;     // its combine done (this engine's stream waits on it)
+  bool ran = false;                 // ev_done recorded by this window's flush
   std::vector<void*> scratch;       // flush scratch (freed at destroy)
   std::vector<size_t> scratch_cap;
 };
@@ -84,6 +86,10 @@ struct vn_engine {
   hipStream_t st2 = nullptr;      // side stream: counters, gauges and sets overlap the histo path
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_h2d = nullptr;    // recorded after a host batch's copies into HBM (vn_submit waits on it)
+  // window milestones (vn_timing.ms_main_ready / ms_split_ready): first ingest call of the
+  // window, this engine's queued ingest work done (recorded as vn_flush starts)
+  hipEvent_t ev_w0 = nullptr, ev_wmain = nullptr;
+  bool w_open = false;
   // replay stream: the exact replay of the keys under the threshold runs here while the hot
   // keys' short prefix and remainder rounds run on st (st itself when timing is enabled)
   hipStream_t st3 = nullptr;

@@ -234,6 +234,8 @@ __device__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double
           if (EMIT) {
             mean[cnt] = m;
             w[cnt] = wt;
+          } else if (d_isnan(m) || d_isinf(m) || wt <= 0.0) {
+            return -1;  // Merge's Add would panic (merging_digest.go:98-100)
           }
           cnt++;
         }
@@ -249,12 +251,16 @@ __device__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double
   return (have && floats == 3) ? cnt : -1;
 }
 
-__global__ void k_gob_count(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+// per payload: its centroid count, the whole payload validated (slot in range, offsets
+// non-decreasing, a well-formed digest, every centroid a valid Add), so the emit cannot fail
+__global__ void k_gob_count(uint64_t n, const uint32_t* __restrict__ slot, uint32_t cap,
+                            const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t len = off[i + 1] - off[i];
-  const int64_t c = len <= 0xffffffffull ? gob_digest<false>(bytes + off[i], (uint32_t)len, nullptr, nullptr) : -1;
+  const bool ok = slot[i] < cap && off[i + 1] >= off[i] && len <= 0xffffffffull;
+  const int64_t c = ok ? gob_digest<false>(bytes + off[i], (uint32_t)len, nullptr, nullptr) : -1;
   if (c < 0 || c > (int64_t)kTagIndex) {
     atomicOr(err, kErrDecode);
     cnt[i] = 0;
@@ -264,12 +270,12 @@ __global__ void k_gob_count(uint64_t n, const uint64_t* __restrict__ off, const 
 }
 
 __global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
-                           const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff,
+                           const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff, uint64_t base,
                            uint32_t* __restrict__ oslot, double* __restrict__ omean, double* __restrict__ ow,
                            uint32_t* __restrict__ err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t o = coff[i];
+  const uint64_t o = base + coff[i];
   const int64_t c = gob_digest<true>(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), omean + o, ow + o);
   if (c < 0) {
     atomicOr(err, kErrDecode);
@@ -285,24 +291,38 @@ __global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const u
 
 }  // namespace
 
+// Histo.Combine of a batch of forwarded digests: decoded and validated now (one host round
+// trip: the centroid count), their centroids appended in arrival order to the engine's import
+// run, which is merged -- re-Add of every centroid through the exact replay / hot remainder
+// -- in one ingest when it fills or before anything reads or adds to a histogram
+// (histo_imports_drain).  Merging a run of imports at once equals merging them one call
+// after another: the replay is the same ordered stream of Adds.
 void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes) {
   if (!n) return;
   hipStream_t st = e->st;
   ImportScratch& s = e->imp;
-  hipLaunchKernelGGL(k_gob_count, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, s.cnt, e->h_err);
+  hipLaunchKernelGGL(k_gob_count, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, e->cap[VN_HISTO], off, bytes,
+                     s.cnt, e->h_err);
   scan_exclusive_u32(s.cnt, s.coff, n, e->ss, st);
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 9, s.coff + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipStreamSynchronize(st));
   take_decode_error(e);
   const uint64_t nc = e->hf_cnt[9];
-  if (nc > e->max_records)
+  if (nc > s.cap_cent)
     throw std::invalid_argument("imported digests hold more centroids than max_batch_records: split the import");
   if (!nc) return;
-  hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.cslot,
-                     s.cmean, s.cw, e->h_err);
-  VN_HIP_CHECK(hipStreamSynchronize(st));
-  take_decode_error(e);
-  ingest_histos(e, nc, s.cslot, s.cmean, nullptr, s.cw);
+  if (s.acc + nc > s.cap_cent) histo_imports_drain(e);
+  hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.acc,
+                     s.cslot, s.cmean, s.cw, e->h_err);
+  s.acc += nc;
+}
+
+void histo_imports_drain(vn_engine* e) {
+  ImportScratch& s = e->imp;
+  if (!s.acc) return;
+  const uint64_t n = s.acc;
+  s.acc = 0;
+  ingest_histos(e, n, s.cslot, s.cmean, nullptr, s.cw);
 }
 
 }  // namespace vn

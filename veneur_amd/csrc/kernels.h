@@ -18,6 +18,8 @@ void take_decode_error(vn_engine* e);
 // Worker.ImportMetric for histograms / timers: Histo.Combine of GobEncode()d digests
 // (payload i = bytes[off[i], off[i+1]), device pointers)
 void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes);
+// merge the pending run of imported histogram centroids (before any read of or add to a histogram)
+void histo_imports_drain(vn_engine* e);
 // Worker.ImportMetric for sets: Set.Combine of MarshalBinary()d sketches
 void import_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes);
 
@@ -52,6 +54,8 @@ void set_replay_ranges(vn_engine* e, const uint64_t* R, const uint32_t* dev_coun
                        uint32_t grid, hipStream_t st);
 // split (hot) keys at flush: combine the ranks' partial states on the owners (split.hip)
 void split_flush(vn_engine* e);
+// first ingest call of a window: its start event (vn_timing.ms_main_ready / ms_split_ready)
+void window_open(vn_engine* e, hipStream_t st);
 void split_destroy(vn_engine* e);
 // mergeAllTemps for the given (distinct) histo slots, device list
 void histo_merge_pending(vn_engine* e, const uint32_t* dev_keys, uint32_t nkeys);

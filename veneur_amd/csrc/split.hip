@@ -105,7 +105,7 @@ vn_engine* split_engine(vn_engine* e, uint64_t records) {
   std::vector<uint32_t> h(kMaxSplitKeys);
   std::iota(h.begin(), h.end(), 0u);
   VN_HIP_CHECK(hipMemcpy(iota, h.data(), kMaxSplitKeys * 4, hipMemcpyHostToDevice));
-  if (!S.ev_done) VN_HIP_CHECK(hipEventCreateWithFlags(&S.ev_done, hipEventDisableTiming));
+  if (!S.ev_done) VN_HIP_CHECK(hipEventCreate(&S.ev_done));
   return a;
 }
 
@@ -1196,6 +1196,7 @@ void split_flush(vn_engine* e) {
     vn_engine* a = S.aux;
     hipLaunchKernelGGL(k_split_errors, dim3(1), dim3(64), 0, a->st, a->h_err, e->h_err);
     VN_HIP_CHECK(hipEventRecord(S.ev_done, a->st));
+    S.ran = true;
     VN_HIP_CHECK(hipStreamWaitEvent(e->st, S.ev_done, 0));
   }
   split_counters(e, c, e->st);
@@ -1313,6 +1314,7 @@ int vn_ingest_split(vn_engine* e, const vn_split_batch* b) {
       throw std::invalid_argument("split batch class with records but a null array");
     vn_engine* a = S.aux;  // exists: this class has split keys
     hipStream_t st = a->st;
+    window_open(e, st);
     if (!S.cap) {
       S.cap = e->cfg.split_max_records;
       VN_HIP_CHECK(hipMalloc(&S.hkey, S.cap * 4));
