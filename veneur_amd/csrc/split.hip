@@ -873,14 +873,19 @@ __device__ __forceinline__ bool epoch_rec(const EpochCtx& x, uint64_t i, uint32_
   decode_hash(code, &idx, &r);
   return true;
 }
+template <class T>
+__device__ __forceinline__ T ld_relaxed(T* p) {  // another wave's atomic may have lowered it
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 // (a) first filler of every zero register: min j with r > b
-__global__ void k_ep_firstfill(EpochCtx x, uint64_t n, uint32_t* __restrict__ ff) {
+__global__ void k_ep_firstfill(EpochCtx x, uint64_t n, uint32_t* ff) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     uint32_t k, j, idx, r, code;
     if (!epoch_rec(x, i, k, j, idx, r, code)) continue;
     const uint32_t s = x.kslot[k];
     if (x.nz[s] == 0 || r <= x.base[s]) continue;
-    if (x.arena8[(uint64_t)s * (kArenaWords * 4) + idx] == 0) atomicMin(&ff[(uint64_t)k * kHllM + idx], j);
+    uint32_t* f = &ff[(uint64_t)k * kHllM + idx];
+    if (x.arena8[(uint64_t)s * (kArenaWords * 4) + idx] == 0 && j < ld_relaxed(f)) atomicMin(f, j);
   }
 }
 // (b) T_full per key: the last first-fill of its zero registers (none missing), or p0 - 1 when full
@@ -924,7 +929,7 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
   }
   return v;
 }
-__global__ void k_ep_cand(EpochCtx x, uint64_t n, unsigned long long* __restrict__ cand) {
+__global__ void k_ep_cand(EpochCtx x, uint64_t n, unsigned long long* cand) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {  // wave-uniform trip count
     const uint64_t i = i0 + threadIdx.x;
@@ -937,9 +942,10 @@ __global__ void k_ep_cand(EpochCtx x, uint64_t n, unsigned long long* __restrict
     }
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(k);
     const bool same = k == k0;
-    if (!same && v != ~0ull) atomicMin(&cand[k], v);
+    // the minimum only falls: a candidate not below the value already there needs no atomic
+    if (!same && v != ~0ull && v < ld_relaxed(&cand[k])) atomicMin(&cand[k], v);
     const unsigned long long m = wave_min_u64(same ? v : ~0ull);
-    if ((threadIdx.x & 63) == 0 && m != ~0ull && k0 != 0xffffffffu) atomicMin(&cand[k0], m);
+    if ((threadIdx.x & 63) == 0 && m != ~0ull && k0 != 0xffffffffu && m < ld_relaxed(&cand[k0])) atomicMin(&cand[k0], m);
   }
 }
 // (d) registers after the plain max updates of every record before the candidate
