@@ -109,14 +109,21 @@ void create_impl(vn_engine* e) {
     for (uint32_t i = 0; i < ncu - ncu / 4; i++) mask[i / 32] |= 1u << (i % 32);
     e->side_cus = ncu - ncu / 4;
     if (ncu < 64 || hipExtStreamCreateWithCUMask(&e->st2, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&e->st3, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+        hipExtStreamCreateWithCUMask(&e->st3, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&e->st5, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
       (void)hipGetLastError();
-      if (e->st2) (void)hipStreamDestroy(e->st2);
-      e->st2 = nullptr;
+      for (hipStream_t* p : {&e->st2, &e->st3, &e->st5})
+        if (*p) {
+          (void)hipStreamDestroy(*p);
+          *p = nullptr;
+        }
       VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st2, hipStreamNonBlocking, prio_lo));
       VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st3, hipStreamNonBlocking, prio_hi));
+      VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st5, hipStreamNonBlocking, prio_hi));
       e->side_cus = ncu;
     }
+    VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork5, hipEventDisableTiming));
+    VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join5, hipEventDisableTiming));
   }
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
@@ -426,6 +433,16 @@ void destroy_impl(vn_engine* e) {
   if (e->ev_fork3) (void)hipEventDestroy(e->ev_fork3);
   if (e->ev_join3) (void)hipEventDestroy(e->ev_join3);
   if (e->st3) (void)hipStreamDestroy(e->st3);
+  if (e->st5) (void)hipStreamSynchronize(e->st5);
+  for (hipEvent_t* ev : {&e->ev_fork5, &e->ev_join5})
+    if (*ev) {
+      (void)hipEventDestroy(*ev);
+      *ev = nullptr;
+    }
+  if (e->st5) {
+    (void)hipStreamDestroy(e->st5);
+    e->st5 = nullptr;
+  }
   if (e->st4) (void)hipStreamSynchronize(e->st4);
   if (e->ev_join4) (void)hipEventDestroy(e->ev_join4);
   if (e->st4) (void)hipStreamDestroy(e->st4);

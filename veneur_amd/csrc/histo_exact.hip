@@ -1011,13 +1011,450 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
   }
 }
 
+// ---- four waves per key, for the longest replays (the critical path: ~780 merges back to
+// back).  The same merge, with each element of a merge on its own lane of the workgroup
+// instead of kR rounds per lane, and workgroup barriers where the single wave syncs its LDS:
+// every value below is computed exactly as in merge_sorted_fast (bit-identical results).
+constexpr int kMW = 4;
+constexpr uint32_t kMWThreads = 64 * kMW;
+constexpr uint32_t kMaxLongKeys = 4096;
+struct MwShared {  // one slot per purpose: a late wave may still read one while others move on
+  double tempW;
+  double tot[kMW];
+  uint32_t wint[kMW], mono[kMW], cnt[kMW];
+  uint32_t extra, walk_nc, walk_of, fb_nm;
+  double fb_w;
+  double red[7][kMW];
+};
+
+// requires nm + np < kMWThreads, np <= 64, capc <= kMWThreads
+__device__ void merge_mw(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np, double tempW,
+                         MwShared& S) {
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const double T = dadd(mainW, tempW);
+  const uint32_t m = nm + np;
+  // ---- merged positions: temp t after the mains strictly below it; main t after the temps <= it
+  {
+    const double tv = L.sv[t < np ? t : 0], mv = L.mm[t < nm ? t : 0];
+    uint32_t tl = 0, th = t < np ? nm : 0, ml = 0, mh = t < nm ? np : 0;
+#pragma unroll
+    for (int it = 0; it < 8; it++) {  // nm < 256, np <= 64
+      const uint32_t tmd = (tl + th) >> 1, mmd = (ml + mh) >> 1;
+      const double tval = L.mm[tmd < nm ? tmd : 0], mval = L.sv[mmd < np ? mmd : 0];
+      const bool tgo = tl < th, tlt = tval < tv, mgo = ml < mh, mle = mval <= mv;
+      tl = (tgo && tlt) ? tmd + 1 : tl;
+      th = (tgo && !tlt) ? tmd : th;
+      ml = (mgo && mle) ? mmd + 1 : ml;
+      mh = (mgo && !mle) ? mmd : mh;
+    }
+    if (t < np) {
+      L.gm[t + tl] = tv;
+      L.gw[t + tl] = L.sw[t];
+    }
+    if (t < nm) {
+      L.gm[t + ml] = mv;
+      L.gw[t + ml] = L.mw[t];
+    }
+  }
+  __syncthreads();
+  // ---- mergedWeight prefix: wave scans plus the waves' carries (integer weights: exact in any
+  // order), else wave 0 folds in Go's order; then k per element
+  const double w = t < m ? L.gw[t] : 0.0;
+  const bool wi = __all(is_int_weight(w));
+  if (lane == 0) S.wint[wv] = wi;
+  __syncthreads();
+  const bool wint = S.wint[0] && S.wint[1] && S.wint[2] && S.wint[3] && T <= 9007199254740992.0;
+  double incl;
+  if (wint) {
+    double v = w;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const double o = __shfl_up(v, d, 64);
+      v = (int)lane >= d ? dadd(v, o) : v;
+    }
+    if (lane == 63) S.tot[wv] = v;
+    __syncthreads();
+    double carry = 0.0;
+    for (uint32_t i = 0; i < wv; i++) carry = dadd(carry, S.tot[i]);
+    incl = dadd(carry, v);
+  } else {
+    if (wv == 0) {
+      double run = 0.0;
+      for (uint32_t b = 0; b < m; b += 64) {
+        const double wb = b + lane < m ? L.gw[b + lane] : 0.0;
+        const uint32_t c = min(64u, m - b);
+        double mine = 0.0;
+        for (uint32_t i = 0; i < c; i++) {
+          run = dadd(run, rl_d(wb, (int)i));
+          if (i == lane) mine = run;
+        }
+        if (b + lane < m) L.kin[b + lane] = mine;
+      }
+    }
+    __syncthreads();
+    incl = t < m ? L.kin[t] : 0.0;
+  }
+  const double kv = index_estimate(x.delta, ddiv(incl, T));
+  if (t < m) L.kin[t] = kv;
+  __syncthreads();
+  const double k0 = index_estimate(x.delta, 0.0);
+  const bool mo = __all(!(t >= 1 && t < m && kv < L.kin[t - 1]));
+  if (lane == 0) S.mono[wv] = mo;
+  __syncthreads();
+  const bool mono = S.mono[0] && S.mono[1] && S.mono[2] && S.mono[3];
+  uint32_t nc = 0;
+  bool overflow = false;
+  const uint32_t capc = x.capc;
+  if (mono) {
+    // next(s) for s = t (entries past m are m), then the power-of-two tables, then the starts
+    uint32_t cur;
+    {
+      const double base = t >= 1 ? L.kin[t - 1] : k0;
+      uint32_t bl = t < m ? t + 1 : m, bh = m;
+#pragma unroll
+      for (int it = 0; it < 8; it++) {
+        const uint32_t md = (bl + bh) >> 1;
+        const double kval = L.kin[md];
+        const bool go = bl < bh, gt = dsub(kval, base) > 1.0;
+        bh = (go && gt) ? md : bh;
+        bl = (go && !gt) ? md + 1 : bl;
+      }
+      L.jump16[t] = (uint16_t)bl;
+      cur = bl;
+    }
+    __syncthreads();
+    for (uint32_t lv = 1; lv < 8; lv++) {  // t < 256: bits 0..7
+      const uint16_t* Jp = L.jump16 + (lv - 1) * L.JW;
+      const uint32_t a = Jp[cur];
+      L.jump16[lv * L.JW + t] = (uint16_t)a;
+      cur = a;
+      __syncthreads();
+    }
+    uint32_t p = 0;
+    for (uint32_t lv = 0; lv < 8; lv++) {
+      const uint32_t nx = L.jump16[lv * L.JW + p];
+      p = ((t >> lv) & 1u) ? nx : p;
+    }
+    const bool on = p < m;
+    if (on && t < capc) L.starts[t] = p;
+    if (t == kMWThreads - 1) S.extra = (on && L.jump16[p] < m) ? 1u : 0u;  // start 256 (overflow check)
+    const uint32_t cnt = (uint32_t)__popcll(__ballot(on));
+    if (lane == 0) S.cnt[wv] = cnt;
+    __syncthreads();
+    const uint32_t raw = S.cnt[0] + S.cnt[1] + S.cnt[2] + S.cnt[3] + S.extra;
+    overflow = raw > capc;
+    nc = raw > capc ? capc : raw;
+  } else {
+    if (wv == 0) {  // the sequential walk (non-monotone k: ulp-level asin wiggle)
+      double base = k0, kprev_carry = k0;
+      uint32_t n2 = 0;
+      bool of = false;
+      for (uint32_t b = 0; b < m && !of; b += 64) {
+        const uint32_t j = b + lane;
+        const bool valid = j < m;
+        const double kj = valid ? L.kin[j] : 0.0;
+        double kp = __shfl_up(kj, 1, 64);
+        if (lane == 0) kp = kprev_carry;
+        uint32_t from = 0;
+        for (;;) {
+          const bool c = valid && lane >= from && (n2 == 0 || dsub(kj, base) > 1.0);
+          const uint64_t bal = __ballot(c);
+          if (!bal) break;
+          const uint32_t f = (uint32_t)__builtin_ctzll(bal);
+          if (n2 >= capc) {
+            of = true;
+            break;
+          }
+          if (lane == 0) L.starts[n2] = b + f;
+          n2++;
+          base = rl_d(kp, (int)f);
+          from = f + 1;
+        }
+        kprev_carry = rl_d(kj, 63);
+      }
+      if (lane == 0) {
+        S.walk_nc = n2;
+        S.walk_of = of ? 1u : 0u;
+      }
+    }
+    __syncthreads();
+    nc = S.walk_nc;
+    overflow = S.walk_of != 0;
+  }
+  if (overflow && t == 0) atomicOr(x.err, 1u);
+  if (t == 0) L.starts[nc] = m;
+  __syncthreads();
+  // ---- Welford per centroid, in element order
+  if (t < nc) {
+    const uint32_t a = L.starts[t], e = L.starts[t + 1];
+    double mean = L.gm[a], W = L.gw[a];
+    for (uint32_t j = a + 1; j < e; j++) {
+      const double wt = L.gw[j];
+      W = dadd(W, wt);
+      mean = dadd(mean, ddiv(dmul(dsub(L.gm[j], mean), wt), W));
+    }
+    L.mm[t] = mean;
+    L.mw[t] = W;
+  }
+  __syncthreads();
+  nm = nc;
+  mainW = T;
+}
+
+// a merge of any shape: the four-wave merge when it fits, else wave 0 runs the single-wave one
+__device__ void merge_mw_any(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
+                             double tempW, MwShared& S) {
+  if (nm + np < kMWThreads && np <= 64 && x.capc <= kMWThreads) {
+    merge_mw(x, L, nm, mainW, np, tempW, S);
+    return;
+  }
+  if (threadIdx.x < 64) {
+    merge_any(x, L, nm, mainW, np, tempW);
+    if (threadIdx.x == 0) {
+      S.fb_nm = nm;
+      S.fb_w = mainW;
+    }
+  }
+  __syncthreads();
+  nm = S.fb_nm;
+  mainW = S.fb_w;
+}
+
+// replay_key with four waves (tcap <= 64, ingest only: no flush-mode adoption)
+__device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwShared& S) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t capc = x.capc, tcap = x.tcap;
+  const uint32_t TP = round64(tcap + 1);
+  Lds L;
+  L.JW = max(capc + TP + 1, 320u);
+  L.levels = 1;
+  while ((1u << L.levels) <= capc) L.levels++;
+  L.mm = reinterpret_cast<double*>(smem);
+  L.mw = L.mm + capc;
+  L.tv = L.mw + capc;
+  L.tw = L.tv + TP;
+  L.sv = L.tw + TP;
+  L.sw = L.sv + TP;
+  L.gm = L.sw + TP;
+  L.gw = L.gm + L.JW;
+  L.kin = L.gw + L.JW;
+  L.starts = reinterpret_cast<uint32_t*>(L.kin + L.JW);
+  L.jump = L.starts + L.JW;
+  L.jump16 = reinterpret_cast<uint16_t*>(L.jump);
+
+  const MergeParams mp{x.delta, x.capc, x.err};
+  const uint64_t* const xA = x.A;
+  const uint64_t* const xB = x.B;
+  const double* const xcsv = x.csv;
+  const double* const xcsw = x.csw;
+  const double* const xctw = x.ctw;
+  const double* const ximpw = x.impw;
+  const uint32_t s = x.keys[k];
+  const uint32_t nex = x.nex ? x.nex[k] : 0u;
+  const bool final_merge = x.hot && x.hot[k];
+  uint32_t np = x.hpend[s];
+  if (nex == 0 && !(final_merge && np > 0)) return;
+
+  const uint8_t cur = x.hcur[s];
+  double* cmg = (cur ? x.cm1 : x.cm0) + (uint64_t)s * capc;
+  double* cwg = (cur ? x.cw1 : x.cw0) + (uint64_t)s * capc;
+  uint32_t nm = x.hncent[s];
+  double* h = x.hst + (uint64_t)s * VN_HISTO_STATS;
+  double mainW = h[7];
+  const uint32_t lo = x.start[s];
+  const ExactSplit sp = exact_split(np, nex, tcap);
+  for (uint32_t j = t; j < nm; j += kMWThreads) {
+    L.mm[j] = cmg[j];
+    L.mw[j] = cwg[j];
+  }
+  const double* pv = x.hpv + (uint64_t)s * tcap;
+  const double* pw = x.hpw + (uint64_t)s * tcap;
+  for (uint32_t j = t; j < np; j += kMWThreads) {
+    L.tv[j] = pv[j];
+    L.tw[j] = pw[j];
+  }
+  __syncthreads();
+
+  double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf, dmn = kInf, dmx = -kInf;
+  auto stat = [&](double v, double wt, bool sample) {
+    dmn = min_go(dmn, v);
+    dmx = max_go(dmx, v);
+    if (!sample) return;
+    sw = dadd(sw, wt);
+    mn = min_go(mn, v);
+    mx = max_go(mx, v);
+    sxw = dadd(sxw, dmul(v, wt));
+    srw = dadd(srw, dmul(ddiv(1.0, v), wt));
+  };
+  auto append = [&](uint32_t a, uint32_t b) {
+    for (uint32_t i = a + t; i < b; i += kMWThreads) {
+      const double v = bitsd(xA[lo + i]);
+      const uint32_t tag = (uint32_t)xB[lo + i];
+      const double wt = tag_weight(tag, ximpw);
+      L.tv[np + (i - a)] = v;
+      L.tw[np + (i - a)] = wt;
+      stat(v, wt, tag_is_sample(tag));
+    }
+    np += b - a;
+    __syncthreads();
+  };
+  auto merge_pend = [&]() {  // sort the pending temps (wave 0), then merge them
+    if (wv == 0) {
+      const double tw_ = temp_weight(L.tw, np);
+      sort_temps(L.tv, L.tw, L.sv, L.sw, np);
+      if (lane == 0) S.tempW = tw_;
+    }
+    __syncthreads();
+    const double tempW = S.tempW;
+    __syncthreads();
+    merge_mw_any(mp, L, nm, mainW, np, tempW, S);
+  };
+
+  if (nex && np == tcap) {
+    merge_pend();
+    np = 0;
+  }
+  if (sp.off0) {
+    append(0, sp.off0);
+    if (np == tcap && sp.off0 < nex) {
+      merge_pend();
+      np = 0;
+    }
+  }
+  if (sp.npure) {
+    double cv = 0.0, cw = 0.0, ctw = 0.0;
+    auto load = [&](uint32_t c) {
+      const uint64_t base = (uint64_t)lo + sp.off0 + (uint64_t)c * tcap;
+      if (t < tcap) {
+        cv = xcsv[base + t];
+        cw = xcsw[base + t];
+      }
+      ctw = xctw[base];
+    };
+    load(0);
+    for (uint32_t c = 0; c < sp.npure; c++) {
+      if (t < tcap) {
+        L.sv[t] = cv;
+        L.sw[t] = __builtin_fabs(cw);
+        stat(cv, __builtin_fabs(cw), cw > 0.0);
+      }
+      const double tempW = ctw;
+      if (c + 1 < sp.npure) load(c + 1);
+      __syncthreads();
+      merge_mw_any(mp, L, nm, mainW, tcap, tempW, S);
+    }
+  }
+  const uint32_t tail = sp.off0 + sp.npure * tcap;
+  if (nex > tail) append(tail, nex);
+  if (final_merge && np > 0) {
+    merge_pend();
+    np = 0;
+  }
+  for (uint32_t j = t; j < nm; j += kMWThreads) {
+    cmg[j] = L.mm[j];
+    cwg[j] = L.mw[j];
+  }
+  double* qv = x.hpv + (uint64_t)s * tcap;
+  double* qw = x.hpw + (uint64_t)s * tcap;
+  for (uint32_t j = t; j < np; j += kMWThreads) {
+    qv[j] = L.tv[j];
+    qw[j] = L.tw[j];
+  }
+  // the statistics: each thread's partials folded over the wave, then the waves in order
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    sw = dadd(sw, __shfl_xor(sw, d, 64));
+    sxw = dadd(sxw, __shfl_xor(sxw, d, 64));
+    srw = dadd(srw, __shfl_xor(srw, d, 64));
+    mn = min_go(mn, __shfl_xor(mn, d, 64));
+    mx = max_go(mx, __shfl_xor(mx, d, 64));
+    dmn = min_go(dmn, __shfl_xor(dmn, d, 64));
+    dmx = max_go(dmx, __shfl_xor(dmx, d, 64));
+  }
+  if (lane == 0) {
+    S.red[0][wv] = sw;
+    S.red[1][wv] = sxw;
+    S.red[2][wv] = srw;
+    S.red[3][wv] = mn;
+    S.red[4][wv] = mx;
+    S.red[5][wv] = dmn;
+    S.red[6][wv] = dmx;
+  }
+  __syncthreads();
+  if (t == 0) {
+    for (int q = 1; q < kMW; q++) {
+      sw = dadd(sw, S.red[0][q]);
+      sxw = dadd(sxw, S.red[1][q]);
+      srw = dadd(srw, S.red[2][q]);
+      mn = min_go(mn, S.red[3][q]);
+      mx = max_go(mx, S.red[4][q]);
+      dmn = min_go(dmn, S.red[5][q]);
+      dmx = max_go(dmx, S.red[6][q]);
+    }
+    x.hncent[s] = nm;
+    x.hpend[s] = np;
+    h[7] = mainW;
+    if (nex) {
+      h[0] = dadd(h[0], sw);
+      h[1] = min_go(h[1], mn);
+      h[2] = max_go(h[2], mx);
+      h[3] = dadd(h[3], sxw);
+      h[4] = dadd(h[4], srw);
+      h[5] = min_go(h[5], dmn);
+      h[6] = max_go(h[6], dmx);
+    }
+  }
+  __syncthreads();
+  if (x.hspn) {
+    uint32_t fn = 0;
+    if (x.spec && !final_merge && np > 0) {
+      merge_pend();
+      double* fmg = (cur ? x.cm0 : x.cm1) + (uint64_t)s * capc;
+      double* fwg = (cur ? x.cw0 : x.cw1) + (uint64_t)s * capc;
+      for (uint32_t j = t; j < nm; j += kMWThreads) {
+        fmg[j] = L.mm[j];
+        fwg[j] = L.mw[j];
+      }
+      fn = nm;
+    }
+    if (t == 0) {
+      x.hspn[s] = fn;
+      if (fn) x.hspw[s] = mainW;
+    }
+  }
+}
+
 // One wave per key: key index blockIdx.x, or the blockIdx.x-th of x.order / x.order64 (the
 // latter longest first, so the longest replays do not start last).
 template <int TPL>
 __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   const uint32_t i = blockIdx.x;
+  if (x.mw_count && i < *x.mw_count) return;  // replayed by k_histo_exact_mw
   const uint32_t k = x.order64 ? (uint32_t)x.order64[i] : x.order ? x.order[i] : i;
   if (k < x.nkeys) replay_key<TPL>(x, k);
+}
+
+// the longest keys of the order (its first *nmw entries), four waves each
+__global__ __launch_bounds__(kMWThreads) void k_histo_exact_mw(ExactCtx x, const uint32_t* __restrict__ nmw) {
+  __shared__ MwShared S;
+  const uint32_t n = *nmw;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t k = x.order64 ? (uint32_t)x.order64[i] : x.order ? x.order[i] : i;
+    if (k < x.nkeys) replay_key_mw(x, k, S);
+    __syncthreads();  // the next key reuses the LDS
+  }
+}
+// how many entries of the longest-first order replay at least min_len samples
+__global__ void k_exact_count_long(uint32_t n, const uint64_t* __restrict__ order64, uint32_t min_len,
+                                   uint32_t cap, uint32_t* __restrict__ out) {
+  uint32_t lo = 0, hi = n;  // first entry shorter than min_len
+  while (lo < hi) {
+    const uint32_t md = (lo + hi) >> 1;
+    if (0xFFFFFu - (uint32_t)(order64[md] >> 32) >= min_len) lo = md + 1;
+    else hi = md;
+  }
+  *out = min(lo, cap);
 }
 
 // keys [0, *cnt) of x.keys, grid-stride: a bounded grid when only the device knows the count
@@ -1083,6 +1520,21 @@ void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uin
   if (max_chunks)
     hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)max_chunks), dim3(64),
                        sizeof(double) * 4 * ((x.tcap + 1 + 63u) & ~63u), st, x);
+}
+
+bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipStream_t st) {
+  x.mw_count = nullptr;
+  if (!x.order64 || !x.norder || x.tcap > 64 || x.capc > kMWThreads || x.flush_mode) return false;
+  hipLaunchKernelGGL(k_exact_count_long, dim3(1), dim3(1), 0, st, x.norder, x.order64, min_len,
+                     std::min<uint32_t>(x.norder, kMaxLongKeys), count);
+  x.mw_count = count;
+  return true;
+}
+
+void histo_exact_replay_long(const ExactCtx& x, hipStream_t st) {
+  if (!x.mw_count) return;
+  hipLaunchKernelGGL(k_histo_exact_mw, dim3(std::min<uint32_t>(x.norder, kMaxLongKeys / 2)), dim3(kMWThreads),
+                     exact_smem_bytes(x.capc, x.tcap), st, x, x.mw_count);
 }
 
 void histo_exact_replay(const ExactCtx& x, hipStream_t st) {

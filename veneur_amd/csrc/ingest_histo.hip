@@ -1196,9 +1196,28 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
     if (a && b) VN_HIP_CHECK(hipEventRecord(b, s));
     if (e->timing) e->kstat_rp.launches++;
   };
+  // the longest keys (a quarter of the threshold and more) replay with four waves each on st5,
+  // beside the one-wave replay of the rest on the same CUs
   auto replay_cold = [&](hipStream_t s, RadixScratch& rs) {
     histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
-    clocked_replay(s);
+    const bool longk = histo_exact_count_long(xc, std::max<uint32_t>(e->exact_threshold / 4, 1024u),
+                                              e->h_cnt + 15, s);
+    const bool side5 = longk && !e->timing && e->st5;
+    hipEvent_t a = e->timing ? e->pool_rp.next() : nullptr, b = e->timing ? e->pool_rp.next() : nullptr;
+    if (a && b) VN_HIP_CHECK(hipEventRecord(a, s));
+    if (side5) {
+      VN_HIP_CHECK(hipEventRecord(e->ev_fork5, s));
+      VN_HIP_CHECK(hipStreamWaitEvent(e->st5, e->ev_fork5, 0));
+      histo_exact_replay_long(xc, e->st5);
+      VN_HIP_CHECK(hipEventRecord(e->ev_join5, e->st5));
+    } else if (longk) {
+      histo_exact_replay_long(xc, s);
+    }
+    histo_exact_replay(xc, s);
+    if (side5) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join5, 0));
+    if (a && b) VN_HIP_CHECK(hipEventRecord(b, s));
+    if (e->timing) e->kstat_rp.launches++;
+    xc.mw_count = nullptr;
   };
   if (e->timing) {
     // 16 B per replayed sample, 40 B of local statistics and 16 B per centroid
