@@ -89,6 +89,112 @@ def rank_error_stats(d, slots, eng_q, ref_q):
     return errs
 
 
+def c5_leg(args, rank):
+    """C5 (BASELINE configs[4]): a global veneur merging every host's forwarded digests and
+    sketches -- ImportMetric -> Histo.Combine / Set.Combine (worker.go:230-268) for each of
+    `hosts` hosts x (histo_keys GobEncode()d digests + set_keys MarshalBinary()d sketches);
+    every key arrives from every host.  The hosts are `distinct` local windows of ~100 timer
+    samples per key (and Pareto-sized sets), ingested and exported by a local engine (device
+    gob / marshal encoders), then cycled host after host; payloads resident in HBM, imported
+    with vn_import_*_device and flushed.  Parity on sampled keys against the restated Go
+    (oracle Worker.ImportMetric in the same order): digest weight/min/max exact, set
+    estimates exact, quantiles by rank error over the imported centroids."""
+    import oracle
+    import veneur_amd as V
+    import veneur_amd._abi as A
+    rng = np.random.default_rng(args.seed + 5)
+    H, S, D, hosts = args.c5_histo_keys, args.c5_set_keys, args.c5_distinct, args.c5_hosts
+    t0 = time.time()
+    hp, sp = [], []
+    with V.Engine((1, 1, H, S), percentiles=PCT, max_batch_records=1 << 23, max_batch_member_bytes=1 << 20) as loc:
+        for d in range(D):
+            cnt = rng.integers(50, 151, H)
+            hs = np.repeat(np.arange(H, dtype=np.uint32), cnt)
+            rng.shuffle(hs)
+            hv = np.exp(rng.normal(3.9 + 0.05 * d, 1.0, len(hs)))
+            hr = np.where(rng.random(len(hs)) < 0.1, np.float32(0.5), np.float32(1.0)).astype(np.float32)
+            sc = np.minimum((rng.pareto(1.2, S) * 50 + 1).astype(np.int64), 20000)
+            ss = np.repeat(np.arange(S, dtype=np.uint32), sc)
+            sh = rng.integers(0, 2 ** 63, len(ss), dtype=np.uint64) * np.uint64(2) + \
+                rng.integers(0, 2, len(ss), dtype=np.uint64)
+            loc.ingest(histos=(hs, hv, hr), set_hashes=(ss, sh))
+            hp.append(loc.export_raw(2, np.arange(H)))
+            sp.append(loc.export_raw(3, np.arange(S)))
+            loc.flush_raw()
+    dev = []  # per distinct host: device (off, bytes) for histos and sets
+    keep = []
+    for (ho, hb), (so, sb) in zip(hp, sp):
+        bufs = [V.DeviceBuffer(ho), V.DeviceBuffer(hb), V.DeviceBuffer(so), V.DeviceBuffer(sb)]
+        keep += bufs
+        dev.append([b.ptr.value for b in bufs])
+    hslot = V.DeviceBuffer(np.arange(H, dtype=np.uint32))
+    sslot = V.DeviceBuffer(np.arange(S, dtype=np.uint32))
+    keep += [hslot, sslot]
+    gen_s = time.time() - t0
+    payload_bytes = sum(int(h[0][-1]) + int(s_[0][-1]) for h, s_ in zip(hp, sp)) / D * hosts
+    with V.Engine((1, 1, H, S), percentiles=PCT, max_batch_records=1 << 25) as g:
+        def window():
+            for h in range(hosts):
+                ho, hb, so, sb = dev[h % D]
+                g.import_device(2, hslot.ptr.value, ho, hb, H)
+                g.import_device(3, sslot.ptr.value, so, sb, S)
+            return g.flush_raw()
+        window()
+        A.lib.vn_device_synchronize(0)
+        tw = time.perf_counter()
+        for _ in range(args.c5_windows):
+            f = window()
+        A.lib.vn_device_synchronize(0)
+        ms = (time.perf_counter() - tw) * 1e3 / args.c5_windows
+        hq = np.ctypeslib.as_array(f.histo_quantiles, shape=(f.n_histo * len(PCT),)).reshape(-1, len(PCT)).copy()
+        hst = np.ctypeslib.as_array(f.histo_stats, shape=(f.n_histo * 8,)).reshape(-1, 8).copy()
+        hsl = np.ctypeslib.as_array(f.histo_slot, shape=(f.n_histo,)).copy()
+        ses = np.ctypeslib.as_array(f.set_estimate, shape=(f.n_set,)).copy()
+        ssl = np.ctypeslib.as_array(f.set_slot, shape=(f.n_set,)).copy()
+    # parity on sampled keys: the restated Go import of the same payload sequence
+    kh = np.sort(rng.choice(H, min(H, args.c5_parity_keys), replace=False))
+    ks = np.sort(rng.choice(S, min(S, args.c5_parity_keys), replace=False))
+    w = oracle.Worker(1, 1, len(kh), len(ks))
+    cents = [[] for _ in kh]
+    for h in range(hosts):
+        (ho, hb), (so, sb) = hp[h % D], sp[h % D]
+        for i, k in enumerate(kh):
+            pl = hb[ho[k]:ho[k + 1]].tobytes()
+            w.import_histo(i, pl)
+            if h < D:
+                t = oracle.MergingDigest(100.0)
+                t.gob_decode(pl)
+                cents[i].append(t.centroids())
+        for i, k in enumerate(ks):
+            w.import_set(i, sb[so[k]:so[k + 1]].tobytes())
+    pos = {int(s_): j for j, s_ in enumerate(hsl)}
+    st_exact, rank_err = True, 0.0
+    for i, k in enumerate(kh):
+        j = pos[int(k)]
+        ost = np.array(w.histo_stats(i))
+        st_exact &= bool(np.array_equal(hst[j, [5, 6, 7]], ost[[5, 6, 7]]))
+        m = np.concatenate([cents[i][h % D][0] for h in range(hosts)])
+        wt = np.concatenate([cents[i][h % D][1] for h in range(hosts)])
+        o = np.argsort(m, kind="stable")
+        sv, cw = m[o], np.cumsum(wt[o])
+        F = lambda q: cw[np.searchsorted(sv, q, side="right") - 1] / cw[-1] if np.searchsorted(sv, q, side="right") \
+            else 0.0
+        for a, p in zip(hq[j], PCT):
+            rank_err = max(rank_err, abs(F(a) - F(w.histo_quantile(i, p))))
+    spos = {int(s_): j for j, s_ in enumerate(ssl)}
+    set_exact = all(int(ses[spos[int(k)]]) == w.set_estimate(i) for i, k in enumerate(ks))
+    n_imp = hosts * (H + S)
+    return {"config": "C5 global import: %d hosts x (%d histo digests + %d set sketches), every key from every host, "
+                      "%d distinct host windows cycled; payloads in HBM (vn_import_*_device), then vn_flush" % (
+                          hosts, H, S, D),
+            "imports_per_s": n_imp / (ms * 1e-3), "payload_GBs": payload_bytes / (ms * 1e-3) / 1e9,
+            "ms_per_window": ms, "windows": args.c5_windows, "payloads_per_window": n_imp,
+            "payload_bytes_per_window": payload_bytes, "generated_in_s": round(gen_s, 2),
+            "parity": {"keys_checked": {"histo": int(len(kh)), "set": int(len(ks))},
+                       "histo_weight_min_max_exact": st_exact, "histo_rank_error_max": rank_err,
+                       "set_estimates_exact": bool(set_exact)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -113,6 +219,12 @@ def main():
                     help="development only: run rank --sim-rank's share of an N-GPU split on this one GPU "
                          "(no exchange partners; not a bench result)")
     ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--c5-hosts", type=int, default=1000, help="C5 leg (rank 0, N=1): hosts per window (0: off)")
+    ap.add_argument("--c5-histo-keys", type=int, default=10000)
+    ap.add_argument("--c5-set-keys", type=int, default=2000)
+    ap.add_argument("--c5-distinct", type=int, default=8, help="distinct host windows, cycled")
+    ap.add_argument("--c5-windows", type=int, default=1)
+    ap.add_argument("--c5-parity-keys", type=int, default=16)
     ap.add_argument("--host-trace", action="store_true",
                     help="development only: report host ms in split_keys+ingest_split / ingest / flush")
     ap.add_argument("--pcie-steps", type=int, default=1,
@@ -168,6 +280,7 @@ def main():
         # combine at flush does not wait behind this engine's ingest
         if sum(stream.split_counts):
             eng.ingest_split_device(stream.split)
+            eng.split_close()  # their combine runs beside this engine's ingest
         if t:
             t.append(time.perf_counter())
         eng.ingest_device(stream.batch)
@@ -178,7 +291,8 @@ def main():
             t.append(time.perf_counter())
             tm = eng.timing()
             host_marks.append(np.concatenate([np.diff(t) * 1e3, [tm["ms_split_host"], tm["ms_main_ready"],
-                                                                 tm["ms_split_ready"]]]))
+                                                                 tm["ms_split_ready"], tm["ms_split_histo_ready"],
+                                                                 tm["ms_split_set_prefix_ready"]]]))
         return r
 
     def sync():
@@ -199,7 +313,7 @@ def main():
     elapsed = ctrl.max(elapsed)
     rank_ms = ctrl.gather_object(t_rank * 1e3 / args.steps)
     if host_marks:
-        log(rank, "[bench] host ms per call (split+ingest_split, ingest, flush; split combine in flush); device ms to main / split ready: %s" %
+        log(rank, "[bench] host ms per call (split+ingest_split, ingest, flush; split combine in flush); device ms to main / split ready / split histos / set prefix: %s" %
             np.round(np.mean(host_marks[args.warmup:] or host_marks, axis=0), 3).tolist())
     rank_records = ctrl.gather_object(stream.n_records)
     ms_per_step = elapsed * 1e3 / args.steps
@@ -340,6 +454,10 @@ def main():
                                   "sample": "the full C4 flush window above (%d samples); C restatement of the Go "
                                             "Worker.ProcessMetric + flush path, %d worker threads routed by key"
                                             % (args.samples, threads)}
+        if args.c5_hosts > 0:
+            t1 = time.time()
+            result["c5"] = c5_leg(args, rank)
+            log(rank, "[bench] C5 leg in %.1fs: %s" % (time.time() - t1, json.dumps(result["c5"])))
         o = last
         npct = len(PCT)
         arr = lambda p, n, dt: np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, dt)

@@ -288,6 +288,9 @@ typedef struct {
    * of it queued before vn_flush), and the split combine done (0 without split keys) */
   float ms_main_ready;
   float ms_split_ready;
+  /* inside the split combine: histograms done, sets' gathered prefix replayed */
+  float ms_split_histo_ready;
+  float ms_split_set_prefix_ready;
 } vn_timing;
 int vn_timing_enable(vn_engine* eng, int enable);
 int vn_get_timing(vn_engine* eng, vn_timing* out);
@@ -350,6 +353,12 @@ typedef struct {
   const uint64_t* set_hash;
 } vn_split_batch;
 int vn_ingest_split(vn_engine* eng, const vn_split_batch* device_batch);
+/* No more split records this window: the split histos / sets start combining now, in a host
+ * thread of the engine's own (their collectives are issued there), while the caller goes on
+ * with vn_ingest; vn_flush / vn_split_combine join it.  Until then vn_split_keys and
+ * vn_ingest_split fail, and the group must not change.  Optional: without it the combine runs
+ * inside vn_flush. */
+int vn_split_close(vn_engine* eng);
 /* Combine the split keys now (collective over the group; vn_flush does it when they are still
  * pending): afterwards the owners hold each split key's state in its slot, the other ranks
  * have cleared theirs, and the split lists are empty. */

@@ -137,3 +137,17 @@ def test_c5_global_import_1000_hosts(exact_threshold):
               "h_rate": np.concatenate([(1.0 / wt).astype(np.float32) for s in range(nh) for _, wt in cents[s]])}
     err = rank_errors(stream, f.histo_slot, f.histo_quantiles, oq)
     assert err.max() <= 1e-3, err.max()
+
+
+def test_c5_bench_leg_small():
+    """bench.py's C5 leg (hosts' payloads exported by a local engine, imported from HBM by a
+    global engine) at a small scale: parity on every key."""
+    from argparse import Namespace
+    import bench
+    r = bench.c5_leg(Namespace(seed=3, c5_histo_keys=300, c5_set_keys=60, c5_distinct=3, c5_hosts=40, c5_windows=1,
+                               c5_parity_keys=300), 0)
+    p = r["parity"]
+    assert p["keys_checked"] == {"histo": 300, "set": 60}
+    assert p["histo_weight_min_max_exact"] and p["set_estimates_exact"]
+    assert p["histo_rank_error_max"] <= 1e-3, p
+    assert r["payloads_per_window"] == 40 * 360 and r["imports_per_s"] > 0

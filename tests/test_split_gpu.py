@@ -37,7 +37,7 @@ def deal(keys, N):
     return j % N, j
 
 
-def run_group(N, build, cap=(8, 8, 8, 8), split_max=1 << 22, **kw):
+def run_group(N, build, cap=(8, 8, 8, 8), split_max=1 << 22, close=False, **kw):
     """N engines in one in-process group; build(rank, engine) feeds a rank; flush in N threads."""
     comms = Comm.local(N)
     engines = [V.Engine(cap, percentiles=PCT, max_batch_records=1 << 20, split_max_records=split_max, **kw)
@@ -47,6 +47,9 @@ def run_group(N, build, cap=(8, 8, 8, 8), split_max=1 << 22, **kw):
         for r, e in enumerate(engines):
             e.set_comm(comms[r])
             build(r, e)
+        if close:  # every rank's combine starts in the engine's own thread (vn_split_close)
+            for e in engines:
+                e.split_close()
 
         def combine(r):
             try:
@@ -250,3 +253,35 @@ def test_rccl_group_of_one():
         assert f.set_slot.tolist() == [3] and f.set_estimate.tolist() == [3]
     finally:
         c.close()
+
+
+@pytest.mark.parametrize("N", [1, 3])
+def test_split_close_runs_combine_in_engine_thread(N):
+    """vn_split_close: the split combine starts in the engine's own host thread; the result is the
+    one vn_flush computes inline (sets bit-identical, histos within the rank bound)."""
+    keys, vals, rates, nk = _histo_stream(4)
+    owners = (np.arange(nk) % N).astype(np.uint32)
+    rank, _ = deal(keys, N)
+    rng = np.random.default_rng(8)
+    skeys = rng.integers(0, 2, 300000).astype(np.uint32)
+    shash = rng.integers(0, 2**63, 300000, dtype=np.uint64) * np.uint64(2)
+    srank, _ = deal(skeys, N)
+    sowners = np.array([0, (N - 1)], np.uint32)
+
+    def build(r, e):
+        e.split_keys(2, np.arange(nk, dtype=np.uint32), owners)
+        e.split_keys(3, np.arange(2, dtype=np.uint32), sowners)
+        m = np.nonzero(rank == r)[0]
+        e.ingest_split(histos=(keys[m], vals[m], rates[m]))
+        ms = np.nonzero(srank == r)[0]
+        e.ingest_split(set_hashes=(skeys[ms], shash[ms]))
+
+    outs = [run_group(N, build, cap=(1, 1, 8, 4), close=c)[0] for c in (False, True)]
+    for o in range(N):
+        a, b = outs[0][o], outs[1][o]
+        assert a.set_slot.tolist() == b.set_slot.tolist()
+        assert a.set_estimate.tolist() == b.set_estimate.tolist()
+        assert a.histo_slot.tolist() == b.histo_slot.tolist()
+        np.testing.assert_array_equal(a.histo_stats[:, [0, 1, 2, 5, 6, 7]], b.histo_stats[:, [0, 1, 2, 5, 6, 7]])
+        # (the micro-centroid sums of large shares are order-free float atomics: close, not identical)
+        np.testing.assert_allclose(a.histo_quantiles, b.histo_quantiles, rtol=1e-2)

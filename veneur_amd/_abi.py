@@ -117,7 +117,8 @@ class Timing(C.Structure):
                 ("histo_replay_launches", C.c_uint64), ("histo_replay_bytes", C.c_uint64),
                 ("ms_set_segments", C.c_float), ("set_segment_launches", C.c_uint64),
                 ("set_segment_bytes", C.c_uint64), ("ms_flush_host", C.c_float), ("ms_split_host", C.c_float),
-                ("ms_main_ready", C.c_float), ("ms_split_ready", C.c_float)]
+                ("ms_main_ready", C.c_float), ("ms_split_ready", C.c_float),
+                ("ms_split_histo_ready", C.c_float), ("ms_split_set_prefix_ready", C.c_float)]
 
 
 class SynthConfig(C.Structure):
@@ -205,6 +206,7 @@ _sig("vn_comm_allreduce", C.c_int, vp, vp, vp, C.c_uint64, C.c_int, C.c_int)
 _sig("vn_engine_set_comm", C.c_int, vp, vp)
 _sig("vn_split_keys", C.c_int, vp, C.c_int, u32p, u32p, C.c_uint32)
 _sig("vn_ingest_split", C.c_int, vp, C.POINTER(SplitBatch))
+_sig("vn_split_close", C.c_int, vp)
 _sig("vn_split_combine", C.c_int, vp)
 _sig("vn_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(vp))
 _sig("vn_device_free", C.c_int, vp)
@@ -229,5 +231,5 @@ EXPORTED = [
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
     "vn_synth_device", "vn_synth_device_free", "vn_synth_key_counts",
     "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",
-    "vn_comm_nranks", "vn_comm_allreduce", "vn_engine_set_comm", "vn_split_keys", "vn_ingest_split", "vn_split_combine",
+    "vn_comm_nranks", "vn_comm_allreduce", "vn_engine_set_comm", "vn_split_keys", "vn_ingest_split", "vn_split_close", "vn_split_combine",
 ]

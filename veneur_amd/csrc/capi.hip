@@ -969,9 +969,14 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
     e->last.ms_flush_host = std::chrono::duration<float, std::milli>(h2 - h0).count();
     e->last.ms_split_host = std::chrono::duration<float, std::milli>(h1 - h0).count();
     e->last.ms_main_ready = e->last.ms_split_ready = 0.0f;
+    e->last.ms_split_histo_ready = e->last.ms_split_set_prefix_ready = 0.0f;
     if (e->w_open) {  // (flush_all synchronised both streams)
       VN_HIP_CHECK(hipEventElapsedTime(&e->last.ms_main_ready, e->ev_w0, e->ev_wmain));
-      if (e->sp.ran) VN_HIP_CHECK(hipEventElapsedTime(&e->last.ms_split_ready, e->ev_w0, e->sp.ev_done));
+      if (e->sp.ran) {
+        VN_HIP_CHECK(hipEventElapsedTime(&e->last.ms_split_ready, e->ev_w0, e->sp.ev_done));
+        VN_HIP_CHECK(hipEventElapsedTime(&e->last.ms_split_histo_ready, e->ev_w0, e->sp.ev_histo));
+        VN_HIP_CHECK(hipEventElapsedTime(&e->last.ms_split_set_prefix_ready, e->ev_w0, e->sp.ev_set_prefix));
+      }
       e->w_open = false;
     }
     e->sp.ran = false;

@@ -9,7 +9,9 @@
 //   sets      header SoA (mode, b, nz, list count/bytes/last, tmp count), tmpSet codes [slot][164],
 //             arena [slot][16640 u32]: the sorted unique sparse codes, or 16384 one-byte registers
 #pragma once
+#include <exception>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/veneur_amd.h"
@@ -72,7 +74,13 @@ struct SplitState {
   uint32_t* s_scratch_bt = nullptr; // set ingest: touched flags of the metro64 pass (unused slots)
   vn_engine* aux = nullptr;         // the split engine (split.hip): split histos / sets combine there
   hipEvent_t ev_done = nullptr;     // its combine done (this engine's stream waits on it)
+  hipEvent_t ev_histo = nullptr, ev_set_prefix = nullptr;  // milestones inside it (vn_timing)
   bool ran = false;                 // ev_done recorded by this window's flush
+  // vn_split_close: the split engine's combine runs in this host thread while the caller goes
+  // on ingesting; vn_flush joins it
+  std::thread worker;
+  bool closed = false;
+  std::exception_ptr worker_err;
   std::vector<void*> scratch;       // flush scratch (freed at destroy)
   std::vector<size_t> scratch_cap;
 };

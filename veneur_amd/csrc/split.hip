@@ -26,6 +26,9 @@
 //             split_compression, tools/split_study.py: within the single-GPU scheme's rank error)
 //             -- moved rank -> owner by grouped ncclSend / ncclRecv.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <new>
 #include <numeric>
 
 #include "histo.h"
@@ -106,6 +109,8 @@ vn_engine* split_engine(vn_engine* e, uint64_t records) {
   std::iota(h.begin(), h.end(), 0u);
   VN_HIP_CHECK(hipMemcpy(iota, h.data(), kMaxSplitKeys * 4, hipMemcpyHostToDevice));
   if (!S.ev_done) VN_HIP_CHECK(hipEventCreate(&S.ev_done));
+  if (!S.ev_histo) VN_HIP_CHECK(hipEventCreate(&S.ev_histo));
+  if (!S.ev_set_prefix) VN_HIP_CHECK(hipEventCreate(&S.ev_set_prefix));
   return a;
 }
 
@@ -116,11 +121,22 @@ int bits_for_n(uint64_t n) {
 }
 
 template <class T>
-void to_host(T* h, const T* d, size_t n, hipStream_t st) {
+void to_host_at(int line, T* h, const T* d, size_t n, hipStream_t st) {
   if (!n) return;
   VN_HIP_CHECK(hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, st));
+#ifdef VN_SPLIT_TRACE  // diagnostics build (make prof): host clock around every wait of the combine
+  const auto a = std::chrono::steady_clock::now();
   VN_HIP_CHECK(hipStreamSynchronize(st));
+  const auto b = std::chrono::steady_clock::now();
+  fprintf(stderr, "split-trace line %d t %.1f wait %.1f\n", line,
+          std::chrono::duration<double, std::micro>(b.time_since_epoch()).count(),
+          std::chrono::duration<double, std::micro>(b - a).count());
+#else
+  (void)line;
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+#endif
 }
+#define to_host(...) to_host_at(__LINE__, __VA_ARGS__)
 template <class T>
 void to_dev(T* d, const T* h, size_t n, hipStream_t st) {
   if (!n) return;
@@ -1134,6 +1150,7 @@ void split_sets(vn_engine* e, vn_comm* c) {
     J = std::min<uint64_t>(J * 4, maxtot);
   }
 
+  VN_HIP_CHECK(hipEventRecord(e->sp.ev_set_prefix, st));
   // 3. the records after J: dense inserts in rebase epochs, all-reduced
   uint32_t* p0 = sbuf<uint32_t>(e, kSP0, H);
   uint32_t* done = sbuf<uint32_t>(e, kSDone, H);
@@ -1187,24 +1204,49 @@ void split_sets(vn_engine* e, vn_comm* c) {
 
 }  // namespace
 
+// the split engine's part of the combine: histograms, then sets, then the error flags; ev_done
+// marks its end on the split engine's stream (a host thread of its own after vn_split_close)
+void split_combine_aux(vn_engine* e, vn_comm* c) {
+  SplitState& S = e->sp;
+  split_histos(e, c);
+  VN_HIP_CHECK(hipEventRecord(S.ev_histo, S.aux->st));
+  VN_HIP_CHECK(hipEventRecord(S.ev_set_prefix, S.aux->st));  // (again after the set prefix, if any)
+  split_sets(e, c);
+  vn_engine* a = S.aux;
+  hipLaunchKernelGGL(k_split_errors, dim3(1), dim3(64), 0, a->st, a->h_err, e->h_err);
+  VN_HIP_CHECK(hipEventRecord(S.ev_done, a->st));
+}
+
+void split_join(vn_engine* e) {
+  SplitState& S = e->sp;
+  if (S.worker.joinable()) S.worker.join();
+  std::exception_ptr err = S.worker_err;
+  S.worker_err = nullptr;
+  if (err) std::rethrow_exception(err);
+}
+
 void split_flush(vn_engine* e) {
   SplitState& S = e->sp;
   if (S.slot[VN_COUNTER].empty() && S.slot[VN_HISTO].empty() && S.slot[VN_SET].empty()) {
     S.nh = S.ns = 0;
+    S.closed = false;
     return;
   }
   vn_comm* c = group_of(e);
   if (S.aux) {
-    // histos and sets on the split engine's stream, beside this engine's work; this engine's
-    // stream waits for the moved states (and the group's collectives stay in one order)
-    split_histos(e, c);
-    split_sets(e, c);
-    vn_engine* a = S.aux;
-    hipLaunchKernelGGL(k_split_errors, dim3(1), dim3(64), 0, a->st, a->h_err, e->h_err);
-    VN_HIP_CHECK(hipEventRecord(S.ev_done, a->st));
+    // histos and sets on the split engine's stream, beside this engine's work (already under
+    // way in the worker thread after vn_split_close); this engine's stream waits for the moved
+    // states, and the counters' collectives follow the split engine's (one order per group)
+    if (S.closed) {
+      S.closed = false;
+      split_join(e);
+    } else {
+      split_combine_aux(e, c);
+    }
     S.ran = true;
     VN_HIP_CHECK(hipStreamWaitEvent(e->st, S.ev_done, 0));
   }
+  S.closed = false;
   split_counters(e, c, e->st);
   for (int k = 0; k < VN_NCLASS; k++) {
     S.slot[k].clear();
@@ -1215,6 +1257,7 @@ void split_flush(vn_engine* e) {
 
 void split_destroy(vn_engine* e) {
   SplitState& S = e->sp;
+  if (S.worker.joinable()) S.worker.join();
   if (S.aux) (void)hipStreamSynchronize(S.aux->st);
   for (void* p : S.scratch)
     if (p) (void)hipFree(p);
@@ -1229,7 +1272,10 @@ void split_destroy(vn_engine* e) {
   if (S.solo) vn_comm_destroy(S.solo);
   if (S.aux) vn_engine_destroy(S.aux);
   if (S.ev_done) (void)hipEventDestroy(S.ev_done);
-  S = SplitState{};
+  if (S.ev_histo) (void)hipEventDestroy(S.ev_histo);
+  if (S.ev_set_prefix) (void)hipEventDestroy(S.ev_set_prefix);
+  S.~SplitState();
+  new (&S) SplitState();
 }
 
 }  // namespace vn
@@ -1274,6 +1320,7 @@ int vn_split_keys(vn_engine* e, int cls, const uint32_t* slot, const uint32_t* o
     if (cls != VN_COUNTER && cls != VN_HISTO && cls != VN_SET)
       throw std::invalid_argument("only counters, histograms and sets can be split");
     SplitState& S = e->sp;
+    if (S.closed) throw std::invalid_argument("split keys change while the window's split combine runs (flush first)");
     if ((cls == VN_HISTO && S.nh) || (cls == VN_SET && S.ns))
       throw std::invalid_argument("split keys change while their records are buffered (flush first)");
     const int N = S.comm ? S.comm->nranks : 1;
@@ -1298,6 +1345,26 @@ int vn_split_keys(vn_engine* e, int cls, const uint32_t* slot, const uint32_t* o
   });
 }
 
+int vn_split_close(vn_engine* e) {
+  if (!e) return VN_EINVAL;
+  return split_guarded(e, [&] {
+    SplitState& S = e->sp;
+    if (S.closed) return;
+    if (S.slot[VN_HISTO].empty() && S.slot[VN_SET].empty()) return;  // nothing for the split engine
+    vn_comm* c = group_of(e);
+    S.closed = true;
+    const int dev = e->device;
+    S.worker = std::thread([e, c, dev] {
+      try {
+        VN_HIP_CHECK(hipSetDevice(dev));
+        split_combine_aux(e, c);
+      } catch (...) {
+        e->sp.worker_err = std::current_exception();
+      }
+    });
+  });
+}
+
 int vn_split_combine(vn_engine* e) {
   if (!e) return VN_EINVAL;
   return split_guarded(e, [&] {
@@ -1311,6 +1378,7 @@ int vn_ingest_split(vn_engine* e, const vn_split_batch* b) {
   if (!e || !b) return VN_EINVAL;
   return split_guarded(e, [&] {
     SplitState& S = e->sp;
+    if (S.closed) throw std::invalid_argument("split records after vn_split_close (flush first)");
     const uint32_t nh = (uint32_t)S.slot[VN_HISTO].size(), ns = (uint32_t)S.slot[VN_SET].size();
     if ((b->n_histo && !nh) || (b->n_set && !ns)) throw std::invalid_argument("records for a class with no split keys");
     if (S.nh + b->n_histo > e->cfg.split_max_records || S.ns + b->n_set > e->cfg.split_max_records)

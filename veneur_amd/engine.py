@@ -169,6 +169,10 @@ class Engine:
             raise ValueError("one owner per split key")
         self._check(A.lib.vn_split_keys(self.h, int(cls), s.ctypes.data_as(A.u32p), o.ctypes.data_as(A.u32p), len(s)))
 
+    def split_close(self):
+        """vn_split_close: this window's split records are all in; their combine starts now."""
+        self._check(A.lib.vn_split_close(self.h))
+
     def split_combine(self):
         """vn_split_combine: meet the group now (collective); vn_flush does it otherwise."""
         self._check(A.lib.vn_split_combine(self.h))
@@ -269,6 +273,21 @@ class Engine:
         off = np.ctypeslib.as_array(x.off, shape=(x.n + 1,)).copy()
         blob = np.ctypeslib.as_array(x.bytes, shape=(max(1, int(off[-1])),)).tobytes()
         return [blob[off[i]:off[i + 1]] for i in range(x.n)]
+
+    def export_raw(self, cls, slot):
+        """Export (cls 2 histo, 3 set) of slot[] as (offsets u64[n+1], bytes u8) host copies."""
+        s = _c(np.atleast_1d(slot), np.uint32)
+        x = A.Export()
+        fn = A.lib.vn_export_histos if cls == 2 else A.lib.vn_export_sets
+        self._check(fn(self.h, s.ctypes.data_as(A.u32p), len(s), C.byref(x)))
+        off = np.ctypeslib.as_array(x.off, shape=(x.n + 1,)).copy()
+        blob = np.ctypeslib.as_array(x.bytes, shape=(max(1, int(off[-1])),)).copy()
+        return off, blob
+
+    def import_device(self, cls, slot_ptr, off_ptr, bytes_ptr, n):
+        """vn_import_histos_device / vn_import_sets_device (cls 2 / 3) of device-resident payloads."""
+        fn = A.lib.vn_import_histos_device if cls == 2 else A.lib.vn_import_sets_device
+        self._check(fn(self.h, slot_ptr, off_ptr, bytes_ptr, int(n)))
 
     def export_histos(self, slot):
         """Histo.Export: GobEncode()d digest of each histo slot (merges its pending temps)."""
