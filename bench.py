@@ -225,6 +225,7 @@ def main():
     ap.add_argument("--c5-distinct", type=int, default=8, help="distinct host windows, cycled")
     ap.add_argument("--c5-windows", type=int, default=1)
     ap.add_argument("--c5-parity-keys", type=int, default=16)
+    ap.add_argument("--split-delay-ms", type=float, default=0.0, help="development only: host delay after split_close")
     ap.add_argument("--host-trace", action="store_true",
                     help="development only: report host ms in split_keys+ingest_split / ingest / flush")
     ap.add_argument("--pcie-steps", type=int, default=1,
@@ -281,6 +282,8 @@ def main():
         if sum(stream.split_counts):
             eng.ingest_split_device(stream.split)
             eng.split_close()  # their combine runs beside this engine's ingest
+            if args.split_delay_ms:
+                time.sleep(args.split_delay_ms * 1e-3)
         if t:
             t.append(time.perf_counter())
         eng.ingest_device(stream.batch)
