@@ -168,6 +168,7 @@ struct vn_engine {
   // exact (Go-incremental) replay state and batch split
   uint32_t exact_threshold = 32768;
   uint32_t hot_prefix = 4096;    // a key past the threshold replays this many samples exactly
+  uint32_t long_replay = 0;      // replays of at least this many samples take four waves (0: threshold / 4)
   uint32_t piece_growth = 25;    // remainder piece size, percent of the window samples before it
   uint32_t temp_cap = 42;        // estimateTempBuffer(compression)
   uint32_t* hseen = nullptr;     // samples seen this window per slot

@@ -843,10 +843,10 @@ struct FusedRounds {
   double *cm0, *cm1, *cw0, *cw1;
   double* val;           // [key][kFuseMaxL]
   double* w;
+  double* kk;            // k of every merged element (global: the kernel needs no large LDS block)
   uint32_t* err;
 };
 __global__ __launch_bounds__(kBlock) void k_rounds_fused(FusedRounds x) {
-  __shared__ double s_k[kFuseMaxL];
   __shared__ uint32_t s_st[kMaxCent + 1];
   __shared__ double s_tmp[4];
   __shared__ uint32_t s_nc;
@@ -855,6 +855,7 @@ __global__ __launch_bounds__(kBlock) void k_rounds_fused(FusedRounds x) {
   const uint32_t s = x.tl[key], npieces = x.pcnt[key], capc = x.capc;
   double* val = x.val + (uint64_t)blockIdx.x * kFuseMaxL;
   double* wgt = x.w + (uint64_t)blockIdx.x * kFuseMaxL;
+  double* s_k = x.kk + (uint64_t)blockIdx.x * kFuseMaxL;
   uint32_t nc = x.hncent[s];
   uint8_t cur = x.hcur[s];
   double* h = x.hst + (uint64_t)s * VN_HISTO_STATS;
@@ -992,7 +993,7 @@ __global__ __launch_bounds__(kBlock) void k_rounds_fused(FusedRounds x) {
 }
 
 void histo_rounds_fused(vn_engine* e, const uint32_t* list, uint32_t nkeys, const uint64_t* PA, const uint64_t* PB,
-                        const double* impw, double* val, double* w, hipStream_t st) {
+                        const double* impw, double* val, double* w, double* kk, hipStream_t st) {
   if (!nkeys) return;
   FusedRounds x;
   x.list = list;
@@ -1016,6 +1017,7 @@ void histo_rounds_fused(vn_engine* e, const uint32_t* list, uint32_t nkeys, cons
   x.cw1 = e->cw[1];
   x.val = val;
   x.w = w;
+  x.kk = kk;
   x.err = e->h_err;
   hipLaunchKernelGGL(k_rounds_fused, dim3(nkeys), dim3(kBlock), 0, st, x);
 }
@@ -1200,8 +1202,8 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   // beside the one-wave replay of the rest on the same CUs
   auto replay_cold = [&](hipStream_t s, RadixScratch& rs) {
     histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
-    const bool longk = histo_exact_count_long(xc, std::max<uint32_t>(e->exact_threshold / 4, 1024u),
-                                              e->h_cnt + 15, s);
+    const uint32_t min_len = e->long_replay ? e->long_replay : std::max<uint32_t>(e->exact_threshold / 4, 1024u);
+    const bool longk = histo_exact_count_long(xc, min_len, e->h_cnt + 15, s);
     const bool side5 = longk && !e->timing && e->st5;
     hipEvent_t a = e->timing ? e->pool_rp.next() : nullptr, b = e->timing ? e->pool_rp.next() : nullptr;
     if (a && b) VN_HIP_CHECK(hipEventRecord(a, s));

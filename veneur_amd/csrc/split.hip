@@ -43,7 +43,7 @@ enum ScratchId {
   kSSegT, kSStarts, kSNcNew, kSAccXw, kSAccW, kSHst, kSHnc, kSHcur, kSHspn, kSCm0, kSCm1, kSCw0, kSCw1, kSElem,
   kSSend, kSRecv, kSKeyOff, kSCntMat, kSCntAll, kSOwnList, kSImpA, kSImpB, kSImpA1, kSImpB1, kSImpSlot, kSImpVal,
   kSImpW, kSMicW, kSCP, kSCM, kSPcnt, kSFF, kSW32, kSCand, kSTfull, kSP0, kSDone, kSR2, kSPre, kSDev1,
-  kSLocalStats, kSCtr, kSTouch, kSIota, kSFuseV, kSFuseW, kSCount
+  kSLocalStats, kSCtr, kSTouch, kSIota, kSFuseV, kSFuseW, kSFuseK, kSCount
 };
 
 template <class T>
@@ -103,6 +103,17 @@ vn_engine* split_engine(vn_engine* e, uint64_t records) {
     throw std::runtime_error("cannot create the split engine: " + m);
   }
   S.aux = a;
+  a->long_replay = 1024;  // the owner's gathered prefixes (4096 records) are its critical path
+  {
+    // a stream of its own hardware queue: the engine's high-priority streams (this engine's
+    // main and hot-prefix streams) share one, and behind their event waits the combine's short
+    // kernels would queue until this engine's replay ends
+    hipStream_t s = nullptr;
+    VN_HIP_CHECK(hipStreamSynchronize(a->st));
+    VN_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    VN_HIP_CHECK(hipStreamDestroy(a->st));
+    a->st = s;
+  }
   radix_scratch_reserve(a->rs, std::max<uint64_t>(e->cfg.split_max_records, a->max_records));
   uint32_t* iota = sbuf<uint32_t>(e, kSIota, kMaxSplitKeys);
   std::vector<uint32_t> h(kMaxSplitKeys);
@@ -805,7 +816,8 @@ void split_histos(vn_engine* e, vn_comm* c) {
       // every piece is at most N ranks' micro-centroids: all rounds in one launch
       double* fv = sbuf<double>(e, kSFuseV, (size_t)K * kFuseMaxL);
       double* fw = sbuf<double>(e, kSFuseW, (size_t)K * kFuseMaxL);
-      histo_rounds_fused(a, olist, K, MA_, MB_, micw, fv, fw, st);
+      double* fk = sbuf<double>(e, kSFuseK, (size_t)K * kFuseMaxL);
+      histo_rounds_fused(a, olist, K, MA_, MB_, micw, fv, fw, fk, st);
     } else {
       VN_HIP_CHECK(hipMemcpyAsync(a->h_hotlist, olist, K * 4, hipMemcpyDeviceToDevice, st));
       std::vector<uint32_t> hpc(K);
