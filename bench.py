@@ -132,7 +132,7 @@ def c5_leg(args, rank):
     keep += [hslot, sslot]
     gen_s = time.time() - t0
     payload_bytes = sum(int(h[0][-1]) + int(s_[0][-1]) for h, s_ in zip(hp, sp)) / D * hosts
-    with V.Engine((1, 1, H, S), percentiles=PCT, max_batch_records=1 << 25) as g:
+    with V.Engine((1, 1, H, S), percentiles=PCT, max_batch_records=getattr(args, "c5_batch", 1 << 25)) as g:
         def window():
             for h in range(hosts):
                 ho, hb, so, sb = dev[h % D]
@@ -168,11 +168,12 @@ def c5_leg(args, rank):
         for i, k in enumerate(ks):
             w.import_set(i, sb[so[k]:so[k + 1]].tobytes())
     pos = {int(s_): j for j, s_ in enumerate(hsl)}
-    st_exact, rank_err = True, 0.0
+    st_exact, rank_err, st_diff = True, 0.0, np.zeros(3)
     for i, k in enumerate(kh):
         j = pos[int(k)]
         ost = np.array(w.histo_stats(i))
         st_exact &= bool(np.array_equal(hst[j, [5, 6, 7]], ost[[5, 6, 7]]))
+        st_diff = np.maximum(st_diff, np.abs(hst[j, [5, 6, 7]] - ost[[5, 6, 7]]))
         m = np.concatenate([cents[i][h % D][0] for h in range(hosts)])
         wt = np.concatenate([cents[i][h % D][1] for h in range(hosts)])
         o = np.argsort(m, kind="stable")
@@ -191,7 +192,8 @@ def c5_leg(args, rank):
             "ms_per_window": ms, "windows": args.c5_windows, "payloads_per_window": n_imp,
             "payload_bytes_per_window": payload_bytes, "generated_in_s": round(gen_s, 2),
             "parity": {"keys_checked": {"histo": int(len(kh)), "set": int(len(ks))},
-                       "histo_weight_min_max_exact": st_exact, "histo_rank_error_max": rank_err,
+                       "histo_weight_min_max_exact": st_exact, "histo_min_max_weight_absdiff": st_diff.tolist(),
+                       "histo_rank_error_max": rank_err,
                        "set_estimates_exact": bool(set_exact)}}
 
 

@@ -349,3 +349,63 @@ def test_histo_quantile_cdf_queries():  # merging_digest.go:247-313 (Quantile, C
     np.testing.assert_array_equal(got_q, exp_q)
     oq = np.array([[w.histo_quantile(int(s), p) for p in PCT] for s in f.histo_slot])
     np.testing.assert_array_equal(f.histo_quantiles, oq)
+
+
+@pytest.mark.parametrize("batches", [5, 10])
+def test_histo_keys_cross_threshold_across_batches(batches):
+    """every key (~48k samples) passes the exact threshold in a later batch than its first (the
+    import run's pattern): weights, min/max exact; the warm keys' rank error stays within the
+    bound the single-batch scheme shows for keys just past the threshold"""
+    d = V.synth(seed=25, n_keys=100, zipf_s=0.0, mix=(0, 0, 1, 0), n_samples=4_800_000)
+    _histo_parity(d, d["n_slots"], batches=batches, max_rank=3e-3)
+
+
+def test_histo_exact_replay_long_keys_multi_batch():
+    """four-wave replays (batches of >= threshold / 4 per key) continuing from pending temps:
+    bit-identical quantiles"""
+    d = V.synth(seed=26, n_keys=100, zipf_s=0.0, mix=(0, 0, 1, 0), n_samples=1_200_000)
+    _histo_parity(d, d["n_slots"], batches=4, exact_threshold=16384)
+
+
+def test_histo_warm_keys_only_single_batch():
+    """every key warm (E < n <= 4E) and none hot: the replay of E samples then the warm rounds,
+    with no hot-prefix stream in the batch"""
+    d = V.synth(seed=27, n_keys=16, zipf_s=0.0, mix=(0, 0, 1, 0), n_samples=1_280_000)
+    _histo_parity(d, d["n_slots"], batches=1, max_rank=3e-3)
+
+
+def test_histo_warm_imports_single_batch():
+    """the same shape as imported centroids (Histo.Combine of many hosts' digests in one run)"""
+    rng = np.random.default_rng(28)
+    nk, hosts = 16, 800
+    w = oracle.Worker(1, 1, nk, 1)
+    with make_engine((1, 1, nk, 1), max_records=1 << 24) as e:
+        for h in range(hosts):
+            pay = []
+            for k in range(nk):
+                t = oracle.MergingDigest(100.0)
+                n = int(rng.integers(50, 150))
+                t.add_many(np.exp(rng.normal(3.9, 1.0, n)), np.where(rng.random(n) < 0.1, 2.0, 1.0))
+                pay.append(t.gob_encode())
+            e.import_histos(np.arange(nk, dtype=np.uint32), pay)
+            for k in range(nk):
+                assert w.import_histo(k, pay[k]) == 0
+        f = e.flush()
+    ost = np.array([w.histo_stats(k) for k in range(nk)])
+    np.testing.assert_array_equal(f.histo_stats[:, [5, 6, 7]], ost[:, [5, 6, 7]])
+
+
+def test_histo_duplicate_values_past_threshold():
+    """integer-valued timers (every value repeated thousands of times) on warm and hot keys:
+    the batch merge's centroid means stay ordered, so no element is lost (weights, min/max
+    exact) and the rank error holds"""
+    rng = np.random.default_rng(29)
+    sizes = [60_000, 90_000, 300_000, 5_000]
+    slot = np.concatenate([np.full(n, k, np.uint32) for k, n in enumerate(sizes)])
+    rng.shuffle(slot)
+    val = np.maximum(1.0, np.round(np.exp(rng.normal(3.0, 0.8, len(slot)))))
+    rate = np.where(rng.random(len(slot)) < 0.1, np.float32(0.5), np.float32(1.0)).astype(np.float32)
+    d = {"c_slot": np.zeros(0, np.uint32), "c_val": np.zeros(0), "c_rate": np.zeros(0, np.float32),
+         "g_slot": np.zeros(0, np.uint32), "g_val": np.zeros(0), "h_slot": slot, "h_val": val, "h_rate": rate,
+         "s_slot": np.zeros(0, np.uint32), "s_off": np.zeros(1, np.uint32), "s_bytes": np.zeros(0, np.uint8)}
+    _histo_parity(d, (1, 1, len(sizes), 1), batches=3, max_rank=3e-3)

@@ -476,9 +476,17 @@ __global__ __launch_bounds__(kBlock) void k_finalize(HistoCtx x) {
   const uint8_t nb = x.hcur[s] ^ 1;
   double* cm = nb ? x.cm1 : x.cm0;
   double* cwn = nb ? x.cw1 : x.cw0;
+  const uint32_t lo = x.start[s], n = x.end[s] - lo;
   for (uint32_t ci = t; ci < nc; ci += kBlock) {
     double w = x.acc_w[(uint64_t)k * capc + ci];
-    cm[(uint64_t)s * capc + ci] = ddiv(x.acc_xw[(uint64_t)k * capc + ci], w);
+    // sum(x w) / sum(w) may round past the centroid's own elements when they are equal (a
+    // Welford mean never does): held to [first, last] element, so the means stay in order --
+    // the next merge's positions (and Go's two-way merge) take them as sorted
+    const uint32_t a = x.starts[(uint64_t)k * capc + ci];
+    const uint32_t b = ci + 1 < nc ? x.starts[(uint64_t)k * capc + ci + 1] : n;
+    const double m = ddiv(x.acc_xw[(uint64_t)k * capc + ci], w);
+    const double lo_v = from_ordered_bits(x.A[lo + a]), hi_v = from_ordered_bits(x.A[lo + b - 1]);
+    cm[(uint64_t)s * capc + ci] = m < lo_v ? lo_v : (m > hi_v ? hi_v : m);
     cwn[(uint64_t)s * capc + ci] = w;
   }
   __syncthreads();
