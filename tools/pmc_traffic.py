@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """HBM traffic of the roofline kernel from two rocprofv3 --pmc passes.
 
-    python tools/pmc_traffic.py gpurun_out/TAG_pmc_fetch gpurun_out/TAG_pmc_write TAG [KERNEL BENCH_JSON]
+    python tools/pmc_traffic.py gpurun_out/TAG_pmc_fetch gpurun_out/TAG_pmc_write TAG [KERNEL BENCH_JSON WINDOWS]
 
 Each pass is its own `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` run of the same bench
 command (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2: they cannot share a pass).  Both counters
@@ -53,20 +53,25 @@ def read_pass(path, counter):
     return out
 
 
-def other_kernel(fetch, write, kernel, bench_json, tag):
+def other_kernel(fetch, write, kernel, bench_json, tag, windows):
+    """every dispatch of the kernel's family in the PMC runs (k_histo_exact: the one-wave and
+    four-wave ingest replays, not the flush's k_histo_exact_list), per window, over the bench's
+    launches per step -- the same unit as its algorithmic bytes per launch"""
     with open(bench_json) as fh:
         line = [ln for ln in fh.read().splitlines() if ln.startswith("{")][-1]
     kern = {k["kernel"]: k for k in json.loads(line)["roofline"]["kernels"]}[kernel]
-    fb = [v * 1024.0 for (name, _, v) in fetch.values() if kernel in name]
-    wb = [v * 1024.0 for (name, _, v) in write.values() if kernel in name]
+    match = lambda name: kernel in name and "_list" not in name
+    fb = [v * 1024.0 for (name, _, v) in fetch.values() if match(name)]
+    wb = [v * 1024.0 for (name, _, v) in write.values() if match(name)]
     if not fb or len(fb) != len(wb):
         raise SystemExit("dispatch mismatch: %d fetch vs %d write rows" % (len(fb), len(wb)))
-    n = len(fb)
+    n = windows * kern["launches_per_step"]
     fetch_b, write_b = 2.0 * sum(fb), sum(wb)
     alg = kern["algorithmic_bytes_per_launch"]
     return {
         "kernel": kernel,
-        "dispatches": n,
+        "dispatches": len(fb),
+        "windows": windows,
         "traffic_per_launch": (fetch_b + write_b) / n,
         "fetch_per_launch": fetch_b / n,
         "write_per_launch": write_b / n,
@@ -83,7 +88,7 @@ def main():
     fetch = read_pass(fetch_dir, "FETCH_SIZE")
     write = read_pass(write_dir, "WRITE_SIZE")
     if len(sys.argv) > 5 and sys.argv[4] != KERNEL:
-        res = other_kernel(fetch, write, sys.argv[4], sys.argv[5], tag)
+        res = other_kernel(fetch, write, sys.argv[4], sys.argv[5], tag, int(sys.argv[6]) if len(sys.argv) > 6 else 1)
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         for p in (os.path.join(root, "roofline_traffic.json"),
                   os.path.join(root, "profiles", "%s_pmc_traffic.json" % tag)):
