@@ -42,6 +42,21 @@ namespace {
 
 constexpr uint32_t kMaxTempPerLane = 4;  // tcap <= 256 (estimateTempBuffer <= 178)
 
+// LDS pointers typed in address space 3, so every access through them is a ds_read/ds_write.
+// A plain double* into LDS that reaches a function through memory (a struct passed by
+// reference, a non-inlined callee) loses its address space and compiles to flat loads, which
+// are slower and wait on both vmcnt and lgkmcnt.
+typedef __attribute__((address_space(3))) double ldsf64;
+typedef __attribute__((address_space(3))) uint32_t ldsu32;
+typedef __attribute__((address_space(3))) uint16_t ldsu16;
+
+// a merge's result (returned by value: references to the caller's locals would put them in
+// scratch memory when the callee is not inlined)
+struct NmW {
+  uint32_t nm;
+  double w;
+};
+
 __device__ __forceinline__ bool is_int_weight(double w) { return w == __builtin_floor(w) && w <= 4503599627370496.0; }
 
 __device__ __forceinline__ double rl_d(double v, int i) {
@@ -58,8 +73,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 
 // ---- Go 1.9 sort.Sort(centroidList) on lane 0 (restated from oracle/oracle.c go_sort)
 struct GoSortCent {
-  double* v;
-  double* w;
+  ldsf64* v;
+  ldsf64* w;
   __device__ bool less(int i, int j) const { return v[i] < v[j]; }
   __device__ void swap(int i, int j) const {
     double a = v[i]; v[i] = v[j]; v[j] = a;
@@ -174,18 +189,39 @@ struct MergeParams {
 };
 
 struct Lds {
-  double *mm, *mw;       // main centroids [capc]
-  double *tv, *tw;       // pending temps in Add order [TP]
-  double *sv, *sw;       // sorted temps of the merge being done [TP]
-  double *gm, *gw, *kin; // merged elements [JW]
-  uint32_t* jump;        // start of the table memory (jump16 aliases it)
-  uint16_t* jump16;      // next-start tables, levels x [JW] u16 (entries <= JW < 65536)
-  uint32_t* starts;      // [JW]
+  ldsf64 *mm, *mw;        // main centroids [capc]
+  ldsf64 *tv, *tw;        // pending temps in Add order [TP]
+  ldsf64 *sv, *sw;        // sorted temps of the merge being done [TP]
+  ldsf64 *gm, *gw, *kin;  // merged elements [JW]
+  ldsu32* jump;           // start of the table memory (jump16 aliases it)
+  ldsu16* jump16;         // next-start tables, levels x [JW] u16 (entries <= JW < 65536)
+  ldsu32* starts;         // [JW]
   uint32_t JW, levels;
 };
 
+// the replay's LDS layout (dynamic shared memory, exact_smem_bytes)
+__device__ __forceinline__ Lds lds_layout(char* smem, uint32_t capc, uint32_t TP) {
+  Lds L;
+  L.JW = max(capc + TP + 1, 320u);  // >= 64 * kR: the fast merge pads its tables
+  L.levels = 1;
+  while ((1u << L.levels) <= capc) L.levels++;
+  L.mm = (ldsf64*)smem;
+  L.mw = L.mm + capc;
+  L.tv = L.mw + capc;
+  L.tw = L.tv + TP;
+  L.sv = L.tw + TP;
+  L.sw = L.sv + TP;
+  L.gm = L.sw + TP;
+  L.gw = L.gm + L.JW;
+  L.kin = L.gw + L.JW;
+  L.starts = (ldsu32*)(L.kin + L.JW);
+  L.jump = L.starts + L.JW;
+  L.jump16 = (ldsu16*)L.jump;
+  return L;
+}
+
 // #main centroids with mean < v (main is sorted by mean)
-__device__ __forceinline__ uint32_t main_below(const double* mm, uint32_t nm, double v) {
+__device__ __forceinline__ uint32_t main_below(const ldsf64* mm, uint32_t nm, double v) {
   uint32_t l = 0, h = nm;
   while (l < h) {
     uint32_t md = (l + h) >> 1;
@@ -195,7 +231,7 @@ __device__ __forceinline__ uint32_t main_below(const double* mm, uint32_t nm, do
   return l;
 }
 // #sorted temps with mean <= v
-__device__ __forceinline__ uint32_t temps_le(const double* sv, uint32_t np, double v) {
+__device__ __forceinline__ uint32_t temps_le(const ldsf64* sv, uint32_t np, double v) {
   uint32_t l = 0, h = np;
   while (l < h) {
     uint32_t md = (l + h) >> 1;
@@ -207,7 +243,7 @@ __device__ __forceinline__ uint32_t temps_le(const double* sv, uint32_t np, doub
 
 // td.tempWeight of np temps in Add order: the sequential fold, computed as a wave sum when
 // every weight is an integer and the total stays below 2^53 (then every order is exact).
-__device__ double temp_weight(const double* tw, uint32_t np) {
+__device__ double temp_weight(const ldsf64* tw, uint32_t np) {
   const uint32_t lane = threadIdx.x & 63;
   bool tint = true;
   double part = 0.0;
@@ -234,7 +270,7 @@ __device__ double temp_weight(const double* tw, uint32_t np) {
 // Sort np temps (tv/tw, Add order) into sv/sw as sort.Sort(centroidList) orders them:
 // counting rank over (mean, Add index); when equal means make the order observable
 // (different weights or signed zeros) lane 0 runs Go's quickSort instead.  One wave.
-__device__ __noinline__ void sort_temps(const double* tv, const double* tw, double* sv, double* sw, uint32_t np) {
+__device__ __noinline__ void sort_temps(const ldsf64* tv, const ldsf64* tw, ldsf64* sv, ldsf64* sw, uint32_t np) {
   const uint32_t lane = threadIdx.x & 63;
   uint32_t rank[kMaxTempPerLane];
   double vr[kMaxTempPerLane], wr[kMaxTempPerLane];
@@ -279,8 +315,8 @@ __device__ __noinline__ void sort_temps(const double* tv, const double* tw, doub
 
 // mergeAllTemps of the sorted temps L.sv/L.sw (np of them, Add-order weight sum tempW)
 // into main L.mm/L.mw.  One wave; every step is a parallel pass of O(log) depth.
-__device__ __noinline__ void merge_sorted(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
-                             double tempW) {
+__device__ __noinline__ NmW merge_sorted(const MergeParams x, const Lds L, const uint32_t nm, const double mainW,
+                                        uint32_t np, double tempW) {
   const uint32_t lane = threadIdx.x;
   PROF_T(p0);
   const double T = dadd(mainW, tempW);  // totalWeight := td.mainWeight + td.tempWeight
@@ -357,7 +393,7 @@ __device__ __noinline__ void merge_sorted(const MergeParams x, const Lds& L, uin
   bool overflow = false;
   const uint32_t capc = x.capc;
   if (mono) {
-    uint16_t* J0 = L.jump16;
+    ldsu16* J0 = L.jump16;
     for (uint32_t s = lane; s <= m; s += 64) {
       uint32_t r = m;
       if (s < m) {
@@ -374,8 +410,8 @@ __device__ __noinline__ void merge_sorted(const MergeParams x, const Lds& L, uin
     }
     wave_lds_sync();
     for (uint32_t lv = 1; lv < L.levels; lv++) {
-      const uint16_t* Jp = L.jump16 + (lv - 1) * L.JW;
-      uint16_t* Jl = L.jump16 + lv * L.JW;
+      const ldsu16* Jp = L.jump16 + (lv - 1) * L.JW;
+      ldsu16* Jl = L.jump16 + lv * L.JW;
       for (uint32_t s = lane; s <= m; s += 64) Jl[s] = (uint16_t)Jp[Jp[s]];
       wave_lds_sync();
     }
@@ -439,8 +475,7 @@ __device__ __noinline__ void merge_sorted(const MergeParams x, const Lds& L, uin
   PROF_ADD(5, 0, 1);
   PROF_ADD(6, 0, (long long)m);
   PROF_ADD(7, 0, (long long)nc);
-  nm = nc;
-  mainW = T;
+  return NmW{nc, T};
 }
 
 // Same merge, written branch-free for a lone wave: every per-lane loop is unrolled over kR
@@ -451,7 +486,7 @@ constexpr int kR = 5;     // largest instantiation: nm + np < 320
 constexpr int kLogT = 7;  // steps of a search over the temps (np <= 64 < 2^7)
 
 template <int kR>
-__device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
+__device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds L, uint32_t& nm, double& mainW, uint32_t np,
                                   double tempW) {
   // steps of a lower-bound search over at most 64 kR - 1 entries: ceil(log2(64 kR))
   constexpr int kLogR = kR <= 1 ? 6 : (kR <= 2 ? 7 : (kR <= 4 ? 8 : 9));
@@ -621,8 +656,8 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
     uint32_t levels = 1;  // t < 64 * kR needs bits 0 .. levels-1
     while ((1u << levels) < 64u * kR) levels++;
     for (uint32_t lv = 1; lv < levels; lv++) {
-      const uint16_t* Jp = L.jump16 + (lv - 1) * L.JW;
-      uint16_t* Jl = L.jump16 + lv * L.JW;
+      const ldsu16* Jp = L.jump16 + (lv - 1) * L.JW;
+      ldsu16* Jl = L.jump16 + lv * L.JW;
       uint32_t a[kR];
 #pragma unroll
       for (int r = 0; r < kR; r++) a[r] = Jp[cur[r]];  // J_lv[s] = J_(lv-1)[J_(lv-1)[s]]
@@ -639,7 +674,7 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
 #pragma unroll
     for (int r = 0; r < kR; r++) p[r] = 0;
     for (uint32_t lv = 0; lv < levels; lv++) {
-      const uint16_t* J = L.jump16 + lv * L.JW;
+      const ldsu16* J = L.jump16 + lv * L.JW;
 #pragma unroll
       for (int r = 0; r < kR; r++) {
         const uint32_t t = 64 * r + lane;
@@ -711,25 +746,34 @@ __device__ void merge_sorted_fast(const MergeParams x, const Lds& L, uint32_t& n
   mainW = T;
 }
 
-__device__ __forceinline__ void merge_any(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
+__device__ __forceinline__ void merge_any(const MergeParams x, const Lds L, uint32_t& nm, double& mainW, uint32_t np,
                                           double tempW) {
   // nc <= m < 64 * R: the fast merge's start enumeration (t < 64 * R) covers every centroid
   const uint32_t m = nm + np;
-  if (np > 64 || m >= 64u * kR) merge_sorted(x, L, nm, mainW, np, tempW);
-  else if (m < 128) merge_sorted_fast<2>(x, L, nm, mainW, np, tempW);
+  if (np > 64 || m >= 64u * kR) {
+    const NmW r = merge_sorted(x, L, nm, mainW, np, tempW);
+    nm = r.nm;
+    mainW = r.w;
+  } else if (m < 128) merge_sorted_fast<2>(x, L, nm, mainW, np, tempW);
   else if (m < 192) merge_sorted_fast<3>(x, L, nm, mainW, np, tempW);
   else if (m < 256) merge_sorted_fast<4>(x, L, nm, mainW, np, tempW);
   else merge_sorted_fast<5>(x, L, nm, mainW, np, tempW);
 }
 
 // sort the pending temps in LDS and merge them
-__device__ __noinline__ void merge_pending(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np) {
+__device__ __noinline__ NmW merge_pending_v(const MergeParams x, const Lds L, uint32_t nm, double mainW, uint32_t np) {
   PROF_T(a0);
   const double tempW = temp_weight(L.tw, np);
   sort_temps(L.tv, L.tw, L.sv, L.sw, np);
   PROF_T(a1);
   PROF_ADD(0, a0, a1);
   merge_any(x, L, nm, mainW, np, tempW);
+  return NmW{nm, mainW};
+}
+__device__ __forceinline__ void merge_pending(const MergeParams x, const Lds L, uint32_t& nm, double& mainW, uint32_t np) {
+  const NmW r = merge_pending_v(x, L, nm, mainW, np);
+  nm = r.nm;
+  mainW = r.w;
 }
 
 __device__ __forceinline__ uint32_t round64(uint32_t v) { return (v + 63u) & ~63u; }
@@ -775,10 +819,10 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
   const uint32_t g = blockIdx.x, lane = threadIdx.x;
   if (g >= x.coff[x.nkeys]) return;
   const uint32_t tcap = x.tcap, TP = round64(tcap + 1);
-  double* tv = reinterpret_cast<double*>(smem);
-  double* tw = tv + TP;
-  double* sv = tw + TP;
-  double* sw = sv + TP;
+  ldsf64* tv = (ldsf64*)smem;
+  ldsf64* tw = tv + TP;
+  ldsf64* sv = tw + TP;
+  ldsf64* sw = sv + TP;
   const uint32_t k = last_le_u32(x.coff, x.nkeys, g);
   const uint32_t s = x.keys[k];
   const ExactSplit sp = exact_split(x.hpend[s], x.nex[k], tcap);
@@ -807,22 +851,7 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
   const uint32_t lane = threadIdx.x;
   const uint32_t capc = x.capc, tcap = x.tcap;
   const uint32_t TP = round64(tcap + 1);
-  Lds L;
-  L.JW = max(capc + TP + 1, 320u);  // >= 64 * kR: the fast merge pads its tables
-  L.levels = 1;
-  while ((1u << L.levels) <= capc) L.levels++;
-  L.mm = reinterpret_cast<double*>(smem);
-  L.mw = L.mm + capc;
-  L.tv = L.mw + capc;
-  L.tw = L.tv + TP;
-  L.sv = L.tw + TP;
-  L.sw = L.sv + TP;
-  L.gm = L.sw + TP;
-  L.gw = L.gm + L.JW;
-  L.kin = L.gw + L.JW;
-  L.starts = reinterpret_cast<uint32_t*>(L.kin + L.JW);
-  L.jump = L.starts + L.JW;
-  L.jump16 = reinterpret_cast<uint16_t*>(L.jump);
+  const Lds L = lds_layout(smem, capc, TP);
 
   PROF_T(k0);
   // kernel arguments into registers: nothing below may take the address of x
@@ -1026,10 +1055,11 @@ struct MwShared {  // one slot per purpose: a late wave may still read one while
   double fb_w;
   double red[7][kMW];
 };
+typedef __attribute__((address_space(3))) MwShared MwSharedL;
 
 // requires nm + np < kMWThreads, np <= 64, capc <= kMWThreads
-__device__ void merge_mw(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np, double tempW,
-                         MwShared& S) {
+__device__ __forceinline__ void merge_mw(const MergeParams x, const Lds L, uint32_t& nm, double& mainW, uint32_t np,
+                                         double tempW, MwSharedL& S) {
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const double T = dadd(mainW, tempW);
   const uint32_t m = nm + np;
@@ -1124,7 +1154,7 @@ __device__ void merge_mw(const MergeParams x, const Lds& L, uint32_t& nm, double
     }
     __syncthreads();
     for (uint32_t lv = 1; lv < 8; lv++) {  // t < 256: bits 0..7
-      const uint16_t* Jp = L.jump16 + (lv - 1) * L.JW;
+      const ldsu16* Jp = L.jump16 + (lv - 1) * L.JW;
       const uint32_t a = Jp[cur];
       L.jump16[lv * L.JW + t] = (uint16_t)a;
       cur = a;
@@ -1202,11 +1232,11 @@ __device__ void merge_mw(const MergeParams x, const Lds& L, uint32_t& nm, double
 }
 
 // a merge of any shape: the four-wave merge when it fits, else wave 0 runs the single-wave one
-__device__ void merge_mw_any(const MergeParams x, const Lds& L, uint32_t& nm, double& mainW, uint32_t np,
-                             double tempW, MwShared& S) {
+__device__ __noinline__ NmW merge_mw_any(const MergeParams x, const Lds L, uint32_t nm, double mainW, uint32_t np,
+                                         double tempW, MwSharedL& S) {
   if (nm + np < kMWThreads && np <= 64 && x.capc <= kMWThreads) {
     merge_mw(x, L, nm, mainW, np, tempW, S);
-    return;
+    return NmW{nm, mainW};
   }
   if (threadIdx.x < 64) {
     merge_any(x, L, nm, mainW, np, tempW);
@@ -1216,32 +1246,16 @@ __device__ void merge_mw_any(const MergeParams x, const Lds& L, uint32_t& nm, do
     }
   }
   __syncthreads();
-  nm = S.fb_nm;
-  mainW = S.fb_w;
+  return NmW{S.fb_nm, S.fb_w};
 }
 
 // replay_key with four waves (tcap <= 64, ingest only: no flush-mode adoption)
-__device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwShared& S) {
+__device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwSharedL& S) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t capc = x.capc, tcap = x.tcap;
   const uint32_t TP = round64(tcap + 1);
-  Lds L;
-  L.JW = max(capc + TP + 1, 320u);
-  L.levels = 1;
-  while ((1u << L.levels) <= capc) L.levels++;
-  L.mm = reinterpret_cast<double*>(smem);
-  L.mw = L.mm + capc;
-  L.tv = L.mw + capc;
-  L.tw = L.tv + TP;
-  L.sv = L.tw + TP;
-  L.sw = L.sv + TP;
-  L.gm = L.sw + TP;
-  L.gw = L.gm + L.JW;
-  L.kin = L.gw + L.JW;
-  L.starts = reinterpret_cast<uint32_t*>(L.kin + L.JW);
-  L.jump = L.starts + L.JW;
-  L.jump16 = reinterpret_cast<uint16_t*>(L.jump);
+  const Lds L = lds_layout(smem, capc, TP);
 
   const MergeParams mp{x.delta, x.capc, x.err};
   const uint64_t* const xA = x.A;
@@ -1308,7 +1322,9 @@ __device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwShared& S) 
     __syncthreads();
     const double tempW = S.tempW;
     __syncthreads();
-    merge_mw_any(mp, L, nm, mainW, np, tempW, S);
+    const NmW r = merge_mw_any(mp, L, nm, mainW, np, tempW, S);
+    nm = r.nm;
+    mainW = r.w;
   };
 
   if (nex && np == tcap) {
@@ -1342,7 +1358,9 @@ __device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwShared& S) 
       const double tempW = ctw;
       if (c + 1 < sp.npure) load(c + 1);
       __syncthreads();
-      merge_mw_any(mp, L, nm, mainW, tcap, tempW, S);
+      const NmW r = merge_mw_any(mp, L, nm, mainW, tcap, tempW, S);
+      nm = r.nm;
+      mainW = r.w;
     }
   }
   const uint32_t tail = sp.off0 + sp.npure * tcap;
@@ -1441,7 +1459,7 @@ __global__ __launch_bounds__(kMWThreads) void k_histo_exact_mw(ExactCtx x, const
   const uint32_t n = *nmw;
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t k = x.order64 ? (uint32_t)x.order64[i] : x.order ? x.order[i] : i;
-    if (k < x.nkeys) replay_key_mw(x, k, S);
+    if (k < x.nkeys) replay_key_mw(x, k, *(MwSharedL*)&S);
     __syncthreads();  // the next key reuses the LDS
   }
 }
