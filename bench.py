@@ -354,7 +354,8 @@ def main():
     for name, ms_k, by_k, n_k in (("k_histo_exact", "ms_histo_replay", "histo_replay_bytes", "histo_replay_launches"),
                                   ("k_set_segments", "ms_set_segments", "set_segment_bytes", "set_segment_launches"),
                                   ("k_radix_scatter", "ms_radix_scatter_total", "radix_scatter_bytes",
-                                   "radix_scatter_launches")):
+                                   "radix_scatter_launches"),
+                                  ("k_part_scatter", "ms_part_scatter", "part_scatter_bytes", "part_scatter_launches")):
         ms, by, nl = mean(ms_k), mean(by_k), mean(n_k)
         if ms > 0 and nl > 0:
             ach = by / (ms * 1e-3) / 1e9

@@ -266,7 +266,7 @@ typedef struct {
   float ms_ingest_counter, ms_ingest_gauge, ms_ingest_histo, ms_ingest_set, ms_flush;
   float ms_sort_histo, ms_sort_set;
   uint64_t sort_passes_histo, sort_passes_set;
-  float ms_radix_scatter_total;   /* sum over radix scatter launches */
+  float ms_radix_scatter_total;   /* sum over k_radix_scatter launches */
   uint64_t radix_scatter_launches;
   uint64_t radix_scatter_bytes;   /* algorithmic bytes moved by those launches */
   /* the exact t-digest replay (k_histo_exact): launches, time, algorithmic bytes = 16 B per
@@ -291,6 +291,11 @@ typedef struct {
   /* inside the split combine: histograms done, sets' gathered prefix replayed */
   float ms_split_histo_ready;
   float ms_split_set_prefix_ready;
+  /* counter / gauge partition scatter (k_part_scatter): 16 + 12 B (counter) or 12 + 12 B (gauge)
+   * per record read and written; the radix figures above cover k_radix_scatter only */
+  float ms_part_scatter;
+  uint64_t part_scatter_launches;
+  uint64_t part_scatter_bytes;
 } vn_timing;
 int vn_timing_enable(vn_engine* eng, int enable);
 int vn_get_timing(vn_engine* eng, vn_timing* out);

@@ -14,7 +14,7 @@ fi
 timeout -k 10 400 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.log || exit $?
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
   python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1 || exit $?
-python3 tools/roofline_check.py gpurun_out/${TAG}_prof gpurun_out/${TAG}_prof.log > gpurun_out/${TAG}_roofline_check.txt 2>&1
+python3 tools/roofline_check.py gpurun_out/${TAG}_prof gpurun_out/${TAG}_prof.log 1 gpurun_out/${TAG}_timing_step_kernel_stats.csv > gpurun_out/${TAG}_roofline_check.txt 2>&1
 if [ "$3" = "pmc" ]; then
   # HBM traffic: FETCH_SIZE and WRITE_SIZE in separate passes (TCC slots), counters only
   timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_pmc_fetch -o run -- \

@@ -118,7 +118,9 @@ class Timing(C.Structure):
                 ("ms_set_segments", C.c_float), ("set_segment_launches", C.c_uint64),
                 ("set_segment_bytes", C.c_uint64), ("ms_flush_host", C.c_float), ("ms_split_host", C.c_float),
                 ("ms_main_ready", C.c_float), ("ms_split_ready", C.c_float),
-                ("ms_split_histo_ready", C.c_float), ("ms_split_set_prefix_ready", C.c_float)]
+                ("ms_split_histo_ready", C.c_float), ("ms_split_set_prefix_ready", C.c_float),
+                ("ms_part_scatter", C.c_float), ("part_scatter_launches", C.c_uint64),
+                ("part_scatter_bytes", C.c_uint64)]
 
 
 class SynthConfig(C.Structure):

@@ -453,6 +453,7 @@ void destroy_impl(vn_engine* e) {
   for (auto ev : e->pool_storage) (void)hipEventDestroy(ev);
   for (auto ev : e->pool_rp_storage) (void)hipEventDestroy(ev);
   for (auto ev : e->pool_ss_storage) (void)hipEventDestroy(ev);
+  for (auto ev : e->pool_ps_storage) (void)hipEventDestroy(ev);
   for (auto& ev : e->ev)
     if (ev) (void)hipEventDestroy(ev);
   if (e->st) (void)hipStreamDestroy(e->st);
@@ -537,9 +538,10 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
     e->pool.used = 0;
     e->pool_rp.used = 0;
     e->pool_ss.used = 0;
+    e->pool_ps.used = 0;
     e->kstat_rp = RadixStats{&e->pool_rp, 0, 0};
     e->kstat_ss = RadixStats{&e->pool_ss, 0, 0};
-    e->rstat_c = RadixStats{&e->pool, 0, 0};
+    e->rstat_c = RadixStats{&e->pool_ps, 0, 0};
     e->rstat_h = RadixStats{&e->pool, 0, 0};
     e->rstat_s = RadixStats{&e->pool, 0, 0};
     VN_HIP_CHECK(hipEventRecord(e->ev[0], st));
@@ -947,8 +949,8 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
         tot += ms;
       }
       t.ms_radix_scatter_total = tot;
-      t.radix_scatter_launches = e->rstat_c.launches + e->rstat_h.launches + e->rstat_s.launches;
-      t.radix_scatter_bytes = e->rstat_c.bytes + e->rstat_h.bytes + e->rstat_s.bytes;
+      t.radix_scatter_launches = e->rstat_h.launches + e->rstat_s.launches;
+      t.radix_scatter_bytes = e->rstat_h.bytes + e->rstat_s.bytes;
       auto pool_ms = [](EventPool& p) {
         float tot = 0;
         for (int i = 0; i + 1 < p.used; i += 2) {
@@ -964,6 +966,9 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
       t.ms_set_segments = pool_ms(e->pool_ss);
       t.set_segment_launches = e->kstat_ss.launches;
       t.set_segment_bytes = e->kstat_ss.bytes;
+      t.ms_part_scatter = pool_ms(e->pool_ps);
+      t.part_scatter_launches = e->rstat_c.launches;
+      t.part_scatter_bytes = e->rstat_c.bytes;
     }
     const auto h2 = std::chrono::steady_clock::now();
     e->last.ms_flush_host = std::chrono::duration<float, std::milli>(h2 - h0).count();
@@ -1002,7 +1007,7 @@ int vn_timing_enable(vn_engine* e, int enable) {
       for (auto& ev : e->pool_storage) VN_HIP_CHECK(hipEventCreate(&ev));
       e->pool.ev = e->pool_storage.data();
       e->pool.cap = (int)e->pool_storage.size();
-      for (auto* ps : {&e->pool_rp_storage, &e->pool_ss_storage}) {
+      for (auto* ps : {&e->pool_rp_storage, &e->pool_ss_storage, &e->pool_ps_storage}) {
         ps->resize(64);
         for (auto& ev : *ps) VN_HIP_CHECK(hipEventCreate(&ev));
       }
@@ -1010,6 +1015,8 @@ int vn_timing_enable(vn_engine* e, int enable) {
       e->pool_rp.cap = (int)e->pool_rp_storage.size();
       e->pool_ss.ev = e->pool_ss_storage.data();
       e->pool_ss.cap = (int)e->pool_ss_storage.size();
+      e->pool_ps.ev = e->pool_ps_storage.data();
+      e->pool_ps.cap = (int)e->pool_ps_storage.size();
     }
   });
 }

@@ -283,7 +283,7 @@ struct vn_engine {
   vn_timing last{};
   vn::RadixStats rstat_c, rstat_h, rstat_s;
   // timed launches of the exact replay and of the set state machine (timing mode)
-  vn::EventPool pool_rp, pool_ss;
-  std::vector<hipEvent_t> pool_rp_storage, pool_ss_storage;
+  vn::EventPool pool_rp, pool_ss, pool_ps;
+  std::vector<hipEvent_t> pool_rp_storage, pool_ss_storage, pool_ps_storage;
   vn::RadixStats kstat_rp, kstat_ss;
 };
