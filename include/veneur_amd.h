@@ -390,6 +390,22 @@ typedef struct {
 int64_t vn_parse_dogstatsd(const char* buf, uint64_t len, vn_parsed_line* out, uint64_t max_lines,
                            char* tags_out, uint64_t tags_cap);
 
+/* The same parse on the GPU (csrc/parse_device.hip): buf, out and tags_out are device memory and
+ * the result is identical to vn_parse_dogstatsd's, line for line and byte for byte in tags_out.
+ * A parser owns its stream and scratch for buffers of up to max_bytes (< 4 GiB) bytes holding up
+ * to max_lines lines.  tags_cap must be at least len (joined tags never outgrow their lines, so
+ * VN_PARSE_TAGS_FULL cannot occur); *n_lines gets the number of non-empty lines.  More than
+ * max_lines lines: VN_EINVAL, nothing written to out. */
+typedef struct vn_parser vn_parser;
+int vn_parser_create(int device, uint64_t max_bytes, uint64_t max_lines, vn_parser** out);
+void vn_parser_destroy(vn_parser* p);
+const char* vn_parser_last_error(const vn_parser* p);
+int vn_parse_dogstatsd_device(vn_parser* p, const char* buf, uint64_t len, vn_parsed_line* out, uint64_t max_lines,
+                              char* tags_out, uint64_t tags_cap, uint64_t* n_lines);
+/* strconv.ParseFloat(s, bits) of Go 1.9 (bits 64 or 32) as the device parser computes it, run on
+ * the host: 0 ok, 1 syntax error, 2 out of range (ErrRange); *out the value (float32 widened). */
+int vn_go_parse_float(const char* s, uint64_t n, int bits, double* out);
+
 #ifdef __cplusplus
 }
 #endif

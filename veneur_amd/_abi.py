@@ -197,6 +197,11 @@ class ParsedLine(C.Structure):  # vn_parsed_line
 
 _sig("vn_parse_dogstatsd", C.c_int64, C.c_char_p, C.c_uint64, C.POINTER(ParsedLine), C.c_uint64, C.c_char_p,
      C.c_uint64)
+_sig("vn_parser_create", C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.POINTER(vp))
+_sig("vn_parser_destroy", None, vp)
+_sig("vn_parser_last_error", C.c_char_p, vp)
+_sig("vn_parse_dogstatsd_device", C.c_int, vp, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, u64p)
+_sig("vn_go_parse_float", C.c_int, C.c_char_p, C.c_uint64, C.c_int, f64p)
 _sig("vn_comm_unique_id", C.c_int, u8p)
 _sig("vn_comm_init", C.c_int, u8p, C.c_int, C.c_int, C.c_int, C.POINTER(vp))
 _sig("vn_comm_init_local", C.c_int, C.c_int, C.c_int, C.POINTER(vp))
@@ -229,7 +234,8 @@ _sig("vn_synth_key_counts", C.c_int, C.POINTER(SynthDevConfig), C.c_uint64, u32p
 EXPORTED = [
     "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
     "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_flush_masked", "vn_sync",
-    "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
+    "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_parser_create", "vn_parser_destroy",
+    "vn_parser_last_error", "vn_parse_dogstatsd_device", "vn_go_parse_float", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
     "vn_synth_device", "vn_synth_device_free", "vn_synth_key_counts",
     "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",
