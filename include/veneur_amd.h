@@ -402,6 +402,44 @@ void vn_parser_destroy(vn_parser* p);
 const char* vn_parser_last_error(const vn_parser* p);
 int vn_parse_dogstatsd_device(vn_parser* p, const char* buf, uint64_t len, vn_parsed_line* out, uint64_t max_lines,
                               char* tags_out, uint64_t tags_cap, uint64_t* n_lines);
+/* Device intake: the ProcessMetric path for DogStatsD text (csrc/intake.hip).  For a buffer of
+ * datagram lines in HBM: the device parse above, then Worker.ProcessMetric (worker.go:187-227) for
+ * every line that parses -- Upsert (worker.go:81-138) of its MetricKey into the window's key table
+ * on the device (ten maps by type x scope; a new key takes the next slot of its class, in line
+ * order, as the host Worker's interning does), then one vn_ingest of the staged records.  Counter
+ * and histogram/timer lines with a NaN sample rate are dropped and counted (the parser accepts
+ * NaN, the engine rejects it).  A buffer whose new keys pass a class's capacity fails with
+ * VN_EINVAL and leaves the table and the window unchanged.  vn_intake_upsert interns keys the
+ * host hands in (ImportMetric's Upsert, worker.go:230-268: map id 0..9 = counters,
+ * global_counters, gauges, global_gauges, histograms, local_histograms, timers, local_timers, sets,
+ * local_sets; digest = FNV-1a of name, type name and joined tags) into the same table; slot_out
+ * gets each key's slot.  vn_intake_read_keys returns the window's keys (creation order) for
+ * Worker.Flush's samplers; vn_intake_reset starts a new window (after vn_flush). */
+typedef struct vn_intake vn_intake;
+typedef struct {
+  uint64_t lines;         /* non-empty lines */
+  uint64_t processed;     /* ProcessMetric calls (records ingested) */
+  uint64_t parse_errors;  /* lines ParseMetric rejects (logged and skipped, server.go:700-704) */
+  uint64_t dropped;       /* NaN sample rates */
+  uint64_t new_keys;      /* keys first seen in this buffer */
+} vn_intake_stats;
+typedef struct {
+  uint64_t n_keys, arena_bytes;
+  uint32_t next_slot[VN_NCLASS];
+} vn_intake_info;
+int vn_intake_create(vn_engine* eng, uint64_t max_bytes, uint64_t max_lines, vn_intake** out);
+void vn_intake_destroy(vn_intake* in);
+const char* vn_intake_last_error(const vn_intake* in);
+int vn_intake_process(vn_intake* in, const char* buf, uint64_t len, vn_intake_stats* stats);
+int vn_intake_upsert(vn_intake* in, uint64_t n, const uint8_t* map, const uint32_t* n_tags, const uint32_t* digest,
+                     const uint32_t* name_off, const uint32_t* name_len, const uint32_t* tags_off,
+                     const uint32_t* tags_len, const uint8_t* bytes, uint64_t nbytes, uint32_t* slot_out);
+int vn_intake_keys_info(vn_intake* in, vn_intake_info* info);
+/* host arrays of info.n_keys entries (arena: info.arena_bytes; a key's joined tags follow its name) */
+int vn_intake_read_keys(vn_intake* in, uint8_t* map, uint32_t* slot, uint32_t* n_tags, uint64_t* name_off,
+                        uint32_t* name_len, uint32_t* tags_len, uint8_t* arena);
+int vn_intake_reset(vn_intake* in);
+
 /* strconv.ParseFloat(s, bits) of Go 1.9 (bits 64 or 32) as the device parser computes it, run on
  * the host: 0 ok, 1 syntax error, 2 out of range (ErrRange); *out the value (float32 widened). */
 int vn_go_parse_float(const char* s, uint64_t n, int bits, double* out);

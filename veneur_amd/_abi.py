@@ -202,6 +202,25 @@ _sig("vn_parser_destroy", None, vp)
 _sig("vn_parser_last_error", C.c_char_p, vp)
 _sig("vn_parse_dogstatsd_device", C.c_int, vp, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, u64p)
 _sig("vn_go_parse_float", C.c_int, C.c_char_p, C.c_uint64, C.c_int, f64p)
+
+
+class IntakeStats(C.Structure):  # vn_intake_stats
+    _fields_ = [("lines", C.c_uint64), ("processed", C.c_uint64), ("parse_errors", C.c_uint64),
+                ("dropped", C.c_uint64), ("new_keys", C.c_uint64)]
+
+
+class IntakeInfo(C.Structure):  # vn_intake_info
+    _fields_ = [("n_keys", C.c_uint64), ("arena_bytes", C.c_uint64), ("next_slot", C.c_uint32 * 4)]
+
+
+_sig("vn_intake_create", C.c_int, vp, C.c_uint64, C.c_uint64, C.POINTER(vp))
+_sig("vn_intake_destroy", None, vp)
+_sig("vn_intake_last_error", C.c_char_p, vp)
+_sig("vn_intake_process", C.c_int, vp, vp, C.c_uint64, C.POINTER(IntakeStats))
+_sig("vn_intake_upsert", C.c_int, vp, C.c_uint64, u8p, u32p, u32p, u32p, u32p, u32p, u32p, u8p, C.c_uint64, u32p)
+_sig("vn_intake_keys_info", C.c_int, vp, C.POINTER(IntakeInfo))
+_sig("vn_intake_read_keys", C.c_int, vp, u8p, u32p, u32p, u64p, u32p, u32p, u8p)
+_sig("vn_intake_reset", C.c_int, vp)
 _sig("vn_comm_unique_id", C.c_int, u8p)
 _sig("vn_comm_init", C.c_int, u8p, C.c_int, C.c_int, C.c_int, C.POINTER(vp))
 _sig("vn_comm_init_local", C.c_int, C.c_int, C.c_int, C.POINTER(vp))
@@ -235,7 +254,9 @@ EXPORTED = [
     "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
     "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_flush_masked", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_parser_create", "vn_parser_destroy",
-    "vn_parser_last_error", "vn_parse_dogstatsd_device", "vn_go_parse_float", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
+    "vn_parser_last_error", "vn_parse_dogstatsd_device", "vn_go_parse_float", "vn_intake_create", "vn_intake_destroy",
+    "vn_intake_last_error", "vn_intake_process", "vn_intake_upsert", "vn_intake_keys_info", "vn_intake_read_keys",
+    "vn_intake_reset", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
     "vn_synth_device", "vn_synth_device_free", "vn_synth_key_counts",
     "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",
