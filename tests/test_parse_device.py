@@ -100,8 +100,31 @@ def test_device_parse_generated(dev_parser):
 
 
 @pytest.mark.gpu
+def test_device_parse_unaligned_buffer(dev_parser):
+    """A datagram buffer that starts at an odd device address (byte loads instead of vector loads)."""
+    import ctypes as C
+    import veneur_amd._abi as A
+    from veneur_amd.intake import PARSED_DTYPE, parse_host
+    rng = np.random.default_rng(5)
+    d = b"\n".join(gen_lines(rng, 3000))
+    A.lib.vn_copy_to_device(0, C.c_void_p(dev_parser.buf.ptr.value + 3), C.c_char_p(d), len(d))
+    n = C.c_uint64()
+    assert A.lib.vn_parse_dogstatsd_device(dev_parser.h, C.c_void_p(dev_parser.buf.ptr.value + 3), len(d),
+                                           dev_parser.out.ptr, dev_parser.max_lines, dev_parser.tags.ptr,
+                                           dev_parser.max_bytes, C.byref(n)) == 0
+    hl, _ = parse_host(d)
+    dl = np.zeros(n.value, PARSED_DTYPE)
+    A.lib.vn_copy_to_host(0, dl.ctypes.data_as(C.c_void_p), dev_parser.out.ptr, n.value * PARSED_DTYPE.itemsize)
+    assert len(dl) == len(hl) and np.array_equal(dl["status"], hl["status"])
+    ok = hl["status"] == 0
+    assert np.array_equal(dl["digest"][ok], hl["digest"][ok]) and np.array_equal(dl["line_off"], hl["line_off"])
+
+
+@pytest.mark.gpu
 def test_device_parse_edges(dev_parser):
-    for buf in (b"", b"\n", b"\n\n\n", b"a:1|c", b"a:1|c\n", b"\na:1|c", b"x" * 5000, b"a:1|c|#" + b"t," * 2000 + b"t"):
+    long_lines = b"\n".join(b"k%d:1.5|ms|#z:%d,a:" % (i, i) + b"t" * 90 for i in range(600))  # > 16 KiB per block
+    for buf in (b"", b"\n", b"\n\n\n", b"a:1|c", b"a:1|c\n", b"\na:1|c", b"x" * 5000, b"a:1|c|#" + b"t," * 2000 + b"t",
+                long_lines):
         compare(buf, dev_parser)
     from veneur_amd.intake import DeviceError
     with pytest.raises(DeviceError):  # more lines than max_lines

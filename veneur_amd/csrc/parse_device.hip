@@ -54,24 +54,40 @@ namespace vn {
 namespace {
 
 constexpr int kLsBlock = 256;
-constexpr int kLsPer = 16;
-constexpr uint32_t kLsTile = kLsBlock * kLsPer;  // 4096 bytes
+constexpr uint32_t kLsTile = kLsBlock * 16;  // 4096 bytes: 16 per thread
 constexpr int kSlowLanes = 2048;
 
-__device__ __forceinline__ bool is_start(const uint8_t* __restrict__ buf, uint64_t i) {
-  return buf[i] != '\n' && (i == 0 || buf[i - 1] == '\n');
+// Line starts of thread t's 16 bytes [base + 16t, +16) as a 16-bit mask: byte j starts a line when
+// it is not '\n' and the byte before it is '\n' (or it is the buffer's first byte).  The bytes come
+// in one 16-byte load (the buffer's last partial chunk byte by byte); the byte before them is the
+// previous lane's last byte, or one load for lane 0 of each wave.
+__device__ __forceinline__ uint32_t start_mask(const uint8_t* __restrict__ buf, uint64_t len, uint64_t pos) {
+  uint32_t w[4] = {0x0a0a0a0au, 0x0a0a0a0au, 0x0a0a0a0au, 0x0a0a0a0au};  // past the end: '\n' (no starts)
+  if (pos + 16 <= len && !(reinterpret_cast<uintptr_t>(buf) & 15u)) {
+    const uint4 v = *reinterpret_cast<const uint4*>(buf + pos);
+    w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+  } else if (pos < len) {  // the last partial chunk, or a buffer that is not 16-byte aligned
+    for (uint32_t j = 0; j < 16 && pos + j < len; j++)
+      w[j >> 2] = (w[j >> 2] & ~(0xffu << (8 * (j & 3)))) | ((uint32_t)buf[pos + j] << (8 * (j & 3)));
+  }
+  const int lane = threadIdx.x & 63;
+  uint32_t prev = __shfl_up(w[3] >> 24, 1, 64);
+  if (lane == 0) prev = pos == 0 ? '\n' : (pos - 1 < len ? buf[pos - 1] : '\n');
+  uint32_t m = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+    m |= (c != '\n' && prev == '\n') ? (1u << j) : 0u;
+    prev = c;
+  }
+  return m;
 }
 
 __global__ __launch_bounds__(kLsBlock) void k_ls_count(const uint8_t* __restrict__ buf, uint64_t len,
                                                        uint32_t* __restrict__ cnt) {
   __shared__ uint32_t s_w[kLsBlock / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kLsTile;
-  uint32_t c = 0;
-#pragma unroll
-  for (int j = 0; j < kLsPer; j++) {
-    const uint64_t i = base + (uint64_t)j * kLsBlock + threadIdx.x;
-    c += (i < len && is_start(buf, i)) ? 1u : 0u;
-  }
+  const uint64_t pos = (uint64_t)blockIdx.x * kLsTile + 16u * threadIdx.x;
+  uint32_t c = __popc(start_mask(buf, len, pos));
   for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
   if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
   __syncthreads();
@@ -80,32 +96,26 @@ __global__ __launch_bounds__(kLsBlock) void k_ls_count(const uint8_t* __restrict
 
 __global__ __launch_bounds__(kLsBlock) void k_ls_emit(const uint8_t* __restrict__ buf, uint64_t len,
                                                       const uint32_t* __restrict__ off, uint32_t* __restrict__ starts) {
-  __shared__ uint32_t s_c[kLsPer][kLsBlock / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * kLsTile;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint64_t masks[kLsPer];
-#pragma unroll
-  for (int j = 0; j < kLsPer; j++) {
-    const uint64_t i = base + (uint64_t)j * kLsBlock + threadIdx.x;
-    masks[j] = __ballot(i < len && is_start(buf, i));
-    if (lane == 0) s_c[j][w] = (uint32_t)__popcll(masks[j]);
+  __shared__ uint32_t s_w[kLsBlock / 64];
+  const uint64_t pos = (uint64_t)blockIdx.x * kLsTile + 16u * threadIdx.x;
+  const uint32_t m = start_mask(buf, len, pos);
+  const uint32_t c = __popc(m);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t incl = c;  // inclusive scan over the wave
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
   }
+  if (lane == 63) s_w[w] = incl;
   __syncthreads();
-  if (threadIdx.x == 0) {  // byte order within the tile is (j, wave, lane)
-    uint32_t run = off[blockIdx.x];
-    for (int j = 0; j < kLsPer; j++)
-      for (int q = 0; q < kLsBlock / 64; q++) {
-        const uint32_t c = s_c[j][q];
-        s_c[j][q] = run;
-        run += c;
-      }
-  }
-  __syncthreads();
-  const uint64_t lt = (1ull << lane) - 1ull;
-#pragma unroll
-  for (int j = 0; j < kLsPer; j++) {
-    if ((masks[j] >> lane) & 1ull)
-      starts[s_c[j][w] + (uint32_t)__popcll(masks[j] & lt)] = (uint32_t)(base + (uint64_t)j * kLsBlock + threadIdx.x);
+  uint32_t run = off[blockIdx.x];
+  for (int q = 0; q < w; q++) run += s_w[q];
+  run += incl - c;
+  uint32_t mm = m;
+  while (mm) {
+    const int j = __ffs(mm) - 1;
+    mm &= mm - 1;
+    starts[run++] = (uint32_t)(pos + j);
   }
 }
 
@@ -139,15 +149,13 @@ __device__ __forceinline__ int str_cmp(const uint8_t* a, uint32_t na, const uint
 constexpr int32_t kValueDeferred = 1 << 16;
 constexpr int32_t kRateDeferred = 1 << 17;
 
-__global__ __launch_bounds__(256) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t len,
-                                                     const uint32_t* __restrict__ starts, uint32_t n,
-                                                     vn_parsed_line* __restrict__ out, uint32_t* __restrict__ tsec,
-                                                     int32_t* __restrict__ removed, uint32_t* __restrict__ tlen,
-                                                     uint32_t* __restrict__ slow) {
-  const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
-  if (li >= n) return;
-  const uint32_t p = starts[li];
-  const uint32_t end = find(buf, p, (uint32_t)len, '\n');
+// One line: buf[p, ...) up to the next '\n' or wend.  buf is the LDS window of the block's lines
+// (off0 = the window's offset in the datagram buffer) or the buffer itself (off0 = 0).
+__device__ __forceinline__ void parse_one(const uint8_t* buf, uint32_t off0, uint32_t p, uint32_t wend, uint32_t li,
+                                          vn_parsed_line* __restrict__ out, uint32_t* __restrict__ tsec,
+                                          int32_t* __restrict__ removed, uint32_t* __restrict__ tlen,
+                                          uint32_t* __restrict__ slow) {
+  const uint32_t end = find(buf, p, wend, '\n');
   vn_parsed_line o;
   o.line_off = p;
   o.line_len = end - p;
@@ -272,6 +280,13 @@ __global__ __launch_bounds__(256) void k_parse_lines(const uint8_t* __restrict__
   const int32_t base = status & 0xffff;
   if (status & (kValueDeferred | kRateDeferred)) slow[1 + atomicAdd(&slow[0], 1u)] = li;
   o.status = status;
+  o.line_off += off0;
+  if (o.name_len || o.value_off) {
+    o.name_off += off0;
+    o.value_off = (o.value_off & 0xffffffff00000000ull) | ((o.value_off & 0xffffffffull) + off0);
+  }
+  if (status & kRateDeferred) o.value_off += (uint64_t)off0 << 32;
+  if (o.has_tags) sec_off += off0;
   out[li] = o;
   tsec[2 * li] = sec_off;
   tsec[2 * li + 1] = sec_len;
@@ -279,6 +294,42 @@ __global__ __launch_bounds__(256) void k_parse_lines(const uint8_t* __restrict__
   tlen[li] = (base == VN_PARSE_OK && o.has_tags && !(status & (kValueDeferred | kRateDeferred))) ? jl : 0;
   // deferred lines set their tag length once their numbers are known (k_parse_slow)
   if ((status & (kValueDeferred | kRateDeferred)) && base == VN_PARSE_OK && o.has_tags) tlen[li] = jl | 0x80000000u;
+}
+
+// one block = 256 consecutive lines; their bytes are staged in LDS when they fit (the usual case:
+// lines of up to 64 bytes on average), else the lanes read the buffer directly
+constexpr uint32_t kWin = 16384;
+
+// copies buf[lo, hi) to win from the word at lo & ~3 (full words, then the tail bytes); returns that base
+__device__ __forceinline__ uint32_t stage_window(const uint8_t* __restrict__ buf, uint64_t len, uint32_t lo,
+                                                 uint32_t hi, uint8_t* win) {
+  const uint32_t wlo = lo & ~3u;
+  // full words (a buffer that is not 4-byte aligned: bytes only)
+  const uint32_t whi = (reinterpret_cast<uintptr_t>(buf) & 3u) ? wlo : min((hi + 3u) & ~3u, (uint32_t)len & ~3u);
+  for (uint32_t w = wlo + 4u * threadIdx.x; w < whi; w += 4u * blockDim.x)
+    *reinterpret_cast<uint32_t*>(win + (w - wlo)) = *reinterpret_cast<const uint32_t*>(buf + w);
+  for (uint32_t i = max(whi, wlo) + threadIdx.x; i < hi; i += blockDim.x) win[i - wlo] = buf[i];
+  return wlo;
+}
+
+__global__ __launch_bounds__(256) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t len,
+                                                     const uint32_t* __restrict__ starts, uint32_t n,
+                                                     vn_parsed_line* __restrict__ out, uint32_t* __restrict__ tsec,
+                                                     int32_t* __restrict__ removed, uint32_t* __restrict__ tlen,
+                                                     uint32_t* __restrict__ slow) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin];
+  const uint32_t first = blockIdx.x * blockDim.x;
+  const uint32_t last = min(first + blockDim.x, n);
+  const uint32_t lo = starts[first];
+  const uint32_t hi = last < n ? starts[last] : (uint32_t)len;
+  const uint32_t li = first + threadIdx.x;
+  if (hi - (lo & ~3u) <= kWin) {  // block-uniform
+    const uint32_t wlo = stage_window(buf, len, lo, hi, s_win);
+    __syncthreads();
+    if (li < n) parse_one(s_win, wlo, starts[li] - wlo, hi - wlo, li, out, tsec, removed, tlen, slow);
+  } else if (li < n) {
+    parse_one(buf, 0, starts[li], (uint32_t)len, li, out, tsec, removed, tlen, slow);
+  }
 }
 
 // The deferred numbers (more than 19 significant digits or a far exponent): Go's decimal path.
@@ -327,25 +378,10 @@ __global__ __launch_bounds__(256) void k_parse_slow(const uint8_t* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(256) void k_parse_tags(const uint8_t* __restrict__ buf, uint32_t n,
-                                                    vn_parsed_line* __restrict__ out,
-                                                    const uint32_t* __restrict__ tsec,
-                                                    const int32_t* __restrict__ removed,
-                                                    const uint32_t* __restrict__ toff, uint8_t* __restrict__ tags_out) {
-  const uint32_t li = blockIdx.x * blockDim.x + threadIdx.x;
-  if (li >= n) return;
-  const uint32_t to = toff[li];
-  const uint32_t jl = toff[li + 1] - to;
-  vn_parsed_line& o = out[li];
-  o.tags_off = to;
-  if (o.status != VN_PARSE_OK || !o.has_tags) {
-    if (o.status == VN_PARSE_OK) o.tags_len = 0;
-    return;
-  }
-  o.tags_len = jl;
-  const uint8_t* q = buf + tsec[2 * li];
-  const uint32_t L = tsec[2 * li + 1];
-  const int32_t rm = removed[li];
+// Tags of one line: q = its tag section (L bytes), written joined at dst; returns the FNV-1a of them
+// continued from h.
+__device__ __forceinline__ uint32_t join_tags(const uint8_t* q, uint32_t L, int32_t rm, uint32_t jl, uint8_t* dst,
+                                              uint32_t h) {
   // tag i at its sorted position: the bytes (+ comma) of every kept tag ranked before it
   uint32_t ai = 0, i = 0;
   for (uint32_t ki = 0; ki <= L; ki++) {
@@ -363,14 +399,50 @@ __global__ __launch_bounds__(256) void k_parse_tags(const uint8_t* __restrict__ 
         aj = kj + 1;
         j++;
       }
-      uint8_t* dst = tags_out + to + pos;
-      for (uint32_t b = 0; b < ni; b++) dst[b] = q[ai + b];
-      if (pos + ni < jl) dst[ni] = ',';
+      for (uint32_t b = 0; b < ni; b++) dst[pos + b] = q[ai + b];
+      if (pos + ni < jl) dst[pos + ni] = ',';
     }
     ai = ki + 1;
     i++;
   }
-  o.digest = fnv(o.digest, tags_out + to, jl);
+  return fnv(h, dst, jl);
+}
+
+__global__ __launch_bounds__(256) void k_parse_tags(const uint8_t* __restrict__ buf, uint64_t len, uint32_t n,
+                                                    vn_parsed_line* __restrict__ out,
+                                                    const uint32_t* __restrict__ tsec,
+                                                    const int32_t* __restrict__ removed,
+                                                    const uint32_t* __restrict__ toff, uint8_t* __restrict__ tags_out) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_win[kWin];
+  __shared__ __attribute__((aligned(16))) uint8_t s_out[kWin];
+  const uint32_t first = blockIdx.x * blockDim.x;
+  const uint32_t last = min(first + blockDim.x, n);
+  const uint32_t li = first + threadIdx.x;
+  const uint32_t lo = (uint32_t)out[first].line_off;
+  const uint32_t hi = last < n ? (uint32_t)out[last].line_off : (uint32_t)len;
+  const uint32_t t0 = toff[first], t1 = toff[last];  // this block's joined tags: tags_out[t0, t1)
+  const bool staged = hi - (lo & ~3u) <= kWin;       // block-uniform (t1 - t0 <= hi - lo)
+  uint32_t wlo = 0;
+  if (staged) {
+    wlo = stage_window(buf, len, lo, hi, s_win);
+    __syncthreads();
+  }
+  if (li < n) {
+    const uint32_t to = toff[li];
+    const uint32_t jl = toff[li + 1] - to;
+    vn_parsed_line& o = out[li];
+    o.tags_off = to;
+    if (o.status == VN_PARSE_OK) o.tags_len = o.has_tags ? jl : 0;
+    if (o.status == VN_PARSE_OK && o.has_tags) {
+      const uint32_t so = tsec[2 * li], L = tsec[2 * li + 1];
+      o.digest = staged ? join_tags(s_win + (so - wlo), L, removed[li], jl, s_out + (to - t0), o.digest)
+                        : join_tags(buf + so, L, removed[li], jl, tags_out + to, o.digest);
+    }
+  }
+  if (staged) {  // the block's joined tags, written out with consecutive lanes on consecutive bytes
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < t1 - t0; i += blockDim.x) tags_out[t0 + i] = s_out[i];
+  }
 }
 
 void check_rc(vn_parser* p, hipError_t rc, const char* what) {
@@ -457,8 +529,8 @@ int vn_parse_dogstatsd_device(vn_parser* p, const char* buf, uint64_t len, vn_pa
                        p->tsec, p->removed, p->tlen, p->slow);
     hipLaunchKernelGGL(k_parse_slow, dim3(kSlowLanes / 256), dim3(256), 0, p->st, b, out, p->slow, p->tlen, p->dec);
     scan_exclusive_u32(p->tlen, p->toff, n, p->scan, p->st);
-    hipLaunchKernelGGL(k_parse_tags, dim3(blocks_for(n, 256)), dim3(256), 0, p->st, b, n, out, p->tsec, p->removed,
-                       p->toff, reinterpret_cast<uint8_t*>(tags_out));
+    hipLaunchKernelGGL(k_parse_tags, dim3(blocks_for(n, 256)), dim3(256), 0, p->st, b, len, n, out, p->tsec,
+                       p->removed, p->toff, reinterpret_cast<uint8_t*>(tags_out));
     check_rc(p, hipGetLastError(), "launch");
     check_rc(p, hipStreamSynchronize(p->st), "parse");
     return VN_OK;
