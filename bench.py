@@ -197,6 +197,61 @@ def c5_leg(args, rank):
                        "set_estimates_exact": bool(set_exact)}}
 
 
+def text_leg(args):
+    """SURVEY §8(f) rank 1 on the device: DogStatsD text already in HBM -> vn_intake_process (parse,
+    Upsert into the device key table, ProcessMetric staging, vn_ingest) -> vn_flush, one window of
+    text_passes buffers of text_lines lines; plus the parse alone (vn_parse_dogstatsd_device)."""
+    import ctypes as C
+
+    import veneur_amd as V
+    import veneur_amd._abi as A
+    from tools.parse_bench import make_buffer
+    from veneur_amd.intake import DeviceParser, Intake
+    buf = make_buffer(args.text_lines, n_keys=args.text_keys)
+    cap = 1 << max(10, (args.text_keys - 1).bit_length())
+    with V.Engine((cap,) * 4, percentiles=PCT, max_batch_records=args.text_lines) as e:
+        it = Intake(e, max_bytes=len(buf) + 1, max_lines=args.text_lines)
+        try:
+            A.lib.vn_copy_to_device(e.device, it.buf.ptr, C.c_char_p(buf), len(buf))
+            stats = []
+
+            def window():
+                stats.clear()
+                for _ in range(args.text_passes):
+                    stats.append(it.process_resident(len(buf)))
+                f = e.flush_raw()
+                it.reset()
+                return f
+            window()
+            A.lib.vn_device_synchronize(e.device)
+            t0 = time.perf_counter()
+            for _ in range(args.text_windows):
+                f = window()
+            A.lib.vn_device_synchronize(e.device)
+            ms = (time.perf_counter() - t0) * 1e3 / args.text_windows
+            processed = sum(s["processed"] for s in stats)
+            ok = processed == args.text_lines * args.text_passes and f.samples_processed == processed
+        finally:
+            it.close()
+    with DeviceParser(max_bytes=len(buf) + 1, max_lines=args.text_lines + 1) as p:
+        A.lib.vn_copy_to_device(0, p.buf.ptr, C.c_char_p(buf), len(buf))
+        p.parse_resident(len(buf))
+        A.lib.vn_device_synchronize(0)
+        t0 = time.perf_counter()
+        for _ in range(5):
+            p.parse_resident(len(buf))
+        A.lib.vn_device_synchronize(0)
+        pms = (time.perf_counter() - t0) * 1e3 / 5
+    lines = args.text_lines * args.text_passes
+    return {"config": "DogStatsD text in HBM: %d buffers of %d lines (%d bytes, %d keys, Zipf 1.3, 3 tags, C3 type "
+                      "mix) per window -> vn_intake_process -> vn_flush" % (args.text_passes, args.text_lines, len(buf),
+                                                                             args.text_keys),
+            "lines_per_s": lines / (ms * 1e-3), "ms_per_window": ms, "text_GBs": len(buf) * args.text_passes /
+            (ms * 1e-3) / 1e9, "parse_only_lines_per_s": args.text_lines / (pms * 1e-3),
+            "parse_only_ms_per_buffer": pms, "new_keys_first_buffer": stats[0]["new_keys"] if stats else 0,
+            "checks": {"every_line_processed": bool(ok)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -227,6 +282,11 @@ def main():
     ap.add_argument("--c5-distinct", type=int, default=8, help="distinct host windows, cycled")
     ap.add_argument("--c5-windows", type=int, default=1)
     ap.add_argument("--c5-parity-keys", type=int, default=16)
+    ap.add_argument("--text-lines", type=int, default=2_000_000,
+                    help="DogStatsD text intake leg (rank 0, N=1): lines per buffer (0: off)")
+    ap.add_argument("--text-passes", type=int, default=8, help="buffers per intake window")
+    ap.add_argument("--text-keys", type=int, default=100_000)
+    ap.add_argument("--text-windows", type=int, default=2)
     ap.add_argument("--split-delay-ms", type=float, default=0.0, help="development only: host delay after split_close")
     ap.add_argument("--host-trace", action="store_true",
                     help="development only: report host ms in split_keys+ingest_split / ingest / flush")
@@ -464,6 +524,10 @@ def main():
             t1 = time.time()
             result["c5"] = c5_leg(args, rank)
             log(rank, "[bench] C5 leg in %.1fs: %s" % (time.time() - t1, json.dumps(result["c5"])))
+        if args.text_lines > 0:
+            t1 = time.time()
+            result["text_intake"] = text_leg(args)
+            log(rank, "[bench] text intake leg in %.1fs: %s" % (time.time() - t1, json.dumps(result["text_intake"])))
         o = last
         npct = len(PCT)
         arr = lambda p, n, dt: np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, dt)

@@ -18,9 +18,9 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def make_buffer(n, seed=7):
+def make_buffer(n, seed=7, n_keys=1_000_000):
     rng = np.random.default_rng(seed)
-    keys = rng.zipf(1.3, n) % 1_000_000
+    keys = rng.zipf(1.3, n) % n_keys
     kind = keys % 20
     out = []
     for i in range(n):
