@@ -440,6 +440,56 @@ int vn_intake_read_keys(vn_intake* in, uint8_t* map, uint32_t* slot, uint32_t* n
                         uint32_t* name_len, uint32_t* tags_len, uint8_t* arena);
 int vn_intake_reset(vn_intake* in);
 
+/* ---------------------------------------------------------------- flush egress (host code)
+ * vn_datadog_flush: Server.Flush's metric output for the Datadog sink, natively from a flush result
+ * (csrc/sink.cpp): generateInterMetrics (flusher.go:168-230) with the is_local rules, the samplers'
+ * Flush (samplers.go:136-498: names, aggregates, "%s.%dpercentile"), finalizeMetrics
+ * (sinks/datadog/datadog.go:160-213: routing, counters as rates, sink tags, host:/device: tags),
+ * Flush's chunking (77-106) and each chunk's body as PostHelper encodes it before compression
+ * (http/http.go:116-135: json.NewEncoder.Encode({"series": chunk}), Go 1.9 encoding/json).  Keys:
+ * the window's MetricKeys as vn_intake_read_keys returns them (map id, slot, tag count, name and
+ * joined tags).  A chunk holding NaN or Inf cannot be encoded (UnsupportedValueError): its status
+ * is VN_EINVAL and its body empty, as Go posts nothing for it.  Output owned by the sink, valid
+ * until its next call. */
+typedef struct {
+  uint64_t n_keys;
+  const uint8_t* map;        /* 0..9: counters, global_counters, gauges, global_gauges, histograms,
+                                local_histograms, timers, local_timers, sets, local_sets */
+  const uint32_t* slot;
+  const uint32_t* n_tags;
+  const uint64_t* name_off;  /* into arena; the joined tags follow the name */
+  const uint32_t* name_len;
+  const uint32_t* tags_len;
+  const uint8_t* arena;
+} vn_keys;
+typedef struct {
+  double interval;                          /* flush interval in seconds (dd.interval) */
+  int64_t timestamp;                        /* InterMetric.Timestamp (Unix seconds) */
+  int32_t is_local;
+  uint32_t aggregates;                      /* HistogramAggregates.Value (samplers.go:60-68 bits) */
+  uint32_t n_percentiles;                   /* Server.HistogramPercentiles */
+  double percentiles[VN_MAX_PERCENTILES];
+  const double* engine_percentiles;         /* the flush result's quantile columns (vn_config order) */
+  const char* hostname;                     /* dd.hostname */
+  const char* sink_tags;                    /* dd.tags joined by ',' */
+  uint32_t n_sink_tags;
+  uint32_t flush_max_per_body;              /* dd.flushMaxPerBody */
+} vn_dd_config;
+typedef struct {
+  uint64_t n_intermetrics;   /* generateInterMetrics output */
+  uint64_t n_metrics;        /* DDMetrics after finalizeMetrics */
+  uint32_t n_bodies;
+  const uint64_t* body_off;  /* n_bodies + 1 offsets into bytes */
+  const int32_t* body_status;
+  const uint8_t* bytes;
+} vn_dd_payload;
+typedef struct vn_sink vn_sink;
+int vn_sink_create(vn_sink** out);
+void vn_sink_destroy(vn_sink* s);
+const char* vn_sink_last_error(const vn_sink* s);
+int vn_datadog_flush(vn_sink* s, const vn_flush_result* f, const vn_keys* keys, const vn_dd_config* cfg,
+                     vn_dd_payload* out);
+
 /* strconv.ParseFloat(s, bits) of Go 1.9 (bits 64 or 32) as the device parser computes it, run on
  * the host: 0 ok, 1 syntax error, 2 out of range (ErrRange); *out the value (float32 widened). */
 int vn_go_parse_float(const char* s, uint64_t n, int bits, double* out);

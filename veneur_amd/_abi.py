@@ -213,6 +213,29 @@ class IntakeInfo(C.Structure):  # vn_intake_info
     _fields_ = [("n_keys", C.c_uint64), ("arena_bytes", C.c_uint64), ("next_slot", C.c_uint32 * 4)]
 
 
+class Keys(C.Structure):  # vn_keys
+    _fields_ = [("n_keys", C.c_uint64), ("map", u8p), ("slot", u32p), ("n_tags", u32p), ("name_off", u64p),
+                ("name_len", u32p), ("tags_len", u32p), ("arena", u8p)]
+
+
+class DDConfig(C.Structure):  # vn_dd_config
+    _fields_ = [("interval", C.c_double), ("timestamp", C.c_int64), ("is_local", C.c_int32),
+                ("aggregates", C.c_uint32), ("n_percentiles", C.c_uint32),
+                ("percentiles", C.c_double * VN_MAX_PERCENTILES), ("engine_percentiles", f64p),
+                ("hostname", C.c_char_p), ("sink_tags", C.c_char_p), ("n_sink_tags", C.c_uint32),
+                ("flush_max_per_body", C.c_uint32)]
+
+
+class DDPayload(C.Structure):  # vn_dd_payload
+    _fields_ = [("n_intermetrics", C.c_uint64), ("n_metrics", C.c_uint64), ("n_bodies", C.c_uint32),
+                ("body_off", u64p), ("body_status", C.POINTER(C.c_int32)), ("bytes", u8p)]
+
+
+_sig("vn_sink_create", C.c_int, C.POINTER(vp))
+_sig("vn_sink_destroy", None, vp)
+_sig("vn_sink_last_error", C.c_char_p, vp)
+_sig("vn_datadog_flush", C.c_int, vp, C.POINTER(FlushResult), C.POINTER(Keys), C.POINTER(DDConfig),
+     C.POINTER(DDPayload))
 _sig("vn_intake_create", C.c_int, vp, C.c_uint64, C.c_uint64, C.POINTER(vp))
 _sig("vn_intake_destroy", None, vp)
 _sig("vn_intake_last_error", C.c_char_p, vp)
@@ -256,7 +279,7 @@ EXPORTED = [
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_parser_create", "vn_parser_destroy",
     "vn_parser_last_error", "vn_parse_dogstatsd_device", "vn_go_parse_float", "vn_intake_create", "vn_intake_destroy",
     "vn_intake_last_error", "vn_intake_process", "vn_intake_upsert", "vn_intake_keys_info", "vn_intake_read_keys",
-    "vn_intake_reset", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
+    "vn_intake_reset", "vn_sink_create", "vn_sink_destroy", "vn_sink_last_error", "vn_datadog_flush", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
     "vn_synth_device", "vn_synth_device_free", "vn_synth_key_counts",
     "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",

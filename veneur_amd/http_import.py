@@ -234,8 +234,8 @@ def _go_json_string(s: str) -> str:
             out.append("\\t")
         elif c < 0x20 or ch in "<>&" or c in (0x2028, 0x2029):
             out.append("\\u%04x" % c)
-        elif 0xD800 <= c <= 0xDFFF:  # a lone surrogate is not valid UTF-8: Go writes U+FFFD
-            out.append("�")
+        elif 0xD800 <= c <= 0xDFFF:  # a lone surrogate is not valid UTF-8: Go writes the \ufffd escape
+            out.append("\\ufffd")
         else:
             out.append(ch)
     out.append('"')

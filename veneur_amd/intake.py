@@ -226,18 +226,11 @@ def DeviceWorker(*args, intake_bytes=1 << 24, **kw):
             self.parse_errors += st["parse_errors"]
             return st
 
-        def flush(self, *a, **k):
-            self._drain()
+        def _take_window(self):
             win = _Window()
-            win.maps = self._win.maps
-            self._win = win
-            try:
-                return Worker.flush(self, *a, **k)
-            finally:
-                self.intake.reset()
-                self._win = _DeviceWindow(self.intake)
-
-        Flush = flush
+            win.maps = self._win.maps  # read back from the device key table
+            self.intake.reset()
+            return win
 
         def close(self):
             self.intake.close()

@@ -521,7 +521,7 @@ class Worker:
         those quantiles and estimates (vn_flush_masked); need_median keeps the quantiles, as
         Histo.Flush evaluates Quantile(0.5) for the median aggregate regardless."""
         self._drain()
-        win, self._win = self._win, _Window()
+        win = self._take_window()
         payload = {}
         if forward:
             for cls, names, fn in ((2, ("histograms", "timers"), self.engine.export_histos),
@@ -531,19 +531,51 @@ class Worker:
                     for s, p in zip(slots, fn(np.array(slots, np.uint32))):
                         payload[(cls, s)] = p
         if is_local:
-            qmask = np.zeros(self.capacity[2], np.uint8)
-            emask = np.zeros(self.capacity[3], np.uint8)
-            for names, mask, on in ((("local_histograms", "local_timers"), qmask, 1),
-                                    (("histograms", "timers"), qmask, 1 if need_median else 0),
-                                    (("local_sets",), emask, 1), (("sets",), emask, 0)):
-                for n in names:
-                    for s_, _ in win.maps[n].values():
-                        mask[s_] = on
+            qmask, emask = self._masks(win, need_median)
             f = self.engine.flush(histo_quantile_mask=qmask, set_estimate_mask=emask)
         else:
             f = self.engine.flush()
         self.processed = 0
         self.imported = 0
+        return self._worker_metrics(win, f, payload)
+
+    def _take_window(self):
+        """The map swap of Worker.Flush (worker.go:277-284): the window's interned keys, and a
+        fresh window."""
+        win, self._win = self._win, _Window()
+        return win
+
+    def _masks(self, win, need_median):
+        qmask = np.zeros(self.capacity[2], np.uint8)
+        emask = np.zeros(self.capacity[3], np.uint8)
+        for names, mask, on in ((("local_histograms", "local_timers"), qmask, 1),
+                                (("histograms", "timers"), qmask, 1 if need_median else 0),
+                                (("local_sets",), emask, 1), (("sets",), emask, 0)):
+            for n in names:
+                for s_, _ in win.maps[n].values():
+                    mask[s_] = on
+        return qmask, emask
+
+    def flush_datadog(self, sink, histogram_percentiles, aggregates: "HistogramAggregates" = None, is_local=False,
+                      timestamp=None):
+        """Worker.Flush, then the window's InterMetrics straight into the Datadog sink's request
+        bodies (veneur_amd.sink, vn_datadog_flush): generateInterMetrics (flusher.go:168-230) +
+        finalizeMetrics and chunking (sinks/datadog/datadog.go:77-106,160-213) + PostHelper's JSON
+        (http/http.go:116-135) in C++, with no per-key Python objects.  Returns ([(ok, body)],
+        (n_intermetrics, n_metrics))."""
+        aggregates = aggregates or DEFAULT_AGGREGATES
+        self._drain()
+        win = self._take_window()
+        if is_local:
+            qm, em = self._masks(win, bool(Aggregate(aggregates.value) & Aggregate.AggregateMedian))
+            f = self.engine.flush_raw(histo_quantile_mask=qm, set_estimate_mask=em)
+        else:
+            f = self.engine.flush_raw()
+        self.processed = 0
+        self.imported = 0
+        return sink.bodies(f, win.maps, self.percentiles, histogram_percentiles, aggregates, is_local, timestamp)
+
+    def _worker_metrics(self, win, f, payload):
         by_cls = [dict(zip(f.counter_slot.tolist(), f.counter_value.tolist())),
                   dict(zip(f.gauge_slot.tolist(), f.gauge_value.tolist())),
                   {int(s): i for i, s in enumerate(f.histo_slot)},
