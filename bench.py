@@ -252,6 +252,62 @@ def text_leg(args):
             "checks": {"every_line_processed": bool(ok)}}
 
 
+def egress_leg(flush_result):
+    """the C4 window's flush result -> InterMetrics -> Datadog request bodies
+    (vn_datadog_flush, native), every touched key named "c4.<class>.<slot>" with two tags."""
+    import veneur_amd._abi as A
+    from veneur_amd.sink import DatadogSink
+    from veneur_amd.worker import DEFAULT_AGGREGATES
+    arr = lambda p, n: np.ctypeslib.as_array(p, shape=(n,)).copy() if n else np.zeros(0, np.uint32)
+    parts = [(0, arr(flush_result.counter_slot, flush_result.n_counter), b"c"),
+             (2, arr(flush_result.gauge_slot, flush_result.n_gauge), b"g"),
+             (6, arr(flush_result.histo_slot, flush_result.n_histo), b"t"),
+             (8, arr(flush_result.set_slot, flush_result.n_set), b"s")]
+    mp, sl, names = [], [], []
+    for m, slots, tag in parts:
+        mp.append(np.full(len(slots), m, np.uint8))
+        sl.append(slots.astype(np.uint32))
+        names += [b"c4.%s.%d" % (tag, s) for s in slots.tolist()]
+    tags = [b"env:prod,host:h%d" % (i % 100) for i in range(len(names))]
+    blob = b"".join(n + t for n, t in zip(names, tags))
+    nlen = np.array([len(n) for n in names], np.uint32)
+    tlen = np.array([len(t) for t in tags], np.uint32)
+    noff = np.zeros(len(names), np.uint64)
+    if len(names):
+        noff[1:] = np.cumsum(nlen.astype(np.uint64) + tlen)[:-1]
+    mp, sl = np.concatenate(mp), np.concatenate(sl)
+    nt = np.full(len(names), 2, np.uint32)
+    bb = np.frombuffer(blob or b"\0", np.uint8)
+    keys = A.Keys(len(names), mp.ctypes.data_as(A.u8p), sl.ctypes.data_as(A.u32p), nt.ctypes.data_as(A.u32p),
+                  noff.ctypes.data_as(A.u64p), nlen.ctypes.data_as(A.u32p), tlen.ctypes.data_as(A.u32p),
+                  bb.ctypes.data_as(A.u8p))
+    sink = DatadogSink(10.0, "bench-host", ["dc:1"], 5000)
+    try:
+        import ctypes as C
+        cfg = A.DDConfig()
+        cfg.interval, cfg.timestamp, cfg.is_local, cfg.aggregates = 10.0, 1_700_000_000, 0, DEFAULT_AGGREGATES.value
+        cfg.n_percentiles = len(PCT)
+        for i, p in enumerate(PCT):
+            cfg.percentiles[i] = p
+        ep = np.array(PCT, np.float64)
+        cfg.engine_percentiles = ep.ctypes.data_as(A.f64p)
+        cfg.hostname, cfg.sink_tags, cfg.n_sink_tags, cfg.flush_max_per_body = b"bench-host", b"dc:1", 1, 5000
+        out = A.DDPayload()
+        t0 = time.perf_counter()
+        rc = A.lib.vn_datadog_flush(sink.h, C.byref(flush_result), C.byref(keys), C.byref(cfg), C.byref(out))
+        dt = time.perf_counter() - t0
+        assert rc == 0
+        nbytes = np.ctypeslib.as_array(out.body_off, shape=(out.n_bodies + 1,))[-1]
+        ok = int(np.ctypeslib.as_array(out.body_status, shape=(out.n_bodies,)).tolist().count(0))
+    finally:
+        sink.close()
+    return {"config": "the C4 window's flush result (%d keys) -> generateInterMetrics -> finalizeMetrics -> JSON "
+                      "bodies of <= 5000 series (vn_datadog_flush, one host core)" % len(names),
+            "intermetrics": int(out.n_intermetrics), "series": int(out.n_metrics), "bodies": int(out.n_bodies),
+            "bodies_encoded": ok, "body_MB": float(nbytes) / 1e6, "ms": dt * 1e3,
+            "intermetrics_per_s": out.n_intermetrics / dt}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -524,6 +580,9 @@ def main():
             t1 = time.time()
             result["c5"] = c5_leg(args, rank)
             log(rank, "[bench] C5 leg in %.1fs: %s" % (time.time() - t1, json.dumps(result["c5"])))
+        t1 = time.time()
+        result["egress"] = egress_leg(last)
+        log(rank, "[bench] egress leg in %.1fs: %s" % (time.time() - t1, json.dumps(result["egress"])))
         if args.text_lines > 0:
             t1 = time.time()
             result["text_intake"] = text_leg(args)

@@ -203,8 +203,8 @@ def test_gpu_worker_flush_datadog_matches_restatement(is_local):
     dg = b"\n".join(lines)
     pct = (0.5, 0.9, 0.99)
     hp = (0.9, 0.99)
-    a = W.Worker(capacity=(512,) * 4, percentiles=pct)
-    b = W.Worker(capacity=(512,) * 4, percentiles=pct)
+    a = W.Worker(capacity=(4096,) * 4, percentiles=pct)
+    b = W.Worker(capacity=(4096,) * 4, percentiles=pct)
     sink = DatadogSink(10.0, "myhost", ["dc:1"], 40)
     try:
         P.read_metric_datagram([a], dg)
