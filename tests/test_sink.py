@@ -218,3 +218,14 @@ def test_gpu_worker_flush_datadog_matches_restatement(is_local):
         sink.close()
         a.close()
         b.close()
+
+
+def test_large_window_threaded_byte_identical():
+    """Enough InterMetrics that the native builder splits them over host threads."""
+    rng = np.random.default_rng(77)
+    engine_pct = (0.5, 0.9, 0.99)
+    wm, maps, ff = window(rng, 20000, engine_pct)
+    got = native(ff, maps, engine_pct, (0.9, 0.99), ALL_AGG, False, 10.0, "h", ["a:b"], 700)
+    want = restated(wm, (0.9, 0.99), ALL_AGG, False, 10.0, "h", ["a:b"], 700)
+    assert got[1] == want[1] and got[1][0] > 50000
+    assert got[0] == want[0]

@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "veneur_amd.h"
@@ -177,11 +178,28 @@ struct Str {
 };
 
 struct InterMetric {  // samplers.go:45-56 (only what the Datadog sink reads)
-  std::string name;
+  uint64_t key;     // index into the key list (name, tags, route info)
   double value;
-  bool counter;  // CounterMetric, else GaugeMetric
-  uint64_t key;  // index into the key list (tags, route info)
+  bool counter;     // CounterMetric, else GaugeMetric
+  uint8_t suffix;   // name suffix: kNone or a Histo.Flush aggregate / percentile
+  int64_t pint;     // int(p*100) of a percentile
 };
+enum { kNone = 0, kSfxMax, kSfxMin, kSfxSum, kSfxAvg, kSfxCount, kSfxMedian, kSfxHmean, kSfxPct };
+const char* const kSuffix[] = {"", ".max", ".min", ".sum", ".avg", ".count", ".median", ".hmean"};
+
+// fn(lo, hi) over [0, n) in contiguous ranges on up to 16 host threads
+template <class F>
+void parallel_ranges(uint64_t n, F&& fn) {
+  const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const uint64_t t = std::min<uint64_t>(hw, std::max<uint64_t>(1, n / 4096));
+  if (t <= 1) {
+    fn(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (uint64_t i = 0; i < t; i++) th.emplace_back([&, i] { fn(n * i / t, n * (i + 1) / t); });
+  for (auto& x : th) x.join();
+}
 
 enum { kMax = 2, kMin = 1, kMedian = 4, kAvg = 8, kCount = 16, kSum = 32, kHmean = 64 };  // samplers.go:60-68
 
@@ -234,9 +252,6 @@ int vn_datadog_flush(vn_sink* sk, const vn_flush_result* f, const vn_keys* keys,
   for (uint64_t k = 0; k < keys->n_keys; k++)
     if (keys->map[k] <= 9) bymap[keys->map[k]].push_back(k);
   static const int kClass[10] = {0, 0, 1, 1, 2, 2, 2, 2, 3, 3};
-  auto name_of = [&](uint64_t k) {
-    return std::string(reinterpret_cast<const char*>(keys->arena + keys->name_off[k]), keys->name_len[k]);
-  };
   std::vector<InterMetric> im;
   std::vector<double> hp(cfg->percentiles, cfg->percentiles + cfg->n_percentiles);
   std::vector<double> none;
@@ -246,11 +261,11 @@ int vn_datadog_flush(vn_sink* sk, const vn_flush_result* f, const vn_keys* keys,
       const uint32_t s = keys->slot[k];
       const int64_t r = s < row[c].size() ? row[c][s] : -1;
       if (c == 0) {  // Counter.Flush: float64(value)
-        im.push_back({name_of(k), r < 0 ? 0.0 : (double)f->counter_value[r], true, k});
+        im.push_back({k, r < 0 ? 0.0 : (double)f->counter_value[r], true, kNone, 0});
       } else if (c == 1) {
-        im.push_back({name_of(k), r < 0 ? 0.0 : f->gauge_value[r], false, k});
+        im.push_back({k, r < 0 ? 0.0 : f->gauge_value[r], false, kNone, 0});
       } else if (c == 3) {  // Set.Flush: float64(Estimate()) as a gauge
-        im.push_back({name_of(k), r < 0 ? 0.0 : (double)f->set_estimate[r], false, k});
+        im.push_back({k, r < 0 ? 0.0 : (double)f->set_estimate[r], false, kNone, 0});
       } else {  // Histo.Flush
         double st[5] = {0.0, INFINITY, -INFINITY, 0.0, 0.0};
         if (r >= 0)
@@ -260,18 +275,17 @@ int vn_datadog_flush(vn_sink* sk, const vn_flush_result* f, const vn_keys* keys,
           const int col = qcol(p);
           return (r < 0 || col < 0) ? nan : f->histo_quantiles[r * f->n_percentiles + col];
         };
-        const std::string nm = name_of(k);
         const uint32_t a = cfg->aggregates;
-        if ((a & kMax) && !std::isinf(mx)) im.push_back({nm + ".max", mx, false, k});
-        if ((a & kMin) && !std::isinf(mn)) im.push_back({nm + ".min", mn, false, k});
-        if ((a & kSum) && sum != 0) im.push_back({nm + ".sum", sum, false, k});
-        if ((a & kAvg) && sum != 0 && W != 0) im.push_back({nm + ".avg", sum / W, false, k});
-        if ((a & kCount) && W != 0) im.push_back({nm + ".count", W, true, k});
-        if (a & kMedian) im.push_back({nm + ".median", q(0.5), false, k});
-        if ((a & kHmean) && rsum != 0 && W != 0) im.push_back({nm + ".hmean", W / rsum, false, k});
+        if ((a & kMax) && !std::isinf(mx)) im.push_back({k, mx, false, kSfxMax, 0});
+        if ((a & kMin) && !std::isinf(mn)) im.push_back({k, mn, false, kSfxMin, 0});
+        if ((a & kSum) && sum != 0) im.push_back({k, sum, false, kSfxSum, 0});
+        if ((a & kAvg) && sum != 0 && W != 0) im.push_back({k, sum / W, false, kSfxAvg, 0});
+        if ((a & kCount) && W != 0) im.push_back({k, W, true, kSfxCount, 0});
+        if (a & kMedian) im.push_back({k, q(0.5), false, kSfxMedian, 0});
+        if ((a & kHmean) && rsum != 0 && W != 0) im.push_back({k, W / rsum, false, kSfxHmean, 0});
         for (double p : *pct) {
           volatile double p100 = p * 100.0;  // int(p*100): one float64 multiply, truncated
-          im.push_back({nm + "." + std::to_string((long long)(double)p100) + "percentile", q(p), false, k});
+          im.push_back({k, q(p), false, kSfxPct, (int64_t)(double)p100});
         }
       }
     }
@@ -308,95 +322,125 @@ int vn_datadog_flush(vn_sink* sk, const vn_flush_result* f, const vn_keys* keys,
     }
   }
   const int32_t interval_i = (int32_t)cfg->interval;  // int32(dd.interval)
-  std::vector<std::string> objs;
-  std::vector<bool> finite;
-  objs.reserve(im.size());
-  std::vector<Str> tags;
-  for (const InterMetric& m : im) {
-    const uint64_t k = m.key;
-    tags.clear();
-    const uint8_t* tp = keys->arena + keys->name_off[k] + keys->name_len[k];
-    const size_t tn = keys->tags_len[k];
-    if (keys->n_tags[k]) {
-      size_t a = 0;
-      for (size_t i = 0; i <= tn; i++)
-        if (i == tn || tp[i] == ',') {
-          tags.push_back({tp + a, i - a});
-          a = i + 1;
-        }
-    }
-    // routeInfo (samplers.go:106-122) + IsAcceptableMetric (sinks/sinks.go:32-37)
-    bool routed = false, to_dd = false;
-    for (const Str& t : tags)
-      if (t.starts("veneursinkonly:")) {
-        routed = true;
-        if (t.n == 15 + 7 && memcmp(t.p + 15, "datadog", 7) == 0) to_dd = true;
+  // one JSON object per InterMetric the sink accepts, built in parallel
+  std::vector<std::string> objs(im.size());
+  std::vector<uint8_t> acc(im.size()), fin(im.size());
+  parallel_ranges(im.size(), [&](uint64_t lo, uint64_t hi) {
+    std::vector<Str> tags;
+    std::string tj, nm;
+    for (uint64_t idx = lo; idx < hi; idx++) {
+      const InterMetric& m = im[idx];
+      const uint64_t k = m.key;
+      tags.clear();
+      const uint8_t* tp = keys->arena + keys->name_off[k] + keys->name_len[k];
+      const size_t tn = keys->tags_len[k];
+      if (keys->n_tags[k]) {
+        size_t a = 0;
+        for (size_t i = 0; i <= tn; i++)
+          if (i == tn || tp[i] == ',') {
+            tags.push_back({tp + a, i - a});
+            a = i + 1;
+          }
       }
-    if (routed && !to_dd) continue;
-    const double v = m.counter ? m.value / cfg->interval : m.value;  // counters are rates
-    Str host{nullptr, 0}, device{nullptr, 0};
-    std::string o = "{\"metric\":";
-    json_string(o, reinterpret_cast<const uint8_t*>(m.name.data()), m.name.size());
-    o += ",\"points\":[[";
-    json_float(o, (double)cfg->timestamp);
-    o.push_back(',');
-    const bool ok = std::isfinite(v);
-    if (ok) json_float(o, v);
-    o += "]]";
-    size_t ntag = 0;
-    std::string tj;
-    for (const Str& t : sink_tags) {
-      if (ntag++) tj.push_back(',');
-      json_string(tj, t.p, t.n);
-    }
-    for (const Str& t : tags) {
-      if (t.starts("host:")) {
-        host = {t.p + 5, t.n - 5};
-      } else if (t.starts("device:")) {
-        device = {t.p + 7, t.n - 7};
-      } else {
+      // routeInfo (samplers.go:106-122) + IsAcceptableMetric (sinks/sinks.go:32-37)
+      bool routed = false, to_dd = false;
+      for (const Str& t : tags)
+        if (t.starts("veneursinkonly:")) {
+          routed = true;
+          if (t.n == 15 + 7 && memcmp(t.p + 15, "datadog", 7) == 0) to_dd = true;
+        }
+      if (routed && !to_dd) continue;
+      acc[idx] = 1;
+      nm.assign(reinterpret_cast<const char*>(keys->arena + keys->name_off[k]), keys->name_len[k]);
+      if (m.suffix == kSfxPct) nm += "." + std::to_string((long long)m.pint) + "percentile";
+      else nm += kSuffix[m.suffix];
+      const double v = m.counter ? m.value / cfg->interval : m.value;  // counters are rates
+      Str host{nullptr, 0}, device{nullptr, 0};
+      std::string& o = objs[idx];
+      o = "{\"metric\":";
+      json_string(o, reinterpret_cast<const uint8_t*>(nm.data()), nm.size());
+      o += ",\"points\":[[";
+      json_float(o, (double)cfg->timestamp);
+      o.push_back(',');
+      const bool ok = std::isfinite(v);
+      if (ok) json_float(o, v);
+      o += "]]";
+      size_t ntag = 0;
+      tj.clear();
+      for (const Str& t : sink_tags) {
         if (ntag++) tj.push_back(',');
         json_string(tj, t.p, t.n);
       }
+      for (const Str& t : tags) {
+        if (t.starts("host:")) {
+          host = {t.p + 5, t.n - 5};
+        } else if (t.starts("device:")) {
+          device = {t.p + 7, t.n - 7};
+        } else {
+          if (ntag++) tj.push_back(',');
+          json_string(tj, t.p, t.n);
+        }
+      }
+      if (ntag) o += ",\"tags\":[" + tj + "]";
+      o += m.counter ? ",\"type\":\"rate\"" : ",\"type\":\"gauge\"";
+      if (!host.p || host.n == 0) host = host_default;  // an empty host: tag leaves the default too
+      if (host.n) {
+        o += ",\"host\":";
+        json_string(o, host.p, host.n);
+      }
+      if (device.p && device.n) {
+        o += ",\"device_name\":";
+        json_string(o, device.p, device.n);
+      }
+      if (interval_i) o += ",\"interval\":" + std::to_string(interval_i);
+      o.push_back('}');
+      fin[idx] = ok;
     }
-    if (ntag) o += ",\"tags\":[" + tj + "]";
-    o += m.counter ? ",\"type\":\"rate\"" : ",\"type\":\"gauge\"";
-    if (!host.p || host.n == 0) host = host_default;  // an empty host: tag leaves the default too
-    if (host.n) {
-      o += ",\"host\":";
-      json_string(o, host.p, host.n);
-    }
-    if (device.p && device.n) {
-      o += ",\"device_name\":";
-      json_string(o, device.p, device.n);
-    }
-    if (interval_i) o += ",\"interval\":" + std::to_string(interval_i);
-    o.push_back('}');
-    objs.push_back(std::move(o));
-    finite.push_back(ok);
-  }
+  });
+  std::vector<uint64_t> sel;
+  sel.reserve(im.size());
+  for (uint64_t i = 0; i < im.size(); i++)
+    if (acc[i]) sel.push_back(i);
   // Flush's chunks (datadog.go:83-101): rounding-up division, every chunk under the limit
-  const int64_t n = (int64_t)objs.size(), mpb = cfg->flush_max_per_body;
+  const int64_t n = (int64_t)sel.size(), mpb = cfg->flush_max_per_body;
   const int64_t workers = (n - 1) / mpb + 1;  // Go: -1 / mpb == 0 -> one (empty) chunk
   const int64_t chunk = (n - 1) / workers + 1;
-  sk->bytes.clear();
-  sk->off.assign(1, 0);
-  sk->status.clear();
+  auto bounds = [&](int64_t w, int64_t* lo, int64_t* hi) {
+    *lo = std::min(n, w * chunk);
+    *hi = w < workers - 1 ? std::min(n, *lo + chunk) : n;
+  };
+  sk->off.assign(workers + 1, 0);
+  sk->status.assign(workers, VN_OK);
   for (int64_t w = 0; w < workers; w++) {
-    const int64_t lo = std::min(n, w * chunk), hi = w < workers - 1 ? std::min(n, lo + chunk) : n;
+    int64_t lo, hi;
+    bounds(w, &lo, &hi);
     bool good = true;
-    for (int64_t i = lo; i < hi; i++) good = good && finite[i];
-    if (good) {
-      sk->bytes += "{\"series\":[";
-      for (int64_t i = lo; i < hi; i++) {
-        if (i > lo) sk->bytes.push_back(',');
-        sk->bytes += objs[i];
-      }
-      sk->bytes += "]}\n";
+    uint64_t sz = 11 + 3;  // {"series":[ ... ]}\n
+    for (int64_t i = lo; i < hi; i++) {
+      good = good && fin[sel[i]];
+      sz += objs[sel[i]].size() + (i > lo ? 1 : 0);
     }
-    sk->off.push_back(sk->bytes.size());
-    sk->status.push_back(good ? VN_OK : VN_EINVAL);  // json: unsupported value: NaN / +Inf / -Inf
+    sk->status[w] = good ? VN_OK : VN_EINVAL;  // json: unsupported value: NaN / +Inf / -Inf
+    sk->off[w + 1] = sk->off[w] + (good ? sz : 0);
   }
+  sk->bytes.resize(sk->off[workers]);
+  parallel_ranges((uint64_t)workers, [&](uint64_t wlo, uint64_t whi) {
+    for (uint64_t w = wlo; w < whi; w++) {
+      if (sk->status[w] != VN_OK) continue;
+      int64_t lo, hi;
+      bounds((int64_t)w, &lo, &hi);
+      char* d = &sk->bytes[0] + sk->off[w];
+      memcpy(d, "{\"series\":[", 11);
+      d += 11;
+      for (int64_t i = lo; i < hi; i++) {
+        if (i > lo) *d++ = ',';
+        const std::string& o = objs[sel[i]];
+        memcpy(d, o.data(), o.size());
+        d += o.size();
+      }
+      memcpy(d, "]}\n", 3);
+    }
+  });
   out->n_intermetrics = im.size();
   out->n_metrics = (uint64_t)n;
   out->n_bodies = (uint32_t)workers;
