@@ -320,8 +320,11 @@ def main():
                     help="split a counter/timer key above samples / (N * hot_div) per window")
     ap.add_argument("--set-hot", type=int, default=1 << 18, help="split a set key above this many records")
     ap.add_argument("--max-split", type=int, default=64, help="split keys per class at most")
-    ap.add_argument("--no-split", action="store_true", help="route every key by digest % N (no hot keys)")
+    ap.add_argument("--no-split", action="store_true", help="route every key by digest %% N (no hot keys)")
     ap.add_argument("--exact-threshold", type=int, default=0)
+    ap.add_argument("--hot-prefix", type=int, default=0,
+                    help="exact window prefix of keys past 4x the exact threshold (0: the engine's default)")
+    ap.add_argument("--piece-growth", type=int, default=0, help="geometric piece growth in %% (0: default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0: min(16, cpus))")
     ap.add_argument("--parity-keys", type=int, default=3000, help="histo keys sampled for the rank-error check")
@@ -379,7 +382,8 @@ def main():
     eng = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,
                    max_batch_records=max(stream.counts) + 1,
                    max_batch_member_bytes=stream.counts[3] * 11 + 64, device=local_rank,
-                   exact_threshold=args.exact_threshold, split_max_records=max(stream.split_counts) + 1)
+                   exact_threshold=args.exact_threshold, hot_prefix=args.hot_prefix, piece_growth=args.piece_growth,
+                   split_max_records=max(stream.split_counts) + 1)
     if comm is not None:
         eng.set_comm(comm)
     split_lists = []
