@@ -63,7 +63,8 @@ def key_classes(seed, n_keys, mix=(0.4, 0.2, 0.25, 0.15)):
 
 
 def rank_error_stats(d, slots, eng_q, ref_q):
-    """|F(q_engine) - F(q_ref)| with F the exact weighted empirical CDF of the key's samples."""
+    """|F(q_engine) - F(q_ref)| with F the exact weighted empirical CDF of the key's samples; and
+    each side's distance from the exact quantile, |F(q) - p| (SURVEY §8(d) accuracy metrics)."""
     want = np.zeros(int(d["h_slot"].max()) + 1 if len(d["h_slot"]) else 1, bool)
     want[slots] = True
     m = want[d["h_slot"]]
@@ -75,6 +76,8 @@ def rank_error_stats(d, slots, eng_q, ref_q):
     lo = np.searchsorted(ss, slots, side="left")
     hi = np.searchsorted(ss, slots, side="right")
     errs = np.zeros((len(slots), len(PCT)))
+    acc_e = np.zeros((len(slots), len(PCT)))
+    acc_r = np.zeros((len(slots), len(PCT)))
     for j in range(len(slots)):
         a, b = lo[j], hi[j]
         base = cw[a - 1] if a > 0 else 0.0
@@ -86,7 +89,9 @@ def rank_error_stats(d, slots, eng_q, ref_q):
             Fe = ((cw[a + fe - 1] - base) / tot) if fe else 0.0
             Fr = ((cw[a + fr - 1] - base) / tot) if fr else 0.0
             errs[j, k] = abs(Fe - Fr)
-    return errs
+            acc_e[j, k] = abs(Fe - PCT[k])
+            acc_r[j, k] = abs(Fr - PCT[k])
+    return errs, acc_e, acc_r
 
 
 def c5_leg(args, rank):
@@ -623,7 +628,7 @@ def main():
         pick = np.array(sorted(split_h | big | set(rng.choice(h_slot, min(args.parity_keys, len(h_slot)),
                                                               replace=False).tolist())), np.uint32)
         idx = np.searchsorted(h_slot, pick)
-        errs = rank_error_stats(d, pick, h_q[idx], ref["histo_q"][pick])
+        errs, acc_e, acc_r = rank_error_stats(d, pick, h_q[idx], ref["histo_q"][pick])
         par["rank_error_keys"] = int(len(pick))
         par["rank_error_max"] = {("p%g" % (100 * p)): float(errs[:, k].max()) for k, p in enumerate(PCT)}
         par["rank_error_mean"] = {("p%g" % (100 * p)): float(errs[:, k].mean()) for k, p in enumerate(PCT)}
@@ -633,10 +638,25 @@ def main():
                 par["rank_error_max_%s_keys" % name] = {("p%g" % (100 * p)): float(errs[m, k].max())
                                                         for k, p in enumerate(PCT)}
                 par["%s_keys" % name] = int(m.sum())
+        # keys past the threshold: how far each side is from the key's exact quantile, |F(q) - p|
+        # (the reference's sequential 42-sample merge is itself an approximation); and for the
+        # keys whose rank error passes 1e-3, which side is nearer the exact quantile
+        mb = np.isin(pick, list(big))
+        if mb.any():
+            pk = lambda a, f: {("p%g" % (100 * p)): float(f(a[mb, k])) for k, p in enumerate(PCT)}
+            over = errs[mb] > 1e-3
+            par["accuracy_vs_exact_quantile_past_threshold"] = {
+                "engine_max": pk(acc_e, np.max), "reference_max": pk(acc_r, np.max),
+                "engine_mean": pk(acc_e, np.mean), "reference_mean": pk(acc_r, np.mean),
+                "quantiles_with_rank_error_over_1e-3": int(over.sum()),
+                "of_those_engine_nearer_exact": int((acc_e[mb][over] < acc_r[mb][over]).sum())}
         worst = np.argsort(-errs.max(axis=1))[:8]
         par["rank_error_worst_keys"] = [{"slot": int(pick[i]), "samples": int(cnt[pick[i]]),
                                          "split": int(pick[i]) in split_h,
-                                         "err": [round(float(x), 7) for x in errs[i]]} for i in worst]
+                                         "err": [round(float(x), 7) for x in errs[i]],
+                                         "engine_vs_exact": [round(float(x), 7) for x in acc_e[i]],
+                                         "reference_vs_exact": [round(float(x), 7) for x in acc_r[i]]}
+                                        for i in worst]
         par["quantiles_bit_exact_frac"] = float(np.mean(np.all(h_q == ref["histo_q"][h_slot], axis=1)))
         result["p99_rank_error"] = par["rank_error_max"]["p99"]
         result["parity"] = par
