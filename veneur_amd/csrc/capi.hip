@@ -524,6 +524,11 @@ void validate_device_batch(vn_engine* e, const vn_batch* b) {
   if (f & kBadOffsets) throw std::invalid_argument("set member offsets must be non-decreasing");
 }
 
+#ifndef VN_SETS_FIRST
+#define VN_SETS_FIRST 0
+#endif
+constexpr bool kSetsFirst = VN_SETS_FIRST;  // side-stream order (compile-time A/B, tools/ab_variant.sh)
+
 void ingest_device(vn_engine* e, const vn_batch* b) {
   histo_imports_drain(e);  // imports that came first merge first
   if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
@@ -564,11 +569,17 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
     // the side work -- it fills the GPU while the replays and remainder rounds run
     side_begin(e);  // the side stream waits for what the main stream held before this call
     const HistoGroups g = histo_group(e, b->n_histo, b->histo_slot, b->histo_value, b->histo_rate);
-    ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
-    ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
-    e->set_defer = true;  // histo_process queues the set merge after the remainder sort
-    ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
-    e->set_defer = false;
+    if (kSetsFirst) {  // the whole set path first: its long per-key merges overlap everything else
+      ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
+      ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
+      ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
+    } else {
+      ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
+      ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
+      e->set_defer = true;  // histo_process queues the set merge after the remainder sort
+      ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
+      e->set_defer = false;
+    }
     histo_process(e, b->n_histo, g);
     set_finish(e);
     side_join(e);

@@ -44,7 +44,54 @@ struct SetCtx {
   uint32_t* tmp;
   uint32_t* arena;
   uint32_t* err;
+  uint32_t skip_small;  // keys k_set_small took (sparse, no mergeSparse trigger possible) are skipped
+  uint32_t* bt;         // touched flags: k_set_small marks the keys it took with 2
 };
+
+// A key that stays sparse and cannot reach a mergeSparse trigger in this batch (tmpSet codes +
+// batch records < 164): Insert only adds the batch's new codes to the tmpSet (hyperloglog.go:
+// 186-200), in arrival order as k_set_segments stores them.  One wave per key, 2.6 KiB of LDS,
+// instead of a 256-thread workgroup holding 70 KiB: the Zipf tail -- half the keys of a C4
+// window -- no longer waits for the heavy kernel's two workgroups per CU.
+__device__ __forceinline__ bool set_small(uint8_t mode, uint32_t tc, uint32_t n) {
+  return mode == 0 && tc + n < kHllTmpTrigger;
+}
+
+__global__ __launch_bounds__(256) void k_set_small(SetCtx x) {
+  __shared__ uint32_t s_old[4][kHllTmpTrigger];
+  __shared__ uint32_t s_rec[4][kHllTmpTrigger];
+  const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + w;
+  if (i >= *x.cnt) return;
+  const uint32_t slot = (uint32_t)x.order[i];
+  const uint32_t lo = x.start[slot], n = x.end[slot] - lo;
+  const uint32_t tc = x.tc[slot];
+  if (!set_small(x.mode[slot], tc, n)) return;
+  uint32_t* tmp = x.tmp + (uint64_t)slot * kTmpCap;
+  for (uint32_t j = lane; j < tc; j += 64) s_old[w][j] = tmp[j];
+  for (uint32_t j = lane; j < n; j += 64) s_rec[w][j] = (uint32_t)x.R[lo + j];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  uint32_t add = tc;
+  for (uint32_t g = 0; g < n; g += 64) {
+    const uint32_t p = g + lane;
+    bool fresh = false;
+    uint32_t c = 0;
+    if (p < n) {
+      c = s_rec[w][p];
+      fresh = true;
+      for (uint32_t j = 0; j < tc && fresh; j++) fresh = s_old[w][j] != c;
+      for (uint32_t j = 0; j < p && fresh; j++) fresh = s_rec[w][j] != c;
+    }
+    const uint64_t bal = __ballot(fresh);
+    if (fresh) tmp[add + (uint32_t)__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = c;
+    add += (uint32_t)__popcll(bal);
+  }
+  if (lane == 0) {
+    x.tc[slot] = add;
+    x.bt[slot] = 2;  // taken: k_set_segments skips it (its tc no longer shows that it was small)
+  }
+}
 
 __global__ void k_set_keys(uint64_t n, const uint32_t* __restrict__ slot, const uint32_t* __restrict__ off,
                            const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ hashes,
@@ -318,7 +365,9 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
 __global__ __launch_bounds__(kBlock) void k_set_segments(SetCtx x) {
   const uint32_t i = blockIdx.x;
   if (i >= *x.cnt) return;
-  set_segment(x, x.order ? (uint32_t)x.order[i] : x.tl[i]);
+  const uint32_t slot = x.order ? (uint32_t)x.order[i] : x.tl[i];
+  if (x.skip_small && x.bt[slot] == 2) return;
+  set_segment(x, slot);
 }
 
 // longest-first order: key = (0xFFFFF - min(records, 0xFFFFF)) << 32 | slot; untouched -> ~0
@@ -399,6 +448,8 @@ void set_replay_ranges(vn_engine* e, const uint64_t* R, const uint32_t* dev_coun
   x.tmp = e->stmp;
   x.arena = e->sarena;
   x.err = e->h_err;
+  x.skip_small = 0;
+  x.bt = nullptr;
   hipLaunchKernelGGL(k_set_segments, dim3(grid), dim3(kBlock), 0, st, x);
 }
 
@@ -426,8 +477,13 @@ void set_finish(vn_engine* e) {
   x.tmp = e->stmp;
   x.arena = e->sarena;
   x.err = e->h_err;
+  x.skip_small = order ? 1u : 0u;
+  x.bt = e->s_bt;
   hipEvent_t ea = e->timing ? e->pool_ss.next() : nullptr, eb = e->timing ? e->pool_ss.next() : nullptr;
   if (ea && eb) VN_HIP_CHECK(hipEventRecord(ea, st));
+  // the small keys (the tail of the longest-first order) take one wave each; the heavy kernel,
+  // queued behind, skips them -- both kernels only read the state that decides which runs a key
+  if (order) hipLaunchKernelGGL(k_set_small, dim3(blocks_for(grid, 4)), dim3(256), 0, st, x);
   hipLaunchKernelGGL(k_set_segments, dim3(grid), dim3(kBlock), 0, st, x);
   if (ea && eb) VN_HIP_CHECK(hipEventRecord(eb, st));
   if (e->timing) {
