@@ -114,6 +114,23 @@ __global__ void k_set_seg_mark(uint64_t n, const uint64_t* __restrict__ R, uint3
   if (i == n - 1 || (uint32_t)(R[i + 1] >> 32) != s) end[s] = (uint32_t)(i + 1);
 }
 
+#ifdef VN_SET_PROF
+// profiling build only (tools/set_profile.py): k_set_segments cycles per phase, summed over
+// workgroups: 0 setup, 1 sparse scan, 2 sparse merge, 3 toNormal, 4 dense, 5 write-back,
+// 6 triggers, 7 heavy keys, 8 records of heavy keys, 9 whole workgroups
+__device__ unsigned long long g_set_prof[16];
+#define SPROF_T(v) const long long v = clock64()
+#define SPROF_ADD(i, a, b) \
+  if (threadIdx.x == 0) atomicAdd(&g_set_prof[i], (unsigned long long)((b) - (a)))
+#define SPROF_INC(i, v) \
+  if (threadIdx.x == 0) atomicAdd(&g_set_prof[i], (unsigned long long)(v))
+#else
+#define SPROF_T(v)
+#define SPROF_ADD(i, a, b)
+#define SPROF_INC(i, v)
+#endif
+
+constexpr uint32_t kScanStage = 256;  // records staged in LDS per scan window (a trigger needs ~170)
 constexpr uint32_t kHashSlots = 512;  // LDS open-addressing table for the tmpSet (<= 163 codes)
 
 __device__ __forceinline__ uint32_t hslot(uint32_t c) { return (c * 2654435761u) >> 23; }  // 9 bits
@@ -154,12 +171,16 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
   __shared__ uint32_t s_tmp[256];       // tmpSet codes in insertion order, then sorted
   __shared__ uint32_t s_new[256];       // tmp codes not yet in the list (sorted)
   __shared__ uint32_t s_red[4];
+  __shared__ uint32_t s_rec[kScanStage];  // the records of the current scan window
   __shared__ uint32_t s_pos, s_trig, s_tc, s_lc, s_mode, s_b, s_nz;
   __shared__ uint32_t s_filled, s_tfull, s_pstar, s_newfill, s_min;
 
+  SPROF_T(p_begin);
   const uint32_t t = threadIdx.x;
   const uint32_t lo = x.start[slot], n = x.end[slot] - lo;
   const uint64_t* R = x.R + lo;
+  SPROF_INC(7, 1);
+  SPROF_INC(8, n);
   uint32_t* arena = x.arena + (uint64_t)slot * kArenaWords;
   uint8_t* regs8 = reinterpret_cast<uint8_t*>(arena);
 
@@ -174,6 +195,8 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
   lds_barrier();
   bool list_in_lds = false, list_dirty = false;
   uint32_t lbytes = x.lb[slot];
+  SPROF_T(p_setup);
+  SPROF_ADD(0, p_begin, p_setup);
 
   if (s_mode == 0) {
     // ------------------------------------------------------------ sparse phase
@@ -190,16 +213,21 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
     }
     lds_barrier();
     while (s_pos < n && s_mode == 0) {
+      SPROF_T(p_scan0);
+      // the next kScanStage records go to LDS in one coalesced load by the whole workgroup
+      const uint32_t wbase = s_pos, wend = min(n, wbase + kScanStage);
+      for (uint32_t i = t; i < wend - wbase; i += kBlock) s_rec[i] = (uint32_t)R[wbase + i];
+      lds_barrier();
       // wave 0 advances to the next mergeSparse trigger -- the record that makes the tmpSet
       // hold kHllTmpTrigger distinct codes -- 64 records per step: a record counts if its
       // code is neither in the tmpSet nor held by a lower lane of the same step.
       if (t < 64) {
-        uint32_t pos = s_pos, tc = s_tc, trig = 0;
+        uint32_t pos = wbase, tc = s_tc, trig = 0;
         const uint64_t below = (t == 0) ? 0ull : (~0ull >> (64 - t));
-        while (pos < n) {
+        while (pos < wend) {
           const uint32_t p = pos + t;
-          const bool valid = p < n;
-          const uint32_t c = valid ? (uint32_t)R[p] : kHllNoCode;
+          const bool valid = p < wend;
+          const uint32_t c = valid ? s_rec[p - wbase] : kHllNoCode;
           const bool fresh = valid && !hash_contains(s_hash, c);
           uint32_t hi = 0;
           if (fresh) {
@@ -221,25 +249,36 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
           }
           if (first && t < take) s_tmp[tc + (uint32_t)__popcll(bal & below)] = c;
           tc += add;
-          pos += take;
+          pos = min(pos + take, wend);
           if (trig) break;
         }
         if (t == 0) {
-          s_pos = min(pos, n);
+          s_pos = pos;
           s_tc = tc;
           s_trig = trig;
         }
       }
       lds_barrier();
-      if (!s_trig) break;
+      SPROF_T(p_scan1);
+      SPROF_ADD(1, p_scan0, p_scan1);
+      if (!s_trig) continue;  // window done without a trigger: the next window, or the end
+      SPROF_INC(6, 1);
       // mergeSparse: sorted union of the list and the tmpSet
       if (!list_in_lds) {
         for (uint32_t i = t; i < s_lc; i += kBlock) U[i] = arena[i];
         list_in_lds = true;
       }
-      if (t >= kHllTmpTrigger) s_tmp[t] = kHllNoCode;
+      // the full tmpSet (kHllTmpTrigger distinct codes) sorted by rank: one pass, two barriers
+      {
+        uint32_t mine = 0, rk = 0;
+        if (t < kHllTmpTrigger) {
+          mine = s_tmp[t];
+          for (uint32_t j = 0; j < kHllTmpTrigger; j++) rk += s_tmp[j] < mine ? 1u : 0u;
+        }
+        lds_barrier();
+        if (t < kHllTmpTrigger) s_tmp[rk] = mine;
+      }
       lds_barrier();
-      bitonic256(s_tmp);
       const uint32_t lc = s_lc;
       uint32_t isnew = 0, lb = 0, code = 0;
       if (t < kHllTmpTrigger) {
@@ -260,15 +299,18 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
       lds_barrier();
       // move list elements up by the number of new codes below them
       constexpr int kPer = (kArenaWords + kBlock - 1) / kBlock;
+      const int jmax = (int)((lc + kBlock - 1) / kBlock);  // rows of the list (uniform)
       uint32_t keep[kPer];
 #pragma unroll
       for (int j = 0; j < kPer; j++) {
+        if (j >= jmax) break;
         uint32_t i = t + j * kBlock;
         keep[j] = i < lc ? U[i] : 0u;
       }
       lds_barrier();
 #pragma unroll
       for (int j = 0; j < kPer; j++) {
+        if (j >= jmax) break;
         uint32_t i = t + j * kBlock;
         if (i < lc) U[i + lower_bound_u32(s_new, nnew, keep[j])] = keep[j];
       }
@@ -290,6 +332,8 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
         s_first[i] = 0xffffffffu;
       }
       lds_barrier();
+      SPROF_T(p_merge1);
+      SPROF_ADD(2, p_scan1, p_merge1);
       if (bytes > kHllM) {
         // toNormal: registers from the merged list (b stays; nz > 0 so no rebase can occur)
 #pragma unroll
@@ -320,11 +364,14 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
         list_in_lds = false;
         list_dirty = false;
         lds_barrier();
+        SPROF_T(p_norm1);
+        SPROF_ADD(3, p_merge1, p_norm1);
       }
     }
     lds_barrier();
     if (s_mode == 0) {
       // write back the sparse state
+      SPROF_T(p_wb0);
       const uint32_t tc = s_tc;
       if (t < tc) x.tmp[(uint64_t)slot * kTmpCap + t] = s_tmp[t];
       if (list_dirty)
@@ -335,6 +382,9 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
         x.lb[slot] = lbytes;
         if (list_dirty && s_lc) x.last[slot] = U[s_lc - 1];
       }
+      SPROF_T(p_wb1);
+      SPROF_ADD(5, p_wb0, p_wb1);
+      SPROF_ADD(9, p_begin, p_wb1);
       return;
     }
   } else {
@@ -344,11 +394,14 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
   }
 
   // -------------------------------------------------------------- dense phase
+  SPROF_T(p_dense0);
   {
     const DenseLds S{U, &s_b, &s_nz, &s_filled, &s_tfull, &s_pstar, &s_newfill, &s_min, s_red};
     dense_insert_codes(S, [R](uint32_t p) { return (uint32_t)R[p]; }, s_pos, n, x.err);
   }
   lds_barrier();
+  SPROF_T(p_dense1);
+  SPROF_ADD(4, p_dense0, p_dense1);
   for (uint32_t i = t; i < kHllM; i += kBlock) regs8[i] = (uint8_t)U[i];
   if (t == 0) {
     x.mode[slot] = 1;
@@ -358,6 +411,9 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
     x.lc[slot] = 0;
     x.lb[slot] = 0;
   }
+  SPROF_T(p_end);
+  SPROF_ADD(5, p_dense1, p_end);
+  SPROF_ADD(9, p_begin, p_end);
 }
 
 // One workgroup per touched key; with an order, workgroup i takes the key with the i-th most
@@ -493,4 +549,14 @@ void set_finish(vn_engine* e) {
   hipLaunchKernelGGL(k_set_clear_flags, dim3(blocks_for(nk, 256)), dim3(256), 0, st, e->s_cnt, e->s_tl, e->s_bt);
 }
 
+#ifdef VN_SET_PROF
+extern "C" int vn_prof_set_read(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_set_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_set_prof), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 }  // namespace vn
