@@ -130,7 +130,7 @@ __device__ unsigned long long g_set_prof[16];
 #define SPROF_INC(i, v)
 #endif
 
-constexpr uint32_t kScanStage = 256;  // records staged in LDS per scan window (a trigger needs ~170)
+constexpr uint32_t kScanStage = 1024;  // records staged in LDS per scan window (a trigger needs ~170)
 constexpr uint32_t kHashSlots = 512;  // LDS open-addressing table for the tmpSet (<= 163 codes)
 
 __device__ __forceinline__ uint32_t hslot(uint32_t c) { return (c * 2654435761u) >> 23; }  // 9 bits
@@ -170,9 +170,10 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
   __shared__ uint32_t s_first[kHashSlots];  // lowest lane of the current group holding the entry
   __shared__ uint32_t s_tmp[256];       // tmpSet codes in insertion order, then sorted
   __shared__ uint32_t s_new[256];       // tmp codes not yet in the list (sorted)
+  __shared__ uint32_t s_lbs[256];       // their insertion points in the old list
   __shared__ uint32_t s_red[4];
   __shared__ uint32_t s_rec[kScanStage];  // the records of the current scan window
-  __shared__ uint32_t s_pos, s_trig, s_tc, s_lc, s_mode, s_b, s_nz;
+  __shared__ uint32_t s_pos, s_trig, s_tc, s_lc, s_mode, s_b, s_nz, s_wbase, s_wend;
   __shared__ uint32_t s_filled, s_tfull, s_pstar, s_newfill, s_min;
 
   SPROF_T(p_begin);
@@ -191,6 +192,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
     s_tc = x.tc[slot];
     s_lc = x.lc[slot];
     s_pos = 0;
+    s_wbase = s_wend = 0;  // no window staged
   }
   lds_barrier();
   bool list_in_lds = false, list_dirty = false;
@@ -214,15 +216,24 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
     lds_barrier();
     while (s_pos < n && s_mode == 0) {
       SPROF_T(p_scan0);
-      // the next kScanStage records go to LDS in one coalesced load by the whole workgroup
-      const uint32_t wbase = s_pos, wend = min(n, wbase + kScanStage);
-      for (uint32_t i = t; i < wend - wbase; i += kBlock) s_rec[i] = (uint32_t)R[wbase + i];
+      // the records are staged in LDS kScanStage at a time by the whole workgroup (coalesced);
+      // a window serves the scans of several triggers
+      if (s_pos >= s_wend) {
+        const uint32_t b0 = s_pos, e0 = min(n, b0 + kScanStage);
+        for (uint32_t i = t; i < e0 - b0; i += kBlock) s_rec[i] = (uint32_t)R[b0 + i];
+        lds_barrier();
+        if (t == 0) {
+          s_wbase = b0;
+          s_wend = e0;
+        }
+      }
       lds_barrier();
+      const uint32_t wbase = s_wbase, wend = s_wend;
       // wave 0 advances to the next mergeSparse trigger -- the record that makes the tmpSet
       // hold kHllTmpTrigger distinct codes -- 64 records per step: a record counts if its
       // code is neither in the tmpSet nor held by a lower lane of the same step.
       if (t < 64) {
-        uint32_t pos = wbase, tc = s_tc, trig = 0;
+        uint32_t pos = s_pos, tc = s_tc, trig = 0;
         const uint64_t below = (t == 0) ? 0ull : (~0ull >> (64 - t));
         while (pos < wend) {
           const uint32_t p = pos + t;
@@ -295,32 +306,65 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
       for (int i = 0; i < w; i++) before += s_red[i];
       const uint32_t nnew = s_red[0] + s_red[1] + s_red[2] + s_red[3];
       uint32_t rank = before + (uint32_t)__popcll(bal & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
-      if (isnew) s_new[rank] = code;
+      // the list around each new code (before anything moves): its neighbours in the old list
+      const uint32_t predS = (isnew && lb > 0) ? U[lb - 1] : 0u;
+      const uint32_t succS = (isnew && lb < lc) ? U[lb] : 0u;
+      if (isnew) {
+        s_new[rank] = code;
+        s_lbs[rank] = lb;
+      }
       lds_barrier();
-      // move list elements up by the number of new codes below them
+      // varint byte length of the delta-encoded list, updated around the insertions: a new code
+      // adds its delta from its predecessor in the merged list, and the last new code of a gap
+      // changes the delta of the old element after it (the first delta is from 0)
+      uint32_t dbytes = 0;
+      if (isnew) {
+        const bool prev_same = rank > 0 && s_lbs[rank - 1] == lb;
+        const uint32_t predM = prev_same ? s_new[rank - 1] : predS;
+        dbytes = varint_len(code - predM);
+        const bool last_in_gap = !(rank + 1 < nnew && s_lbs[rank + 1] == lb);
+        if (last_in_gap && lb < lc) dbytes += varint_len(succS - code) - varint_len(succS - predS);
+      }
+      // move list elements up by the number of new codes below them: thread t moves the
+      // contiguous rows [t*jmax, (t+1)*jmax), walking the insertion points alongside
       constexpr int kPer = (kArenaWords + kBlock - 1) / kBlock;
-      const int jmax = (int)((lc + kBlock - 1) / kBlock);  // rows of the list (uniform)
+      const int jmax = (int)((lc + kBlock - 1) / kBlock);  // list elements per thread (uniform)
+      const uint32_t i0 = t * (uint32_t)jmax;
       uint32_t keep[kPer];
 #pragma unroll
       for (int j = 0; j < kPer; j++) {
         if (j >= jmax) break;
-        uint32_t i = t + j * kBlock;
+        const uint32_t i = i0 + (uint32_t)j;
         keep[j] = i < lc ? U[i] : 0u;
       }
+      uint32_t r = 0;  // new codes inserted at or before i0
+      {
+        uint32_t l = 0, h = nnew;
+        while (l < h) {
+          const uint32_t m = (l + h) >> 1;
+          if (s_lbs[m] <= i0) l = m + 1;
+          else h = m;
+        }
+        r = l;
+      }
+      uint32_t nextlb = r < nnew ? s_lbs[r] : 0xffffffffu;
       lds_barrier();
 #pragma unroll
       for (int j = 0; j < kPer; j++) {
         if (j >= jmax) break;
-        uint32_t i = t + j * kBlock;
-        if (i < lc) U[i + lower_bound_u32(s_new, nnew, keep[j])] = keep[j];
+        const uint32_t i = i0 + (uint32_t)j;
+        if (i < lc) {
+          while (nextlb <= i) {
+            r++;
+            nextlb = r < nnew ? s_lbs[r] : 0xffffffffu;
+          }
+          U[i + r] = keep[j];
+        }
       }
       if (isnew) U[lb + rank] = code;
       lds_barrier();
       const uint32_t nlc = lc + nnew;
-      // varint byte length of the delta-encoded list
-      uint32_t bytes = 0;
-      for (uint32_t i = t; i < nlc; i += kBlock) bytes += varint_len(U[i] - (i ? U[i - 1] : 0u));
-      bytes = block_allreduce_u32_sum(bytes, s_red);
+      const uint32_t bytes = lbytes + block_allreduce_u32_sum(dbytes, s_red);
       lbytes = bytes;
       list_dirty = true;
       if (t == 0) {
