@@ -517,6 +517,31 @@ __global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, 
   htouch[s] = 1;
 }
 
+// After the (piece, top 40 value bits) sort: each run of records with equal piece and equal top
+// 40 bits (values within 2^-28 relative of each other; rare) is insertion-sorted by the full
+// ordered 64-bit value, stably -- the record order a full 64-bit LSD sort produces.  One lane per
+// run (its first record); every other lane returns after two compares.
+__global__ void k_fix_ties(uint64_t* __restrict__ A, uint64_t* __restrict__ B, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i + 1 >= n) return;
+  auto same = [&](uint64_t a, uint64_t b) { return (B[a] >> 32) == (B[b] >> 32) && (A[a] >> 24) == (A[b] >> 24); };
+  if (!same(i, i + 1)) return;
+  if (i > 0 && same(i - 1, i)) return;  // not the run's first record
+  uint64_t j = i + 2;
+  while (j < n && same(i, j)) j++;
+  for (uint64_t k = i + 1; k < j; k++) {  // stable insertion sort of [i, j) by A
+    const uint64_t a = A[k], b = B[k];
+    uint64_t m = k;
+    while (m > i && A[m - 1] > a) {
+      A[m] = A[m - 1];
+      B[m] = B[m - 1];
+      m--;
+    }
+    A[m] = a;
+    B[m] = b;
+  }
+}
+
 // Per touched key: how many of its batch samples the exact replay takes, by the key's window
 // count after this batch, tot:
 //   cold  tot <= E            the whole batch replays exactly (bit-exact);
@@ -1266,14 +1291,18 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   hipLaunchKernelGGL(k_histo_gather_hot, dim3(blocks_for(nremrec, kTile)), dim3(kBlock), 0, st, ntouched, nremrec,
                      e->h_tl, e->h_start, e->h_ex, e->h_hotoff, e->h_seen0, e->h_pbase, e->h_pi0, e->h_geo,
                      e->n_geo, As, Bs, Ao, Bo);
+  // (the value passes take the top 40 bits of the ordered value; k_fix_ties then orders the rare
+  // runs that share them by the full 64 bits -- the same stable order a 64-bit sort gives)
   RadixPass passes[16];
   int np = 0;
-  np = make_passes(passes, false, 0, 64);
+  np = make_passes(passes, false, 24, 40);
   int pbits = 1;
   while (pbits < 32 && (1ull << pbits) < npieces) pbits++;
   np += make_passes(passes + np, true, 32, pbits);
   const bool fl2 = radix_sort(Ao, Bo, e->hA2, e->hB2, nremrec, passes, np, e->rs, st,
                               e->timing ? &e->rstat_h : nullptr);
+  hipLaunchKernelGGL(k_fix_ties, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, fl2 ? e->hA2 : Ao,
+                     fl2 ? e->hB2 : Bo, nremrec);
   const uint64_t* PA = fl2 ? e->hA2 : Ao;  // sorted pieces
   const uint64_t* PB = fl2 ? e->hB2 : Bo;
   uint64_t* MA = fl2 ? Ao : e->hA2;        // per-round merged segments
