@@ -316,7 +316,7 @@ def egress_leg(flush_result):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)  # ~1.3 s timed at C4: long enough for SMI sampling
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--keys", type=int, default=1_000_000)
     ap.add_argument("--samples", type=int, default=1_000_000_000, help="samples per flush window, all ranks")
