@@ -222,6 +222,12 @@ void create_impl(vn_engine* e) {
          b += std::max<uint64_t>(1, b * e->piece_growth / 100))
       geo.push_back(b);
     e->n_geo = (uint32_t)geo.size();
+    // the first pieces of a hot key are small: merged all in one launch (k_rounds_fused) while
+    // piece + centroids fit its per-key scratch
+    e->fuse_pieces = 0;
+    while (e->fuse_pieces + 1 < geo.size() &&
+           geo[e->fuse_pieces + 1] - geo[e->fuse_pieces] + e->cap_cent <= kFuseMaxL)
+      e->fuse_pieces++;
     dalloc(e->h_geo, geo.size());
     VN_HIP_CHECK(hipMemcpyAsync(e->h_geo, geo.data(), geo.size() * sizeof(uint64_t), hipMemcpyHostToDevice, st));
     VN_HIP_CHECK(hipStreamSynchronize(st));
@@ -398,6 +404,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw);
   dfree(e->h_lpt0); dfree(e->h_lpt1); dfree(e->s_lpt0); dfree(e->s_lpt1);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);
+  dfree(e->fz_val); dfree(e->fz_w); dfree(e->fz_k); dfree(e->fz_done);
   dfree(e->h_geo); dfree(e->h_seen0); dfree(e->h_pcnt); dfree(e->h_pi0); dfree(e->h_pbase); dfree(e->p_start);
   dfree(e->p_end); dfree(e->r_flag); dfree(e->r_len); dfree(e->r_list); dfree(e->r_off); dfree(e->r_pos);
   dfree(e->smode); dfree(e->sbase); dfree(e->snz); dfree(e->slc); dfree(e->slb); dfree(e->slast); dfree(e->stc);

@@ -205,6 +205,10 @@ struct vn_engine {
   // geometric remainder of hot keys (ingest_histo.hip)
   uint64_t* h_geo = nullptr;     // piece boundaries b_0 = hot_prefix, b_{i+1} = b_i + max(1, b_i / 10)
   uint32_t n_geo = 0;
+  uint32_t fuse_pieces = 0;        // leading geometric pieces small enough for k_rounds_fused
+  double *fz_val = nullptr, *fz_w = nullptr, *fz_k = nullptr;  // its scratch, fz_cap keys
+  uint32_t* fz_done = nullptr;
+  uint32_t fz_cap = 0;
   uint32_t* h_seen0 = nullptr;   // per touched key: window samples before this batch
   uint32_t* h_pcnt = nullptr;    // per touched key: remainder pieces in this batch
   uint32_t* h_pi0 = nullptr;     // per touched key: first boundary index after its remainder start

@@ -93,7 +93,8 @@ void histo_rounds(vn_engine* e, const uint32_t* list, uint32_t nkeys, uint32_t m
 // elements with the key's centroids); val / w / kk: nkeys * kFuseMaxL doubles each of scratch
 constexpr uint32_t kFuseMaxL = 12288;
 void histo_rounds_fused(vn_engine* e, const uint32_t* list, uint32_t nkeys, const uint64_t* PA, const uint64_t* PB,
-                        const double* impw, double* val, double* w, double* kk, hipStream_t st);
+                        const double* impw, double* val, double* w, double* kk, hipStream_t st,
+                        uint32_t max_pieces = ~0u, uint32_t* done = nullptr);
 // One mergeAllTemps of each segment [start[k], end[k]) of (A = ordered value bits, B = tag) alone,
 // at compression delta, into the pseudo-slot tiles k = tl[k] of the given arrays (the split-key
 // micro-centroids, split.hip).  Per segment a capc-wide tile; w/wk sized nrec; chunk arrays sized

@@ -597,11 +597,19 @@ __device__ __forceinline__ uint32_t geo_upper(const uint64_t* geo, uint32_t ngeo
   return l;
 }
 
-// maxp[0]: most pieces of a hot key, maxp[1]: of a warm key (the two round loops)
+// A hot key's pieces ending at boundary 1..fuse (every one fits kFuseMaxL with the centroids)
+// are merged by k_rounds_fused: how many of its leading pieces that is
+__device__ __forceinline__ uint32_t fused_pieces(uint32_t pi0, uint32_t npieces, uint32_t fuse) {
+  if (pi0 < 1 || pi0 > fuse) return 0;
+  return min(npieces, fuse + 1 - pi0);
+}
+
+// maxp[0]: most pieces of a hot key, maxp[1]: of a warm key, maxp[2]: most pieces of a hot key
+// left to the round pipeline after the fused launch (fuse > 0)
 __global__ void k_histo_pieces(uint32_t ntouched, const uint32_t* __restrict__ ex, const uint32_t* __restrict__ hotcnt,
                                const uint32_t* __restrict__ seen0, const uint32_t* __restrict__ warmflag,
-                               const uint64_t* __restrict__ geo, uint32_t ngeo, uint32_t* __restrict__ pcnt,
-                               uint32_t* __restrict__ pi0, uint32_t* __restrict__ maxp) {
+                               const uint64_t* __restrict__ geo, uint32_t ngeo, uint32_t fuse,
+                               uint32_t* __restrict__ pcnt, uint32_t* __restrict__ pi0, uint32_t* __restrict__ maxp) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= ntouched) return;
   const uint32_t n = hotcnt[k];
@@ -615,6 +623,7 @@ __global__ void k_histo_pieces(uint32_t ntouched, const uint32_t* __restrict__ e
   pi0[k] = i0;
   pcnt[k] = 1 + (i1 - i0);
   atomicMax(maxp + (warmflag[k] ? 1 : 0), 1 + (i1 - i0));
+  if (!warmflag[k]) atomicMax(maxp + 2, 1 + (i1 - i0) - fused_pieces(i0, 1 + (i1 - i0), fuse));
 }
 
 // copy the hot remainder into the piece-sort input: A = ordered value bits, B = piece id << 32 |
@@ -878,6 +887,11 @@ struct FusedRounds {
   double* w;
   double* kk;            // k of every merged element (global: the kernel needs no large LDS block)
   uint32_t* err;
+  // partial mode (done != null): merge only the leading pieces that end at geometric boundary
+  // 1..max_pieces (fused_pieces); done[block] = pieces merged (the round pipeline takes the rest)
+  uint32_t max_pieces;
+  const uint32_t* pi0;
+  uint32_t* done;
 };
 __global__ __launch_bounds__(kBlock) void k_rounds_fused(FusedRounds x) {
   __shared__ uint32_t s_st[kMaxCent + 1];
@@ -892,14 +906,19 @@ __global__ __launch_bounds__(kBlock) void k_rounds_fused(FusedRounds x) {
   uint32_t nc = x.hncent[s];
   uint8_t cur = x.hcur[s];
   double* h = x.hst + (uint64_t)s * VN_HISTO_STATS;
-  for (uint32_t j = 0; j < npieces; j++) {
+  uint32_t jdone = 0;
+  const uint32_t jend = x.done ? fused_pieces(x.pi0[key], npieces, x.max_pieces) : npieces;
+  for (uint32_t j = 0; j < jend; j++) {
     const uint32_t g = x.pbase[key] + j;
     const uint32_t ps = x.pstart[g], np = x.pend[g] - ps;
     const double* cm = (cur ? x.cm1 : x.cm0) + (uint64_t)s * capc;
     const double* cw = (cur ? x.cw1 : x.cw0) + (uint64_t)s * capc;
     const uint32_t L = nc + np;
-    if (np == 0) continue;  // (block-uniform) nothing to merge
-    if (L > kFuseMaxL) {  // the host sizes pieces below this
+    if (np == 0) {  // (block-uniform) nothing to merge
+      jdone = j + 1;
+      continue;
+    }
+    if (L > kFuseMaxL) {  // the host sizes pieces (or max_pieces) below this
       if (t == 0) atomicOr(x.err, 1u);
       return;
     }
@@ -1016,19 +1035,35 @@ __global__ __launch_bounds__(kBlock) void k_rounds_fused(FusedRounds x) {
     }
     nc = ncn;
     cur = nb;
+    jdone = j + 1;
     __syncthreads();  // the new centroids are the next piece's merge input
   }
-  if (t == 0 && npieces) {
+  if (t == 0 && jdone) {
     x.hncent[s] = nc;
     x.hcur[s] = cur;
     x.hspn[s] = 0;
   }
+  if (t == 0 && x.done) x.done[blockIdx.x] = jdone;
+}
+
+// after a partial fused launch: the round pipeline starts at each key's first unmerged piece
+__global__ void k_fuse_shift(const uint32_t* __restrict__ list, uint32_t n, const uint32_t* __restrict__ done,
+                             uint32_t* __restrict__ pbase, uint32_t* __restrict__ pcnt) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = list[i], d = done[i];
+  pbase[k] += d;
+  pcnt[k] -= d;
 }
 
 void histo_rounds_fused(vn_engine* e, const uint32_t* list, uint32_t nkeys, const uint64_t* PA, const uint64_t* PB,
-                        const double* impw, double* val, double* w, double* kk, hipStream_t st) {
+                        const double* impw, double* val, double* w, double* kk, hipStream_t st, uint32_t max_pieces,
+                        uint32_t* done) {
   if (!nkeys) return;
   FusedRounds x;
+  x.max_pieces = max_pieces;
+  x.pi0 = e->h_pi0;
+  x.done = done;
   x.list = list;
   x.tl = e->h_tl;
   x.pcnt = e->h_pcnt;
@@ -1164,9 +1199,10 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   compact_flags(e->h_warmflag, e->h_pos, e->h_warmlist, e->h_cnt + 8, ntouched, e->ss, st);
   compact_flags(e->h_coldflag, e->h_pos, e->h_coldlist, e->h_cnt + 6, ntouched, e->ss, st);
   scan_exclusive_u32(e->h_hotcnt, e->h_hotoff, ntouched, e->ss, st);
-  VN_HIP_CHECK(hipMemsetAsync(e->h_cnt + 9, 0, 2 * sizeof(uint32_t), st));
+  VN_HIP_CHECK(hipMemsetAsync(e->h_cnt + 9, 0, 3 * sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_histo_pieces, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_ex,
-                     e->h_hotcnt, e->h_seen0, e->h_warmflag, e->h_geo, e->n_geo, e->h_pcnt, e->h_pi0, e->h_cnt + 9);
+                     e->h_hotcnt, e->h_seen0, e->h_warmflag, e->h_geo, e->n_geo, e->fuse_pieces, e->h_pcnt, e->h_pi0,
+                     e->h_cnt + 9);
   scan_exclusive_u32(e->h_pcnt, e->h_pbase, ntouched, e->ss, st);
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 1, e->h_cnt + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 2, e->h_hotoff + ntouched, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -1174,12 +1210,14 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 4, e->h_cnt + 9, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 6, e->h_cnt + 6, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 7, e->h_cnt + 8, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 11, e->h_cnt + 11, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipStreamSynchronize(st));
   const uint32_t nhot = e->hf_cnt[1];
   const uint64_t nremrec = e->hf_cnt[2];  // remainder records of warm and hot keys
   const uint32_t npieces = e->hf_cnt[3];
   const uint32_t maxp_hot = e->hf_cnt[4];
   const uint32_t maxp_warm = e->hf_cnt[5];
+  const uint32_t maxp_hot_left = e->hf_cnt[11];  // after the fused launch of the leading pieces
   const uint32_t nreplay = e->hf_cnt[6];  // cold + warm keys
   const uint32_t nwarm = e->hf_cnt[7];
 
@@ -1323,10 +1361,41 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   auto rounds = [&](const uint32_t* list, uint32_t nkeys, uint32_t maxp) {
     histo_rounds(e, list, nkeys, maxp, nremrec, nrem, PA, PB, MA, MB, impw, st);
   };
-  if (nhot) rounds(e->h_hotlist, nhot, maxp_hot);
-  // the warm keys' rounds start from their exact prefixes: after the replay stream
+  // the warm keys' rounds start from their exact prefixes (the replay stream), which at C4 are
+  // done before the remainder sort is: hot and warm keys then share one loop of
+  // max(hot, warm) rounds instead of hot rounds followed by warm rounds
   if (fork) VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_join3, 0));
-  if (nwarm) rounds(e->h_warmlist, nwarm, maxp_warm);
+  // the hot keys' leading (small) pieces: merged by one workgroup per key in one launch (every
+  // one fits kFuseMaxL with the centroids, by the geometry); the round loop then starts at each
+  // key's next piece
+  uint32_t hot_rounds = maxp_hot;
+  if (nhot && e->fuse_pieces) {
+    hot_rounds = maxp_hot_left;
+    if (e->fz_cap < nhot) {
+      VN_HIP_CHECK(hipStreamSynchronize(st));
+      for (void* q : {(void*)e->fz_val, (void*)e->fz_w, (void*)e->fz_k, (void*)e->fz_done})
+        if (q) VN_HIP_CHECK(hipFree(q));
+      const uint32_t cap = std::max<uint32_t>(nhot, 256);
+      VN_HIP_CHECK(hipMalloc(&e->fz_val, (uint64_t)cap * kFuseMaxL * sizeof(double)));
+      VN_HIP_CHECK(hipMalloc(&e->fz_w, (uint64_t)cap * kFuseMaxL * sizeof(double)));
+      VN_HIP_CHECK(hipMalloc(&e->fz_k, (uint64_t)cap * kFuseMaxL * sizeof(double)));
+      VN_HIP_CHECK(hipMalloc(&e->fz_done, (uint64_t)cap * sizeof(uint32_t)));
+      e->fz_cap = cap;
+    }
+    histo_rounds_fused(e, e->h_hotlist, nhot, PA, PB, impw, e->fz_val, e->fz_w, e->fz_k, st, e->fuse_pieces,
+                       e->fz_done);
+    hipLaunchKernelGGL(k_fuse_shift, dim3(blocks_for(nhot, 256)), dim3(256), 0, st, e->h_hotlist, nhot, e->fz_done,
+                       e->h_pbase, e->h_pcnt);
+  }
+  if (nhot && nwarm) {
+    VN_HIP_CHECK(hipMemcpyAsync(e->h_hotlist + nhot, e->h_warmlist, (uint64_t)nwarm * sizeof(uint32_t),
+                                hipMemcpyDeviceToDevice, st));
+    rounds(e->h_hotlist, nhot + nwarm, std::max(hot_rounds, maxp_warm));
+  } else if (nhot) {
+    rounds(e->h_hotlist, nhot, hot_rounds);
+  } else if (nwarm) {
+    rounds(e->h_warmlist, nwarm, maxp_warm);
+  }
   hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
 }
 
