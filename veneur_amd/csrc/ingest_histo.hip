@@ -1361,10 +1361,6 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   auto rounds = [&](const uint32_t* list, uint32_t nkeys, uint32_t maxp) {
     histo_rounds(e, list, nkeys, maxp, nremrec, nrem, PA, PB, MA, MB, impw, st);
   };
-  // the warm keys' rounds start from their exact prefixes (the replay stream), which at C4 are
-  // done before the remainder sort is: hot and warm keys then share one loop of
-  // max(hot, warm) rounds instead of hot rounds followed by warm rounds
-  if (fork) VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_join3, 0));
   // the hot keys' leading (small) pieces: merged by one workgroup per key in one launch (every
   // one fits kFuseMaxL with the centroids, by the geometry); the round loop then starts at each
   // key's next piece
@@ -1387,6 +1383,11 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
     hipLaunchKernelGGL(k_fuse_shift, dim3(blocks_for(nhot, 256)), dim3(256), 0, st, e->h_hotlist, nhot, e->fz_done,
                        e->h_pbase, e->h_pcnt);
   }
+  // the warm keys' rounds start from their exact prefixes (the replay stream), which at C4 are
+  // done about when the remainder sort is: hot and warm keys then share one loop of
+  // max(hot, warm) rounds instead of hot rounds followed by warm rounds (the fused launch above
+  // needs only the hot prefixes: it runs beside the tail of the replay)
+  if (fork) VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_join3, 0));
   if (nhot && nwarm) {
     VN_HIP_CHECK(hipMemcpyAsync(e->h_hotlist + nhot, e->h_warmlist, (uint64_t)nwarm * sizeof(uint32_t),
                                 hipMemcpyDeviceToDevice, st));

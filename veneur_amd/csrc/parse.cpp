@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <locale.h>
 #include <string>
 #include <vector>
 
@@ -72,12 +73,17 @@ int parse_float(const char* p, size_t n, bool f32, double* out) {
   const char* z;
   if (n < sizeof(small)) { memcpy(small, p, n); small[n] = 0; z = small; }
   else { big.assign(p, n); z = big.c_str(); }
+  // the "C" locale whatever LC_NUMERIC the host process set (Go's ParseFloat has no locale)
+  static const locale_t c_locale = newlocale(LC_ALL_MASK, "C", (locale_t)0);
+  char* end = nullptr;
   if (f32) {
-    float v = strtof(z, nullptr);
+    float v = strtof_l(z, &end, c_locale);
+    if (end != z + n) return 1;
     if (std::isinf(v)) return 2;
     *out = (double)v;
   } else {
-    double v = strtod(z, nullptr);
+    double v = strtod_l(z, &end, c_locale);
+    if (end != z + n) return 1;
     if (std::isinf(v)) return 2;
     *out = v;
   }
