@@ -409,3 +409,20 @@ def test_histo_duplicate_values_past_threshold():
          "g_slot": np.zeros(0, np.uint32), "g_val": np.zeros(0), "h_slot": slot, "h_val": val, "h_rate": rate,
          "s_slot": np.zeros(0, np.uint32), "s_off": np.zeros(1, np.uint32), "s_bytes": np.zeros(0, np.uint8)}
     _histo_parity(d, (1, 1, len(sizes), 1), batches=3, max_rank=3e-3)
+
+
+def test_histo_hot_key_near_tie_values():
+    """a hot key whose values share their top 40 ordered bits by the thousand (1000 + U(0, 1e-4):
+    runs far longer than k_fix_ties sorts in place, not in full-value order) -- the tie check
+    sets the device flag and the full-width re-sort of the remainder runs; rank error holds
+    although every quantile sits inside a 1e-4 wide cluster"""
+    rng = np.random.default_rng(31)
+    sizes = [300_000, 50_000]
+    slot = np.concatenate([np.full(n, k, np.uint32) for k, n in enumerate(sizes)])
+    rng.shuffle(slot)
+    val = np.where(slot == 0, 1000.0 + rng.random(len(slot)) * 1e-4, rng.lognormal(2.0, 1.0, len(slot)))
+    rate = np.ones(len(slot), np.float32)
+    d = {"c_slot": np.zeros(0, np.uint32), "c_val": np.zeros(0), "c_rate": np.zeros(0, np.float32),
+         "g_slot": np.zeros(0, np.uint32), "g_val": np.zeros(0), "h_slot": slot, "h_val": val, "h_rate": rate,
+         "s_slot": np.zeros(0, np.uint32), "s_off": np.zeros(1, np.uint32), "s_bytes": np.zeros(0, np.uint8)}
+    _histo_parity(d, (1, 1, len(sizes), 1), batches=2, exact_threshold=20000)

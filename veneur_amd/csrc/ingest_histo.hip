@@ -518,17 +518,27 @@ __global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, 
 }
 
 // After the (piece, top 40 value bits) sort: each run of records with equal piece and equal top
-// 40 bits (values within 2^-28 relative of each other; rare) is insertion-sorted by the full
-// ordered 64-bit value, stably -- the record order a full 64-bit LSD sort produces.  One lane per
-// run (its first record); every other lane returns after two compares.
+// 40 bits (values within 2^-28 relative of each other) of at most kTieRun records is
+// insertion-sorted by the full ordered 64-bit value, stably -- the record order a full 64-bit LSD
+// sort produces.  One lane per run (its first record); every other lane returns after two
+// compares, and no lane walks more than kTieRun + 1 records.  A longer run is left to
+// k_tie_check: long runs of one repeated value (integer-valued timers) are in order already; a
+// long run that is not sets the flag for the conditional full-width re-sort.
+constexpr uint64_t kTieRun = 64;
+#ifndef VN_TIE_RESORT
+#define VN_TIE_RESORT 1  // 0: no tie check (negative control for the near-tie test, tools/ab_variant.sh)
+#endif
+__device__ __forceinline__ bool same_top(const uint64_t* A, const uint64_t* B, uint64_t a, uint64_t b) {
+  return (B[a] >> 32) == (B[b] >> 32) && (A[a] >> 24) == (A[b] >> 24);
+}
 __global__ void k_fix_ties(uint64_t* __restrict__ A, uint64_t* __restrict__ B, uint64_t n) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i + 1 >= n) return;
-  auto same = [&](uint64_t a, uint64_t b) { return (B[a] >> 32) == (B[b] >> 32) && (A[a] >> 24) == (A[b] >> 24); };
-  if (!same(i, i + 1)) return;
-  if (i > 0 && same(i - 1, i)) return;  // not the run's first record
+  if (!same_top(A, B, i, i + 1)) return;
+  if (i > 0 && same_top(A, B, i - 1, i)) return;  // not the run's first record
   uint64_t j = i + 2;
-  while (j < n && same(i, j)) j++;
+  while (j < n && j - i <= kTieRun && same_top(A, B, i, j)) j++;
+  if (j - i > kTieRun) return;  // long run: k_tie_check
   for (uint64_t k = i + 1; k < j; k++) {  // stable insertion sort of [i, j) by A
     const uint64_t a = A[k], b = B[k];
     uint64_t m = k;
@@ -540,6 +550,15 @@ __global__ void k_fix_ties(uint64_t* __restrict__ A, uint64_t* __restrict__ B, u
     A[m] = a;
     B[m] = b;
   }
+}
+
+// After k_fix_ties: any adjacent pair still out of full-value order (only inside a long run) sets
+// *resort, and the (piece, full value) sort queued behind it runs (radix_sort's cond).
+__global__ void k_tie_check(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B, uint64_t n,
+                            uint32_t* __restrict__ resort) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (i >= n) return;
+  if (A[i - 1] > A[i] && same_top(A, B, i - 1, i)) *resort = 1u;
 }
 
 // Per touched key: how many of its batch samples the exact replay takes, by the key's window
@@ -1339,12 +1358,34 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   np += make_passes(passes + np, true, 32, pbits);
   const bool fl2 = radix_sort(Ao, Bo, e->hA2, e->hB2, nremrec, passes, np, e->rs, st,
                               e->timing ? &e->rstat_h : nullptr);
-  hipLaunchKernelGGL(k_fix_ties, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, fl2 ? e->hA2 : Ao,
-                     fl2 ? e->hB2 : Bo, nremrec);
-  const uint64_t* PA = fl2 ? e->hA2 : Ao;  // sorted pieces
-  const uint64_t* PB = fl2 ? e->hB2 : Bo;
+  uint64_t* const SA = fl2 ? e->hA2 : Ao;  // sorted pieces
+  uint64_t* const SB = fl2 ? e->hB2 : Bo;
   uint64_t* MA = fl2 ? Ao : e->hA2;        // per-round merged segments
   uint64_t* MB = fl2 ? Bo : e->hB2;
+  hipLaunchKernelGGL(k_fix_ties, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, SA, SB, nremrec);
+  {
+    // a long run out of full-value order (rare): the whole (piece, 64-bit value) sort, queued
+    // behind a device flag so no host round trip decides it; an even pass count leaves the
+    // result in (SA, SB) whether it runs or not (MA / MB are free until the rounds)
+    uint32_t* const resort = e->h_cnt + 14;
+    VN_HIP_CHECK(hipMemsetAsync(resort, 0, sizeof(uint32_t), st));
+    if (VN_TIE_RESORT)
+      hipLaunchKernelGGL(k_tie_check, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, SA, SB, nremrec, resort);
+    RadixPass full[16];
+    int nf = 0;
+    const int npb = (pbits + 7) / 8;
+    if ((8 + npb) % 2) {  // 4 passes of 6 bits over the low 24 value bits: an even total
+      for (int q = 0; q < 4; q++) full[nf++] = RadixPass{false, 6 * q, 6};
+      nf += make_passes(full + nf, false, 24, 40);
+    } else {
+      nf += make_passes(full + nf, false, 0, 64);
+    }
+    nf += make_passes(full + nf, true, 32, pbits);
+    if (nf % 2) throw std::logic_error("conditional re-sort needs an even pass count");
+    (void)radix_sort(SA, SB, MA, MB, nremrec, full, nf, e->rs, st, nullptr, resort);
+  }
+  const uint64_t* PA = SA;
+  const uint64_t* PB = SB;
   hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, nremrec, PB, e->p_start,
                      e->p_end);
   if (fork) {

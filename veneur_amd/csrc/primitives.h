@@ -14,7 +14,8 @@ struct ScanScratch {
   uint32_t* partials = nullptr;  // >= ceil(n / kTile) + 1
   size_t cap = 0;
 };
-void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, ScanScratch& s, hipStream_t st);
+void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, ScanScratch& s, hipStream_t st,
+                        const uint32_t* cond = nullptr);
 
 // ---- stable LSD radix sort over 64-bit words.
 // Records are (A[i], B[i]) pairs (B may be null for key-only sorts).  Each pass sorts
@@ -54,7 +55,10 @@ struct RadixStats {
 };
 bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t n,
                 const RadixPass* passes, int npasses, RadixScratch& s, hipStream_t st,
-                RadixStats* stats);
+                RadixStats* stats, const uint32_t* cond = nullptr);
+// cond (device word, may be null): every kernel of the sort returns at once when it reads 0, so
+// the sort is queued without a host round trip and runs only when a kernel before it set the
+// word.  With an even pass count the result is in (a0, b0) either way.
 
 void radix_scratch_reserve(RadixScratch& s, uint64_t max_n);
 void radix_scratch_free(RadixScratch& s);

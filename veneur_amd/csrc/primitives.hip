@@ -36,8 +36,12 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t* s_
 }
 
 // ---------------------------------------------------------------- exclusive scan u32
-__global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ in, uint64_t n,
+// cond (may be null): when it points at 0 the kernels return at once (radix_sort's conditional
+// passes)
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restrict__ cond,
+                                                        const uint32_t* __restrict__ in, uint64_t n,
                                                         uint32_t* __restrict__ partials) {
+  if (cond && !*cond) return;
   __shared__ uint32_t s_wave[4];
   uint64_t base = (uint64_t)blockIdx.x * kTile;
   uint32_t sum = 0;
@@ -52,7 +56,9 @@ __global__ __launch_bounds__(kBlock) void k_scan_reduce(const uint32_t* __restri
 }
 
 // single block: exclusive scan of the partials in place, total into partials[np]
-__global__ __launch_bounds__(kBlock) void k_scan_partials(uint32_t* partials, uint32_t np) {
+__global__ __launch_bounds__(kBlock) void k_scan_partials(const uint32_t* __restrict__ cond, uint32_t* partials,
+                                                          uint32_t np) {
+  if (cond && !*cond) return;
   __shared__ uint32_t s_wave[4];
   uint32_t carry = 0;
   for (uint32_t base = 0; base < np; base += kBlock) {
@@ -66,9 +72,11 @@ __global__ __launch_bounds__(kBlock) void k_scan_partials(uint32_t* partials, ui
   if (threadIdx.x == 0) partials[np] = carry;
 }
 
-__global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+__global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t* __restrict__ cond,
+                                                      const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
                                                       uint64_t n, const uint32_t* __restrict__ partials,
                                                       uint32_t np) {
+  if (cond && !*cond) return;
   __shared__ uint32_t s_wave[4];
   // blocked layout: thread t owns items [t*16, t*16+16) of the tile
   uint64_t base = (uint64_t)blockIdx.x * kTile + (uint64_t)threadIdx.x * kItems;
@@ -91,7 +99,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_down(const uint32_t* __restrict
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = partials[np];
 }
 
-void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, ScanScratch& s, hipStream_t st) {
+void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, ScanScratch& s, hipStream_t st,
+                        const uint32_t* cond) {
   uint32_t np = (uint32_t)blocks_for(n ? n : 1, kTile);
   if (s.cap < np + 1) {
     if (s.partials) VN_HIP_CHECK(hipFree(s.partials));
@@ -102,9 +111,9 @@ void scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint64_t n, ScanScrat
     VN_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(uint32_t), st));
     return;
   }
-  hipLaunchKernelGGL(k_scan_reduce, dim3(np), dim3(kBlock), 0, st, in, n, s.partials);
-  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kBlock), 0, st, s.partials, np);
-  hipLaunchKernelGGL(k_scan_down, dim3(np), dim3(kBlock), 0, st, in, out, n, s.partials, np);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(np), dim3(kBlock), 0, st, cond, in, n, s.partials);
+  hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(kBlock), 0, st, cond, s.partials, np);
+  hipLaunchKernelGGL(k_scan_down, dim3(np), dim3(kBlock), 0, st, cond, in, out, n, s.partials, np);
 }
 
 // ---------------------------------------------------------------- compaction
@@ -136,7 +145,9 @@ __device__ __forceinline__ uint32_t digit_of(uint64_t a, uint64_t b, bool from_b
 template <bool HASB>
 __global__ __launch_bounds__(kBlock) void k_radix_count(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B,
                                                         uint64_t n, bool from_b, int shift, uint32_t mask,
-                                                        uint32_t* __restrict__ counts, uint32_t nblocks) {
+                                                        uint32_t* __restrict__ counts, uint32_t nblocks,
+                                                        const uint32_t* __restrict__ cond) {
+  if (cond && !*cond) return;  // a conditional sort that is not needed (radix_sort)
   __shared__ uint32_t s_hist[4][256];
   const int w = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < 4 * 256; i += kBlock) (&s_hist[0][0])[i] = 0;
@@ -178,7 +189,9 @@ __global__ __launch_bounds__(NW * 64) void k_radix_scatter(const uint64_t* __res
                                                            uint64_t* __restrict__ A2, uint64_t* __restrict__ B2,
                                                            uint64_t n, bool from_b, int shift, int bits,
                                                            const uint32_t* __restrict__ counts,
-                                                           const uint32_t* __restrict__ offsets, uint32_t nblocks) {
+                                                           const uint32_t* __restrict__ offsets, uint32_t nblocks,
+                                                           const uint32_t* __restrict__ cond) {
+  if (cond && !*cond) return;
   constexpr int kRWaves = NW, kRBlock = NW * 64, kRItems = kTile / kRBlock;
   __shared__ uint64_t s_x[kTile];
   __shared__ uint8_t s_dig[HASB ? kTile : 1];
@@ -289,7 +302,7 @@ void radix_scratch_free(RadixScratch& s) {
 
 
 bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t n, const RadixPass* passes,
-                int npasses, RadixScratch& s, hipStream_t st, RadixStats* stats) {
+                int npasses, RadixScratch& s, hipStream_t st, RadixStats* stats, const uint32_t* cond) {
   if (n == 0 || npasses == 0) return false;
   radix_scratch_reserve(s, n);
   const uint32_t nblocks = (uint32_t)blocks_for(n, kTile);
@@ -304,20 +317,20 @@ bool radix_sort(uint64_t* a0, uint64_t* b0, uint64_t* a1, uint64_t* b1, uint64_t
     const uint32_t mask = (1u << ps.bits) - 1u;
     if (hasb)
       hipLaunchKernelGGL(k_radix_count<true>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, n, ps.from_b, ps.shift, mask,
-                         s.counts, nblocks);
+                         s.counts, nblocks, cond);
     else
       hipLaunchKernelGGL(k_radix_count<false>, dim3(nblocks), dim3(kBlock), 0, st, sa, sb, n, ps.from_b, ps.shift,
-                         mask, s.counts, nblocks);
-    scan_exclusive_u32(s.counts, s.offsets, (uint64_t)(mask + 1) * nblocks, s.scan, st);
+                         mask, s.counts, nblocks, cond);
+    scan_exclusive_u32(s.counts, s.offsets, (uint64_t)(mask + 1) * nblocks, s.scan, st, cond);
     hipEvent_t e0 = (stats && stats->pool) ? stats->pool->next() : nullptr;
     hipEvent_t e1 = (stats && stats->pool) ? stats->pool->next() : nullptr;
     if (e0 && e1) VN_HIP_CHECK(hipEventRecord(e0, st));
     if (hasb)
       hipLaunchKernelGGL((k_radix_scatter<true, 8>), dim3(nblocks), dim3(512), 0, st, sa, sb, da, db, n, ps.from_b,
-                         ps.shift, ps.bits, s.counts, s.offsets, nblocks);
+                         ps.shift, ps.bits, s.counts, s.offsets, nblocks, cond);
     else  // 8-byte records also scatter with 8 waves (measured ~1% faster on C3 than 4)
       hipLaunchKernelGGL((k_radix_scatter<false, 8>), dim3(nblocks), dim3(512), 0, st, sa, sb, da, db, n, ps.from_b,
-                         ps.shift, ps.bits, s.counts, s.offsets, nblocks);
+                         ps.shift, ps.bits, s.counts, s.offsets, nblocks, cond);
     if (e0 && e1) VN_HIP_CHECK(hipEventRecord(e1, st));
     if (stats) {
       stats->launches += 1;
