@@ -193,9 +193,8 @@ struct Lds {
   ldsf64 *tv, *tw;        // pending temps in Add order [TP]
   ldsf64 *sv, *sw;        // sorted temps of the merge being done [TP]
   ldsf64 *gm, *gw, *kin;  // merged elements [JW]
-  ldsu32* jump;           // start of the table memory (jump16 aliases it)
   ldsu16* jump16;         // next-start tables, levels x [JW] u16 (entries <= JW < 65536)
-  ldsu32* starts;         // [JW]
+  ldsu16* starts;         // [JW]
   uint32_t JW, levels;
 };
 
@@ -213,10 +212,13 @@ __device__ __forceinline__ Lds lds_layout(char* smem, uint32_t capc, uint32_t TP
   L.sw = L.sv + TP;
   L.gm = L.sw + TP;
   L.gw = L.gm + L.JW;
-  L.kin = L.gw + L.JW;
-  L.starts = (ldsu32*)(L.kin + L.JW);
-  L.jump = L.starts + L.JW;
-  L.jump16 = (ldsu16*)L.jump;
+  // k of the merged elements: written after the merge has read the main centroids for the last
+  // time and dead before the centroid pass writes the new ones, so it lives in the main tile
+  // when it fits (delta 100: 17.3 KiB per key, 9 waves per CU instead of 8)
+  const bool kin_in_main = L.JW <= 2 * capc;
+  L.kin = kin_in_main ? L.mm : L.gw + L.JW;
+  L.starts = (ldsu16*)(L.gw + L.JW + (kin_in_main ? 0 : L.JW));
+  L.jump16 = L.starts + L.JW;
   return L;
 }
 
@@ -1512,11 +1514,17 @@ void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* 
   x.order64 = radix_sort(buf0, nullptr, buf1, nullptr, n, passes, np, rs, st, nullptr) ? buf1 : buf0;
 }
 
+#ifndef VN_EXACT_LDS_PAD
+#define VN_EXACT_LDS_PAD 0  // occupancy experiments only (tools/ab_variant.sh)
+#endif
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap) {
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = std::max(capc + TP + 1, 320u);
   uint32_t levels = 1;
   while ((1u << levels) <= capc) levels++;
-  return sizeof(double) * (2 * capc + 4 * TP + 3 * JW) + sizeof(uint32_t) * JW + sizeof(uint16_t) * std::max(levels, 9u) * JW + 16;
+  const uint32_t kin = JW <= 2 * capc ? 0 : JW;  // lds_layout: kin in the main tile when it fits
+  return sizeof(double) * (2 * capc + 4 * TP + 2 * JW + kin) + sizeof(uint16_t) * JW +
+         sizeof(uint16_t) * std::max(levels, 9u) * JW + 16 +
+         VN_EXACT_LDS_PAD;
 }
 
 #ifdef VN_EXACT_PROF
