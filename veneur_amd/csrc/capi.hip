@@ -87,6 +87,9 @@ void check_slots_host(const uint32_t* slot, uint64_t n, uint32_t cap, const char
     if (slot[i] >= cap) throw std::invalid_argument(std::string(what) + " slot out of range");
 }
 
+#ifndef VN_REPLAY_EIGHTHS
+#define VN_REPLAY_EIGHTHS 6
+#endif
 void create_impl(vn_engine* e) {
   VN_HIP_CHECK(hipSetDevice(e->device));
   // the histo path (main and replay streams) is the critical path: it gets the high queue
@@ -105,12 +108,15 @@ void create_impl(vn_engine* e) {
     hipDeviceProp_t prop;
     VN_HIP_CHECK(hipGetDeviceProperties(&prop, e->device));
     const uint32_t ncu = (uint32_t)prop.multiProcessorCount;
-    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u), rmask((ncu + 31) / 32, 0u);
     for (uint32_t i = 0; i < ncu - ncu / 4; i++) mask[i / 32] |= 1u << (i % 32);
+    // the replay streams' share in eighths of the CUs (bits [0, n/8 ncu): whole shader-engine
+    // columns of every XCC, as above)
+    for (uint32_t i = 0; i < ncu * VN_REPLAY_EIGHTHS / 8; i++) rmask[i / 32] |= 1u << (i % 32);
     e->side_cus = ncu - ncu / 4;
     if (ncu < 64 || hipExtStreamCreateWithCUMask(&e->st2, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&e->st3, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&e->st5, (uint32_t)mask.size(), mask.data()) != hipSuccess) {
+        hipExtStreamCreateWithCUMask(&e->st3, (uint32_t)rmask.size(), rmask.data()) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&e->st5, (uint32_t)rmask.size(), rmask.data()) != hipSuccess) {
       (void)hipGetLastError();
       for (hipStream_t* p : {&e->st2, &e->st3, &e->st5})
         if (*p) {
