@@ -61,12 +61,20 @@ struct HistoCtx {
 };
 
 // segment [start, end) of every slot present in a sorted (slot<<32 | x) array
+// bt / touch (may be null): the key-grouping sort marks each key batch-touched and
+// window-touched here, once per key, rather than once per record before the sort
 __global__ void k_seg_mark(uint64_t n, const uint64_t* __restrict__ B, uint32_t* __restrict__ start,
-                           uint32_t* __restrict__ end) {
+                           uint32_t* __restrict__ end, uint32_t* __restrict__ bt, uint32_t* __restrict__ touch) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t s = (uint32_t)(B[i] >> 32);
-  if (i == 0 || (uint32_t)(B[i - 1] >> 32) != s) start[s] = (uint32_t)i;
+  if (i == 0 || (uint32_t)(B[i - 1] >> 32) != s) {
+    start[s] = (uint32_t)i;
+    if (bt) {
+      bt[s] = 1;
+      touch[s] = 1;
+    }
+  }
   if (i == n - 1 || (uint32_t)(B[i + 1] >> 32) != s) end[s] = (uint32_t)(i + 1);
 }
 
@@ -505,16 +513,13 @@ __global__ void k_clear_flags(uint32_t n, const uint32_t* __restrict__ list, uin
 // raw (arrival-order) keys: A = float64 bits, B = slot<<32 | float32 rate bits
 // (rate == nullptr: imported centroids, weights in impw, tagged kTagImport | i)
 __global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, const double* __restrict__ val,
-                                 const float* __restrict__ rate, uint64_t* __restrict__ A, uint64_t* __restrict__ B,
-                                 uint32_t* __restrict__ bt, uint32_t* __restrict__ htouch) {
+                                 const float* __restrict__ rate, uint64_t* __restrict__ A, uint64_t* __restrict__ B) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t s = slot[i];
   A[i] = dbits(val[i]);
   const uint32_t tag = rate ? __float_as_uint(rate[i]) : (kTagImport | (uint32_t)i);
   B[i] = ((uint64_t)s << 32) | (uint64_t)tag;
-  bt[s] = 1;
-  htouch[s] = 1;
 }
 
 // After the (piece, top 40 value bits) sort: each run of records with equal piece and equal top
@@ -1175,8 +1180,7 @@ HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const do
   const uint32_t caph = e->cap[VN_HISTO];
   // ---- 1. group by key, arrival order kept (stable radix by slot); nothing here waits on
   // the host, so the caller can queue other streams' work before histo_process syncs
-  hipLaunchKernelGGL(k_histo_keys_raw, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, val, rate, e->hA0, e->hB0,
-                     e->h_bt, e->htouch);
+  hipLaunchKernelGGL(k_histo_keys_raw, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, val, rate, e->hA0, e->hB0);
   RadixPass spass[4];
   int nsp = 0;
   nsp = make_passes(spass, true, 32, e->slot_bits[VN_HISTO]);
@@ -1185,7 +1189,8 @@ HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const do
   g.Bs = fl ? e->hB1 : e->hB0;
   g.Ao = fl ? e->hA0 : e->hA1;
   g.Bo = fl ? e->hB0 : e->hB1;
-  hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, g.Bs, e->h_start, e->h_end);
+  hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, g.Bs, e->h_start, e->h_end, e->h_bt,
+                     e->htouch);
   compact_flags(e->h_bt, e->h_pos, e->h_tl, e->h_cnt, caph, e->ss, st);
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt, e->h_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   return g;
@@ -1387,7 +1392,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   const uint64_t* PA = SA;
   const uint64_t* PB = SB;
   hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, nremrec, PB, e->p_start,
-                     e->p_end);
+                     e->p_end, nullptr, nullptr);
   if (fork) {
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
     if (e->set_pending) {

@@ -95,22 +95,26 @@ __global__ __launch_bounds__(256) void k_set_small(SetCtx x) {
 
 __global__ void k_set_keys(uint64_t n, const uint32_t* __restrict__ slot, const uint32_t* __restrict__ off,
                            const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ hashes,
-                           uint64_t* __restrict__ R, uint32_t* __restrict__ bt, uint32_t* __restrict__ stouch) {
+                           uint64_t* __restrict__ R) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t s = slot[i];
   uint64_t x = hashes ? hashes[i] : metro64(bytes + off[i], off[i + 1] - off[i], kMetroSeed);
   R[i] = ((uint64_t)s << 32) | (uint64_t)encode_hash(x);
-  bt[s] = 1;
-  stouch[s] = 1;
 }
 
+// after the grouping sort: segment bounds, and each key marked batch- and window-touched once
+// (not once per record)
 __global__ void k_set_seg_mark(uint64_t n, const uint64_t* __restrict__ R, uint32_t* __restrict__ start,
-                               uint32_t* __restrict__ end) {
+                               uint32_t* __restrict__ end, uint32_t* __restrict__ bt, uint32_t* __restrict__ stouch) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t s = (uint32_t)(R[i] >> 32);
-  if (i == 0 || (uint32_t)(R[i - 1] >> 32) != s) start[s] = (uint32_t)i;
+  if (i == 0 || (uint32_t)(R[i - 1] >> 32) != s) {
+    start[s] = (uint32_t)i;
+    bt[s] = 1;
+    stouch[s] = 1;
+  }
   if (i == n - 1 || (uint32_t)(R[i + 1] >> 32) != s) end[s] = (uint32_t)(i + 1);
 }
 
@@ -495,15 +499,15 @@ void ingest_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint32_t*
   if (!n) return;
   hipStream_t st = e->side;
   const uint32_t caps = e->cap[VN_SET];
-  hipLaunchKernelGGL(k_set_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, off, bytes, hashes, e->sR0,
-                     e->s_bt, e->stouch);
+  hipLaunchKernelGGL(k_set_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, off, bytes, hashes, e->sR0);
   RadixPass passes[4];
   int np = 0;
   np = make_passes(passes, false, 32, e->slot_bits[VN_SET]);
   bool fl = radix_sort(e->sR0, nullptr, e->sR1, nullptr, n, passes, np, *e->side_rs, st,
                        e->timing ? &e->rstat_s : nullptr);
   const uint64_t* R = fl ? e->sR1 : e->sR0;
-  hipLaunchKernelGGL(k_set_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, R, e->s_start, e->s_end);
+  hipLaunchKernelGGL(k_set_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, R, e->s_start, e->s_end, e->s_bt,
+                     e->stouch);
   compact_flags(e->s_bt, e->s_pos, e->s_tl, e->s_cnt, caps, *e->side_ss, st);
   // no host round trip: the touched-key count stays on the device and the grid is its upper
   // bound, so the whole set path is queued before the histogram path blocks the host
