@@ -209,6 +209,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_tl2, touch_max);
   dalloc(e->h_ccnt, touch_max);
   dalloc(e->h_coff, (size_t)touch_max + 1);
+  dalloc(e->h_cown, ch ? e->h_sort_cap / std::max<uint32_t>(e->temp_cap, 1) + 2 : 0);
   dalloc(e->h_tw, e->h_sort_cap);
   dalloc(e->h_seen0, touch_max);
   dalloc(e->h_pcnt, touch_max);
@@ -409,7 +410,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->hseen); dfree(e->hpend); dfree(e->hspn); dfree(e->hspw); dfree(e->hm_flag); dfree(e->hm_pos); dfree(e->hm_idx); dfree(e->hm_list); dfree(e->hm_cnt); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
   dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw);
   dfree(e->h_lpt0); dfree(e->h_lpt1); dfree(e->s_lpt0); dfree(e->s_lpt1);
-  dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_tw);
+  dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_cown); dfree(e->h_tw);
   dfree(e->fz_val); dfree(e->fz_w); dfree(e->fz_k); dfree(e->fz_done);
   dfree(e->h_geo); dfree(e->h_seen0); dfree(e->h_pcnt); dfree(e->h_pi0); dfree(e->h_pbase); dfree(e->p_start);
   dfree(e->p_end); dfree(e->r_flag); dfree(e->r_len); dfree(e->r_list); dfree(e->r_off); dfree(e->r_pos);

@@ -66,6 +66,7 @@ struct ExactCtx {
   double* csv;
   double* csw;
   double* ctw;
+  uint32_t* cown;  // [chunks] the key index of every pure chunk (null: searched in coff)
 };
 
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap);

@@ -816,6 +816,14 @@ __global__ void k_exact_chunk_count(ExactCtx x) {
   x.ccnt[k] = exact_split(x.hpend[x.keys[k]], nex, x.tcap).npure;
 }
 
+// owner key of every pure chunk, so a sorting wave starts without a dependent binary search
+__global__ void k_exact_chunk_owner(ExactCtx x) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= x.nkeys) return;
+  const uint32_t a = x.coff[k], b = x.coff[k + 1];
+  for (uint32_t g = a; g < b; g++) x.cown[g] = k;
+}
+
 __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t g = blockIdx.x, lane = threadIdx.x;
@@ -825,7 +833,7 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
   ldsf64* tw = tv + TP;
   ldsf64* sv = tw + TP;
   ldsf64* sw = sv + TP;
-  const uint32_t k = last_le_u32(x.coff, x.nkeys, g);
+  const uint32_t k = x.cown ? x.cown[g] : last_le_u32(x.coff, x.nkeys, g);
   const uint32_t s = x.keys[k];
   const ExactSplit sp = exact_split(x.hpend[s], x.nex[k], tcap);
   const uint64_t base = (uint64_t)x.start[s] + sp.off0 + (uint64_t)(g - x.coff[k]) * tcap;
@@ -1543,6 +1551,8 @@ void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uin
   // sort every pure chunk in parallel first
   hipLaunchKernelGGL(k_exact_chunk_count, dim3(blocks_for(x.nkeys, 256)), dim3(256), 0, st, x);
   scan_exclusive_u32(x.ccnt, x.coff, x.nkeys, *ss, st);
+  if (x.cown && max_chunks)
+    hipLaunchKernelGGL(k_exact_chunk_owner, dim3(blocks_for(x.nkeys, 256)), dim3(256), 0, st, x);
   if (max_chunks)
     hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)max_chunks), dim3(64),
                        sizeof(double) * 4 * ((x.tcap + 1 + 63u) & ~63u), st, x);

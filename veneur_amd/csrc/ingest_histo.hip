@@ -63,19 +63,25 @@ struct HistoCtx {
 // segment [start, end) of every slot present in a sorted (slot<<32 | x) array
 // bt / touch (may be null): the key-grouping sort marks each key batch-touched and
 // window-touched here, once per key, rather than once per record before the sort
+// Each record's key is loaded once: the neighbours' come from the adjacent lanes (the wave's
+// first and last lanes load the one key beyond the wave).
 __global__ void k_seg_mark(uint64_t n, const uint64_t* __restrict__ B, uint32_t* __restrict__ start,
                            uint32_t* __restrict__ end, uint32_t* __restrict__ bt, uint32_t* __restrict__ touch) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t s = i < n ? (uint32_t)(B[i] >> 32) : 0xFFFFFFFFu;
+  uint32_t prev = __shfl_up(s, 1, 64), next = __shfl_down(s, 1, 64);
+  if (lane == 0 && i > 0 && i < n) prev = (uint32_t)(B[i - 1] >> 32);
+  if (lane == 63 && i + 1 < n) next = (uint32_t)(B[i + 1] >> 32);
   if (i >= n) return;
-  uint32_t s = (uint32_t)(B[i] >> 32);
-  if (i == 0 || (uint32_t)(B[i - 1] >> 32) != s) {
+  if (i == 0 || prev != s) {
     start[s] = (uint32_t)i;
     if (bt) {
       bt[s] = 1;
       touch[s] = 1;
     }
   }
-  if (i == n - 1 || (uint32_t)(B[i + 1] >> 32) != s) end[s] = (uint32_t)(i + 1);
+  if (i == n - 1 || next != s) end[s] = (uint32_t)(i + 1);
 }
 
 __device__ __forceinline__ uint32_t find_seg(const uint32_t* chb, uint32_t ntouched, uint32_t c) {
@@ -1276,6 +1282,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.flush_mode = 0;
   xc.ccnt = e->h_ccnt;
   xc.coff = e->h_coff;
+  xc.cown = e->h_cown;
   xc.csv = e->h_csv;
   xc.csw = e->h_csw;
   xc.ctw = e->h_tw;

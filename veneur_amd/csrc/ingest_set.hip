@@ -107,15 +107,19 @@ __global__ void k_set_keys(uint64_t n, const uint32_t* __restrict__ slot, const 
 // (not once per record)
 __global__ void k_set_seg_mark(uint64_t n, const uint64_t* __restrict__ R, uint32_t* __restrict__ start,
                                uint32_t* __restrict__ end, uint32_t* __restrict__ bt, uint32_t* __restrict__ stouch) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;  // neighbours' keys from the adjacent lanes
+  const uint32_t s = i < n ? (uint32_t)(R[i] >> 32) : 0xFFFFFFFFu;
+  uint32_t prev = __shfl_up(s, 1, 64), next = __shfl_down(s, 1, 64);
+  if (lane == 0 && i > 0 && i < n) prev = (uint32_t)(R[i - 1] >> 32);
+  if (lane == 63 && i + 1 < n) next = (uint32_t)(R[i + 1] >> 32);
   if (i >= n) return;
-  uint32_t s = (uint32_t)(R[i] >> 32);
-  if (i == 0 || (uint32_t)(R[i - 1] >> 32) != s) {
+  if (i == 0 || prev != s) {
     start[s] = (uint32_t)i;
     bt[s] = 1;
     stouch[s] = 1;
   }
-  if (i == n - 1 || (uint32_t)(R[i + 1] >> 32) != s) end[s] = (uint32_t)(i + 1);
+  if (i == n - 1 || next != s) end[s] = (uint32_t)(i + 1);
 }
 
 #ifdef VN_SET_PROF
