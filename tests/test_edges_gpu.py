@@ -132,11 +132,16 @@ def test_key_touched_only_by_imports():  # worker.go:237-242: imports Upsert the
     assert f.samples_imported == 4 and f.samples_processed == 0
 
 
-def _device_batch(bufs, **cls):
-    """An A.Batch whose arrays are copied to device memory (kept alive in bufs)."""
+def _device_batch(bufs, misalign=False, **cls):
+    """An A.Batch whose arrays are copied to device memory (kept alive in bufs); misalign: every
+    array starts one element past a 16-byte boundary (the validator's scalar path)."""
     import veneur_amd._abi as A
 
     def dev(a):
+        if misalign:
+            b = V.DeviceBuffer(np.concatenate([a[:1], a]))
+            bufs.append(b)
+            return b.ptr.value + a.itemsize
         b = V.DeviceBuffer(a)
         bufs.append(b)
         return b.ptr.value
@@ -157,12 +162,15 @@ def _device_batch(bufs, **cls):
     return b
 
 
+@pytest.mark.parametrize("where", ["mid", "quad_lane3", "tail", "misaligned"])
 @pytest.mark.parametrize("fault", ["counter_slot", "gauge_slot", "histo_slot", "set_slot", "histo_nan",
                                    "histo_inf", "histo_rate_zero", "counter_rate_big", "counter_rate_nan",
                                    "set_offsets"])
-def test_device_batch_validation_rejects_and_leaves_state(fault):
-    """vn_ingest validates a device-resident batch before applying anything (VN_EINVAL)."""
-    n, cap = 4096, 64
+def test_device_batch_validation_rejects_and_leaves_state(fault, where):
+    """vn_ingest validates a device-resident batch before applying anything (VN_EINVAL): a fault in
+    a 16-byte quad (either lane), in the records past the last full quad, or in arrays that are not
+    16-byte aligned (scalar checks)."""
+    n, cap = 4099, 64
     rng = np.random.default_rng(3)
     slots = rng.integers(0, cap, n).astype(np.uint32)
     vals = np.round(rng.lognormal(3, 1, n), 3)
@@ -174,7 +182,7 @@ def test_device_batch_validation_rejects_and_leaves_state(fault):
     good = dict(counters=(slots, vals, rates), gauges=(slots, vals), histos=(slots, vals, rates),
                 sets=(slots, off, mb))
     bad = {k: tuple(a.copy() for a in v) for k, v in good.items()}
-    i = n // 2
+    i = {"mid": n // 2 - 1, "quad_lane3": n // 2 + 1, "tail": n - 2, "misaligned": n // 2}[where]
     if fault.endswith("_slot"):
         bad[{"counter": "counters", "gauge": "gauges", "histo": "histos", "set": "sets"}[fault[:-5]]][0][i] = cap
     elif fault == "histo_nan":
@@ -191,9 +199,10 @@ def test_device_batch_validation_rejects_and_leaves_state(fault):
         bad["sets"][1][i] = bad["sets"][1][i + 1] + 1
     bufs = []
     with make_engine((cap,) * 4) as e, make_engine((cap,) * 4) as ref:
-        e.ingest_device(_device_batch(bufs, **good))
+        mis = where == "misaligned"
+        e.ingest_device(_device_batch(bufs, misalign=mis, **good))
         with pytest.raises(V.EngineError, match="out of range|invalid value|sample rate|offsets"):
-            e.ingest_device(_device_batch(bufs, **bad))
+            e.ingest_device(_device_batch(bufs, misalign=mis, **bad))
         ref.ingest(**good)
         fe, fr = e.flush(), ref.flush()
     for b in bufs:

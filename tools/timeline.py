@@ -17,9 +17,8 @@ def main(path, step=1, min_us=30.0):
     agg = defaultdict(lambda: [0, 0.0, 1e18, 0.0])
     for r in rows[lo:hi]:
         s, e = (int(r["Start_Timestamp"]) - t0) / 1e3, (int(r["End_Timestamp"]) - t0) / 1e3
-        name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("vn::", "")
-        if not name:
-            name = r["Kernel_Name"].replace("void vn::(anonymous namespace)::", "").split("(")[0]
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0]
+        name = name.replace("void ", "").replace("vn::", "")
         a = agg[(r["Stream_Id"], name[:34])]
         a[0] += 1
         a[1] += e - s
