@@ -531,25 +531,33 @@ __global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, 
 // After the (piece, top 40 value bits) sort: each run of records with equal piece and equal top
 // 40 bits (values within 2^-28 relative of each other) of at most kTieRun records is
 // insertion-sorted by the full ordered 64-bit value, stably -- the record order a full 64-bit LSD
-// sort produces.  One lane per run (its first record); every other lane returns after two
-// compares, and no lane walks more than kTieRun + 1 records.  A longer run is left to
-// k_tie_check: long runs of one repeated value (integer-valued timers) are in order already; a
-// long run that is not sets the flag for the conditional full-width re-sort.
+// sort produces.  One lane per run (its first record); no lane walks more than kTieRun + 1
+// records.  A longer run is left as it is: long runs of one repeated value (integer-valued
+// timers) are in order already; a lane that sees an adjacent pair out of full-value order inside
+// one sets *resort, and the (piece, full value) sort queued behind this kernel runs (radix_sort's
+// cond).  Sorting permutes records inside a run only, so every lane sees the same run bounds.
 constexpr uint64_t kTieRun = 64;
 #ifndef VN_TIE_RESORT
-#define VN_TIE_RESORT 1  // 0: no tie check (negative control for the near-tie test, tools/ab_variant.sh)
+#define VN_TIE_RESORT 1  // 0: no long-run check (negative control for the near-tie test, tools/ab_variant.sh)
 #endif
 __device__ __forceinline__ bool same_top(const uint64_t* A, const uint64_t* B, uint64_t a, uint64_t b) {
   return (B[a] >> 32) == (B[b] >> 32) && (A[a] >> 24) == (A[b] >> 24);
 }
-__global__ void k_fix_ties(uint64_t* __restrict__ A, uint64_t* __restrict__ B, uint64_t n) {
+__global__ void k_fix_ties(uint64_t* __restrict__ A, uint64_t* __restrict__ B, uint64_t n,
+                           uint32_t* __restrict__ resort) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i + 1 >= n) return;
   if (!same_top(A, B, i, i + 1)) return;
+  if (VN_TIE_RESORT && A[i] > A[i + 1]) {  // an inversion: does it sit in a long run?
+    uint64_t lo = i, hi = i + 1;
+    while (lo > 0 && i - lo < kTieRun && same_top(A, B, lo - 1, i)) lo--;
+    while (hi + 1 < n && hi - lo < kTieRun && same_top(A, B, i, hi + 1)) hi++;
+    if (hi - lo + 1 > kTieRun) *resort = 1u;
+  }
   if (i > 0 && same_top(A, B, i - 1, i)) return;  // not the run's first record
   uint64_t j = i + 2;
   while (j < n && j - i <= kTieRun && same_top(A, B, i, j)) j++;
-  if (j - i > kTieRun) return;  // long run: k_tie_check
+  if (j - i > kTieRun) return;  // long run: left to the re-sort (if out of order)
   for (uint64_t k = i + 1; k < j; k++) {  // stable insertion sort of [i, j) by A
     const uint64_t a = A[k], b = B[k];
     uint64_t m = k;
@@ -561,15 +569,6 @@ __global__ void k_fix_ties(uint64_t* __restrict__ A, uint64_t* __restrict__ B, u
     A[m] = a;
     B[m] = b;
   }
-}
-
-// After k_fix_ties: any adjacent pair still out of full-value order (only inside a long run) sets
-// *resort, and the (piece, full value) sort queued behind it runs (radix_sort's cond).
-__global__ void k_tie_check(const uint64_t* __restrict__ A, const uint64_t* __restrict__ B, uint64_t n,
-                            uint32_t* __restrict__ resort) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
-  if (i >= n) return;
-  if (A[i - 1] > A[i] && same_top(A, B, i - 1, i)) *resort = 1u;
 }
 
 // Per touched key: how many of its batch samples the exact replay takes, by the key's window
@@ -1374,15 +1373,13 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   uint64_t* const SB = fl2 ? e->hB2 : Bo;
   uint64_t* MA = fl2 ? Ao : e->hA2;        // per-round merged segments
   uint64_t* MB = fl2 ? Bo : e->hB2;
-  hipLaunchKernelGGL(k_fix_ties, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, SA, SB, nremrec);
   {
     // a long run out of full-value order (rare): the whole (piece, 64-bit value) sort, queued
     // behind a device flag so no host round trip decides it; an even pass count leaves the
     // result in (SA, SB) whether it runs or not (MA / MB are free until the rounds)
     uint32_t* const resort = e->h_cnt + 14;
     VN_HIP_CHECK(hipMemsetAsync(resort, 0, sizeof(uint32_t), st));
-    if (VN_TIE_RESORT)
-      hipLaunchKernelGGL(k_tie_check, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, SA, SB, nremrec, resort);
+    hipLaunchKernelGGL(k_fix_ties, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, SA, SB, nremrec, resort);
     RadixPass full[16];
     int nf = 0;
     const int npb = (pbits + 7) / 8;
