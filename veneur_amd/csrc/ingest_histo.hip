@@ -680,6 +680,8 @@ __global__ __launch_bounds__(kBlock) void k_histo_gather_hot(uint32_t ntouched, 
                                                              const uint64_t* __restrict__ B,
                                                              uint64_t* __restrict__ A2, uint64_t* __restrict__ B2) {
   __shared__ uint32_t s_k[2];
+  __shared__ uint64_t s_geo[256];  // the piece boundaries (ngeo <= 255), searched once per record
+  for (uint32_t g = threadIdx.x; g < ngeo; g += kBlock) s_geo[g] = geo[g];
   const uint64_t base = (uint64_t)blockIdx.x * kTile;
   if (threadIdx.x < 2) {
     uint64_t o = base + (threadIdx.x ? (uint64_t)kTile - 1 : 0);
@@ -695,7 +697,13 @@ __global__ __launch_bounds__(kBlock) void k_histo_gather_hot(uint32_t ntouched, 
     const uint32_t i = (uint32_t)(o - hotoff[k]);
     const uint64_t src = (uint64_t)start[tl[k]] + ex[k] + i;
     const uint64_t pos = (uint64_t)seen0[k] + ex[k] + i;  // window position of the sample
-    const uint32_t gid = pbase[k] + (geo_upper(geo, ngeo, pos) - pi0[k]);
+    uint32_t l = 0, h = ngeo;  // geo_upper over the LDS copy: first boundary above pos
+    while (l < h) {
+      const uint32_t m = (l + h) >> 1;
+      if (s_geo[m] <= pos) l = m + 1;
+      else h = m;
+    }
+    const uint32_t gid = pbase[k] + (l - pi0[k]);
     A2[o] = ordered_bits(bitsd(A[src]));
     B2[o] = ((uint64_t)gid << 32) | (B[src] & 0xffffffffull);
   }
