@@ -546,32 +546,15 @@ __device__ __forceinline__ bool same_top(const uint64_t* A, const uint64_t* B, u
 __global__ void k_fix_ties(uint64_t* __restrict__ A, uint64_t* __restrict__ B, uint64_t n,
                            uint32_t* __restrict__ resort) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t lane = threadIdx.x & 63;
-  // this record and its neighbours: one load per record, the neighbours from the adjacent lanes
-  const bool in = i < n;
-  const uint64_t a = in ? A[i] : 0, b = in ? B[i] : 0;
-  uint64_t an = (uint64_t)__shfl_down((long long)a, 1, 64), bn = (uint64_t)__shfl_down((long long)b, 1, 64);
-  uint64_t ap = (uint64_t)__shfl_up((long long)a, 1, 64), bp = (uint64_t)__shfl_up((long long)b, 1, 64);
-  if (lane == 63 && i + 1 < n) {
-    an = A[i + 1];
-    bn = B[i + 1];
-  }
-  if (lane == 0 && i > 0 && in) {
-    ap = A[i - 1];
-    bp = B[i - 1];
-  }
   if (i + 1 >= n) return;
-  auto same = [](uint64_t a1, uint64_t b1, uint64_t a2, uint64_t b2) {
-    return (b1 >> 32) == (b2 >> 32) && (a1 >> 24) == (a2 >> 24);
-  };
-  if (!same(a, b, an, bn)) return;
-  if (VN_TIE_RESORT && a > an) {  // an inversion: does it sit in a long run?
+  if (!same_top(A, B, i, i + 1)) return;
+  if (VN_TIE_RESORT && A[i] > A[i + 1]) {  // an inversion: does it sit in a long run?
     uint64_t lo = i, hi = i + 1;
     while (lo > 0 && i - lo < kTieRun && same_top(A, B, lo - 1, i)) lo--;
     while (hi + 1 < n && hi - lo < kTieRun && same_top(A, B, i, hi + 1)) hi++;
     if (hi - lo + 1 > kTieRun) *resort = 1u;
   }
-  if (i > 0 && same(ap, bp, a, b)) return;  // not the run's first record
+  if (i > 0 && same_top(A, B, i - 1, i)) return;  // not the run's first record
   uint64_t j = i + 2;
   while (j < n && j - i <= kTieRun && same_top(A, B, i, j)) j++;
   if (j - i > kTieRun) return;  // long run: left to the re-sort (if out of order)
