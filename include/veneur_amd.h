@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VN_ABI_VERSION 1
+#define VN_ABI_VERSION 2
 
 enum {
   VN_OK = 0,
@@ -62,8 +62,10 @@ typedef struct {
   uint64_t max_batch_records;       /* largest batch per class passed to one ingest call */
   uint64_t max_batch_member_bytes;  /* largest set member blob per ingest call */
   /* t-digest: a key's first `histo_exact_threshold` samples of a window replay
-   * MergingDigest's 42-sample incremental merge bit-for-bit; samples beyond it are merged
-   * in one batch per ingest (rank-error parity).  0 -> 32768; UINT32_MAX -> always exact. */
+   * MergingDigest's 42-sample incremental merge bit-for-bit (every merge of the reference,
+   * in arrival order).  0 (the default) or UINT32_MAX -> every sample of every key: the
+   * digests are the reference's.  A smaller value is the opt-in fast mode: samples beyond
+   * it are merged in geometric pieces (rank-error parity only). */
   uint32_t histo_exact_threshold;
   /* a key that passes the threshold is not bit-exact anyway: only its first
    * `histo_hot_prefix` samples are replayed exactly, the rest merge in geometric pieces
@@ -167,6 +169,12 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out);
 void vn_engine_destroy(vn_engine* eng);
 const char* vn_last_error(const vn_engine* eng);
 int vn_abi_version(void);
+/* sizeof the library's structs, so a binding built against another header revision fails at
+ * load time instead of passing a short vn_config or receiving a long vn_timing.  Returns 0
+ * for an unknown id. */
+enum { VN_STRUCT_CONFIG = 0, VN_STRUCT_BATCH = 1, VN_STRUCT_FLUSH_RESULT = 2, VN_STRUCT_TIMING = 3,
+       VN_STRUCT_SPLIT_BATCH = 4, VN_STRUCT_STAGE = 5 };
+size_t vn_struct_size(int which);
 
 int vn_stage_acquire(vn_engine* eng, vn_stage* out);
 /* stage -> HBM -> ingest; returns once the stage has been copied (it may be refilled at once) */

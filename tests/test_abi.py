@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     for s in sorted(syms):
         assert hasattr(A.lib, s), "missing export %s" % s
     assert set(A.EXPORTED) == syms
-    assert A.lib.vn_abi_version() == 1
+    assert A.lib.vn_abi_version() == 2
 
 
 def test_struct_layouts_match_header():
@@ -35,6 +35,11 @@ def test_struct_layouts_match_header():
     assert C.sizeof(A.Batch) == 16 * 8
     assert C.sizeof(A.SplitBatch) == 9 * 8
     assert C.sizeof(A.SetState) == 4 + 5 * 4
+    # and the library's own sizeof of every struct the binding passes (vn_struct_size)
+    for which, st in ((0, A.Config), (1, A.Batch), (2, A.FlushResult), (3, A.Timing), (4, A.SplitBatch),
+                      (5, A.Stage)):
+        assert A.lib.vn_struct_size(which) == C.sizeof(st), st.__name__
+    assert A.lib.vn_struct_size(99) == 0
 
 
 def test_synth_deterministic_and_thread_independent():

@@ -109,7 +109,7 @@ def test_histo_import_fixture_digest_quantiles():
 def _histo_parity(stream, n_slots, batches=1, compression=100.0, max_rank=1e-3, exact_threshold=0):
     w = run_oracle(stream, n_slots)
     counts = np.bincount(stream["h_slot"], minlength=n_slots[2])
-    thr = exact_threshold or 32768
+    thr = exact_threshold if exact_threshold and exact_threshold < 0xFFFFFFFF else 1 << 62  # 0: exact
     with make_engine(n_slots, compression=compression, max_records=max(1 << 16, len(stream["h_slot"])),
                      exact_threshold=exact_threshold) as e:
         for d in split_batches(stream, batches):
@@ -170,8 +170,13 @@ def test_histo_compression_1000_accuracy():  # histo_test.go:11-25 (delta=1000)
         m, w, st = e.read_histo(0)
         f = e.flush()
     assert f.histo_quantiles[0][0] == pytest.approx(0.5, rel=0.02)
-    assert w.sum() == len(vals)
+    # the main centroids hold every merged sample; the rest are still pending temps (178 at
+    # delta 1000), as in the reference
+    assert w.sum() == st[7] and 0 < len(vals) - w.sum() <= 178 and f.histo_stats[0][0] == len(vals)
     assert st[5] >= 0 and st[6] < 1
+    t = oracle.MergingDigest(1000.0)
+    t.add_many(vals, np.ones(len(vals)))
+    assert f.histo_quantiles[0][0] == t.quantile(0.5)
 
 
 def test_histo_signed_zero_and_negative():  # math.Min(-0, +0) = -0
@@ -357,7 +362,7 @@ def test_histo_keys_cross_threshold_across_batches(batches):
     import run's pattern): weights, min/max exact; the warm keys' rank error stays within the
     bound the single-batch scheme shows for keys just past the threshold"""
     d = V.synth(seed=25, n_keys=100, zipf_s=0.0, mix=(0, 0, 1, 0), n_samples=4_800_000)
-    _histo_parity(d, d["n_slots"], batches=batches, max_rank=3e-3)
+    _histo_parity(d, d["n_slots"], batches=batches, max_rank=3e-3, exact_threshold=32768)
 
 
 def test_histo_exact_replay_long_keys_multi_batch():
@@ -371,7 +376,7 @@ def test_histo_warm_keys_only_single_batch():
     """every key warm (E < n <= 4E) and none hot: the replay of E samples then the warm rounds,
     with no hot-prefix stream in the batch"""
     d = V.synth(seed=27, n_keys=16, zipf_s=0.0, mix=(0, 0, 1, 0), n_samples=1_280_000)
-    _histo_parity(d, d["n_slots"], batches=1, max_rank=3e-3)
+    _histo_parity(d, d["n_slots"], batches=1, max_rank=3e-3, exact_threshold=32768)
 
 
 def test_histo_warm_imports_single_batch():
@@ -379,7 +384,7 @@ def test_histo_warm_imports_single_batch():
     rng = np.random.default_rng(28)
     nk, hosts = 16, 800
     w = oracle.Worker(1, 1, nk, 1)
-    with make_engine((1, 1, nk, 1), max_records=1 << 24) as e:
+    with make_engine((1, 1, nk, 1), max_records=1 << 24, exact_threshold=32768) as e:
         for h in range(hosts):
             pay = []
             for k in range(nk):
@@ -408,7 +413,8 @@ def test_histo_duplicate_values_past_threshold():
     d = {"c_slot": np.zeros(0, np.uint32), "c_val": np.zeros(0), "c_rate": np.zeros(0, np.float32),
          "g_slot": np.zeros(0, np.uint32), "g_val": np.zeros(0), "h_slot": slot, "h_val": val, "h_rate": rate,
          "s_slot": np.zeros(0, np.uint32), "s_off": np.zeros(1, np.uint32), "s_bytes": np.zeros(0, np.uint8)}
-    _histo_parity(d, (1, 1, len(sizes), 1), batches=3, max_rank=3e-3)
+    _histo_parity(d, (1, 1, len(sizes), 1), batches=3, max_rank=3e-3, exact_threshold=32768)
+    _histo_parity(d, (1, 1, len(sizes), 1), batches=3, max_rank=0.0)  # the default: every merge replayed
 
 
 def test_histo_hot_key_near_tie_values():
@@ -426,3 +432,37 @@ def test_histo_hot_key_near_tie_values():
          "g_slot": np.zeros(0, np.uint32), "g_val": np.zeros(0), "h_slot": slot, "h_val": val, "h_rate": rate,
          "s_slot": np.zeros(0, np.uint32), "s_off": np.zeros(1, np.uint32), "s_bytes": np.zeros(0, np.uint8)}
     _histo_parity(d, (1, 1, len(sizes), 1), batches=2, exact_threshold=20000)
+
+
+def _c4_hot_stream(seed, sizes, rates=(1.0, 0.5, 0.1), noise_keys=200, noise=40_000):
+    """histo keys with the window sizes of C4's hottest timers (slots 16 / 33 / 68 / 119 / 255
+    hold 979k / 469k / 224k / 145k / 63k samples at N = 1), lognormal values, mixed sample rates,
+    interleaved with a tail of small keys"""
+    rng = np.random.default_rng(seed)
+    slot = np.concatenate([np.full(n, k, np.uint32) for k, n in enumerate(sizes)] +
+                          [rng.integers(len(sizes), len(sizes) + noise_keys, noise).astype(np.uint32)])
+    rng.shuffle(slot)
+    val = rng.lognormal(np.log(50.0), 1.0, len(slot))
+    rate = np.asarray(rates, np.float32)[rng.choice(len(rates), len(slot), p=(0.9, 0.05, 0.05)[:len(rates)])]
+    return {"c_slot": np.zeros(0, np.uint32), "c_val": np.zeros(0), "c_rate": np.zeros(0, np.float32),
+            "g_slot": np.zeros(0, np.uint32), "g_val": np.zeros(0), "h_slot": slot, "h_val": val, "h_rate": rate,
+            "s_slot": np.zeros(0, np.uint32), "s_off": np.zeros(1, np.uint32), "s_bytes": np.zeros(0, np.uint8)}
+
+
+def test_histo_c4_hot_key_sizes_exact():
+    """one 400k-sample lognormal key and keys of 250k / 145k / 63k / 40k
+    samples (the C4 slots whose quantiles the geometric merge took past 1e-3), sample rates 1 /
+    0.5 / 0.1, in two batches: the default mode replays every merge -- the four-wave long replay
+    (replay_key_fast) for these keys -- so every quantile is the reference's, bit for bit"""
+    sizes = [400_000, 250_000, 145_000, 63_000, 40_000]
+    d = _c4_hot_stream(61, sizes)
+    errs = _histo_parity(d, (1, 1, len(sizes) + 200, 1), batches=2, max_rank=0.0)
+    assert errs.shape[0] >= len(sizes)
+
+
+def test_histo_c4_hot_key_sizes_fast_mode_bound():
+    """the same keys through the opt-in fast mode (geometric pieces past 32768 samples): within
+    the 1e-3 bound only by luck of the order, so this checks the looser 3e-3 it documents"""
+    sizes = [400_000, 250_000, 145_000, 63_000, 40_000]
+    d = _c4_hot_stream(61, sizes)
+    _histo_parity(d, (1, 1, len(sizes) + 200, 1), batches=2, max_rank=3e-3, exact_threshold=32768)

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Latency of the exact replay on hot keys: one window of K keys x n samples each (lognormal,
+rate 1), ingested from HBM and flushed; reports ms per window and us per merge of the longest
+key (n / 42 merges back to back), in the default (exact) mode and, with --fast, the opt-in
+geometric mode.  Checks the quantiles against the oracle (bit-exact in exact mode).
+
+  python tools/hot_replay_bench.py --n 1000000 --keys 1
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--keys", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--fast", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    a = ap.parse_args()
+    import veneur_amd as V
+    import veneur_amd._abi as A
+    rng = np.random.default_rng(1)
+    slot = np.repeat(np.arange(a.keys, dtype=np.uint32), a.n)
+    rng.shuffle(slot)
+    val = rng.lognormal(np.log(50.0), 1.0, len(slot))
+    rate = np.ones(len(slot), np.float32)
+    pct = (0.5, 0.9, 0.99, 0.999)
+    bufs = [V.DeviceBuffer(slot), V.DeviceBuffer(val), V.DeviceBuffer(rate)]
+    with V.Engine((1, 1, a.keys, 1), percentiles=pct, max_batch_records=len(slot) + 1,
+                  exact_threshold=32768 if a.fast else 0) as e:
+        b = A.Batch()
+        b.n_histo = len(slot)
+        b.histo_slot, b.histo_value, b.histo_rate = (x.ptr.value for x in bufs)
+        times = []
+        for r in range(a.reps + 1):
+            A.lib.vn_device_synchronize(0)
+            t0 = time.perf_counter()
+            e.ingest_device(b)
+            f = e.flush()
+            A.lib.vn_device_synchronize(0)
+            times.append(time.perf_counter() - t0)
+        ms = min(times[1:]) * 1e3
+    merges = a.n // 42
+    out = {"mode": "fast" if a.fast else "exact", "keys": a.keys, "samples_per_key": a.n, "ms_window": ms,
+           "us_per_merge_longest": ms * 1e3 / max(1, merges)}
+    if not a.no_check:
+        import oracle
+        w = oracle.Worker(1, 1, a.keys, 1)
+        w.histo(slot, val, rate)
+        oq = np.array([[w.histo_quantile(k, p) for p in pct] for k in range(a.keys)])
+        out["quantiles_bit_exact"] = bool(np.array_equal(f.histo_quantiles, oq))
+    print(out, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -163,6 +163,8 @@ def _sig(name, res, *args):
 
 vp = C.c_void_p
 _sig("vn_abi_version", C.c_int)
+_sig("vn_struct_size", C.c_size_t, C.c_int)
+ABI_VERSION = 2
 _sig("vn_engine_create", C.c_int, C.POINTER(Config), C.POINTER(vp))
 _sig("vn_engine_destroy", None, vp)
 _sig("vn_last_error", C.c_char_p, vp)
@@ -274,7 +276,7 @@ _sig("vn_synth_key_counts", C.c_int, C.POINTER(SynthDevConfig), C.c_uint64, u32p
 
 # every symbol include/*.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
-    "vn_abi_version", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
+    "vn_abi_version", "vn_struct_size", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
     "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_flush_masked", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_parser_create", "vn_parser_destroy",
     "vn_parser_last_error", "vn_parse_dogstatsd_device", "vn_go_parse_float", "vn_intake_create", "vn_intake_destroy",
@@ -285,3 +287,18 @@ EXPORTED = [
     "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",
     "vn_comm_nranks", "vn_comm_allreduce", "vn_engine_set_comm", "vn_split_keys", "vn_ingest_split", "vn_split_close", "vn_split_combine",
 ]
+
+
+def _check_abi():
+    """The library must match this binding: ABI version and every struct the two share."""
+    v = lib.vn_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError("libveneur_amd.so ABI %d, binding expects %d" % (v, ABI_VERSION))
+    for which, st in ((0, Config), (1, Batch), (2, FlushResult), (3, Timing), (4, SplitBatch), (5, Stage)):
+        n = lib.vn_struct_size(which)
+        if n != C.sizeof(st):
+            raise ImportError("libveneur_amd.so struct %s is %d bytes, binding has %d" % (st.__name__, n,
+                                                                                          C.sizeof(st)))
+
+
+_check_abi()

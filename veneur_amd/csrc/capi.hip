@@ -786,6 +786,18 @@ extern "C" {
 
 int vn_abi_version(void) { return VN_ABI_VERSION; }
 
+size_t vn_struct_size(int which) {
+  switch (which) {
+    case VN_STRUCT_CONFIG: return sizeof(vn_config);
+    case VN_STRUCT_BATCH: return sizeof(vn_batch);
+    case VN_STRUCT_FLUSH_RESULT: return sizeof(vn_flush_result);
+    case VN_STRUCT_TIMING: return sizeof(vn_timing);
+    case VN_STRUCT_SPLIT_BATCH: return sizeof(vn_split_batch);
+    case VN_STRUCT_STAGE: return sizeof(vn_stage);
+    default: return 0;
+  }
+}
+
 int vn_engine_create(const vn_config* cfg, vn_engine** out) {
   if (!cfg || !out) return VN_EINVAL;
   *out = nullptr;
@@ -808,7 +820,7 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
     delete e;
     return VN_EINVAL;
   }
-  e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 32768u;
+  e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 0xFFFFFFFFu;  // exact
   e->hot_prefix = std::min(e->exact_threshold, cfg->histo_hot_prefix ? cfg->histo_hot_prefix : 4096u);
   e->piece_growth = cfg->histo_piece_growth ? std::min(cfg->histo_piece_growth, 1000u) : 25u;
   e->temp_cap = temp_buffer_cap(e->cfg.compression);

@@ -70,6 +70,7 @@ struct ExactCtx {
 };
 
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap);
+size_t exact_fast_smem_bytes(uint32_t capc, uint32_t tcap);  // the long replays' (k_histo_exact_mw)
 // max_chunks: upper bound on the pure chunks of the batch (grid of the chunk sorter)
 void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks);
 // the pure-chunk pre-sort alone, and the replay alone (over x.order when set)

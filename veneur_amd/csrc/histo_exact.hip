@@ -27,6 +27,19 @@
 
 namespace vn {
 
+#ifndef VN_EXACT_LDS_PAD
+#define VN_EXACT_LDS_PAD 0  // occupancy experiments only (tools/ab_variant.sh)
+#endif
+// LDS bytes of the replay's layout (lds_layout), on the host and the device
+__host__ __device__ inline size_t exact_smem_bytes_hd(uint32_t capc, uint32_t tcap) {
+  const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = capc + TP + 1 > 320u ? capc + TP + 1 : 320u;
+  uint32_t levels = 1;
+  while ((1u << levels) <= capc) levels++;
+  const uint32_t kin = JW <= 2 * capc ? 0 : JW;  // lds_layout: kin in the main tile when it fits
+  return sizeof(double) * (2 * capc + 4 * TP + 2 * JW + kin) + sizeof(uint16_t) * JW +
+         sizeof(uint16_t) * (levels > 9u ? levels : 9u) * JW + 16 + VN_EXACT_LDS_PAD;
+}
+
 #ifdef VN_EXACT_PROF
 // profiling build only (tools/exact_profile.py): cycles per merge phase of block 0
 __device__ unsigned long long g_exact_prof[16];
@@ -846,11 +859,29 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
   wave_lds_sync();
   const double tempW = temp_weight(tw, tcap);
   sort_temps(tv, tw, sv, sw, tcap);
-  for (uint32_t t = lane; t < tcap; t += 64) {
-    x.csv[base + t] = sv[t];
-    x.csw[base + t] = sw[t];
+  // for the long replays (replay_key_fast): the exclusive prefix of the sorted |weights| after
+  // the first record, the Add-order tempW at it (negated when a weight is not an integer)
+  bool tint = true;
+  double carry = 0.0;
+  for (uint32_t b = 0; b < tcap; b += 64) {
+    const uint32_t t = b + lane;
+    const double w = t < tcap ? __builtin_fabs(sw[t]) : 0.0;
+    tint &= is_int_weight(w);
+    double v = w;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const double o = __shfl_up(v, d, 64);
+      v = (int)lane >= d ? dadd(v, o) : v;
+    }
+    if (t < tcap) {
+      x.csv[base + t] = sv[t];
+      x.csw[base + t] = sw[t];
+      if (t) x.ctw[base + t] = dadd(carry, dsub(v, w));
+    }
+    carry = dadd(carry, rl_d(v, 63));
   }
-  if (lane == 0) x.ctw[base] = tempW;
+  tint = __all(tint);
+  if (lane == 0) x.ctw[base] = tint ? tempW : -tempW;
 }
 
 // ---- the replay: one 64-thread block (one wave) per key.  TPL = temps per lane of a chunk
@@ -965,7 +996,7 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
           cw[q] = xcsw[base + t];
         }
       }
-      ctw = xctw[base];
+      ctw = __builtin_fabs(xctw[base]);  // (negative: not all weights integers)
     };
     load(0);
     for (uint32_t c = 0; c < sp.npure; c++) {
@@ -1050,222 +1081,367 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
   }
 }
 
-// ---- four waves per key, for the longest replays (the critical path: ~780 merges back to
-// back).  The same merge, with each element of a merge on its own lane of the workgroup
-// instead of kR rounds per lane, and workgroup barriers where the single wave syncs its LDS:
-// every value below is computed exactly as in merge_sorted_fast (bit-identical results).
-constexpr int kMW = 4;
-constexpr uint32_t kMWThreads = 64 * kMW;
-constexpr uint32_t kMaxLongKeys = 4096;
-struct MwShared {  // one slot per purpose: a late wave may still read one while others move on
-  double tempW;
-  double tot[kMW];
-  uint32_t wint[kMW], mono[kMW], cnt[kMW];
-  uint32_t extra, walk_nc, walk_of, fb_nm;
-  double fb_w;
-  double red[7][kMW];
-};
-typedef __attribute__((address_space(3))) MwShared MwSharedL;
+#ifdef VN_FAST_MERGE_CHECK
+__device__ unsigned long long g_fast_dbg[64];
+extern "C" int vn_fast_dbg_read(unsigned long long* out64) {
+  return hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_fast_dbg), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
+}
+#endif
+// ---- the long replays: NW waves per key, built for the latency of ONE merge (the hottest C4
+// key replays ~23k merges back to back, so its merge latency is the window's critical path).
+// Bit-identical to merge_sorted_fast; a different dependence structure:
+//   positions     a merge-path search on each output diagonal (<= 7 steps over <= 64 temps);
+//                 the element is read straight into registers
+//   mergedWeight  no scan: with integer weights (every weight the key has seen, T <= 2^53) the
+//                 weight before output e is mp[j] + sp[i], the exclusive prefix of the j main
+//                 centroids before it (kept from the previous merge: a centroid's prefix is that
+//                 of its first element) plus that of the i sorted temps (the chunk sorter's).
+//                 Every partial sum is an exact integer, so it equals Go's running sum
+//   chain         element s surely starts a centroid when k_s - k_{s-2} > 1 ("forced"): the
+//                 centroid holding s-1 began at some c <= s-1, and with k monotone its base
+//                 k_{c-1} <= k_{s-2}.  Each forced start walks the elements up to the next
+//                 forced one exactly as mergeOne does (about 9 at delta 100), all in parallel
+//   Welford       one thread per new centroid, its end from the start masks
+// One element per thread with four waves (R = 4 / NW elements per thread in general).  A merge
+// it cannot take (non-integer weights, > 64 temps, >= 256 elements) is the one-wave merge run
+// by wave 0; a non-monotone k (an ulp wiggle of asin) takes the sequential walk of wave 0.
+typedef __attribute__((address_space(3))) uint64_t ldsu64;
 
-// requires nm + np < kMWThreads, np <= 64, capc <= kMWThreads
-__device__ __forceinline__ void merge_mw(const MergeParams x, const Lds L, uint32_t& nm, double& mainW, uint32_t np,
-                                         double tempW, MwSharedL& S) {
-  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const double T = dadd(mainW, tempW);
-  const uint32_t m = nm + np;
-  // ---- merged positions: temp t after the mains strictly below it; main t after the temps <= it
-  {
-    const double tv = L.sv[t < np ? t : 0], mv = L.mm[t < nm ? t : 0];
-    uint32_t tl = 0, th = t < np ? nm : 0, ml = 0, mh = t < nm ? np : 0;
-#pragma unroll
-    for (int it = 0; it < 8; it++) {  // nm < 256, np <= 64
-      const uint32_t tmd = (tl + th) >> 1, mmd = (ml + mh) >> 1;
-      const double tval = L.mm[tmd < nm ? tmd : 0], mval = L.sv[mmd < np ? mmd : 0];
-      const bool tgo = tl < th, tlt = tval < tv, mgo = ml < mh, mle = mval <= mv;
-      tl = (tgo && tlt) ? tmd + 1 : tl;
-      th = (tgo && !tlt) ? tmd : th;
-      ml = (mgo && mle) ? mmd + 1 : ml;
-      mh = (mgo && !mle) ? mmd : mh;
+struct FastLds {
+  ldsf64* mp;     // [capc + 2] exclusive prefix of the main centroids' weights; mp[nm] = mainW
+  ldsf64* sp;     // [TP] exclusive prefix of the sorted temps' weights; sp[np] = tempW
+  ldsf64* kk;     // [JW] k of every merged element
+  ldsu64* gmask;  // [4] start mask of each 64-element group
+  ldsf64* miscd;  // [2] 0: tempW broadcast
+  ldsu32* flag;   // [JW] start flag of every element (written by the walkers)
+  ldsu32* misc;   // [4] 0: non-monotone k seen; 1: fast path ok (integer weights); 2: temps integer
+};
+
+__host__ __device__ inline uint32_t fast_extra_bytes(uint32_t capc, uint32_t TP, uint32_t JW) {
+  return 8u * (capc + 2) + 8u * TP + 8u * JW + 8u * 4 + 8u * 2 + 4u * JW + 4u * 4 + 16u;
+}
+__device__ __forceinline__ FastLds fast_layout(char* p, uint32_t capc, uint32_t TP, uint32_t JW) {
+  FastLds F;
+  F.mp = (ldsf64*)p;
+  F.sp = F.mp + (capc + 2);
+  F.kk = F.sp + TP;
+  F.gmask = (ldsu64*)(F.kk + JW);
+  F.miscd = (ldsf64*)(F.gmask + 4);
+  F.flag = (ldsu32*)(F.miscd + 2);
+  F.misc = F.flag + JW;
+  return F;
+}
+
+template <int NW>
+__device__ __forceinline__ void fast_sync() {
+  if constexpr (NW == 1) wave_lds_sync();
+  else lds_barrier();
+}
+
+__device__ __forceinline__ uint64_t sel4(uint32_t q, uint64_t g0, uint64_t g1, uint64_t g2, uint64_t g3) {
+  return q == 0 ? g0 : (q == 1 ? g1 : (q == 2 ? g2 : g3));
+}
+
+// start flags of the m merged elements by mergeOne's sequential walk (wave 0; non-monotone k)
+__device__ void walk_flags(const FastLds F, uint32_t m, double k0) {
+  const uint32_t lane = threadIdx.x & 63;
+  double base = k0, kprev_carry = k0;
+  bool first = true;
+  for (uint32_t b = 0; b < m; b += 64) {
+    const uint32_t j = b + lane;
+    const bool valid = j < m;
+    const double kj = valid ? F.kk[j] : 0.0;
+    double kp = __shfl_up(kj, 1, 64);
+    if (lane == 0) kp = kprev_carry;
+    uint32_t from = 0;
+    uint64_t chosen = 0;
+    for (;;) {
+      const bool c = valid && lane >= from && (first || dsub(kj, base) > 1.0);
+      const uint64_t bal = __ballot(c);
+      if (!bal) break;
+      const uint32_t f = (uint32_t)__builtin_ctzll(bal);
+      chosen |= 1ull << f;
+      first = false;
+      base = rl_d(kp, (int)f);
+      from = f + 1;
     }
-    if (t < np) {
-      L.gm[t + tl] = tv;
-      L.gw[t + tl] = L.sw[t];
-    }
-    if (t < nm) {
-      L.gm[t + ml] = mv;
-      L.gw[t + ml] = L.mw[t];
-    }
+    if (valid) F.flag[j] = (uint32_t)((chosen >> lane) & 1u);
+    kprev_carry = rl_d(kj, 63);
   }
-  __syncthreads();
-  // ---- mergedWeight prefix: wave scans plus the waves' carries (integer weights: exact in any
-  // order), else wave 0 folds in Go's order; then k per element
-  const double w = t < m ? L.gw[t] : 0.0;
-  const bool wi = __all(is_int_weight(w));
-  if (lane == 0) S.wint[wv] = wi;
-  __syncthreads();
-  const bool wint = S.wint[0] && S.wint[1] && S.wint[2] && S.wint[3] && T <= 9007199254740992.0;
-  double incl;
-  if (wint) {
+}
+
+// mp[0..nm] from the main weights (wave 0); misc[1] = every weight an integer and their sum
+// equal to mainW (then every prefix is exact)
+__device__ void prefix_main_w0(const Lds L, const FastLds F, uint32_t nm, double mainW) {
+  const uint32_t lane = threadIdx.x & 63;
+  double carry = 0.0;
+  bool ok = true;
+  for (uint32_t b = 0; b < nm; b += 64) {
+    const uint32_t j = b + lane;
+    const double w = j < nm ? L.mw[j] : 0.0;
+    ok &= is_int_weight(w);
     double v = w;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const double o = __shfl_up(v, d, 64);
       v = (int)lane >= d ? dadd(v, o) : v;
     }
-    if (lane == 63) S.tot[wv] = v;
-    __syncthreads();
-    double carry = 0.0;
-    for (uint32_t i = 0; i < wv; i++) carry = dadd(carry, S.tot[i]);
-    incl = dadd(carry, v);
-  } else {
-    if (wv == 0) {
-      double run = 0.0;
-      for (uint32_t b = 0; b < m; b += 64) {
-        const double wb = b + lane < m ? L.gw[b + lane] : 0.0;
-        const uint32_t c = min(64u, m - b);
-        double mine = 0.0;
-        for (uint32_t i = 0; i < c; i++) {
-          run = dadd(run, rl_d(wb, (int)i));
-          if (i == lane) mine = run;
-        }
-        if (b + lane < m) L.kin[b + lane] = mine;
-      }
-    }
-    __syncthreads();
-    incl = t < m ? L.kin[t] : 0.0;
+    if (j < nm) F.mp[j] = dadd(carry, dsub(v, w));
+    carry = dadd(carry, rl_d(v, 63));
   }
-  const double kv = index_estimate(x.delta, ddiv(incl, T));
-  if (t < m) L.kin[t] = kv;
-  __syncthreads();
-  const double k0 = index_estimate(x.delta, 0.0);
-  const bool mo = __all(!(t >= 1 && t < m && kv < L.kin[t - 1]));
-  if (lane == 0) S.mono[wv] = mo;
-  __syncthreads();
-  const bool mono = S.mono[0] && S.mono[1] && S.mono[2] && S.mono[3];
-  uint32_t nc = 0;
-  bool overflow = false;
-  const uint32_t capc = x.capc;
-  if (mono) {
-    // next(s) for s = t (entries past m are m), then the power-of-two tables, then the starts
-    uint32_t cur;
-    {
-      const double base = t >= 1 ? L.kin[t - 1] : k0;
-      uint32_t bl = t < m ? t + 1 : m, bh = m;
+  ok = __all(ok) && carry == mainW && mainW <= 9007199254740992.0;
+  if (lane == 0) {
+    F.mp[nm] = mainW;
+    F.misc[1] = ok ? 1u : 0u;
+  }
+}
+
+// sp[0..np] from the sorted temps' weights (wave 0, np <= 64); misc[2] = all integers
+__device__ void prefix_temps_w0(const Lds L, const FastLds F, uint32_t np) {
+  const uint32_t lane = threadIdx.x & 63;
+  const double w = lane < np ? L.sw[lane] : 0.0;
+  const bool ok = __all(is_int_weight(w));
+  double v = w;
 #pragma unroll
-      for (int it = 0; it < 8; it++) {
-        const uint32_t md = (bl + bh) >> 1;
-        const double kval = L.kin[md];
-        const bool go = bl < bh, gt = dsub(kval, base) > 1.0;
-        bh = (go && gt) ? md : bh;
-        bl = (go && !gt) ? md + 1 : bl;
+  for (int d = 1; d < 64; d <<= 1) {
+    const double o = __shfl_up(v, d, 64);
+    v = (int)lane >= d ? dadd(v, o) : v;
+  }
+  const double tot = rl_d(v, 63);
+  if (lane < np) F.sp[lane] = dsub(v, w);
+  if (lane == 0) {
+    F.sp[np] = tot;
+    F.misc[2] = ok ? 1u : 0u;
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, const FastLds F, uint32_t& nm,
+                                           double& mainW, const uint32_t np, const double tempW, const double k0) {
+  constexpr int NT = 64 * NW, R = 4 / NW;
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const double T = dadd(mainW, tempW);
+  const uint32_t m = nm + np, nmc = nm ? nm - 1 : 0u;
+  double xv[R], xw[R], wb[R], kv[R];
+#ifdef VN_FAST_MERGE_CHECK
+  if (t == 0 && (F.sp[np] != tempW || F.mp[nm] != mainW || F.sp[0] != 0.0) &&
+      atomicCAS(&g_fast_dbg[32], 0ull, 1ull) == 0ull) {
+    g_fast_dbg[33] = np;
+    g_fast_dbg[34] = nm;
+    g_fast_dbg[35] = dbits(F.sp[np]);
+    g_fast_dbg[36] = dbits(tempW);
+    g_fast_dbg[37] = dbits(F.mp[nm]);
+    g_fast_dbg[38] = dbits(mainW);
+    g_fast_dbg[39] = dbits(F.sp[0]);
+  }
+#endif
+  // ---- A: the element at each output position e: i temps and e - i mains precede it
+  {
+    uint32_t lo[R], hi[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint32_t e = r * NT + t;
+      lo[r] = (e < m && e > nm) ? e - nm : 0u;
+      hi[r] = e < m ? min(e, np) : 0u;
+    }
+#pragma unroll
+    for (int it = 0; it < 7; it++) {  // hi - lo <= np <= 64
+      uint32_t md[R];
+      double a[R], b[R];
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const uint32_t e = r * NT + t;
+        md[r] = (lo[r] + hi[r]) >> 1;
+        a[r] = L.sv[md[r]];
+        b[r] = L.mm[lo[r] < hi[r] ? e - 1 - md[r] : 0u];
       }
-      L.jump16[t] = (uint16_t)bl;
-      cur = bl;
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const bool go = lo[r] < hi[r], tf = a[r] <= b[r];  // main first only if strictly smaller
+        lo[r] = (go && tf) ? md[r] + 1 : lo[r];
+        hi[r] = (go && !tf) ? md[r] : hi[r];
+      }
     }
-    __syncthreads();
-    for (uint32_t lv = 1; lv < 8; lv++) {  // t < 256: bits 0..7
-      const ldsu16* Jp = L.jump16 + (lv - 1) * L.JW;
-      const uint32_t a = Jp[cur];
-      L.jump16[lv * L.JW + t] = (uint16_t)a;
-      cur = a;
-      __syncthreads();
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint32_t e = r * NT + t, i = lo[r], j = e < m ? e - i : 0u, jc = min(j, nmc);
+      const double tv = L.sv[i], tw = L.sw[i], mv = L.mm[jc], mw = L.mw[jc];
+      const bool tk = i < np && (j >= nm || tv <= mv);
+      xv[r] = tk ? tv : mv;
+      xw[r] = tk ? tw : mw;
+      wb[r] = dadd(F.mp[min(j, nm)], F.sp[i]);
     }
-    uint32_t p = 0;
-    for (uint32_t lv = 0; lv < 8; lv++) {
-      const uint32_t nx = L.jump16[lv * L.JW + p];
-      p = ((t >> lv) & 1u) ? nx : p;
+  }
+  // ---- B: k of every element (indexEstimate of the inclusive weight)
+#pragma unroll
+  for (int r = 0; r < R; r++) kv[r] = index_estimate(x.delta, ddiv(dadd(wb[r], xw[r]), T));
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t e = r * NT + t;
+    if (e < m) {
+      L.gm[e] = xv[r];
+      L.gw[e] = xw[r];
+      F.kk[e] = kv[r];
     }
-    const bool on = p < m;
-    if (on && t < capc) L.starts[t] = p;
-    if (t == kMWThreads - 1) S.extra = (on && L.jump16[p] < m) ? 1u : 0u;  // start 256 (overflow check)
-    const uint32_t cnt = (uint32_t)__popcll(__ballot(on));
-    if (lane == 0) S.cnt[wv] = cnt;
-    __syncthreads();
-    const uint32_t raw = S.cnt[0] + S.cnt[1] + S.cnt[2] + S.cnt[3] + S.extra;
-    overflow = raw > capc;
-    nc = raw > capc ? capc : raw;
-  } else {
-    if (wv == 0) {  // the sequential walk (non-monotone k: ulp-level asin wiggle)
-      double base = k0, kprev_carry = k0;
-      uint32_t n2 = 0;
-      bool of = false;
-      for (uint32_t b = 0; b < m && !of; b += 64) {
-        const uint32_t j = b + lane;
-        const bool valid = j < m;
-        const double kj = valid ? L.kin[j] : 0.0;
-        double kp = __shfl_up(kj, 1, 64);
-        if (lane == 0) kp = kprev_carry;
-        uint32_t from = 0;
-        for (;;) {
-          const bool c = valid && lane >= from && (n2 == 0 || dsub(kj, base) > 1.0);
-          const uint64_t bal = __ballot(c);
-          if (!bal) break;
-          const uint32_t f = (uint32_t)__builtin_ctzll(bal);
-          if (n2 >= capc) {
-            of = true;
-            break;
+  }
+  if (t == 0) F.misc[0] = 0u;
+  fast_sync<NW>();
+  // ---- C: forced starts, then each one walks its segment
+  bool fr[R];
+  double km1[R];
+  {
+    bool nonmono = false;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint32_t e = r * NT + t;
+      const double a = F.kk[e >= 1 ? e - 1 : 0u], b = F.kk[e >= 2 ? e - 2 : 0u];
+      km1[r] = e >= 1 ? a : k0;
+      const double km2 = e >= 2 ? b : k0;
+      fr[r] = e < m && (e == 0 || dsub(kv[r], km2) > 1.0);
+      nonmono |= e < m && e >= 1 && kv[r] < km1[r];
+    }
+    if (__any(nonmono) && lane == 0) F.misc[0] = 1u;
+  }
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (fr[r]) {
+      const uint32_t e = r * NT + t;
+      F.flag[e] = 1u;
+      double base = km1[r], p2 = km1[r], p1 = kv[r];  // p2 = k_{j-2}, p1 = k_{j-1}
+      uint32_t j = e + 1;
+      bool run = j < m;
+      while (run) {
+        double kb[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) kb[u] = F.kk[min(j + u, m - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (run) {
+            if (j >= m || dsub(kb[u], p2) > 1.0) {
+              run = false;  // j is forced (its own thread starts it) or past the end
+            } else {
+              const bool s = dsub(kb[u], base) > 1.0;
+              F.flag[j] = s ? 1u : 0u;
+              base = s ? p1 : base;
+              p2 = p1;
+              p1 = kb[u];
+              j++;
+            }
           }
-          if (lane == 0) L.starts[n2] = b + f;
-          n2++;
-          base = rl_d(kp, (int)f);
-          from = f + 1;
         }
-        kprev_carry = rl_d(kj, 63);
-      }
-      if (lane == 0) {
-        S.walk_nc = n2;
-        S.walk_of = of ? 1u : 0u;
       }
     }
-    __syncthreads();
-    nc = S.walk_nc;
-    overflow = S.walk_of != 0;
   }
-  if (overflow && t == 0) atomicOr(x.err, 1u);
-  if (t == 0) L.starts[nc] = m;
-  __syncthreads();
-  // ---- Welford per centroid, in element order
-  if (t < nc) {
-    const uint32_t a = L.starts[t], e = L.starts[t + 1];
-    double mean = L.gm[a], W = L.gw[a];
-    for (uint32_t j = a + 1; j < e; j++) {
-      const double wt = L.gw[j];
-      W = dadd(W, wt);
-      mean = dadd(mean, ddiv(dmul(dsub(L.gm[j], mean), wt), W));
+  fast_sync<NW>();
+#ifdef VN_FAST_MERGE_CHECK
+  // debugging variant: the walkers' flags against mergeOne's sequential walk (wave 0); the first
+  // mismatch of the run is recorded in g_fast_dbg
+  {
+    bool mine[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) mine[r] = (r * NT + t) < m && F.flag[r * NT + t] != 0u;
+    fast_sync<NW>();
+    if (wv == 0) walk_flags(F, m, k0);
+    fast_sync<NW>();
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const uint32_t e = r * NT + t;
+      const bool ref = e < m && F.flag[e] != 0u;
+      if (e < m && ref != mine[r] && atomicCAS(&g_fast_dbg[0], 0ull, 1ull) == 0ull) {
+        g_fast_dbg[1] = m;
+        g_fast_dbg[2] = np;
+        g_fast_dbg[3] = e;
+        g_fast_dbg[4] = mine[r];
+        g_fast_dbg[5] = F.misc[0];
+        for (int q = 0; q < 8; q++) {
+          const int ix = (int)e - 5 + q;
+          g_fast_dbg[8 + q] = ix >= 0 && ix < (int)m ? dbits(F.kk[ix]) : 0ull;
+          g_fast_dbg[16 + q] = ix >= 0 && ix < (int)m ? F.flag[ix] : 9ull;
+          g_fast_dbg[24 + q] = ix >= 0 && ix < (int)m ? dbits(L.gw[ix]) : 0ull;
+        }
+        g_fast_dbg[6] = dbits(T);
+        g_fast_dbg[7] = dbits(kv[r]);
+      }
     }
-    L.mm[t] = mean;
-    L.mw[t] = W;
+    fast_sync<NW>();
   }
-  __syncthreads();
+#endif
+  if (F.misc[0]) {  // non-monotone k: the forced-start argument does not hold
+    if (wv == 0) walk_flags(F, m, k0);
+    fast_sync<NW>();
+  }
+  // ---- D: centroid index and end of every start, Welford over its elements
+  bool st[R];
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint32_t e = r * NT + t;
+    st[r] = e < m && F.flag[e] != 0u;
+    const uint64_t bal = __ballot(st[r]);
+    if (lane == 0) F.gmask[r * NW + wv] = bal;
+  }
+  fast_sync<NW>();
+  const uint64_t g0 = F.gmask[0], g1 = F.gmask[1], g2 = F.gmask[2], g3 = F.gmask[3];
+  const uint32_t c0 = (uint32_t)__popcll(g0), c1 = (uint32_t)__popcll(g1), c2 = (uint32_t)__popcll(g2);
+  const uint32_t nc = c0 + c1 + c2 + (uint32_t)__popcll(g3);
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    if (st[r]) {
+      const uint32_t e = r * NT + t, q = e >> 6, ln = e & 63;
+      const uint64_t gq = sel4(q, g0, g1, g2, g3);
+      const uint32_t c = (q > 0 ? c0 : 0u) + (q > 1 ? c1 : 0u) + (q > 2 ? c2 : 0u) +
+                         (uint32_t)__popcll(gq & ((1ull << ln) - 1ull));
+      const uint64_t rest = ln == 63 ? 0ull : (gq >> (ln + 1));
+      uint32_t end = m;
+      if (rest) {
+        end = e + 1 + (uint32_t)__builtin_ctzll(rest);
+      } else {
+        if (q < 3 && g3) end = 192 + (uint32_t)__builtin_ctzll(g3);
+        if (q < 2 && g2) end = 128 + (uint32_t)__builtin_ctzll(g2);
+        if (q < 1 && g1) end = 64 + (uint32_t)__builtin_ctzll(g1);
+        end = min(end, m);
+      }
+      double mean = xv[r], W = xw[r];
+      for (uint32_t j = e + 1; j < end; j++) {
+        const double wt = L.gw[j];
+        W = dadd(W, wt);
+        mean = dadd(mean, ddiv(dmul(dsub(L.gm[j], mean), wt), W));
+      }
+      L.mm[c] = mean;
+      L.mw[c] = W;
+      F.mp[c] = wb[r];
+    }
+  }
+  if (t == 0) F.mp[nc] = T;
+  fast_sync<NW>();
   nm = nc;
   mainW = T;
 }
 
-// a merge of any shape: the four-wave merge when it fits, else wave 0 runs the single-wave one
-__device__ __noinline__ NmW merge_mw_any(const MergeParams x, const Lds L, uint32_t nm, double mainW, uint32_t np,
-                                         double tempW, MwSharedL& S) {
-  if (nm + np < kMWThreads && np <= 64 && x.capc <= kMWThreads) {
-    merge_mw(x, L, nm, mainW, np, tempW, S);
-    return NmW{nm, mainW};
-  }
-  if (threadIdx.x < 64) {
-    merge_any(x, L, nm, mainW, np, tempW);
-    if (threadIdx.x == 0) {
-      S.fb_nm = nm;
-      S.fb_w = mainW;
-    }
-  }
-  __syncthreads();
-  return NmW{S.fb_nm, S.fb_w};
+constexpr int kMW = 4;
+constexpr uint32_t kMWThreads = 64 * kMW;
+constexpr uint32_t kMaxLongKeys = 4096;
+struct MwShared {  // one slot per purpose: a late wave may still read one while others move on
+  uint32_t fb_nm;
+  double fb_w;
+  double red[7][kMW];
+};
+typedef __attribute__((address_space(3))) MwShared MwSharedL;
+
+__host__ __device__ inline uint32_t fast_offset(uint32_t capc, uint32_t tcap) {
+  return ((uint32_t)exact_smem_bytes_hd(capc, tcap) + 15u) & ~15u;
 }
 
-// replay_key with four waves (tcap <= 64, ingest only: no flush-mode adoption)
-__device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwSharedL& S) {
+// replay of one key with NW waves (tcap <= 64, ingest only: no flush-mode adoption)
+template <int NW>
+__device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& S) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr uint32_t NT = 64 * NW;
+  constexpr uint32_t R = 4 / NW;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t capc = x.capc, tcap = x.tcap;
   const uint32_t TP = round64(tcap + 1);
   const Lds L = lds_layout(smem, capc, TP);
+  const FastLds F = fast_layout(smem + fast_offset(capc, tcap), capc, TP, L.JW);
 
   const MergeParams mp{x.delta, x.capc, x.err};
   const uint64_t* const xA = x.A;
@@ -1288,17 +1464,21 @@ __device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwSharedL& S)
   double mainW = h[7];
   const uint32_t lo = x.start[s];
   const ExactSplit sp = exact_split(np, nex, tcap);
-  for (uint32_t j = t; j < nm; j += kMWThreads) {
+  const double k0 = index_estimate(x.delta, 0.0);
+  for (uint32_t j = t; j < nm; j += NT) {
     L.mm[j] = cmg[j];
     L.mw[j] = cwg[j];
   }
   const double* pv = x.hpv + (uint64_t)s * tcap;
   const double* pw = x.hpw + (uint64_t)s * tcap;
-  for (uint32_t j = t; j < np; j += kMWThreads) {
+  for (uint32_t j = t; j < np; j += NT) {
     L.tv[j] = pv[j];
     L.tw[j] = pw[j];
   }
-  __syncthreads();
+  fast_sync<NW>();
+  if (wv == 0) prefix_main_w0(L, F, nm, mainW);
+  fast_sync<NW>();
+  bool fok = F.misc[1] != 0u;  // the key's weights are all integers: the fast merge applies
 
   double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf, dmn = kInf, dmx = -kInf;
   auto stat = [&](double v, double wt, bool sample) {
@@ -1312,7 +1492,7 @@ __device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwSharedL& S)
     srw = dadd(srw, dmul(ddiv(1.0, v), wt));
   };
   auto append = [&](uint32_t a, uint32_t b) {
-    for (uint32_t i = a + t; i < b; i += kMWThreads) {
+    for (uint32_t i = a + t; i < b; i += NT) {
       const double v = bitsd(xA[lo + i]);
       const uint32_t tag = (uint32_t)xB[lo + i];
       const double wt = tag_weight(tag, ximpw);
@@ -1321,20 +1501,52 @@ __device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwSharedL& S)
       stat(v, wt, tag_is_sample(tag));
     }
     np += b - a;
-    __syncthreads();
+    fast_sync<NW>();
+  };
+  // a merge of the sorted temps sv/sw (with sp when tint): the fast merge when it applies, else
+  // wave 0's one-wave merge (and the main prefix rebuilt after it)
+  auto merge_sorted_any = [&](uint32_t n_, double tempW, bool tint) {
+    const uint32_t m = nm + n_;
+#ifdef VN_FAST_MERGE_OFF
+    if (false) {  // A/B and debugging variant: every merge by wave 0's one-wave merge
+#else
+    if (fok && tint && n_ <= 64 && m < NT * R && m <= capc && dadd(mainW, tempW) <= 9007199254740992.0) {
+#endif
+      merge_fast<NW>(mp, L, F, nm, mainW, n_, tempW, k0);
+      return;
+    }
+    if (wv == 0) {
+      merge_any(mp, L, nm, mainW, n_, tempW);
+      if (lane == 0) {
+        S.fb_nm = nm;
+        S.fb_w = mainW;
+      }
+    }
+    fast_sync<NW>();
+    nm = S.fb_nm;
+    mainW = S.fb_w;
+    if (fok && tint) {
+      if (wv == 0) prefix_main_w0(L, F, nm, mainW);
+      fast_sync<NW>();
+      fok = F.misc[1] != 0u;
+    } else {
+      fok = false;
+    }
+    fast_sync<NW>();  // S and misc are read before anyone writes them again
   };
   auto merge_pend = [&]() {  // sort the pending temps (wave 0), then merge them
     if (wv == 0) {
       const double tw_ = temp_weight(L.tw, np);
       sort_temps(L.tv, L.tw, L.sv, L.sw, np);
-      if (lane == 0) S.tempW = tw_;
+      if (np <= 64) prefix_temps_w0(L, F, np);
+      else if (lane == 0) F.misc[2] = 0u;
+      if (lane == 0) F.miscd[0] = tw_;
     }
-    __syncthreads();
-    const double tempW = S.tempW;
-    __syncthreads();
-    const NmW r = merge_mw_any(mp, L, nm, mainW, np, tempW, S);
-    nm = r.nm;
-    mainW = r.w;
+    fast_sync<NW>();
+    const double tempW = F.miscd[0];
+    const bool tint = F.misc[2] != 0u;
+    fast_sync<NW>();
+    merge_sorted_any(np, tempW, tint);
   };
 
   if (nex && np == tcap) {
@@ -1349,28 +1561,33 @@ __device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwSharedL& S)
     }
   }
   if (sp.npure) {
-    double cv = 0.0, cw = 0.0, ctw = 0.0;
+    // the chunk sorter's arrays at the chunk's records: sorted means and signed weights (an
+    // imported centroid negative), and in ctw the temps' Add-order weight sum at the first
+    // record (negative when a weight is not an integer), their sorted exclusive prefix after it
+    double cv = 0.0, cw = 0.0, cp = 0.0, ctw = 0.0;
     auto load = [&](uint32_t c) {
       const uint64_t base = (uint64_t)lo + sp.off0 + (uint64_t)c * tcap;
       if (t < tcap) {
         cv = xcsv[base + t];
         cw = xcsw[base + t];
+        cp = xctw[base + t];
       }
       ctw = xctw[base];
     };
     load(0);
     for (uint32_t c = 0; c < sp.npure; c++) {
+      const double tempW = __builtin_fabs(ctw);
+      const bool tint = ctw >= 0.0;
       if (t < tcap) {
         L.sv[t] = cv;
         L.sw[t] = __builtin_fabs(cw);
+        F.sp[t] = t ? cp : 0.0;
         stat(cv, __builtin_fabs(cw), cw > 0.0);
       }
-      const double tempW = ctw;
+      if (t == tcap) F.sp[tcap] = tempW;
       if (c + 1 < sp.npure) load(c + 1);
-      __syncthreads();
-      const NmW r = merge_mw_any(mp, L, nm, mainW, tcap, tempW, S);
-      nm = r.nm;
-      mainW = r.w;
+      fast_sync<NW>();
+      merge_sorted_any(tcap, tempW, tint);
     }
   }
   const uint32_t tail = sp.off0 + sp.npure * tcap;
@@ -1379,13 +1596,13 @@ __device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwSharedL& S)
     merge_pend();
     np = 0;
   }
-  for (uint32_t j = t; j < nm; j += kMWThreads) {
+  for (uint32_t j = t; j < nm; j += NT) {
     cmg[j] = L.mm[j];
     cwg[j] = L.mw[j];
   }
   double* qv = x.hpv + (uint64_t)s * tcap;
   double* qw = x.hpw + (uint64_t)s * tcap;
-  for (uint32_t j = t; j < np; j += kMWThreads) {
+  for (uint32_t j = t; j < np; j += NT) {
     qv[j] = L.tv[j];
     qw[j] = L.tw[j];
   }
@@ -1409,9 +1626,9 @@ __device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwSharedL& S)
     S.red[5][wv] = dmn;
     S.red[6][wv] = dmx;
   }
-  __syncthreads();
+  fast_sync<NW>();
   if (t == 0) {
-    for (int q = 1; q < kMW; q++) {
+    for (int q = 1; q < NW; q++) {
       sw = dadd(sw, S.red[0][q]);
       sxw = dadd(sxw, S.red[1][q]);
       srw = dadd(srw, S.red[2][q]);
@@ -1433,14 +1650,14 @@ __device__ void replay_key_mw(const ExactCtx& x, const uint32_t k, MwSharedL& S)
       h[6] = max_go(h[6], dmx);
     }
   }
-  __syncthreads();
+  fast_sync<NW>();
   if (x.hspn) {
     uint32_t fn = 0;
     if (x.spec && !final_merge && np > 0) {
       merge_pend();
       double* fmg = (cur ? x.cm0 : x.cm1) + (uint64_t)s * capc;
       double* fwg = (cur ? x.cw0 : x.cw1) + (uint64_t)s * capc;
-      for (uint32_t j = t; j < nm; j += kMWThreads) {
+      for (uint32_t j = t; j < nm; j += NT) {
         fmg[j] = L.mm[j];
         fwg[j] = L.mw[j];
       }
@@ -1469,7 +1686,7 @@ __global__ __launch_bounds__(kMWThreads) void k_histo_exact_mw(ExactCtx x, const
   const uint32_t n = *nmw;
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t k = x.order64 ? (uint32_t)x.order64[i] : x.order ? x.order[i] : i;
-    if (k < x.nkeys) replay_key_mw(x, k, *(MwSharedL*)&S);
+    if (k < x.nkeys) replay_key_fast<kMW>(x, k, *(MwSharedL*)&S);
     __syncthreads();  // the next key reuses the LDS
   }
 }
@@ -1522,19 +1739,11 @@ void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* 
   x.order64 = radix_sort(buf0, nullptr, buf1, nullptr, n, passes, np, rs, st, nullptr) ? buf1 : buf0;
 }
 
-#ifndef VN_EXACT_LDS_PAD
-#define VN_EXACT_LDS_PAD 0  // occupancy experiments only (tools/ab_variant.sh)
-#endif
-size_t exact_smem_bytes(uint32_t capc, uint32_t tcap) {
+size_t exact_smem_bytes(uint32_t capc, uint32_t tcap) { return exact_smem_bytes_hd(capc, tcap); }
+size_t exact_fast_smem_bytes(uint32_t capc, uint32_t tcap) {
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = std::max(capc + TP + 1, 320u);
-  uint32_t levels = 1;
-  while ((1u << levels) <= capc) levels++;
-  const uint32_t kin = JW <= 2 * capc ? 0 : JW;  // lds_layout: kin in the main tile when it fits
-  return sizeof(double) * (2 * capc + 4 * TP + 2 * JW + kin) + sizeof(uint16_t) * JW +
-         sizeof(uint16_t) * std::max(levels, 9u) * JW + 16 +
-         VN_EXACT_LDS_PAD;
+  return fast_offset(capc, tcap) + fast_extra_bytes(capc, TP, JW);
 }
-
 #ifdef VN_EXACT_PROF
 extern "C" int vn_prof_exact_read(unsigned long long* out16, int reset) {
   if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_exact_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
@@ -1560,7 +1769,8 @@ void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uin
 
 bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipStream_t st) {
   x.mw_count = nullptr;
-  if (!x.order64 || !x.norder || x.tcap > 64 || x.capc > kMWThreads || x.flush_mode) return false;
+  if (!x.order64 || !x.norder || x.tcap > 64 || x.flush_mode) return false;
+  if (exact_fast_smem_bytes(x.capc, x.tcap) > 160 * 1024) return false;
   hipLaunchKernelGGL(k_exact_count_long, dim3(1), dim3(1), 0, st, x.norder, x.order64, min_len,
                      std::min<uint32_t>(x.norder, kMaxLongKeys), count);
   x.mw_count = count;
@@ -1570,7 +1780,7 @@ bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipS
 void histo_exact_replay_long(const ExactCtx& x, hipStream_t st) {
   if (!x.mw_count) return;
   hipLaunchKernelGGL(k_histo_exact_mw, dim3(std::min<uint32_t>(x.norder, kMaxLongKeys / 2)), dim3(kMWThreads),
-                     exact_smem_bytes(x.capc, x.tcap), st, x, x.mw_count);
+                     exact_fast_smem_bytes(x.capc, x.tcap), st, x, x.mw_count);
 }
 
 void histo_exact_replay(const ExactCtx& x, hipStream_t st) {

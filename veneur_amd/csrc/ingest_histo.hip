@@ -1307,11 +1307,13 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
     if (a && b) VN_HIP_CHECK(hipEventRecord(b, s));
     if (e->timing) e->kstat_rp.launches++;
   };
-  // the longest keys (a quarter of the threshold and more) replay with four waves each on st5,
-  // beside the one-wave replay of the rest on the same CUs
+  // the longest keys (a quarter of the threshold, at most 8192 samples, and more) replay with
+  // four waves each on st5 (replay_key_fast: built for one merge's latency), beside the one-wave
+  // replay of the rest on the same CUs
   auto replay_cold = [&](hipStream_t s, RadixScratch& rs) {
     histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
-    const uint32_t min_len = e->long_replay ? e->long_replay : std::max<uint32_t>(e->exact_threshold / 4, 1024u);
+    const uint32_t min_len =
+        e->long_replay ? e->long_replay : std::min<uint32_t>(std::max<uint32_t>(e->exact_threshold / 4, 1024u), 8192u);
     const bool longk = histo_exact_count_long(xc, min_len, e->h_cnt + 15, s);
     const bool side5 = longk && !e->timing && e->st5;
     hipEvent_t a = e->timing ? e->pool_rp.next() : nullptr, b = e->timing ? e->pool_rp.next() : nullptr;

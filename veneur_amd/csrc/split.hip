@@ -551,7 +551,9 @@ void split_histos(vn_engine* e, vn_comm* c) {
   if (!H) return;
   const int N = c->nranks, me = c->rank;
   const uint64_t n = S.nh;
-  const uint32_t P = e->hot_prefix;
+  // the exact mode (the default) gathers every record of a split key to its owner, in window
+  // order, and replays all of them: the owner's digest is the one a single consumer builds
+  const uint32_t P = e->exact_threshold == 0xFFFFFFFFu ? 0xFFFFFFFFu : e->hot_prefix;
   const uint32_t G = e->n_geo;
   if ((uint64_t)H * G >= (1ull << 31)) throw std::invalid_argument("too many split histograms");
   const int kb = bits_for_n(H);
