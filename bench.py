@@ -41,11 +41,18 @@ def log(rank, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def hot_keys(counts, scale, classes, thr_cs, thr_set, max_split):
-    """Top keys by window count above the class threshold (counters and timers: a share of the
-    per-GPU load; sets: also any key that would keep one workgroup busy for long)."""
+def hot_keys(counts, scale, classes, thr_cs, thr_set, max_split, split_histos=False):
+    """Top keys by window count above the class threshold (counters: a share of the per-GPU
+    load; sets: also any key that would keep one workgroup busy for long).  Timers only in the
+    opt-in fast mode: the default exact mode replays every merge of a key on its owner, so a
+    split timer would only move its records there."""
     from veneur_amd.dist import hot_keys as pick
-    return pick(counts.astype(np.float64) * scale, classes, {0: thr_cs, 2: thr_cs, 3: thr_set}, max_split)
+    thr = {0: thr_cs, 3: thr_set}
+    if split_histos:
+        thr[2] = thr_cs
+    out = pick(counts.astype(np.float64) * scale, classes, thr, max_split)
+    out.setdefault(2, np.zeros(0, np.uint32))
+    return out
 
 
 def key_classes(seed, n_keys, mix=(0.4, 0.2, 0.25, 0.15)):
@@ -326,7 +333,9 @@ def main():
     ap.add_argument("--set-hot", type=int, default=1 << 18, help="split a set key above this many records")
     ap.add_argument("--max-split", type=int, default=64, help="split keys per class at most")
     ap.add_argument("--no-split", action="store_true", help="route every key by digest %% N (no hot keys)")
-    ap.add_argument("--exact-threshold", type=int, default=0)
+    ap.add_argument("--exact-threshold", type=int, default=0,
+                    help="0 (default): every histogram merge replayed exactly; N: the opt-in fast mode "
+                         "(geometric pieces past N samples per key, rank-error parity only)")
     ap.add_argument("--hot-prefix", type=int, default=0,
                     help="exact window prefix of keys past 4x the exact threshold (0: the engine's default)")
     ap.add_argument("--piece-growth", type=int, default=0, help="geometric piece growth in %% (0: default)")
@@ -375,7 +384,8 @@ def main():
         counts = V.synth_key_counts(args.seed, args.keys, args.samples, sample, device=local_rank)
         classes = key_classes(args.seed, args.keys)
         thr = args.samples / ((args.sim_world if sim else world) * args.hot_div)
-        split = hot_keys(counts, args.samples / sample, classes, thr, min(thr, args.set_hot), args.max_split)
+        split = hot_keys(counts, args.samples / sample, classes, thr, min(thr, args.set_hot), args.max_split,
+                         split_histos=args.exact_threshold > 0)
     stream = V.DeviceStream(args.seed, args.keys, args.samples, args.sim_rank if sim else rank,
                             args.sim_world if sim else world, device=local_rank, split=split)
     n_slots = stream.n_slots
@@ -520,7 +530,11 @@ def main():
         "dtype": "f64/u64",
         "data": "synthetic (one global DogStatsD-shaped C4 stream generated in HBM, seeded)",
         "config": {"workload": "C4 mixed counters/gauges/timers/sets, %d keys, %d samples per flush window over %d "
-                               "GPU(s), Zipf(1.0), hot keys split" % (args.keys, args.samples, world),
+                               "GPU(s), Zipf(1.0), hot counter/set keys split, %s" % (
+                                   args.keys, args.samples, world,
+                                   "t-digest fast mode (geometric pieces past %d samples)" % args.exact_threshold
+                                   if args.exact_threshold else "every t-digest merge replayed exactly"),
+                   "histo_mode": "fast" if args.exact_threshold else "exact",
                    "keys": args.keys, "samples_per_window": args.samples, "percentiles": list(PCT),
                    "compression": 100, "hll_precision": 14,
                    "parallelism": "key-sharded FNV %% %d + %d split hot keys (RCCL)" %
@@ -624,6 +638,8 @@ def main():
         rng = np.random.default_rng(7)
         split_h = set((stream.split_slot0[2] + np.arange(len(split[2]))).tolist())
         cnt = np.bincount(d["h_slot"], minlength=n_slots[2])
+        # (the exact mode approximates nothing; its keys past 32768 samples -- the ones the fast
+        # mode would take through geometric pieces -- are all checked)
         big = set(np.nonzero(cnt > (args.exact_threshold or 32768))[0].tolist())
         pick = np.array(sorted(split_h | big | set(rng.choice(h_slot, min(args.parity_keys, len(h_slot)),
                                                               replace=False).tolist())), np.uint32)

@@ -476,3 +476,64 @@ def test_import_chunk_batches_per_class_and_skips_bad_payloads(caplog):
     assert ok == [[0], [1], [3]]  # the failing batch retried one by one, the bad one skipped
     assert "Could not merge histograms" in caplog.text
     assert w2.imported == 4
+
+
+def test_flush_reports_worker_self_metrics():  # worker.go:286-295
+    w = cpu_worker()
+    w.ProcessMetric(W.UDPMetric(K("a", "counter"), 1.0))
+    w.ProcessMetric(W.UDPMetric(K("b", "counter"), 2.0))
+    w.ImportMetric(W.JSONMetric(K("c", "counter"), [], struct.pack("<q", 9)))
+    w.Flush()
+    calls = w.stats.calls
+    assert [c[:2] for c in calls] == [("timing", "flush.worker_duration_ns"),
+                                     ("count", "worker.metrics_processed_total"),
+                                     ("count", "worker.metrics_imported_total")]
+    assert calls[0][2] > 0 and calls[0][3] is None and calls[0][4] == 1.0
+    assert calls[1][2:] == (2, [], 1.0) and calls[2][2:] == (1, [], 1.0)
+    assert w.processed == 0 and w.imported == 0
+    w.Flush()  # an empty window reports zeros
+    assert calls[-2][2] == 0 and calls[-1][2] == 0
+
+
+def test_flush_self_metrics_through_a_statsd_client():
+    class Client:
+        def __init__(self):
+            self.seen = []
+
+        def TimeInMilliseconds(self, name, value, tags, rate):
+            self.seen.append(name)
+
+        def Count(self, name, value, tags, rate):
+            self.seen.append((name, value))
+
+    c = Client()
+    w = W.Worker(engine=RecordingEngine(), batch_records=1000, stats=c)
+    w.ProcessMetric(W.UDPMetric(K("a", "counter"), 1.0))
+    w.Flush()
+    assert c.seen == ["flush.worker_duration_ns", ("worker.metrics_processed_total", 1),
+                      ("worker.metrics_imported_total", 0)]
+
+
+def test_counter_gauge_payload_longer_than_8_bytes():  # binary.Read takes the first 8 (samplers.go:171-183)
+    w = cpu_worker()
+    w.ImportMetric(W.JSONMetric(K("c", "counter"), [], struct.pack("<q", 7) + b"\x99"))
+    w.ImportMetric(W.JSONMetric(K("g", "gauge"), [], struct.pack("<d", 2.5) + b"\x01\x02"))
+    w.import_chunk([W.JSONMetric(K("c", "counter"), [], struct.pack("<q", 5) + b"\x00")])
+    imp = [c for c in w.engine.calls if c[0].startswith("import")]
+    assert imp == [("import_counters", [0], [7]), ("import_gauges", [0], [2.5]), ("import_counters", [0], [5])]
+    assert w.Flush().global_counters[K("c", "counter")].value == 12
+
+
+def test_rejected_batch_is_dropped_not_resubmitted(caplog):
+    class Rejecting(RecordingEngine):
+        def ingest(self, **kw):
+            self.calls.append(("ingest",))
+            raise EngineError("slot out of range (rc=-1)")
+
+    w = W.Worker(engine=Rejecting(), batch_records=2)
+    for i in range(5):
+        w.ProcessMetric(W.UDPMetric(K("a%d" % i, "counter"), 1.0))
+    # batches of 2 rejected twice; the fifth record still staged, the stage never grows past 2
+    assert w.dropped == 4 and w._staged == 1 and "dropping a batch" in caplog.text
+    w.Flush()
+    assert w.dropped == 5 and [c[0] for c in w.engine.calls].count("ingest") == 3

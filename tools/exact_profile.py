@@ -55,4 +55,7 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
 
 
 if __name__ == "__main__":
-    run(32768, 0, 0)
+    # one hot key: with the default (exact) engine it replays on the four-wave kernel, whose
+    # phases are A = merge-path positions + weight prefix, B = k values, C = forced starts and
+    # walks, D = masks + Welford (merge_fast); the one-wave kernel reports the old phase names
+    run(int(sys.argv[1]) if len(sys.argv) > 1 else 1000000, 0, 0)

@@ -43,7 +43,14 @@ __host__ __device__ inline size_t exact_smem_bytes_hd(uint32_t capc, uint32_t tc
 #ifdef VN_EXACT_PROF
 // profiling build only (tools/exact_profile.py): cycles per merge phase of block 0
 __device__ unsigned long long g_exact_prof[16];
-#define PROF_T(v) const long long v = clock64()
+__device__ __forceinline__ long long prof_stamp() {  // a scheduling fence around the stamp
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return (long long)t;
+}
+#define PROF_T(v) const long long v = prof_stamp()
 #define PROF_ADD(i, a, b) \
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_exact_prof[i], (unsigned long long)((b) - (a)))
 #else
@@ -1220,6 +1227,7 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
                                            double& mainW, const uint32_t np, const double tempW, const double k0) {
   constexpr int NT = 64 * NW, R = 4 / NW;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  PROF_T(f0);
   const double T = dadd(mainW, tempW);
   const uint32_t m = nm + np, nmc = nm ? nm - 1 : 0u;
   double xv[R], xw[R], wb[R], kv[R];
@@ -1235,7 +1243,10 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
     g_fast_dbg[39] = dbits(F.sp[0]);
   }
 #endif
-  // ---- A: the element at each output position e: i temps and e - i mains precede it
+  // ---- A: the element at each output position e: i temps and e - i mains precede it.
+  // i is the number of p in [lo, hi) with P(p) = "temp p precedes main e-1-p" (true below i):
+  // a four-way search, three probes per step (hi - lo <= 64 -> 16 -> 4 -> 1 -> 0: three steps
+  // settle it), then one read of the element
   {
     uint32_t lo[R], hi[R];
 #pragma unroll
@@ -1245,21 +1256,32 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
       hi[r] = e < m ? min(e, np) : 0u;
     }
 #pragma unroll
-    for (int it = 0; it < 7; it++) {  // hi - lo <= np <= 64
-      uint32_t md[R];
-      double a[R], b[R];
+    for (int it = 0; it < 3; it++) {
+      uint32_t p1[R], p2[R], p3[R];
+      double a1[R], a2[R], a3[R], b1[R], b2[R], b3[R];
 #pragma unroll
       for (int r = 0; r < R; r++) {
-        const uint32_t e = r * NT + t;
-        md[r] = (lo[r] + hi[r]) >> 1;
-        a[r] = L.sv[md[r]];
-        b[r] = L.mm[lo[r] < hi[r] ? e - 1 - md[r] : 0u];
+        const uint32_t e = r * NT + t, len = hi[r] - lo[r];
+        p1[r] = lo[r] + (len >> 2);
+        p2[r] = lo[r] + (len >> 1);
+        p3[r] = lo[r] + ((3u * len) >> 2);
+        const bool go = len > 0;  // then every probe p < hi <= e, and e - 1 - p < nm
+        a1[r] = L.sv[p1[r]];
+        a2[r] = L.sv[p2[r]];
+        a3[r] = L.sv[p3[r]];
+        b1[r] = L.mm[go ? e - 1 - p1[r] : 0u];
+        b2[r] = L.mm[go ? e - 1 - p2[r] : 0u];
+        b3[r] = L.mm[go ? e - 1 - p3[r] : 0u];
       }
 #pragma unroll
       for (int r = 0; r < R; r++) {
-        const bool go = lo[r] < hi[r], tf = a[r] <= b[r];  // main first only if strictly smaller
-        lo[r] = (go && tf) ? md[r] + 1 : lo[r];
-        hi[r] = (go && !tf) ? md[r] : hi[r];
+        if (hi[r] > lo[r]) {  // main first only if strictly smaller: temp p precedes iff a <= b
+          const bool q1 = a1[r] <= b1[r], q2 = a2[r] <= b2[r], q3 = a3[r] <= b3[r];
+          const uint32_t nlo = q3 ? p3[r] + 1 : (q2 ? p2[r] + 1 : (q1 ? p1[r] + 1 : lo[r]));
+          const uint32_t nhi = q3 ? hi[r] : (q2 ? p3[r] : (q1 ? p2[r] : p1[r]));
+          lo[r] = nlo;
+          hi[r] = nhi;
+        }
       }
     }
 #pragma unroll
@@ -1272,6 +1294,7 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
       wb[r] = dadd(F.mp[min(j, nm)], F.sp[i]);
     }
   }
+  PROF_T(f1);
   // ---- B: k of every element (indexEstimate of the inclusive weight)
 #pragma unroll
   for (int r = 0; r < R; r++) kv[r] = index_estimate(x.delta, ddiv(dadd(wb[r], xw[r]), T));
@@ -1286,6 +1309,7 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
   }
   if (t == 0) F.misc[0] = 0u;
   fast_sync<NW>();
+  PROF_T(f2);
   // ---- C: forced starts, then each one walks its segment
   bool fr[R];
   double km1[R];
@@ -1307,28 +1331,38 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
     if (fr[r]) {
       const uint32_t e = r * NT + t;
       F.flag[e] = 1u;
+      // walk: element j starts a centroid when k_j - base > 1 (base = k before the current
+      // centroid's first element); it stops at the next forced element (k_j - k_{j-2} > 1),
+      // whose own thread starts it.  Eight k values per LDS round trip; the forced tests of a
+      // batch do not depend on base, only the start tests chain through it.
       double base = km1[r], p2 = km1[r], p1 = kv[r];  // p2 = k_{j-2}, p1 = k_{j-1}
       uint32_t j = e + 1;
       bool run = j < m;
       while (run) {
-        double kb[4];
+        double kb[8];
 #pragma unroll
-        for (int u = 0; u < 4; u++) kb[u] = F.kk[min(j + u, m - 1)];
+        for (int u = 0; u < 8; u++) kb[u] = F.kk[min(j + u, m - 1)];
+        bool frc[8];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < 8; u++) {
+          const double k2 = u == 0 ? p2 : (u == 1 ? p1 : kb[u - 2]);
+          frc[u] = j + u >= m || dsub(kb[u], k2) > 1.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
           if (run) {
-            if (j >= m || dsub(kb[u], p2) > 1.0) {
-              run = false;  // j is forced (its own thread starts it) or past the end
+            if (frc[u]) {
+              run = false;
             } else {
-              const bool s = dsub(kb[u], base) > 1.0;
-              F.flag[j] = s ? 1u : 0u;
-              base = s ? p1 : base;
-              p2 = p1;
-              p1 = kb[u];
+              const bool st_ = dsub(kb[u], base) > 1.0;
+              F.flag[j] = st_ ? 1u : 0u;
+              base = st_ ? (u == 0 ? p1 : kb[u - 1]) : base;
               j++;
             }
           }
         }
+        p2 = kb[6];
+        p1 = kb[7];
       }
     }
   }
@@ -1370,6 +1404,7 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
     if (wv == 0) walk_flags(F, m, k0);
     fast_sync<NW>();
   }
+  PROF_T(f3);
   // ---- D: centroid index and end of every start, Welford over its elements
   bool st[R];
 #pragma unroll
@@ -1401,7 +1436,21 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
         end = min(end, m);
       }
       double mean = xv[r], W = xw[r];
-      for (uint32_t j = e + 1; j < end; j++) {
+      double gv[4], gw[4];  // the next four elements, loaded at once
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t ix = min(e + 1 + u, m - 1);
+        gv[u] = L.gm[ix];
+        gw[u] = L.gw[ix];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (e + 1 + u < end) {
+          W = dadd(W, gw[u]);
+          mean = dadd(mean, ddiv(dmul(dsub(gv[u], mean), gw[u]), W));
+        }
+      }
+      for (uint32_t j = e + 5; j < end; j++) {
         const double wt = L.gw[j];
         W = dadd(W, wt);
         mean = dadd(mean, ddiv(dmul(dsub(L.gm[j], mean), wt), W));
@@ -1413,11 +1462,22 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
   }
   if (t == 0) F.mp[nc] = T;
   fast_sync<NW>();
+  PROF_T(f4);
+  PROF_ADD(1, f0, f1);
+  PROF_ADD(2, f1, f2);
+  PROF_ADD(3, f2, f3);
+  PROF_ADD(4, f3, f4);
+  PROF_ADD(5, 0, 1);
+  PROF_ADD(6, 0, (long long)m);
+  PROF_ADD(7, 0, (long long)nc);
   nm = nc;
   mainW = T;
 }
 
-constexpr int kMW = 4;
+#ifndef VN_LONG_NW
+#define VN_LONG_NW 4  // waves per long replay (A/B variants: 1, 2, 4)
+#endif
+constexpr int kMW = VN_LONG_NW;
 constexpr uint32_t kMWThreads = 64 * kMW;
 constexpr uint32_t kMaxLongKeys = 4096;
 struct MwShared {  // one slot per purpose: a late wave may still read one while others move on

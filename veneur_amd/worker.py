@@ -328,6 +328,21 @@ class _Window:
         return s
 
 
+class WorkerStats:
+    """The two calls Worker.Flush makes on its statsd client (worker.go:286-295), recorded:
+    ("timing" | "count", name, value, tags, rate) per call, in call order.  Pass any object with
+    the same two methods (a statsd client) as Worker(stats=...) to send them instead."""
+
+    def __init__(self):
+        self.calls = []
+
+    def TimeInMilliseconds(self, name, value, tags, rate):
+        self.calls.append(("timing", name, float(value), tags, rate))
+
+    def Count(self, name, value, tags, rate):
+        self.calls.append(("count", name, int(value), tags, rate))
+
+
 class Worker:
     """veneur Worker (worker.go) whose samplers live in HBM.
 
@@ -336,8 +351,10 @@ class Worker:
     computes (0.5 is always added for the median aggregate)."""
 
     def __init__(self, id=0, capacity=(1 << 16, 1 << 16, 1 << 16, 1 << 16), percentiles=(0.5, 0.9, 0.99),
-                 batch_records=1 << 16, engine=None, **engine_kw):
+                 batch_records=1 << 16, engine=None, stats=None, **engine_kw):
         self.id = id
+        # the worker's own statsd client (worker.go:30,286-295); a WorkerStats recorder by default
+        self.stats = stats if stats is not None else WorkerStats()
         pct = tuple(sorted(set(float(p) for p in percentiles) | {0.5}))
         if engine is None:
             from .engine import Engine
@@ -382,8 +399,15 @@ class Worker:
             off = np.zeros(len(mem) + 1, np.uint32)
             off[1:] = np.cumsum([len(m) for m in mem])
             kw["sets"] = (np.array(self._s[0], np.uint32), off, np.frombuffer(b"".join(mem) or b"\0", np.uint8))
-        self.engine.ingest(**kw)
-        self._reset_stage()  # only once the engine took the batch
+        from .engine import EngineError
+        try:
+            self.engine.ingest(**kw)
+        except EngineError as err:
+            # a batch the engine rejects is dropped and counted, never resubmitted: one bad batch
+            # must not block every later ProcessMetric and the window's flush
+            self.dropped += self._staged
+            log.error("dropping a batch of %d staged samples: %s", self._staged, err)
+        self._reset_stage()
 
     # ------------------------------------------------------------ the reference's operations
     def process_metric(self, m: UDPMetric):
@@ -453,14 +477,18 @@ class Worker:
         cls = _MAPS[map_name][0]
         from .engine import EngineError
         try:
+            # Counter/Gauge.Combine decode with binary.Read, which reads the first 8 bytes and
+            # fails only on a shorter payload (samplers.go:171-183, 237-249)
             if cls == 0:
-                if len(other.value) != 8:
-                    raise EngineError("counter payload is %d bytes, not 8" % len(other.value))
-                self.engine.import_counters(np.array([slot], np.uint32), np.array(struct.unpack("<q", other.value)))
+                if len(other.value) < 8:
+                    raise EngineError("counter payload is %d bytes, fewer than 8" % len(other.value))
+                self.engine.import_counters(np.array([slot], np.uint32),
+                                            np.array(struct.unpack("<q", bytes(other.value[:8]))))
             elif cls == 1:
-                if len(other.value) != 8:
-                    raise EngineError("gauge payload is %d bytes, not 8" % len(other.value))
-                self.engine.import_gauges(np.array([slot], np.uint32), np.array(struct.unpack("<d", other.value)))
+                if len(other.value) < 8:
+                    raise EngineError("gauge payload is %d bytes, fewer than 8" % len(other.value))
+                self.engine.import_gauges(np.array([slot], np.uint32),
+                                          np.array(struct.unpack("<d", bytes(other.value[:8]))))
             elif cls == 2:
                 self.engine.import_histos(np.array([slot], np.uint32), [bytes(other.value)])
             else:
@@ -487,18 +515,20 @@ class Worker:
                 continue
             slot = self._win.upsert(map_name, m.key, m.tags, self.capacity)
             cls = _MAPS[map_name][0]
-            if cls in (0, 1) and len(m.value) != 8:
-                log.error("Could not merge %s: payload is %d bytes, not 8", map_name.replace("global_", ""),
+            if cls in (0, 1) and len(m.value) < 8:
+                log.error("Could not merge %s: payload is %d bytes, fewer than 8", map_name.replace("global_", ""),
                           len(m.value))
                 continue
             groups[cls].append((slot, m, map_name))
         self._drain()  # samples staged before the chunk are aggregated first
         if groups[0]:
             self.engine.import_counters(np.array([g[0] for g in groups[0]], np.uint32),
-                                        np.array([struct.unpack("<q", g[1].value)[0] for g in groups[0]], np.int64))
+                                        np.array([struct.unpack("<q", bytes(g[1].value[:8]))[0] for g in groups[0]],
+                                                 np.int64))
         if groups[1]:
             self.engine.import_gauges(np.array([g[0] for g in groups[1]], np.uint32),
-                                      np.array([struct.unpack("<d", g[1].value)[0] for g in groups[1]], np.float64))
+                                      np.array([struct.unpack("<d", bytes(g[1].value[:8]))[0] for g in groups[1]],
+                                               np.float64))
         for cls, fn in ((2, self.engine.import_histos), (3, self.engine.import_sets)):
             items = groups[cls]
             if not items:
@@ -520,6 +550,7 @@ class Worker:
         and flushes no mixed-scope sets (flusher.go:41-48,181-211) -- the engine then skips
         those quantiles and estimates (vn_flush_masked); need_median keeps the quantiles, as
         Histo.Flush evaluates Quantile(0.5) for the median aggregate regardless."""
+        start = time.perf_counter_ns()
         self._drain()
         win = self._take_window()
         payload = {}
@@ -535,9 +566,19 @@ class Worker:
             f = self.engine.flush(histo_quantile_mask=qmask, set_estimate_mask=emask)
         else:
             f = self.engine.flush()
+        wm = self._worker_metrics(win, f, payload)
+        self._flush_stats(start)
+        return wm
+
+    def _flush_stats(self, start):
+        """The end of Worker.Flush (worker.go:286-295): reset processed/imported and report the
+        flush's duration and the window's counts through the worker's statsd client."""
+        processed, imported = self.processed, self.imported
         self.processed = 0
         self.imported = 0
-        return self._worker_metrics(win, f, payload)
+        self.stats.TimeInMilliseconds("flush.worker_duration_ns", float(time.perf_counter_ns() - start), None, 1.0)
+        self.stats.Count("worker.metrics_processed_total", processed, [], 1.0)
+        self.stats.Count("worker.metrics_imported_total", imported, [], 1.0)
 
     def _take_window(self):
         """The map swap of Worker.Flush (worker.go:277-284): the window's interned keys, and a
@@ -564,6 +605,7 @@ class Worker:
         (http/http.go:116-135) in C++, with no per-key Python objects.  Returns ([(ok, body)],
         (n_intermetrics, n_metrics))."""
         aggregates = aggregates or DEFAULT_AGGREGATES
+        start = time.perf_counter_ns()
         self._drain()
         win = self._take_window()
         if is_local:
@@ -571,8 +613,7 @@ class Worker:
             f = self.engine.flush_raw(histo_quantile_mask=qm, set_estimate_mask=em)
         else:
             f = self.engine.flush_raw()
-        self.processed = 0
-        self.imported = 0
+        self._flush_stats(start)
         return sink.bodies(f, win.maps, self.percentiles, histogram_percentiles, aggregates, is_local, timestamp)
 
     def _worker_metrics(self, win, f, payload):
