@@ -104,52 +104,68 @@ def rank_error_stats(d, slots, eng_q, ref_q):
 def c5_leg(args, rank):
     """C5 (BASELINE configs[4]): a global veneur merging every host's forwarded digests and
     sketches -- ImportMetric -> Histo.Combine / Set.Combine (worker.go:230-268) for each of
-    `hosts` hosts x (histo_keys GobEncode()d digests + set_keys MarshalBinary()d sketches);
-    every key arrives from every host.  The hosts are `distinct` local windows of ~100 timer
-    samples per key (and Pareto-sized sets), ingested and exported by a local engine (device
-    gob / marshal encoders), then cycled host after host; payloads resident in HBM, imported
-    with vn_import_*_device and flushed.  Parity on sampled keys against the restated Go
-    (oracle Worker.ImportMetric in the same order): digest weight/min/max exact, set
-    estimates exact, quantiles by rank error over the imported centroids."""
+    `hosts` DISTINCT hosts x (histo_keys GobEncode()d digests + set_keys MarshalBinary()d
+    sketches); every key arrives from every host.  Each host's local window (~100 timer samples
+    per key, Lomax-sized sets; vn_synth_hosts_device) is generated, ingested and exported on the
+    GPU in groups of c5_group hosts (one local engine per group); the payloads stay in HBM,
+    concatenated host-major.  One window = ONE vn_import_histos_device and ONE
+    vn_import_sets_device call over all hosts' payloads, then vn_flush.  Parity on sampled keys
+    against the restated Go (oracle Worker.ImportMetric of the same payloads in the same host
+    order): digest weight/min/max exact, set estimates exact, quantiles bit-exact (the default
+    exact mode) -- rank error over the imported centroids reported as well."""
+    import ctypes as C
+
     import oracle
     import veneur_amd as V
     import veneur_amd._abi as A
+    H, S, hosts, G = args.c5_histo_keys, args.c5_set_keys, args.c5_hosts, max(1, args.c5_group)
     rng = np.random.default_rng(args.seed + 5)
-    H, S, D, hosts = args.c5_histo_keys, args.c5_set_keys, args.c5_distinct, args.c5_hosts
+    kh = np.sort(rng.choice(H, min(H, args.c5_parity_keys), replace=False))
+    ks = np.sort(rng.choice(S, min(S, args.c5_parity_keys), replace=False))
     t0 = time.time()
-    hp, sp = [], []
-    with V.Engine((1, 1, H, S), percentiles=PCT, max_batch_records=1 << 23, max_batch_member_bytes=1 << 20) as loc:
-        for d in range(D):
-            cnt = rng.integers(50, 151, H)
-            hs = np.repeat(np.arange(H, dtype=np.uint32), cnt)
-            rng.shuffle(hs)
-            hv = np.exp(rng.normal(3.9 + 0.05 * d, 1.0, len(hs)))
-            hr = np.where(rng.random(len(hs)) < 0.1, np.float32(0.5), np.float32(1.0)).astype(np.float32)
-            sc = np.minimum((rng.pareto(1.2, S) * 50 + 1).astype(np.int64), 20000)
-            ss = np.repeat(np.arange(S, dtype=np.uint32), sc)
-            sh = rng.integers(0, 2 ** 63, len(ss), dtype=np.uint64) * np.uint64(2) + \
-                rng.integers(0, 2, len(ss), dtype=np.uint64)
-            loc.ingest(histos=(hs, hv, hr), set_hashes=(ss, sh))
-            hp.append(loc.export_raw(2, np.arange(H)))
-            sp.append(loc.export_raw(3, np.arange(S)))
+    parts = {2: [], 3: []}  # per group: (offsets, DeviceBuffer)
+    par = {2: {int(k): [] for k in kh}, 3: {int(k): [] for k in ks}}  # sampled keys' payloads, host order
+    n_samples = 0
+    for h0 in range(0, hosts, G):
+        g = min(G, hosts - h0)
+        win = V.HostWindows(args.seed + 55, h0, g, H, S)
+        n_samples += win.n_histo + win.n_set
+        with V.Engine((1, 1, g * H, g * S), percentiles=PCT, max_batch_records=max(win.n_histo, win.n_set) + 1,
+                      max_batch_member_bytes=64) as loc:
+            loc.ingest_device(win.batch)
+            for cls, nk, keys in ((2, H, kh), (3, S, ks)):
+                off, buf, view = loc.export_device(cls, np.arange(g * nk, dtype=np.uint32))
+                parts[cls].append((off, buf))
+                for hh in range(g):
+                    for k in keys:
+                        i = hh * nk + int(k)
+                        par[cls][int(k)].append(view[off[i]:off[i + 1]].tobytes())
             loc.flush_raw()
-    dev = []  # per distinct host: device (off, bytes) for histos and sets
-    keep = []
-    for (ho, hb), (so, sb) in zip(hp, sp):
-        bufs = [V.DeviceBuffer(ho), V.DeviceBuffer(hb), V.DeviceBuffer(so), V.DeviceBuffer(sb)]
-        keep += bufs
-        dev.append([b.ptr.value for b in bufs])
-    hslot = V.DeviceBuffer(np.arange(H, dtype=np.uint32))
-    sslot = V.DeviceBuffer(np.arange(S, dtype=np.uint32))
-    keep += [hslot, sslot]
+        win.free()
+    dev = {}
+    payload_bytes = 0
+    for cls, nk in ((2, H), (3, S)):
+        total = sum(int(o[-1]) for o, _ in parts[cls])
+        big = V.DeviceBuffer.empty(total)
+        offs, base = [], 0
+        for o, b in parts[cls]:
+            if int(o[-1]):
+                A.lib.vn_device_copy(0, C.c_void_p(big.ptr.value + base), b.ptr, int(o[-1]))
+            offs.append(o[:-1] + base)
+            base += int(o[-1])
+            b.free()
+        offs.append(np.array([base], np.uint64))
+        off_all = np.concatenate(offs).astype(np.uint64)
+        slots = np.tile(np.arange(nk, dtype=np.uint32), hosts)
+        dev[cls] = (V.DeviceBuffer(slots), V.DeviceBuffer(off_all), big, len(slots))
+        payload_bytes += total
+    A.lib.vn_device_synchronize(0)
     gen_s = time.time() - t0
-    payload_bytes = sum(int(h[0][-1]) + int(s_[0][-1]) for h, s_ in zip(hp, sp)) / D * hosts
-    with V.Engine((1, 1, H, S), percentiles=PCT, max_batch_records=getattr(args, "c5_batch", 1 << 25)) as g:
+    with V.Engine((1, 1, H, S), percentiles=PCT, max_batch_records=args.c5_batch) as g:
         def window():
-            for h in range(hosts):
-                ho, hb, so, sb = dev[h % D]
-                g.import_device(2, hslot.ptr.value, ho, hb, H)
-                g.import_device(3, sslot.ptr.value, so, sb, S)
+            for cls in (2, 3):
+                sl, of, by, n = dev[cls]
+                g.import_device(cls, sl.ptr.value, of.ptr.value, by.ptr.value, n)
             return g.flush_raw()
         window()
         A.lib.vn_device_synchronize(0)
@@ -164,48 +180,52 @@ def c5_leg(args, rank):
         ses = np.ctypeslib.as_array(f.set_estimate, shape=(f.n_set,)).copy()
         ssl = np.ctypeslib.as_array(f.set_slot, shape=(f.n_set,)).copy()
     # parity on sampled keys: the restated Go import of the same payload sequence
-    kh = np.sort(rng.choice(H, min(H, args.c5_parity_keys), replace=False))
-    ks = np.sort(rng.choice(S, min(S, args.c5_parity_keys), replace=False))
+    t1 = time.time()
     w = oracle.Worker(1, 1, len(kh), len(ks))
-    cents = [[] for _ in kh]
-    for h in range(hosts):
-        (ho, hb), (so, sb) = hp[h % D], sp[h % D]
-        for i, k in enumerate(kh):
-            pl = hb[ho[k]:ho[k + 1]].tobytes()
-            w.import_histo(i, pl)
-            if h < D:
-                t = oracle.MergingDigest(100.0)
-                t.gob_decode(pl)
-                cents[i].append(t.centroids())
-        for i, k in enumerate(ks):
-            w.import_set(i, sb[so[k]:so[k + 1]].tobytes())
     pos = {int(s_): j for j, s_ in enumerate(hsl)}
-    st_exact, rank_err, st_diff = True, 0.0, np.zeros(3)
+    st_exact, bit_exact, rank_err, st_diff = True, True, 0.0, np.zeros(3)
     for i, k in enumerate(kh):
+        ms_, ws_ = [], []
+        for pl in par[2][int(k)]:
+            assert w.import_histo(i, pl) == 0
+            t = oracle.MergingDigest(100.0)
+            t.gob_decode(pl)
+            m_, w_ = t.centroids()
+            ms_.append(m_)
+            ws_.append(w_)
         j = pos[int(k)]
         ost = np.array(w.histo_stats(i))
         st_exact &= bool(np.array_equal(hst[j, [5, 6, 7]], ost[[5, 6, 7]]))
         st_diff = np.maximum(st_diff, np.abs(hst[j, [5, 6, 7]] - ost[[5, 6, 7]]))
-        m = np.concatenate([cents[i][h % D][0] for h in range(hosts)])
-        wt = np.concatenate([cents[i][h % D][1] for h in range(hosts)])
+        ref_q = [w.histo_quantile(i, p) for p in PCT]
+        bit_exact &= bool(np.array_equal(hq[j], ref_q))
+        m, wt = np.concatenate(ms_), np.concatenate(ws_)
         o = np.argsort(m, kind="stable")
         sv, cw = m[o], np.cumsum(wt[o])
         F = lambda q: cw[np.searchsorted(sv, q, side="right") - 1] / cw[-1] if np.searchsorted(sv, q, side="right") \
             else 0.0
-        for a, p in zip(hq[j], PCT):
-            rank_err = max(rank_err, abs(F(a) - F(w.histo_quantile(i, p))))
+        for a, r in zip(hq[j], ref_q):
+            rank_err = max(rank_err, abs(F(a) - F(r)))
+    for i, k in enumerate(ks):
+        for pl in par[3][int(k)]:
+            w.import_set(i, pl)
     spos = {int(s_): j for j, s_ in enumerate(ssl)}
     set_exact = all(int(ses[spos[int(k)]]) == w.set_estimate(i) for i, k in enumerate(ks))
     n_imp = hosts * (H + S)
-    return {"config": "C5 global import: %d hosts x (%d histo digests + %d set sketches), every key from every host, "
-                      "%d distinct host windows cycled; payloads in HBM (vn_import_*_device), then vn_flush" % (
-                          hosts, H, S, D),
+    return {"config": "C5 global import: %d distinct hosts x (%d histo digests + %d set sketches), every key from "
+                      "every host; host windows generated, ingested and exported on the GPU (%d local samples); "
+                      "payloads in HBM, ONE vn_import_histos_device + ONE vn_import_sets_device call, then vn_flush"
+                      % (hosts, H, S, n_samples),
             "imports_per_s": n_imp / (ms * 1e-3), "payload_GBs": payload_bytes / (ms * 1e-3) / 1e9,
             "ms_per_window": ms, "windows": args.c5_windows, "payloads_per_window": n_imp,
-            "payload_bytes_per_window": payload_bytes, "generated_in_s": round(gen_s, 2),
+            "payload_bytes_per_window": payload_bytes,
+            "roofline": {"bound": "hbm", "achieved_GBs": payload_bytes / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                         "frac": payload_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "unit": "payload bytes decoded per second over the window"},
+            "generated_in_s": round(gen_s, 2), "parity_checked_in_s": round(time.time() - t1, 2),
             "parity": {"keys_checked": {"histo": int(len(kh)), "set": int(len(ks))},
                        "histo_weight_min_max_exact": st_exact, "histo_min_max_weight_absdiff": st_diff.tolist(),
-                       "histo_rank_error_max": rank_err,
+                       "histo_quantiles_bit_exact": bit_exact, "histo_rank_error_max": rank_err,
                        "set_estimates_exact": bool(set_exact)}}
 
 
@@ -352,9 +372,10 @@ def main():
     ap.add_argument("--c5-hosts", type=int, default=1000, help="C5 leg (rank 0, N=1): hosts per window (0: off)")
     ap.add_argument("--c5-histo-keys", type=int, default=10000)
     ap.add_argument("--c5-set-keys", type=int, default=2000)
-    ap.add_argument("--c5-distinct", type=int, default=8, help="distinct host windows, cycled")
+    ap.add_argument("--c5-group", type=int, default=50, help="hosts generated per local engine")
+    ap.add_argument("--c5-batch", type=int, default=64 << 20, help="the global engine's max_batch_records")
     ap.add_argument("--c5-windows", type=int, default=1)
-    ap.add_argument("--c5-parity-keys", type=int, default=16)
+    ap.add_argument("--c5-parity-keys", type=int, default=256)
     ap.add_argument("--text-lines", type=int, default=2_000_000,
                     help="DogStatsD text intake leg (rank 0, N=1): lines per buffer (0: off)")
     ap.add_argument("--text-passes", type=int, default=8, help="buffers per intake window")

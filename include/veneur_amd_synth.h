@@ -81,6 +81,31 @@ void vn_synth_device_free(vn_synth_dev_out* out);
 /* record count of every key over the first n_positions of the stream (hot-key detection) */
 int vn_synth_key_counts(const vn_synth_dev_config* cfg, uint64_t n_positions, uint32_t* counts /* n_keys */);
 
+/* C5 (BASELINE configs[4]): the local flush windows of hosts [host0, host0 + n_hosts) of a
+ * global aggregator's fleet, generated in HBM.  Host h's histogram key k (< n_histo_keys) gets
+ * 50 + (x % 101) timer samples (lognormal, mu 3.9 + 0.05 (h % 8), sigma 1; 10% at rate 0.5), its
+ * set key k (< n_set_keys) min(20000, int(50 * Lomax(1.2)) + 1) member hashes (x a counter-based
+ * draw of (seed, h, k)).  Records of host h, key k sit at local slot (h - host0) * n_keys + k,
+ * host-major then key-major, each key's samples in draw order: ingested into one local engine of
+ * n_hosts * n_keys slots per class and exported, they are every host's forwarded payloads. */
+typedef struct {
+  uint64_t seed;
+  uint32_t host0, n_hosts, n_histo_keys, n_set_keys;
+  int device;
+} vn_synth_hosts_config;
+
+typedef struct {
+  uint64_t n_histo, n_set;
+  uint32_t* h_slot;             /* device arrays, freed by vn_synth_hosts_free */
+  double* h_val;
+  float* h_rate;
+  uint32_t* s_slot;
+  uint64_t* s_hash;
+} vn_synth_hosts_out;
+
+int vn_synth_hosts_device(const vn_synth_hosts_config* cfg, vn_synth_hosts_out* out);
+void vn_synth_hosts_free(vn_synth_hosts_out* out);
+
 #ifdef __cplusplus
 }
 #endif

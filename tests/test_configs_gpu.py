@@ -144,10 +144,22 @@ def test_c5_bench_leg_small():
     global engine) at a small scale: parity on every key."""
     from argparse import Namespace
     import bench
-    r = bench.c5_leg(Namespace(seed=3, c5_histo_keys=300, c5_set_keys=60, c5_distinct=3, c5_hosts=40, c5_windows=1,
-                               c5_parity_keys=300), 0)
+    r = bench.c5_leg(Namespace(seed=3, c5_histo_keys=300, c5_set_keys=60, c5_group=7, c5_hosts=40, c5_windows=1,
+                               c5_parity_keys=300, c5_batch=1 << 20), 0)
     p = r["parity"]
     assert p["keys_checked"] == {"histo": 300, "set": 60}
     assert p["histo_weight_min_max_exact"] and p["set_estimates_exact"]
-    assert p["histo_rank_error_max"] <= 1e-3, p
+    assert p["histo_quantiles_bit_exact"] and p["histo_rank_error_max"] == 0.0, p
     assert r["payloads_per_window"] == 40 * 360 and r["imports_per_s"] > 0
+
+
+def test_c5_import_sliced_by_centroids():
+    """one vn_import_histos_device call whose centroids exceed max_batch_records: the engine cuts
+    it into payload slices (k_import_slices) and drains each in arrival order -- the quantiles
+    are those of importing the payloads one call after another (bit-exact vs the oracle)"""
+    from argparse import Namespace
+    import bench
+    r = bench.c5_leg(Namespace(seed=4, c5_histo_keys=64, c5_set_keys=8, c5_group=16, c5_hosts=64, c5_windows=2,
+                               c5_parity_keys=64, c5_batch=60_000), 0)
+    p = r["parity"]
+    assert p["histo_weight_min_max_exact"] and p["set_estimates_exact"] and p["histo_quantiles_bit_exact"], p

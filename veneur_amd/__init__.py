@@ -6,11 +6,12 @@ and the benchmark -- Engine (the C-ABI) and Worker (veneur's Worker / samplers A
 importing it without the built library raises ImportError.
 """
 from . import _abi
-from .engine import (Comm, DeviceBuffer, DeviceStream, Engine, EngineError, FlushOutput, device_count, metro64_device,
+from .engine import (Comm, DeviceBuffer, DeviceStream, Engine, EngineError, FlushOutput, HostWindows, device_count,
+                     metro64_device,
                      synth, synth_key_counts)
 from .worker import (Aggregate, HistogramAggregates, InterMetric, JSONMetric, MetricKey, MetricScope, MetricType,
                      UDPMetric, Worker, WorkerMetrics)
 
-__all__ = ["Comm", "DeviceStream", "synth_key_counts", "Engine", "EngineError", "FlushOutput", "DeviceBuffer", "device_count", "metro64_device", "synth",
+__all__ = ["Comm", "DeviceStream", "HostWindows", "synth_key_counts", "Engine", "EngineError", "FlushOutput", "DeviceBuffer", "device_count", "metro64_device", "synth",
            "_abi", "Worker", "WorkerMetrics", "UDPMetric", "JSONMetric", "MetricKey", "MetricScope", "MetricType",
            "InterMetric", "Aggregate", "HistogramAggregates"]

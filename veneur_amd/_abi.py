@@ -154,6 +154,16 @@ class SynthDevOut(C.Structure):
                 ("counter_sum", C.c_int64), ("histo_weight", C.c_double)]
 
 
+class SynthHostsConfig(C.Structure):  # vn_synth_hosts_config
+    _fields_ = [("seed", C.c_uint64), ("host0", C.c_uint32), ("n_hosts", C.c_uint32), ("n_histo_keys", C.c_uint32),
+                ("n_set_keys", C.c_uint32), ("device", C.c_int)]
+
+
+class SynthHostsOut(C.Structure):  # vn_synth_hosts_out
+    _fields_ = [("n_histo", C.c_uint64), ("n_set", C.c_uint64), ("h_slot", C.c_void_p), ("h_val", C.c_void_p),
+                ("h_rate", C.c_void_p), ("s_slot", C.c_void_p), ("s_hash", C.c_void_p)]
+
+
 def _sig(name, res, *args):
     f = getattr(lib, name)
     f.restype = res
@@ -273,6 +283,8 @@ _sig("vn_synth_free", None, C.POINTER(SynthOut))
 _sig("vn_synth_device", C.c_int, C.POINTER(SynthDevConfig), C.POINTER(SynthDevOut))
 _sig("vn_synth_device_free", None, C.POINTER(SynthDevOut))
 _sig("vn_synth_key_counts", C.c_int, C.POINTER(SynthDevConfig), C.c_uint64, u32p)
+_sig("vn_synth_hosts_device", C.c_int, C.POINTER(SynthHostsConfig), C.POINTER(SynthHostsOut))
+_sig("vn_synth_hosts_free", None, C.POINTER(SynthHostsOut))
 
 # every symbol include/*.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
@@ -283,7 +295,8 @@ EXPORTED = [
     "vn_intake_last_error", "vn_intake_process", "vn_intake_upsert", "vn_intake_keys_info", "vn_intake_read_keys",
     "vn_intake_reset", "vn_sink_create", "vn_sink_destroy", "vn_sink_last_error", "vn_datadog_flush", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",
-    "vn_synth_device", "vn_synth_device_free", "vn_synth_key_counts",
+    "vn_synth_device", "vn_synth_device_free", "vn_synth_key_counts", "vn_synth_hosts_device",
+    "vn_synth_hosts_free",
     "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",
     "vn_comm_nranks", "vn_comm_allreduce", "vn_engine_set_comm", "vn_split_keys", "vn_ingest_split", "vn_split_close", "vn_split_combine",
 ]

@@ -85,6 +85,17 @@ __device__ __forceinline__ double rl_d(double v, int i) {
   return __hiloint2double(hi, lo);
 }
 
+// Fence the next chunk's prefetch behind the current chunk's values: each listed value is
+// materialised in a register here (its load waited for) and no memory access below may move
+// above.  Without it the loads of chunk c + 1 issue first and the compiler's wait-count
+// insertion, conservative across their exec-masked blocks, then waits for those NEW loads at the
+// first use of an old value -- an L2/HBM round trip at the start of every merge.
+__device__ __forceinline__ void hold2(double& a, double& b) { asm volatile("" : "+v"(a), "+v"(b)::"memory"); }
+__device__ __forceinline__ void hold_stats(double& a, double& b, double& c, double& d, double& e, double& f,
+                                           double& g) {
+  asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g)::"memory");
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v = dadd(v, __shfl_xor(v, d, 64));
@@ -1016,7 +1027,9 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
           stat(cv[q], __builtin_fabs(cw[q]), cw[q] > 0.0);
         }
       }
-      const double tempW = ctw;
+      double tempW = ctw, tpad = 0.0;
+      hold2(tempW, tpad);
+      hold_stats(sw, sxw, srw, mn, mx, dmn, dmx);
       if (c + 1 < sp.npure) load(c + 1);
       wave_lds_sync();
       merge_any(mp, L, nm, mainW, tcap, tempW);
@@ -1088,12 +1101,6 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
   }
 }
 
-#ifdef VN_FAST_MERGE_CHECK
-__device__ unsigned long long g_fast_dbg[64];
-extern "C" int vn_fast_dbg_read(unsigned long long* out64) {
-  return hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_fast_dbg), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
-}
-#endif
 // ---- the long replays: NW waves per key, built for the latency of ONE merge (the hottest C4
 // key replays ~23k merges back to back, so its merge latency is the window's critical path).
 // Bit-identical to merge_sorted_fast; a different dependence structure:
@@ -1113,6 +1120,11 @@ extern "C" int vn_fast_dbg_read(unsigned long long* out64) {
 // it cannot take (non-integer weights, > 64 temps, >= 256 elements) is the one-wave merge run
 // by wave 0; a non-monotone k (an ulp wiggle of asin) takes the sequential walk of wave 0.
 typedef __attribute__((address_space(3))) uint64_t ldsu64;
+
+#ifndef VN_FAST_BAND
+#define VN_FAST_BAND 1e-9  // (a variant build with a huge band sends every merge down the fallback)
+#endif
+constexpr double kBand = VN_FAST_BAND;  // certainty band of the close k's comparisons (merge_fast)
 
 struct FastLds {
   ldsf64* mp;     // [capc + 2] exclusive prefix of the main centroids' weights; mp[nm] = mainW
@@ -1231,18 +1243,6 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
   const double T = dadd(mainW, tempW);
   const uint32_t m = nm + np, nmc = nm ? nm - 1 : 0u;
   double xv[R], xw[R], wb[R], kv[R];
-#ifdef VN_FAST_MERGE_CHECK
-  if (t == 0 && (F.sp[np] != tempW || F.mp[nm] != mainW || F.sp[0] != 0.0) &&
-      atomicCAS(&g_fast_dbg[32], 0ull, 1ull) == 0ull) {
-    g_fast_dbg[33] = np;
-    g_fast_dbg[34] = nm;
-    g_fast_dbg[35] = dbits(F.sp[np]);
-    g_fast_dbg[36] = dbits(tempW);
-    g_fast_dbg[37] = dbits(F.mp[nm]);
-    g_fast_dbg[38] = dbits(mainW);
-    g_fast_dbg[39] = dbits(F.sp[0]);
-  }
-#endif
   // ---- A: the element at each output position e: i temps and e - i mains precede it.
   // i is the number of p in [lo, hi) with P(p) = "temp p precedes main e-1-p" (true below i):
   // a four-way search, three probes per step (hi - lo <= 64 -> 16 -> 4 -> 1 -> 0: three steps
@@ -1295,9 +1295,19 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
     }
   }
   PROF_T(f1);
-  // ---- B: k of every element (indexEstimate of the inclusive weight)
+  // ---- B: k of every element.  Only the chain's comparisons of k differences with 1 use k, so
+  // a close k serves: q = mergedWeight / totalWeight exactly as Go divides, then the device
+  // libm's asin (a few ulps, no divisions) in place of Go's (three divisions and a square root).
+  // Every comparison below is taken only when its difference lies outside 1 +- kBand, where the
+  // close and the exact k certainly agree (their k differ by < 1e-13); one inside the band makes
+  // the whole merge recompute exact k and walk the chain sequentially (misc[0]).  With integer
+  // weights >= 1 and T <= 2^40 (the fast merge's conditions) consecutive exact k differ by more
+  // than 5e-11, far above asin's ulps, so exact k is increasing and the forced-start argument holds.
 #pragma unroll
-  for (int r = 0; r < R; r++) kv[r] = index_estimate(x.delta, ddiv(dadd(wb[r], xw[r]), T));
+  for (int r = 0; r < R; r++) {
+    const double q = ddiv(dadd(wb[r], xw[r]), T);
+    kv[r] = x.delta * (asin(dsub(dmul(2.0, q), 1.0)) * (1.0 / kPi) + 0.5);
+  }
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const uint32_t e = r * NT + t;
@@ -1311,96 +1321,63 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
   fast_sync<NW>();
   PROF_T(f2);
   // ---- C: forced starts, then each one walks its segment
+  constexpr double kHi = 1.0 + kBand, kLo = 1.0 - kBand;
   bool fr[R];
   double km1[R];
-  {
-    bool nonmono = false;
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-      const uint32_t e = r * NT + t;
-      const double a = F.kk[e >= 1 ? e - 1 : 0u], b = F.kk[e >= 2 ? e - 2 : 0u];
-      km1[r] = e >= 1 ? a : k0;
-      const double km2 = e >= 2 ? b : k0;
-      fr[r] = e < m && (e == 0 || dsub(kv[r], km2) > 1.0);
-      nonmono |= e < m && e >= 1 && kv[r] < km1[r];
-    }
-    if (__any(nonmono) && lane == 0) F.misc[0] = 1u;
-  }
+  bool unsure = false;
 #pragma unroll
   for (int r = 0; r < R; r++) {
-    if (fr[r]) {
-      const uint32_t e = r * NT + t;
-      F.flag[e] = 1u;
-      // walk: element j starts a centroid when k_j - base > 1 (base = k before the current
-      // centroid's first element); it stops at the next forced element (k_j - k_{j-2} > 1),
-      // whose own thread starts it.  Eight k values per LDS round trip; the forced tests of a
-      // batch do not depend on base, only the start tests chain through it.
-      double base = km1[r], p2 = km1[r], p1 = kv[r];  // p2 = k_{j-2}, p1 = k_{j-1}
-      uint32_t j = e + 1;
-      bool run = j < m;
-      while (run) {
-        double kb[8];
+    const uint32_t e = r * NT + t;
+    const double a = F.kk[e >= 1 ? e - 1 : 0u], b = F.kk[e >= 2 ? e - 2 : 0u];
+    km1[r] = e >= 1 ? a : k0;
+    const double d = kv[r] - (e >= 2 ? b : k0);
+    fr[r] = e < m && (e == 0 || d > kHi);
+    unsure |= e < m && e >= 1 && d >= kLo && d <= kHi;
+  }
+  // walk: element j starts a centroid when k_j - base > 1 (base = k before the current
+  // centroid's first element); a walker stops at the next forced element (k_j - k_{j-2} > 1),
+  // whose own thread starts it.  Eight k per LDS round trip, branch-free: every lane steps until
+  // no walker of its wave is left.
 #pragma unroll
-        for (int u = 0; u < 8; u++) kb[u] = F.kk[min(j + u, m - 1)];
-        bool frc[8];
+  for (int r = 0; r < R; r++) {
+    const uint32_t e = r * NT + t;
+    if (fr[r]) F.flag[e] = 1u;
+    bool alive = fr[r] && e + 1 < m;
+    double base = km1[r], p2 = km1[r], p1 = kv[r];  // p2 = k_{j-2}, p1 = k_{j-1}
+    uint32_t j = e + 1;
+    while (__any(alive)) {
+      double kb[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const double k2 = u == 0 ? p2 : (u == 1 ? p1 : kb[u - 2]);
-          frc[u] = j + u >= m || dsub(kb[u], k2) > 1.0;
-        }
+      for (int u = 0; u < 8; u++) kb[u] = F.kk[min(j + u, m - 1)];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          if (run) {
-            if (frc[u]) {
-              run = false;
-            } else {
-              const bool st_ = dsub(kb[u], base) > 1.0;
-              F.flag[j] = st_ ? 1u : 0u;
-              base = st_ ? (u == 0 ? p1 : kb[u - 1]) : base;
-              j++;
-            }
-          }
-        }
-        p2 = kb[6];
-        p1 = kb[7];
+      for (int u = 0; u < 8; u++) {
+        const double k2 = u == 0 ? p2 : (u == 1 ? p1 : kb[u - 2]);
+        const double km = u == 0 ? p1 : kb[u - 1];
+        const double dF = kb[u] - k2, dS = kb[u] - base;
+        const bool in = alive && j + u < m;
+        const bool stop = !in || dF > kHi;
+        unsure |= in && dF >= kLo && dF <= kHi;
+        const bool go = in && !stop;
+        const bool st_ = dS > kHi;
+        unsure |= go && dS >= kLo && dS <= kHi;
+        if (go) F.flag[j + u] = st_ ? 1u : 0u;
+        base = (go && st_) ? km : base;
+        alive = go;
       }
+      j += 8;
+      p2 = kb[6];
+      p1 = kb[7];
     }
   }
+  if (__any(unsure) && lane == 0) F.misc[0] = 1u;
   fast_sync<NW>();
-#ifdef VN_FAST_MERGE_CHECK
-  // debugging variant: the walkers' flags against mergeOne's sequential walk (wave 0); the first
-  // mismatch of the run is recorded in g_fast_dbg
-  {
-    bool mine[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) mine[r] = (r * NT + t) < m && F.flag[r * NT + t] != 0u;
-    fast_sync<NW>();
-    if (wv == 0) walk_flags(F, m, k0);
-    fast_sync<NW>();
+  if (F.misc[0]) {  // a comparison within the band: exact k, then mergeOne's sequential walk
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const uint32_t e = r * NT + t;
-      const bool ref = e < m && F.flag[e] != 0u;
-      if (e < m && ref != mine[r] && atomicCAS(&g_fast_dbg[0], 0ull, 1ull) == 0ull) {
-        g_fast_dbg[1] = m;
-        g_fast_dbg[2] = np;
-        g_fast_dbg[3] = e;
-        g_fast_dbg[4] = mine[r];
-        g_fast_dbg[5] = F.misc[0];
-        for (int q = 0; q < 8; q++) {
-          const int ix = (int)e - 5 + q;
-          g_fast_dbg[8 + q] = ix >= 0 && ix < (int)m ? dbits(F.kk[ix]) : 0ull;
-          g_fast_dbg[16 + q] = ix >= 0 && ix < (int)m ? F.flag[ix] : 9ull;
-          g_fast_dbg[24 + q] = ix >= 0 && ix < (int)m ? dbits(L.gw[ix]) : 0ull;
-        }
-        g_fast_dbg[6] = dbits(T);
-        g_fast_dbg[7] = dbits(kv[r]);
-      }
+      if (e < m) F.kk[e] = index_estimate(x.delta, ddiv(dadd(wb[r], xw[r]), T));
     }
     fast_sync<NW>();
-  }
-#endif
-  if (F.misc[0]) {  // non-monotone k: the forced-start argument does not hold
     if (wv == 0) walk_flags(F, m, k0);
     fast_sync<NW>();
   }
@@ -1444,11 +1421,12 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
         gw[u] = L.gw[ix];
       }
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        if (e + 1 + u < end) {
-          W = dadd(W, gw[u]);
-          mean = dadd(mean, ddiv(dmul(dsub(gv[u], mean), gw[u]), W));
-        }
+      for (int u = 0; u < 4; u++) {  // (branch-free: a step past the end keeps W and mean)
+        const bool in = e + 1 + u < end;
+        const double W2 = dadd(W, gw[u]);
+        const double mean2 = dadd(mean, ddiv(dmul(dsub(gv[u], mean), gw[u]), W2));
+        W = in ? W2 : W;
+        mean = in ? mean2 : mean;
       }
       for (uint32_t j = e + 5; j < end; j++) {
         const double wt = L.gw[j];
@@ -1570,7 +1548,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
 #ifdef VN_FAST_MERGE_OFF
     if (false) {  // A/B and debugging variant: every merge by wave 0's one-wave merge
 #else
-    if (fok && tint && n_ <= 64 && m < NT * R && m <= capc && dadd(mainW, tempW) <= 9007199254740992.0) {
+    if (fok && tint && n_ <= 64 && m < NT * R && m <= capc && dadd(mainW, tempW) <= 1099511627776.0) {
 #endif
       merge_fast<NW>(mp, L, F, nm, mainW, n_, tempW, k0);
       return;
@@ -1636,8 +1614,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     };
     load(0);
     for (uint32_t c = 0; c < sp.npure; c++) {
-      const double tempW = __builtin_fabs(ctw);
-      const bool tint = ctw >= 0.0;
+      double tempW = __builtin_fabs(ctw), tintd = ctw >= 0.0 ? 1.0 : 0.0;
       if (t < tcap) {
         L.sv[t] = cv;
         L.sw[t] = __builtin_fabs(cw);
@@ -1645,9 +1622,11 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
         stat(cv, __builtin_fabs(cw), cw > 0.0);
       }
       if (t == tcap) F.sp[tcap] = tempW;
+      hold2(tempW, tintd);
+      hold_stats(sw, sxw, srw, mn, mx, dmn, dmx);
       if (c + 1 < sp.npure) load(c + 1);
       fast_sync<NW>();
-      merge_sorted_any(tcap, tempW, tint);
+      merge_sorted_any(tcap, tempW, tintd != 0.0);
     }
   }
   const uint32_t tail = sp.off0 + sp.npure * tcap;

@@ -289,6 +289,29 @@ __global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const u
   }
 }
 
+// payload index of every slice boundary: bnd[j] = the last payload i with coff[i] <= j * step
+// (j = 0..nslices), and the centroid offset there
+__global__ void k_import_slices(uint64_t n, const uint32_t* __restrict__ coff, uint64_t step, uint32_t nslices,
+                                uint32_t* __restrict__ bnd) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j > nslices) return;
+  uint64_t b;
+  if (j == nslices) {
+    b = n;
+  } else {
+    const uint64_t thr = (uint64_t)j * step;
+    uint64_t lo = 0, hi = n;  // last i in [0, n] with coff[i] <= thr
+    while (lo < hi) {
+      const uint64_t md = (lo + hi + 1) >> 1;
+      if (coff[md] <= thr) lo = md;
+      else hi = md - 1;
+    }
+    b = lo;
+  }
+  bnd[2 * j] = (uint32_t)b;
+  bnd[2 * j + 1] = coff[b];
+}
+
 }  // namespace
 
 // Histo.Combine of a batch of forwarded digests: decoded and validated now (one host round
@@ -296,7 +319,10 @@ __global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const u
 // run, which is merged -- re-Add of every centroid through the exact replay / hot remainder
 // -- in one ingest when it fills or before anything reads or adds to a histogram
 // (histo_imports_drain).  Merging a run of imports at once equals merging them one call
-// after another: the replay is the same ordered stream of Adds.
+// after another: the replay is the same ordered stream of Adds.  A batch holding more
+// centroids than the run (a global veneur's whole fleet in one call) is cut into slices of
+// payloads at centroid offsets j * run / 2, found on the device (one more round trip), each
+// appended and drained in arrival order.
 void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes) {
   if (!n) return;
   hipStream_t st = e->st;
@@ -308,13 +334,31 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   VN_HIP_CHECK(hipStreamSynchronize(st));
   take_decode_error(e);
   const uint64_t nc = e->hf_cnt[9];
-  if (nc > s.cap_cent)
-    throw std::invalid_argument("imported digests hold more centroids than max_batch_records: split the import");
   if (!nc) return;
-  if (s.acc + nc > s.cap_cent) histo_imports_drain(e);
-  hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.acc,
-                     s.cslot, s.cmean, s.cw, e->h_err);
-  s.acc += nc;
+  if (nc <= s.cap_cent) {
+    if (s.acc + nc > s.cap_cent) histo_imports_drain(e);
+    hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.acc,
+                       s.cslot, s.cmean, s.cw, e->h_err);
+    s.acc += nc;
+    return;
+  }
+  // slices of at most run / 2 centroids plus one payload
+  const uint64_t step = s.cap_cent / 2;
+  const uint32_t nsl = (uint32_t)((nc + step - 1) / step);
+  std::vector<uint32_t> bnd(2 * ((size_t)nsl + 1));
+  uint32_t* dbnd = s.cnt;  // the counts are consumed (coff holds their scan)
+  hipLaunchKernelGGL(k_import_slices, dim3(blocks_for(nsl + 1, 256)), dim3(256), 0, st, n, s.coff, step, nsl, dbnd);
+  VN_HIP_CHECK(hipMemcpyAsync(bnd.data(), dbnd, bnd.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+  for (uint32_t j = 0; j < nsl; j++) {
+    const uint64_t b0 = bnd[2 * j], b1 = bnd[2 * j + 2], c0 = bnd[2 * j + 1], c1 = bnd[2 * j + 3];
+    if (b1 <= b0) continue;
+    if (c1 - c0 > s.cap_cent) throw std::invalid_argument("one imported digest holds more centroids than max_batch_records");
+    if (s.acc + (c1 - c0) > s.cap_cent) histo_imports_drain(e);
+    hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
+                       slot + b0, s.coff + b0, s.acc - c0, s.cslot, s.cmean, s.cw, e->h_err);
+    s.acc += c1 - c0;
+  }
 }
 
 void histo_imports_drain(vn_engine* e) {

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/veneur_amd_synth.h"
+#include "kernels.h"
 #include "primitives.h"
 #include "sketch.h"
 
@@ -320,6 +321,54 @@ __global__ void k_gen_key_counts(GenCtx g, uint64_t n, uint32_t* __restrict__ cn
     atomicAdd(&cnt[draw_key(g, smix(g.seed * 0x100000001B3ull + p))], 1u);
 }
 
+// ---- C5 host windows (vn_synth_hosts_device)
+struct HostsGen {
+  uint64_t seed;
+  uint32_t host0, nh, H, S;
+};
+__device__ __forceinline__ uint64_t host_key_draw(const HostsGen& g, uint32_t h, uint32_t k, uint64_t salt) {
+  return smix(g.seed ^ smix(((uint64_t)h << 32 | k) ^ salt));
+}
+__device__ __forceinline__ uint32_t histo_count(const HostsGen& g, uint32_t h, uint32_t k) {
+  return 50u + (uint32_t)(host_key_draw(g, h, k, 0x1111) % 101u);
+}
+__device__ __forceinline__ uint32_t set_count(const HostsGen& g, uint32_t h, uint32_t k) {
+  const double u = 1.0 - u01d(host_key_draw(g, h, k, 0x2222));  // (0, 1]
+  const double x = pow(u, -1.0 / 1.2) - 1.0;                     // Lomax(1.2)
+  return x * 50.0 >= 19999.0 ? 20000u : (uint32_t)(x * 50.0) + 1u;
+}
+__global__ void k_hosts_counts(HostsGen g, uint32_t* __restrict__ hc, uint32_t* __restrict__ sc) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nH = (uint64_t)g.nh * g.H, nS = (uint64_t)g.nh * g.S;
+  if (i < nH) hc[i] = histo_count(g, g.host0 + (uint32_t)(i / g.H), (uint32_t)(i % g.H));
+  if (i < nS) sc[i] = set_count(g, g.host0 + (uint32_t)(i / g.S), (uint32_t)(i % g.S));
+}
+__global__ void k_hosts_histo(HostsGen g, const uint64_t* __restrict__ off, uint32_t* __restrict__ slot,
+                              double* __restrict__ val, float* __restrict__ rate) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)g.nh * g.H) return;
+  const uint32_t h = g.host0 + (uint32_t)(i / g.H), k = (uint32_t)(i % g.H);
+  const double mu = 3.9 + 0.05 * (double)(h % 8u);
+  for (uint64_t o = off[i], j = 0; o < off[i + 1]; o++, j++) {
+    const uint64_t a = host_key_draw(g, h, k, 0x3333 + 2 * j), b = host_key_draw(g, h, k, 0x3334 + 2 * j);
+    const double u1 = 1.0 - u01d(a), u2 = u01d(b);
+    const double z = sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+    slot[o] = (uint32_t)i;
+    val[o] = exp(mu + z);
+    rate[o] = (b & 0x3ffu) < 102u ? 0.5f : 1.0f;  // about 10% at rate 0.5
+  }
+}
+__global__ void k_hosts_set(HostsGen g, const uint64_t* __restrict__ off, uint32_t* __restrict__ slot,
+                            uint64_t* __restrict__ hash) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)g.nh * g.S) return;
+  const uint32_t h = g.host0 + (uint32_t)(i / g.S), k = (uint32_t)(i % g.S);
+  for (uint64_t o = off[i], j = 0; o < off[i + 1]; o++, j++) {
+    slot[o] = (uint32_t)i;
+    hash[o] = host_key_draw(g, h, k, 0x4444 + j);
+  }
+}
+
 }  // namespace
 }  // namespace vn
 
@@ -496,6 +545,50 @@ int vn_synth_device(const vn_synth_dev_config* c, vn_synth_dev_out* out) {
   } catch (const HipError&) {
     return -2;
   }
+}
+
+int vn_synth_hosts_device(const vn_synth_hosts_config* c, vn_synth_hosts_out* out) {
+  if (!c || !out || !c->n_hosts || (!c->n_histo_keys && !c->n_set_keys)) return -1;
+  std::memset(out, 0, sizeof(*out));
+  try {
+    VN_HIP_CHECK(hipSetDevice(c->device));
+    HostsGen g{c->seed, c->host0, c->n_hosts, c->n_histo_keys, c->n_set_keys};
+    const uint64_t nH = (uint64_t)g.nh * g.H, nS = (uint64_t)g.nh * g.S, nmax = std::max(nH, nS);
+    if (nH >= (1ull << 32) || nS >= (1ull << 32)) return -1;
+    uint32_t* hc = dmalloc<uint32_t>(nH);
+    uint32_t* sc = dmalloc<uint32_t>(nS);
+    uint64_t* ho = dmalloc<uint64_t>(nH + 1);
+    uint64_t* so = dmalloc<uint64_t>(nS + 1);
+    hipLaunchKernelGGL(k_hosts_counts, dim3((uint32_t)((nmax + 255) / 256)), dim3(256), 0, 0, g, hc, sc);
+    scan_sizes_u64(hc, ho, nH, 0);
+    scan_sizes_u64(sc, so, nS, 0);
+    VN_HIP_CHECK(hipMemcpy(&out->n_histo, ho + nH, 8, hipMemcpyDeviceToHost));
+    VN_HIP_CHECK(hipMemcpy(&out->n_set, so + nS, 8, hipMemcpyDeviceToHost));
+    out->h_slot = dmalloc<uint32_t>(out->n_histo);
+    out->h_val = dmalloc<double>(out->n_histo);
+    out->h_rate = dmalloc<float>(out->n_histo);
+    out->s_slot = dmalloc<uint32_t>(out->n_set);
+    out->s_hash = dmalloc<uint64_t>(out->n_set);
+    if (nH)
+      hipLaunchKernelGGL(k_hosts_histo, dim3((uint32_t)((nH + 255) / 256)), dim3(256), 0, 0, g, ho, out->h_slot,
+                         out->h_val, out->h_rate);
+    if (nS)
+      hipLaunchKernelGGL(k_hosts_set, dim3((uint32_t)((nS + 255) / 256)), dim3(256), 0, 0, g, so, out->s_slot,
+                         out->s_hash);
+    VN_HIP_CHECK(hipDeviceSynchronize());
+    for (void* q : {(void*)hc, (void*)sc, (void*)ho, (void*)so}) (void)hipFree(q);
+    return 0;
+  } catch (const HipError&) {
+    vn_synth_hosts_free(out);
+    return -2;
+  }
+}
+
+void vn_synth_hosts_free(vn_synth_hosts_out* o) {
+  if (!o) return;
+  for (void* q : {(void*)o->h_slot, (void*)o->h_val, (void*)o->h_rate, (void*)o->s_slot, (void*)o->s_hash})
+    if (q) (void)hipFree(q);
+  std::memset(o, 0, sizeof(*o));
 }
 
 void vn_synth_device_free(vn_synth_dev_out* o) {

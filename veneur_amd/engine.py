@@ -284,6 +284,23 @@ class Engine:
         blob = np.ctypeslib.as_array(x.bytes, shape=(max(1, int(off[-1])),)).copy()
         return off, blob
 
+    def export_device(self, cls, slot):
+        """Export (cls 2 histo, 3 set) of slot[] into a DeviceBuffer of its own: (offsets u64[n+1]
+        host copy, DeviceBuffer of the bytes, zero-copy numpy view of the engine's pinned host
+        bytes -- valid until the engine's next export)."""
+        s = _c(np.atleast_1d(slot), np.uint32)
+        x = A.Export()
+        fn = A.lib.vn_export_histos if cls == 2 else A.lib.vn_export_sets
+        self._check(fn(self.h, s.ctypes.data_as(A.u32p), len(s), C.byref(x)))
+        off = np.ctypeslib.as_array(x.off, shape=(x.n + 1,)).copy()
+        nb = int(off[-1])
+        buf = DeviceBuffer.empty(nb, self.device)
+        if nb and A.lib.vn_device_copy(self.device, buf.ptr, C.c_void_p(x.dev_bytes),
+                                       nb) != 0:
+            raise EngineError("device copy of the export failed")
+        view = np.ctypeslib.as_array(x.bytes, shape=(max(1, nb),))
+        return off, buf, view
+
     def import_device(self, cls, slot_ptr, off_ptr, bytes_ptr, n):
         """vn_import_histos_device / vn_import_sets_device (cls 2 / 3) of device-resident payloads."""
         fn = A.lib.vn_import_histos_device if cls == 2 else A.lib.vn_import_sets_device
@@ -464,6 +481,16 @@ class DeviceBuffer:
         if a.nbytes and A.lib.vn_copy_to_device(device, self.ptr, a.ctypes.data_as(C.c_void_p), a.nbytes) != 0:
             raise EngineError("host to device copy failed")
 
+    @classmethod
+    def empty(cls, nbytes, device=0):
+        """An uninitialised device allocation of nbytes."""
+        b = cls.__new__(cls)
+        b.nbytes = int(nbytes)
+        b.ptr = C.c_void_p()
+        if A.lib.vn_device_alloc(device, max(1, b.nbytes), C.byref(b.ptr)) != 0:
+            raise EngineError("device allocation of %d bytes failed" % b.nbytes)
+        return b
+
     def free(self):
         if self.ptr:
             A.lib.vn_device_free(self.ptr)
@@ -531,6 +558,31 @@ def synth_key_counts(seed, n_keys, n_samples, n_positions, device=0, **kw):
     if A.lib.vn_synth_key_counts(C.byref(cfg), n_positions, out.ctypes.data_as(A.u32p)) != 0:
         raise EngineError("vn_synth_key_counts failed")
     return out
+
+
+class HostWindows:
+    """vn_synth_hosts_device: the C5 local windows of hosts [host0, host0 + n_hosts) in HBM
+    (slot (h - host0) * n_keys + k per class), as a device batch for one local engine."""
+
+    def __init__(self, seed, host0, n_hosts, n_histo_keys, n_set_keys, device=0):
+        cfg = A.SynthHostsConfig(seed, host0, n_hosts, n_histo_keys, n_set_keys, device)
+        self.out = A.SynthHostsOut()
+        rc = A.lib.vn_synth_hosts_device(C.byref(cfg), C.byref(self.out))
+        if rc != 0:
+            raise EngineError("vn_synth_hosts_device failed (rc=%d)" % rc)
+        o = self.out
+        self.batch = A.Batch()
+        self.batch.n_histo, self.batch.histo_slot, self.batch.histo_value, self.batch.histo_rate = (
+            o.n_histo, o.h_slot, o.h_val, o.h_rate)
+        self.batch.n_set, self.batch.set_slot, self.batch.set_hash = o.n_set, o.s_slot, o.s_hash
+        self.n_histo, self.n_set = int(o.n_histo), int(o.n_set)
+
+    def free(self):
+        if getattr(self, "out", None) is not None:
+            A.lib.vn_synth_hosts_free(C.byref(self.out))
+            self.out = None
+
+    __del__ = free
 
 
 class DeviceStream:
