@@ -611,15 +611,33 @@ def main():
                                         "path": "vn_ingest_host from pageable host arrays (host checks + pinned "
                                                 "staging + H2D + kernels); split-key records from HBM"}
         import oracle
+        # num_workers = the CPUs this process may use: the GPU box's share is 16 of a machine whose
+        # nproc counts every CPU of the host (the guide for the pool), so 16 unless fewer exist
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         streams = {k: d[k] for k in ("c_slot", "c_val", "c_rate", "g_slot", "g_val", "h_slot", "h_val", "h_rate",
                                      "s_slot", "s_off", "s_bytes")}
         secs, _, ref = oracle.baseline_run_full(threads, n_slots, streams, PCT)
+        model = "unknown"
+        try:
+            with open("/proc/cpuinfo") as fh:
+                for line in fh:
+                    if line.startswith("model name"):
+                        model = line.split(":", 1)[1].strip()
+                        break
+        except OSError:
+            pass
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            affinity = os.cpu_count() or 1
         result["cpu_baseline"] = {"value": args.samples / secs, "unit": "samples/s", "cores": threads,
-                                  "kind": "port", "seconds": secs,
+                                  "kind": "port", "seconds": secs, "num_workers": threads,
+                                  "nproc": os.cpu_count(), "cpus_usable": affinity, "cpu_model": model,
                                   "sample": "the full C4 flush window above (%d samples); C restatement of the Go "
-                                            "Worker.ProcessMetric + flush path, %d worker threads routed by key"
-                                            % (args.samples, threads)}
+                                            "Worker.ProcessMetric + flush path (oracle/), num_workers = %d worker "
+                                            "threads routed by key digest %% num_workers (SURVEY 8(d)); the GPU box "
+                                            "grants this process a share of %d CPUs of the machine's nproc = %s"
+                                            % (args.samples, threads, threads, os.cpu_count())}
         if args.c5_hosts > 0:
             t1 = time.time()
             result["c5"] = c5_leg(args, rank)

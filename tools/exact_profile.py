@@ -49,8 +49,9 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     for i in range(5):
         out["cyc_per_merge_" + NAMES[i]] = round(p[i] / merges, 1)
     out["cyc_per_merge_total"] = round(sum(p[:5]) / merges, 1)
-    for i, nme in zip(range(9, 13), ("chain.mono", "chain.bsearch", "chain.levels", "chain.compose")):
+    for i, nme in zip(range(9, 12), ("chain.forced", "chain.predict+verify", "chain.walks")):
         out["cyc_" + nme] = round(p[i] / merges, 1)
+    out["merges_walked"] = p[12]
     print(out, flush=True)
 
 

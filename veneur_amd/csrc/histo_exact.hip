@@ -643,8 +643,8 @@ __device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds
 #ifdef VN_CHAIN_WALK
   mono = false;
 #endif
-  PROF_T(c1);
-  PROF_ADD(9, p2, c1);
+  PROF_T(cq1);
+  PROF_ADD(9, p2, cq1);
   uint32_t nc = 0;
   bool overflow = false;
   const uint32_t capc = x.capc;
@@ -684,8 +684,8 @@ __device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds
       }
     }
     wave_lds_sync();
-    PROF_T(c2);
-    PROF_ADD(10, c1, c2);
+    PROF_T(cq2);
+    PROF_ADD(10, cq1, cq2);
     uint32_t levels = 1;  // t < 64 * kR needs bits 0 .. levels-1
     while ((1u << levels) < 64u * kR) levels++;
     for (uint32_t lv = 1; lv < levels; lv++) {
@@ -701,8 +701,8 @@ __device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds
       }
       wave_lds_sync();
     }
-    PROF_T(c3);
-    PROF_ADD(11, c2, c3);
+    PROF_T(cq3);
+    PROF_ADD(11, cq2, cq3);
     uint32_t p[kR];
 #pragma unroll
     for (int r = 0; r < kR; r++) p[r] = 0;
@@ -726,7 +726,7 @@ __device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds
     overflow = __any(overflow);
     if (nc > capc) nc = capc;
     PROF_T(c4);
-    PROF_ADD(12, c3, c4);
+    PROF_ADD(12, cq3, c4);
   } else {
     double base = k0, kprev_carry = k0;
     for (uint32_t b = 0; b < m && !overflow; b += 64) {
@@ -1133,11 +1133,13 @@ struct FastLds {
   ldsu64* gmask;  // [4] start mask of each 64-element group
   ldsf64* miscd;  // [2] 0: tempW broadcast
   ldsu32* flag;   // [JW] start flag of every element (written by the walkers)
-  ldsu32* misc;   // [4] 0: non-monotone k seen; 1: fast path ok (integer weights); 2: temps integer
+  ldsu32* ism;    // [JW] 1: the element is a main centroid (0: a temp)
+  ldsu32* misc;   // [8] 0: the predicted chain failed; 1: fast path ok (integer weights); 2: temps
+                  //     integer; 3: a walk comparison within the band
 };
 
 __host__ __device__ inline uint32_t fast_extra_bytes(uint32_t capc, uint32_t TP, uint32_t JW) {
-  return 8u * (capc + 2) + 8u * TP + 8u * JW + 8u * 4 + 8u * 2 + 4u * JW + 4u * 4 + 16u;
+  return 8u * (capc + 2) + 8u * TP + 8u * JW + 8u * 4 + 8u * 2 + 4u * JW + 4u * JW + 4u * 8 + 16u;
 }
 __device__ __forceinline__ FastLds fast_layout(char* p, uint32_t capc, uint32_t TP, uint32_t JW) {
   FastLds F;
@@ -1147,7 +1149,8 @@ __device__ __forceinline__ FastLds fast_layout(char* p, uint32_t capc, uint32_t 
   F.gmask = (ldsu64*)(F.kk + JW);
   F.miscd = (ldsf64*)(F.gmask + 4);
   F.flag = (ldsu32*)(F.miscd + 2);
-  F.misc = F.flag + JW;
+  F.ism = F.flag + JW;
+  F.misc = F.ism + JW;
   return F;
 }
 
@@ -1243,6 +1246,7 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
   const double T = dadd(mainW, tempW);
   const uint32_t m = nm + np, nmc = nm ? nm - 1 : 0u;
   double xv[R], xw[R], wb[R], kv[R];
+  bool ism[R];
   // ---- A: the element at each output position e: i temps and e - i mains precede it.
   // i is the number of p in [lo, hi) with P(p) = "temp p precedes main e-1-p" (true below i):
   // a four-way search, three probes per step (hi - lo <= 64 -> 16 -> 4 -> 1 -> 0: three steps
@@ -1291,6 +1295,7 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
       const bool tk = i < np && (j >= nm || tv <= mv);
       xv[r] = tk ? tv : mv;
       xw[r] = tk ? tw : mw;
+      ism[r] = !tk;
       wb[r] = dadd(F.mp[min(j, nm)], F.sp[i]);
     }
   }
@@ -1299,10 +1304,11 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
   // a close k serves: q = mergedWeight / totalWeight exactly as Go divides, then the device
   // libm's asin (a few ulps, no divisions) in place of Go's (three divisions and a square root).
   // Every comparison below is taken only when its difference lies outside 1 +- kBand, where the
-  // close and the exact k certainly agree (their k differ by < 1e-13); one inside the band makes
-  // the whole merge recompute exact k and walk the chain sequentially (misc[0]).  With integer
-  // weights >= 1 and T <= 2^40 (the fast merge's conditions) consecutive exact k differ by more
-  // than 5e-11, far above asin's ulps, so exact k is increasing and the forced-start argument holds.
+  // close and the exact k certainly agree (their k differ by < 1e-13); one inside the band sends
+  // the merge to the walks and then, if still inside it there, to exact k and the sequential walk.
+  // With integer weights >= 1 and T <= 2^40 (the fast merge's conditions) consecutive exact k
+  // differ by more than 5e-11, far above asin's ulps, so exact k is increasing and the
+  // forced-start argument holds.
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const double q = ddiv(dadd(wb[r], xw[r]), T);
@@ -1315,16 +1321,26 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
       L.gm[e] = xv[r];
       L.gw[e] = xw[r];
       F.kk[e] = kv[r];
+      F.ism[e] = ism[r] ? 1u : 0u;
     }
   }
-  if (t == 0) F.misc[0] = 0u;
+  if (t == 0) {
+    F.misc[0] = 0u;
+    F.misc[3] = 0u;
+  }
   fast_sync<NW>();
   PROF_T(f2);
-  // ---- C: forced starts, then each one walks its segment
+  // ---- C: the chain.  Predicted: every old main centroid and every forced element starts a
+  // centroid, every other temp joins the one before it (in a hot key's steady state the
+  // prediction is exact in ~99% of merges).  Each predicted start s verifies it in parallel:
+  // with base = k_{s-1} and s' its next predicted start, k_{s'-1} - base <= 1 (every element
+  // between joins, k increasing) and k_{s'} - base > 1 (s' starts).  Element 0 starts, so if
+  // every check holds the predicted starts are exactly mergeOne's, by induction.  A failed or
+  // in-band check sends the merge to the forced-start walks below.
   constexpr double kHi = 1.0 + kBand, kLo = 1.0 - kBand;
-  bool fr[R];
+  bool fr[R], pr[R];
   double km1[R];
-  bool unsure = false;
+  bool bad = false;
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const uint32_t e = r * NT + t;
@@ -1332,67 +1348,135 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
     km1[r] = e >= 1 ? a : k0;
     const double d = kv[r] - (e >= 2 ? b : k0);
     fr[r] = e < m && (e == 0 || d > kHi);
-    unsure |= e < m && e >= 1 && d >= kLo && d <= kHi;
+    bad |= e < m && e >= 1 && d >= kLo && d <= kHi;
+    pr[r] = e < m && (fr[r] || ism[r]);
   }
-  // walk: element j starts a centroid when k_j - base > 1 (base = k before the current
-  // centroid's first element); a walker stops at the next forced element (k_j - k_{j-2} > 1),
-  // whose own thread starts it.  Eight k per LDS round trip, branch-free: every lane steps until
-  // no walker of its wave is left.
+  PROF_T(cq1);
 #pragma unroll
   for (int r = 0; r < R; r++) {
-    const uint32_t e = r * NT + t;
-    if (fr[r]) F.flag[e] = 1u;
-    bool alive = fr[r] && e + 1 < m;
-    double base = km1[r], p2 = km1[r], p1 = kv[r];  // p2 = k_{j-2}, p1 = k_{j-1}
-    uint32_t j = e + 1;
-    while (__any(alive)) {
-      double kb[8];
+    if (pr[r]) {
+      const uint32_t e = r * NT + t;
+      double p2 = km1[r], p1 = kv[r];  // k_{j-2}, k_{j-1} for the forced test of element j
+      uint32_t j = e + 1, sn = m;
+      double ksn = 0.0, ksn1 = kv[r];    // k_{s'} and k_{s'-1}
+      while (j < m && sn == m) {
+        double kb[4];
+        uint32_t im[4];
 #pragma unroll
-      for (int u = 0; u < 8; u++) kb[u] = F.kk[min(j + u, m - 1)];
+        for (int u = 0; u < 4; u++) {
+          kb[u] = F.kk[min(j + u, m - 1)];
+          im[u] = F.ism[min(j + u, m - 1)];
+        }
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
-        const double k2 = u == 0 ? p2 : (u == 1 ? p1 : kb[u - 2]);
-        const double km = u == 0 ? p1 : kb[u - 1];
-        const double dF = kb[u] - k2, dS = kb[u] - base;
-        const bool in = alive && j + u < m;
-        const bool stop = !in || dF > kHi;
-        unsure |= in && dF >= kLo && dF <= kHi;
-        const bool go = in && !stop;
-        const bool st_ = dS > kHi;
-        unsure |= go && dS >= kLo && dS <= kHi;
-        if (go) F.flag[j + u] = st_ ? 1u : 0u;
-        base = (go && st_) ? km : base;
-        alive = go;
+        for (int u = 0; u < 4; u++) {
+          const double k2 = u == 0 ? p2 : (u == 1 ? p1 : kb[u - 2]);
+          const double d = kb[u] - k2;
+          const bool look = sn == m && j + u < m;
+          bad |= look && d >= kLo && d <= kHi;
+          if (look && (im[u] != 0u || d > kHi)) {
+            sn = j + u;
+            ksn = kb[u];
+            ksn1 = u == 0 ? p1 : kb[u - 1];
+          }
+        }
+        p2 = kb[2];
+        p1 = kb[3];
+        j += 4;
       }
-      j += 8;
-      p2 = kb[6];
-      p1 = kb[7];
+      if (sn > e + 1) bad |= ksn1 - km1[r] > kLo;       // the last element before s' joins
+      if (sn < m) bad |= !(ksn - km1[r] > kHi);         // s' starts
     }
   }
-  if (__any(unsure) && lane == 0) F.misc[0] = 1u;
+#pragma unroll
+  for (int r = 0; r < R; r++) {
+    const uint64_t bal = __ballot(pr[r]);
+    if (lane == 0) F.gmask[r * NW + wv] = bal;
+  }
+#ifdef VN_FAST_NOPRED
+  bad = true;  // (variant: every merge takes the forced-start walks)
+#endif
+  if (__any(bad) && lane == 0) F.misc[0] = 1u;
   fast_sync<NW>();
-  if (F.misc[0]) {  // a comparison within the band: exact k, then mergeOne's sequential walk
+  PROF_T(cq2);
+  if (F.misc[0]) {
+    // forced-start walks: element j starts a centroid when k_j - base > 1 (base = k before the
+    // current centroid's first element); a walker stops at the next forced element (k_j -
+    // k_{j-2} > 1), whose own thread starts it.  Eight k per LDS round trip; the forced tests
+    // of a batch do not depend on base, only the start tests chain through it.
+    bool unsure = false;
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      if (fr[r]) {
+        const uint32_t e = r * NT + t;
+        F.flag[e] = 1u;
+        double base = km1[r], p2 = km1[r], p1 = kv[r];  // p2 = k_{j-2}, p1 = k_{j-1}
+        uint32_t j = e + 1;
+        bool run = j < m;
+        while (run) {
+          double kb[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) kb[u] = F.kk[min(j + u, m - 1)];
+          bool frc[8];
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            const double dF = kb[u] - (u == 0 ? p2 : (u == 1 ? p1 : kb[u - 2]));
+            frc[u] = j + u >= m || dF > kHi;
+            unsure |= j + u < m && dF >= kLo && dF <= kHi;
+          }
+#pragma unroll
+          for (int u = 0; u < 8; u++) {
+            if (run) {
+              if (frc[u]) {
+                run = false;
+              } else {
+                const double dS = kb[u] - base;
+                const bool st_ = dS > kHi;
+                unsure |= dS >= kLo && dS <= kHi;
+                F.flag[j] = st_ ? 1u : 0u;
+                base = st_ ? (u == 0 ? p1 : kb[u - 1]) : base;
+                j++;
+              }
+            }
+          }
+          p2 = kb[6];
+          p1 = kb[7];
+        }
+      }
+    }
+    if (__any(unsure) && lane == 0) F.misc[3] = 1u;
+    fast_sync<NW>();
+    if (F.misc[3]) {  // a comparison within the band: exact k, then mergeOne's sequential walk
+#pragma unroll
+      for (int r = 0; r < R; r++) {
+        const uint32_t e = r * NT + t;
+        if (e < m) F.kk[e] = index_estimate(x.delta, ddiv(dadd(wb[r], xw[r]), T));
+      }
+      fast_sync<NW>();
+      if (wv == 0) walk_flags(F, m, k0);
+      fast_sync<NW>();
+    }
 #pragma unroll
     for (int r = 0; r < R; r++) {
       const uint32_t e = r * NT + t;
-      if (e < m) F.kk[e] = index_estimate(x.delta, ddiv(dadd(wb[r], xw[r]), T));
+      const uint64_t bal = __ballot(e < m && F.flag[e] != 0u);
+      if (lane == 0) F.gmask[r * NW + wv] = bal;
     }
     fast_sync<NW>();
-    if (wv == 0) walk_flags(F, m, k0);
-    fast_sync<NW>();
   }
+  PROF_T(cq3);
+  PROF_ADD(9, f2, cq1);
+  PROF_ADD(10, cq1, cq2);
+  PROF_ADD(11, cq2, cq3);
+  PROF_ADD(12, 0, F.misc[0] ? 1 : 0);
   PROF_T(f3);
   // ---- D: centroid index and end of every start, Welford over its elements
+  const uint64_t g0 = F.gmask[0], g1 = F.gmask[1], g2 = F.gmask[2], g3 = F.gmask[3];
   bool st[R];
 #pragma unroll
   for (int r = 0; r < R; r++) {
     const uint32_t e = r * NT + t;
-    st[r] = e < m && F.flag[e] != 0u;
-    const uint64_t bal = __ballot(st[r]);
-    if (lane == 0) F.gmask[r * NW + wv] = bal;
+    st[r] = e < m && ((sel4((e >> 6) & 3u, g0, g1, g2, g3) >> (e & 63u)) & 1ull);
   }
-  fast_sync<NW>();
-  const uint64_t g0 = F.gmask[0], g1 = F.gmask[1], g2 = F.gmask[2], g3 = F.gmask[3];
   const uint32_t c0 = (uint32_t)__popcll(g0), c1 = (uint32_t)__popcll(g1), c2 = (uint32_t)__popcll(g2);
   const uint32_t nc = c0 + c1 + c2 + (uint32_t)__popcll(g3);
 #pragma unroll
