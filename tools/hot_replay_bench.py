@@ -23,17 +23,25 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--fast", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--cold-keys", type=int, default=0, help="extra short keys in the same batch")
+    ap.add_argument("--cold-n", type=int, default=100, help="samples per short key")
+    ap.add_argument("--rates", action="store_true", help="10%% of samples at rate 0.5 or 0.1 (C4's mix)")
     a = ap.parse_args()
     import veneur_amd as V
     import veneur_amd._abi as A
     rng = np.random.default_rng(1)
-    slot = np.repeat(np.arange(a.keys, dtype=np.uint32), a.n)
+    slot = np.concatenate([np.repeat(np.arange(a.keys, dtype=np.uint32), a.n),
+                           np.repeat(np.arange(a.keys, a.keys + a.cold_keys, dtype=np.uint32), a.cold_n)])
     rng.shuffle(slot)
     val = rng.lognormal(np.log(50.0), 1.0, len(slot))
     rate = np.ones(len(slot), np.float32)
+    if a.rates:
+        u = rng.random(len(slot))
+        rate = np.where(u < 0.05, np.float32(0.1), np.where(u < 0.1, np.float32(0.5), np.float32(1.0))).astype(np.float32)
     pct = (0.5, 0.9, 0.99, 0.999)
     bufs = [V.DeviceBuffer(slot), V.DeviceBuffer(val), V.DeviceBuffer(rate)]
-    with V.Engine((1, 1, a.keys, 1), percentiles=pct, max_batch_records=len(slot) + 1,
+    nk = a.keys + a.cold_keys
+    with V.Engine((1, 1, nk, 1), percentiles=pct, max_batch_records=len(slot) + 1,
                   exact_threshold=32768 if a.fast else 0) as e:
         b = A.Batch()
         b.n_histo = len(slot)
@@ -48,13 +56,14 @@ def main():
             times.append(time.perf_counter() - t0)
         ms = min(times[1:]) * 1e3
     merges = a.n // 42
-    out = {"mode": "fast" if a.fast else "exact", "keys": a.keys, "samples_per_key": a.n, "ms_window": ms,
+    out = {"mode": "fast" if a.fast else "exact", "keys": a.keys, "samples_per_key": a.n, "cold_keys": a.cold_keys,
+           "rates": a.rates, "ms_window": ms,
            "us_per_merge_longest": ms * 1e3 / max(1, merges)}
     if not a.no_check:
         import oracle
-        w = oracle.Worker(1, 1, a.keys, 1)
+        w = oracle.Worker(1, 1, nk, 1)
         w.histo(slot, val, rate)
-        oq = np.array([[w.histo_quantile(k, p) for p in pct] for k in range(a.keys)])
+        oq = np.array([[w.histo_quantile(k, p) for p in pct] for k in range(nk)])
         out["quantiles_bit_exact"] = bool(np.array_equal(f.histo_quantiles, oq))
     print(out, flush=True)
 

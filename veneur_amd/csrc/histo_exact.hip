@@ -793,6 +793,13 @@ __device__ __forceinline__ void merge_any(const MergeParams x, const Lds L, uint
   else merge_sorted_fast<5>(x, L, nm, mainW, np, tempW);
 }
 
+// merge_any out of line: the long replays' rare fallback, kept out of their merge loop's code
+__device__ __noinline__ NmW merge_any_v(const MergeParams x, const Lds L, uint32_t nm, double mainW, uint32_t np,
+                                       double tempW) {
+  merge_any(x, L, nm, mainW, np, tempW);
+  return NmW{nm, mainW};
+}
+
 // sort the pending temps in LDS and merge them
 __device__ __noinline__ NmW merge_pending_v(const MergeParams x, const Lds L, uint32_t nm, double mainW, uint32_t np) {
   PROF_T(a0);
@@ -1165,7 +1172,7 @@ __device__ __forceinline__ uint64_t sel4(uint32_t q, uint64_t g0, uint64_t g1, u
 }
 
 // start flags of the m merged elements by mergeOne's sequential walk (wave 0; non-monotone k)
-__device__ void walk_flags(const FastLds F, uint32_t m, double k0) {
+__device__ __noinline__ void walk_flags(const FastLds F, uint32_t m, double k0) {
   const uint32_t lane = threadIdx.x & 63;
   double base = k0, kprev_carry = k0;
   bool first = true;
@@ -1194,7 +1201,7 @@ __device__ void walk_flags(const FastLds F, uint32_t m, double k0) {
 
 // mp[0..nm] from the main weights (wave 0); misc[1] = every weight an integer and their sum
 // equal to mainW (then every prefix is exact)
-__device__ void prefix_main_w0(const Lds L, const FastLds F, uint32_t nm, double mainW) {
+__device__ __noinline__ void prefix_main_w0(const Lds L, const FastLds F, uint32_t nm, double mainW) {
   const uint32_t lane = threadIdx.x & 63;
   double carry = 0.0;
   bool ok = true;
@@ -1219,7 +1226,7 @@ __device__ void prefix_main_w0(const Lds L, const FastLds F, uint32_t nm, double
 }
 
 // sp[0..np] from the sorted temps' weights (wave 0, np <= 64); misc[2] = all integers
-__device__ void prefix_temps_w0(const Lds L, const FastLds F, uint32_t np) {
+__device__ __noinline__ void prefix_temps_w0(const Lds L, const FastLds F, uint32_t np) {
   const uint32_t lane = threadIdx.x & 63;
   const double w = lane < np ? L.sw[lane] : 0.0;
   const bool ok = __all(is_int_weight(w));
@@ -1553,6 +1560,54 @@ __host__ __device__ inline uint32_t fast_offset(uint32_t capc, uint32_t tcap) {
   return ((uint32_t)exact_smem_bytes_hd(capc, tcap) + 15u) & ~15u;
 }
 
+struct MergeState {
+  uint32_t nm;
+  double w;
+  bool fok;  // the key's weights are all integers: the fast merge applies
+};
+
+// one mergeAllTemps of the sorted temps sv/sw (with sp when tint): the fast merge when it
+// applies, else wave 0's one-wave merge (out of line) and the main prefix rebuilt after it
+template <int NW>
+__device__ __forceinline__ MergeState merge_step(const MergeParams mp, const Lds L, const FastLds F, MwSharedL& S,
+                                                 MergeState st, uint32_t n_, double tempW, bool tint, double k0) {
+  constexpr uint32_t NT = 64 * NW, R = 4 / NW;
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t m = st.nm + n_;
+#ifdef VN_FAST_MERGE_OFF
+  if (false) {  // A/B and debugging variant: every merge by wave 0's one-wave merge
+#else
+  if (st.fok && tint && n_ <= 64 && m < NT * R && m <= mp.capc && dadd(st.w, tempW) <= 1099511627776.0) {
+#endif
+    merge_fast<NW>(mp, L, F, st.nm, st.w, n_, tempW, k0);
+    return st;
+  }
+  if (wv == 0) {
+    const NmW r = merge_any_v(mp, L, st.nm, st.w, n_, tempW);
+    if (lane == 0) {
+      S.fb_nm = r.nm;
+      S.fb_w = r.w;
+    }
+  }
+  fast_sync<NW>();
+  st.nm = S.fb_nm;
+  st.w = S.fb_w;
+  if (st.fok && tint) {
+    if (wv == 0) prefix_main_w0(L, F, st.nm, st.w);
+    fast_sync<NW>();
+    st.fok = F.misc[1] != 0u;
+  } else {
+    st.fok = false;
+  }
+  fast_sync<NW>();  // S and misc are read before anyone writes them again
+  return st;
+}
+template <int NW>
+__device__ __noinline__ MergeState merge_step_cold(const MergeParams mp, const Lds L, const FastLds F, MwSharedL& S,
+                                                   MergeState st, uint32_t n_, double tempW, bool tint, double k0) {
+  return merge_step<NW>(mp, L, F, S, st, n_, tempW, tint, k0);
+}
+
 // replay of one key with NW waves (tcap <= 64, ingest only: no flush-mode adoption)
 template <int NW>
 __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& S) {
@@ -1628,33 +1683,16 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
   // a merge of the sorted temps sv/sw (with sp when tint): the fast merge when it applies, else
   // wave 0's one-wave merge (and the main prefix rebuilt after it)
   auto merge_sorted_any = [&](uint32_t n_, double tempW, bool tint) {
-    const uint32_t m = nm + n_;
-#ifdef VN_FAST_MERGE_OFF
-    if (false) {  // A/B and debugging variant: every merge by wave 0's one-wave merge
-#else
-    if (fok && tint && n_ <= 64 && m < NT * R && m <= capc && dadd(mainW, tempW) <= 1099511627776.0) {
-#endif
-      merge_fast<NW>(mp, L, F, nm, mainW, n_, tempW, k0);
-      return;
-    }
-    if (wv == 0) {
-      merge_any(mp, L, nm, mainW, n_, tempW);
-      if (lane == 0) {
-        S.fb_nm = nm;
-        S.fb_w = mainW;
-      }
-    }
-    fast_sync<NW>();
-    nm = S.fb_nm;
-    mainW = S.fb_w;
-    if (fok && tint) {
-      if (wv == 0) prefix_main_w0(L, F, nm, mainW);
-      fast_sync<NW>();
-      fok = F.misc[1] != 0u;
-    } else {
-      fok = false;
-    }
-    fast_sync<NW>();  // S and misc are read before anyone writes them again
+    const MergeState r = merge_step<NW>(mp, L, F, S, MergeState{nm, mainW, fok}, n_, tempW, tint, k0);
+    nm = r.nm;
+    mainW = r.w;
+    fok = r.fok;
+  };
+  auto merge_sorted_cold = [&](uint32_t n_, double tempW, bool tint) {
+    const MergeState r = merge_step_cold<NW>(mp, L, F, S, MergeState{nm, mainW, fok}, n_, tempW, tint, k0);
+    nm = r.nm;
+    mainW = r.w;
+    fok = r.fok;
   };
   auto merge_pend = [&]() {  // sort the pending temps (wave 0), then merge them
     if (wv == 0) {
@@ -1668,7 +1706,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     const double tempW = F.miscd[0];
     const bool tint = F.misc[2] != 0u;
     fast_sync<NW>();
-    merge_sorted_any(np, tempW, tint);
+    merge_sorted_cold(np, tempW, tint);
   };
 
   if (nex && np == tcap) {
