@@ -58,11 +58,13 @@ def test_ranks_partition_one_global_stream():
 
 
 def test_c4_window_through_engine_matches_oracle():
-    """One rank, the hottest keys split (the single-GPU split path): counters, gauges and sets
-    bit-exact, histogram Local* stats exact, quantiles within 1e-3 rank error."""
+    """One rank, the hottest keys split (the single-GPU split path; split timers are gathered whole
+    to their owner and replayed there): counters, gauges and sets bit-exact, histogram Local*
+    stats exact, quantiles identical to the restated Go (the default exact mode)."""
     import bench
     counts = V.synth_key_counts(SEED, KEYS, N_SAMPLES, N_SAMPLES)
-    split = bench.hot_keys(counts, 1.0, bench.key_classes(SEED, KEYS), N_SAMPLES / 128, 10000, 16)
+    split = bench.hot_keys(counts, 1.0, bench.key_classes(SEED, KEYS), N_SAMPLES / 128, 10000, 16,
+                           split_histos=True)
     assert all(len(split[c]) for c in (0, 2, 3))
     st = V.DeviceStream(SEED, KEYS, N_SAMPLES, 0, 1, split=split)
     d = st.to_host()
@@ -88,4 +90,5 @@ def test_c4_window_through_engine_matches_oracle():
     oq = np.array([[w.histo_quantile(int(s), p) for p in PCT] for s in f.histo_slot])
     err = rank_errors(d, f.histo_slot, f.histo_quantiles, oq)
     assert err.max() <= 1e-3, err.max()
+    np.testing.assert_array_equal(f.histo_quantiles, oq)
     st.free()
