@@ -292,3 +292,33 @@ def test_split_close_runs_combine_in_engine_thread(N):
         np.testing.assert_array_equal(a.histo_quantiles, b.histo_quantiles)
         for i, k in enumerate(a.histo_slot.tolist()):
             np.testing.assert_array_equal(a.histo_quantiles[i], [w.histo_quantile(k, p) for p in PCT])
+
+
+def test_split_slot_with_direct_records_is_reported_not_mixed():
+    """A split key's records belong to vn_ingest_split.  A window in which its slot also gets
+    vn_ingest records (or imports) keeps the split combine's state -- moved on the engine's own
+    stream after every ingest of the window -- and the flush reports the misuse (VN_EINVAL) once;
+    the next window is unaffected."""
+    from veneur_amd.engine import EngineError
+    rng = np.random.default_rng(11)
+    v = rng.lognormal(3.0, 1.0, 5000)
+    comms = Comm.local(1)
+    e = V.Engine((1, 1, 4, 4), percentiles=PCT, max_batch_records=1 << 16, split_max_records=1 << 16)
+    try:
+        e.set_comm(comms[0])
+        e.split_keys(2, np.array([1], np.uint32), np.array([0], np.uint32))
+        e.ingest_split(histos=(np.zeros(len(v), np.uint32), v, np.ones(len(v), np.float32)))
+        e.ingest(histos=(np.array([1, 2], np.uint32), np.array([7.0, 8.0]), np.ones(2, np.float32)))
+        with pytest.raises(EngineError, match="split key"):
+            e.flush()
+        # the next window: split records only, no error, the single consumer's digest
+        e.split_keys(2, np.array([1], np.uint32), np.array([0], np.uint32))
+        e.ingest_split(histos=(np.zeros(len(v), np.uint32), v, np.ones(len(v), np.float32)))
+        f = e.flush()
+        assert f.histo_slot.tolist() == [1]
+        w = oracle.Worker(1, 1, 1, 1)
+        w.histo(np.zeros(len(v), np.uint32), v, np.ones(len(v), np.float32))
+        np.testing.assert_array_equal(f.histo_quantiles[0], [w.histo_quantile(0, p) for p in PCT])
+    finally:
+        e.close()
+        comms[0].close()

@@ -32,7 +32,7 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     with V.Engine((1, 1, nk, 1), compression=100.0, percentiles=(0.5, 0.99),
                   max_batch_records=len(slots) + 1) as e:
         e.timing_enable(True)
-        buf = (C.c_ulonglong * 16)()
+        buf = (C.c_ulonglong * 32)()
         A.lib.vn_prof_exact_read(buf, 1)
         t0 = time.perf_counter()
         e.ingest(histos=(slots, vals, rates))
@@ -52,6 +52,19 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     for i, nme in zip(range(9, 12), ("chain.forced", "chain.predict+verify", "chain.walks")):
         out["cyc_" + nme] = round(p[i] / merges, 1)
     out["merges_walked"] = p[12]
+    nb = max(1, p[23])
+    out["batches"] = p[23]
+    out["batch_committed"] = p[24]
+    out["batch_avg_committed"] = round(p[24] / nb, 2)
+    out["batch_avg_usable"] = round(p[26] / nb, 2)
+    out["batch_avg_flagged"] = round(p[25] / nb, 2)
+    for i, nme in zip(range(16, 23), ("load", "totals", "assign", "scatter", "lanes", "bounds", "flagged+commit")):
+        out["batch_cyc_" + nme] = round(p[i] / nb, 1)
+    out["batch_cyc_stats"] = round(p[27] / nb, 1)
+    out["singles_after_reject"] = p[29]
+    out["singles_after_reject_cyc"] = p[28]
+    out["singles_unbatchable"] = p[31]
+    out["singles_unbatchable_cyc"] = p[30]
     print(out, flush=True)
 
 
@@ -59,4 +72,5 @@ if __name__ == "__main__":
     # one hot key: with the default (exact) engine it replays on the four-wave kernel, whose
     # phases are A = merge-path positions + weight prefix, B = k values, C = forced starts and
     # walks, D = masks + Welford (merge_fast); the one-wave kernel reports the old phase names
-    run(int(sys.argv[1]) if len(sys.argv) > 1 else 1000000, 0, 0)
+    for n in (sys.argv[1:] or ["1000000"]):
+        run(int(n), 0, 0)

@@ -473,12 +473,24 @@ void destroy_impl(vn_engine* e) {
   if (e->st) (void)hipStreamDestroy(e->st);
 }
 
-void check_error_flags(vn_engine* e) {
+// throws on the engine's invariant flags; returns the caller-error flags (cleared on the device)
+uint32_t check_error_flags(vn_engine* e) {
   uint32_t flags = 0;
   VN_HIP_CHECK(hipMemcpy(&flags, e->h_err, sizeof(uint32_t), hipMemcpyDeviceToHost));
   if (flags & 1u) throw std::runtime_error("t-digest centroid tile overflow (compression too large for cap_cent)");
   if (flags & 2u) throw std::runtime_error("HLL rebase invariant violated");
   if (flags & 4u) throw std::runtime_error("t-digest chain window hand-off stalled");
+  const uint32_t caller = flags & kErrSplitTouched;  // the caller's error, not the engine's: reported once
+  if (caller) {
+    flags &= ~caller;
+    VN_HIP_CHECK(hipMemcpy(e->h_err, &flags, sizeof(uint32_t), hipMemcpyHostToDevice));
+  }
+  return caller;
+}
+void throw_caller_errors(uint32_t caller) {
+  if (caller & kErrSplitTouched)
+    throw std::invalid_argument("a split key's slot also received vn_ingest records or imports this window "
+                                "(its records go through vn_ingest_split); the split combine's state was kept");
 }
 
 // Validation of a device-resident batch (vn_ingest), where the reference would panic or the
@@ -1041,7 +1053,7 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
     flush_all(e, out, histo_quantile_mask, set_estimate_mask);
     VN_HIP_CHECK(hipGetLastError());
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[6], e->st));
-    check_error_flags(e);
+    const uint32_t caller = check_error_flags(e);
     if (e->timing) {
       VN_HIP_CHECK(hipEventSynchronize(e->ev[6]));
       vn_timing& t = e->last;
@@ -1096,6 +1108,7 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
       e->w_open = false;
     }
     e->sp.ran = false;
+    throw_caller_errors(caller);  // (the window is flushed; the error is the caller's)
   });
 }
 
@@ -1104,7 +1117,7 @@ int vn_sync(vn_engine* e) {
   return guarded(e, [&] {
     histo_imports_drain(e);
     VN_HIP_CHECK(hipStreamSynchronize(e->st));
-    check_error_flags(e);
+    throw_caller_errors(check_error_flags(e));
   });
 }
 

@@ -76,6 +76,20 @@ struct SplitState {
   hipEvent_t ev_done = nullptr;     // its combine done (this engine's stream waits on it)
   hipEvent_t ev_histo = nullptr, ev_set_prefix = nullptr;  // milestones inside it (vn_timing)
   bool ran = false;                 // ev_done recorded by this window's flush
+  // the finished states' moves into this engine's slots, launched by vn_flush on this engine's
+  // stream (after every ingest and import of the window), not by the combine beside it
+  struct HistoMove {
+    uint32_t K = 0;
+    const uint32_t* okeys = nullptr;
+    const uint64_t* tot = nullptr;
+    const double *sums = nullptr, *mins = nullptr, *maxs = nullptr;
+  } mv_histo;
+  struct SetMove {
+    uint32_t H = 0;
+    const uint32_t* owner = nullptr;
+    int me = 0;
+    const uint64_t* tot = nullptr;
+  } mv_set;
   // vn_split_close: the split engine's combine runs in this host thread while the caller goes
   // on ingesting; vn_flush joins it
   std::thread worker;

@@ -42,7 +42,7 @@ __host__ __device__ inline size_t exact_smem_bytes_hd(uint32_t capc, uint32_t tc
 
 #ifdef VN_EXACT_PROF
 // profiling build only (tools/exact_profile.py): cycles per merge phase of block 0
-__device__ unsigned long long g_exact_prof[16];
+__device__ unsigned long long g_exact_prof[32];
 __device__ __forceinline__ long long prof_stamp() {  // a scheduling fence around the stamp
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -1608,6 +1608,337 @@ __device__ __noinline__ MergeState merge_step_cold(const MergeParams mp, const L
   return merge_step<NW>(mp, L, F, S, st, n_, tempW, tint, k0);
 }
 
+// ---- batched replay of consecutive pure chunks (the long replays' steady state).
+//
+// In a long key's steady state almost every merge keeps one structure: every old main centroid
+// starts a centroid and every temp joins the one before it (the prediction merge_fast verifies
+// one merge at a time).  While it holds the centroid count stays fixed and the centroids evolve
+// independently: centroid i's mean is a sequential Welford over the temps that land between it
+// and centroid i+1, merge after merge.  merge_batch takes up to kBB pure chunks at once, one lane
+// per centroid walking the chunks in order:
+//   assign   n[j][i] = temps of chunk j placed before main i, guessed from the means at the batch
+//            start (#temps with v <= mean_i: an upper bound search per chunk)
+//   prefix   the exact integer prefix P of main i in merge j (MP0 + the temps before it) and its
+//            weight, so q = P/T of every structure test (the chunk totals T are exact integers)
+//   decide   the merge-path decisions of merge j around main i, against the mean merge j really
+//            sees: main i before temp n[j][i] (mean < v), temp n[j][i]-1 before main i (v <= mean)
+//   Welford  the temps of the centroid, in Go's Centroid.Add order
+//   k bounds k is increasing, so min/max of each centroid's q bound all its k tests of the batch;
+//            a centroid whose bounds are not certain (outside 1 +- kBand) is tested merge by merge
+// and commits the merges before the first one any check rejects.  Those are exactly the
+// reference's merges (the checks of merge j hold given merges < j; by induction); the rejected
+// merge is then done alone by merge_step.  tools/study/batch_replay_sim.c restates this on the CPU:
+// bit-identical to the per-merge replay, 28 of 32 merges committed per batch on a 16M-sample key.
+// The chunk sorter's arrays are copied into an LDS ring (chunk c at slot c % kRing) by
+// global->LDS loads that need no registers: the chunks after the batch are in flight while it runs.
+#ifndef VN_BATCH_MERGES
+#define VN_BATCH_MERGES 32
+#endif
+constexpr uint32_t kBB = VN_BATCH_MERGES;  // merges per batch
+constexpr uint32_t kRing = kBB + 24;        // chunk slots in LDS
+constexpr uint32_t kBM = 160;               // most centroids a batch takes (delta 100: ~135)
+constexpr uint32_t kBN = kBM + 1;           // lanes of a batch (one per centroid, one for the end)
+constexpr uint32_t kBTmax = 48;             // largest temp buffer batched (delta <= ~110)
+#ifndef VN_BATCH_MIN_W
+#define VN_BATCH_MIN_W 8192.0
+#endif
+constexpr double kBatchMinW = VN_BATCH_MIN_W;  // batches start once the digest holds this weight
+constexpr uint32_t kBatchBackoff = 4;          // single merges after a batch that took none
+constexpr uint32_t kWelfK = 4;                 // temps per (centroid, chunk) in straight-line code
+
+typedef __attribute__((address_space(3))) uint8_t ldsu8;
+
+struct BatchLds {
+  ldsf64* rv;   // [kRing][tcap] the chunk sorter's csv: sorted temp means
+  ldsf64* rw;   // [kRing][tcap] csw: their signed weights (negative: an imported centroid)
+  ldsf64* rt;   // [kRing][tcap] ctw: [0] signed Add-order tempW (negative: a non-integer
+                //               weight), [p] the exclusive prefix of the sorted |weights|
+  ldsf64* bT;   // [kBB] total weight after chunk j of the batch
+  ldsf64* brT;  // [kBB] 1 / bT
+  ldsf64* kb;   // [3][kBN] k(min qe), k(max qb), k(min qb) per centroid
+  ldsf64* mh;   // [kBB][kBN] mean of centroid i before chunk j
+  ldsu32* ch;   // [kBB][kBN] temps' weight before main i, chunks 0..j
+  ldsu32* ctl;  // [4] 0: first rejected merge; 1: #flagged; 2: usable chunks
+  ldsu16* flagged;  // [kBM] centroids whose bound tests are not certain
+  ldsu8* nT;        // [kBN][kBB] n[j][i], lane-major
+};
+
+__host__ __device__ inline uint32_t batch_bytes(uint32_t tcap) {
+  return 24u * kRing * tcap + 16u * kBB + 24u * kBN + 8u * kBB * kBN + 4u * kBB * kBN + 16u + 2u * kBM + 16u +
+         kBN * kBB;
+}
+__host__ __device__ inline uint32_t batch_offset(uint32_t capc, uint32_t tcap) {
+  const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = capc + TP + 1 > 320u ? capc + TP + 1 : 320u;
+  return (fast_offset(capc, tcap) + fast_extra_bytes(capc, TP, JW) + 15u) & ~15u;
+}
+__device__ __forceinline__ BatchLds batch_layout(char* p, uint32_t tcap) {
+  BatchLds B;
+  B.rv = (ldsf64*)p;
+  B.rw = B.rv + kRing * tcap;
+  B.rt = B.rw + kRing * tcap;
+  B.bT = B.rt + kRing * tcap;
+  B.brT = B.bT + kBB;
+  B.kb = B.brT + kBB;
+  B.mh = B.kb + 3 * kBN;
+  B.ch = (ldsu32*)(B.mh + kBB * kBN);
+  B.ctl = B.ch + kBB * kBN;
+  B.flagged = (ldsu16*)(B.ctl + 4);
+  B.nT = (ldsu8*)(((uintptr_t)(B.flagged + kBM) + 15u) & ~(uintptr_t)15u);
+  return B;
+}
+
+__device__ __forceinline__ double k_close(double delta, double q) {
+  return delta * (asin(dsub(dmul(2.0, q), 1.0)) * (1.0 / kPi) + 0.5);
+}
+__device__ __forceinline__ void lds_min(ldsu32* p, uint32_t v) { __atomic_fetch_min(p, v, __ATOMIC_RELAXED); }
+__device__ __forceinline__ uint32_t lds_inc(ldsu32* p) { return __atomic_fetch_add(p, 1u, __ATOMIC_RELAXED); }
+
+// n doubles from global src into LDS dst by global->LDS dword loads: each wave instruction moves
+// 64 dwords (the destination is wave-uniform, lane l its dword l).  Completion: vmcnt.
+template <int NW>
+__device__ __forceinline__ void dma_doubles(ldsf64* dst, const double* __restrict__ src, uint32_t n) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nd = 2 * n;
+  const uint32_t* s = (const uint32_t*)src;
+  ldsu32* d = (ldsu32*)dst;
+  for (uint32_t q = wv; 64 * q < nd; q += NW) {
+    const uint32_t k = 64 * q + lane;
+    if (k < nd) __builtin_amdgcn_global_load_lds(s + k, (__attribute__((address_space(3))) void*)(d + 64 * q), 4, 0, 0);
+  }
+}
+// chunks [x, y) (y - x <= kRing) of the chunk sorter's arrays into their ring slots
+template <int NW>
+__device__ __forceinline__ void ring_fill(const BatchLds B, const double* gv, const double* gw, const double* gt,
+                                          uint32_t x, uint32_t y, uint32_t tcap) {
+  const uint32_t s0 = x % kRing, n = y - x, n1 = min(n, kRing - s0);
+  const uint64_t g0 = (uint64_t)x * tcap;
+  dma_doubles<NW>(B.rv + s0 * tcap, gv + g0, n1 * tcap);
+  dma_doubles<NW>(B.rw + s0 * tcap, gw + g0, n1 * tcap);
+  dma_doubles<NW>(B.rt + s0 * tcap, gt + g0, n1 * tcap);
+  if (n > n1) {
+    const uint64_t g1 = (uint64_t)(x + n1) * tcap;
+    dma_doubles<NW>(B.rv, gv + g1, (n - n1) * tcap);
+    dma_doubles<NW>(B.rw, gw + g1, (n - n1) * tcap);
+    dma_doubles<NW>(B.rt, gt + g1, (n - n1) * tcap);
+  }
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Merges chunks c .. c+b-1 (in the ring) as far as the checks allow.  Returns the merges
+// committed (0..b): L.mm/L.mw/F.mp/mainW then hold the digest after them.
+template <int NW>
+__device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L, const FastLds F, const BatchLds B,
+                                                const uint32_t nm, double& mainW, const uint32_t c, uint32_t b,
+                                                const uint32_t tcap) {
+  constexpr uint32_t NT = 64 * NW;
+  constexpr double kHi = 1.0 + kBand, kLo = 1.0 - kBand;
+  static_assert(NT >= kBN, "one lane per centroid");
+  const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  PROF_T(b0);
+  // ---- totals: the usable chunks are the leading ones with integer weights, T <= 2^40 and the
+  // batch's temp weight < 2^32 (the ch table)
+  if (wv == 0) {
+    const double tws = lane < b ? B.rt[((c + lane) % kRing) * tcap] : -1.0;
+    bool ok = lane < b && tws >= 0.0;
+    double v = ok ? tws : 0.0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const double o = __shfl_up(v, d, 64);
+      v = (int)lane >= d ? dadd(v, o) : v;
+    }
+    const double T = dadd(mainW, v);
+    ok = ok && T <= 1099511627776.0 && v < 4294967296.0;
+    const uint64_t bad = __ballot(!ok);
+    const uint32_t nb = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+    if (lane < b) {
+      B.bT[lane] = T;
+      B.brT[lane] = ddiv(1.0, T);
+    }
+    if (lane == 0) {
+      B.ctl[0] = min(nb, b);
+      B.ctl[1] = 0u;
+      B.ctl[2] = min(nb, b);
+    }
+  }
+  fast_sync<NW>();
+  PROF_T(b1);
+  b = B.ctl[2];
+  if (b < 2) {
+    fast_sync<NW>();
+    return 0u;
+  }
+  // ---- assign: lane i, every chunk: #temps with v <= mean_i (branch-free upper bound searches;
+  // every lane searches, so each round's loads issue back to back)
+  const uint32_t i = t;
+  const bool cen = i < nm, act = i <= nm;
+  const double m0 = cen ? L.mm[i] : 0.0;
+  uint32_t na[kBB / 4];  // n[.][i], four chunks per word (the end lane: tcap everywhere)
+  {
+    uint32_t ni[kBB];
+#pragma unroll
+    for (uint32_t j = 0; j < kBB; j++) ni[j] = 0u;
+    if (wv * 64u <= nm) {  // (a wave with no centroid skips the searches)
+#pragma unroll
+    for (uint32_t step = 32; step >= 1; step >>= 1) {  // (tcap <= 48 < 64)
+      double v[kBB];
+#pragma unroll
+      for (uint32_t j = 0; j < kBB; j++) v[j] = B.rv[((c + j) % kRing) * tcap + min(ni[j] + step, tcap) - 1];
+#pragma unroll
+      for (uint32_t j = 0; j < kBB; j++) {
+        const uint32_t q = ni[j] + step;
+        ni[j] = ((q <= tcap) & (v[j] <= m0)) ? q : ni[j];
+      }
+    }
+    }
+#pragma unroll
+    for (uint32_t g = 0; g < kBB / 4; g++) {
+      uint32_t wd = 0;
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) wd |= (cen ? ni[4 * g + u] : tcap) << (8 * u);
+      na[g] = wd;
+      if (act) *(ldsu32*)(B.nT + i * kBB + 4 * g) = wd;
+    }
+  }
+  fast_sync<NW>();
+  PROF_T(b2);
+  // ---- one lane per centroid: prefix, decisions, Welford; the end lane (i = nm): the prefix
+  uint32_t jf = b;
+  double mean = m0, W = cen ? L.mw[i] : 0.0;
+  if (act) {
+    const double mp0 = F.mp[i];
+    double qbmin = 2.0, qbmax = -1.0, qemin = 2.0, C = 0.0;
+    const ldsu8* const nrow = B.nT + i * kBB;
+    const ldsu8* const nrow1 = B.nT + (cen ? i + 1 : i) * kBB;
+    // chunk j's operands, loaded during chunk j-1 (a rolled loop: the loaded registers are its
+    // loop-carried values, so nothing waits for them before their use)
+    double nv[kWelfK + 1], nw[kWelfK], ns0 = 0.0, ntw = 0.0, nrT = 0.0;
+    uint32_t na_ = 0, ne_ = 0;
+    auto fetch = [&](uint32_t j) {
+      const uint32_t sl = ((c + j) % kRing) * tcap, a = nrow[j];
+      na_ = a;
+      ne_ = nrow1[j];
+      ns0 = B.rt[sl + min(a, tcap - 1)];
+      ntw = B.rt[sl];
+      nrT = B.brT[j];
+      nv[0] = B.rv[sl + (a ? a - 1 : 0)];
+#pragma unroll
+      for (uint32_t u = 0; u < kWelfK; u++) {
+        nv[u + 1] = B.rv[sl + min(a + u, tcap - 1)];
+        nw[u] = B.rw[sl + min(a + u, tcap - 1)];
+      }
+    };
+    fetch(0);
+#pragma unroll 1
+    for (uint32_t j = 0; j < b; j++) {
+      B.mh[j * kBN + i] = mean;
+      const uint32_t a = na_, e = cen ? ne_ : a;
+      // the chunk's temp weight before main i: the prefix at a (0 at a = 0, tempW at a = tcap)
+      const double s0 = a >= tcap ? ntw : (a == 0 ? 0.0 : ns0);
+      const double rT = nrT;
+      double cv[kWelfK + 1], cw[kWelfK];
+#pragma unroll
+      for (uint32_t u = 0; u <= kWelfK; u++) cv[u] = nv[u];
+#pragma unroll
+      for (uint32_t u = 0; u < kWelfK; u++) cw[u] = nw[u];
+      fetch(min(j + 1, kBB - 1));  // (past b: read and unused)
+      C = dadd(C, s0);
+      B.ch[j * kBN + i] = (uint32_t)C;
+      const double P = dadd(mp0, C);
+      const double qb = P * rT, qe = dadd(P, W) * rT;
+      qbmin = __builtin_fmin(qbmin, qb);
+      qbmax = __builtin_fmax(qbmax, qb);
+      qemin = __builtin_fmin(qemin, qe);
+      // merge j's decisions around main i, with the mean merge j sees (branch-free)
+      const bool ok = cen & ((a >= tcap) | (mean < cv[1])) & ((a == 0) | ((i > 0) & (cv[0] <= mean)));
+      jf = (cen & !ok & (jf == b)) ? j : jf;
+      const uint32_t cnt = e - a;
+#pragma unroll
+      for (uint32_t u = 0; u < kWelfK; u++) {
+        if (__any(u < cnt)) {
+          const double w = __builtin_fabs(cw[u]);
+          const double W2 = dadd(W, w);
+          const double mean2 = dadd(mean, ddiv(dmul(dsub(cv[u + 1], mean), w), W2));
+          W = u < cnt ? W2 : W;
+          mean = u < cnt ? mean2 : mean;
+        }
+      }
+      if (__any(cnt > kWelfK)) {  // the rare long run of one chunk
+        const uint32_t sl = ((c + j) % kRing) * tcap;
+        for (uint32_t p = a + kWelfK; p < a + cnt; p++) {
+          const double w = __builtin_fabs(B.rw[sl + p]);
+          W = dadd(W, w);
+          mean = dadd(mean, ddiv(dmul(dsub(B.rv[sl + p], mean), w), W));
+        }
+      }
+    }
+    if (b < kBB) B.mh[b * kBN + i] = mean;
+    B.kb[i] = k_close(delta, qemin);
+    B.kb[kBN + i] = k_close(delta, qbmax);
+    B.kb[2 * kBN + i] = k_close(delta, qbmin);
+    if (jf < b) lds_min(&B.ctl[0], jf);
+  }
+  fast_sync<NW>();
+  PROF_T(b3);
+  // ---- bound tests: main i starts (i >= 1) and its temps join, in every merge
+  if (cen) {
+    bool sure = true;
+    if (i >= 1) sure = B.kb[i] - B.kb[kBN + i - 1] > kHi;
+    sure = sure && B.kb[kBN + i + 1] - B.kb[2 * kBN + i] < kLo;
+    if (!sure) B.flagged[lds_inc(&B.ctl[1])] = (uint16_t)i;
+  }
+  fast_sync<NW>();
+  PROF_T(b4);
+  const uint32_t nflag = B.ctl[1];
+  if (nflag) {
+    // exact tests of the flagged centroids, merge by merge (before the first decision reject)
+    const uint32_t jp = B.ctl[0];
+    for (uint32_t f = t; f < nflag * jp; f += NT) {
+      const uint32_t q = f / jp, j = f - q * jp, ic = B.flagged[q];
+      const double rT = B.brT[j];
+      const double Pi = dadd(F.mp[ic], (double)B.ch[j * kBN + ic]);
+      const double Pn = dadd(F.mp[ic + 1], (double)B.ch[j * kBN + ic + 1]);
+      const double Wi = j ? dadd(L.mw[ic], (double)(B.ch[(j - 1) * kBN + ic + 1] - B.ch[(j - 1) * kBN + ic]))
+                          : L.mw[ic];
+      bool ok = true;
+      if (ic >= 1) {
+        const double Pp = dadd(F.mp[ic - 1], (double)B.ch[j * kBN + ic - 1]);
+        ok = k_close(delta, dadd(Pi, Wi) * rT) - k_close(delta, Pp * rT) > kHi;
+      }
+      const uint32_t na_ = B.nT[ic * kBB + j], nb_ = B.nT[(ic + 1) * kBB + j];
+      if (nb_ > na_) ok = ok && k_close(delta, Pn * rT) - k_close(delta, Pi * rT) < kLo;
+      if (!ok) lds_min(&B.ctl[0], j);
+    }
+    fast_sync<NW>();
+  }
+  PROF_T(b5);
+  const uint32_t js = B.ctl[0];
+  if (js > 0) {
+    // commit merges 0..js-1: means, weights, the main prefix
+    if (act) {
+      const uint32_t c0 = B.ch[(js - 1) * kBN + i];
+      if (cen) {
+        const uint32_t c1 = B.ch[(js - 1) * kBN + i + 1];
+        L.mm[i] = js < kBB ? B.mh[js * kBN + i] : mean;  // (mean before chunk js)
+        L.mw[i] = dadd(L.mw[i], (double)(c1 - c0));
+      }
+      F.mp[i] = dadd(F.mp[i], (double)c0);  // (i = nm: the new total)
+    }
+    mainW = B.bT[js - 1];
+  }
+  fast_sync<NW>();
+  PROF_T(b6);
+  PROF_ADD(16, b0, b1);
+  PROF_ADD(17, b1, b2);
+  PROF_ADD(18, b2, b3);
+  PROF_ADD(19, b3, b4);
+  PROF_ADD(20, b4, b5);
+  PROF_ADD(21, b5, b6);
+  PROF_ADD(23, 0, 1);
+  PROF_ADD(24, 0, (long long)js);
+  PROF_ADD(25, 0, (long long)nflag);
+  PROF_ADD(26, 0, (long long)b);
+  return js;
+}
+
 // replay of one key with NW waves (tcap <= 64, ingest only: no flush-mode adoption)
 template <int NW>
 __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& S) {
@@ -1734,22 +2065,85 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       }
       ctw = xctw[base];
     };
-    load(0);
-    for (uint32_t c = 0; c < sp.npure; c++) {
-      double tempW = __builtin_fabs(ctw), tintd = ctw >= 0.0 ? 1.0 : 0.0;
-      if (t < tcap) {
-        L.sv[t] = cv;
-        L.sw[t] = __builtin_fabs(cw);
-        F.sp[t] = t ? cp : 0.0;
-        stat(cv, __builtin_fabs(cw), cw > 0.0);
+    // chunks [c0, c1) one merge at a time, the next chunk's loads in flight during each merge
+    auto singles = [&](uint32_t c0, uint32_t c1) {
+      load(c0);
+      for (uint32_t c = c0; c < c1; c++) {
+        double tempW = __builtin_fabs(ctw), tintd = ctw >= 0.0 ? 1.0 : 0.0;
+        if (t < tcap) {
+          L.sv[t] = cv;
+          L.sw[t] = __builtin_fabs(cw);
+          F.sp[t] = t ? cp : 0.0;
+          stat(cv, __builtin_fabs(cw), cw > 0.0);
+        }
+        if (t == tcap) F.sp[tcap] = tempW;
+        hold2(tempW, tintd);
+        hold_stats(sw, sxw, srw, mn, mx, dmn, dmx);
+        if (c + 1 < c1) load(c + 1);
+        fast_sync<NW>();
+        merge_sorted_any(tcap, tempW, tintd != 0.0);
       }
-      if (t == tcap) F.sp[tcap] = tempW;
-      hold2(tempW, tintd);
-      hold_stats(sw, sxw, srw, mn, mx, dmn, dmx);
-      if (c + 1 < sp.npure) load(c + 1);
+    };
+#ifdef VN_BATCH_OFF
+    singles(0, sp.npure);
+#else
+    const BatchLds Bt = batch_layout(smem + batch_offset(capc, tcap), tcap);
+    const uint64_t cb = (uint64_t)lo + sp.off0;
+    const double* const gv = xcsv + cb;
+    const double* const gw = xcsw + cb;
+    const double* const gt = xctw + cb;
+    uint32_t ring_lo = 0, ring_hi = 0;  // chunks [ring_lo, ring_hi) are in the ring (or on their way)
+    uint32_t c = 0;
+    while (c < sp.npure) {
+      const uint32_t left = sp.npure - c;
+      if (!(fok && nm >= 1 && nm <= kBM && left >= 2 && mainW >= kBatchMinW && tcap <= kBTmax)) {
+        // not (yet) batchable: a run of single merges, then look again
+        const uint32_t c1 = min(sp.npure, c + kBatchBackoff);
+        PROF_T(s3);
+        singles(c, c1);
+        PROF_T(s4);
+        PROF_ADD(30, s3, s4);
+        PROF_ADD(31, 0, (long long)(c1 - c));
+        c = c1;
+        continue;
+      }
+      const uint32_t b = min(kBB, left);
+      if (c < ring_lo || c > ring_hi) ring_lo = ring_hi = c;  // (after a run of singles)
+      if (c + b > ring_hi) {  // the rest of the batch, now
+        ring_fill<NW>(Bt, gv, gw, gt, ring_hi, c + b, tcap);
+        ring_hi = c + b;
+      }
+      dma_wait();
       fast_sync<NW>();
-      merge_sorted_any(tcap, tempW, tintd != 0.0);
+      // the chunks after it, while it runs (their slots hold chunks < c)
+      const uint32_t pe = min(c + kRing, sp.npure);
+      if (pe > ring_hi) {
+        ring_fill<NW>(Bt, gv, gw, gt, ring_hi, pe, tcap);
+        ring_hi = pe;
+      }
+      ring_lo = max(c, ring_hi > kRing ? ring_hi - kRing : 0u);
+      const uint32_t js = merge_batch<NW>(x.delta, L, F, Bt, nm, mainW, c, b, tcap);
+      PROF_T(s0);
+      for (uint32_t e = t; e < js * tcap; e += NT) {  // the committed chunks' Local* statistics
+        const uint32_t j = e / tcap, p = e - j * tcap;
+        const uint32_t sl = ((c + j) % kRing) * tcap + p;
+        const double w = Bt.rw[sl];
+        stat(Bt.rv[sl], __builtin_fabs(w), w > 0.0);
+      }
+      PROF_T(s1);
+      PROF_ADD(27, s0, s1);
+      c += js;
+      if (js < b) {  // the rejected merge alone (after a batch that took nothing: a run of them)
+        const uint32_t c1 = min(sp.npure, c + (js == 0 ? kBatchBackoff : 1u));
+        singles(c, c1);
+        PROF_T(s2);
+        PROF_ADD(28, s1, s2);
+        PROF_ADD(29, 0, (long long)(c1 - c));
+        c = c1;
+      }
     }
+    dma_wait();  // (nothing may still be landing in LDS when the block moves on)
+#endif
   }
   const uint32_t tail = sp.off0 + sp.npure * tcap;
   if (nex > tail) append(tail, nex);
@@ -1902,14 +2296,18 @@ void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* 
 
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap) { return exact_smem_bytes_hd(capc, tcap); }
 size_t exact_fast_smem_bytes(uint32_t capc, uint32_t tcap) {
+#ifdef VN_BATCH_OFF
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = std::max(capc + TP + 1, 320u);
   return fast_offset(capc, tcap) + fast_extra_bytes(capc, TP, JW);
+#else
+  return batch_offset(capc, tcap) + batch_bytes(tcap);
+#endif
 }
 #ifdef VN_EXACT_PROF
 extern "C" int vn_prof_exact_read(unsigned long long* out16, int reset) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_exact_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_exact_prof), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_exact_prof), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

@@ -8,6 +8,9 @@
 namespace vn {
 
 constexpr uint32_t kErrDecode = 8u;  // device error flag: malformed import payload
+// device error flag: a split key's slot also received vn_ingest records or imports this window
+// (its state comes whole from the split combine; the split key's records go through vn_ingest_split)
+constexpr uint32_t kErrSplitTouched = 16u;
 
 // A malformed import payload (where the reference's decoder errors or panics): VN_EDECODE.
 struct DecodeError : std::runtime_error {

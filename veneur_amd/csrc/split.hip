@@ -81,11 +81,15 @@ vn_comm* group_of(vn_engine* e) {
 // replay of the ordinary keys; its host waits only wait for its own stream.  The finished
 // states move into this engine's slots (k_split_move_*), before this engine's flush reads them.
 constexpr uint32_t kMaxSplitKeys = 256;  // per class
+__global__ void k_split_errors(uint32_t* __restrict__ from, uint32_t* __restrict__ to);
 
 vn_engine* split_engine(vn_engine* e, uint64_t records) {
   SplitState& S = e->sp;
   if (S.aux && S.aux->max_records >= records) return S.aux;
   if (S.aux) {
+    // (its error flags, e.g. a tile overflow of this window's compression, carry over)
+    hipLaunchKernelGGL(k_split_errors, dim3(1), dim3(64), 0, S.aux->st, S.aux->h_err, e->h_err);
+    VN_HIP_CHECK(hipStreamSynchronize(S.aux->st));
     vn_engine_destroy(S.aux);
     S.aux = nullptr;
   }
@@ -497,10 +501,12 @@ __global__ __launch_bounds__(256) void k_split_move_histo(const uint32_t* __rest
                                                           const double* __restrict__ sums,
                                                           const double* __restrict__ mins,
                                                           const double* __restrict__ maxs, HistoSlots src,
-                                                          HistoSlots dst, uint32_t capc, uint32_t tcap) {
+                                                          HistoSlots dst, uint32_t capc, uint32_t tcap,
+                                                          uint32_t* __restrict__ err) {
   const uint32_t k = blockIdx.x, h = okeys[k];
   if (tot[h]) {
     const uint32_t s = kslot[h];
+    if (threadIdx.x == 0 && dst.htouch[s]) atomicOr(err, kErrSplitTouched);
     const uint64_t fo = (uint64_t)k * capc, to = (uint64_t)s * capc;
     for (uint32_t i = threadIdx.x; i < capc; i += blockDim.x) {
       dst.cm0[to + i] = src.cm0[fo + i];
@@ -828,9 +834,7 @@ void split_histos(vn_engine* e, vn_comm* c) {
       histo_rounds(a, a->h_hotlist, K, maxp, nmic, K, MA_, MB_, a->hA2, a->hB2, micw, st);
     }
   }
-  HistoSlots src = histo_slots(a), dst = histo_slots(e);
-  hipLaunchKernelGGL(k_split_move_histo, dim3(K), dim3(256), 0, st, dok, S.d_slot[VN_HISTO], tot, sums, mins, maxs,
-                     src, dst, e->cap_cent, e->temp_cap);
+  S.mv_histo = SplitState::HistoMove{K, dok, tot, sums, mins, maxs};  // (moved by split_flush)
 }
 
 // ---------------------------------------------------------------- sets
@@ -1067,10 +1071,11 @@ SetSlots set_slots(vn_engine* e) {
 __global__ __launch_bounds__(256) void k_split_move_set(const uint32_t* __restrict__ kslot,
                                                         const uint32_t* __restrict__ owner, int me,
                                                         const uint64_t* __restrict__ tot, SetSlots src,
-                                                        SetSlots dst) {
+                                                        SetSlots dst, uint32_t* __restrict__ err) {
   const uint32_t k = blockIdx.x;
   if (owner[k] == (uint32_t)me && tot[k]) {
     const uint32_t s = kslot[k];
+    if (threadIdx.x == 0 && dst.touch[s]) atomicOr(err, kErrSplitTouched);
     for (uint32_t i = threadIdx.x; i < kArenaWords; i += blockDim.x)
       dst.arena[(uint64_t)s * kArenaWords + i] = src.arena[(uint64_t)k * kArenaWords + i];
     for (uint32_t i = threadIdx.x; i < kTmpCap; i += blockDim.x)
@@ -1216,8 +1221,7 @@ void split_sets(vn_engine* e, vn_comm* c) {
     hipLaunchKernelGGL(k_ep_finish, dim3(H), dim3(kBlock), 0, st, H, kslot, W, cand,
                        reinterpret_cast<uint8_t*>(a->sarena), a->sbase, a->snz, p0, done, a->h_err);
   }
-  hipLaunchKernelGGL(k_split_move_set, dim3(H), dim3(256), 0, st, S.d_slot[VN_SET], downer, me, tot, set_slots(a),
-                     set_slots(e));
+  S.mv_set = SplitState::SetMove{H, downer, me, tot};  // (moved by split_flush)
 }
 
 }  // namespace
@@ -1263,6 +1267,18 @@ void split_flush(vn_engine* e) {
     }
     S.ran = true;
     VN_HIP_CHECK(hipStreamWaitEvent(e->st, S.ev_done, 0));
+    // the finished states into this engine's slots, behind every ingest and import of the window
+    // on this stream: a slot that also got records here is reported (kErrSplitTouched), not mixed
+    vn_engine* a = S.aux;
+    if (S.mv_histo.K)
+      hipLaunchKernelGGL(k_split_move_histo, dim3(S.mv_histo.K), dim3(256), 0, e->st, S.mv_histo.okeys,
+                         S.d_slot[VN_HISTO], S.mv_histo.tot, S.mv_histo.sums, S.mv_histo.mins, S.mv_histo.maxs,
+                         histo_slots(a), histo_slots(e), e->cap_cent, e->temp_cap, e->h_err);
+    if (S.mv_set.H)
+      hipLaunchKernelGGL(k_split_move_set, dim3(S.mv_set.H), dim3(256), 0, e->st, S.d_slot[VN_SET], S.mv_set.owner,
+                         S.mv_set.me, S.mv_set.tot, set_slots(a), set_slots(e), e->h_err);
+    S.mv_histo = SplitState::HistoMove{};
+    S.mv_set = SplitState::SetMove{};
   }
   S.closed = false;
   split_counters(e, c, e->st);
