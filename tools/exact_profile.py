@@ -58,9 +58,13 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     out["batch_avg_committed"] = round(p[24] / nb, 2)
     out["batch_avg_usable"] = round(p[26] / nb, 2)
     out["batch_avg_flagged"] = round(p[25] / nb, 2)
-    for i, nme in zip(range(16, 23), ("load", "totals", "assign", "scatter", "lanes", "bounds", "flagged+commit")):
+    for i, nme in zip(range(16, 22), ("totals", "assign", "lanes", "bounds", "flagged", "commit")):
         out["batch_cyc_" + nme] = round(p[i] / nb, 1)
     out["batch_cyc_stats"] = round(p[27] / nb, 1)
+    out["batch_w0_prefix_loop"] = round(p[13] / nb, 1)
+    out["batch_w0_welford_loop"] = round(p[14] / nb, 1)
+    out["batch_w0_decision_loop"] = round(p[15] / nb, 1)
+    out["batch_lane0_nonempty_chunks"] = round(p[22] / nb, 2)
     out["singles_after_reject"] = p[29]
     out["singles_after_reject_cyc"] = p[28]
     out["singles_unbatchable"] = p[31]

@@ -165,7 +165,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_bt, ch); dzero(e->h_bt, ch, st);
   dalloc(e->h_pos, (size_t)ch + 1);
   dalloc(e->h_tl, ch);
-  dalloc(e->h_cnt, 16);
+  dalloc(e->h_cnt, 32);
   const uint64_t touch_max = ch ? std::min<uint64_t>(ch, R) : 0;
   e->h_sort_cap = ch ? R + touch_max * capc : 0;
   dalloc(e->hA0, e->h_sort_cap); dalloc(e->hB0, e->h_sort_cap);

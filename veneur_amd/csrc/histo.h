@@ -32,7 +32,8 @@ struct ExactCtx {
   const uint32_t* keys;      // slot of each processed key
   const uint32_t* order;     // replay only: key indices of this launch (nullptr: 0..nkeys-1)
   uint32_t norder;           // replay grid when order is set
-  const uint32_t* mw_count;  // replay: the first *mw_count entries of order64 are replayed by the four-wave kernel
+  const uint32_t* mw_count;  // replay: the first *mw_count entries of order64 are replayed by the four-wave kernel,
+                             // the first mw_count[1] of them batched (k_histo_exact_mwb)
   const uint64_t* order64;   // replay only: key index in the low 32 bits, longest first (norder)
   const uint32_t* start;     // per slot: first record of its segment (arrival order)
   const uint32_t* nex;       // per processed key: records to replay exactly (nullptr: none)
@@ -77,10 +78,12 @@ void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint
 void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks);
 void histo_exact_replay(const ExactCtx& x, hipStream_t st);
 // The longest keys of x.order64 (>= min_len samples to replay, at most 4096) replay with four
-// waves each: histo_exact_count_long counts them into *count on st and sets x.mw_count, so
+// waves each: histo_exact_count_long counts them into count[0] (and those of at least
+// kBatchMinLen samples, batched, into count[1]) on st and sets x.mw_count, so
 // histo_exact_replay skips them; histo_exact_replay_long replays them (any stream after st).
 bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipStream_t st);
-void histo_exact_replay_long(const ExactCtx& x, hipStream_t st);
+// the batched kernel (the longest keys) on st, the rest of the long keys on st_rest
+void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest);
 // the replay over x.keys[0, *dev_count) (count known on the device only; <= max_keys)
 void histo_exact_replay_list(const ExactCtx& x, const uint32_t* dev_count, uint32_t max_keys, hipStream_t st);
 // replay list[0..n) longest first: sorts the order into buf0/buf1 (n each) on st and sets x

@@ -1644,6 +1644,11 @@ constexpr uint32_t kBTmax = 48;             // largest temp buffer batched (delt
 #endif
 constexpr double kBatchMinW = VN_BATCH_MIN_W;  // batches start once the digest holds this weight
 constexpr uint32_t kBatchBackoff = 4;          // single merges after a batch that took none
+#ifndef VN_BATCH_MIN_LEN
+#define VN_BATCH_MIN_LEN 65536u
+#endif
+// keys replaying at least this many samples take the batched kernel (its LDS: one block per CU)
+constexpr uint32_t kBatchMinLen = VN_BATCH_MIN_LEN;
 constexpr uint32_t kWelfK = 4;                 // temps per (centroid, chunk) in straight-line code
 
 typedef __attribute__((address_space(3))) uint8_t ldsu8;
@@ -1656,16 +1661,19 @@ struct BatchLds {
   ldsf64* bT;   // [kBB] total weight after chunk j of the batch
   ldsf64* brT;  // [kBB] 1 / bT
   ldsf64* kb;   // [3][kBN] k(min qe), k(max qb), k(min qb) per centroid
-  ldsf64* mh;   // [kBB][kBN] mean of centroid i before chunk j
+  ldsf64* ms;   // [kBB * kBTmax] each centroid's means after each of its temps (its list's slice)
   ldsu32* ch;   // [kBB][kBN] temps' weight before main i, chunks 0..j
   ldsu32* ctl;  // [4] 0: first rejected merge; 1: #flagged; 2: usable chunks
   ldsu16* flagged;  // [kBM] centroids whose bound tests are not certain
   ldsu8* nT;        // [kBN][kBB] n[j][i], lane-major
+  ldsu8* bcnt;      // [kBB][kBTmax] #batch-start means < v of each temp
+  ldsu16* al;       // [kBB * kBTmax] each centroid's temps (ring offsets), in merge order; centroid
+                    //                i's slice starts at sum_j n[j][i]
 };
 
 __host__ __device__ inline uint32_t batch_bytes(uint32_t tcap) {
-  return 24u * kRing * tcap + 16u * kBB + 24u * kBN + 8u * kBB * kBN + 4u * kBB * kBN + 16u + 2u * kBM + 16u +
-         kBN * kBB;
+  return 24u * kRing * tcap + 16u * kBB + 24u * kBN + 8u * kBB * kBTmax + 4u * kBB * kBN + 16u + 2u * kBM + 16u +
+         kBN * kBB + kBB * kBTmax + 16u + 2u * kBB * kBTmax;
 }
 __host__ __device__ inline uint32_t batch_offset(uint32_t capc, uint32_t tcap) {
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = capc + TP + 1 > 320u ? capc + TP + 1 : 320u;
@@ -1679,11 +1687,13 @@ __device__ __forceinline__ BatchLds batch_layout(char* p, uint32_t tcap) {
   B.bT = B.rt + kRing * tcap;
   B.brT = B.bT + kBB;
   B.kb = B.brT + kBB;
-  B.mh = B.kb + 3 * kBN;
-  B.ch = (ldsu32*)(B.mh + kBB * kBN);
+  B.ms = B.kb + 3 * kBN;
+  B.ch = (ldsu32*)(B.ms + kBB * kBTmax);
   B.ctl = B.ch + kBB * kBN;
   B.flagged = (ldsu16*)(B.ctl + 4);
   B.nT = (ldsu8*)(((uintptr_t)(B.flagged + kBM) + 15u) & ~(uintptr_t)15u);
+  B.bcnt = B.nT + kBN * kBB;
+  B.al = (ldsu16*)(((uintptr_t)(B.bcnt + kBB * kBTmax) + 15u) & ~(uintptr_t)15u);
   return B;
 }
 
@@ -1731,13 +1741,19 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
                                                 const uint32_t tcap) {
   constexpr uint32_t NT = 64 * NW;
   constexpr double kHi = 1.0 + kBand, kLo = 1.0 - kBand;
+  constexpr uint32_t kItems = (kBB * kBTmax + NT - 1) / NT;  // batch temps per thread
   static_assert(NT >= kBN, "one lane per centroid");
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const uint32_t cr = c % kRing;
+  auto slot = [&](uint32_t j) {  // ring offset of the batch's chunk j
+    const uint32_t s = cr + j;
+    return (s >= kRing ? s - kRing : s) * tcap;
+  };
   PROF_T(b0);
   // ---- totals: the usable chunks are the leading ones with integer weights, T <= 2^40 and the
   // batch's temp weight < 2^32 (the ch table)
   if (wv == 0) {
-    const double tws = lane < b ? B.rt[((c + lane) % kRing) * tcap] : -1.0;
+    const double tws = lane < b ? B.rt[slot(lane)] : -1.0;
     bool ok = lane < b && tws >= 0.0;
     double v = ok ? tws : 0.0;
 #pragma unroll
@@ -1766,116 +1782,227 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
     fast_sync<NW>();
     return 0u;
   }
-  // ---- assign: lane i, every chunk: #temps with v <= mean_i (branch-free upper bound searches;
-  // every lane searches, so each round's loads issue back to back)
-  const uint32_t i = t;
-  const bool cen = i < nm, act = i <= nm;
-  const double m0 = cen ? L.mm[i] : 0.0;
-  uint32_t na[kBB / 4];  // n[.][i], four chunks per word (the end lane: tcap everywhere)
+  // ---- assign: lane i, every chunk: n[j][i] = #temps with v <= mean_i (branch-free upper bound
+  // searches, every lane's 32 in step so each round's loads issue back to back; a wave with no
+  // centroid skips them), into nT (lane-major)
   {
+    const uint32_t i = t;
+    const double mi = i < nm ? L.mm[i] : 0.0;
     uint32_t ni[kBB];
 #pragma unroll
     for (uint32_t j = 0; j < kBB; j++) ni[j] = 0u;
-    if (wv * 64u <= nm) {  // (a wave with no centroid skips the searches)
+    if (wv * 64u <= nm) {
 #pragma unroll
-    for (uint32_t step = 32; step >= 1; step >>= 1) {  // (tcap <= 48 < 64)
-      double v[kBB];
+      for (uint32_t step = 32; step >= 1; step >>= 1) {  // (tcap <= 48 < 64)
+        double v[kBB];
 #pragma unroll
-      for (uint32_t j = 0; j < kBB; j++) v[j] = B.rv[((c + j) % kRing) * tcap + min(ni[j] + step, tcap) - 1];
+        for (uint32_t j = 0; j < kBB; j++) v[j] = B.rv[slot(j) + min(ni[j] + step, tcap) - 1];
 #pragma unroll
-      for (uint32_t j = 0; j < kBB; j++) {
-        const uint32_t q = ni[j] + step;
-        ni[j] = ((q <= tcap) & (v[j] <= m0)) ? q : ni[j];
+        for (uint32_t j = 0; j < kBB; j++) {
+          const uint32_t q = ni[j] + step;
+          ni[j] = ((q <= tcap) & (v[j] <= mi)) ? q : ni[j];
+        }
       }
     }
-    }
+    if (i <= nm) {
 #pragma unroll
-    for (uint32_t g = 0; g < kBB / 4; g++) {
-      uint32_t wd = 0;
+      for (uint32_t g = 0; g < kBB / 4; g++) {
+        uint32_t wd = 0;
 #pragma unroll
-      for (uint32_t u = 0; u < 4; u++) wd |= (cen ? ni[4 * g + u] : tcap) << (8 * u);
-      na[g] = wd;
-      if (act) *(ldsu32*)(B.nT + i * kBB + 4 * g) = wd;
+        for (uint32_t u = 0; u < 4; u++) wd |= (i < nm ? ni[4 * g + u] : tcap) << (8 * u);
+        *(ldsu32*)(B.nT + i * kBB + 4 * g) = wd;
+      }
     }
   }
   fast_sync<NW>();
   PROF_T(b2);
-  // ---- one lane per centroid: prefix, decisions, Welford; the end lane (i = nm): the prefix
-  uint32_t jf = b;
-  double mean = m0, W = cen ? L.mw[i] : 0.0;
-  if (act) {
-    const double mp0 = F.mp[i];
-    double qbmin = 2.0, qbmax = -1.0, qemin = 2.0, C = 0.0;
-    const ldsu8* const nrow = B.nT + i * kBB;
-    const ldsu8* const nrow1 = B.nT + (cen ? i + 1 : i) * kBB;
-    // chunk j's operands, loaded during chunk j-1 (a rolled loop: the loaded registers are its
-    // loop-carried values, so nothing waits for them before their use)
-    double nv[kWelfK + 1], nw[kWelfK], ns0 = 0.0, ntw = 0.0, nrT = 0.0;
-    uint32_t na_ = 0, ne_ = 0;
-    auto fetch = [&](uint32_t j) {
-      const uint32_t sl = ((c + j) % kRing) * tcap, a = nrow[j];
-      na_ = a;
-      ne_ = nrow1[j];
-      ns0 = B.rt[sl + min(a, tcap - 1)];
-      ntw = B.rt[sl];
-      nrT = B.brT[j];
-      nv[0] = B.rv[sl + (a ? a - 1 : 0)];
+  // ---- one lane per centroid (i = nm: the end, for the prefixes).  The chunk loops are unrolled
+  // (compile-time chunk indices: the lane's n bytes stay in registers) and load a group of chunks
+  // ahead; a rolled loop would copy its prefetched registers at the back edge and wait for them.
+  const uint32_t i = t;
+  const bool cen = i < nm, act = i <= nm;
+  const double m0 = cen ? L.mm[i] : 0.0;
+  uint32_t jf = b, mask = 0u, off = 0u, m = 0u;
+  uint32_t ra[kBB / 4], re[kBB / 4];  // n[j][i], n[j][i+1], four chunks per word
 #pragma unroll
-      for (uint32_t u = 0; u < kWelfK; u++) {
-        nv[u + 1] = B.rv[sl + min(a + u, tcap - 1)];
-        nw[u] = B.rw[sl + min(a + u, tcap - 1)];
-      }
-    };
-    fetch(0);
+  for (uint32_t g = 0; g < kBB / 4; g++) ra[g] = re[g] = 0u;
+  auto bmask = [&](uint32_t g) {  // the bytes of word g that are chunks < b
+    const uint32_t v = b > 4 * g ? min(b - 4 * g, 4u) : 0u;
+    return v >= 4 ? 0xffffffffu : ((1u << (8 * v)) - 1u);
+  };
+  auto bsum = [](uint32_t x) {  // sum of the four bytes
+    x = (x & 0x00ff00ffu) + ((x >> 8) & 0x00ff00ffu);
+    return (x & 0xffffu) + (x >> 16);
+  };
+  if (act) {
+#pragma unroll
+    for (uint32_t g = 0; g < kBB / 4; g++) {
+      ra[g] = *(const ldsu32*)(B.nT + i * kBB + 4 * g);
+      re[g] = cen ? *(const ldsu32*)(B.nT + (i + 1) * kBB + 4 * g) : ra[g];
+      off += bsum(ra[g] & bmask(g));  // the lane's list: [sum_j n[j][i], sum_j n[j][i+1])
+      m += bsum(re[g] & bmask(g));
+    }
+    m -= off;
+  }
+  auto by = [&](const uint32_t(&w)[kBB / 4], uint32_t j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xffu; };
+  constexpr uint32_t kG = 4;  // chunks per load group (the decisions)
+#ifdef VN_PREFIX_ROLLED
+  // -- prefixes (exact integers, so q = P/T of every structure test): a rolled loop, the n bytes
+  // two chunks ahead, the prefixes they select one chunk ahead (A/B variant)
+  if (act) {
+    const ldsu8* const nra = B.nT + i * kBB;
+    const ldsu8* const nre = B.nT + (cen ? i + 1 : i) * kBB;
+    const double mp0 = F.mp[i];
+    double qbmin = 2.0, qbmax = -1.0, qemin = 2.0, C = 0.0, W = cen ? L.mw[i] : 0.0;
+    uint32_t aN = nra[0], eN = nre[0], aNN = nra[1], eNN = nre[1];
+    double sa = B.rt[slot(0) + min(aN, tcap - 1)], se = B.rt[slot(0) + min(eN, tcap - 1)];
+    double tw = B.rt[slot(0)], rT = B.brT[0];
 #pragma unroll 1
     for (uint32_t j = 0; j < b; j++) {
-      B.mh[j * kBN + i] = mean;
-      const uint32_t a = na_, e = cen ? ne_ : a;
-      // the chunk's temp weight before main i: the prefix at a (0 at a = 0, tempW at a = tcap)
-      const double s0 = a >= tcap ? ntw : (a == 0 ? 0.0 : ns0);
-      const double rT = nrT;
-      double cv[kWelfK + 1], cw[kWelfK];
-#pragma unroll
-      for (uint32_t u = 0; u <= kWelfK; u++) cv[u] = nv[u];
-#pragma unroll
-      for (uint32_t u = 0; u < kWelfK; u++) cw[u] = nw[u];
-      fetch(min(j + 1, kBB - 1));  // (past b: read and unused)
+      const uint32_t a = aN, e = eN;
+      const double pa = sa, pe = se, twj = tw, rTj = rT;
+      const uint32_t jn = min(j + 1, kBB - 1), sn = slot(jn), jnn = min(j + 2, kBB - 1);
+      sa = B.rt[sn + min(aNN, tcap - 1)];
+      se = B.rt[sn + min(eNN, tcap - 1)];
+      tw = B.rt[sn];
+      rT = B.brT[jn];
+      aN = aNN;
+      eN = eNN;
+      aNN = nra[jnn];
+      eNN = nre[jnn];
+      const double s0 = a >= tcap ? twj : (a == 0 ? 0.0 : pa);  // chunk j's temp weight before main i
+      const double s1 = e >= tcap ? twj : (e == 0 ? 0.0 : pe);  // ... before main i + 1
       C = dadd(C, s0);
       B.ch[j * kBN + i] = (uint32_t)C;
       const double P = dadd(mp0, C);
-      const double qb = P * rT, qe = dadd(P, W) * rT;
+      const double qb = P * rTj, qe = dadd(P, W) * rTj;
       qbmin = __builtin_fmin(qbmin, qb);
       qbmax = __builtin_fmax(qbmax, qb);
       qemin = __builtin_fmin(qemin, qe);
-      // merge j's decisions around main i, with the mean merge j sees (branch-free)
-      const bool ok = cen & ((a >= tcap) | (mean < cv[1])) & ((a == 0) | ((i > 0) & (cv[0] <= mean)));
-      jf = (cen & !ok & (jf == b)) ? j : jf;
-      const uint32_t cnt = e - a;
-#pragma unroll
-      for (uint32_t u = 0; u < kWelfK; u++) {
-        if (__any(u < cnt)) {
-          const double w = __builtin_fabs(cw[u]);
-          const double W2 = dadd(W, w);
-          const double mean2 = dadd(mean, ddiv(dmul(dsub(cv[u + 1], mean), w), W2));
-          W = u < cnt ? W2 : W;
-          mean = u < cnt ? mean2 : mean;
-        }
-      }
-      if (__any(cnt > kWelfK)) {  // the rare long run of one chunk
-        const uint32_t sl = ((c + j) % kRing) * tcap;
-        for (uint32_t p = a + kWelfK; p < a + cnt; p++) {
-          const double w = __builtin_fabs(B.rw[sl + p]);
-          W = dadd(W, w);
-          mean = dadd(mean, ddiv(dmul(dsub(B.rv[sl + p], mean), w), W));
-        }
-      }
+      W = dadd(W, dsub(s1, s0));  // (the end lane: e = a)
+      mask |= (e > a ? 1u : 0u) << j;
     }
-    if (b < kBB) B.mh[b * kBN + i] = mean;
     B.kb[i] = k_close(delta, qemin);
     B.kb[kBN + i] = k_close(delta, qbmax);
     B.kb[2 * kBN + i] = k_close(delta, qbmin);
-    if (jf < b) lds_min(&B.ctl[0], jf);
   }
+#else
+  // -- prefixes (exact integers, so q = P/T of every structure test), unrolled over the chunks:
+  // the n bytes are in registers (compile-time chunk indices), so a group's loads all issue at
+  // once, a group ahead of its use
+  if (act) {
+    const double mp0 = F.mp[i];
+    double qbmin = 2.0, qbmax = -1.0, qemin = 2.0, C = 0.0, W = cen ? L.mw[i] : 0.0;
+    constexpr uint32_t kP = 8;  // chunks per load group
+    double gsa[2][kP], gse[2][kP], gtw[2][kP], grT[2][kP];
+#pragma unroll
+    for (uint32_t g = 0; g <= kBB / kP; g++) {
+      if (g < kBB / kP) {
+#pragma unroll
+        for (uint32_t u = 0; u < kP; u++) {
+          const uint32_t j = kP * g + u, sl = slot(j);
+          gsa[g & 1][u] = B.rt[sl + min(by(ra, j), tcap - 1)];
+          gse[g & 1][u] = B.rt[sl + min(by(re, j), tcap - 1)];
+          gtw[g & 1][u] = B.rt[sl];
+          grT[g & 1][u] = B.brT[j];
+        }
+      }
+      if (g == 0) continue;
+      const uint32_t h = g - 1;
+#pragma unroll
+      for (uint32_t u = 0; u < kP; u++) {
+        const uint32_t j = kP * h + u, a = by(ra, j), e = by(re, j);
+        const bool in = j < b;
+        const double twj = gtw[h & 1][u], rTj = grT[h & 1][u];
+        const double s0 = in ? (a >= tcap ? twj : (a == 0 ? 0.0 : gsa[h & 1][u])) : 0.0;  // temps before main i
+        const double s1 = in ? (e >= tcap ? twj : (e == 0 ? 0.0 : gse[h & 1][u])) : 0.0;  // ... before main i+1
+        C = dadd(C, s0);
+        B.ch[j * kBN + i] = (uint32_t)C;  // (rows j >= b: unused)
+        const double P = dadd(mp0, C);
+        const double qb = P * rTj, qe = dadd(P, W) * rTj;
+        qbmin = in ? __builtin_fmin(qbmin, qb) : qbmin;
+        qbmax = in ? __builtin_fmax(qbmax, qb) : qbmax;
+        qemin = in ? __builtin_fmin(qemin, qe) : qemin;
+        W = dadd(W, dsub(s1, s0));
+        mask |= (in && e > a ? 1u : 0u) << j;
+      }
+    }
+    B.kb[i] = k_close(delta, qemin);
+    B.kb[kBN + i] = k_close(delta, qbmax);
+    B.kb[2 * kBN + i] = k_close(delta, qbmin);
+  }
+#endif
+  PROF_T(l1);
+  PROF_ADD(13, b2, l1);
+  // -- Welford over the lane's temps in order (Go's Centroid.Add): a cursor over the chunks that
+  // gave it temps (the mask); the mean after each temp into ms (the lane's slice: off + k).  The
+  // next temp's loads are in flight during each add.
+  if (cen && m) {
+    const ldsu8* const nra = B.nT + i * kBB;
+    const ldsu8* const nre = B.nT + (i + 1) * kBB;
+    ldsf64* const ms = B.ms + off;
+    double W = L.mw[i], mean = m0;
+    uint32_t jc = (uint32_t)__builtin_ctz(mask), pc = nra[jc], ec = nre[jc];
+    uint32_t sc = slot(jc);
+    double cv = B.rv[sc + pc], cw = B.rw[sc + pc];
+    for (uint32_t q = 0; q < m; q++) {
+      uint32_t jn = jc, pn = pc + 1, en = ec;
+      if (pn >= ec) {  // the next chunk with temps of this centroid
+        const uint64_t rest = (uint64_t)mask & ~((2ull << jc) - 1ull);
+        jn = rest ? (uint32_t)__builtin_ctzll(rest) : jc;
+        pn = rest ? nra[jn] : pc;
+        en = rest ? nre[jn] : ec;
+      }
+      const uint32_t sn = slot(jn);
+      const double nv = B.rv[sn + min(pn, tcap - 1)], nw = B.rw[sn + min(pn, tcap - 1)];
+      const double w = __builtin_fabs(cw);
+      W = dadd(W, w);
+      mean = dadd(mean, ddiv(dmul(dsub(cv, mean), w), W));
+      ms[q] = mean;
+      jc = jn;
+      pc = pn;
+      ec = en;
+      cv = nv;
+      cw = nw;
+    }
+  }
+  PROF_T(l2);
+  PROF_ADD(14, l1, l2);
+  // -- merge j's decisions around main i, with the mean merge j saw: main i before temp
+  // n[j][i] (mean < v), temp n[j][i] - 1 before main i (v <= mean).  Every chunk is checked;
+  // the first failure counts.
+  if (cen) {
+    const ldsf64* const ms = B.ms + off;
+    double gv1[2][kG], gv0[2][kG], gmb[2][kG];
+    uint32_t kload = 0;  // the lane's temps before chunk j (load side)
+#pragma unroll
+    for (uint32_t g = 0; g <= kBB / kG; g++) {
+      if (g < kBB / kG) {
+#pragma unroll
+        for (uint32_t u = 0; u < kG; u++) {
+          const uint32_t j = kG * g + u, a = by(ra, j), sl = slot(j);
+          gv1[g & 1][u] = B.rv[sl + min(a, tcap - 1)];
+          gv0[g & 1][u] = B.rv[sl + (a ? a - 1 : 0)];
+          gmb[g & 1][u] = ms[kload ? kload - 1 : 0];
+          kload += j < b ? by(re, j) - a : 0u;
+        }
+      }
+      if (g == 0) continue;
+      const uint32_t h = g - 1;
+#pragma unroll
+      for (uint32_t u = 0; u < kG; u++) {
+        const uint32_t j = kG * h + u, a = by(ra, j);
+        const double mb = (mask & ((1u << j) - 1u)) ? gmb[h & 1][u] : m0;
+        const double v1 = gv1[h & 1][u], v0 = gv0[h & 1][u];
+        const bool ok = ((a >= tcap) | (mb < v1)) & ((a == 0) | ((i > 0) & (v0 <= mb)));
+        jf = (j < b && !ok && jf == b) ? j : jf;
+      }
+    }
+  }
+  PROF_T(l3);
+  PROF_ADD(15, l2, l3);
+  PROF_ADD(22, 0, (long long)m);
+  if (jf < b) lds_min(&B.ctl[0], jf);
   fast_sync<NW>();
   PROF_T(b3);
   // ---- bound tests: main i starts (i >= 1) and its temps join, in every merge
@@ -1912,12 +2039,19 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
   PROF_T(b5);
   const uint32_t js = B.ctl[0];
   if (js > 0) {
-    // commit merges 0..js-1: means, weights, the main prefix
+    // commit merges 0..js-1: means (after the last chunk before js that gave temps), weights,
+    // the main prefix
     if (act) {
       const uint32_t c0 = B.ch[(js - 1) * kBN + i];
       if (cen) {
         const uint32_t c1 = B.ch[(js - 1) * kBN + i + 1];
-        L.mm[i] = js < kBB ? B.mh[js * kBN + i] : mean;  // (mean before chunk js)
+        uint32_t kc = 0;  // the lane's temps in chunks < js
+#pragma unroll
+        for (uint32_t g = 0; g < kBB / 4; g++) {
+          const uint32_t v = js > 4 * g ? min(js - 4 * g, 4u) : 0u, bm = v >= 4 ? 0xffffffffu : ((1u << (8 * v)) - 1u);
+          kc += bsum(re[g] & bm) - bsum(ra[g] & bm);
+        }
+        L.mm[i] = kc ? B.ms[off + kc - 1] : m0;
         L.mw[i] = dadd(L.mw[i], (double)(c1 - c0));
       }
       F.mp[i] = dadd(F.mp[i], (double)c0);  // (i = nm: the new total)
@@ -1939,8 +2073,9 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
   return js;
 }
 
-// replay of one key with NW waves (tcap <= 64, ingest only: no flush-mode adoption)
-template <int NW>
+// replay of one key with NW waves (tcap <= 64, ingest only: no flush-mode adoption); BATCH:
+// merge_batch where the key's state allows (the dynamic LDS then holds the batch tables)
+template <int NW, bool BATCH>
 __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& S) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr uint32_t NT = 64 * NW;
@@ -2084,9 +2219,9 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
         merge_sorted_any(tcap, tempW, tintd != 0.0);
       }
     };
-#ifdef VN_BATCH_OFF
-    singles(0, sp.npure);
-#else
+    if constexpr (!BATCH) {
+      singles(0, sp.npure);
+    } else {
     const BatchLds Bt = batch_layout(smem + batch_offset(capc, tcap), tcap);
     const uint64_t cb = (uint64_t)lo + sp.off0;
     const double* const gv = xcsv + cb;
@@ -2143,7 +2278,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       }
     }
     dma_wait();  // (nothing may still be landing in LDS when the block moves on)
-#endif
+    }
   }
   const uint32_t tail = sp.off0 + sp.npure * tcap;
   if (nex > tail) append(tail, nex);
@@ -2235,26 +2370,38 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
   if (k < x.nkeys) replay_key<TPL>(x, k);
 }
 
-// the longest keys of the order (its first *nmw entries), four waves each
-__global__ __launch_bounds__(kMWThreads) void k_histo_exact_mw(ExactCtx x, const uint32_t* __restrict__ nmw) {
+// the long keys of the order, four waves each: entries [nmw[1], nmw[0]) (k_histo_exact_mw) and,
+// batched with the larger LDS, the longest [0, nmw[1]) (k_histo_exact_mwb)
+template <bool BATCH>
+__device__ __forceinline__ void replay_long(const ExactCtx& x, const uint32_t* __restrict__ nmw) {
   __shared__ MwShared S;
-  const uint32_t n = *nmw;
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+  const uint32_t n = BATCH ? nmw[1] : nmw[0];
+  for (uint32_t i = (BATCH ? 0u : nmw[1]) + blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t k = x.order64 ? (uint32_t)x.order64[i] : x.order ? x.order[i] : i;
-    if (k < x.nkeys) replay_key_fast<kMW>(x, k, *(MwSharedL*)&S);
+    if (k < x.nkeys) replay_key_fast<kMW, BATCH>(x, k, *(MwSharedL*)&S);
     __syncthreads();  // the next key reuses the LDS
   }
 }
-// how many entries of the longest-first order replay at least min_len samples
+__global__ __launch_bounds__(kMWThreads) void k_histo_exact_mw(ExactCtx x, const uint32_t* __restrict__ nmw) {
+  replay_long<false>(x, nmw);
+}
+__global__ __launch_bounds__(kMWThreads) void k_histo_exact_mwb(ExactCtx x, const uint32_t* __restrict__ nmw) {
+  replay_long<true>(x, nmw);
+}
+// how many entries of the longest-first order replay at least min_len samples (out[0]), and at
+// least batch_len (out[1], <= out[0])
 __global__ void k_exact_count_long(uint32_t n, const uint64_t* __restrict__ order64, uint32_t min_len,
-                                   uint32_t cap, uint32_t* __restrict__ out) {
-  uint32_t lo = 0, hi = n;  // first entry shorter than min_len
-  while (lo < hi) {
-    const uint32_t md = (lo + hi) >> 1;
-    if (0xFFFFFu - (uint32_t)(order64[md] >> 32) >= min_len) lo = md + 1;
-    else hi = md;
+                                   uint32_t batch_len, uint32_t cap, uint32_t* __restrict__ out) {
+  for (int q = 0; q < 2; q++) {
+    const uint32_t len = q ? max(batch_len, min_len) : min_len;
+    uint32_t lo = 0, hi = n;  // first entry shorter than len
+    while (lo < hi) {
+      const uint32_t md = (lo + hi) >> 1;
+      if (0xFFFFFu - (uint32_t)(order64[md] >> 32) >= len) lo = md + 1;
+      else hi = md;
+    }
+    out[q] = min(lo, cap);
   }
-  *out = min(lo, cap);
 }
 
 // keys [0, *cnt) of x.keys, grid-stride: a bounded grid when only the device knows the count
@@ -2296,12 +2443,11 @@ void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* 
 
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap) { return exact_smem_bytes_hd(capc, tcap); }
 size_t exact_fast_smem_bytes(uint32_t capc, uint32_t tcap) {
-#ifdef VN_BATCH_OFF
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = std::max(capc + TP + 1, 320u);
   return fast_offset(capc, tcap) + fast_extra_bytes(capc, TP, JW);
-#else
+}
+static size_t exact_batch_smem_bytes(uint32_t capc, uint32_t tcap) {
   return batch_offset(capc, tcap) + batch_bytes(tcap);
-#endif
 }
 #ifdef VN_EXACT_PROF
 extern "C" int vn_prof_exact_read(unsigned long long* out16, int reset) {
@@ -2330,16 +2476,22 @@ bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipS
   x.mw_count = nullptr;
   if (!x.order64 || !x.norder || x.tcap > 64 || x.flush_mode) return false;
   if (exact_fast_smem_bytes(x.capc, x.tcap) > 160 * 1024) return false;
+  // (no batching where its tables do not fit: the long keys all take k_histo_exact_mw)
+  const bool batch = x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024;
   hipLaunchKernelGGL(k_exact_count_long, dim3(1), dim3(1), 0, st, x.norder, x.order64, min_len,
-                     std::min<uint32_t>(x.norder, kMaxLongKeys), count);
+                     batch ? kBatchMinLen : 0xFFFFFFFFu, std::min<uint32_t>(x.norder, kMaxLongKeys), count);
   x.mw_count = count;
   return true;
 }
 
-void histo_exact_replay_long(const ExactCtx& x, hipStream_t st) {
+void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest) {
   if (!x.mw_count) return;
-  hipLaunchKernelGGL(k_histo_exact_mw, dim3(std::min<uint32_t>(x.norder, kMaxLongKeys / 2)), dim3(kMWThreads),
-                     exact_fast_smem_bytes(x.capc, x.tcap), st, x, x.mw_count);
+  const uint32_t grid = std::min<uint32_t>(x.norder, kMaxLongKeys / 2);
+  if (x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024)
+    hipLaunchKernelGGL(k_histo_exact_mwb, dim3(grid), dim3(kMWThreads), exact_batch_smem_bytes(x.capc, x.tcap), st, x,
+                       x.mw_count);
+  hipLaunchKernelGGL(k_histo_exact_mw, dim3(grid), dim3(kMWThreads), exact_fast_smem_bytes(x.capc, x.tcap), st_rest, x,
+                     x.mw_count);
 }
 
 void histo_exact_replay(const ExactCtx& x, hipStream_t st) {

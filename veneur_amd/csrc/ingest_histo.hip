@@ -1318,13 +1318,13 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
     const bool side5 = longk && !e->timing && e->st5;
     hipEvent_t a = e->timing ? e->pool_rp.next() : nullptr, b = e->timing ? e->pool_rp.next() : nullptr;
     if (a && b) VN_HIP_CHECK(hipEventRecord(a, s));
-    if (side5) {
+    if (side5) {  // the batched longest keys on st5, the other long keys ahead of the rest on s
       VN_HIP_CHECK(hipEventRecord(e->ev_fork5, s));
       VN_HIP_CHECK(hipStreamWaitEvent(e->st5, e->ev_fork5, 0));
-      histo_exact_replay_long(xc, e->st5);
+      histo_exact_replay_long(xc, e->st5, s);
       VN_HIP_CHECK(hipEventRecord(e->ev_join5, e->st5));
     } else if (longk) {
-      histo_exact_replay_long(xc, s);
+      histo_exact_replay_long(xc, s, s);
     }
     histo_exact_replay(xc, s);
     if (side5) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join5, 0));
