@@ -517,6 +517,14 @@ def main():
             ach = by / (ms * 1e-3) / 1e9
             kern.append({"kernel": name, "ms_per_step": ms, "launches_per_step": nl,
                          "algorithmic_bytes_per_launch": by / nl, "achieved": ach, "frac": ach / HBM_PEAK_GBS})
+    # the counter aggregation (k_scalar_direct, one launch; 16 B per record of the window)
+    ms_c = mean("ms_ingest_counter")
+    if ms_c > 0:
+        by_c = 16.0 * stream.counts[0]
+        kern.append({"kernel": "k_scalar_direct", "ms_per_step": ms_c, "launches_per_step": 1.0,
+                     "algorithmic_bytes_per_launch": by_c, "achieved": by_c / (ms_c * 1e-3) / 1e9,
+                     "frac": by_c / (ms_c * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "note": "timed as the serialised counter phase; bound by memory-side atomic requests"})
     kern.sort(key=lambda k: -k["ms_per_step"])
     phase = {k: round(mean(k), 4) for k in
              ("ms_ingest_counter", "ms_ingest_gauge", "ms_ingest_histo", "ms_ingest_set", "ms_flush")}

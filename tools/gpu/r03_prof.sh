@@ -1,5 +1,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-VN_LIB=libveneur_amd_prof.so timeout -k 10 120 python -u tools/exact_profile.py 1000000 > gpurun_out/r03_exact_prof.log 2>&1
-VN_LIB=libveneur_amd_variant.so timeout -k 10 120 python -u tools/exact_profile.py 1000000 >> gpurun_out/r03_exact_prof.log 2>&1
-echo done
+export TMPDIR=/tmp
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/r03_v3_prof -o c4 --output-format csv -- python3 -u bench.py --steps 1 --warmup 1 --timing-steps 1 --no-cpu-baseline --pcie-steps 0 --text-lines 0 > gpurun_out/r03_v3_prof.json 2> gpurun_out/r03_v3_prof.log
+echo "rc=$?"

@@ -1,15 +1,15 @@
 #!/usr/bin/env python3
-"""Cross-check of bench.py's roofline line against the rocprofv3 kernel trace of the same run.
+"""Cross-check of bench.py's roofline table against the rocprofv3 kernel trace of the same run.
 
-bench.py times the scatter launches (k_radix_scatter) of its last --timing-steps steps with HIP
-events on the engine stream, every class serialised on that stream (the earlier, timed steps run
-the classes concurrently on four streams, so their launches share the GPU and last longer).
-This reads the trace of `rocprofv3 --kernel-trace ... -- python3 bench.py ... --timing-steps N`
-(gpu_check.sh's profile run: the timing steps are the run's last steps), takes the scatter
-launches of those last N steps that move >= 1M records (the longest-first key orderings of a few
-hundred thousand keys are not part of bench's count), and prints their mean duration beside
-bench's mean per launch.  With an output path it also writes the per-kernel statistics of those
-N steps (rocprofv3 --stats layout) -- the summary the bench figures are compared with.
+bench.py times its kernels over its last --timing-steps steps with HIP events on the engine
+stream, every class serialised on that stream (the earlier, timed steps run the classes
+concurrently on several streams, so their launches share the GPU and last longer).  This reads
+the trace of `rocprofv3 --kernel-trace ... -- python3 bench.py ... --timing-steps N` (the timing
+steps are the run's last steps: tools/gpu/r03_prof.sh), and for every row of the bench's
+roofline.kernels prints the trace's time of the same launches (the bench's launch count of that
+kernel, largest grids first) beside the bench's figure, and the roofline fraction at the trace's
+time.  With an output path it also writes the per-kernel statistics of those N steps (rocprofv3
+--stats layout) -- the summary the bench figures are compared with.
     python tools/roofline_check.py gpurun_out/TAG_prof gpurun_out/TAG_prof.log [N [stats.csv]]
 """
 import csv
@@ -30,28 +30,33 @@ def main(prof_dir, bench_json, nsteps=1, stats_out=None):
     lo = ends[-nsteps - 1] + 1
     durs = []
     per = defaultdict(list)
+    launches = defaultdict(list)  # base kernel name -> [(duration ns, grid)]
     for r in rows[lo:ends[-1] + 1]:
         name = r["Kernel_Name"]
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
         per[name].append(d)
-        if "k_radix_scatter" not in name:
-            continue
-        grid = int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
-        per_tile = int(r.get("Workgroup_Size_X") or 512)
-        if grid // per_tile * 4096 < (1 << 20):
-            continue
-        durs.append(d / 1e3)
+        base = name.replace("(anonymous namespace)", "").split("(")[0].split("<")[0].split("::")[-1].split()[-1]
+        key = "k_histo_exact" if base.startswith("k_histo_exact") else base
+        launches[key].append((d, int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)))
     with open(bench_json) as fh:  # the bench JSON line (alone, or the last one in a log)
         b = json.loads([ln for ln in fh if ln.startswith("{")][-1])["roofline"]
-    k = [x for x in b["kernels"] if x["kernel"] == "k_radix_scatter"][0]
-    bench_us = k["ms_per_step"] * 1e3 / k["launches_per_step"]
-    trace_us = sum(durs) / len(durs)
-    print("scatter launches in the last %d (timing) steps of the trace: %d (bench: %.0f per step)" %
-          (nsteps, len(durs), k["launches_per_step"]))
-    print("mean duration: trace %.1f us, bench HIP events %.1f us (ratio %.3f)" % (trace_us, bench_us,
-                                                                                  trace_us / bench_us))
-    print("achieved at the trace's mean: %.0f GB/s (bench: %.0f GB/s)" %
-          (k["algorithmic_bytes_per_launch"] / (trace_us * 1e-6) / 1e9, k["achieved"]))
+    # every kernel row of the bench table: the trace's launches of that kernel (template and
+    # variant suffixes included) in the same timing step(s) -- the bench's launch count of them, the
+    # largest grids first (bench times the window's big launches; small sorts of key orders and the
+    # split engine's own launches run beside them) -- against bench's HIP-event figure
+    for row in b["kernels"]:
+        kname = row["kernel"]
+        nb = max(1, int(round(row["launches_per_step"])) * nsteps)
+        ls = sorted(launches.get(kname, []), key=lambda x: -x[1])
+        pick = ls[:nb]
+        ms_trace = sum(d for d, _ in pick) / 1e6 / nsteps
+        rest = sum(d for d, _ in ls[nb:]) / 1e6 / nsteps
+        print("%-16s trace %.3f ms/step over its %d largest launches (+%.3f ms in %d others), bench %.3f ms/step: "
+              "ratio %.3f; frac at the trace's time %.4f (bench %.4f)" %
+              (kname, ms_trace, len(pick), rest, len(ls) - len(pick), row["ms_per_step"],
+               ms_trace / row["ms_per_step"] if row["ms_per_step"] else float("nan"),
+               row["algorithmic_bytes_per_launch"] * row["launches_per_step"] / (ms_trace * 1e-3) / 1e9 / 8000.0
+               if ms_trace else float("nan"), row["frac"]))
     if stats_out:
         tot = sum(sum(v) for v in per.values())
         with open(stats_out, "w", newline="") as fh:
