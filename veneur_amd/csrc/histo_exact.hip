@@ -1737,8 +1737,10 @@ __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" :
 // committed (0..b): L.mm/L.mw/F.mp/mainW then hold the digest after them.
 template <int NW>
 __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L, const FastLds F, const BatchLds B,
-                                                const uint32_t nm, double& mainW, const uint32_t c, uint32_t b,
+                                                const uint32_t nm_in, double& mainW, const uint32_t c_in, uint32_t b,
                                                 const uint32_t tcap) {
+  // (wave-uniform values in scalar registers: every chunk address below is then scalar math)
+  const uint32_t nm = __builtin_amdgcn_readfirstlane(nm_in), c = __builtin_amdgcn_readfirstlane(c_in);
   constexpr uint32_t NT = 64 * NW;
   constexpr double kHi = 1.0 + kBand, kLo = 1.0 - kBand;
   constexpr uint32_t kItems = (kBB * kBTmax + NT - 1) / NT;  // batch temps per thread
@@ -1777,7 +1779,7 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
   }
   fast_sync<NW>();
   PROF_T(b1);
-  b = B.ctl[2];
+  b = __builtin_amdgcn_readfirstlane(B.ctl[2]);
   if (b < 2) {
     fast_sync<NW>();
     return 0u;
@@ -1889,7 +1891,8 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
 #else
   // -- prefixes (exact integers, so q = P/T of every structure test), unrolled over the chunks:
   // the n bytes are in registers (compile-time chunk indices), so a group's loads all issue at
-  // once, a group ahead of its use
+  // once, a group ahead of its use.  (Bounds from the batch's ends alone were measured: a long
+  // key's centroids sit near their k-size limit, so they flagged 8 centroids per batch, not 1.)
   if (act) {
     const double mp0 = F.mp[i];
     double qbmin = 2.0, qbmax = -1.0, qemin = 2.0, C = 0.0, W = cen ? L.mw[i] : 0.0;
@@ -1927,9 +1930,9 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
         mask |= (in && e > a ? 1u : 0u) << j;
       }
     }
-    B.kb[i] = k_close(delta, qemin);
-    B.kb[kBN + i] = k_close(delta, qbmax);
-    B.kb[2 * kBN + i] = k_close(delta, qbmin);
+    B.kb[i] = k_close(delta, __builtin_fmin(qemin, 1.0));  // (q <= 1: the reciprocal's rounding)
+    B.kb[kBN + i] = k_close(delta, __builtin_fmin(qbmax, 1.0));
+    B.kb[2 * kBN + i] = k_close(delta, __builtin_fmin(qbmin, 1.0));
   }
 #endif
   PROF_T(l1);
@@ -2014,10 +2017,10 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
   }
   fast_sync<NW>();
   PROF_T(b4);
-  const uint32_t nflag = B.ctl[1];
+  const uint32_t nflag = __builtin_amdgcn_readfirstlane(B.ctl[1]);
   if (nflag) {
     // exact tests of the flagged centroids, merge by merge (before the first decision reject)
-    const uint32_t jp = B.ctl[0];
+    const uint32_t jp = __builtin_amdgcn_readfirstlane(B.ctl[0]);
     for (uint32_t f = t; f < nflag * jp; f += NT) {
       const uint32_t q = f / jp, j = f - q * jp, ic = B.flagged[q];
       const double rT = B.brT[j];
@@ -2037,7 +2040,7 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
     fast_sync<NW>();
   }
   PROF_T(b5);
-  const uint32_t js = B.ctl[0];
+  const uint32_t js = __builtin_amdgcn_readfirstlane(B.ctl[0]);
   if (js > 0) {
     // commit merges 0..js-1: means (after the last chunk before js that gave temps), weights,
     // the main prefix
@@ -2209,7 +2212,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
           L.sv[t] = cv;
           L.sw[t] = __builtin_fabs(cw);
           F.sp[t] = t ? cp : 0.0;
-          stat(cv, __builtin_fabs(cw), cw > 0.0);
+          if (!BATCH) stat(cv, __builtin_fabs(cw), cw > 0.0);  // (batched: the prologue's)
         }
         if (t == tcap) F.sp[tcap] = tempW;
         hold2(tempW, tintd);
@@ -2227,6 +2230,23 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     const double* const gv = xcsv + cb;
     const double* const gw = xcsw + cb;
     const double* const gt = xctw + cb;
+    // the pure chunks' Local* statistics first, every thread streaming its share (off the merge
+    // chain: the replay below adds none); the loads of four records in flight per thread
+    {
+      const uint64_t ne = (uint64_t)sp.npure * tcap;
+      uint64_t e = t;
+      for (; e + 3 * NT < ne; e += 4 * NT) {
+        double v[4], w[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          v[u] = gv[e + u * NT];
+          w[u] = gw[e + u * NT];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) stat(v[u], __builtin_fabs(w[u]), w[u] > 0.0);
+      }
+      for (; e < ne; e += NT) stat(gv[e], __builtin_fabs(gw[e]), gw[e] > 0.0);
+    }
     uint32_t ring_lo = 0, ring_hi = 0;  // chunks [ring_lo, ring_hi) are in the ring (or on their way)
     uint32_t c = 0;
     while (c < sp.npure) {
@@ -2259,12 +2279,6 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       ring_lo = max(c, ring_hi > kRing ? ring_hi - kRing : 0u);
       const uint32_t js = merge_batch<NW>(x.delta, L, F, Bt, nm, mainW, c, b, tcap);
       PROF_T(s0);
-      for (uint32_t e = t; e < js * tcap; e += NT) {  // the committed chunks' Local* statistics
-        const uint32_t j = e / tcap, p = e - j * tcap;
-        const uint32_t sl = ((c + j) % kRing) * tcap + p;
-        const double w = Bt.rw[sl];
-        stat(Bt.rv[sl], __builtin_fabs(w), w > 0.0);
-      }
       PROF_T(s1);
       PROF_ADD(27, s0, s1);
       c += js;
