@@ -174,7 +174,19 @@ def c5_leg(args, rank):
             f = window()
         A.lib.vn_device_synchronize(0)
         ms = (time.perf_counter() - tw) * 1e3 / args.c5_windows
-        hq = np.ctypeslib.as_array(f.histo_quantiles, shape=(f.n_histo * len(PCT),)).reshape(-1, len(PCT)).copy()
+        # one more window, synchronised between its phases (the split only; not the headline)
+        phases = {}
+        tp = time.perf_counter()
+        for cls, name in ((2, "import_histos"), (3, "import_sets")):
+            sl, of, by, n = dev[cls]
+            g.import_device(cls, sl.ptr.value, of.ptr.value, by.ptr.value, n)
+            A.lib.vn_device_synchronize(0)
+            phases[name] = (time.perf_counter() - tp) * 1e3
+            tp = time.perf_counter()
+        f = g.flush_raw()
+        A.lib.vn_device_synchronize(0)
+        phases["flush"] = (time.perf_counter() - tp) * 1e3
+        hq =np.ctypeslib.as_array(f.histo_quantiles, shape=(f.n_histo * len(PCT),)).reshape(-1, len(PCT)).copy()
         hst = np.ctypeslib.as_array(f.histo_stats, shape=(f.n_histo * 8,)).reshape(-1, 8).copy()
         hsl = np.ctypeslib.as_array(f.histo_slot, shape=(f.n_histo,)).copy()
         ses = np.ctypeslib.as_array(f.set_estimate, shape=(f.n_set,)).copy()
@@ -218,6 +230,7 @@ def c5_leg(args, rank):
                       % (hosts, H, S, n_samples),
             "imports_per_s": n_imp / (ms * 1e-3), "payload_GBs": payload_bytes / (ms * 1e-3) / 1e9,
             "ms_per_window": ms, "windows": args.c5_windows, "payloads_per_window": n_imp,
+            "phases_ms_synchronised": {k: round(v, 2) for k, v in phases.items()},
             "payload_bytes_per_window": payload_bytes,
             "roofline": {"bound": "hbm", "achieved_GBs": payload_bytes / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                          "frac": payload_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,

@@ -228,6 +228,53 @@ def test_import_sets_many_hosts_sparse_trigger_path():
     assert f.set_estimate.tolist() == [w.set_estimate(s) for s in touched]
 
 
+def overflow_payload(rng, n, n_over):
+    """A sparse sketch holding n random members plus n_over members whose rho is 50 (hash bits
+    below the register index all zero): overflow codes for any base below 35."""
+    sk = oracle.Sketch(14)
+    for h in random_hashes(rng, n):
+        sk.insert_hash(int(h))
+    for i in rng.integers(0, 1 << 14, n_over):
+        sk.insert_hash((int(i) << 50) | 1)
+    return sk.marshal()
+
+
+def test_import_sets_dense_keys_many_sparse_payloads_bit_exact():
+    """Dense keys (fresh, nearly full, rebased b > 0) receiving hundreds of sparse payloads of
+    Lomax sizes in one call -- the run of plain register maxes, its long payloads block-wide --
+    mixed with payloads carrying overflow codes, dense payloads and skipped precisions, so the
+    runs are cut where a rebase may happen; registers, b, nz and estimates bit-exact."""
+    rng = np.random.default_rng(24)
+    nk = 6
+    w = oracle.Worker(1, 1, 1, nk)
+    loc_slots, loc_h = [], []
+    for s, n in ((0, 20000), (1, 60000), (2, 400_000), (3, 150_000), (5, 9000)):
+        loc_slots.append(np.full(n, s, np.uint32))
+        loc_h.append(random_hashes(rng, n))
+    ls, lh = np.concatenate(loc_slots), np.concatenate(loc_h)
+    w.set_hashed(ls, lh)
+    sizes = np.minimum((rng.pareto(1.2, 400) * 50).astype(int) + 1, 6000)
+    pool = [sketch_payload(rng, int(n)) for n in sizes[:360]]
+    pool += [overflow_payload(rng, int(n), int(k)) for n, k in zip(sizes[360:], rng.integers(1, 4, 40))]
+    pool += [sketch_payload(rng, 12000), sketch_payload(rng, 100, p=16)]
+    with make_engine((1, 1, 1, nk), max_records=1 << 20) as e:
+        e.ingest(set_hashes=(ls, lh))
+        for call in range(3):
+            slots = rng.integers(0, nk, 700).astype(np.uint32)
+            idx = rng.integers(0, len(pool), len(slots))
+            idx[rng.random(len(slots)) < 0.01] = len(pool) - 2  # a few dense payloads
+            pl = [pool[i] for i in idx]
+            e.import_sets(slots, pl)
+            for s, p in zip(slots, pl):
+                w.import_set(int(s), p)
+            for s in range(nk):
+                if w.touched(3, s):
+                    _set_state_equal(e, w, s)
+        assert w.set_sketch(3).b > 0 and w.set_sketch(4).b == 0  # a rebase inside the imports
+        f = e.flush()
+    assert f.set_estimate.tolist() == [w.set_estimate(s) for s in range(nk) if w.touched(3, s)]
+
+
 def test_import_sets_malformed_fails_loudly():
     rng = np.random.default_rng(23)
     good = sketch_payload(rng, 50)

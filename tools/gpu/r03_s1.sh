@@ -1,8 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_parity_gpu.py tests/test_split_gpu.py tests/test_configs_gpu.py tests/test_import_gpu.py > gpurun_out/r03_t1.log 2>&1 ; echo "tests rc=$?" >> gpurun_out/r03_t1.log
-timeout -k 10 200 python -u tools/hot_replay_bench.py --n 1000000 --keys 1 > gpurun_out/r03_hb1.log 2>&1 && \
-timeout -k 10 200 python -u tools/hot_replay_bench.py --n 200000 --keys 64 --reps 2 >> gpurun_out/r03_hb1.log 2>&1 && \
-timeout -k 10 200 python -u tools/hot_replay_bench.py --n 1000000 --keys 1 --fast >> gpurun_out/r03_hb1.log 2>&1
-echo done
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_import_gpu.py > gpurun_out/r03_s1_tests.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --keys 10000 --samples 10000000 --steps 1 --warmup 0 --timing-steps 0 --pcie-steps 0 --text-lines 0 > gpurun_out/r03_s1_bench.json 2> gpurun_out/r03_s1_bench.log
+echo "rc=$?"

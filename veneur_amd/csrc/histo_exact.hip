@@ -1740,7 +1740,11 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
                                                 const uint32_t nm_in, double& mainW, const uint32_t c_in, uint32_t b,
                                                 const uint32_t tcap) {
   // (wave-uniform values in scalar registers: every chunk address below is then scalar math)
+#ifdef VN_NO_RFL
+  const uint32_t nm = nm_in, c = c_in;
+#else
   const uint32_t nm = __builtin_amdgcn_readfirstlane(nm_in), c = __builtin_amdgcn_readfirstlane(c_in);
+#endif
   constexpr uint32_t NT = 64 * NW;
   constexpr double kHi = 1.0 + kBand, kLo = 1.0 - kBand;
   constexpr uint32_t kItems = (kBB * kBTmax + NT - 1) / NT;  // batch temps per thread
@@ -2232,6 +2236,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     const double* const gt = xctw + cb;
     // the pure chunks' Local* statistics first, every thread streaming its share (off the merge
     // chain: the replay below adds none); the loads of four records in flight per thread
+#ifndef VN_NO_PROLOGUE
     {
       const uint64_t ne = (uint64_t)sp.npure * tcap;
       uint64_t e = t;
@@ -2247,6 +2252,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       }
       for (; e < ne; e += NT) stat(gv[e], __builtin_fabs(gw[e]), gw[e] > 0.0);
     }
+#endif
     uint32_t ring_lo = 0, ring_hi = 0;  // chunks [ring_lo, ring_hi) are in the ring (or on their way)
     uint32_t c = 0;
     while (c < sp.npure) {

@@ -33,7 +33,8 @@ struct HllPart {
   uint32_t ntmp;      // tmpSet codes (big-endian u32) at tmp_off
   uint32_t list_len;  // varint list bytes at list_off
   uint32_t regs_len;  // dense: tailcut bytes at regs_off (<= 8192; missing bytes are zero registers)
-  uint32_t pad;
+  uint32_t rr;        // sparse: min rho | max rho << 8 over its codes (0xff: no codes)
+  uint32_t ncodes;    // sparse: tmpSet + list codes
   uint64_t tmp_off, list_off, regs_off;
 };
 static_assert(sizeof(HllPart) <= 64, "ImportScratch.parts holds 64 bytes per payload");
@@ -42,6 +43,7 @@ constexpr uint32_t kMaxImportTmp = 256;   // tmpSet codes per payload (Go keeps 
 constexpr uint32_t kPer = (kArenaWords + kBlock - 1) / kBlock;  // 65 codes per thread
 constexpr uint32_t kCWords = kArenaWords + 512;                 // payload codes + the key's tmpSet
 constexpr uint32_t kCPer = (kCWords + kBlock - 1) / kBlock;     // 67
+constexpr uint32_t kLaneBytes = 2048;  // a dense key's plain run: longer sparse payloads go block-wide
 
 __device__ __forceinline__ uint32_t be32(const uint8_t* d) {
   return ((uint32_t)d[0] << 24) | ((uint32_t)d[1] << 16) | ((uint32_t)d[2] << 8) | d[3];
@@ -70,7 +72,13 @@ __global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const 
           if (!bad) {
             // the list must decode completely into strictly increasing codes
             const uint8_t* lb = d + last + 12;
-            uint32_t prev = 0, x = 0, sh = 0, k = 0;
+            uint32_t prev = 0, x = 0, sh = 0, k = 0, rmin = 0xffu, rmax = 0u;
+            for (uint32_t j = 0; j < (uint32_t)tssz; j++) {
+              uint32_t ri, r;
+              decode_hash(be32(d + 8 + 4 * j), &ri, &r);
+              rmin = min(rmin, r);
+              rmax = max(rmax, r);
+            }
             for (uint64_t j = 0; j < sz && !bad; j++) {
               const uint32_t b = lb[j];
               if (sh < 32) x |= (b & 0x7fu) << sh;
@@ -78,6 +86,10 @@ __global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const 
               if (!(b & 0x80u)) {
                 const uint32_t c = prev + x;
                 if (k > 0 && c <= prev) bad = true;
+                uint32_t ri, r;
+                decode_hash(c, &ri, &r);
+                rmin = min(rmin, r);
+                rmax = max(rmax, r);
                 prev = c;
                 k++;
                 x = 0;
@@ -90,6 +102,8 @@ __global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const 
             p.tmp_off = o + 8;
             p.list_off = o + last + 12;
             p.list_len = (uint32_t)sz;
+            p.rr = rmin | (rmax << 8);
+            p.ncodes = (uint32_t)tssz + k;
           }
         }
       }
@@ -114,6 +128,29 @@ __global__ void k_hll_keys(uint64_t n, const uint32_t* __restrict__ slot, uint64
   keys[i] = ((uint64_t)s << 32) | (uint64_t)i;
   bt[s] = 1;
   stouch[s] = 1;  // Upsert happens before Combine (worker.go:241), even if the merge fails
+}
+
+// f(byte) over global bytes [p, p + len) in order, read as aligned 16-byte blocks with the next
+// block's load in flight while this one is consumed (one lane walking its own payload).  The
+// blocks never leave the 16-byte-aligned span holding the bytes (so no page the bytes do not touch).
+template <class F>
+__device__ __forceinline__ void for_bytes(const uint8_t* p, uint32_t len, F&& f) {
+  if (!len) return;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(p), a0 = s & ~(uintptr_t)15;
+  const uint32_t lo = (uint32_t)(s - a0), end = lo + len, nblk = (end + 15u) >> 4;
+  const uint4* b = reinterpret_cast<const uint4*>(a0);
+  uint4 cur = b[0];
+  for (uint32_t k = 0; k < nblk; k++) {
+    const uint4 nxt = b[min(k + 1u, nblk - 1u)];
+    const uint32_t base = k << 4;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t w = j < 4 ? cur.x : j < 8 ? cur.y : j < 12 ? cur.z : cur.w;
+      const uint32_t pos = base + (uint32_t)j;
+      if (pos >= lo && pos < end) f((w >> ((j & 3) * 8)) & 0xffu);
+    }
+    cur = nxt;
+  }
 }
 
 // ---- block-wide helpers (256 threads)
@@ -342,7 +379,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   __shared__ uint32_t s_tmp[256];      // the key's tmpSet, sorted (kHllNoCode padding)
   __shared__ uint32_t s_ptmp[256];     // the payload's tmpSet, sorted
   __shared__ uint32_t s_red[4];
-  __shared__ uint32_t s_b, s_nz, s_filled, s_tfull, s_pstar, s_newfill, s_min;
+  __shared__ uint32_t s_b, s_nz, s_filled, s_tfull, s_pstar, s_newfill, s_min, s_nh;
   const uint32_t k = blockIdx.x, t = threadIdx.x;
   const uint32_t slot = x.tl[k];
   const uint32_t p0 = x.start[slot], p1 = x.end[slot];
@@ -367,6 +404,79 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const DenseLds S{U, &s_b, &s_nz, &s_filled, &s_tfull, &s_pstar, &s_newfill, &s_min, s_red};
 
   for (uint32_t q = p0; q < p1; q++) {
+    if (dense) {
+      // A dense key and a run of sparse payloads none of whose inserts can rebase: a rebase
+      // needs an overflow code (uint8(rho - b) >= capacity, hyperloglog.go:169-176) while no
+      // register is zero, so a payload whose codes all have b <= rho < b + 16, or one that
+      // starts while more zero registers remain than codes arrive before its end, only does
+      // plain register maxes -- commutative, so the run's payloads apply at once, one per
+      // lane (the long ones block-wide), and nz is recounted after.
+      const uint32_t b = s_b, nz = s_nz;
+      HllPart R{};
+      R.kind = 1;
+      if (q + t < p1) R = x.parts[(uint32_t)x.keys[q + t]];
+      const uint32_t rmin = R.rr & 0xffu, rmax = R.rr >> 8;
+      const bool cand = R.kind == 0 && (rmin < b || rmax >= b + kHllCapacity);
+      uint32_t tot;
+      const uint32_t before = block_scan_u32<false>(R.kind == 0 ? R.ncodes : 0u, s_red, tot);
+      const bool safe = R.kind == 2 || (R.kind == 0 && (!cand || before + R.ncodes < nz));
+      if (t == 0) {
+        s_min = kBlock;
+        s_nh = 0;
+      }
+      __syncthreads();
+      if (!safe) atomicMin(&s_min, t);
+      __syncthreads();
+      const uint32_t nrun = s_min;
+      if (nrun) {
+        auto ins = [&](uint32_t code) {
+          uint32_t ri, r;
+          decode_hash(code, &ri, &r);
+          if (r > b) atomicMax(&U[ri], min(r - b, kHllCapacity - 1));
+        };
+        if (t < nrun && R.kind == 0) {
+          if (4u * R.ntmp + R.list_len > kLaneBytes) {
+            s_ptmp[atomicAdd(&s_nh, 1u)] = t;
+          } else {
+            uint32_t c = 0, nb = 0;
+            for_bytes(x.bytes + R.tmp_off, 4u * R.ntmp, [&](uint32_t by) {
+              c = (c << 8) | by;
+              if (++nb == 4) {
+                ins(c);
+                nb = 0;
+              }
+            });
+            uint32_t prev = 0, v = 0, sh = 0;
+            for_bytes(x.bytes + R.list_off, R.list_len, [&](uint32_t by) {
+              if (sh < 32) v |= (by & 0x7fu) << sh;
+              sh += 7;
+              if (!(by & 0x80u)) {
+                prev += v;
+                ins(prev);
+                v = 0;
+                sh = 0;
+              }
+            });
+          }
+        }
+        __syncthreads();
+        const uint32_t nh = s_nh;
+        for (uint32_t h = 0; h < nh; h++) {  // the long payloads, block-wide
+          const HllPart H = x.parts[(uint32_t)x.keys[q + s_ptmp[h]]];
+          if (t < H.ntmp) ins(be32(x.bytes + H.tmp_off + 4ull * t));
+          const uint32_t nl = decode_list(x.bytes + H.list_off, H.list_len, Cb, s_red);
+          for (uint32_t i = t; i < nl; i += kBlock) ins(Cb[i]);
+          __syncthreads();
+        }
+        uint32_t z = 0;
+        for (uint32_t i = t; i < kHllM; i += kBlock) z += U[i] == 0;
+        z = block_allreduce_u32_sum(z, s_red);
+        if (t == 0) s_nz = z;
+        __syncthreads();
+        q += nrun - 1;
+        continue;
+      }
+    }
     const HllPart P = x.parts[(uint32_t)x.keys[q]];
     if (P.kind == 2) continue;
     if (P.kind == 0) {
