@@ -1,7 +1,5 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-VN_LIB=libveneur_amd_prof.so timeout -k 10 120 python -u tools/exact_profile.py 1000000 > gpurun_out/r03_exact_prof.log 2>&1
-VN_LIB=libveneur_amd_variant.so timeout -k 10 120 python -u tools/exact_profile.py 1000000 >> gpurun_out/r03_exact_prof.log 2>&1
-timeout -k 10 200 python -u tools/hot_replay_bench.py --n 1000000 --keys 1 >> gpurun_out/r03_exact_prof.log 2>&1
-timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_configs_gpu.py -k c5 > gpurun_out/r03_c5_tests.log 2>&1
-echo done
+export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/r03_s2 -o c5 --output-format csv -- python3 -u bench.py --keys 10000 --samples 10000000 --steps 1 --warmup 0 --timing-steps 0 --pcie-steps 0 --text-lines 0 > gpurun_out/r03_s2.json 2> gpurun_out/r03_s2.log
+echo "rc=$?"

@@ -1,8 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-VN_LIB=libveneur_amd_prof.so timeout -k 10 120 python -u tools/exact_profile.py 1000000 > gpurun_out/r03_exact_prof.log 2>&1
-timeout -k 10 200 python -u tools/hot_replay_bench.py --n 1000000 --keys 1 >> gpurun_out/r03_exact_prof.log 2>&1
-timeout -k 10 200 python -u tools/hot_replay_bench.py --n 200000 --keys 64 --reps 2 >> gpurun_out/r03_exact_prof.log 2>&1
-timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_parity_gpu.py -k histo > gpurun_out/r03_t3.log 2>&1; echo "rc=$?" >> gpurun_out/r03_t3.log
-VN_LIB=libveneur_amd_variant.so timeout -k 10 600 python -u -m pytest -x -q --timeout 240 --timeout-method thread tests/test_parity_gpu.py -k "c4_hot_key_sizes_exact or exact_replay" > gpurun_out/r03_t3_fallback.log 2>&1; echo "rc=$?" >> gpurun_out/r03_t3_fallback.log
-echo done
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_import_gpu.py tests/test_edges_gpu.py tests/test_http_import.py > gpurun_out/r03_s3_tests.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --keys 10000 --samples 10000000 --steps 1 --warmup 0 --timing-steps 0 --pcie-steps 0 --text-lines 0 > gpurun_out/r03_s3_bench.json 2> gpurun_out/r03_s3_bench.log &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r03_s3 -o c5 --output-format csv -- python3 -u bench.py --keys 10000 --samples 10000000 --steps 1 --warmup 0 --timing-steps 0 --pcie-steps 0 --text-lines 0 > gpurun_out/r03_s3_prof.json 2> gpurun_out/r03_s3_prof.log
+echo "rc=$?"

@@ -19,17 +19,58 @@ namespace vn {
 
 namespace {
 
-// encoding/gob reader over one payload (the subset MergingDigest.GobEncode writes)
+// encoding/gob reader over one payload (the subset MergingDigest.GobEncode writes).  One lane
+// walks its own payload: bytes come from 16-byte-aligned blocks held in registers, the next
+// block's load in flight while this one is parsed (a byte-at-a-time global load per step would
+// leave every lane waiting on memory latency once per byte).  The blocks never leave the
+// 16-byte-aligned span holding the payload.
 struct GobIn {
-  const uint8_t* d;
+  const uint4* blk;  // the aligned blocks covering the payload
+  uint32_t lo;       // payload start within blk[0]
   uint32_t n, i;
   bool err;
-  __device__ uint64_t u() {  // gob unsigned integer
+  uint32_t nb, cb;   // blocks, block held in c0:c1
+  uint64_t c0, c1, n0, n1;  // the current block and the next one (low, high 8 bytes)
+  __device__ __forceinline__ void load(uint32_t k, uint64_t& a, uint64_t& b) const {
+    const uint4 v = blk[k];
+    a = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    b = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  }
+  __device__ GobIn(const uint8_t* d, uint32_t len) : n(len), i(0), err(false) {
+    const uintptr_t s = reinterpret_cast<uintptr_t>(d), a0 = s & ~(uintptr_t)15;
+    blk = reinterpret_cast<const uint4*>(a0);
+    lo = (uint32_t)(s - a0);
+    nb = (lo + len + 15u) >> 4;
+    cb = 0;
+    c0 = c1 = n0 = n1 = 0;
+    if (nb) {
+      load(0, c0, c1);
+      load(min(1u, nb - 1u), n0, n1);
+    }
+  }
+  __device__ __forceinline__ uint32_t at(uint32_t pos) {  // byte pos (< n)
+    const uint32_t a = lo + pos, k = a >> 4;
+    if (k != cb) {
+      if (k == cb + 1) {
+        c0 = n0;
+        c1 = n1;
+      } else {
+        load(k, c0, c1);
+      }
+      load(min(k + 1u, nb - 1u), n0, n1);
+      cb = k;
+    }
+    // mask blend, not a select: a select of two fields can become a load through a selected
+    // pointer, which keeps the reader in scratch memory
+    const uint64_t m = 0ull - (uint64_t)((a >> 3) & 1u), h = (c0 & ~m) | (c1 & m);
+    return (uint32_t)(h >> ((a & 7u) * 8u)) & 0xffu;
+  }
+  __device__ __forceinline__ uint64_t u() {  // gob unsigned integer
     if (i >= n) {
       err = true;
       return 0;
     }
-    const uint32_t b = d[i++];
+    const uint32_t b = at(i++);
     if (b < 0x80u) return b;
     const uint32_t cnt = 256u - b;  // byte count, sent negated
     if (cnt > 8u || cnt > n - i) {
@@ -37,14 +78,14 @@ struct GobIn {
       return 0;
     }
     uint64_t v = 0;
-    for (uint32_t k = 0; k < cnt; k++) v = (v << 8) | d[i++];
+    for (uint32_t k = 0; k < cnt; k++) v = (v << 8) | at(i++);
     return v;
   }
-  __device__ int64_t s() {  // gob signed integer: sign in bit 0
+  __device__ __forceinline__ int64_t s() {  // gob signed integer: sign in bit 0
     const uint64_t x = u();
     return (x & 1) ? ~(int64_t)(x >> 1) : (int64_t)(x >> 1);
   }
-  __device__ double f() {  // gob float64: IEEE bits byte-reversed, sent as an unsigned integer
+  __device__ __forceinline__ double f() {  // gob float64: IEEE bits byte-reversed, sent as an unsigned integer
     uint64_t x = u(), v = 0;
     for (int k = 0; k < 8; k++) {
       v = (v << 8) | (x & 0xffu);
@@ -52,7 +93,7 @@ struct GobIn {
     }
     return bitsd(v);
   }
-  __device__ void skip_string() {
+  __device__ __forceinline__ void skip_string() {
     const uint64_t l = u();
     if (l > n - i) {
       err = true;
@@ -60,20 +101,21 @@ struct GobIn {
     }
     i += (uint32_t)l;
   }
-  __device__ int field_name() {  // 1 = "Mean", 2 = "Weight", 0 = any other name
+  __device__ __forceinline__ int field_name() {  // 1 = "Mean", 2 = "Weight", 0 = any other name
     const uint64_t l = u();
     if (l > n - i) {
       err = true;
       return 0;
     }
-    const uint8_t* p = d + i;
     int r = 0;
-    if (l == 4 && p[0] == 'M' && p[1] == 'e' && p[2] == 'a' && p[3] == 'n') r = 1;
-    if (l == 6 && p[0] == 'W' && p[1] == 'e' && p[2] == 'i' && p[3] == 'g' && p[4] == 'h' && p[5] == 't') r = 2;
+    if (l == 4 && at(i) == 'M' && at(i + 1) == 'e' && at(i + 2) == 'a' && at(i + 3) == 'n') r = 1;
+    if (l == 6 && at(i) == 'W' && at(i + 1) == 'e' && at(i + 2) == 'i' && at(i + 3) == 'g' && at(i + 4) == 'h' &&
+        at(i + 5) == 't')
+      r = 2;
     i += (uint32_t)l;
     return r;
   }
-  __device__ int64_t common_type() {  // CommonType {Name string; Id typeId} -> Id
+  __device__ __forceinline__ int64_t common_type() {  // CommonType {Name string; Id typeId} -> Id
     int64_t id = 0, f = -1;
     for (;;) {
       const uint64_t dl = u();
@@ -102,7 +144,7 @@ struct GobTypes {
 };
 
 // one wireType message (encoding/gob type.go: ArrayT 0, SliceT 1, StructT 2)
-__device__ void gob_wiretype(GobIn& r, GobTypes& T) {
+__device__ __forceinline__ void gob_wiretype(GobIn& r, GobTypes& T) {
   int64_t f = -1;
   for (;;) {
     const uint64_t dl = r.u();
@@ -174,7 +216,7 @@ __device__ void gob_wiretype(GobIn& r, GobTypes& T) {
 
 // skip one field value of type id tid: builtin scalars, strings, or a slice of scalars
 // (Centroid.Samples []float64, only sent by debug digests)
-__device__ void gob_skip(GobIn& r, const GobTypes& T, int64_t tid) {
+__device__ __forceinline__ void gob_skip(GobIn& r, const GobTypes& T, int64_t tid) {
   if (tid >= 1 && tid <= 4) {  // bool, int, uint, float
     (void)r.u();
     return;
@@ -195,8 +237,9 @@ __device__ void gob_skip(GobIn& r, const GobTypes& T, int64_t tid) {
 // One GobEncode()d MergingDigest ([]Centroid, then compression, min, max as float64):
 // the number of centroids, written to mean/w when EMIT; -1 if the stream is malformed.
 template <bool EMIT>
-__device__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double* w) {
-  GobIn r{d, n, 0, false};
+__device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double* w, uint32_t* oslot = nullptr,
+                              uint32_t slot = 0) {
+  GobIn r(d, n);
   GobTypes T;
   bool have = false;
   int floats = 0;
@@ -215,6 +258,9 @@ __device__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double
         for (int k = 0; k < T.ns; k++)
           if (T.sid[k] == id) si = k;
         if (si < 0 || T.selem[si] != T.st) return -1;
+        uint32_t fk = 0;  // per field: 1 Mean, 2 Weight (float64), 0 skipped -- 2 bits each
+        for (int k = 0; k < T.nf; k++)
+          fk |= (uint32_t)(T.fid[k] == 4 ? (T.fname[k] == 1 ? 1 : T.fname[k] == 2 ? 2 : 0) : 0) << (2 * k);
         const uint64_t c = r.u();
         for (uint64_t j = 0; j < c && !r.err; j++) {
           double m = 0.0, wt = 0.0;  // gob omits zero fields
@@ -227,13 +273,15 @@ __device__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double
               r.err = true;
               break;
             }
-            if (T.fname[f] == 1 && T.fid[f] == 4) m = r.f();
-            else if (T.fname[f] == 2 && T.fid[f] == 4) wt = r.f();
+            const uint32_t kind = (fk >> (2 * f)) & 3u;
+            if (kind == 1) m = r.f();
+            else if (kind == 2) wt = r.f();
             else gob_skip(r, T, T.fid[f]);
           }
           if (EMIT) {
             mean[cnt] = m;
             w[cnt] = wt;
+            oslot[cnt] = slot;
           } else if (d_isnan(m) || d_isinf(m) || wt <= 0.0) {
             return -1;  // Merge's Add would panic (merging_digest.go:98-100)
           }
@@ -276,17 +324,10 @@ __global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const u
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t o = base + coff[i];
-  const int64_t c = gob_digest<true>(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), omean + o, ow + o);
-  if (c < 0) {
-    atomicOr(err, kErrDecode);
-    return;
-  }
-  const uint32_t s = slot[i];
-  for (int64_t j = 0; j < c; j++) {
-    oslot[o + j] = s;
-    const double m = omean[o + j], wt = ow[o + j];
-    if (d_isnan(m) || d_isinf(m) || wt <= 0.0) atomicOr(err, kErrDecode);  // Add panics (merging_digest.go:98-100)
-  }
+  // k_gob_count validated the payload (every centroid a valid Add), so this pass only writes
+  const int64_t c = gob_digest<true>(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), omean + o, ow + o,
+                                     oslot + o, slot[i]);
+  if (c < 0) atomicOr(err, kErrDecode);
 }
 
 // payload index of every slice boundary: bnd[j] = the last payload i with coff[i] <= j * step
