@@ -55,6 +55,54 @@ def hot_keys(counts, scale, classes, thr_cs, thr_set, max_split, split_histos=Fa
     return out
 
 
+def split_thresholds(args, thr):
+    """{class: min window count} of the classes that split (timers only in the fast mode)."""
+    t = {0: thr, 3: min(thr, args.set_hot)}
+    if args.exact_threshold > 0:
+        t[2] = thr
+    return t
+
+
+def split_from_engine(e, key_of_slot, thresholds, ctrl, max_split, keep=None):
+    """vn_hot_keys of the flushed window on every rank, mapped to key ids and summed over the
+    ranks (a split key's records are dealt over all of them); per class the hottest max_split
+    above the threshold (sorted ids).  keep: the split list in use -- its keys stay while above
+    half the threshold (hysteresis: a strided count near the threshold must not flip the list)."""
+    local = {}
+    for c, t in thresholds.items():
+        slots, counts = e.hot_keys(c, int(t / (2 * ctrl.world)) + 1, 16 * max_split)
+        local[c] = list(zip(key_of_slot[c][slots].tolist(), counts.tolist()))
+    split = {0: np.zeros(0, np.uint32), 2: np.zeros(0, np.uint32), 3: np.zeros(0, np.uint32)}
+    tot = {c: {} for c in thresholds}
+    for part in ctrl.gather_object(local):
+        for c, items in part.items():
+            for k, n in items:
+                tot[c][k] = tot[c].get(k, 0) + n
+    for c, d in tot.items():
+        t = thresholds[c]
+        kept = set() if keep is None else set(np.asarray(keep.get(c, [])).tolist())
+        hot = [(k, n) for k, n in d.items() if n > t or (k in kept and n > t / 2)]
+        top = sorted(hot, key=lambda kv: (-kv[1], kv[0]))[:max_split]
+        split[c] = np.sort(np.array([k for k, _ in top], np.uint32))
+    return split
+
+
+def detect_split(args, V, ctrl, world, rank, local_rank, thr):
+    """The split list from the engines' hot-key detector over one unsplit window of the stream
+    on every rank (detection stride args.hot_stride)."""
+    s0 = V.DeviceStream(args.seed, args.keys, args.samples, rank, world, device=local_rank, split=None)
+    with V.Engine(tuple(max(1, x) for x in s0.n_slots), compression=100.0, percentiles=PCT,
+                  max_batch_records=max(s0.counts) + 1, max_batch_member_bytes=s0.counts[3] * 11 + 64,
+                  device=local_rank, exact_threshold=args.exact_threshold) as e0:
+        e0.hot_detect(args.hot_stride)
+        e0.ingest_device(s0.batch)
+        e0.flush_raw()
+        split = split_from_engine(e0, s0.key_of_slot, split_thresholds(args, thr), ctrl, args.max_split)
+    s0.free()
+    return split, {"source": "engine hot-key detector (vn_hot_keys) over one unsplit window",
+                   "stride": args.hot_stride}
+
+
 def key_classes(seed, n_keys, mix=(0.4, 0.2, 0.25, 0.15)):
     """Class of every key (the generators' draw: splitmix64 of the key id)."""
     k = np.arange(n_keys, dtype=np.uint64)
@@ -365,6 +413,8 @@ def main():
                     help="split a counter/timer key above samples / (N * hot_div) per window")
     ap.add_argument("--set-hot", type=int, default=1 << 18, help="split a set key above this many records")
     ap.add_argument("--max-split", type=int, default=64, help="split keys per class at most")
+    ap.add_argument("--hot-stride", type=int, default=256,
+                    help="hot-key detector: count every hot_stride-th record (vn_hot_detect)")
     ap.add_argument("--no-split", action="store_true", help="route every key by digest %% N (no hot keys)")
     ap.add_argument("--exact-threshold", type=int, default=0,
                     help="0 (default): every histogram merge replayed exactly; N: the opt-in fast mode "
@@ -410,16 +460,22 @@ def main():
     ctrl = Group(backend="gloo")  # host control plane: barrier, max / sum of scalars, the RCCL id
     comm = make_comm(ctrl, local_rank)  # the engines' RCCL group (None at N = 1)
 
-    # ---- hot keys: top keys by count in the first 2^24 records of the window (every rank alike)
+    # ---- hot keys: chosen by the engines' own detector (vn_hot_detect / vn_hot_keys) from a
+    # window they have seen -- one unsplit window of the stream, every rank counting its share,
+    # the ranks' candidates summed by key (the --sim-world development mode, which sees one
+    # rank's share only, keeps the count of the stream's first 2^24 records)
     t0 = time.time()
     split = {0: np.zeros(0, np.uint32), 2: np.zeros(0, np.uint32), 3: np.zeros(0, np.uint32)}
+    detect = None
     if not args.no_split:
-        sample = min(args.samples, 1 << 24)
-        counts = V.synth_key_counts(args.seed, args.keys, args.samples, sample, device=local_rank)
-        classes = key_classes(args.seed, args.keys)
         thr = args.samples / ((args.sim_world if sim else world) * args.hot_div)
-        split = hot_keys(counts, args.samples / sample, classes, thr, min(thr, args.set_hot), args.max_split,
-                         split_histos=args.exact_threshold > 0)
+        if sim:
+            sample = min(args.samples, 1 << 24)
+            counts = V.synth_key_counts(args.seed, args.keys, args.samples, sample, device=local_rank)
+            split = hot_keys(counts, args.samples / sample, key_classes(args.seed, args.keys), thr,
+                             min(thr, args.set_hot), args.max_split, split_histos=args.exact_threshold > 0)
+        else:
+            split, detect = detect_split(args, V, ctrl, world, rank, local_rank, thr)
     stream = V.DeviceStream(args.seed, args.keys, args.samples, args.sim_rank if sim else rank,
                             args.sim_world if sim else world, device=local_rank, split=split)
     n_slots = stream.n_slots
@@ -435,6 +491,8 @@ def main():
                    split_max_records=max(stream.split_counts) + 1)
     if comm is not None:
         eng.set_comm(comm)
+    if detect is not None:
+        eng.hot_detect(args.hot_stride)  # the live detector keeps counting inside the timed steps
     split_lists = []
     for c in (0, 2, 3):
         slots = (stream.split_slot0[c] + np.arange(len(split[c]))).astype(np.uint32)
@@ -489,6 +547,11 @@ def main():
     if host_marks:
         log(rank, "[bench] host ms per call (split+ingest_split, ingest, flush; split combine in flush); device ms to main / split ready / split histos / set prefix: %s" %
             np.round(np.mean(host_marks[args.warmup:] or host_marks, axis=0), 3).tolist())
+    if detect is not None:
+        # the split list the detector picks from the last timed window: the one in use
+        redetect = split_from_engine(eng, stream.key_of_slot, split_thresholds(args, thr), ctrl, args.max_split,
+                                     keep=split)
+        detect["stable_over_timed_windows"] = all(np.array_equal(redetect[c], split[c]) for c in split)
     rank_records = ctrl.gather_object(stream.n_records)
     ms_per_step = elapsed * 1e3 / args.steps
     value = float(args.samples) * args.steps / elapsed
@@ -581,7 +644,9 @@ def main():
                    "compression": 100, "hll_precision": 14,
                    "parallelism": "key-sharded FNV %% %d + %d split hot keys (RCCL)" %
                                   (world, sum(len(split[c]) for c in split)),
-                   "split_keys": {"counter": len(split[0]), "histo": len(split[2]), "set": len(split[3])}},
+                   "split_keys": {"counter": len(split[0]), "histo": len(split[2]), "set": len(split[3])},
+                   "split_key_choice": detect if detect is not None else
+                   ("none" if args.no_split else "count of the stream's first 2^24 records (--sim-world)")},
         "roofline": {"bound": "hbm", "kernel": top.get("kernel"), "achieved": top.get("achieved"),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": top.get("frac"), "traffic": traffic,
                      "traffic_unit": "bytes per launch (HBM, PMC FETCH_SIZE x2 + WRITE_SIZE)",

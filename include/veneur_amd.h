@@ -238,6 +238,18 @@ typedef struct {
 int vn_export_histos(vn_engine* eng, const uint32_t* slot, uint64_t n, vn_export* out);
 int vn_export_sets(vn_engine* eng, const uint32_t* slot, uint64_t n, vn_export* out);
 
+/* Hot-key detector: the split list of the next window (vn_split_keys), chosen by the engine
+ * from the window it has seen.  The reference routes every record of a key to one worker
+ * (server.go:655); the split is this build's addition, so it brings its own detector.
+ * vn_hot_detect: from now on count every stride-th record of each vn_ingest / vn_ingest_host
+ * call and of the split records of vn_ingest_split (counters, histos, sets), per slot; 0 turns
+ * it off, 1 counts exactly.  vn_hot_keys: after vn_flush, the slots of class cls (VN_COUNTER,
+ * VN_HISTO or VN_SET) of the flushed window whose estimated count (sampled count x stride) is
+ * at least min_count, hottest first (ties: ascending slot), at most cap of them, with their
+ * estimated counts (count may be NULL); *n = how many were written. */
+int vn_hot_detect(vn_engine* eng, uint32_t stride);
+int vn_hot_keys(vn_engine* eng, int cls, uint64_t min_count, uint32_t cap, uint32_t* slot, uint64_t* count,
+                uint32_t* n);
 int vn_flush(vn_engine* eng, vn_flush_result* out);
 /* vn_flush for a local veneur (flusher.go:41-48,168-230): the percentiles of a histogram are
  * evaluated only where histo_quantile_mask[slot] != 0 (the others come back NaN: Server.Flush

@@ -269,6 +269,8 @@ _sig("vn_split_keys", C.c_int, vp, C.c_int, u32p, u32p, C.c_uint32)
 _sig("vn_ingest_split", C.c_int, vp, C.POINTER(SplitBatch))
 _sig("vn_split_close", C.c_int, vp)
 _sig("vn_split_combine", C.c_int, vp)
+_sig("vn_hot_detect", C.c_int, vp, C.c_uint32)
+_sig("vn_hot_keys", C.c_int, vp, C.c_int, C.c_uint64, C.c_uint32, u32p, C.POINTER(C.c_uint64), u32p)
 _sig("vn_device_alloc", C.c_int, C.c_int, C.c_uint64, C.POINTER(vp))
 _sig("vn_device_free", C.c_int, vp)
 _sig("vn_copy_to_device", C.c_int, C.c_int, vp, vp, C.c_uint64)
@@ -299,6 +301,7 @@ EXPORTED = [
     "vn_synth_hosts_free",
     "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",
     "vn_comm_nranks", "vn_comm_allreduce", "vn_engine_set_comm", "vn_split_keys", "vn_ingest_split", "vn_split_close", "vn_split_combine",
+    "vn_hot_detect", "vn_hot_keys",
 ]
 
 

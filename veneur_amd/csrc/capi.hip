@@ -399,6 +399,7 @@ void destroy_impl(vn_engine* e) {
     }
   if (e->st) (void)hipStreamSynchronize(e->st);
   split_destroy(e);
+  hot_destroy(e);
   dfree(e->cval); dfree(e->ctouch); dfree(e->gseq); dfree(e->gval); dfree(e->gtouch); dfree(e->pk); dfree(e->pp);
   dfree(e->hst); dfree(e->hncent); dfree(e->hcur); dfree(e->htouch);
   for (int b = 0; b < 2; b++) { dfree(e->cmean[b]); dfree(e->cw[b]); }
@@ -638,6 +639,9 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
       (b->n_histo && !e->cap[VN_HISTO]) || (b->n_set && !e->cap[VN_SET]))
     throw std::invalid_argument("records for a class with zero capacity");
   hipStream_t st = e->st;
+  hot_sample(e, VN_COUNTER, b->n_counter, b->counter_slot, nullptr, 0, st);
+  hot_sample(e, VN_HISTO, b->n_histo, b->histo_slot, nullptr, 0, st);
+  hot_sample(e, VN_SET, b->n_set, b->set_slot, nullptr, 0, st);
   const bool tm = e->timing;
   if (tm) {
     e->pool.used = 0;
@@ -1038,6 +1042,17 @@ int vn_export_sets(vn_engine* e, const uint32_t* slot, uint64_t n, vn_export* ou
   return guarded(e, [&] { export_impl(e, VN_SET, slot, n, out); });
 }
 
+int vn_hot_detect(vn_engine* e, uint32_t stride) {
+  if (!e) return VN_EINVAL;
+  return guarded(e, [&] { hot_enable(e, stride); });
+}
+
+int vn_hot_keys(vn_engine* e, int cls, uint64_t min_count, uint32_t cap, uint32_t* slot, uint64_t* count,
+                uint32_t* n) {
+  if (!e || !n || cls < 0 || cls >= VN_NCLASS || cls == VN_GAUGE) return VN_EINVAL;
+  return guarded(e, [&] { *n = hot_collect(e, cls, min_count, cap, slot, count); });
+}
+
 int vn_flush(vn_engine* e, vn_flush_result* out) { return vn_flush_masked(e, nullptr, nullptr, out); }
 
 int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint8_t* set_estimate_mask,
@@ -1054,6 +1069,7 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
     VN_HIP_CHECK(hipGetLastError());
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[6], e->st));
     const uint32_t caller = check_error_flags(e);
+    hot_rotate(e);
     if (e->timing) {
       VN_HIP_CHECK(hipEventSynchronize(e->ev[6]));
       vn_timing& t = e->last;

@@ -132,6 +132,12 @@ struct vn_engine {
   // stream + scratch the counter / gauge / set launchers use for the current call
   // (st2 normally; st when timing is enabled, so per-kernel durations are measured alone)
   hipStream_t side = nullptr;
+  // hot-key detector (hotkeys.hip): every hot_stride-th record's slot counted per class, this
+  // window (hk_cnt[hk_cur]) and the last flushed one (hk_cnt[hk_cur ^ 1], stride hk_prev_stride)
+  uint32_t hot_stride = 0, hk_prev_stride = 0;
+  int hk_cur = 0;
+  uint32_t* hk_cnt[2][VN_NCLASS] = {{nullptr, nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr, nullptr}};
+  uint64_t* hk_list = nullptr;
   std::string err;
   uint32_t cap[VN_NCLASS] = {0, 0, 0, 0};
   uint32_t cap_cent = 256;      // centroids per histo slot (>= 2*compression + 4)

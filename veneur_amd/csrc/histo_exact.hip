@@ -1649,7 +1649,6 @@ constexpr uint32_t kBatchBackoff = 4;          // single merges after a batch th
 #endif
 // keys replaying at least this many samples take the batched kernel (its LDS: one block per CU)
 constexpr uint32_t kBatchMinLen = VN_BATCH_MIN_LEN;
-constexpr uint32_t kWelfK = 4;                 // temps per (centroid, chunk) in straight-line code
 
 typedef __attribute__((address_space(3))) uint8_t ldsu8;
 
@@ -1747,7 +1746,6 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
 #endif
   constexpr uint32_t NT = 64 * NW;
   constexpr double kHi = 1.0 + kBand, kLo = 1.0 - kBand;
-  constexpr uint32_t kItems = (kBB * kBTmax + NT - 1) / NT;  // batch temps per thread
   static_assert(NT >= kBN, "one lane per centroid");
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t cr = c % kRing;
@@ -2086,7 +2084,6 @@ template <int NW, bool BATCH>
 __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& S) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr uint32_t NT = 64 * NW;
-  constexpr uint32_t R = 4 / NW;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t capc = x.capc, tcap = x.tcap;
   const uint32_t TP = round64(tcap + 1);

@@ -57,6 +57,14 @@ void set_replay_ranges(vn_engine* e, const uint64_t* R, const uint32_t* dev_coun
                        uint32_t grid, hipStream_t st);
 // split (hot) keys at flush: combine the ranks' partial states on the owners (split.hip)
 void split_flush(vn_engine* e);
+// hot-key detector (hotkeys.hip): vn_hot_detect, the strided count of a class's records (map:
+// split key index -> slot, or null), vn_flush's close of the window, vn_hot_keys
+void hot_enable(vn_engine* e, uint32_t stride);
+void hot_sample(vn_engine* e, int cls, uint64_t n, const uint32_t* key, const uint32_t* map, uint32_t nmap,
+                hipStream_t st);
+void hot_rotate(vn_engine* e);
+uint32_t hot_collect(vn_engine* e, int cls, uint64_t min_count, uint32_t cap, uint32_t* slot, uint64_t* count);
+void hot_destroy(vn_engine* e);
 // first ingest call of a window: its start event (vn_timing.ms_main_ready / ms_split_ready)
 void window_open(vn_engine* e, hipStream_t st);
 void split_destroy(vn_engine* e);

@@ -1442,6 +1442,8 @@ int vn_ingest_split(vn_engine* e, const vn_split_batch* b) {
     if (f & 2u) throw std::invalid_argument("invalid value added");
     if (f & 4u) throw std::invalid_argument("sample rate must be >0 and <=1");
     if (f & 8u) throw std::invalid_argument("set member offsets must be non-decreasing");
+    hot_sample(e, VN_HISTO, b->n_histo, b->histo_key, S.d_slot[VN_HISTO], nh, st);
+    hot_sample(e, VN_SET, b->n_set, b->set_key, S.d_slot[VN_SET], ns, st);
     if (b->n_histo) {
       VN_HIP_CHECK(hipMemcpyAsync(S.hkey + S.nh, b->histo_key, b->n_histo * 4, hipMemcpyDeviceToDevice, st));
       VN_HIP_CHECK(hipMemcpyAsync(S.hval + S.nh, b->histo_value, b->n_histo * 8, hipMemcpyDeviceToDevice, st));

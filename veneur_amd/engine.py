@@ -169,6 +169,20 @@ class Engine:
             raise ValueError("one owner per split key")
         self._check(A.lib.vn_split_keys(self.h, int(cls), s.ctypes.data_as(A.u32p), o.ctypes.data_as(A.u32p), len(s)))
 
+    def hot_detect(self, stride=1):
+        """vn_hot_detect: count every stride-th ingested record per slot (0: off, 1: exact)."""
+        self._check(A.lib.vn_hot_detect(self.h, int(stride)))
+
+    def hot_keys(self, cls, min_count, cap=64):
+        """vn_hot_keys after a flush: (slots, estimated counts) of class cls at or above
+        min_count in the flushed window, hottest first, at most cap."""
+        slots = np.zeros(max(1, cap), np.uint32)
+        counts = np.zeros(max(1, cap), np.uint64)
+        n = C.c_uint32(0)
+        self._check(A.lib.vn_hot_keys(self.h, int(cls), int(min_count), int(cap), slots.ctypes.data_as(A.u32p),
+                                      counts.ctypes.data_as(C.POINTER(C.c_uint64)), C.byref(n)))
+        return slots[:n.value].copy(), counts[:n.value].copy()
+
     def split_close(self):
         """vn_split_close: this window's split records are all in; their combine starts now."""
         self._check(A.lib.vn_split_close(self.h))
