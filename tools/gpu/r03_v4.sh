@@ -1,0 +1,8 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu tests > gpurun_out/r03_v4_tests.log 2>&1
+echo "tests rc=$?"
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_v4_smoke.log 2>&1 &&
+timeout -k 10 600 python -u bench.py --gpus 1 --steps 10 --warmup 2 > gpurun_out/r03_v4_bench.json 2> gpurun_out/r03_v4_bench.log
+echo "bench rc=$?"
