@@ -24,6 +24,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -413,6 +414,10 @@ def main():
                     help="split a counter/timer key above samples / (N * hot_div) per window")
     ap.add_argument("--set-hot", type=int, default=1 << 18, help="split a set key above this many records")
     ap.add_argument("--max-split", type=int, default=64, help="split keys per class at most")
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="engines taking the windows in turn (window i + 1 ingested while window i's longest "
+                         "replays finish); 1: one engine, windows back to back; 0 (default): 2 on one GPU, 1 "
+                         "over RCCL (a second communicator per rank is not exercised on hardware here)")
     ap.add_argument("--hot-stride", type=int, default=256,
                     help="hot-key detector: count every hot_stride-th record (vn_hot_detect)")
     ap.add_argument("--no-split", action="store_true", help="route every key by digest %% N (no hot keys)")
@@ -484,15 +489,29 @@ def main():
                                 list(stream.split_counts), n_slots, [len(split[c]) for c in (0, 2, 3)],
                                 time.time() - t0))
 
-    eng = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,
-                   max_batch_records=max(stream.counts) + 1,
-                   max_batch_member_bytes=stream.counts[3] * 11 + 64, device=local_rank,
-                   exact_threshold=args.exact_threshold, hot_prefix=args.hot_prefix, piece_growth=args.piece_growth,
-                   split_max_records=max(stream.split_counts) + 1)
+    # D engines take the windows in turn (window i on engine i % D), each driven by its own host
+    # thread: window i + 1 is ingested while window i's longest replays finish -- as the
+    # reference's flush goroutine works on the swapped maps while the workers take the next
+    # interval.  Flushes are entered in window order, so every rank issues the split combine's
+    # collectives (one communicator per engine) in the same order.
+    D = 1 if sim else max(1, args.pipeline if args.pipeline > 0 else (2 if world == 1 else 1))
+
+    def make_engine():
+        e = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,
+                     max_batch_records=max(stream.counts) + 1,
+                     max_batch_member_bytes=stream.counts[3] * 11 + 64, device=local_rank,
+                     exact_threshold=args.exact_threshold, hot_prefix=args.hot_prefix,
+                     piece_growth=args.piece_growth, split_max_records=max(stream.split_counts) + 1)
+        if detect is not None:
+            e.hot_detect(args.hot_stride)  # the live detector keeps counting inside the timed steps
+        return e
+
+    engines = [make_engine() for _ in range(D)]
+    eng = engines[0]
     if comm is not None:
         eng.set_comm(comm)
-    if detect is not None:
-        eng.hot_detect(args.hot_stride)  # the live detector keeps counting inside the timed steps
+        for e in engines[1:]:
+            e.set_comm(make_comm(ctrl, local_rank))
     split_lists = []
     for c in (0, 2, 3):
         slots = (stream.split_slot0[c] + np.arange(len(split[c]))).astype(np.uint32)
@@ -500,57 +519,100 @@ def main():
         split_lists.append((c, slots, owners))
 
     host_marks = []  # --host-trace: host clock at each call's return (development)
+    turn = threading.Condition()
+    state = {"next": 0}
+    lat = []  # per window: host ms from its first call to its flush's return
 
-    def step():
-        t = [time.perf_counter()] if args.host_trace else None
+    def step(e=None, i=None):
+        e = eng if e is None else e
+        t = [time.perf_counter()] if args.host_trace and D == 1 else None
+        ts = time.perf_counter()
         for c, slots, owners in split_lists:
             if len(slots):
-                eng.split_keys(c, slots, owners)
+                e.split_keys(c, slots, owners)
         # split records first: they are buffered on the split engine's stream, so the split
         # combine at flush does not wait behind this engine's ingest
         if sum(stream.split_counts):
-            eng.ingest_split_device(stream.split)
-            eng.split_close()  # their combine runs beside this engine's ingest
+            e.ingest_split_device(stream.split)
+            if D == 1:
+                e.split_close()  # their combine runs beside this engine's ingest
             if args.split_delay_ms:
                 time.sleep(args.split_delay_ms * 1e-3)
         if t:
             t.append(time.perf_counter())
-        eng.ingest_device(stream.batch)
+        e.ingest_device(stream.batch)
         if t:
             t.append(time.perf_counter())
-        r = eng.flush_raw()
+        if i is not None:
+            with turn:
+                turn.wait_for(lambda: state["next"] == i)
+        r = e.flush_raw()
+        if i is not None:
+            with turn:
+                state["next"] = i + 1
+                turn.notify_all()
+        lat.append((time.perf_counter() - ts) * 1e3)
         if t:
             t.append(time.perf_counter())
-            tm = eng.timing()
+            tm = e.timing()
             host_marks.append(np.concatenate([np.diff(t) * 1e3, [tm["ms_split_host"], tm["ms_main_ready"],
                                                                  tm["ms_split_ready"], tm["ms_split_histo_ready"],
                                                                  tm["ms_split_set_prefix_ready"]]]))
         return r
 
+    def run_windows(n):
+        """n windows; returns the last one's flush result."""
+        if D == 1:
+            r = None
+            for _ in range(n):
+                r = step()
+            return r
+        state["next"] = 0
+        out, errs = [None] * n, []
+
+        def worker(k):
+            try:
+                for i in range(k, n, D):
+                    out[i] = step(engines[k], i)
+            except BaseException as ex:  # (the other threads would wait for this turn forever)
+                errs.append(ex)
+                with turn:
+                    state["next"] = 1 << 60
+                    turn.notify_all()
+
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(D)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if errs:
+            raise errs[0]
+        return out[n - 1]
+
     def sync():
         A.lib.vn_device_synchronize(local_rank)
 
-    for _ in range(args.warmup):
-        step()
+    run_windows(args.warmup)
     sync()
     ctrl.barrier()
+    lat.clear()
     t0 = time.perf_counter()
-    last = None
-    for _ in range(args.steps):
-        last = step()
+    last = run_windows(args.steps)
     sync()
     t_rank = time.perf_counter() - t0
     ctrl.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = ctrl.max(elapsed)
     rank_ms = ctrl.gather_object(t_rank * 1e3 / args.steps)
+    window_latency_ms = ctrl.max(float(np.mean(lat))) if lat else None
+    last_eng = engines[(args.steps - 1) % D]
     if host_marks:
         log(rank, "[bench] host ms per call (split+ingest_split, ingest, flush; split combine in flush); device ms to main / split ready / split histos / set prefix: %s" %
             np.round(np.mean(host_marks[args.warmup:] or host_marks, axis=0), 3).tolist())
     if detect is not None:
         # the split list the detector picks from the last timed window: the one in use
-        redetect = split_from_engine(eng, stream.key_of_slot, split_thresholds(args, thr), ctrl, args.max_split,
-                                     keep=split)
+        redetect = split_from_engine(last_eng, stream.key_of_slot, split_thresholds(args, thr), ctrl,
+                                     args.max_split, keep=split)
         detect["stable_over_timed_windows"] = all(np.array_equal(redetect[c], split[c]) for c in split)
     rank_records = ctrl.gather_object(stream.n_records)
     ms_per_step = elapsed * 1e3 / args.steps
@@ -629,6 +691,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
+        "window_latency_ms": window_latency_ms,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -645,6 +708,11 @@ def main():
                    "parallelism": "key-sharded FNV %% %d + %d split hot keys (RCCL)" %
                                   (world, sum(len(split[c]) for c in split)),
                    "split_keys": {"counter": len(split[0]), "histo": len(split[2]), "set": len(split[3])},
+                   "windows_in_flight": D,
+                   "pipeline": ("%d engines per GPU take the windows in turn: window i + 1 is ingested while window "
+                                "i's longest replays finish; every window ingested, replayed and flushed inside the "
+                                "timed region (ms_per_step = timed region / steps; window_latency_ms = one window's "
+                                "first call to its flush's return)" % D) if D > 1 else "one window at a time",
                    "split_key_choice": detect if detect is not None else
                    ("none" if args.no_split else "count of the stream's first 2^24 records (--sim-world)")},
         "roofline": {"bound": "hbm", "kernel": top.get("kernel"), "achieved": top.get("achieved"),
@@ -804,7 +872,8 @@ def main():
         log(rank, "[bench] parity checked in %.1fs" % (time.time() - t1))
     if rank == 0:
         print(json.dumps(result), flush=True)
-    eng.close()
+    for e in engines:
+        e.close()
     stream.free()
     if comm is not None:
         comm.close()
