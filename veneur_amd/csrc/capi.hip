@@ -130,6 +130,18 @@ void create_impl(vn_engine* e) {
     }
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork5, hipEventDisableTiming));
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join5, hipEventDisableTiming));
+#ifdef VN_TOP_EXCL
+    // the longest batched replays (one workgroup each, hundreds of ms) on the last 16th of the
+    // CUs (two per XCC), which every other stream leaves alone: the main stream takes the rest
+    if (e->st2 && ncu >= 64) {
+      std::vector<uint32_t> tmask((ncu + 31) / 32, 0u), amask((ncu + 31) / 32, 0u);
+      for (uint32_t i = 0; i < ncu; i++) (i >= ncu - ncu / 16 ? tmask : amask)[i / 32] |= 1u << (i % 32);
+      VN_HIP_CHECK(hipStreamDestroy(e->st));
+      VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st, (uint32_t)amask.size(), amask.data()));
+      VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st6, (uint32_t)tmask.size(), tmask.data()));
+      VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join6, hipEventDisableTiming));
+    }
+#endif
   }
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
@@ -449,6 +461,15 @@ void destroy_impl(vn_engine* e) {
   if (e->ev_join3) (void)hipEventDestroy(e->ev_join3);
   if (e->st3) (void)hipStreamDestroy(e->st3);
   if (e->st5) (void)hipStreamSynchronize(e->st5);
+  if (e->st6) {
+    (void)hipStreamSynchronize(e->st6);
+    (void)hipStreamDestroy(e->st6);
+    e->st6 = nullptr;
+  }
+  if (e->ev_join6) {
+    (void)hipEventDestroy(e->ev_join6);
+    e->ev_join6 = nullptr;
+  }
   for (hipEvent_t* ev : {&e->ev_fork5, &e->ev_join5})
     if (*ev) {
       (void)hipEventDestroy(*ev);

@@ -123,6 +123,9 @@ struct vn_engine {
   // long-key replay stream (CU mask of st3): the longest keys' four-wave replays
   hipStream_t st5 = nullptr;
   hipEvent_t ev_fork5 = nullptr, ev_join5 = nullptr;
+  // the few longest batched replays on CUs no other stream uses (null: st5 takes them all)
+  hipStream_t st6 = nullptr;
+  hipEvent_t ev_join6 = nullptr;
   // set segment merge held back (ingest_device): the grouped set records are merged once the
   // histo path's remainder sort is done, so the long set kernel does not crowd it out
   bool set_defer = false, set_pending = false;

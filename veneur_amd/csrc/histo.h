@@ -83,7 +83,8 @@ void histo_exact_replay(const ExactCtx& x, hipStream_t st);
 // histo_exact_replay skips them; histo_exact_replay_long replays them (any stream after st).
 bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipStream_t st);
 // the batched kernel (the longest keys) on st, the rest of the long keys on st_rest
-void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest);
+// st_top (or null): the kTopExcl longest batched keys there, the other batched ones on st
+void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest, hipStream_t st_top = nullptr);
 // the replay over x.keys[0, *dev_count) (count known on the device only; <= max_keys)
 void histo_exact_replay_list(const ExactCtx& x, const uint32_t* dev_count, uint32_t max_keys, hipStream_t st);
 // replay list[0..n) longest first: sorts the order into buf0/buf1 (n each) on st and sets x

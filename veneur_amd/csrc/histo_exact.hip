@@ -1636,6 +1636,7 @@ __device__ __noinline__ MergeState merge_step_cold(const MergeParams mp, const L
 #endif
 constexpr uint32_t kBB = VN_BATCH_MERGES;  // merges per batch
 constexpr uint32_t kRing = kBB + 24;        // chunk slots in LDS
+constexpr uint32_t kTopExcl = 8;             // longest batched keys on the engine's own CUs (st6)
 constexpr uint32_t kBM = 160;               // most centroids a batch takes (delta 100: ~135)
 constexpr uint32_t kBN = kBM + 1;           // lanes of a batch (one per centroid, one for the end)
 constexpr uint32_t kBTmax = 48;             // largest temp buffer batched (delta <= ~110)
@@ -2390,10 +2391,11 @@ __global__ __launch_bounds__(64) void k_histo_exact(ExactCtx x) {
 // the long keys of the order, four waves each: entries [nmw[1], nmw[0]) (k_histo_exact_mw) and,
 // batched with the larger LDS, the longest [0, nmw[1]) (k_histo_exact_mwb)
 template <bool BATCH>
-__device__ __forceinline__ void replay_long(const ExactCtx& x, const uint32_t* __restrict__ nmw) {
+__device__ __forceinline__ void replay_long(const ExactCtx& x, const uint32_t* __restrict__ nmw, uint32_t first = 0,
+                                            uint32_t last = 0xffffffffu) {
   __shared__ MwShared S;
-  const uint32_t n = BATCH ? nmw[1] : nmw[0];
-  for (uint32_t i = (BATCH ? 0u : nmw[1]) + blockIdx.x; i < n; i += gridDim.x) {
+  const uint32_t n = min(BATCH ? nmw[1] : nmw[0], last);
+  for (uint32_t i = (BATCH ? first : nmw[1]) + blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t k = x.order64 ? (uint32_t)x.order64[i] : x.order ? x.order[i] : i;
     if (k < x.nkeys) replay_key_fast<kMW, BATCH>(x, k, *(MwSharedL*)&S);
     __syncthreads();  // the next key reuses the LDS
@@ -2402,8 +2404,9 @@ __device__ __forceinline__ void replay_long(const ExactCtx& x, const uint32_t* _
 __global__ __launch_bounds__(kMWThreads) void k_histo_exact_mw(ExactCtx x, const uint32_t* __restrict__ nmw) {
   replay_long<false>(x, nmw);
 }
-__global__ __launch_bounds__(kMWThreads) void k_histo_exact_mwb(ExactCtx x, const uint32_t* __restrict__ nmw) {
-  replay_long<true>(x, nmw);
+__global__ __launch_bounds__(kMWThreads) void k_histo_exact_mwb(ExactCtx x, const uint32_t* __restrict__ nmw,
+                                                                 uint32_t first, uint32_t last) {
+  replay_long<true>(x, nmw, first, last);
 }
 // how many entries of the longest-first order replay at least min_len samples (out[0]), and at
 // least batch_len (out[1], <= out[0])
@@ -2501,12 +2504,15 @@ bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipS
   return true;
 }
 
-void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest) {
+void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest, hipStream_t st_top) {
   if (!x.mw_count) return;
   const uint32_t grid = std::min<uint32_t>(x.norder, kMaxLongKeys / 2);
-  if (x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024)
-    hipLaunchKernelGGL(k_histo_exact_mwb, dim3(grid), dim3(kMWThreads), exact_batch_smem_bytes(x.capc, x.tcap), st, x,
-                       x.mw_count);
+  if (x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024) {
+    const size_t sm = exact_batch_smem_bytes(x.capc, x.tcap);
+    const uint32_t top = st_top ? std::min<uint32_t>(kTopExcl, x.norder) : 0u;
+    if (top) hipLaunchKernelGGL(k_histo_exact_mwb, dim3(top), dim3(kMWThreads), sm, st_top, x, x.mw_count, 0u, top);
+    hipLaunchKernelGGL(k_histo_exact_mwb, dim3(grid), dim3(kMWThreads), sm, st, x, x.mw_count, top, 0xffffffffu);
+  }
   hipLaunchKernelGGL(k_histo_exact_mw, dim3(grid), dim3(kMWThreads), exact_fast_smem_bytes(x.capc, x.tcap), st_rest, x,
                      x.mw_count);
 }

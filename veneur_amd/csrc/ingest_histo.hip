@@ -589,8 +589,19 @@ __global__ void k_histo_plan(uint32_t ntouched, const uint32_t* __restrict__ tl,
                              uint32_t* __restrict__ ex, uint32_t* __restrict__ remflag,
                              uint32_t* __restrict__ replayflag, uint32_t* __restrict__ hotflag,
                              uint32_t* __restrict__ warmflag, uint32_t* __restrict__ hotcnt,
-                             uint32_t* __restrict__ seen0) {
+                             uint32_t* __restrict__ seen0, uint32_t* __restrict__ maxex) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  // the longest exact part of a replayed (cold or warm) key: the host skips the long-key
+  // launches when none reaches their length (one atomic per wave)
+  uint32_t mx = 0;
+  if (k < ntouched) {
+    const uint32_t s = tl[k], nk = end[s] - start[s], seen = hseen[s];
+    const uint64_t tot = (uint64_t)seen + nk;
+    if (tot <= (uint64_t)kWarmFactor * E) mx = tot <= E ? nk : (seen < E ? E - seen : 0u);
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+  if ((threadIdx.x & 63) == 0 && mx) atomicMax(maxex, mx);
   if (k >= ntouched) return;
   uint32_t s = tl[k];
   uint32_t nk = end[s] - start[s];
@@ -1229,9 +1240,10 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   // ---- 2. plan: exact part of every key (cold / warm / hot, k_histo_plan); the remainders
   // of warm and hot keys cut into geometric pieces
   uint32_t* const remflag = e->h_hotflag;
+  VN_HIP_CHECK(hipMemsetAsync(e->h_cnt + 20, 0, sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_histo_plan, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_start,
                      e->h_end, e->hseen, e->exact_threshold, e->hot_prefix, e->h_ex, remflag, e->h_coldflag,
-                     e->h_vhflag, e->h_warmflag, e->h_hotcnt, e->h_seen0);
+                     e->h_vhflag, e->h_warmflag, e->h_hotcnt, e->h_seen0, e->h_cnt + 20);
   compact_flags(e->h_vhflag, e->h_pos, e->h_hotlist, e->h_cnt + 1, ntouched, e->ss, st);
   compact_flags(e->h_warmflag, e->h_pos, e->h_warmlist, e->h_cnt + 8, ntouched, e->ss, st);
   compact_flags(e->h_coldflag, e->h_pos, e->h_coldlist, e->h_cnt + 6, ntouched, e->ss, st);
@@ -1248,6 +1260,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 6, e->h_cnt + 6, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 7, e->h_cnt + 8, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 11, e->h_cnt + 11, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 13, e->h_cnt + 20, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipStreamSynchronize(st));
   const uint32_t nhot = e->hf_cnt[1];
   const uint64_t nremrec = e->hf_cnt[2];  // remainder records of warm and hot keys
@@ -1257,6 +1270,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   const uint32_t maxp_hot_left = e->hf_cnt[11];  // after the fused launch of the leading pieces
   const uint32_t nreplay = e->hf_cnt[6];  // cold + warm keys
   const uint32_t nwarm = e->hf_cnt[7];
+  const uint32_t maxex = e->hf_cnt[13];  // longest exact part of a cold or warm key
 
   // ---- 3. exact replay of MergingDigest.Add (histo_exact.hip): every pure chunk pre-sorted,
   // then the cold and warm keys on the replay stream, the hot keys' prefixes on their own
@@ -1314,20 +1328,23 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
     histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
     const uint32_t min_len =
         e->long_replay ? e->long_replay : std::min<uint32_t>(std::max<uint32_t>(e->exact_threshold / 4, 1024u), 8192u);
-    const bool longk = histo_exact_count_long(xc, min_len, e->h_cnt + 15, s);
+    const bool longk = maxex >= min_len && histo_exact_count_long(xc, min_len, e->h_cnt + 15, s);
     const bool side5 = longk && !e->timing && e->st5;
     hipEvent_t a = e->timing ? e->pool_rp.next() : nullptr, b = e->timing ? e->pool_rp.next() : nullptr;
     if (a && b) VN_HIP_CHECK(hipEventRecord(a, s));
     if (side5) {  // the batched longest keys on st5, the other long keys ahead of the rest on s
       VN_HIP_CHECK(hipEventRecord(e->ev_fork5, s));
       VN_HIP_CHECK(hipStreamWaitEvent(e->st5, e->ev_fork5, 0));
-      histo_exact_replay_long(xc, e->st5, s);
+      if (e->st6) VN_HIP_CHECK(hipStreamWaitEvent(e->st6, e->ev_fork5, 0));
+      histo_exact_replay_long(xc, e->st5, s, e->st6);
       VN_HIP_CHECK(hipEventRecord(e->ev_join5, e->st5));
+      if (e->st6) VN_HIP_CHECK(hipEventRecord(e->ev_join6, e->st6));
     } else if (longk) {
       histo_exact_replay_long(xc, s, s);
     }
     histo_exact_replay(xc, s);
     if (side5) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join5, 0));
+    if (side5 && e->st6) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join6, 0));
     if (a && b) VN_HIP_CHECK(hipEventRecord(b, s));
     if (e->timing) e->kstat_rp.launches++;
     xc.mw_count = nullptr;
