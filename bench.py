@@ -56,6 +56,66 @@ def hot_keys(counts, scale, classes, thr_cs, thr_set, max_split, split_histos=Fa
     return out
 
 
+class InTurn:
+    """Windows over D engines: window i runs on engine i % D, each engine's windows in order in a
+    host thread of its own (D > 1), and the flushes entered in window order -- work(k, i, turn)
+    calls `with turn(i):` around its flush.  run(n) returns the n results in window order."""
+
+    def __init__(self, D):
+        self.D = D
+        self.cv = threading.Condition()
+        self.next = 0
+        self.failed = False
+
+    def turn(self, i):
+        pipe = self
+
+        class _T:
+            def __enter__(self):
+                with pipe.cv:
+                    pipe.cv.wait_for(lambda: pipe.next == i or pipe.failed)
+                    if pipe.failed:
+                        raise RuntimeError("an earlier window failed")
+
+            def __exit__(self, *exc):
+                with pipe.cv:
+                    if exc[0] is None:
+                        pipe.next = i + 1
+                    else:
+                        pipe.failed = True  # (the other engines' waits end)
+                    pipe.cv.notify_all()
+                return False
+
+        return _T()
+
+    def run(self, n, work):
+        self.next, self.failed = 0, False
+        out, errs = [None] * n, []
+        if self.D == 1:
+            for i in range(n):
+                out[i] = work(0, i, self.turn)
+            return out
+
+        def worker(k):
+            try:
+                for i in range(k, n, self.D):
+                    out[i] = work(k, i, self.turn)
+            except BaseException as ex:
+                errs.append(ex)
+                with self.cv:
+                    self.failed = True
+                    self.cv.notify_all()
+
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(self.D)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if errs:
+            raise errs[0]
+        return out
+
+
 def split_thresholds(args, thr):
     """{class: min window count} of the classes that split (timers only in the fast mode)."""
     t = {0: thr, 3: min(thr, args.set_hot)}
@@ -519,12 +579,11 @@ def main():
         split_lists.append((c, slots, owners))
 
     host_marks = []  # --host-trace: host clock at each call's return (development)
-    turn = threading.Condition()
-    state = {"next": 0}
+    pipe = InTurn(D)
     lat = []  # per window: host ms from its first call to its flush's return
 
-    def step(e=None, i=None):
-        e = eng if e is None else e
+    def step(k=0, i=None, turn=None):
+        e = engines[k]
         t = [time.perf_counter()] if args.host_trace and D == 1 else None
         ts = time.perf_counter()
         for c, slots, owners in split_lists:
@@ -543,14 +602,11 @@ def main():
         e.ingest_device(stream.batch)
         if t:
             t.append(time.perf_counter())
-        if i is not None:
-            with turn:
-                turn.wait_for(lambda: state["next"] == i)
-        r = e.flush_raw()
-        if i is not None:
-            with turn:
-                state["next"] = i + 1
-                turn.notify_all()
+        if turn is not None:
+            with turn(i):
+                r = e.flush_raw()
+        else:
+            r = e.flush_raw()
         lat.append((time.perf_counter() - ts) * 1e3)
         if t:
             t.append(time.perf_counter())
@@ -562,32 +618,7 @@ def main():
 
     def run_windows(n):
         """n windows; returns the last one's flush result."""
-        if D == 1:
-            r = None
-            for _ in range(n):
-                r = step()
-            return r
-        state["next"] = 0
-        out, errs = [None] * n, []
-
-        def worker(k):
-            try:
-                for i in range(k, n, D):
-                    out[i] = step(engines[k], i)
-            except BaseException as ex:  # (the other threads would wait for this turn forever)
-                errs.append(ex)
-                with turn:
-                    state["next"] = 1 << 60
-                    turn.notify_all()
-
-        th = [threading.Thread(target=worker, args=(k,)) for k in range(D)]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        if errs:
-            raise errs[0]
-        return out[n - 1]
+        return pipe.run(n, step)[-1] if n else None
 
     def sync():
         A.lib.vn_device_synchronize(local_rank)

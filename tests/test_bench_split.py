@@ -50,3 +50,42 @@ def test_hysteresis_keeps_a_split_key_above_half_the_threshold():
     e2 = FakeEngine({0: [(0, 200), (1, 700)]})
     assert bench.split_from_engine(e2, key_of_slot, {0: 500}, ctrl, max_split=8,
                                    keep={0: np.array([10, 11])})[0].tolist() == [11]
+
+
+def test_windows_in_turn_flush_in_window_order_and_fail_without_hanging():
+    import random
+    import threading
+    import time
+
+    import pytest
+
+    order, per_engine, lock = [], {}, threading.Lock()
+
+    def work(k, i, turn):
+        time.sleep(random.random() * 0.01)  # ingest of a varying length
+        with lock:
+            per_engine.setdefault(k, []).append(i)
+        with turn(i):
+            with lock:
+                order.append(i)
+        return (k, i)
+
+    for D in (1, 2, 3):
+        order.clear()
+        per_engine.clear()
+        out = bench.InTurn(D).run(10, work)
+        assert order == list(range(10))
+        assert out == [(i % D, i) for i in range(10)]
+        assert all(v == sorted(v) and all(i % D == k for i in v) for k, v in per_engine.items())
+
+    def bad(k, i, turn):
+        if i == 4:
+            raise RuntimeError("window 4")
+        with turn(i):
+            pass
+        return i
+
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="window 4"):
+        bench.InTurn(2).run(10, bad)
+    assert time.time() - t0 < 5
