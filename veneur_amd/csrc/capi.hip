@@ -131,8 +131,11 @@ void create_impl(vn_engine* e) {
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork5, hipEventDisableTiming));
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join5, hipEventDisableTiming));
 #ifdef VN_TOP_EXCL
-    // the longest batched replays (one workgroup each, hundreds of ms) on the last 16th of the
-    // CUs (two per XCC), which every other stream leaves alone: the main stream takes the rest
+    // (opt-in build) the longest batched replays (one workgroup each, hundreds of ms) on the last
+    // 16th of the CUs (two per XCC), which every other stream leaves alone: the main stream takes
+    // the rest.  Measured at C4 (profiles/r03_v6_*, r03_v7_*, r03_v8_*): two engines in turn 305-316
+    // ms per window against 359 without it, one engine 395 against 385 -- but with it the other
+    // engines of the process slowed down (the C5 leg 510 ms against 311), so it is not the default
     if (e->st2 && ncu >= 64) {
       std::vector<uint32_t> tmask((ncu + 31) / 32, 0u), amask((ncu + 31) / 32, 0u);
       for (uint32_t i = 0; i < ncu; i++) (i >= ncu - ncu / 16 ? tmask : amask)[i / 32] |= 1u << (i % 32);

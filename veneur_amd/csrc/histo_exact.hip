@@ -1636,7 +1636,7 @@ __device__ __noinline__ MergeState merge_step_cold(const MergeParams mp, const L
 #endif
 constexpr uint32_t kBB = VN_BATCH_MERGES;  // merges per batch
 constexpr uint32_t kRing = kBB + 24;        // chunk slots in LDS
-constexpr uint32_t kTopExcl = 8;             // longest batched keys on the engine's own CUs (st6)
+constexpr uint32_t kTopExcl = 8;             // longest batched keys on CUs no other stream uses (st6)
 constexpr uint32_t kBM = 160;               // most centroids a batch takes (delta 100: ~135)
 constexpr uint32_t kBN = kBM + 1;           // lanes of a batch (one per centroid, one for the end)
 constexpr uint32_t kBTmax = 48;             // largest temp buffer batched (delta <= ~110)
