@@ -49,6 +49,29 @@ __device__ __forceinline__ uint32_t be32(const uint8_t* d) {
   return ((uint32_t)d[0] << 24) | ((uint32_t)d[1] << 16) | ((uint32_t)d[2] << 8) | d[3];
 }
 
+// f(byte) over global bytes [p, p + len) in order, read as aligned 16-byte blocks with the next
+// block's load in flight while this one is consumed (one lane walking its own payload).  The
+// blocks never leave the 16-byte-aligned span holding the bytes (so no page the bytes do not touch).
+template <class F>
+__device__ __forceinline__ void for_bytes(const uint8_t* p, uint32_t len, F&& f) {
+  if (!len) return;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(p), a0 = s & ~(uintptr_t)15;
+  const uint32_t lo = (uint32_t)(s - a0), end = lo + len, nblk = (end + 15u) >> 4;
+  const uint4* b = reinterpret_cast<const uint4*>(a0);
+  uint4 cur = b[0];
+  for (uint32_t k = 0; k < nblk; k++) {
+    const uint4 nxt = b[min(k + 1u, nblk - 1u)];
+    const uint32_t base = k << 4;
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint32_t w = j < 4 ? cur.x : j < 8 ? cur.y : j < 12 ? cur.z : cur.w;
+      const uint32_t pos = base + (uint32_t)j;
+      if (pos >= lo && pos < end) f((w >> ((j & 3) * 8)) & 0xffu);
+    }
+    cur = nxt;
+  }
+}
+
 // parse + validate one MarshalBinary payload (hyperloglog.go:318-376, compressed.go:83-97)
 __global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
                             HllPart* __restrict__ parts, uint32_t* __restrict__ err) {
@@ -72,17 +95,22 @@ __global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const 
           if (!bad) {
             // the list must decode completely into strictly increasing codes
             const uint8_t* lb = d + last + 12;
-            uint32_t prev = 0, x = 0, sh = 0, k = 0, rmin = 0xffu, rmax = 0u;
-            for (uint32_t j = 0; j < (uint32_t)tssz; j++) {
-              uint32_t ri, r;
-              decode_hash(be32(d + 8 + 4 * j), &ri, &r);
-              rmin = min(rmin, r);
-              rmax = max(rmax, r);
-            }
-            for (uint64_t j = 0; j < sz && !bad; j++) {
-              const uint32_t b = lb[j];
+            uint32_t prev = 0, x = 0, sh = 0, k = 0, rmin = 0xffu, rmax = 0u, tc = 0, tn = 0, lastb = 0;
+            // (both read as 16-byte blocks, the next in flight: one lane walks the payload)
+            for_bytes(d + 8, 4u * (uint32_t)tssz, [&](uint32_t b) {
+              tc = (tc << 8) | b;
+              if (++tn == 4) {
+                uint32_t ri, r;
+                decode_hash(tc, &ri, &r);
+                rmin = min(rmin, r);
+                rmax = max(rmax, r);
+                tn = 0;
+              }
+            });
+            for_bytes(lb, (uint32_t)sz, [&](uint32_t b) {
               if (sh < 32) x |= (b & 0x7fu) << sh;
               sh += 7;
+              lastb = b;
               if (!(b & 0x80u)) {
                 const uint32_t c = prev + x;
                 if (k > 0 && c <= prev) bad = true;
@@ -95,8 +123,8 @@ __global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const 
                 x = 0;
                 sh = 0;
               }
-            }
-            if (sz && (lb[sz - 1] & 0x80u)) bad = true;  // a code without its last byte
+            });
+            if (sz && (lastb & 0x80u)) bad = true;  // a code without its last byte
             p.kind = 0;
             p.ntmp = (uint32_t)tssz;
             p.tmp_off = o + 8;
@@ -128,29 +156,6 @@ __global__ void k_hll_keys(uint64_t n, const uint32_t* __restrict__ slot, uint64
   keys[i] = ((uint64_t)s << 32) | (uint64_t)i;
   bt[s] = 1;
   stouch[s] = 1;  // Upsert happens before Combine (worker.go:241), even if the merge fails
-}
-
-// f(byte) over global bytes [p, p + len) in order, read as aligned 16-byte blocks with the next
-// block's load in flight while this one is consumed (one lane walking its own payload).  The
-// blocks never leave the 16-byte-aligned span holding the bytes (so no page the bytes do not touch).
-template <class F>
-__device__ __forceinline__ void for_bytes(const uint8_t* p, uint32_t len, F&& f) {
-  if (!len) return;
-  const uintptr_t s = reinterpret_cast<uintptr_t>(p), a0 = s & ~(uintptr_t)15;
-  const uint32_t lo = (uint32_t)(s - a0), end = lo + len, nblk = (end + 15u) >> 4;
-  const uint4* b = reinterpret_cast<const uint4*>(a0);
-  uint4 cur = b[0];
-  for (uint32_t k = 0; k < nblk; k++) {
-    const uint4 nxt = b[min(k + 1u, nblk - 1u)];
-    const uint32_t base = k << 4;
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const uint32_t w = j < 4 ? cur.x : j < 8 ? cur.y : j < 12 ? cur.z : cur.w;
-      const uint32_t pos = base + (uint32_t)j;
-      if (pos >= lo && pos < end) f((w >> ((j & 3) * 8)) & 0xffu);
-    }
-    cur = nxt;
-  }
 }
 
 // ---- block-wide helpers (256 threads)
