@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VN_ABI_VERSION 2
+#define VN_ABI_VERSION 3
 
 enum {
   VN_OK = 0,
@@ -152,7 +152,13 @@ typedef struct {
 
   uint64_t samples_processed;          /* records ingested this window (worker.processed) */
   uint64_t samples_imported;           /* imported values this window (worker.imported) */
+  /* The caller's misuse seen this window; the flush itself completed (VN_OK) and every output
+   * above is valid.  VN_WARN_SPLIT_TOUCHED: a split key's slot also received vn_ingest records
+   * or imports (its records belong to vn_ingest_split); the split combine's state was kept and
+   * those records were dropped. */
+  uint64_t warn_flags;
 } vn_flush_result;
+#define VN_WARN_SPLIT_TOUCHED 16u
 #define VN_HISTO_STATS 8
 
 /* Sparse / dense sketch state of one set slot (axiomhq Sketch fields). */

@@ -122,6 +122,38 @@ def test_import_histos_hot_key_rank_error():
     assert f.histo_stats[0][5] == w.histo_stats(0)[5] and f.histo_stats[0][6] == w.histo_stats(0)[6]
 
 
+def test_import_histos_sliced_through_a_small_run_bit_exact():
+    """a call holding far more centroids than the import run (max_batch_records 256)
+    is cut into slices of whole payloads, each at most the run -- payloads of 50-250 samples
+    (up to ~130 centroids) can no longer make a slice of up to 1.5x the run -- and merged in
+    arrival order: bit-exact against the restated Go's per-payload Merge."""
+    rng = np.random.default_rng(23)
+    nk, npay = 6, 180
+    w = oracle.Worker(1, 1, nk, 1)
+    slots = rng.integers(0, nk, npay).astype(np.uint32)
+    pays = [digest_payload(rng, int(rng.integers(50, 250)), rate_tenth=0.1) for _ in slots]
+    for s, p in zip(slots, pays):
+        t = oracle.MergingDigest(100.0)
+        t.gob_decode(p)
+        assert w.import_histo(int(s), p, identity(len(t.centroids()[0]))) == 0
+    with make_engine((1, 1, nk, 1), max_records=256) as e:
+        e.import_histos(slots, pays)
+        _check_histos(e, w, range(nk))
+
+
+def test_import_histos_oversize_digest_refused_before_anything_applies():
+    """a payload larger than the run is refused up front: nothing of the call is applied"""
+    rng = np.random.default_rng(24)
+    small = digest_payload(rng, 30)
+    big = digest_payload(rng, 400)  # > 64 centroids
+    with make_engine((1, 1, 4, 1), max_records=64) as e:
+        with pytest.raises(V.EngineError):
+            e.import_histos([0, 1, 2], [small, small, big])
+        e.import_histos([3], [small])
+        f = e.flush()
+    assert f.histo_slot.tolist() == [3]
+
+
 def test_import_histos_malformed_fails_loudly():
     good = digest_payload(np.random.default_rng(1), 20)
     with make_engine((1, 1, 4, 1)) as e:

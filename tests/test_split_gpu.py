@@ -297,9 +297,9 @@ def test_split_close_runs_combine_in_engine_thread(N):
 def test_split_slot_with_direct_records_is_reported_not_mixed():
     """A split key's records belong to vn_ingest_split.  A window in which its slot also gets
     vn_ingest records (or imports) keeps the split combine's state -- moved on the engine's own
-    stream after every ingest of the window -- and the flush reports the misuse (VN_EINVAL) once;
-    the next window is unaffected."""
-    from veneur_amd.engine import EngineError
+    stream after every ingest of the window -- and the flush reports the misuse once
+    (warn_flags, a RuntimeWarning) while still returning the window: ADVICE r3, one misrouted
+    record must not lose every other key's aggregates.  The next window is unaffected."""
     rng = np.random.default_rng(11)
     v = rng.lognormal(3.0, 1.0, 5000)
     comms = Comm.local(1)
@@ -309,8 +309,15 @@ def test_split_slot_with_direct_records_is_reported_not_mixed():
         e.split_keys(2, np.array([1], np.uint32), np.array([0], np.uint32))
         e.ingest_split(histos=(np.zeros(len(v), np.uint32), v, np.ones(len(v), np.float32)))
         e.ingest(histos=(np.array([1, 2], np.uint32), np.array([7.0, 8.0]), np.ones(2, np.float32)))
-        with pytest.raises(EngineError, match="split key"):
-            e.flush()
+        with pytest.warns(RuntimeWarning, match="split key"):
+            f0 = e.flush()
+        assert f0.warn_flags & 16
+        # the window survived: slot 2's own histogram, and slot 1 as the split combine left it
+        assert f0.histo_slot.tolist() == [1, 2]
+        assert f0.histo_stats[1][0] == 1.0 and f0.histo_stats[1][1] == 8.0
+        w0 = oracle.Worker(1, 1, 1, 1)
+        w0.histo(np.zeros(len(v), np.uint32), v, np.ones(len(v), np.float32))
+        np.testing.assert_array_equal(f0.histo_quantiles[0], [w0.histo_quantile(0, p) for p in PCT])
         # the next window: split records only, no error, the single consumer's digest
         e.split_keys(2, np.array([1], np.uint32), np.array([0], np.uint32))
         e.ingest_split(histos=(np.zeros(len(v), np.uint32), v, np.ones(len(v), np.float32)))

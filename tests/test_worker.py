@@ -533,7 +533,25 @@ def test_rejected_batch_is_dropped_not_resubmitted(caplog):
     w = W.Worker(engine=Rejecting(), batch_records=2)
     for i in range(5):
         w.ProcessMetric(W.UDPMetric(K("a%d" % i, "counter"), 1.0))
-    # batches of 2 rejected twice; the fifth record still staged, the stage never grows past 2
-    assert w.dropped == 4 and w._staged == 1 and "dropping a batch" in caplog.text
+    # batches of 2 rejected twice; the fifth record still staged, the stage never grows past 2;
+    # counted as refused batches, apart from the per-record NaN-rate drops
+    assert w.dropped_batches == 2 and w.dropped_batch_records == 4 and w.dropped == 0
+    assert w._staged == 1 and "dropping a batch" in caplog.text
     w.Flush()
-    assert w.dropped == 5 and [c[0] for c in w.engine.calls].count("ingest") == 3
+    assert w.dropped_batches == 3 and w.dropped_batch_records == 5
+    assert [c[0] for c in w.engine.calls].count("ingest") == 3
+
+
+def test_invalid_records_screened_so_valid_batch_mates_are_kept():
+    """a NaN-rate record is dropped alone before staging (the engine would refuse the
+    whole batch), a NaN / Inf histogram value raises as Add panics -- the valid records staged
+    beside them reach the engine."""
+    w = W.Worker(engine=RecordingEngine(), batch_records=4)
+    w.ProcessMetric(W.UDPMetric(K("c", "counter"), 1.0))
+    w.ProcessMetric(W.UDPMetric(K("c", "counter"), 2.0, sample_rate=float("nan")))
+    with pytest.raises(ValueError):
+        w.ProcessMetric(W.UDPMetric(K("h", "histogram"), float("inf")))
+    w.ProcessMetric(W.UDPMetric(K("h", "histogram"), 3.0))
+    w.Flush()
+    ing = [c for c in w.engine.calls if c[0] == "ingest"]
+    assert len(ing) == 1 and w.dropped == 1 and w.dropped_batches == 0

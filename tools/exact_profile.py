@@ -32,7 +32,7 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     with V.Engine((1, 1, nk, 1), compression=100.0, percentiles=(0.5, 0.99),
                   max_batch_records=len(slots) + 1) as e:
         e.timing_enable(True)
-        buf = (C.c_ulonglong * 32)()
+        buf = (C.c_ulonglong * 64)()
         A.lib.vn_prof_exact_read(buf, 1)
         t0 = time.perf_counter()
         e.ingest(histos=(slots, vals, rates))
@@ -58,13 +58,17 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     out["batch_avg_committed"] = round(p[24] / nb, 2)
     out["batch_avg_usable"] = round(p[26] / nb, 2)
     out["batch_avg_flagged"] = round(p[25] / nb, 2)
-    for i, nme in zip(range(16, 22), ("totals", "assign", "lanes", "bounds", "flagged", "commit")):
+    out["batch_structural_rejects"] = p[22]
+    # merge_batch phases (histo_exact.hip): totals, A pos search, B n table + offsets,
+    # C1+E+C2 lists / Welford / bounds, F decisions + bound tests, G flagged tests, H commit
+    for i, nme in zip((16, 17, 18, 19, 15, 20, 21, 48, 13), ("totals", "A_pos", "B_ntable", "C_offsets_K_bounds",
+                                                            "D_lists", "E_welford", "F_decisions", "G_flagged",
+                                                            "H_commit")):
         out["batch_cyc_" + nme] = round(p[i] / nb, 1)
-    out["batch_cyc_stats"] = round(p[27] / nb, 1)
-    out["batch_w0_prefix_loop"] = round(p[13] / nb, 1)
-    out["batch_w0_welford_loop"] = round(p[14] / nb, 1)
-    out["batch_w0_decision_loop"] = round(p[15] / nb, 1)
-    out["batch_lane0_nonempty_chunks"] = round(p[22] / nb, 2)
+    out["batch_cyc_column0_welford"] = round(p[14] / nb, 1)
+    out["batch_cyc_call"] = round(p[27] / nb, 1)
+    for base, nme in ((36, "E"), (40, "C2")):
+        out["batch_cyc_" + nme + "_per_wave"] = [round(p[base + w] / nb, 1) for w in range(4)]
     out["singles_after_reject"] = p[29]
     out["singles_after_reject_cyc"] = p[28]
     out["singles_unbatchable"] = p[31]

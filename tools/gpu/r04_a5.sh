@@ -1,0 +1,5 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+VN_LIB=libveneur_amd_variant.so timeout -k 10 120 python -u tools/debug_prefix.py debug/debug_rising.npz 25362 > gpurun_out/r04_a5.log 2>&1
+echo "rc=$?"

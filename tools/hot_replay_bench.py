@@ -55,6 +55,11 @@ def main():
             A.lib.vn_device_synchronize(0)
             times.append(time.perf_counter() - t0)
         ms = min(times[1:]) * 1e3
+        gobs = None
+        if not a.no_check:  # the whole digest of the longest keys (GobEncode, pending merged)
+            e.ingest_device(b)
+            gobs = e.export_histos(np.arange(min(a.keys, 4), dtype=np.uint32))
+            e.flush()
     merges = a.n // 42
     out = {"mode": "fast" if a.fast else "exact", "keys": a.keys, "samples_per_key": a.n, "cold_keys": a.cold_keys,
            "rates": a.rates, "ms_window": ms,
@@ -65,6 +70,7 @@ def main():
         w.histo(slot, val, rate)
         oq = np.array([[w.histo_quantile(k, p) for p in pct] for k in range(nk)])
         out["quantiles_bit_exact"] = bool(np.array_equal(f.histo_quantiles, oq))
+        out["digests_bit_exact"] = all(g == w.histo_gob(k) for k, g in enumerate(gobs))
     print(out, flush=True)
 
 

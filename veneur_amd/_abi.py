@@ -95,7 +95,11 @@ class FlushResult(C.Structure):
                 ("n_histo", C.c_uint64), ("histo_slot", u32p), ("histo_stats", f64p),
                 ("histo_quantiles", f64p), ("n_percentiles", C.c_uint32),
                 ("n_set", C.c_uint64), ("set_slot", u32p), ("set_estimate", u64p), ("set_sparse", u8p),
-                ("samples_processed", C.c_uint64), ("samples_imported", C.c_uint64)]
+                ("samples_processed", C.c_uint64), ("samples_imported", C.c_uint64),
+                ("warn_flags", C.c_uint64)]
+
+
+VN_WARN_SPLIT_TOUCHED = 16
 
 
 class SetState(C.Structure):
@@ -174,7 +178,7 @@ def _sig(name, res, *args):
 vp = C.c_void_p
 _sig("vn_abi_version", C.c_int)
 _sig("vn_struct_size", C.c_size_t, C.c_int)
-ABI_VERSION = 2
+ABI_VERSION = 3
 _sig("vn_engine_create", C.c_int, C.POINTER(Config), C.POINTER(vp))
 _sig("vn_engine_destroy", None, vp)
 _sig("vn_last_error", C.c_char_p, vp)

@@ -219,7 +219,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_warmflag, touch_max);
   dalloc(e->h_warmlist, touch_max);
   dalloc(e->hA2, e->h_sort_cap); dalloc(e->hB2, e->h_sort_cap);
-  dalloc(e->h_csv, ch ? R : 0); dalloc(e->h_csw, ch ? R : 0);
+  dalloc(e->h_csv, ch ? R : 0); dalloc(e->h_csw, ch ? R : 0); dalloc(e->h_cpk, ch ? R : 0);  // (u32 per record)
   dalloc(e->h_lpt0, touch_max); dalloc(e->h_lpt1, touch_max);
   dalloc(e->h_tl2, touch_max);
   dalloc(e->h_ccnt, touch_max);
@@ -424,7 +424,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
   dfree(e->hseen); dfree(e->hpend); dfree(e->hspn); dfree(e->hspw); dfree(e->hm_flag); dfree(e->hm_pos); dfree(e->hm_idx); dfree(e->hm_list); dfree(e->hm_cnt); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
-  dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw);
+  dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw); dfree(e->h_cpk);
   dfree(e->h_lpt0); dfree(e->h_lpt1); dfree(e->s_lpt0); dfree(e->s_lpt1);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_cown); dfree(e->h_tw);
   dfree(e->fz_val); dfree(e->fz_w); dfree(e->fz_k); dfree(e->fz_done);
@@ -825,6 +825,7 @@ void side_join(vn_engine* e) {
 extern "C" {
 
 int vn_abi_version(void) { return VN_ABI_VERSION; }
+static_assert(kErrSplitTouched == VN_WARN_SPLIT_TOUCHED, "the flush reports the device flag as is");
 
 size_t vn_struct_size(int which) {
   switch (which) {
@@ -1092,8 +1093,8 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
     flush_all(e, out, histo_quantile_mask, set_estimate_mask);
     VN_HIP_CHECK(hipGetLastError());
     if (e->timing) VN_HIP_CHECK(hipEventRecord(e->ev[6], e->st));
+    hot_rotate(e);  // (first: the detector's window closes on every exit path, a thrown flag included)
     const uint32_t caller = check_error_flags(e);
-    hot_rotate(e);
     if (e->timing) {
       VN_HIP_CHECK(hipEventSynchronize(e->ev[6]));
       vn_timing& t = e->last;
@@ -1148,7 +1149,7 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
       e->w_open = false;
     }
     e->sp.ran = false;
-    throw_caller_errors(caller);  // (the window is flushed; the error is the caller's)
+    out->warn_flags = caller;  // (the window is flushed; the misuse is reported, not thrown)
   });
 }
 

@@ -67,6 +67,11 @@ struct ExactCtx {
   double* csv;
   double* csw;
   double* ctw;
+  // the batched replay's packed weights (null: no batched replay): per record the exclusive prefix
+  // of the chunk's sorted weights (u16) << 16 | |w| (u16); a chunk's first record carries its
+  // tempW as the prefix, or 0xffffffff when the chunk cannot be batched (a weight that is not an
+  // integer, or a tempW of 65536 or more)
+  uint32_t* cpk;
   uint32_t* cown;  // [chunks] the key index of every pure chunk (null: searched in coff)
 };
 

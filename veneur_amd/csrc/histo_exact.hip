@@ -42,7 +42,7 @@ __host__ __device__ inline size_t exact_smem_bytes_hd(uint32_t capc, uint32_t tc
 
 #ifdef VN_EXACT_PROF
 // profiling build only (tools/exact_profile.py): cycles per merge phase of block 0
-__device__ unsigned long long g_exact_prof[32];
+__device__ unsigned long long g_exact_prof[64];
 __device__ __forceinline__ long long prof_stamp() {  // a scheduling fence around the stamp
   unsigned long long t;
   __builtin_amdgcn_sched_barrier(0);
@@ -53,7 +53,11 @@ __device__ __forceinline__ long long prof_stamp() {  // a scheduling fence aroun
 #define PROF_T(v) const long long v = prof_stamp()
 #define PROF_ADD(i, a, b) \
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_exact_prof[i], (unsigned long long)((b) - (a)))
+// per wave (lane 0 of each wave of block 0): slot i + wave
+#define PROF_ADDW(i, a, b) \
+  if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) atomicAdd(&g_exact_prof[(i) + (threadIdx.x >> 6)], (unsigned long long)((b) - (a)))
 #else
+#define PROF_ADDW(i, a, b)
 #define PROF_T(v)
 #define PROF_ADD(i, a, b)
 #endif
@@ -886,6 +890,8 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
   sort_temps(tv, tw, sv, sw, tcap);
   // for the long replays (replay_key_fast): the exclusive prefix of the sorted |weights| after
   // the first record, the Add-order tempW at it (negated when a weight is not an integer)
+  // and for the batched replay (cpk) the same prefix as a u16 beside |w| as a u16, slot 0 carrying
+  // tempW -- or 0xffffffff when some weight is not an integer or tempW >= 2^16
   bool tint = true;
   double carry = 0.0;
   for (uint32_t b = 0; b < tcap; b += 64) {
@@ -899,14 +905,20 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
       v = (int)lane >= d ? dadd(v, o) : v;
     }
     if (t < tcap) {
+      const double ex = dadd(carry, dsub(v, w));
       x.csv[base + t] = sv[t];
       x.csw[base + t] = sw[t];
-      if (t) x.ctw[base + t] = dadd(carry, dsub(v, w));
+      if (t) x.ctw[base + t] = ex;
+      if (x.cpk && t) x.cpk[base + t] = (ex < 65536.0 ? (uint32_t)ex << 16 : 0xffff0000u) | (w < 65536.0 ? (uint32_t)w : 0xffffu);
     }
     carry = dadd(carry, rl_d(v, 63));
   }
   tint = __all(tint);
-  if (lane == 0) x.ctw[base] = tint ? tempW : -tempW;
+  if (lane == 0) {
+    x.ctw[base] = tint ? tempW : -tempW;
+    // (every weight is at least 1, so tempW < 2^16 bounds each weight and prefix below 2^16 too)
+    if (x.cpk) x.cpk[base] = tint && tempW < 65536.0 ? (uint32_t)tempW << 16 | (uint32_t)__builtin_fabs(sw[0]) : 0xffffffffu;
+  }
 }
 
 // ---- the replay: one 64-thread block (one wave) per key.  TPL = temps per lane of a chunk
@@ -1390,6 +1402,7 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
         p1 = kb[3];
         j += 4;
       }
+      if (sn == m) ksn1 = F.kk[m - 1];                  // the last centroid: its last element
       if (sn > e + 1) bad |= ksn1 - km1[r] > kLo;       // the last element before s' joins
       if (sn < m) bad |= !(ksn - km1[r] > kHi);         // s' starts
     }
@@ -1611,35 +1624,51 @@ __device__ __noinline__ MergeState merge_step_cold(const MergeParams mp, const L
 // ---- batched replay of consecutive pure chunks (the long replays' steady state).
 //
 // In a long key's steady state almost every merge keeps one structure: every old main centroid
-// starts a centroid and every temp joins the one before it (the prediction merge_fast verifies
-// one merge at a time).  While it holds the centroid count stays fixed and the centroids evolve
-// independently: centroid i's mean is a sequential Welford over the temps that land between it
-// and centroid i+1, merge after merge.  merge_batch takes up to kBB pure chunks at once, one lane
-// per centroid walking the chunks in order:
-//   assign   n[j][i] = temps of chunk j placed before main i, guessed from the means at the batch
-//            start (#temps with v <= mean_i: an upper bound search per chunk)
-//   prefix   the exact integer prefix P of main i in merge j (MP0 + the temps before it) and its
-//            weight, so q = P/T of every structure test (the chunk totals T are exact integers)
-//   decide   the merge-path decisions of merge j around main i, against the mean merge j really
-//            sees: main i before temp n[j][i] (mean < v), temp n[j][i]-1 before main i (v <= mean)
-//   Welford  the temps of the centroid, in Go's Centroid.Add order
-//   k bounds k is increasing, so min/max of each centroid's q bound all its k tests of the batch;
-//            a centroid whose bounds are not certain (outside 1 +- kBand) is tested merge by merge
-// and commits the merges before the first one any check rejects.  Those are exactly the
-// reference's merges (the checks of merge j hold given merges < j; by induction); the rejected
-// merge is then done alone by merge_step.  tools/study/batch_replay_sim.c restates this on the CPU:
-// bit-identical to the per-merge replay, 28 of 32 merges committed per batch on a 16M-sample key.
-// The chunk sorter's arrays are copied into an LDS ring (chunk c at slot c % kRing) by
-// global->LDS loads that need no registers: the chunks after the batch are in flight while it runs.
+// starts a centroid and every temp joins the one before it.  While it holds the centroid count
+// stays fixed and the centroids evolve independently: centroid i's mean is a sequential Welford
+// over the temps that land between it and centroid i+1, merge after merge.  merge_batch takes up
+// to kBB pure chunks at once, every phase against the means at the batch start:
+//   A  pos[j][p]  #means < v of every temp (all threads): the temp's column is pos - 1; pos 0
+//                 ("Z") places it before main 0, where it starts the first centroid and main 0
+//                 joins it (merging_digest.go:216: the first element always starts one)
+//   B  n[j][i]    #temps of chunk j before main i, filled from the pos runs; the list offsets
+//                 from a histogram of pos
+//   C1 column i's list: its temps in (chunk, position) order -- column 0's with its chunks' Z
+//                 temps, flagged -- one lane per column
+//   E  Welford along each list in Go's Centroid.Add order (a chunk's Z temps start a fresh
+//                 centroid that main 0 then joins), the mean after every entry recorded, and
+//                 the range [lo_i, hi_i] of the column's means over the batch
+//   C2 k bounds   the exact integer prefix P of main i in merge j and its weight, so q = P/T of
+//                 every structure test; k is increasing, so min/max of each column's q bound
+//                 all its k tests (on the waves E leaves idle, beside it)
+//   F  decisions  per temp: main c before it (mean_c < v) and it before main c+1 (v <=
+//                 mean_{c+1}) against the mean merge j saw -- checked exactly only for the temps
+//                 inside a column's range; with hi_i <= lo_{i+1} (means sorted at every merge)
+//                 these cover every main's merge-path decision
+//   G  the columns whose bounds are not certain (within 1 +- kBand) tested merge by merge, one
+//                 wave per column (lane = chunk, a wave scan for the prefixes)
+// and commits the merges before the first failure.  Those are exactly the reference's merges
+// (the checks of merge j hold given merges < j; by induction).  A decision failure (a temp the
+// moving mean passed) is not a structure change: the next batch starts at that merge with its
+// means fresh.  A structural failure (a centroid starts or fuses) sends that merge to
+// merge_step.  tools/study/batch2_sim.c restates these phases on the CPU and compares them bit
+// for bit with the per-merge replay (51.7 of 64 merges per batch on a 17M-sample key).
+// The chunk sorter's means and packed weights are copied into an LDS ring (chunk c at slot
+// c % kRing) by global->LDS loads that need no registers: later chunks land while a batch runs.
 #ifndef VN_BATCH_MERGES
-#define VN_BATCH_MERGES 32
+#define VN_BATCH_MERGES 64
 #endif
-constexpr uint32_t kBB = VN_BATCH_MERGES;  // merges per batch
-constexpr uint32_t kRing = kBB + 24;        // chunk slots in LDS
+constexpr uint32_t kBB = VN_BATCH_MERGES;  // merges per batch (list entries hold j < 64)
+static_assert(kBB <= 64, "list entries and the flagged-column scan hold a chunk index below 64");
+#ifndef VN_BATCH_RING
+#define VN_BATCH_RING 128
+#endif
+constexpr uint32_t kRing = VN_BATCH_RING;  // chunk slots in LDS
 constexpr uint32_t kTopExcl = 8;             // longest batched keys on CUs no other stream uses (st6)
 constexpr uint32_t kBM = 160;               // most centroids a batch takes (delta 100: ~135)
-constexpr uint32_t kBN = kBM + 1;           // lanes of a batch (one per centroid, one for the end)
+constexpr uint32_t kBN = kBM + 1;           // columns + the end
 constexpr uint32_t kBTmax = 48;             // largest temp buffer batched (delta <= ~110)
+constexpr uint32_t kBMinAvail = 32;         // chunks in the ring below which a batch waits for more
 #ifndef VN_BATCH_MIN_W
 #define VN_BATCH_MIN_W 8192.0
 #endif
@@ -1653,47 +1682,60 @@ constexpr uint32_t kBatchMinLen = VN_BATCH_MIN_LEN;
 
 typedef __attribute__((address_space(3))) uint8_t ldsu8;
 
+constexpr uint32_t kRS = kBB + 8;  // row stride (bytes) of the n and K tables: 18 dwords, so the
+                                   // rows of consecutive columns fall on different banks
+
 struct BatchLds {
-  ldsf64* rv;   // [kRing][tcap] the chunk sorter's csv: sorted temp means
-  ldsf64* rw;   // [kRing][tcap] csw: their signed weights (negative: an imported centroid)
-  ldsf64* rt;   // [kRing][tcap] ctw: [0] signed Add-order tempW (negative: a non-integer
-                //               weight), [p] the exclusive prefix of the sorted |weights|
-  ldsf64* bT;   // [kBB] total weight after chunk j of the batch
-  ldsf64* brT;  // [kBB] 1 / bT
-  ldsf64* kb;   // [3][kBN] k(min qe), k(max qb), k(min qb) per centroid
-  ldsf64* ms;   // [kBB * kBTmax] each centroid's means after each of its temps (its list's slice)
-  ldsu32* ch;   // [kBB][kBN] temps' weight before main i, chunks 0..j
-  ldsu32* ctl;  // [4] 0: first rejected merge; 1: #flagged; 2: usable chunks
-  ldsu16* flagged;  // [kBM] centroids whose bound tests are not certain
-  ldsu8* nT;        // [kBN][kBB] n[j][i], lane-major
-  ldsu8* bcnt;      // [kBB][kBTmax] #batch-start means < v of each temp
-  ldsu16* al;       // [kBB * kBTmax] each centroid's temps (ring offsets), in merge order; centroid
-                    //                i's slice starts at sum_j n[j][i]
+  ldsf64* rv;       // [kRing * tcap] the chunk sorter's csv: sorted temp means
+  ldsu32* rp;       // [kRing * tcap] cpk: exclusive prefix of the sorted weights << 16 | |w|;
+                    //                slot 0's prefix: the chunk's tempW (0xffffffff: not batchable)
+  ldsf64* bT;       // [kBB] total weight after chunk j of the batch
+  ldsf64* brT;      // [kBB] 1 / bT
+  ldsf64* lo;       // [kBM] each column's lowest mean over the batch
+  ldsf64* hi;       // [kBM] ... highest
+  ldsf64* kb;       // [3][kBN] k(min qe), k(max qb), k(min qb) per column
+  ldsf64* lv;       // [kBB * tcap] the lists: each column's temps' means in (chunk, position)
+                    //              order; the Welford pass overwrites each with the mean after it
+  ldsu32* lw;       // [kBB * tcap] ... their weights; overwritten with the weight gained so far
+  ldsu32* off;      // [kBN + 1] list start of column i (column 0 at 0, its Z temps included)
+  ldsu32* ctl;      // [8] 0: first decision failure; 1: #flagged; 2: usable chunks; 3: first
+                    //     structural failure; 4: no batch (means out of order, a list over 255,
+                    //     a value outside the fast division's range)
+  ldsu16* flagged;  // [kBM] columns whose bound tests are not certain
+  ldsu8* lj;        // [kBB * tcap] each list entry's chunk, 0x80: a Z temp (column 0)
+  ldsu8* pos;       // [kBB * tcap] #means < v of temp p of chunk j (j * tcap + p)
+  ldsu8* nT;        // [kBN][kRS] n[j][i] -- temps of chunk j before main i -- at i * kRS + j
+  ldsu8* kT;        // [kBM][kRS] K[j][i] -- column i's list entries from chunks before j
 };
 
 __host__ __device__ inline uint32_t batch_bytes(uint32_t tcap) {
-  return 24u * kRing * tcap + 16u * kBB + 24u * kBN + 8u * kBB * kBTmax + 4u * kBB * kBN + 16u + 2u * kBM + 16u +
-         kBN * kBB + kBB * kBTmax + 16u + 2u * kBB * kBTmax;
+  const uint32_t nl = kBB * tcap;
+  return 12u * kRing * tcap + 16u * kBB + 16u * kBM + 24u * kBN + 8u * nl + 4u * nl + 4u * (kBN + 1) + 32u +
+         2u * kBM + nl + nl + 16u + kBN * kRS + kBM * kRS + 16u;
 }
 __host__ __device__ inline uint32_t batch_offset(uint32_t capc, uint32_t tcap) {
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = capc + TP + 1 > 320u ? capc + TP + 1 : 320u;
   return (fast_offset(capc, tcap) + fast_extra_bytes(capc, TP, JW) + 15u) & ~15u;
 }
 __device__ __forceinline__ BatchLds batch_layout(char* p, uint32_t tcap) {
+  const uint32_t nl = kBB * tcap;
   BatchLds B;
   B.rv = (ldsf64*)p;
-  B.rw = B.rv + kRing * tcap;
-  B.rt = B.rw + kRing * tcap;
-  B.bT = B.rt + kRing * tcap;
+  B.bT = B.rv + kRing * tcap;
   B.brT = B.bT + kBB;
-  B.kb = B.brT + kBB;
-  B.ms = B.kb + 3 * kBN;
-  B.ch = (ldsu32*)(B.ms + kBB * kBTmax);
-  B.ctl = B.ch + kBB * kBN;
-  B.flagged = (ldsu16*)(B.ctl + 4);
-  B.nT = (ldsu8*)(((uintptr_t)(B.flagged + kBM) + 15u) & ~(uintptr_t)15u);
-  B.bcnt = B.nT + kBN * kBB;
-  B.al = (ldsu16*)(((uintptr_t)(B.bcnt + kBB * kBTmax) + 15u) & ~(uintptr_t)15u);
+  B.lo = B.brT + kBB;
+  B.hi = B.lo + kBM;
+  B.kb = B.hi + kBM;
+  B.lv = B.kb + 3 * kBN;
+  B.rp = (ldsu32*)(B.lv + nl);
+  B.lw = B.rp + kRing * tcap;
+  B.off = B.lw + nl;
+  B.ctl = B.off + (kBN + 1);
+  B.flagged = (ldsu16*)(B.ctl + 8);
+  B.lj = (ldsu8*)(B.flagged + kBM);
+  B.pos = B.lj + nl;
+  B.nT = (ldsu8*)(((uintptr_t)(B.pos + nl) + 15u) & ~(uintptr_t)15u);
+  B.kT = B.nT + kBN * kRS;
   return B;
 }
 
@@ -1703,81 +1745,95 @@ __device__ __forceinline__ double k_close(double delta, double q) {
 __device__ __forceinline__ void lds_min(ldsu32* p, uint32_t v) { __atomic_fetch_min(p, v, __ATOMIC_RELAXED); }
 __device__ __forceinline__ uint32_t lds_inc(ldsu32* p) { return __atomic_fetch_add(p, 1u, __ATOMIC_RELAXED); }
 
-// n doubles from global src into LDS dst by global->LDS dword loads: each wave instruction moves
+// n dwords from global src into LDS dst by global->LDS dword loads: each wave instruction moves
 // 64 dwords (the destination is wave-uniform, lane l its dword l).  Completion: vmcnt.
 template <int NW>
-__device__ __forceinline__ void dma_doubles(ldsf64* dst, const double* __restrict__ src, uint32_t n) {
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nd = 2 * n;
-  const uint32_t* s = (const uint32_t*)src;
-  ldsu32* d = (ldsu32*)dst;
+__device__ __forceinline__ void dma_dwords(ldsu32* d, const uint32_t* __restrict__ s, uint32_t nd) {
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (uint32_t q = wv; 64 * q < nd; q += NW) {
     const uint32_t k = 64 * q + lane;
     if (k < nd) __builtin_amdgcn_global_load_lds(s + k, (__attribute__((address_space(3))) void*)(d + 64 * q), 4, 0, 0);
   }
 }
-// chunks [x, y) (y - x <= kRing) of the chunk sorter's arrays into their ring slots
+// chunks [x, y) (y - x <= kRing) of the chunk sorter's means and packed weights into their slots
 template <int NW>
-__device__ __forceinline__ void ring_fill(const BatchLds B, const double* gv, const double* gw, const double* gt,
-                                          uint32_t x, uint32_t y, uint32_t tcap) {
+__device__ __forceinline__ void ring_fill(const BatchLds B, const double* gv, const uint32_t* gp, uint32_t x,
+                                          uint32_t y, uint32_t tcap) {
   const uint32_t s0 = x % kRing, n = y - x, n1 = min(n, kRing - s0);
   const uint64_t g0 = (uint64_t)x * tcap;
-  dma_doubles<NW>(B.rv + s0 * tcap, gv + g0, n1 * tcap);
-  dma_doubles<NW>(B.rw + s0 * tcap, gw + g0, n1 * tcap);
-  dma_doubles<NW>(B.rt + s0 * tcap, gt + g0, n1 * tcap);
+  dma_dwords<NW>((ldsu32*)(B.rv + s0 * tcap), (const uint32_t*)(gv + g0), 2 * n1 * tcap);
+  dma_dwords<NW>(B.rp + s0 * tcap, gp + g0, n1 * tcap);
   if (n > n1) {
     const uint64_t g1 = (uint64_t)(x + n1) * tcap;
-    dma_doubles<NW>(B.rv, gv + g1, (n - n1) * tcap);
-    dma_doubles<NW>(B.rw, gw + g1, (n - n1) * tcap);
-    dma_doubles<NW>(B.rt, gt + g1, (n - n1) * tcap);
+    dma_dwords<NW>((ldsu32*)B.rv, (const uint32_t*)(gv + g1), 2 * (n - n1) * tcap);
+    dma_dwords<NW>(B.rp, gp + g1, (n - n1) * tcap);
   }
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Merges chunks c .. c+b-1 (in the ring) as far as the checks allow.  Returns the merges
-// committed (0..b): L.mm/L.mw/F.mp/mainW then hold the digest after them.
+struct BatchResult {
+  uint32_t js;      // merges committed
+  bool structural;  // merge js failed a structure test (it runs alone); else the next batch starts there
+};
+
+// |x| is 0 or within [2^-400, 2^400]: the Welford division of the batch then never needs
+// v_div_scale's rescaling (see merge_batch, E)
+__device__ __forceinline__ bool div_safe(double x) {
+  const double a = __builtin_fabs(x);
+  return a == 0.0 || (a >= 3.872591914849318e-121 && a <= 2.5822498780869086e120);
+}
+
+// Merges chunks c .. c+b-1 (in the ring) as far as the checks allow: L.mm/L.mw/F.mp/mainW then
+// hold the digest after the committed merges.  Every phase is written for latency at one wave
+// per SIMD: a thread's independent LDS loads issue together and are waited for once.
 template <int NW>
-__device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L, const FastLds F, const BatchLds B,
-                                                const uint32_t nm_in, double& mainW, const uint32_t c_in, uint32_t b,
-                                                const uint32_t tcap) {
+__device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds L, const FastLds F, const BatchLds B,
+                                                   const uint32_t nm_in, double& mainW, const uint32_t c_in,
+                                                   uint32_t b, const uint32_t tcap) {
   // (wave-uniform values in scalar registers: every chunk address below is then scalar math)
-#ifdef VN_NO_RFL
-  const uint32_t nm = nm_in, c = c_in;
-#else
   const uint32_t nm = __builtin_amdgcn_readfirstlane(nm_in), c = __builtin_amdgcn_readfirstlane(c_in);
-#endif
   constexpr uint32_t NT = 64 * NW;
   constexpr double kHi = 1.0 + kBand, kLo = 1.0 - kBand;
-  static_assert(NT >= kBN, "one lane per centroid");
+  constexpr uint32_t kA = (kBB * kBTmax + NT - 1) / NT;  // temps per thread (all threads)
+  static_assert(NW == 4, "column lanes on waves 0-2, bounds on waves 2-3");
+  static_assert(kBM <= 192 && kBM >= 128, "one lane of waves 0-2 per column; wave 3 takes columns 64..127");
+  static_assert(kBB % 8 == 0 && kRS % 8 == 0, "rows are read and written as 8-byte words");
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const uint32_t cr = c % kRing;
-  auto slot = [&](uint32_t j) {  // ring offset of the batch's chunk j
+  auto sbase = [&](uint32_t j) {  // ring offset of the batch's chunk j
     const uint32_t s = cr + j;
     return (s >= kRing ? s - kRing : s) * tcap;
   };
+  auto tw_of = [&](uint32_t j, uint32_t n) -> uint32_t {  // chunk j's sorted weight before temp n
+    const uint32_t v = B.rp[sbase(j) + (n >= tcap ? 0u : n)] >> 16;
+    return n == 0 ? 0u : v;  // (n = tcap: slot 0 holds tempW)
+  };
   PROF_T(b0);
-  // ---- totals: the usable chunks are the leading ones with integer weights, T <= 2^40 and the
-  // batch's temp weight < 2^32 (the ch table)
+  // ---- totals: the usable chunks are the leading batchable ones with T <= 2^40 (every prefix
+  // below is then an exact u32 / f64 integer: a chunk's tempW < 2^16, the batch's < 2^22)
   if (wv == 0) {
-    const double tws = lane < b ? B.rt[slot(lane)] : -1.0;
-    bool ok = lane < b && tws >= 0.0;
-    double v = ok ? tws : 0.0;
+    const uint32_t tw0 = B.rp[sbase(min(lane, b - 1))], tw = lane < b ? tw0 : 0xffffffffu;
+    bool ok = lane < b && tw != 0xffffffffu;
+    double v = ok ? (double)(tw >> 16) : 0.0;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const double o = __shfl_up(v, d, 64);
       v = (int)lane >= d ? dadd(v, o) : v;
     }
     const double T = dadd(mainW, v);
-    ok = ok && T <= 1099511627776.0 && v < 4294967296.0;
+    ok = ok && T <= 1099511627776.0;
     const uint64_t bad = __ballot(!ok);
-    const uint32_t nb = bad ? (uint32_t)__builtin_ctzll(bad) : 64u;
+    const uint32_t nb = min(bad ? (uint32_t)__builtin_ctzll(bad) : 64u, b);
     if (lane < b) {
       B.bT[lane] = T;
       B.brT[lane] = ddiv(1.0, T);
     }
     if (lane == 0) {
-      B.ctl[0] = min(nb, b);
+      B.ctl[0] = nb;
       B.ctl[1] = 0u;
-      B.ctl[2] = min(nb, b);
+      B.ctl[2] = nb;
+      B.ctl[3] = nb;
+      B.ctl[4] = 0u;
     }
   }
   fast_sync<NW>();
@@ -1785,298 +1841,454 @@ __device__ __forceinline__ uint32_t merge_batch(const double delta, const Lds L,
   b = __builtin_amdgcn_readfirstlane(B.ctl[2]);
   if (b < 2) {
     fast_sync<NW>();
-    return 0u;
+    return BatchResult{0u, true};
   }
-  // ---- assign: lane i, every chunk: n[j][i] = #temps with v <= mean_i (branch-free upper bound
-  // searches, every lane's 32 in step so each round's loads issue back to back; a wave with no
-  // centroid skips them), into nT (lane-major)
+  const uint32_t nt = b * tcap;
+  // ---- A: pos of every temp: lower-bound searches over the means, a thread's temps in step;
+  // the first three levels from seven pivots held in registers, the rest from LDS
+  uint32_t gj[kA], gp[kA], ps[kA];
+  double gv[kA];
   {
-    const uint32_t i = t;
-    const double mi = i < nm ? L.mm[i] : 0.0;
-    uint32_t ni[kBB];
+    const double p0 = L.mm[min(128u, nm) - 1], p1 = L.mm[min(64u, nm) - 1], p2 = L.mm[min(192u, nm) - 1];
+    const double p3 = L.mm[min(32u, nm) - 1], p4 = L.mm[min(96u, nm) - 1], p5 = L.mm[min(160u, nm) - 1],
+                 p6 = L.mm[min(224u, nm) - 1];
+    bool safe = true;
 #pragma unroll
-    for (uint32_t j = 0; j < kBB; j++) ni[j] = 0u;
-    if (wv * 64u <= nm) {
-#pragma unroll
-      for (uint32_t step = 32; step >= 1; step >>= 1) {  // (tcap <= 48 < 64)
-        double v[kBB];
-#pragma unroll
-        for (uint32_t j = 0; j < kBB; j++) v[j] = B.rv[slot(j) + min(ni[j] + step, tcap) - 1];
-#pragma unroll
-        for (uint32_t j = 0; j < kBB; j++) {
-          const uint32_t q = ni[j] + step;
-          ni[j] = ((q <= tcap) & (v[j] <= mi)) ? q : ni[j];
-        }
-      }
+    for (uint32_t u = 0; u < kA; u++) {
+      const uint32_t g = t + u * NT;
+      gj[u] = g / tcap;
+      gp[u] = g - gj[u] * tcap;
+      const double x = B.rv[sbase(min(gj[u], kBB - 1)) + gp[u]];  // (unconditional: see D)
+      gv[u] = g < nt ? x : 0.0;
+      safe &= div_safe(gv[u]);
     }
-    if (i <= nm) {
 #pragma unroll
-      for (uint32_t g = 0; g < kBB / 4; g++) {
-        uint32_t wd = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++) wd |= (i < nm ? ni[4 * g + u] : tcap) << (8 * u);
-        *(ldsu32*)(B.nT + i * kBB + 4 * g) = wd;
-      }
+    for (uint32_t u = 0; u < kA; u++) {
+      const double v = gv[u];
+      uint32_t l = (128u <= nm && p0 < v) ? 128u : 0u;
+      l = (l + 64u <= nm && (l ? p2 : p1) < v) ? l + 64u : l;
+      const double q = l >= 128u ? (l >= 192u ? p6 : p5) : (l >= 64u ? p4 : p3);
+      l = (l + 32u <= nm && q < v) ? l + 32u : l;
+      ps[u] = l;
     }
+#pragma unroll
+    for (uint32_t step = 16; step >= 1; step >>= 1) {
+      double mv[kA];
+#pragma unroll
+      for (uint32_t u = 0; u < kA; u++) mv[u] = L.mm[min(ps[u] + step, nm) - 1];
+#pragma unroll
+      for (uint32_t u = 0; u < kA; u++) ps[u] = (ps[u] + step <= nm && mv[u] < gv[u]) ? ps[u] + step : ps[u];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kA; u++)
+      if (t + u * NT < nt) B.pos[t + u * NT] = (uint8_t)ps[u];
+    if (t < nm) safe &= div_safe(L.mm[t]);
+    if ((t + 1 < nm && !(L.mm[t] <= L.mm[t + 1])) || !safe) B.ctl[4] = 1u;  // (t < 256: nm <= 160)
   }
   fast_sync<NW>();
   PROF_T(b2);
-  // ---- one lane per centroid (i = nm: the end, for the prefixes).  The chunk loops are unrolled
-  // (compile-time chunk indices: the lane's n bytes stay in registers) and load a group of chunks
-  // ahead; a rolled loop would copy its prefetched registers at the back edge and wait for them.
-  const uint32_t i = t;
-  const bool cen = i < nm, act = i <= nm;
-  const double m0 = cen ? L.mm[i] : 0.0;
-  uint32_t jf = b, mask = 0u, off = 0u, m = 0u;
-  uint32_t ra[kBB / 4], re[kBB / 4];  // n[j][i], n[j][i+1], four chunks per word
-#pragma unroll
-  for (uint32_t g = 0; g < kBB / 4; g++) ra[g] = re[g] = 0u;
-  auto bmask = [&](uint32_t g) {  // the bytes of word g that are chunks < b
-    const uint32_t v = b > 4 * g ? min(b - 4 * g, 4u) : 0u;
-    return v >= 4 ? 0xffffffffu : ((1u << (8 * v)) - 1u);
-  };
-  auto bsum = [](uint32_t x) {  // sum of the four bytes
-    x = (x & 0x00ff00ffu) + ((x >> 8) & 0x00ff00ffu);
-    return (x & 0xffffu) + (x >> 16);
-  };
-  if (act) {
-#pragma unroll
-    for (uint32_t g = 0; g < kBB / 4; g++) {
-      ra[g] = *(const ldsu32*)(B.nT + i * kBB + 4 * g);
-      re[g] = cen ? *(const ldsu32*)(B.nT + (i + 1) * kBB + 4 * g) : ra[g];
-      off += bsum(ra[g] & bmask(g));  // the lane's list: [sum_j n[j][i], sum_j n[j][i+1])
-      m += bsum(re[g] & bmask(g));
-    }
-    m -= off;
+  if (B.ctl[4]) {  // means out of order (the pos runs would not be monotone), or a value outside
+    fast_sync<NW>();  // the fast division's range: no batch
+    return BatchResult{0u, true};
   }
-  auto by = [&](const uint32_t(&w)[kBB / 4], uint32_t j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xffu; };
-  constexpr uint32_t kG = 4;  // chunks per load group (the decisions)
-#ifdef VN_PREFIX_ROLLED
-  // -- prefixes (exact integers, so q = P/T of every structure test): a rolled loop, the n bytes
-  // two chunks ahead, the prefixes they select one chunk ahead (A/B variant)
-  if (act) {
-    const ldsu8* const nra = B.nT + i * kBB;
-    const ldsu8* const nre = B.nT + (cen ? i + 1 : i) * kBB;
-    const double mp0 = F.mp[i];
-    double qbmin = 2.0, qbmax = -1.0, qemin = 2.0, C = 0.0, W = cen ? L.mw[i] : 0.0;
-    uint32_t aN = nra[0], eN = nre[0], aNN = nra[1], eNN = nre[1];
-    double sa = B.rt[slot(0) + min(aN, tcap - 1)], se = B.rt[slot(0) + min(eN, tcap - 1)];
-    double tw = B.rt[slot(0)], rT = B.brT[0];
-#pragma unroll 1
-    for (uint32_t j = 0; j < b; j++) {
-      const uint32_t a = aN, e = eN;
-      const double pa = sa, pe = se, twj = tw, rTj = rT;
-      const uint32_t jn = min(j + 1, kBB - 1), sn = slot(jn), jnn = min(j + 2, kBB - 1);
-      sa = B.rt[sn + min(aNN, tcap - 1)];
-      se = B.rt[sn + min(eNN, tcap - 1)];
-      tw = B.rt[sn];
-      rT = B.brT[jn];
-      aN = aNN;
-      eN = eNN;
-      aNN = nra[jnn];
-      eNN = nre[jnn];
-      const double s0 = a >= tcap ? twj : (a == 0 ? 0.0 : pa);  // chunk j's temp weight before main i
-      const double s1 = e >= tcap ? twj : (e == 0 ? 0.0 : pe);  // ... before main i + 1
-      C = dadd(C, s0);
-      B.ch[j * kBN + i] = (uint32_t)C;
-      const double P = dadd(mp0, C);
-      const double qb = P * rTj, qe = dadd(P, W) * rTj;
-      qbmin = __builtin_fmin(qbmin, qb);
-      qbmax = __builtin_fmax(qbmax, qb);
-      qemin = __builtin_fmin(qemin, qe);
-      W = dadd(W, dsub(s1, s0));  // (the end lane: e = a)
-      mask |= (e > a ? 1u : 0u) << j;
+  // ---- B: the n table from the pos runs: temp p of chunk j fills rows [pos_p, pos_{p+1}) of
+  // column j with p + 1 (p = 0 also rows [0, pos_0) with 0)
+  {
+    uint32_t c1[kA];
+#pragma unroll
+    for (uint32_t u = 0; u < kA; u++) {
+      const uint32_t g = t + u * NT;
+      const uint32_t x = B.pos[min(g + 1, nt - 1)];
+      c1[u] = g < nt && gp[u] + 1 < tcap ? x : nm + 1;
     }
-    B.kb[i] = k_close(delta, qemin);
-    B.kb[kBN + i] = k_close(delta, qbmax);
-    B.kb[2 * kBN + i] = k_close(delta, qbmin);
-  }
-#else
-  // -- prefixes (exact integers, so q = P/T of every structure test), unrolled over the chunks:
-  // the n bytes are in registers (compile-time chunk indices), so a group's loads all issue at
-  // once, a group ahead of its use.  (Bounds from the batch's ends alone were measured: a long
-  // key's centroids sit near their k-size limit, so they flagged 8 centroids per batch, not 1.)
-  if (act) {
-    const double mp0 = F.mp[i];
-    double qbmin = 2.0, qbmax = -1.0, qemin = 2.0, C = 0.0, W = cen ? L.mw[i] : 0.0;
-    constexpr uint32_t kP = 8;  // chunks per load group
-    double gsa[2][kP], gse[2][kP], gtw[2][kP], grT[2][kP];
 #pragma unroll
-    for (uint32_t g = 0; g <= kBB / kP; g++) {
-      if (g < kBB / kP) {
-#pragma unroll
-        for (uint32_t u = 0; u < kP; u++) {
-          const uint32_t j = kP * g + u, sl = slot(j);
-          gsa[g & 1][u] = B.rt[sl + min(by(ra, j), tcap - 1)];
-          gse[g & 1][u] = B.rt[sl + min(by(re, j), tcap - 1)];
-          gtw[g & 1][u] = B.rt[sl];
-          grT[g & 1][u] = B.brT[j];
-        }
-      }
-      if (g == 0) continue;
-      const uint32_t h = g - 1;
-#pragma unroll
-      for (uint32_t u = 0; u < kP; u++) {
-        const uint32_t j = kP * h + u, a = by(ra, j), e = by(re, j);
-        const bool in = j < b;
-        const double twj = gtw[h & 1][u], rTj = grT[h & 1][u];
-        const double s0 = in ? (a >= tcap ? twj : (a == 0 ? 0.0 : gsa[h & 1][u])) : 0.0;  // temps before main i
-        const double s1 = in ? (e >= tcap ? twj : (e == 0 ? 0.0 : gse[h & 1][u])) : 0.0;  // ... before main i+1
-        C = dadd(C, s0);
-        B.ch[j * kBN + i] = (uint32_t)C;  // (rows j >= b: unused)
-        const double P = dadd(mp0, C);
-        const double qb = P * rTj, qe = dadd(P, W) * rTj;
-        qbmin = in ? __builtin_fmin(qbmin, qb) : qbmin;
-        qbmax = in ? __builtin_fmax(qbmax, qb) : qbmax;
-        qemin = in ? __builtin_fmin(qemin, qe) : qemin;
-        W = dadd(W, dsub(s1, s0));
-        mask |= (in && e > a ? 1u : 0u) << j;
-      }
-    }
-    B.kb[i] = k_close(delta, __builtin_fmin(qemin, 1.0));  // (q <= 1: the reciprocal's rounding)
-    B.kb[kBN + i] = k_close(delta, __builtin_fmin(qbmax, 1.0));
-    B.kb[2 * kBN + i] = k_close(delta, __builtin_fmin(qbmin, 1.0));
-  }
-#endif
-  PROF_T(l1);
-  PROF_ADD(13, b2, l1);
-  // -- Welford over the lane's temps in order (Go's Centroid.Add): a cursor over the chunks that
-  // gave it temps (the mask); the mean after each temp into ms (the lane's slice: off + k).  The
-  // next temp's loads are in flight during each add.
-  if (cen && m) {
-    const ldsu8* const nra = B.nT + i * kBB;
-    const ldsu8* const nre = B.nT + (i + 1) * kBB;
-    ldsf64* const ms = B.ms + off;
-    double W = L.mw[i], mean = m0;
-    uint32_t jc = (uint32_t)__builtin_ctz(mask), pc = nra[jc], ec = nre[jc];
-    uint32_t sc = slot(jc);
-    double cv = B.rv[sc + pc], cw = B.rw[sc + pc];
-    for (uint32_t q = 0; q < m; q++) {
-      uint32_t jn = jc, pn = pc + 1, en = ec;
-      if (pn >= ec) {  // the next chunk with temps of this centroid
-        const uint64_t rest = (uint64_t)mask & ~((2ull << jc) - 1ull);
-        jn = rest ? (uint32_t)__builtin_ctzll(rest) : jc;
-        pn = rest ? nra[jn] : pc;
-        en = rest ? nre[jn] : ec;
-      }
-      const uint32_t sn = slot(jn);
-      const double nv = B.rv[sn + min(pn, tcap - 1)], nw = B.rw[sn + min(pn, tcap - 1)];
-      const double w = __builtin_fabs(cw);
-      W = dadd(W, w);
-      mean = dadd(mean, ddiv(dmul(dsub(cv, mean), w), W));
-      ms[q] = mean;
-      jc = jn;
-      pc = pn;
-      ec = en;
-      cv = nv;
-      cw = nw;
-    }
-  }
-  PROF_T(l2);
-  PROF_ADD(14, l1, l2);
-  // -- merge j's decisions around main i, with the mean merge j saw: main i before temp
-  // n[j][i] (mean < v), temp n[j][i] - 1 before main i (v <= mean).  Every chunk is checked;
-  // the first failure counts.
-  if (cen) {
-    const ldsf64* const ms = B.ms + off;
-    double gv1[2][kG], gv0[2][kG], gmb[2][kG];
-    uint32_t kload = 0;  // the lane's temps before chunk j (load side)
-#pragma unroll
-    for (uint32_t g = 0; g <= kBB / kG; g++) {
-      if (g < kBB / kG) {
-#pragma unroll
-        for (uint32_t u = 0; u < kG; u++) {
-          const uint32_t j = kG * g + u, a = by(ra, j), sl = slot(j);
-          gv1[g & 1][u] = B.rv[sl + min(a, tcap - 1)];
-          gv0[g & 1][u] = B.rv[sl + (a ? a - 1 : 0)];
-          gmb[g & 1][u] = ms[kload ? kload - 1 : 0];
-          kload += j < b ? by(re, j) - a : 0u;
-        }
-      }
-      if (g == 0) continue;
-      const uint32_t h = g - 1;
-#pragma unroll
-      for (uint32_t u = 0; u < kG; u++) {
-        const uint32_t j = kG * h + u, a = by(ra, j);
-        const double mb = (mask & ((1u << j) - 1u)) ? gmb[h & 1][u] : m0;
-        const double v1 = gv1[h & 1][u], v0 = gv0[h & 1][u];
-        const bool ok = ((a >= tcap) | (mb < v1)) & ((a == 0) | ((i > 0) & (v0 <= mb)));
-        jf = (j < b && !ok && jf == b) ? j : jf;
+    for (uint32_t u = 0; u < kA; u++) {
+      if (t + u * NT < nt) {
+        ldsu8* const col = B.nT + gj[u];
+        if (gp[u] == 0)
+          for (uint32_t r = 0; r < ps[u]; r++) col[r * kRS] = 0;
+        for (uint32_t r = ps[u]; r < c1[u]; r++) col[r * kRS] = (uint8_t)(gp[u] + 1);
       }
     }
   }
-  PROF_T(l3);
-  PROF_ADD(15, l2, l3);
-  PROF_ADD(22, 0, (long long)m);
-  if (jf < b) lds_min(&B.ctl[0], jf);
   fast_sync<NW>();
   PROF_T(b3);
-  // ---- bound tests: main i starts (i >= 1) and its temps join, in every merge
-  if (cen) {
+  // ---- C.  A column lane holds rows n[.][i] and n[.][i+1] as words (chunks j < b count):
+  // the list offset off_i = sum_j n[j][i] (the temps of the columns before it, Z included;
+  // column 0 at 0), the K row (a prefix over the chunks of its per-chunk counts), and the k
+  // bounds (C2: waves 2 and 3, beside the others)
+  constexpr uint32_t kW = kBB / 4;  // u32 words of a row
+  auto load_row = [&](const ldsu8* tab, uint32_t r, uint32_t (&w)[kW]) {
+    const ldsu64* const rw = (const ldsu64*)(tab + r * kRS);
+#pragma unroll
+    for (uint32_t q = 0; q < kW / 2; q++) {
+      const uint64_t x = rw[q];
+      w[2 * q] = (uint32_t)x;
+      w[2 * q + 1] = (uint32_t)(x >> 32);
+    }
+  };
+  auto byte_at = [](const uint32_t (&w)[kW], uint32_t j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xffu; };
+  auto wmask = [&](uint32_t q) {  // the bytes of word q that are chunks < b
+    const uint32_t v = b > 4 * q ? min(b - 4 * q, 4u) : 0u;
+    return v >= 4 ? 0xffffffffu : ((1u << (8 * v)) - 1u);
+  };
+  // C2: k bounds of column ci (min / max over the batch of q = P / T from exact integer prefixes)
+  auto c2_column = [&](uint32_t ci, const uint32_t (&ra)[kW], const uint32_t (&re)[kW]) {
+    const double mp0 = F.mp[ci], mpw = dadd(F.mp[ci], L.mw[ci]);
+    double qbmin = 2.0, qbmax = -1.0, qemin = 2.0;
+    uint32_t C = 0, X = 0;  // sum of s0 (temps before main ci), of s1 (before main ci + 1)
+    constexpr uint32_t kP = 16;
+#pragma unroll
+    for (uint32_t j0 = 0; j0 < kBB; j0 += kP) {
+      if (j0 >= b) break;
+      uint32_t sa[kP], se[kP];
+      double rT[kP];
+#pragma unroll
+      for (uint32_t u = 0; u < kP; u++) {
+        const uint32_t j = min(j0 + u, b - 1);
+        sa[u] = tw_of(j, byte_at(ra, j0 + u));
+        se[u] = tw_of(j, byte_at(re, j0 + u));
+        rT[u] = B.brT[j];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kP; u++) {
+        if (j0 + u < b) {
+          C += sa[u];
+          // P = mp0 + C; qe = (P + W) / T with W = w0 + the gain before chunk j = w0 + X - (C - sa)
+          const double qe = dadd(mpw, (double)(X + sa[u])) * rT[u];
+          qemin = __builtin_fmin(qemin, qe);
+          const double qb = dadd(mp0, (double)C) * rT[u];
+          qbmin = __builtin_fmin(qbmin, qb);
+          qbmax = __builtin_fmax(qbmax, qb);
+          X += se[u];
+        }
+      }
+    }
+    if (!ci) qbmin = qbmax = 0.0;  // (column 0 starts at q = 0: with Z temps or main 0 itself)
+    B.kb[ci] = k_close(delta, __builtin_fmin(qemin, 1.0));  // (q <= 1: the reciprocal's rounding)
+    B.kb[kBN + ci] = k_close(delta, __builtin_fmin(qbmax, 1.0));
+    B.kb[2 * kBN + ci] = k_close(delta, __builtin_fmin(qbmin, 1.0));
+  };
+  const uint32_t i = t;
+  uint32_t ra[kW], re[kW];
+  if (wv < 3) {
+    if (i < nm) {
+      load_row(B.nT, i, ra);
+      load_row(B.nT, i + 1, re);
+      uint32_t o = 0, carry = 0;
+      uint64_t kw[kW / 2];
+#pragma unroll
+      for (uint32_t q = 0; q < kW; q++) {
+        const uint32_t mk = wmask(q);
+        const uint32_t a = i == 0 ? 0u : ra[q] & mk, e = re[q] & mk;
+        uint32_t x = a;
+        x = (x & 0x00ff00ffu) + ((x >> 8) & 0x00ff00ffu);
+        o += (x & 0xffffu) + (x >> 16);
+        // per-chunk counts e - a (bytewise, e >= a: no borrows), their bytewise prefix (x * 0x01010101
+        // while sums stay below 256; the column's total is checked below)
+        const uint32_t cnt = e - a, incl = cnt * 0x01010101u;
+        const uint32_t ex = incl - cnt + carry * 0x01010101u;
+        carry += incl >> 24;
+        if (q & 1) kw[q >> 1] |= (uint64_t)ex << 32;
+        else kw[q >> 1] = ex;
+      }
+      if (carry > 255u) B.ctl[4] = 1u;  // (a list over 255 entries: no batch)
+      B.off[i] = o;
+      if (i + 1 == nm) B.off[nm] = o + carry;
+      ldsu64* const kr = (ldsu64*)(B.kT + i * kRS);
+#pragma unroll
+      for (uint32_t q = 0; q < kW / 2; q++) kr[q] = kw[q];
+    }
+  }
+  PROF_T(cw1);
+  // C2 on waves 2 (columns 0..63, then its own 128.. once its lists are done) and 3 (64..127)
+  if (wv == 3) {
+    const uint32_t ci = 64 + lane;
+    if (ci < nm) {
+      load_row(B.nT, ci, ra);
+      load_row(B.nT, ci + 1, re);
+      c2_column(ci, ra, re);
+    }
+    if (lane == 0) {  // the end
+      B.kb[kBN + nm] = k_close(delta, 1.0);
+      B.kb[2 * kBN + nm] = k_close(delta, 1.0);
+    }
+  } else if (wv == 2) {
+    if (lane < nm) {
+      uint32_t ra2[kW], re2[kW];
+      load_row(B.nT, lane, ra2);
+      load_row(B.nT, lane + 1, re2);
+      c2_column(lane, ra2, re2);
+    }
+  }
+  PROF_T(cw2);
+  PROF_ADDW(40, cw1, cw2);
+  fast_sync<NW>();
+  PROF_T(b4);
+  if (B.ctl[4]) {
+    fast_sync<NW>();
+    return BatchResult{0u, true};
+  }
+  // ---- D: every temp into its column's list at off_c + K[j][c] + its place in the chunk's run
+  // (column 0: Z temps and main 0's own temps, p itself), with its mean and weight
+  {
+    // (every load unconditional, at a clamped address, and selected afterwards: a conditional load
+    // compiles to a branch whose join waits for all LDS traffic in flight)
+    uint32_t kk[kA], nn[kA], wq[kA], oo[kA];
+#pragma unroll
+    for (uint32_t u = 0; u < kA; u++) {
+      const uint32_t cc = ps[u] ? min(ps[u] - 1, nm - 1) : 0u, jc = min(gj[u], kBB - 1);
+      kk[u] = B.kT[cc * kRS + jc];
+      const uint32_t n0 = B.nT[cc * kRS + jc];
+      nn[u] = cc ? n0 : 0u;
+      oo[u] = B.off[cc];
+      wq[u] = B.rp[sbase(jc) + gp[u]] & 0xffffu;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kA; u++) {
+      if (t + u * NT < nt) {
+        const uint32_t x = oo[u] + kk[u] + gp[u] - nn[u];
+        B.lv[x] = gv[u];
+        B.lw[x] = wq[u];
+        B.lj[x] = (uint8_t)(gj[u] | (ps[u] == 0 ? 0x80u : 0u));
+      }
+    }
+  }
+  fast_sync<NW>();
+  PROF_T(b5);
+  // ---- E: Welford along each list (waves 0-2, lane = column), two blocks of four entries in
+  // flight.  The division ((v - mean) * w) / W is the hardware's own sequence -- v_rcp and two
+  // Newton steps on W, q0 = t * y, r = fma(-W, q0, t), q = fma(r, y, q0), v_div_fixup -- without
+  // v_div_scale, which rescales nothing for these operands: W is an integer in [1, 2^40], every
+  // value and mean 0 or of magnitude [2^-400, 2^400] (checked in A), so t = 0 or 2^-505 <= |t| <=
+  // 2^425 (the quotient exponent stays far from the range where the hardware rescales).  The W
+  // chain and the reciprocals do not depend on the means, so they are computed ahead of them.
+  // A block holding a Z entry (column 0 only) takes the exact Z walk: the chunk's Z temps start
+  // a fresh centroid (main 0, the column so far, waiting) and main 0 joins it after the chunk's
+  // last Z temp.
+  PROF_T(e0);
+  if (wv < 3) {
+    const bool col = i < nm;
+    const uint32_t ic = min(i, nm - 1), o0 = B.off[ic], o1 = B.off[ic + 1];
+    const double mm0 = L.mm[ic], mw0 = L.mw[ic];
+    const uint32_t o = col ? o0 : 0u, m = col ? o1 - o0 : 0u;
+    double mean = col ? mm0 : 0.0, W = col ? mw0 : 1.0, lo = mean, hi = mean, sm = 0.0, sw = 0.0;
+    uint32_t gain = 0, prev = 0;
+    bool tiny = false;  // a numerator near the hardware's rescaling range (then no batch)
+    uint32_t mmax = m;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) mmax = max(mmax, (uint32_t)__shfl_xor((int)mmax, d, 64));
+    mmax = __builtin_amdgcn_readfirstlane(mmax);
+    auto ld = [&](uint32_t q, double (&v)[4], uint32_t (&w)[4]) {
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        const uint32_t x = o + min(q + u, m ? m - 1 : 0u);
+        v[u] = B.lv[x];
+        w[u] = B.lw[x];
+      }
+    };
+    double v0[4], v1[4];
+    uint32_t w0[4], w1[4];
+    ld(0, v0, w0);
+#pragma unroll 1
+    for (uint32_t q = 0; q < mmax; q += 4) {
+      ld(q + 4, v1, w1);
+      bool zb = false;
+      if (i == 0) {  // (only column 0's list holds Z temps)
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+          const uint32_t x = B.lj[o + min(q + u, m ? m - 1 : 0u)];
+          zb |= q + u < m && (x & 0x80u);
+        }
+      }
+      if (__builtin_expect(__any(zb), 0)) {
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+          if (q + u < m) {
+            const uint32_t e = B.lj[o + q + u], nx = q + u + 1 < m ? B.lj[o + q + u + 1] : 0u;
+            const bool z = (e & 0x80u) != 0u;
+            const bool zstart = z && (q + u == 0 || !(prev & 0x80u) || ((prev ^ e) & 63u));
+            const bool zend = z && (!(nx & 0x80u) || ((nx ^ e) & 63u));
+            const double w = (double)w0[u];
+            if (zstart) {
+              sm = mean;
+              sw = W;
+              mean = v0[u];
+              W = w;
+            } else {
+              W = dadd(W, w);
+              mean = dadd(mean, ddiv(dmul(dsub(v0[u], mean), w), W));
+            }
+            if (zend) {
+              W = dadd(W, sw);
+              mean = dadd(mean, ddiv(dmul(dsub(sm, mean), sw), W));
+            }
+            if (!z || zend) {
+              lo = __builtin_fmin(lo, mean);
+              hi = __builtin_fmax(hi, mean);
+            }
+            gain += w0[u];
+            B.lv[o + q + u] = mean;
+            B.lw[o + q + u] = gain;
+            prev = e;
+          }
+        }
+      } else {
+        double Wn[4], y[4];
+        bool in[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {  // the W chain and the reciprocals, ahead of the means
+          in[u] = q + u < m;
+          Wn[u] = dadd(u ? Wn[u - 1] : W, in[u] ? (double)w0[u] : 0.0);
+          const double r0 = __builtin_amdgcn_rcp(Wn[u]);
+          const double e0_ = __builtin_fma(-Wn[u], r0, 1.0);
+          const double r1 = __builtin_fma(r0, e0_, r0);
+          const double e1_ = __builtin_fma(-Wn[u], r1, 1.0);
+          y[u] = __builtin_fma(r1, e1_, r1);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+          const double tq = dmul(dsub(v0[u], mean), (double)w0[u]);
+          tiny |= tq != 0.0 && __builtin_fabs(tq) < 1e-250;
+          const double q0 = dmul(tq, y[u]);
+          const double rr = __builtin_fma(-Wn[u], q0, tq);
+          const double qq = __builtin_amdgcn_div_fixup(__builtin_fma(rr, y[u], q0), Wn[u], tq);
+          const double m2 = dadd(mean, qq);
+          mean = in[u] ? m2 : mean;
+          gain += in[u] ? w0[u] : 0u;
+          if (in[u]) {
+            B.lv[o + q + u] = mean;
+            B.lw[o + q + u] = gain;
+          }
+          lo = __builtin_fmin(lo, mean);
+          hi = __builtin_fmax(hi, mean);
+        }
+        W = Wn[3];
+        prev = 0u;  // (no Z entry in the block: the next Z entry starts a centroid)
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        v0[u] = v1[u];
+        w0[u] = w1[u];
+      }
+    }
+    if (col) {
+      B.lo[i] = lo;
+      B.hi[i] = hi;
+    }
+    if (tiny) B.ctl[4] = 1u;
+    PROF_T(e1);
+    PROF_ADD(14, e0, e1);
+    PROF_ADDW(36, e0, e1);
+  }
+  // C2 of wave 2's own columns (128..), after its (short, tail) lists
+  if (wv == 2 && i < nm) c2_column(i, ra, re);
+  fast_sync<NW>();
+  PROF_T(b6);
+  // ---- F: decisions per temp against the columns' mean ranges (the exact mean merge j saw
+  // only for a temp inside a range); bound tests per column
+  auto mean_before = [&](uint32_t ci, uint32_t j) {
+    const uint32_t kq = B.kT[ci * kRS + j];
+    return kq ? B.lv[B.off[ci] + kq - 1] : L.mm[ci];
+  };
+  {
+    double hl[kA], lr[kA];
+#pragma unroll
+    for (uint32_t u = 0; u < kA; u++) {
+      hl[u] = B.hi[ps[u] >= 1 ? ps[u] - 1 : 0];
+      lr[u] = B.lo[min(ps[u], nm - 1)];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kA; u++) {
+      const bool in = t + u * NT < nt;
+      const bool rl = in && ps[u] >= 1 && gv[u] <= hl[u], rr = in && ps[u] < nm && gv[u] > lr[u];
+      if (rl || rr) {  // (rare) inside a column's range: the exact order against the mean merge j saw
+        bool bad = false;
+        if (rl) bad = !(mean_before(ps[u] - 1, gj[u]) < gv[u]);     // main ps-1 before it
+        if (rr) bad = bad || !(gv[u] <= mean_before(ps[u], gj[u]));  // it before main ps
+        if (bad) lds_min(&B.ctl[0], gj[u]);
+      }
+    }
+  }
+  if (i < nm) {
+    if (i + 1 < nm && !(B.hi[i] <= B.lo[i + 1])) B.ctl[4] = 1u;
     bool sure = true;
-    if (i >= 1) sure = B.kb[i] - B.kb[kBN + i - 1] > kHi;
-    sure = sure && B.kb[kBN + i + 1] - B.kb[2 * kBN + i] < kLo;
+    if (i >= 1) sure = B.kb[i] - B.kb[kBN + i - 1] > kHi;         // main i starts
+    sure = sure && B.kb[kBN + i + 1] - B.kb[2 * kBN + i] < kLo;  // its temps join
     if (!sure) B.flagged[lds_inc(&B.ctl[1])] = (uint16_t)i;
   }
   fast_sync<NW>();
-  PROF_T(b4);
+  PROF_T(b7);
+  // ---- G: exact tests of the flagged columns, one wave per column, lane = chunk
   const uint32_t nflag = __builtin_amdgcn_readfirstlane(B.ctl[1]);
-  if (nflag) {
-    // exact tests of the flagged centroids, merge by merge (before the first decision reject)
-    const uint32_t jp = __builtin_amdgcn_readfirstlane(B.ctl[0]);
-    for (uint32_t f = t; f < nflag * jp; f += NT) {
-      const uint32_t q = f / jp, j = f - q * jp, ic = B.flagged[q];
-      const double rT = B.brT[j];
-      const double Pi = dadd(F.mp[ic], (double)B.ch[j * kBN + ic]);
-      const double Pn = dadd(F.mp[ic + 1], (double)B.ch[j * kBN + ic + 1]);
-      const double Wi = j ? dadd(L.mw[ic], (double)(B.ch[(j - 1) * kBN + ic + 1] - B.ch[(j - 1) * kBN + ic]))
-                          : L.mw[ic];
-      bool ok = true;
-      if (ic >= 1) {
-        const double Pp = dadd(F.mp[ic - 1], (double)B.ch[j * kBN + ic - 1]);
-        ok = k_close(delta, dadd(Pi, Wi) * rT) - k_close(delta, Pp * rT) > kHi;
-      }
-      const uint32_t na_ = B.nT[ic * kBB + j], nb_ = B.nT[(ic + 1) * kBB + j];
-      if (nb_ > na_) ok = ok && k_close(delta, Pn * rT) - k_close(delta, Pi * rT) < kLo;
-      if (!ok) lds_min(&B.ctl[0], j);
-    }
-    fast_sync<NW>();
-  }
-  PROF_T(b5);
-  const uint32_t js = __builtin_amdgcn_readfirstlane(B.ctl[0]);
-  if (js > 0) {
-    // commit merges 0..js-1: means (after the last chunk before js that gave temps), weights,
-    // the main prefix
-    if (act) {
-      const uint32_t c0 = B.ch[(js - 1) * kBN + i];
-      if (cen) {
-        const uint32_t c1 = B.ch[(js - 1) * kBN + i + 1];
-        uint32_t kc = 0;  // the lane's temps in chunks < js
+  for (uint32_t f = wv; f < nflag; f += NW) {
+    const uint32_t ic = B.flagged[f], j = lane;
+    const bool in = j < b;
+    const uint32_t jj = in ? j : 0u;
+    const uint32_t nP = ic >= 1 ? B.nT[(ic - 1) * kRS + jj] : 0u, nI = ic >= 1 ? B.nT[ic * kRS + jj] : 0u,
+                   nN = B.nT[(ic + 1) * kRS + jj];
+    const uint32_t xP = in ? tw_of(jj, nP) : 0u, xI = in ? tw_of(jj, nI) : 0u, xN = in ? tw_of(jj, nN) : 0u;
+    uint32_t cP = xP, cI = xI, cN = xN;
 #pragma unroll
-        for (uint32_t g = 0; g < kBB / 4; g++) {
-          const uint32_t v = js > 4 * g ? min(js - 4 * g, 4u) : 0u, bm = v >= 4 ? 0xffffffffu : ((1u << (8 * v)) - 1u);
-          kc += bsum(re[g] & bm) - bsum(ra[g] & bm);
-        }
-        L.mm[i] = kc ? B.ms[off + kc - 1] : m0;
-        L.mw[i] = dadd(L.mw[i], (double)(c1 - c0));
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t a = __shfl_up(cP, d, 64), bI = __shfl_up(cI, d, 64), e = __shfl_up(cN, d, 64);
+      if ((int)lane >= d) {
+        cP += a;
+        cI += bI;
+        cN += e;
       }
-      F.mp[i] = dadd(F.mp[i], (double)c0);  // (i = nm: the new total)
     }
-    mainW = B.bT[js - 1];
+    const double T = B.bT[jj];
+    const double Pi = dadd(F.mp[ic], (double)cI), Pn = dadd(F.mp[ic + 1], (double)cN);
+    const double Wi = dadd(L.mw[ic], (double)((cN - xN) - (cI - xI)));  // weight before merge j
+    bool ok = true;
+    if (ic >= 1) {
+      const double qp = ic == 1 ? 0.0 : ddiv(dadd(F.mp[ic - 1], (double)cP), T);
+      ok = dsub(index_estimate(delta, ddiv(dadd(Pi, Wi), T)), index_estimate(delta, qp)) > 1.0;
+    }
+    if (nN > nI)
+      ok = ok && !(dsub(index_estimate(delta, ddiv(Pn, T)), index_estimate(delta, ic == 0 ? 0.0 : ddiv(Pi, T))) > 1.0);
+    const uint64_t fail = __ballot(in && !ok);
+    if (fail && lane == 0) lds_min(&B.ctl[3], (uint32_t)__builtin_ctzll(fail));
   }
   fast_sync<NW>();
-  PROF_T(b6);
+  PROF_T(b8);
+  uint32_t jd = __builtin_amdgcn_readfirstlane(B.ctl[0]);
+  const uint32_t jst = __builtin_amdgcn_readfirstlane(B.ctl[3]);
+  if (B.ctl[4]) jd = 0;  // (means out of order somewhere: no batch)
+  const uint32_t js = min(jd, jst);
+  const bool structural = jst <= jd || js == 0;
+  if (js > 0) {
+    // commit merges 0..js-1: each column's mean and weight after its last entry before js
+    if (i < nm) {
+      const uint32_t o = B.off[i];
+      const uint32_t kq = js < b ? (uint32_t)B.kT[i * kRS + js] : B.off[i + 1] - o;
+      if (kq) {
+        L.mm[i] = B.lv[o + kq - 1];
+        L.mw[i] = dadd(L.mw[i], (double)B.lw[o + kq - 1]);
+      }
+    }
+    mainW = B.bT[js - 1];
+    fast_sync<NW>();
+    if (wv == 0) prefix_main_w0(L, F, nm, mainW);
+  }
+  fast_sync<NW>();
+  PROF_T(b9);
   PROF_ADD(16, b0, b1);
   PROF_ADD(17, b1, b2);
   PROF_ADD(18, b2, b3);
   PROF_ADD(19, b3, b4);
-  PROF_ADD(20, b4, b5);
-  PROF_ADD(21, b5, b6);
+  PROF_ADD(15, b4, b5);
+  PROF_ADD(20, b5, b6);
+  PROF_ADD(21, b6, b7);
+  PROF_ADD(48, b7, b8);
+  PROF_ADD(13, b8, b9);
   PROF_ADD(23, 0, 1);
   PROF_ADD(24, 0, (long long)js);
   PROF_ADD(25, 0, (long long)nflag);
   PROF_ADD(26, 0, (long long)b);
-  return js;
+  PROF_ADD(22, 0, (long long)(structural ? 1 : 0));
+  return BatchResult{js, structural};
 }
 
 // replay of one key with NW waves (tcap <= 64, ingest only: no flush-mode adoption); BATCH:
@@ -2231,7 +2443,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     const uint64_t cb = (uint64_t)lo + sp.off0;
     const double* const gv = xcsv + cb;
     const double* const gw = xcsw + cb;
-    const double* const gt = xctw + cb;
+    const uint32_t* const gp = x.cpk + cb;
     // the pure chunks' Local* statistics first, every thread streaming its share (off the merge
     // chain: the replay below adds none); the loads of four records in flight per thread
 #ifndef VN_NO_PROLOGUE
@@ -2266,28 +2478,30 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
         c = c1;
         continue;
       }
-      const uint32_t b = min(kBB, left);
       if (c < ring_lo || c > ring_hi) ring_lo = ring_hi = c;  // (after a run of singles)
-      if (c + b > ring_hi) {  // the rest of the batch, now
-        ring_fill<NW>(Bt, gv, gw, gt, ring_hi, c + b, tcap);
-        ring_hi = c + b;
+      dma_wait();  // everything issued so far has landed (this wave's share; the barrier: all)
+      if (ring_hi - c < min(left, kBMinAvail)) {  // too few chunks at hand: fill the batch now
+        const uint32_t e = min(sp.npure, c + kBB);
+        ring_fill<NW>(Bt, gv, gp, ring_hi, e, tcap);
+        ring_hi = e;
+        dma_wait();
       }
-      dma_wait();
       fast_sync<NW>();
+      const uint32_t b = min(min(kBB, left), ring_hi - c);
       // the chunks after it, while it runs (their slots hold chunks < c)
       const uint32_t pe = min(c + kRing, sp.npure);
       if (pe > ring_hi) {
-        ring_fill<NW>(Bt, gv, gw, gt, ring_hi, pe, tcap);
+        ring_fill<NW>(Bt, gv, gp, ring_hi, pe, tcap);
         ring_hi = pe;
       }
       ring_lo = max(c, ring_hi > kRing ? ring_hi - kRing : 0u);
-      const uint32_t js = merge_batch<NW>(x.delta, L, F, Bt, nm, mainW, c, b, tcap);
       PROF_T(s0);
+      const BatchResult r = merge_batch<NW>(mp.delta, L, F, Bt, nm, mainW, c, b, tcap);
       PROF_T(s1);
       PROF_ADD(27, s0, s1);
-      c += js;
-      if (js < b) {  // the rejected merge alone (after a batch that took nothing: a run of them)
-        const uint32_t c1 = min(sp.npure, c + (js == 0 ? kBatchBackoff : 1u));
+      c += r.js;
+      if (r.js < b && r.structural) {  // that merge alone (after a batch that took nothing: a run)
+        const uint32_t c1 = min(sp.npure, c + (r.js == 0 ? kBatchBackoff : 1u));
         singles(c, c1);
         PROF_T(s2);
         PROF_ADD(28, s1, s2);
@@ -2417,7 +2631,7 @@ __global__ void k_exact_count_long(uint32_t n, const uint64_t* __restrict__ orde
     uint32_t lo = 0, hi = n;  // first entry shorter than len
     while (lo < hi) {
       const uint32_t md = (lo + hi) >> 1;
-      if (0xFFFFFu - (uint32_t)(order64[md] >> 32) >= len) lo = md + 1;
+      if (0xFFFFFFFu - (uint32_t)(order64[md] >> 32) >= len) lo = md + 1;
       else hi = md;
     }
     out[q] = min(lo, cap);
@@ -2441,13 +2655,14 @@ void histo_exact_replay_list(const ExactCtx& x, const uint32_t* dev_count, uint3
   else hipLaunchKernelGGL(k_histo_exact_list<kMaxTempPerLane>, dim3(grid), dim3(64), sm, st, x, dev_count);
 }
 
-// longest-first order of the listed keys: (0xFFFFF - min(nex, 0xFFFFF)) << 32 | key index
+// longest-first order of the listed keys: (0xFFFFFFF - min(nex, 0xFFFFFFF)) << 32 | key index
+// (28 bits of length: a window's hot keys hold millions of samples, and the longest must start first)
 __global__ void k_exact_lpt_keys(uint32_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ nex,
                                  uint64_t* __restrict__ out) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint32_t k = list[i], c = min(nex[k], 0xFFFFFu);
-  out[i] = ((uint64_t)(0xFFFFFu - c) << 32) | k;
+  const uint32_t k = list[i], c = min(nex[k], 0xFFFFFFFu);
+  out[i] = ((uint64_t)(0xFFFFFFFu - c) << 32) | k;
 }
 
 void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* buf0, uint64_t* buf1,
@@ -2457,7 +2672,7 @@ void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* 
   if (!n) return;
   hipLaunchKernelGGL(k_exact_lpt_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, list, x.nex, buf0);
   RadixPass passes[4];
-  const int np = make_passes(passes, false, 32, 20);
+  const int np = make_passes(passes, false, 32, 28);
   x.order64 = radix_sort(buf0, nullptr, buf1, nullptr, n, passes, np, rs, st, nullptr) ? buf1 : buf0;
 }
 
@@ -2471,9 +2686,9 @@ static size_t exact_batch_smem_bytes(uint32_t capc, uint32_t tcap) {
 }
 #ifdef VN_EXACT_PROF
 extern "C" int vn_prof_exact_read(unsigned long long* out16, int reset) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_exact_prof), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_exact_prof), sizeof(unsigned long long) * 64) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[32] = {};
+    unsigned long long z[64] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_exact_prof), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;
@@ -2497,7 +2712,7 @@ bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipS
   if (!x.order64 || !x.norder || x.tcap > 64 || x.flush_mode) return false;
   if (exact_fast_smem_bytes(x.capc, x.tcap) > 160 * 1024) return false;
   // (no batching where its tables do not fit: the long keys all take k_histo_exact_mw)
-  const bool batch = x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024;
+  const bool batch = x.cpk && x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024;
   hipLaunchKernelGGL(k_exact_count_long, dim3(1), dim3(1), 0, st, x.norder, x.order64, min_len,
                      batch ? kBatchMinLen : 0xFFFFFFFFu, std::min<uint32_t>(x.norder, kMaxLongKeys), count);
   x.mw_count = count;
@@ -2507,7 +2722,7 @@ bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipS
 void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest, hipStream_t st_top) {
   if (!x.mw_count) return;
   const uint32_t grid = std::min<uint32_t>(x.norder, kMaxLongKeys / 2);
-  if (x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024) {
+  if (x.cpk && x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024) {
     const size_t sm = exact_batch_smem_bytes(x.capc, x.tcap);
     const uint32_t top = st_top ? std::min<uint32_t>(kTopExcl, x.norder) : 0u;
     if (top) hipLaunchKernelGGL(k_histo_exact_mwb, dim3(top), dim3(kMWThreads), sm, st_top, x, x.mw_count, 0u, top);

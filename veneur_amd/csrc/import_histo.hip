@@ -330,29 +330,6 @@ __global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const u
   if (c < 0) atomicOr(err, kErrDecode);
 }
 
-// payload index of every slice boundary: bnd[j] = the last payload i with coff[i] <= j * step
-// (j = 0..nslices), and the centroid offset there
-__global__ void k_import_slices(uint64_t n, const uint32_t* __restrict__ coff, uint64_t step, uint32_t nslices,
-                                uint32_t* __restrict__ bnd) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j > nslices) return;
-  uint64_t b;
-  if (j == nslices) {
-    b = n;
-  } else {
-    const uint64_t thr = (uint64_t)j * step;
-    uint64_t lo = 0, hi = n;  // last i in [0, n] with coff[i] <= thr
-    while (lo < hi) {
-      const uint64_t md = (lo + hi + 1) >> 1;
-      if (coff[md] <= thr) lo = md;
-      else hi = md - 1;
-    }
-    b = lo;
-  }
-  bnd[2 * j] = (uint32_t)b;
-  bnd[2 * j + 1] = coff[b];
-}
-
 }  // namespace
 
 // Histo.Combine of a batch of forwarded digests: decoded and validated now (one host round
@@ -362,8 +339,8 @@ __global__ void k_import_slices(uint64_t n, const uint32_t* __restrict__ coff, u
 // (histo_imports_drain).  Merging a run of imports at once equals merging them one call
 // after another: the replay is the same ordered stream of Adds.  A batch holding more
 // centroids than the run (a global veneur's whole fleet in one call) is cut into slices of
-// payloads at centroid offsets j * run / 2, found on the device (one more round trip), each
-// appended and drained in arrival order.
+// whole payloads of at most the run each (one more round trip for the offsets), each appended
+// and drained in arrival order.
 void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes) {
   if (!n) return;
   hipStream_t st = e->st;
@@ -383,22 +360,25 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
     s.acc += nc;
     return;
   }
-  // slices of at most run / 2 centroids plus one payload
-  const uint64_t step = s.cap_cent / 2;
-  const uint32_t nsl = (uint32_t)((nc + step - 1) / step);
-  std::vector<uint32_t> bnd(2 * ((size_t)nsl + 1));
-  uint32_t* dbnd = s.cnt;  // the counts are consumed (coff holds their scan)
-  hipLaunchKernelGGL(k_import_slices, dim3(blocks_for(nsl + 1, 256)), dim3(256), 0, st, n, s.coff, step, nsl, dbnd);
-  VN_HIP_CHECK(hipMemcpyAsync(bnd.data(), dbnd, bnd.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  // slices of whole payloads in arrival order, each at most the run, cut greedily on the host;
+  // a payload larger than the run is refused before anything is emitted
+  std::vector<uint32_t> co((size_t)n + 1);
+  VN_HIP_CHECK(hipMemcpyAsync(co.data(), s.coff, co.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipStreamSynchronize(st));
-  for (uint32_t j = 0; j < nsl; j++) {
-    const uint64_t b0 = bnd[2 * j], b1 = bnd[2 * j + 2], c0 = bnd[2 * j + 1], c1 = bnd[2 * j + 3];
-    if (b1 <= b0) continue;
-    if (c1 - c0 > s.cap_cent) throw std::invalid_argument("one imported digest holds more centroids than max_batch_records");
-    if (s.acc + (c1 - c0) > s.cap_cent) histo_imports_drain(e);
-    hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
-                       slot + b0, s.coff + b0, s.acc - c0, s.cslot, s.cmean, s.cw, e->h_err);
-    s.acc += c1 - c0;
+  for (uint64_t i = 0; i < n; i++)
+    if (co[i + 1] - co[i] > s.cap_cent)
+      throw std::invalid_argument("one imported digest holds more centroids than max_batch_records");
+  for (uint64_t b0 = 0; b0 < n;) {
+    uint64_t b1 = b0 + 1;
+    while (b1 < n && co[b1 + 1] - co[b0] <= s.cap_cent) b1++;
+    const uint64_t c0 = co[b0], c1 = co[b1];
+    if (c1 > c0) {
+      if (s.acc + (c1 - c0) > s.cap_cent) histo_imports_drain(e);
+      hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
+                         slot + b0, s.coff + b0, s.acc - c0, s.cslot, s.cmean, s.cw, e->h_err);
+      s.acc += c1 - c0;
+    }
+    b0 = b1;
   }
 }
 

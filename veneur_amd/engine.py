@@ -5,6 +5,7 @@ Mirrors the part of veneur's Worker the hot path owns: ProcessMetric batches go 
 the samplers' Flush methods compute (worker.go:187-298, samplers/samplers.go:125-526).
 """
 import ctypes as C
+import warnings
 from dataclasses import dataclass
 
 import numpy as np
@@ -38,6 +39,7 @@ class FlushOutput:
     set_sparse: np.ndarray
     samples_processed: int
     samples_imported: int
+    warn_flags: int = 0            # the caller's misuse this window (VN_WARN_*); the flush completed
 
 
 def _arr(ptr, n, dt, shape=None):
@@ -355,7 +357,7 @@ class Engine:
         histograms get percentiles and which sets an estimate (a local veneur, vn_flush_masked)."""
         o = self.flush_raw(histo_quantile_mask, set_estimate_mask)
         npct = len(self.percentiles)
-        return FlushOutput(
+        out = FlushOutput(
             counter_slot=_arr(o.counter_slot, o.n_counter, np.uint32),
             counter_value=_arr(o.counter_value, o.n_counter, np.int64),
             gauge_slot=_arr(o.gauge_slot, o.n_gauge, np.uint32),
@@ -369,7 +371,12 @@ class Engine:
             set_sparse=_arr(o.set_sparse, o.n_set, np.uint8),
             samples_processed=o.samples_processed,
             samples_imported=o.samples_imported,
+            warn_flags=int(o.warn_flags),
         )
+        if out.warn_flags & A.VN_WARN_SPLIT_TOUCHED:
+            warnings.warn("a split key's slot also received vn_ingest records or imports this window (its "
+                          "records go through vn_ingest_split); the split combine's state was kept", RuntimeWarning)
+        return out
 
     # ---------------------------------------------------------------- introspection
     def read_histo(self, slot, cap=4096):

@@ -367,6 +367,10 @@ class Worker:
         self.processed = 0
         self.imported = 0
         self.dropped = 0  # records with a NaN sample rate (see process_metric)
+        # whole staged batches the engine refused (ingest raised), and their records: every value
+        # the engine validates is screened in process_metric first, so these stay exceptional
+        self.dropped_batches = 0
+        self.dropped_batch_records = 0
         # set member bytes one ingest call may carry (the engine's max_batch_member_bytes)
         self.max_member_bytes = int(getattr(engine, "max_batch_member_bytes", 0) or max(batch_records, 1) * 64)
         self._win = _Window()
@@ -405,7 +409,8 @@ class Worker:
         except EngineError as err:
             # a batch the engine rejects is dropped and counted, never resubmitted: one bad batch
             # must not block every later ProcessMetric and the window's flush
-            self.dropped += self._staged
+            self.dropped_batches += 1
+            self.dropped_batch_records += self._staged
             log.error("dropping a batch of %d staged samples: %s", self._staged, err)
         self._reset_stage()
 
