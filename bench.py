@@ -24,7 +24,6 @@ import argparse
 import json
 import os
 import sys
-import threading
 import time
 
 import numpy as np
@@ -54,66 +53,6 @@ def hot_keys(counts, scale, classes, thr_cs, thr_set, max_split, split_histos=Fa
     out = pick(counts.astype(np.float64) * scale, classes, thr, max_split)
     out.setdefault(2, np.zeros(0, np.uint32))
     return out
-
-
-class InTurn:
-    """Windows over D engines: window i runs on engine i % D, each engine's windows in order in a
-    host thread of its own (D > 1), and the flushes entered in window order -- work(k, i, turn)
-    calls `with turn(i):` around its flush.  run(n) returns the n results in window order."""
-
-    def __init__(self, D):
-        self.D = D
-        self.cv = threading.Condition()
-        self.next = 0
-        self.failed = False
-
-    def turn(self, i):
-        pipe = self
-
-        class _T:
-            def __enter__(self):
-                with pipe.cv:
-                    pipe.cv.wait_for(lambda: pipe.next == i or pipe.failed)
-                    if pipe.failed:
-                        raise RuntimeError("an earlier window failed")
-
-            def __exit__(self, *exc):
-                with pipe.cv:
-                    if exc[0] is None:
-                        pipe.next = i + 1
-                    else:
-                        pipe.failed = True  # (the other engines' waits end)
-                    pipe.cv.notify_all()
-                return False
-
-        return _T()
-
-    def run(self, n, work):
-        self.next, self.failed = 0, False
-        out, errs = [None] * n, []
-        if self.D == 1:
-            for i in range(n):
-                out[i] = work(0, i, self.turn)
-            return out
-
-        def worker(k):
-            try:
-                for i in range(k, n, self.D):
-                    out[i] = work(k, i, self.turn)
-            except BaseException as ex:
-                errs.append(ex)
-                with self.cv:
-                    self.failed = True
-                    self.cv.notify_all()
-
-        th = [threading.Thread(target=worker, args=(k,)) for k in range(self.D)]
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        if errs:
-            raise errs[0]
-        return out
 
 
 def split_thresholds(args, thr):
@@ -462,6 +401,28 @@ def egress_leg(flush_result):
             "intermetrics_per_s": out.n_intermetrics / dt}
 
 
+def cgroup_cpus():
+    """The cgroup v2 (cpu.max) or v1 (cfs quota / period) CPU limit of this process, rounded up;
+    None when no limit is set or none can be read."""
+    import math
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            p = int(fh.read())
+        return max(1, math.ceil(q / p)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -475,9 +436,9 @@ def main():
     ap.add_argument("--set-hot", type=int, default=1 << 18, help="split a set key above this many records")
     ap.add_argument("--max-split", type=int, default=64, help="split keys per class at most")
     ap.add_argument("--pipeline", type=int, default=0,
-                    help="engines taking the windows in turn (window i + 1 ingested while window i's longest "
-                         "replays finish); 1: one engine, windows back to back; 0 (default): 2 on one GPU, 1 "
-                         "over RCCL (a second communicator per rank is not exercised on hardware here)")
+                    help="engines per GPU taking the windows in turn (window i + 1 ingested and combined while "
+                         "window i's longest replays finish; one communicator per engine, the combines entered in "
+                         "window order); 1: one engine, windows back to back; 0 (default): 2")
     ap.add_argument("--hot-stride", type=int, default=256,
                     help="hot-key detector: count every hot_stride-th record (vn_hot_detect)")
     ap.add_argument("--no-split", action="store_true", help="route every key by digest %% N (no hot keys)")
@@ -518,7 +479,7 @@ def main():
 
     import veneur_amd as V
     import veneur_amd._abi as A
-    from veneur_amd.dist import Group, env_world, make_comm
+    from veneur_amd.dist import Group, InTurn, env_world, make_comm
 
     world, rank, local_rank = env_world()
     sim = args.sim_world > 1 and world == 1
@@ -554,7 +515,7 @@ def main():
     # reference's flush goroutine works on the swapped maps while the workers take the next
     # interval.  Flushes are entered in window order, so every rank issues the split combine's
     # collectives (one communicator per engine) in the same order.
-    D = 1 if sim else max(1, args.pipeline if args.pipeline > 0 else (2 if world == 1 else 1))
+    D = max(1, args.pipeline if args.pipeline > 0 else 2)
 
     def make_engine():
         e = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,
@@ -602,11 +563,13 @@ def main():
         e.ingest_device(stream.batch)
         if t:
             t.append(time.perf_counter())
-        if turn is not None:
+        if turn is not None and D > 1:
+            # only the split combine's collectives need the window order (one communicator per
+            # engine, every rank issuing them in the same order); the replays and the flush of
+            # window i then run beside window i + 1's ingest and combine on the other engines
             with turn(i):
-                r = e.flush_raw()
-        else:
-            r = e.flush_raw()
+                e.split_combine()
+        r = e.flush_raw()
         lat.append((time.perf_counter() - ts) * 1e3)
         if t:
             t.append(time.perf_counter())
@@ -733,7 +696,8 @@ def main():
                                    args.keys, args.samples, world,
                                    "t-digest fast mode (geometric pieces past %d samples)" % args.exact_threshold
                                    if args.exact_threshold else "every t-digest merge replayed exactly"),
-                   "histo_mode": "fast" if args.exact_threshold else "exact",
+                   "histo_mode": "fast (non-conforming: rank-error bound 3e-3, not the reference's digests)"
+                                 if args.exact_threshold else "exact",
                    "keys": args.keys, "samples_per_window": args.samples, "percentiles": list(PCT),
                    "compression": 100, "hll_precision": 14,
                    "parallelism": "key-sharded FNV %% %d + %d split hot keys (RCCL)" %
@@ -798,7 +762,15 @@ def main():
         import oracle
         # num_workers = the CPUs this process may use: the GPU box's share is 16 of a machine whose
         # nproc counts every CPU of the host (the guide for the pool), so 16 unless fewer exist
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        quota = cgroup_cpus()
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            affinity = os.cpu_count() or 1
+        # the CPUs this process may actually run on: the cgroup's CPU quota where one is set, the
+        # affinity mask otherwise, and at most 16 (the GPU box's documented share per GPU)
+        usable = min(affinity, quota) if quota else affinity
+        threads = args.cpu_threads or max(1, min(16, usable))
         streams = {k: d[k] for k in ("c_slot", "c_val", "c_rate", "g_slot", "g_val", "h_slot", "h_val", "h_rate",
                                      "s_slot", "s_off", "s_bytes")}
         secs, _, ref = oracle.baseline_run_full(threads, n_slots, streams, PCT)
@@ -811,18 +783,15 @@ def main():
                         break
         except OSError:
             pass
-        try:
-            affinity = len(os.sched_getaffinity(0))
-        except (AttributeError, OSError):
-            affinity = os.cpu_count() or 1
         result["cpu_baseline"] = {"value": args.samples / secs, "unit": "samples/s", "cores": threads,
                                   "kind": "port", "seconds": secs, "num_workers": threads,
-                                  "nproc": os.cpu_count(), "cpus_usable": affinity, "cpu_model": model,
+                                  "nproc": os.cpu_count(), "cpus_affinity": affinity,
+                                  "cgroup_cpu_quota": quota, "cpus_usable": usable, "cpu_model": model,
                                   "sample": "the full C4 flush window above (%d samples); C restatement of the Go "
                                             "Worker.ProcessMetric + flush path (oracle/), num_workers = %d worker "
-                                            "threads routed by key digest %% num_workers (SURVEY 8(d)); the GPU box "
-                                            "grants this process a share of %d CPUs of the machine's nproc = %s"
-                                            % (args.samples, threads, threads, os.cpu_count())}
+                                            "threads routed by key digest %% num_workers (SURVEY 8(d)); usable CPUs "
+                                            "= min(affinity %d, cgroup quota %s), capped at the box's share of 16"
+                                            % (args.samples, threads, affinity, quota)}
         if args.c5_hosts > 0:
             t1 = time.time()
             result["c5"] = c5_leg(args, rank)

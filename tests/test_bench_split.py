@@ -4,6 +4,7 @@ hysteresis that keeps a split key while it stays above half the threshold."""
 import numpy as np
 
 import bench
+from veneur_amd.dist import InTurn
 
 
 class FakeEngine:
@@ -73,7 +74,7 @@ def test_windows_in_turn_flush_in_window_order_and_fail_without_hanging():
     for D in (1, 2, 3):
         order.clear()
         per_engine.clear()
-        out = bench.InTurn(D).run(10, work)
+        out = InTurn(D).run(10, work)
         assert order == list(range(10))
         assert out == [(i % D, i) for i in range(10)]
         assert all(v == sorted(v) and all(i % D == k for i in v) for k, v in per_engine.items())
@@ -87,5 +88,5 @@ def test_windows_in_turn_flush_in_window_order_and_fail_without_hanging():
 
     t0 = time.time()
     with pytest.raises(RuntimeError, match="window 4"):
-        bench.InTurn(2).run(10, bad)
+        InTurn(2).run(10, bad)
     assert time.time() - t0 < 5

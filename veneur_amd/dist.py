@@ -9,6 +9,7 @@ plane -- barrier around the timed region, max of the per-rank times, the RCCL id
 torch.distributed group, gloo on the host.
 """
 import os
+import threading
 
 import numpy as np
 
@@ -144,3 +145,68 @@ def make_comm(group, device):
     uid = Comm.unique_id() if group.rank == 0 else None
     uid = group.broadcast_object(uid)
     return Comm.rccl(uid, group.world, group.rank, device)
+
+
+class InTurn:
+    """Flush windows over D engines per rank: window i runs on engine i % D, each engine's windows
+    in order in a host thread of its own (D > 1), as veneur's flush goroutine works on the swapped
+    maps while the workers take the next interval (server.go Flush / worker.go Flush).  work(k, i,
+    turn) calls `with turn(i):` around the part of window i that issues collectives (the split
+    combine, one communicator per engine), so every rank enters them in window order: engine k's
+    communicator sees windows k, k + D, ... on every rank, and no two communicators' collectives
+    are ever issued in different orders on two ranks.  run(n) returns the n results in window
+    order; a failure in any window ends the others' waits."""
+
+    def __init__(self, D):
+        self.D = D
+        self.cv = threading.Condition()
+        self.next = 0
+        self.failed = False
+
+    def turn(self, i):
+        pipe = self
+
+        class _T:
+            def __enter__(self):
+                with pipe.cv:
+                    pipe.cv.wait_for(lambda: pipe.next == i or pipe.failed)
+                    if pipe.failed:
+                        raise RuntimeError("an earlier window failed")
+
+            def __exit__(self, *exc):
+                with pipe.cv:
+                    if exc[0] is None:
+                        pipe.next = i + 1
+                    else:
+                        pipe.failed = True  # (the other engines' waits end)
+                    pipe.cv.notify_all()
+                return False
+
+        return _T()
+
+    def run(self, n, work):
+        self.next, self.failed = 0, False
+        out, errs = [None] * n, []
+        if self.D == 1:
+            for i in range(n):
+                out[i] = work(0, i, self.turn)
+            return out
+
+        def worker(k):
+            try:
+                for i in range(k, n, self.D):
+                    out[i] = work(k, i, self.turn)
+            except BaseException as ex:
+                errs.append(ex)
+                with self.cv:
+                    self.failed = True
+                    self.cv.notify_all()
+
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(self.D)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        if errs:
+            raise errs[0]
+        return out
