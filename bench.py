@@ -149,15 +149,25 @@ def rank_error_stats(d, slots, eng_q, ref_q):
     return errs, acc_e, acc_r
 
 
-def c5_leg(args, rank):
+def c5_owners(n_keys, typ, world):
+    """Owner rank of each C5 key, digest % N of its name and type (newJSONMetricsByWorker,
+    http.go:71-139, with the GPUs as the workers): key k of a class is "c5.<typ>.<k>"."""
+    from veneur_amd.worker import MetricKey, metric_digest
+    return np.array([metric_digest(MetricKey("c5.%s.%d" % (typ, k), typ, "")) % world for k in range(n_keys)],
+                    np.int64)
+
+
+def c5_leg(args, rank, world, ctrl, device):
     """C5 (BASELINE configs[4]): a global veneur merging every host's forwarded digests and
     sketches -- ImportMetric -> Histo.Combine / Set.Combine (worker.go:230-268) for each of
     `hosts` DISTINCT hosts x (histo_keys GobEncode()d digests + set_keys MarshalBinary()d
     sketches); every key arrives from every host.  Each host's local window (~100 timer samples
     per key, Lomax-sized sets; vn_synth_hosts_device) is generated, ingested and exported on the
     GPU in groups of c5_group hosts (one local engine per group); the payloads stay in HBM,
-    concatenated host-major.  One window = ONE vn_import_histos_device and ONE
-    vn_import_sets_device call over all hosts' payloads, then vn_flush.  Parity on sampled keys
+    concatenated host-major.  Over N GPUs every rank sees every host and keeps the payloads of
+    the keys it owns (digest % N, c5_owners: each key on exactly one rank, no collective).  One
+    window = ONE vn_import_histos_device and ONE vn_import_sets_device call over the rank's
+    payloads, then vn_flush; the window time is the max over the ranks.  Parity on sampled keys
     against the restated Go (oracle Worker.ImportMetric of the same payloads in the same host
     order): digest weight/min/max exact, set estimates exact, quantiles bit-exact (the default
     exact mode) -- rank error over the imported centroids reported as well."""
@@ -167,81 +177,100 @@ def c5_leg(args, rank):
     import veneur_amd as V
     import veneur_amd._abi as A
     H, S, hosts, G = args.c5_histo_keys, args.c5_set_keys, args.c5_hosts, max(1, args.c5_group)
-    rng = np.random.default_rng(args.seed + 5)
-    kh = np.sort(rng.choice(H, min(H, args.c5_parity_keys), replace=False))
-    ks = np.sort(rng.choice(S, min(S, args.c5_parity_keys), replace=False))
+    own = {2: np.nonzero(c5_owners(H, "timer", world) == rank)[0],
+           3: np.nonzero(c5_owners(S, "set", world) == rank)[0]}
+    nown = {c: len(own[c]) for c in own}
+    rng = np.random.default_rng(args.seed + 5 + rank)
+    # sampled keys, as indices into the rank's owned keys
+    kh = np.sort(rng.choice(nown[2], min(nown[2], max(1, args.c5_parity_keys // world)), replace=False)) \
+        if nown[2] else np.zeros(0, np.int64)
+    ks = np.sort(rng.choice(nown[3], min(nown[3], max(1, args.c5_parity_keys // world)), replace=False)) \
+        if nown[3] else np.zeros(0, np.int64)
     t0 = time.time()
     parts = {2: [], 3: []}  # per group: (offsets, DeviceBuffer)
     par = {2: {int(k): [] for k in kh}, 3: {int(k): [] for k in ks}}  # sampled keys' payloads, host order
     n_samples = 0
     for h0 in range(0, hosts, G):
         g = min(G, hosts - h0)
-        win = V.HostWindows(args.seed + 55, h0, g, H, S)
+        win = V.HostWindows(args.seed + 55, h0, g, H, S, device=device)
         n_samples += win.n_histo + win.n_set
         with V.Engine((1, 1, g * H, g * S), percentiles=PCT, max_batch_records=max(win.n_histo, win.n_set) + 1,
-                      max_batch_member_bytes=64) as loc:
+                      max_batch_member_bytes=64, device=device) as loc:
             loc.ingest_device(win.batch)
             for cls, nk, keys in ((2, H, kh), (3, S, ks)):
-                off, buf, view = loc.export_device(cls, np.arange(g * nk, dtype=np.uint32))
+                # this rank's keys of every host of the group, host-major
+                sl = (np.arange(g, dtype=np.uint32)[:, None] * np.uint32(nk) + own[cls][None, :].astype(np.uint32))
+                off, buf, view = loc.export_device(cls, sl.ravel().astype(np.uint32))
                 parts[cls].append((off, buf))
                 for hh in range(g):
                     for k in keys:
-                        i = hh * nk + int(k)
+                        i = hh * nown[cls] + int(k)
                         par[cls][int(k)].append(view[off[i]:off[i + 1]].tobytes())
             loc.flush_raw()
         win.free()
     dev = {}
     payload_bytes = 0
-    for cls, nk in ((2, H), (3, S)):
+    for cls in (2, 3):
         total = sum(int(o[-1]) for o, _ in parts[cls])
-        big = V.DeviceBuffer.empty(total)
+        big = V.DeviceBuffer.empty(total, device=device)
         offs, base = [], 0
         for o, b in parts[cls]:
             if int(o[-1]):
-                A.lib.vn_device_copy(0, C.c_void_p(big.ptr.value + base), b.ptr, int(o[-1]))
+                A.lib.vn_device_copy(device, C.c_void_p(big.ptr.value + base), b.ptr, int(o[-1]))
             offs.append(o[:-1] + base)
             base += int(o[-1])
             b.free()
         offs.append(np.array([base], np.uint64))
         off_all = np.concatenate(offs).astype(np.uint64)
-        slots = np.tile(np.arange(nk, dtype=np.uint32), hosts)
-        dev[cls] = (V.DeviceBuffer(slots), V.DeviceBuffer(off_all), big, len(slots))
+        slots = np.tile(np.arange(nown[cls], dtype=np.uint32), hosts)
+        dev[cls] = (V.DeviceBuffer(slots, device=device), V.DeviceBuffer(off_all, device=device), big, len(slots))
         payload_bytes += total
-    A.lib.vn_device_synchronize(0)
+    A.lib.vn_device_synchronize(device)
     gen_s = time.time() - t0
-    with V.Engine((1, 1, H, S), percentiles=PCT, max_batch_records=args.c5_batch) as g:
+    with V.Engine((1, 1, max(1, nown[2]), max(1, nown[3])), percentiles=PCT, max_batch_records=args.c5_batch,
+                  device=device) as g:
         def window():
             for cls in (2, 3):
                 sl, of, by, n = dev[cls]
-                g.import_device(cls, sl.ptr.value, of.ptr.value, by.ptr.value, n)
+                if n:
+                    g.import_device(cls, sl.ptr.value, of.ptr.value, by.ptr.value, n)
             return g.flush_raw()
         window()
-        A.lib.vn_device_synchronize(0)
+        A.lib.vn_device_synchronize(device)
+        ctrl.barrier()
         tw = time.perf_counter()
         for _ in range(args.c5_windows):
             f = window()
-        A.lib.vn_device_synchronize(0)
-        ms = (time.perf_counter() - tw) * 1e3 / args.c5_windows
+        A.lib.vn_device_synchronize(device)
+        ms_rank = (time.perf_counter() - tw) * 1e3 / args.c5_windows
+        ctrl.barrier()
+        ms = ctrl.max(ms_rank)
         # one more window, synchronised between its phases (the split only; not the headline)
         phases = {}
         tp = time.perf_counter()
         for cls, name in ((2, "import_histos"), (3, "import_sets")):
             sl, of, by, n = dev[cls]
-            g.import_device(cls, sl.ptr.value, of.ptr.value, by.ptr.value, n)
-            A.lib.vn_device_synchronize(0)
+            if n:
+                g.import_device(cls, sl.ptr.value, of.ptr.value, by.ptr.value, n)
+            A.lib.vn_device_synchronize(device)
             phases[name] = (time.perf_counter() - tp) * 1e3
             tp = time.perf_counter()
         f = g.flush_raw()
-        A.lib.vn_device_synchronize(0)
+        A.lib.vn_device_synchronize(device)
         phases["flush"] = (time.perf_counter() - tp) * 1e3
-        hq =np.ctypeslib.as_array(f.histo_quantiles, shape=(f.n_histo * len(PCT),)).reshape(-1, len(PCT)).copy()
-        hst = np.ctypeslib.as_array(f.histo_stats, shape=(f.n_histo * 8,)).reshape(-1, 8).copy()
-        hsl = np.ctypeslib.as_array(f.histo_slot, shape=(f.n_histo,)).copy()
-        ses = np.ctypeslib.as_array(f.set_estimate, shape=(f.n_set,)).copy()
-        ssl = np.ctypeslib.as_array(f.set_slot, shape=(f.n_set,)).copy()
+        hq = np.ctypeslib.as_array(f.histo_quantiles, shape=(f.n_histo * len(PCT),)).reshape(-1, len(PCT)).copy() \
+            if f.n_histo else np.zeros((0, len(PCT)))
+        hst = np.ctypeslib.as_array(f.histo_stats, shape=(f.n_histo * 8,)).reshape(-1, 8).copy() \
+            if f.n_histo else np.zeros((0, 8))
+        hsl = np.ctypeslib.as_array(f.histo_slot, shape=(f.n_histo,)).copy() if f.n_histo else np.zeros(0, np.uint32)
+        ses = np.ctypeslib.as_array(f.set_estimate, shape=(f.n_set,)).copy() if f.n_set else np.zeros(0, np.uint64)
+        ssl = np.ctypeslib.as_array(f.set_slot, shape=(f.n_set,)).copy() if f.n_set else np.zeros(0, np.uint32)
+    for d in dev.values():
+        for b in d[:3]:
+            b.free()
     # parity on sampled keys: the restated Go import of the same payload sequence
     t1 = time.time()
-    w = oracle.Worker(1, 1, len(kh), len(ks))
+    w = oracle.Worker(1, 1, max(1, len(kh)), max(1, len(ks)))
     pos = {int(s_): j for j, s_ in enumerate(hsl)}
     st_exact, bit_exact, rank_err, st_diff = True, True, 0.0, np.zeros(3)
     for i, k in enumerate(kh):
@@ -271,23 +300,34 @@ def c5_leg(args, rank):
             w.import_set(i, pl)
     spos = {int(s_): j for j, s_ in enumerate(ssl)}
     set_exact = all(int(ses[spos[int(k)]]) == w.set_estimate(i) for i, k in enumerate(ks))
+    per_rank = ctrl.gather_object({"ms": ms_rank, "keys": [nown[2], nown[3]], "payload_bytes": payload_bytes,
+                                   "phases": phases, "checked": [len(kh), len(ks)], "st_exact": st_exact,
+                                   "st_diff": st_diff.tolist(), "bit_exact": bit_exact, "rank_err": rank_err,
+                                   "set_exact": bool(set_exact)})
     n_imp = hosts * (H + S)
+    all_bytes = sum(r["payload_bytes"] for r in per_rank)
     return {"config": "C5 global import: %d distinct hosts x (%d histo digests + %d set sketches), every key from "
-                      "every host; host windows generated, ingested and exported on the GPU (%d local samples); "
-                      "payloads in HBM, ONE vn_import_histos_device + ONE vn_import_sets_device call, then vn_flush"
-                      % (hosts, H, S, n_samples),
-            "imports_per_s": n_imp / (ms * 1e-3), "payload_GBs": payload_bytes / (ms * 1e-3) / 1e9,
+                      "every host; host windows generated, ingested and exported on the GPU (%d local samples per "
+                      "rank); payloads in HBM, each rank keeping its keys' (digest %% %d), ONE "
+                      "vn_import_histos_device + ONE vn_import_sets_device call per rank, then vn_flush"
+                      % (hosts, H, S, n_samples, world),
+            "n_gpus": world, "imports_per_s": n_imp / (ms * 1e-3), "payload_GBs": all_bytes / (ms * 1e-3) / 1e9,
             "ms_per_window": ms, "windows": args.c5_windows, "payloads_per_window": n_imp,
-            "phases_ms_synchronised": {k: round(v, 2) for k, v in phases.items()},
-            "payload_bytes_per_window": payload_bytes,
-            "roofline": {"bound": "hbm", "achieved_GBs": payload_bytes / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                         "frac": payload_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "unit": "payload bytes decoded per second over the window"},
+            "phases_ms_synchronised": {k: round(v, 2) for k, v in per_rank[0]["phases"].items()},
+            "ranks": {"ms_per_window": [round(r["ms"], 2) for r in per_rank],
+                      "histo_set_keys": [r["keys"] for r in per_rank]},
+            "payload_bytes_per_window": all_bytes,
+            "roofline": {"bound": "hbm", "achieved_GBs": all_bytes / (ms * 1e-3) / 1e9 / world, "peak": HBM_PEAK_GBS,
+                         "frac": all_bytes / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS,
+                         "unit": "payload bytes decoded per second per GPU over the window"},
             "generated_in_s": round(gen_s, 2), "parity_checked_in_s": round(time.time() - t1, 2),
-            "parity": {"keys_checked": {"histo": int(len(kh)), "set": int(len(ks))},
-                       "histo_weight_min_max_exact": st_exact, "histo_min_max_weight_absdiff": st_diff.tolist(),
-                       "histo_quantiles_bit_exact": bit_exact, "histo_rank_error_max": rank_err,
-                       "set_estimates_exact": bool(set_exact)}}
+            "parity": {"keys_checked": {"histo": int(sum(r["checked"][0] for r in per_rank)),
+                                        "set": int(sum(r["checked"][1] for r in per_rank))},
+                       "histo_weight_min_max_exact": all(r["st_exact"] for r in per_rank),
+                       "histo_min_max_weight_absdiff": np.max([r["st_diff"] for r in per_rank], axis=0).tolist(),
+                       "histo_quantiles_bit_exact": all(r["bit_exact"] for r in per_rank),
+                       "histo_rank_error_max": max(r["rank_err"] for r in per_rank),
+                       "set_estimates_exact": all(r["set_exact"] for r in per_rank)}}
 
 
 def text_leg(args):
@@ -792,10 +832,6 @@ def main():
                                             "threads routed by key digest %% num_workers (SURVEY 8(d)); usable CPUs "
                                             "= min(affinity %d, cgroup quota %s), capped at the box's share of 16"
                                             % (args.samples, threads, affinity, quota)}
-        if args.c5_hosts > 0:
-            t1 = time.time()
-            result["c5"] = c5_leg(args, rank)
-            log(rank, "[bench] C5 leg in %.1fs: %s" % (time.time() - t1, json.dumps(result["c5"])))
         t1 = time.time()
         result["egress"] = egress_leg(last)
         log(rank, "[bench] egress leg in %.1fs: %s" % (time.time() - t1, json.dumps(result["egress"])))
@@ -870,6 +906,13 @@ def main():
         result["p99_rank_error"] = par["rank_error_max"]["p99"]
         result["parity"] = par
         log(rank, "[bench] parity checked in %.1fs" % (time.time() - t1))
+    if args.c5_hosts > 0 and not sim:
+        # C5 on every rank: each keeps the imports of the keys it owns (no collective)
+        t1 = time.time()
+        c5 = c5_leg(args, rank, world, ctrl, local_rank)
+        if rank == 0:
+            result["c5"] = c5
+            log(rank, "[bench] C5 leg in %.1fs: %s" % (time.time() - t1, json.dumps(c5)))
     if rank == 0:
         print(json.dumps(result), flush=True)
     for e in engines:

@@ -16,6 +16,7 @@ import pytest
 
 import oracle
 import veneur_amd as V
+from veneur_amd.dist import Group
 from tests.util import PCT, engine_ingest, rank_errors, run_oracle
 
 pytestmark = pytest.mark.gpu
@@ -145,12 +146,31 @@ def test_c5_bench_leg_small():
     from argparse import Namespace
     import bench
     r = bench.c5_leg(Namespace(seed=3, c5_histo_keys=300, c5_set_keys=60, c5_group=7, c5_hosts=40, c5_windows=1,
-                               c5_parity_keys=300, c5_batch=1 << 20), 0)
+                               c5_parity_keys=300, c5_batch=1 << 20), 0, 1, Group(), 0)
     p = r["parity"]
     assert p["keys_checked"] == {"histo": 300, "set": 60}
     assert p["histo_weight_min_max_exact"] and p["set_estimates_exact"]
     assert p["histo_quantiles_bit_exact"] and p["histo_rank_error_max"] == 0.0, p
     assert r["payloads_per_window"] == 40 * 360 and r["imports_per_s"] > 0
+
+
+def test_c5_bench_leg_sharded_over_two_ranks():
+    """the C5 leg as rank 0 and rank 1 of N = 2 (run one after the other on this GPU): each rank
+    keeps its keys' payloads (digest % 2), the two shares cover every key once, and each rank's
+    imports are bit-exact against the oracle on every key it owns"""
+    from argparse import Namespace
+    import bench
+    keys = [0, 0]
+    for r in range(2):
+        res = bench.c5_leg(Namespace(seed=5, c5_histo_keys=120, c5_set_keys=30, c5_group=8, c5_hosts=24,
+                                     c5_windows=1, c5_parity_keys=300, c5_batch=1 << 20), r, 2, Group(), 0)
+        p = res["parity"]
+        assert p["histo_weight_min_max_exact"] and p["set_estimates_exact"] and p["histo_quantiles_bit_exact"], p
+        hk, sk = res["ranks"]["histo_set_keys"][0]
+        assert p["keys_checked"] == {"histo": hk, "set": sk} and hk > 0 and sk > 0
+        keys[0] += hk
+        keys[1] += sk
+    assert keys == [120, 30]
 
 
 def test_c5_import_sliced_by_centroids():
@@ -160,6 +180,6 @@ def test_c5_import_sliced_by_centroids():
     from argparse import Namespace
     import bench
     r = bench.c5_leg(Namespace(seed=4, c5_histo_keys=64, c5_set_keys=8, c5_group=16, c5_hosts=64, c5_windows=2,
-                               c5_parity_keys=64, c5_batch=60_000), 0)
+                               c5_parity_keys=64, c5_batch=60_000), 0, 1, Group(), 0)
     p = r["parity"]
     assert p["histo_weight_min_max_exact"] and p["set_estimates_exact"] and p["histo_quantiles_bit_exact"], p

@@ -122,6 +122,15 @@ def deal(n_records, n_ranks):
     return np.arange(n_records, dtype=np.int64) % int(n_ranks)
 
 
+def route_imports(metrics, rank, world):
+    """This rank's share of imported JSONMetrics in arrival order: newJSONMetricsByWorker's worker
+    index, digest % N of name, type and joined tags (http.go:71-139, worker.go MetricKey), with
+    the GPUs as the workers.  Each key lands on exactly one rank, so a global veneur over N GPUs
+    merges every import where the key lives, with no data-path collective."""
+    from .worker import metric_digest
+    return [m for m in metrics if metric_digest(m.key) % int(world) == int(rank)]
+
+
 def hot_keys(counts, classes, thresholds, max_split=64):
     """Top keys by window count above their class threshold: {class: sorted key ids}.
     counts: records per key (e.g. the previous window's), classes: class of every key,

@@ -201,15 +201,23 @@ def unmarshal_metrics_from_http(body: bytes, content_encoding: str = "") -> List
 UnmarshalMetricsFromHTTP = unmarshal_metrics_from_http
 
 
-def handle_import(workers, body: bytes, content_encoding: str = "") -> Tuple[int, int]:
+def handle_import(workers, body: bytes, content_encoding: str = "", shard=None) -> Tuple[int, int]:
     """handleImport (handlers_global.go:53-63) for a POST /import: returns (HTTP status, number
     of metrics handed to the workers).  Go runs ImportMetrics in a goroutine after answering
-    202; here it runs before returning, so a caller sees the merge done on the device."""
+    202; here it runs before returning, so a caller sees the merge done on the device.
+
+    shard=(rank, world): a global veneur spread over `world` GPUs, one process each, every
+    process handed the same bodies -- this rank imports only the keys it owns (digest % world,
+    dist.route_imports), so no imported key spans ranks and the import needs no collective.  The
+    count returned is then this rank's share."""
     try:
         metrics = unmarshal_metrics_from_http(body, content_encoding)
     except ImportRequestError as e:
         log.error("Could not decode /import request (%s): %s", e.cause or "empty", e)
         return e.status, 0
+    if shard is not None:
+        from .dist import route_imports
+        metrics = route_imports(metrics, *shard)
     import_metrics(workers, metrics)
     return StatusAccepted, len(metrics)
 
