@@ -693,10 +693,12 @@ def main():
     ms_c = mean("ms_ingest_counter")
     if ms_c > 0:
         by_c = 16.0 * stream.counts[0]
-        kern.append({"kernel": "k_scalar_direct", "ms_per_step": ms_c, "launches_per_step": 1.0,
+        kern.append({"kernel": "counter aggregation", "ms_per_step": ms_c, "launches_per_step": 1.0,
                      "algorithmic_bytes_per_launch": by_c, "achieved": by_c / (ms_c * 1e-3) / 1e9,
                      "frac": by_c / (ms_c * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "note": "timed as the serialised counter phase; bound by memory-side atomic requests"})
+                     "note": "the serialised counter phase: key-range partition pass (k_part_count, "
+                             "k_part_scatter) + k_counter_runs (LDS sums per slot range, one device add per "
+                             "touched slot per 128Ki-record slice)"})
     kern.sort(key=lambda k: -k["ms_per_step"])
     phase = {k: round(mean(k), 4) for k in
              ("ms_ingest_counter", "ms_ingest_gauge", "ms_ingest_histo", "ms_ingest_set", "ms_flush")}

@@ -1684,6 +1684,8 @@ typedef __attribute__((address_space(3))) uint8_t ldsu8;
 
 constexpr uint32_t kRS = kBB + 8;  // row stride (bytes) of the n and K tables: 18 dwords, so the
                                    // rows of consecutive columns fall on different banks
+constexpr uint32_t kSR = 168;      // bytes of a chunk's run-end row (columns 0..kBN, 8-byte multiple)
+static_assert(kSR >= kBN + 1 && kSR % 8 == 0 && kSR / 4 <= 64, "a run-end row: a dword per lane");
 
 struct BatchLds {
   ldsf64* rv;       // [kRing * tcap] the chunk sorter's csv: sorted temp means
@@ -1775,6 +1777,22 @@ struct BatchResult {
   uint32_t js;      // merges committed
   bool structural;  // merge js failed a structure test (it runs alone); else the next batch starts there
 };
+
+// inclusive max-scan over the 64 lanes of a wave by DPP moves (no LDS): row shifts 1, 2, 4, 8, then
+// the row broadcasts of lanes 15 and 31 (lanes without a source take 0, the identity here)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t v) {
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false));  // row_shr:1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false));  // row_shr:2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false));  // row_shr:4
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false));  // row_shr:8
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return v;
+}
+// the value of lane l - 1 (0 in lane 0): DPP wave_shr:1
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
+}
 
 // |x| is 0 or within [2^-400, 2^400]: the Welford division of the batch then never needs
 // v_div_scale's rescaling (see merge_batch, E)
@@ -1882,6 +1900,9 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
 #pragma unroll
     for (uint32_t u = 0; u < kA; u++)
       if (t + u * NT < nt) B.pos[t + u * NT] = (uint8_t)ps[u];
+    // the run-end rows of B (kSR bytes per chunk, in the list area, which D fills later) zeroed
+    ldsu64* const sr = (ldsu64*)B.lv;
+    for (uint32_t q = t; q < kBB * kSR / 8; q += NT) sr[q] = 0ull;
     if (t < nm) safe &= div_safe(L.mm[t]);
     if ((t + 1 < nm && !(L.mm[t] <= L.mm[t + 1])) || !safe) B.ctl[4] = 1u;  // (t < 256: nm <= 160)
   }
@@ -1891,24 +1912,44 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
     fast_sync<NW>();  // the fast division's range: no batch
     return BatchResult{0u, true};
   }
-  // ---- B: the n table from the pos runs: temp p of chunk j fills rows [pos_p, pos_{p+1}) of
-  // column j with p + 1 (p = 0 also rows [0, pos_0) with 0)
+  // ---- B: the n table.  n[j][i] = #temps of chunk j with pos <= i, a step function of i: the last
+  // temp p of each run of equal pos c writes p + 1 at column c of chunk j's run-end row (B1); a
+  // wave then takes four chunks at a time, a lane four columns, and max-scans each row over the
+  // columns (within the lane's dword, then across lanes by DPP), packing the four chunks' bytes of
+  // each column into one dword of the column-major table (B2)
   {
-    uint32_t c1[kA];
+    ldsu8* const sr = (ldsu8*)B.lv;
 #pragma unroll
     for (uint32_t u = 0; u < kA; u++) {
       const uint32_t g = t + u * NT;
-      const uint32_t x = B.pos[min(g + 1, nt - 1)];
-      c1[u] = g < nt && gp[u] + 1 < tcap ? x : nm + 1;
+      const uint32_t nx = B.pos[min(g + 1, nt - 1)];
+      if (g < nt && (gp[u] + 1 == tcap || nx != ps[u])) sr[gj[u] * kSR + ps[u]] = (uint8_t)(gp[u] + 1);
     }
+  }
+  fast_sync<NW>();
+  {
+    const ldsu32* const sr = (const ldsu32*)B.lv;
+    for (uint32_t g4 = wv; 4 * g4 < b; g4 += NW) {
+      uint32_t x[4];
 #pragma unroll
-    for (uint32_t u = 0; u < kA; u++) {
-      if (t + u * NT < nt) {
-        ldsu8* const col = B.nT + gj[u];
-        if (gp[u] == 0)
-          for (uint32_t r = 0; r < ps[u]; r++) col[r * kRS] = 0;
-        for (uint32_t r = ps[u]; r < c1[u]; r++) col[r * kRS] = (uint8_t)(gp[u] + 1);
+      for (uint32_t s4 = 0; s4 < 4; s4++) {
+        const uint32_t y = sr[(4 * g4 + s4) * (kSR / 4) + min(lane, kSR / 4 - 1)];
+        x[s4] = lane < kSR / 4 ? y : 0u;
       }
+      uint32_t out[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (uint32_t s4 = 0; s4 < 4; s4++) {
+        const uint32_t b0 = x[s4] & 0xffu, m1 = max(b0, (x[s4] >> 8) & 0xffu), m2 = max(m1, (x[s4] >> 16) & 0xffu),
+                       m3 = max(m2, x[s4] >> 24);
+        const uint32_t carry = wave_shr1(wave_incl_max(m3));
+        out[0] |= max(b0, carry) << (8 * s4);
+        out[1] |= max(m1, carry) << (8 * s4);
+        out[2] |= max(m2, carry) << (8 * s4);
+        out[3] |= max(m3, carry) << (8 * s4);
+      }
+#pragma unroll
+      for (uint32_t k = 0; k < 4; k++)
+        if (4 * lane + k <= nm) *(ldsu32*)(B.nT + (4 * lane + k) * kRS + 4 * g4) = out[k];
     }
   }
   fast_sync<NW>();
@@ -2056,29 +2097,29 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
   }
   fast_sync<NW>();
   PROF_T(b5);
-  // ---- E: Welford along each list (waves 0-2, lane = column), two blocks of four entries in
-  // flight.  The division ((v - mean) * w) / W is the hardware's own sequence -- v_rcp and two
-  // Newton steps on W, q0 = t * y, r = fma(-W, q0, t), q = fma(r, y, q0), v_div_fixup -- without
-  // v_div_scale, which rescales nothing for these operands: W is an integer in [1, 2^40], every
-  // value and mean 0 or of magnitude [2^-400, 2^400] (checked in A), so t = 0 or 2^-505 <= |t| <=
-  // 2^425 (the quotient exponent stays far from the range where the hardware rescales).  The W
-  // chain and the reciprocals do not depend on the means, so they are computed ahead of them.
-  // A block holding a Z entry (column 0 only) takes the exact Z walk: the chunk's Z temps start
-  // a fresh centroid (main 0, the column so far, waiting) and main 0 joins it after the chunk's
-  // last Z temp.
+  // ---- E: Welford along each list, two blocks of four entries in flight.  The division
+  // ((v - mean) * w) / W is the hardware's own sequence -- v_rcp and two Newton steps on W, q0 = t *
+  // y, r = fma(-W, q0, t), q = fma(r, y, q0), v_div_fixup -- without v_div_scale, which rescales
+  // nothing for these operands: W is an integer in [1, 2^40], every value and mean 0 or of
+  // magnitude [2^-400, 2^400] (checked in A), so t = 0 or 2^-505 <= |t| <= 2^425, far from the
+  // exponents where the hardware rescales (a numerator below 1e-250 is caught and the batch
+  // dropped).  The W chain and the reciprocals do not depend on the means: each block's are
+  // issued ahead of its mean chain (sched_barrier), so only the seven dependent operations of
+  // the mean update stay on the critical path.
+  // Columns 1.. on waves 0-2 (lane = column); column 0, whose list also holds the Z temps, on
+  // lane 0 of wave 3 beside them: a chunk's Z temps start a fresh centroid (main 0, the column
+  // so far, waiting) and main 0 joins it after the chunk's last Z temp.
   PROF_T(e0);
   if (wv < 3) {
-    const bool col = i < nm;
+    const bool col = i >= 1 && i < nm;
     const uint32_t ic = min(i, nm - 1), o0 = B.off[ic], o1 = B.off[ic + 1];
     const double mm0 = L.mm[ic], mw0 = L.mw[ic];
     const uint32_t o = col ? o0 : 0u, m = col ? o1 - o0 : 0u;
-    double mean = col ? mm0 : 0.0, W = col ? mw0 : 1.0, lo = mean, hi = mean, sm = 0.0, sw = 0.0;
-    uint32_t gain = 0, prev = 0;
+    double mean = col ? mm0 : 0.0, W = col ? mw0 : 1.0, lo = mean, hi = mean;
+    uint32_t gain = 0;
     bool tiny = false;  // a numerator near the hardware's rescaling range (then no batch)
-    uint32_t mmax = m;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) mmax = max(mmax, (uint32_t)__shfl_xor((int)mmax, d, 64));
-    mmax = __builtin_amdgcn_readfirstlane(mmax);
+    uint32_t mmax = wave_incl_max(m);
+    mmax = __builtin_amdgcn_readlane(mmax, 63);
     auto ld = [&](uint32_t q, double (&v)[4], uint32_t (&w)[4]) {
 #pragma unroll
       for (uint32_t u = 0; u < 4; u++) {
@@ -2093,79 +2134,38 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
 #pragma unroll 1
     for (uint32_t q = 0; q < mmax; q += 4) {
       ld(q + 4, v1, w1);
-      bool zb = false;
-      if (i == 0) {  // (only column 0's list holds Z temps)
+      double Wn[4], y[4];
+      bool in[4];
 #pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
-          const uint32_t x = B.lj[o + min(q + u, m ? m - 1 : 0u)];
-          zb |= q + u < m && (x & 0x80u);
-        }
+      for (uint32_t u = 0; u < 4; u++) {  // the W chain and the reciprocals
+        in[u] = q + u < m;
+        Wn[u] = dadd(u ? Wn[u - 1] : W, in[u] ? (double)w0[u] : 0.0);
+        const double r0 = __builtin_amdgcn_rcp(Wn[u]);
+        const double e0_ = __builtin_fma(-Wn[u], r0, 1.0);
+        const double r1 = __builtin_fma(r0, e0_, r0);
+        const double e1_ = __builtin_fma(-Wn[u], r1, 1.0);
+        y[u] = __builtin_fma(r1, e1_, r1);
       }
-      if (__builtin_expect(__any(zb), 0)) {
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
-          if (q + u < m) {
-            const uint32_t e = B.lj[o + q + u], nx = q + u + 1 < m ? B.lj[o + q + u + 1] : 0u;
-            const bool z = (e & 0x80u) != 0u;
-            const bool zstart = z && (q + u == 0 || !(prev & 0x80u) || ((prev ^ e) & 63u));
-            const bool zend = z && (!(nx & 0x80u) || ((nx ^ e) & 63u));
-            const double w = (double)w0[u];
-            if (zstart) {
-              sm = mean;
-              sw = W;
-              mean = v0[u];
-              W = w;
-            } else {
-              W = dadd(W, w);
-              mean = dadd(mean, ddiv(dmul(dsub(v0[u], mean), w), W));
-            }
-            if (zend) {
-              W = dadd(W, sw);
-              mean = dadd(mean, ddiv(dmul(dsub(sm, mean), sw), W));
-            }
-            if (!z || zend) {
-              lo = __builtin_fmin(lo, mean);
-              hi = __builtin_fmax(hi, mean);
-            }
-            gain += w0[u];
-            B.lv[o + q + u] = mean;
-            B.lw[o + q + u] = gain;
-            prev = e;
-          }
+      for (uint32_t u = 0; u < 4; u++) {  // the mean chain
+        const double tq = dmul(dsub(v0[u], mean), (double)w0[u]);
+        tiny |= tq != 0.0 && __builtin_fabs(tq) < 1e-250;
+        const double q0 = dmul(tq, y[u]);
+        const double rr = __builtin_fma(-Wn[u], q0, tq);
+        const double qq = __builtin_amdgcn_div_fixup(__builtin_fma(rr, y[u], q0), Wn[u], tq);
+        const double m2 = dadd(mean, qq);
+        mean = in[u] ? m2 : mean;
+        gain += in[u] ? w0[u] : 0u;
+        if (in[u]) {
+          B.lv[o + q + u] = mean;
+          B.lw[o + q + u] = gain;
         }
-      } else {
-        double Wn[4], y[4];
-        bool in[4];
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {  // the W chain and the reciprocals, ahead of the means
-          in[u] = q + u < m;
-          Wn[u] = dadd(u ? Wn[u - 1] : W, in[u] ? (double)w0[u] : 0.0);
-          const double r0 = __builtin_amdgcn_rcp(Wn[u]);
-          const double e0_ = __builtin_fma(-Wn[u], r0, 1.0);
-          const double r1 = __builtin_fma(r0, e0_, r0);
-          const double e1_ = __builtin_fma(-Wn[u], r1, 1.0);
-          y[u] = __builtin_fma(r1, e1_, r1);
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
-          const double tq = dmul(dsub(v0[u], mean), (double)w0[u]);
-          tiny |= tq != 0.0 && __builtin_fabs(tq) < 1e-250;
-          const double q0 = dmul(tq, y[u]);
-          const double rr = __builtin_fma(-Wn[u], q0, tq);
-          const double qq = __builtin_amdgcn_div_fixup(__builtin_fma(rr, y[u], q0), Wn[u], tq);
-          const double m2 = dadd(mean, qq);
-          mean = in[u] ? m2 : mean;
-          gain += in[u] ? w0[u] : 0u;
-          if (in[u]) {
-            B.lv[o + q + u] = mean;
-            B.lw[o + q + u] = gain;
-          }
-          lo = __builtin_fmin(lo, mean);
-          hi = __builtin_fmax(hi, mean);
-        }
-        W = Wn[3];
-        prev = 0u;  // (no Z entry in the block: the next Z entry starts a centroid)
+        lo = __builtin_fmin(lo, mean);
+        hi = __builtin_fmax(hi, mean);
       }
+      __builtin_amdgcn_sched_barrier(0);
+      W = Wn[3];
 #pragma unroll
       for (uint32_t u = 0; u < 4; u++) {
         v0[u] = v1[u];
@@ -2177,10 +2177,45 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
       B.hi[i] = hi;
     }
     if (tiny) B.ctl[4] = 1u;
-    PROF_T(e1);
-    PROF_ADD(14, e0, e1);
-    PROF_ADDW(36, e0, e1);
+  } else if (lane == 0) {
+    // column 0: the exact walk, Z temps included (its list is short: the lowest centroid's)
+    const uint32_t o = 0, m = B.off[1];
+    double mean = L.mm[0], W = L.mw[0], lo = mean, hi = mean, sm = 0.0, sw = 0.0;
+    uint32_t gain = 0, prev = 0;
+    for (uint32_t q = 0; q < m; q++) {
+      const uint32_t e = B.lj[o + q], nx = q + 1 < m ? B.lj[o + q + 1] : 0u;
+      const double v = B.lv[o + q], w = (double)B.lw[o + q];
+      const bool z = (e & 0x80u) != 0u;
+      const bool zstart = z && (q == 0 || !(prev & 0x80u) || ((prev ^ e) & 63u));
+      const bool zend = z && (!(nx & 0x80u) || ((nx ^ e) & 63u));
+      if (zstart) {
+        sm = mean;
+        sw = W;
+        mean = v;
+        W = w;
+      } else {
+        W = dadd(W, w);
+        mean = dadd(mean, ddiv(dmul(dsub(v, mean), w), W));
+      }
+      if (zend) {
+        W = dadd(W, sw);
+        mean = dadd(mean, ddiv(dmul(dsub(sm, mean), sw), W));
+      }
+      if (!z || zend) {
+        lo = __builtin_fmin(lo, mean);
+        hi = __builtin_fmax(hi, mean);
+      }
+      gain += B.lw[o + q];
+      B.lv[o + q] = mean;
+      B.lw[o + q] = gain;
+      prev = e;
+    }
+    B.lo[0] = lo;
+    B.hi[0] = hi;
   }
+  PROF_T(e1);
+  PROF_ADD(14, e0, e1);
+  PROF_ADDW(36, e0, e1);
   // C2 of wave 2's own columns (128..), after its (short, tail) lists
   if (wv == 2 && i < nm) c2_column(i, ra, re);
   fast_sync<NW>();
@@ -2467,7 +2502,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     uint32_t c = 0;
     while (c < sp.npure) {
       const uint32_t left = sp.npure - c;
-      if (!(fok && nm >= 1 && nm <= kBM && left >= 2 && mainW >= kBatchMinW && tcap <= kBTmax)) {
+      if (!(fok && nm >= 1 && nm <= kBM && left >= 2 && mainW >= kBatchMinW && tcap <= kBTmax && 8 * tcap >= kSR)) {
         // not (yet) batchable: a run of single merges, then look again
         const uint32_t c1 = min(sp.npure, c + kBatchBackoff);
         PROF_T(s3);

@@ -37,6 +37,10 @@ constexpr int kProbe = 32;
 // (alone the two are 11.6 vs 10.3 ms).  Gauges keep the partition: their direct max-position
 // aggregation took 28.5 ms there against ~6.5 (alone 5.8 vs 3.3 ms).
 constexpr bool kScalarDirect = true;
+#ifndef VN_COUNTER_RUNS
+#define VN_COUNTER_RUNS 1
+#endif
+constexpr bool kCounterRuns = VN_COUNTER_RUNS;  // k_counter_runs below (else k_scalar_direct)
 constexpr bool kGaugeDirect = false;
 
 struct CounterSrc {
@@ -171,6 +175,68 @@ __global__ __launch_bounds__(kAggThreads) void k_scalar_direct(uint64_t n, const
   }
 }
 
+// Counters by key range (the default): one stable partition pass by the slot's high bits puts
+// every record of a range of 2^shift slots in one bucket (partition.h), then each block takes a
+// kRunChunk slice of the partitioned batch and sums it bucket run by bucket run into an LDS
+// array indexed by the slot's low bits -- no hashing, no probing -- and adds each touched slot's
+// partial to its device word once per slice.  Device atomics: at most 2^shift per slice (about
+// 6M for a 400M-record C4 batch), against one per distinct slot per 16384 records (about 180M)
+// for k_scalar_direct, whose requests all go to the memory side.
+constexpr int kRunThreads = 512;
+constexpr uint64_t kRunChunk = 131072;
+constexpr uint32_t kRunMaxW = 4096;  // slots per bucket (LDS: 8 B + 1 B each)
+constexpr int kRunUnroll = 4;
+
+__global__ __launch_bounds__(kRunThreads) void k_counter_runs(uint64_t n, const uint32_t* __restrict__ pk,
+                                                              const uint64_t* __restrict__ pp,
+                                                              const uint32_t* __restrict__ offsets, uint32_t nparts,
+                                                              int shift, uint64_t* __restrict__ cval,
+                                                              uint32_t* __restrict__ ctouch) {
+  __shared__ unsigned long long s_sum[kRunMaxW];
+  __shared__ uint8_t s_hit[kRunMaxW];
+  const uint32_t W = 1u << shift, t = threadIdx.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kRunChunk, c1 = min(n, c0 + kRunChunk);
+  for (uint64_t i = c0; i < c1;) {
+    // the bucket of record i and where its run ends in this slice (every thread alike)
+    const uint32_t d = pk[i] >> shift;
+    const uint64_t e = min(c1, (uint64_t)offsets[(uint64_t)(d + 1) * nparts]);
+    for (uint32_t j = t; j < W; j += kRunThreads) {
+      s_sum[j] = 0;
+      s_hit[j] = 0;
+    }
+    __syncthreads();
+    uint64_t r = i + t;
+    for (; r + (kRunUnroll - 1) * kRunThreads < e; r += kRunUnroll * kRunThreads) {
+      uint32_t k[kRunUnroll];
+      uint64_t p[kRunUnroll];
+#pragma unroll
+      for (int u = 0; u < kRunUnroll; u++) {
+        k[u] = pk[r + u * kRunThreads] & (W - 1);
+        p[u] = pp[r + u * kRunThreads];
+      }
+#pragma unroll
+      for (int u = 0; u < kRunUnroll; u++) {
+        atomicAdd(&s_sum[k[u]], (unsigned long long)p[u]);
+        s_hit[k[u]] = 1;
+      }
+    }
+    for (; r < e; r += kRunThreads) {
+      const uint32_t k = pk[r] & (W - 1);
+      atomicAdd(&s_sum[k], (unsigned long long)pp[r]);
+      s_hit[k] = 1;
+    }
+    __syncthreads();
+    const uint32_t sb = d << shift;
+    for (uint32_t j = t; j < W; j += kRunThreads)
+      if (s_hit[j]) {
+        atomicAdd((unsigned long long*)&cval[sb + j], s_sum[j]);
+        ctouch[sb + j] = 1;
+      }
+    __syncthreads();  // the table is cleared for the next run only after every thread read it
+    i = e;
+  }
+}
+
 // gauges of the direct path: the winning position indexes the caller's value array
 __global__ void k_gauge_resolve_direct(uint32_t cap, uint64_t base, const uint64_t* __restrict__ gseq,
                                        const double* __restrict__ val, double* __restrict__ gval) {
@@ -200,6 +266,18 @@ __global__ void k_counter_import(uint64_t n, const uint32_t* __restrict__ slot, 
 
 void ingest_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate) {
   if (!n) return;
+  // buckets of 2^shift slots, at most 256 of them (one partition pass)
+  const uint32_t cap = std::max<uint32_t>(e->cap[VN_COUNTER], 1u);
+  int shift = 0;
+  while (((cap - 1u) >> shift) >= 256u) shift++;
+  if (kCounterRuns && (1u << shift) <= kRunMaxW) {
+    RadixStats* rs = e->timing ? &e->rstat_c : nullptr;
+    const uint32_t nparts =
+        partition_pass(CounterSrc{slot, val, rate}, KV64Dst{e->pk, e->pp}, n, shift, *e->side_rs, e->side, rs, 16 + 12);
+    hipLaunchKernelGGL(k_counter_runs, dim3((uint32_t)((n + kRunChunk - 1) / kRunChunk)), dim3(kRunThreads), 0,
+                       e->side, n, e->pk, e->pp, e->side_rs->offsets, nparts, shift, (uint64_t*)e->cval, e->ctouch);
+    return;
+  }
   if (kScalarDirect) {
     hipLaunchKernelGGL(k_scalar_direct<false>, dim3(blocks_for(n, kAggChunk)), dim3(kAggThreads), 0, e->side, n,
                        slot, val, rate, 0, (uint64_t*)e->cval, e->ctouch);
