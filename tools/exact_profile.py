@@ -62,13 +62,16 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     # merge_batch phases (histo_exact.hip): totals, A pos search, B n table + offsets,
     # C1+E+C2 lists / Welford / bounds, F decisions + bound tests, G flagged tests, H commit
     for i, nme in zip((16, 17, 18, 19, 15, 20, 21, 48, 13), ("totals", "A_pos", "B_ntable", "C_offsets_K_bounds",
-                                                            "D_lists", "E_welford", "F_decisions", "G_flagged",
+                                                            "D_lists", "E_welford_C2", "F_decisions", "G_flagged",
                                                             "H_commit")):
         out["batch_cyc_" + nme] = round(p[i] / nb, 1)
     out["batch_cyc_column0_welford"] = round(p[14] / nb, 1)
     out["batch_cyc_call"] = round(p[27] / nb, 1)
-    for base, nme in ((36, "E"), (40, "C2")):
+    for base, nme in ((36, "E"), (40, "C_rows"), (44, "C2_queue")):
         out["batch_cyc_" + nme + "_per_wave"] = [round(p[base + w] / nb, 1) for w in range(4)]
+    out["study_columns"] = p[52]
+    out["study_cheap_certified"] = p[53]
+    out["study_exact_certified"] = p[54]
     out["singles_after_reject"] = p[29]
     out["singles_after_reject_cyc"] = p[28]
     out["singles_unbatchable"] = p[31]

@@ -40,6 +40,11 @@ __host__ __device__ inline size_t exact_smem_bytes_hd(uint32_t capc, uint32_t tc
          sizeof(uint16_t) * (levels > 9u ? levels : 9u) * JW + 16 + VN_EXACT_LDS_PAD;
 }
 
+#ifdef VN_ASM_MARK  // (reading the assembly: a comment at a phase boundary)
+#define ASM_MARK(x) asm volatile("; MARK " x)
+#else
+#define ASM_MARK(x)
+#endif
 #ifdef VN_EXACT_PROF
 // profiling build only (tools/exact_profile.py): cycles per merge phase of block 0
 __device__ unsigned long long g_exact_prof[64];
@@ -56,7 +61,14 @@ __device__ __forceinline__ long long prof_stamp() {  // a scheduling fence aroun
 // per wave (lane 0 of each wave of block 0): slot i + wave
 #define PROF_ADDW(i, a, b) \
   if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) atomicAdd(&g_exact_prof[(i) + (threadIdx.x >> 6)], (unsigned long long)((b) - (a)))
+// per wave: the number of lanes where pred holds
+#define PROF_CNT(i, pred)                                                                              \
+  {                                                                                                    \
+    const uint64_t _m = __ballot(pred);                                                                \
+    if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) atomicAdd(&g_exact_prof[i], (unsigned long long)__popcll(_m)); \
+  }
 #else
+#define PROF_CNT(i, pred)
 #define PROF_ADDW(i, a, b)
 #define PROF_T(v)
 #define PROF_ADD(i, a, b)
@@ -1211,6 +1223,24 @@ __device__ __noinline__ void walk_flags(const FastLds F, uint32_t m, double k0) 
   }
 }
 
+// a double from another lane by DPP (two dword moves); lanes without a source take ident
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_d(double v, double ident) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v), z = (uint64_t)__double_as_longlong(ident);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)z, (int)(uint32_t)b, CTRL, RM, 0xf, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(z >> 32), (int)(uint32_t)(b >> 32), CTRL, RM, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// inclusive sum over the wave's 64 lanes (row shifts, then the row broadcasts of lanes 15 and 31)
+__device__ __forceinline__ double wave_incl_add_d(double v) {
+  v = dadd(v, dpp_d<0x111, 0xf>(v, 0.0));
+  v = dadd(v, dpp_d<0x112, 0xf>(v, 0.0));
+  v = dadd(v, dpp_d<0x114, 0xf>(v, 0.0));
+  v = dadd(v, dpp_d<0x118, 0xf>(v, 0.0));
+  v = dadd(v, dpp_d<0x142, 0xa>(v, 0.0));
+  return dadd(v, dpp_d<0x143, 0xc>(v, 0.0));
+}
 // mp[0..nm] from the main weights (wave 0); misc[1] = every weight an integer and their sum
 // equal to mainW (then every prefix is exact)
 __device__ __noinline__ void prefix_main_w0(const Lds L, const FastLds F, uint32_t nm, double mainW) {
@@ -1221,11 +1251,18 @@ __device__ __noinline__ void prefix_main_w0(const Lds L, const FastLds F, uint32
     const uint32_t j = b + lane;
     const double w = j < nm ? L.mw[j] : 0.0;
     ok &= is_int_weight(w);
+    // (integers: exact in any order).  DPP reads other lanes' registers, so it needs every lane
+    // of the wave active: a caller that reaches here with some masked off (the compiler may
+    // keep a uniform condition as a lane mask) takes the shuffle scan instead
     double v = w;
+    if (__builtin_amdgcn_read_exec() == ~0ull) {
+      v = wave_incl_add_d(w);
+    } else {
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const double o = __shfl_up(v, d, 64);
-      v = (int)lane >= d ? dadd(v, o) : v;
+      for (int d = 1; d < 64; d <<= 1) {
+        const double o = __shfl_up(v, d, 64);
+        v = (int)lane >= d ? dadd(v, o) : v;
+      }
     }
     if (j < nm) F.mp[j] = dadd(carry, dsub(v, w));
     carry = dadd(carry, rl_d(v, 63));
@@ -1695,7 +1732,7 @@ struct BatchLds {
   ldsf64* brT;      // [kBB] 1 / bT
   ldsf64* lo;       // [kBM] each column's lowest mean over the batch
   ldsf64* hi;       // [kBM] ... highest
-  ldsf64* kb;       // [3][kBN] k(min qe), k(max qb), k(min qb) per column
+  ldsf64* kb;       // [3][kBN] min qe, max qb, min qb per column (F takes k of them)
   ldsf64* lv;       // [kBB * tcap] the lists: each column's temps' means in (chunk, position)
                     //              order; the Welford pass overwrites each with the mean after it
   ldsu32* lw;       // [kBB * tcap] ... their weights; overwritten with the weight gained so far
@@ -1712,7 +1749,7 @@ struct BatchLds {
 
 __host__ __device__ inline uint32_t batch_bytes(uint32_t tcap) {
   const uint32_t nl = kBB * tcap;
-  return 12u * kRing * tcap + 16u * kBB + 16u * kBM + 24u * kBN + 8u * nl + 4u * nl + 4u * (kBN + 1) + 32u +
+  return 12u * kRing * tcap + 16u * kBB + 16u * kBM + 24u * kBN + 8u * (nl + 1) + 4u * (nl + 1) + 4u * (kBN + 1) + 32u +
          2u * kBM + nl + nl + 16u + kBN * kRS + kBM * kRS + 16u;
 }
 __host__ __device__ inline uint32_t batch_offset(uint32_t capc, uint32_t tcap) {
@@ -1729,9 +1766,9 @@ __device__ __forceinline__ BatchLds batch_layout(char* p, uint32_t tcap) {
   B.hi = B.lo + kBM;
   B.kb = B.hi + kBM;
   B.lv = B.kb + 3 * kBN;
-  B.rp = (ldsu32*)(B.lv + nl);
+  B.rp = (ldsu32*)(B.lv + nl + 1);  // (lv[nl], lw[nl]: where E's idle lanes store)
   B.lw = B.rp + kRing * tcap;
-  B.off = B.lw + nl;
+  B.off = B.lw + nl + 1;
   B.ctl = B.off + (kBN + 1);
   B.flagged = (ldsu16*)(B.ctl + 8);
   B.lj = (ldsu8*)(B.flagged + kBM);
@@ -1741,9 +1778,6 @@ __device__ __forceinline__ BatchLds batch_layout(char* p, uint32_t tcap) {
   return B;
 }
 
-__device__ __forceinline__ double k_close(double delta, double q) {
-  return delta * (asin(dsub(dmul(2.0, q), 1.0)) * (1.0 / kPi) + 0.5);
-}
 __device__ __forceinline__ void lds_min(ldsu32* p, uint32_t v) { __atomic_fetch_min(p, v, __ATOMIC_RELAXED); }
 __device__ __forceinline__ uint32_t lds_inc(ldsu32* p) { return __atomic_fetch_add(p, 1u, __ATOMIC_RELAXED); }
 
@@ -1794,6 +1828,37 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// inclusive sum over the 16 lanes of each DPP row (row_shr 1, 2, 4, 8; lanes without a source add 0)
+__device__ __forceinline__ uint32_t row_incl_add(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  return v;
+}
+// a double from lane l - n of the same row (ident where there is none), as two dword moves
+template <int CTRL>
+__device__ __forceinline__ double row_shr_d(double v, double ident) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v), z = (uint64_t)__double_as_longlong(ident);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)z, (int)(uint32_t)b, CTRL, 0xf, 0xf, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(z >> 32), (int)(uint32_t)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// min / max over each row's 16 lanes, complete in lane 15 of the row
+__device__ __forceinline__ double row_min_d(double v) {
+  v = __builtin_fmin(v, row_shr_d<0x111>(v, 2.0));
+  v = __builtin_fmin(v, row_shr_d<0x112>(v, 2.0));
+  v = __builtin_fmin(v, row_shr_d<0x114>(v, 2.0));
+  return __builtin_fmin(v, row_shr_d<0x118>(v, 2.0));
+}
+__device__ __forceinline__ double row_max_d(double v) {
+  v = __builtin_fmax(v, row_shr_d<0x111>(v, -1.0));
+  v = __builtin_fmax(v, row_shr_d<0x112>(v, -1.0));
+  v = __builtin_fmax(v, row_shr_d<0x114>(v, -1.0));
+  return __builtin_fmax(v, row_shr_d<0x118>(v, -1.0));
+}
+
 // |x| is 0 or within [2^-400, 2^400]: the Welford division of the batch then never needs
 // v_div_scale's rescaling (see merge_batch, E)
 __device__ __forceinline__ bool div_safe(double x) {
@@ -1805,13 +1870,13 @@ __device__ __forceinline__ bool div_safe(double x) {
 // hold the digest after the committed merges.  Every phase is written for latency at one wave
 // per SIMD: a thread's independent LDS loads issue together and are waited for once.
 template <int NW>
-__device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds L, const FastLds F, const BatchLds B,
+__device__ __forceinline__ BatchResult merge_batch(const double delta, const double sin_hi, const double sin_lo,
+                                                   const Lds L, const FastLds F, const BatchLds B,
                                                    const uint32_t nm_in, double& mainW, const uint32_t c_in,
                                                    uint32_t b, const uint32_t tcap) {
   // (wave-uniform values in scalar registers: every chunk address below is then scalar math)
   const uint32_t nm = __builtin_amdgcn_readfirstlane(nm_in), c = __builtin_amdgcn_readfirstlane(c_in);
   constexpr uint32_t NT = 64 * NW;
-  constexpr double kHi = 1.0 + kBand, kLo = 1.0 - kBand;
   constexpr uint32_t kA = (kBB * kBTmax + NT - 1) / NT;  // temps per thread (all threads)
   static_assert(NW == 4, "column lanes on waves 0-2, bounds on waves 2-3");
   static_assert(kBM <= 192 && kBM >= 128, "one lane of waves 0-2 per column; wave 3 takes columns 64..127");
@@ -1852,10 +1917,14 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
       B.ctl[2] = nb;
       B.ctl[3] = nb;
       B.ctl[4] = 0u;
+      B.ctl[5] = 0u;  // C2's next column group
+      B.kb[kBN + nm] = 1.0;  // the end (q = 1)
+      B.kb[2 * kBN + nm] = 1.0;
     }
   }
   fast_sync<NW>();
   PROF_T(b1);
+  ASM_MARK("A_BEGIN");
   b = __builtin_amdgcn_readfirstlane(B.ctl[2]);
   if (b < 2) {
     fast_sync<NW>();
@@ -1912,6 +1981,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
     fast_sync<NW>();  // the fast division's range: no batch
     return BatchResult{0u, true};
   }
+  ASM_MARK("B_BEGIN");
   // ---- B: the n table.  n[j][i] = #temps of chunk j with pos <= i, a step function of i: the last
   // temp p of each run of equal pos c writes p + 1 at column c of chunk j's run-end row (B1); a
   // wave then takes four chunks at a time, a lane four columns, and max-scans each row over the
@@ -1968,47 +2038,95 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
       w[2 * q + 1] = (uint32_t)(x >> 32);
     }
   };
-  auto byte_at = [](const uint32_t (&w)[kW], uint32_t j) { return (w[j >> 2] >> (8 * (j & 3))) & 0xffu; };
   auto wmask = [&](uint32_t q) {  // the bytes of word q that are chunks < b
     const uint32_t v = b > 4 * q ? min(b - 4 * q, 4u) : 0u;
     return v >= 4 ? 0xffffffffu : ((1u << (8 * v)) - 1u);
   };
-  // C2: k bounds of column ci (min / max over the batch of q = P / T from exact integer prefixes)
-  auto c2_column = [&](uint32_t ci, const uint32_t (&ra)[kW], const uint32_t (&re)[kW]) {
-    const double mp0 = F.mp[ci], mpw = dadd(F.mp[ci], L.mw[ci]);
-    double qbmin = 2.0, qbmax = -1.0, qemin = 2.0;
-    uint32_t C = 0, X = 0;  // sum of s0 (temps before main ci), of s1 (before main ci + 1)
-    constexpr uint32_t kP = 16;
+  // C2: the q bounds of four columns at once (q = P / T from exact integer prefixes; k is
+  // increasing, so F's k bounds are k of these), one DPP row per column: lane q of the row takes
+  // chunks 4q .. 4q+3 (their n bytes one dword of each row), the prefixes over the chunks a row
+  // scan, the min / max a row reduction.  Same integers and operations per chunk as a sequential
+  // walk over the chunks, so the same bounds bit for bit
+  // (two groups per queue entry, interleaved: their LDS round trips overlap)
+  constexpr uint32_t kC2H = 2, kC2Cols = 4 * kC2H;
+  const uint32_t c2q = lane & 15;
+  uint32_t c2base[4];
+  double c2rT[4];
+  bool c2j[4];
 #pragma unroll
-    for (uint32_t j0 = 0; j0 < kBB; j0 += kP) {
-      if (j0 >= b) break;
-      uint32_t sa[kP], se[kP];
-      double rT[kP];
+  for (uint32_t u = 0; u < 4; u++) {  // the lane's chunks: the same in every group
+    const uint32_t j = 4 * c2q + u, jc = min(j, b - 1);
+    c2j[u] = j < b;
+    c2base[u] = sbase(jc);
+    c2rT[u] = B.brT[jc];
+  }
+  auto c2_group = [&](uint32_t g0) {
+    ASM_MARK("C2_GROUP");
+    uint32_t wa[kC2H], we[kC2H], ci[kC2H];
+    bool cok[kC2H];
+    double mp0[kC2H], mpw[kC2H];
 #pragma unroll
-      for (uint32_t u = 0; u < kP; u++) {
-        const uint32_t j = min(j0 + u, b - 1);
-        sa[u] = tw_of(j, byte_at(ra, j0 + u));
-        se[u] = tw_of(j, byte_at(re, j0 + u));
-        rT[u] = B.brT[j];
+    for (uint32_t h = 0; h < kC2H; h++) {
+      ci[h] = g0 + 4 * h + (lane >> 4);
+      cok[h] = ci[h] < nm;
+      const uint32_t cc = min(ci[h], nm - 1);
+      wa[h] = *(const ldsu32*)(B.nT + cc * kRS + 4 * c2q);
+      we[h] = *(const ldsu32*)(B.nT + (cc + 1) * kRS + 4 * c2q);
+      mp0[h] = F.mp[cc];
+      mpw[h] = L.mw[cc];
+    }
+    uint32_t sa[kC2H][4], se[kC2H][4];
+#pragma unroll
+    for (uint32_t h = 0; h < kC2H; h++)
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        const uint32_t na = (wa[h] >> (8 * u)) & 0xffu, ne = (we[h] >> (8 * u)) & 0xffu;
+        const uint32_t x = B.rp[c2base[u] + (na >= tcap ? 0u : na)] >> 16;
+        const uint32_t y = B.rp[c2base[u] + (ne >= tcap ? 0u : ne)] >> 16;
+        const bool ok = cok[h] && c2j[u];
+        sa[h][u] = ok && na ? x : 0u;
+        se[h][u] = ok && ne ? y : 0u;
       }
 #pragma unroll
-      for (uint32_t u = 0; u < kP; u++) {
-        if (j0 + u < b) {
-          C += sa[u];
-          // P = mp0 + C; qe = (P + W) / T with W = w0 + the gain before chunk j = w0 + X - (C - sa)
-          const double qe = dadd(mpw, (double)(X + sa[u])) * rT[u];
-          qemin = __builtin_fmin(qemin, qe);
-          const double qb = dadd(mp0, (double)C) * rT[u];
-          qbmin = __builtin_fmin(qbmin, qb);
-          qbmax = __builtin_fmax(qbmax, qb);
-          X += se[u];
-        }
+    for (uint32_t h = 0; h < kC2H; h++) {
+      mpw[h] = dadd(mp0[h], mpw[h]);
+      const uint32_t ta = sa[h][0] + sa[h][1] + sa[h][2] + sa[h][3], te = se[h][0] + se[h][1] + se[h][2] + se[h][3];
+      uint32_t C = row_incl_add(ta) - ta, X = row_incl_add(te) - te;  // sums over the chunks before 4q
+      double qemin = 2.0, qbmin = 2.0, qbmax = -1.0;
+#pragma unroll
+      for (uint32_t u = 0; u < 4; u++) {
+        C += sa[h][u];
+        // P = mp0 + C; qe = (P + W) / T with W = w0 + the gain before chunk j = w0 + X - (C - sa)
+        const double qe = dadd(mpw[h], (double)(X + sa[h][u])) * c2rT[u];
+        const double qb = dadd(mp0[h], (double)C) * c2rT[u];
+        X += se[h][u];
+        const bool ok = cok[h] && c2j[u];
+        qemin = __builtin_fmin(qemin, ok ? qe : 2.0);
+        qbmin = __builtin_fmin(qbmin, ok ? qb : 2.0);
+        qbmax = __builtin_fmax(qbmax, ok ? qb : -1.0);
+      }
+      qemin = row_min_d(qemin);
+      qbmin = row_min_d(qbmin);
+      qbmax = row_max_d(qbmax);
+      if (c2q == 15 && cok[h]) {
+        B.kb[ci[h]] = qemin;
+        B.kb[kBN + ci[h]] = ci[h] ? qbmax : 0.0;  // (column 0 starts at q = 0: with Z temps or main 0 itself)
+        B.kb[2 * kBN + ci[h]] = ci[h] ? qbmin : 0.0;
       }
     }
-    if (!ci) qbmin = qbmax = 0.0;  // (column 0 starts at q = 0: with Z temps or main 0 itself)
-    B.kb[ci] = k_close(delta, __builtin_fmin(qemin, 1.0));  // (q <= 1: the reciprocal's rounding)
-    B.kb[kBN + ci] = k_close(delta, __builtin_fmin(qbmax, 1.0));
-    B.kb[2 * kBN + ci] = k_close(delta, __builtin_fmin(qbmin, 1.0));
+  };
+  // column groups taken from a queue by whichever wave is free (after its Welford lists); the
+  // next entry is drawn before this one is worked
+  auto c2_queue = [&]() {
+    uint32_t g = 0;
+    if (lane == 0) g = lds_inc(&B.ctl[5]);
+    g = kC2Cols * __builtin_amdgcn_readfirstlane(g);
+    while (g < nm) {
+      uint32_t gn = 0;
+      if (lane == 0) gn = lds_inc(&B.ctl[5]);
+      c2_group(g);
+      g = kC2Cols * __builtin_amdgcn_readfirstlane(gn);
+    }
   };
   const uint32_t i = t;
   uint32_t ra[kW], re[kW];
@@ -2042,26 +2160,6 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
     }
   }
   PROF_T(cw1);
-  // C2 on waves 2 (columns 0..63, then its own 128.. once its lists are done) and 3 (64..127)
-  if (wv == 3) {
-    const uint32_t ci = 64 + lane;
-    if (ci < nm) {
-      load_row(B.nT, ci, ra);
-      load_row(B.nT, ci + 1, re);
-      c2_column(ci, ra, re);
-    }
-    if (lane == 0) {  // the end
-      B.kb[kBN + nm] = k_close(delta, 1.0);
-      B.kb[2 * kBN + nm] = k_close(delta, 1.0);
-    }
-  } else if (wv == 2) {
-    if (lane < nm) {
-      uint32_t ra2[kW], re2[kW];
-      load_row(B.nT, lane, ra2);
-      load_row(B.nT, lane + 1, re2);
-      c2_column(lane, ra2, re2);
-    }
-  }
   PROF_T(cw2);
   PROF_ADDW(40, cw1, cw2);
   fast_sync<NW>();
@@ -2110,6 +2208,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
   // lane 0 of wave 3 beside them: a chunk's Z temps start a fresh centroid (main 0, the column
   // so far, waiting) and main 0 joins it after the chunk's last Z temp.
   PROF_T(e0);
+  const uint32_t nt_all = kBB * tcap;  // the lists' spare slot
   if (wv < 3) {
     const bool col = i >= 1 && i < nm;
     const uint32_t ic = min(i, nm - 1), o0 = B.off[ic], o1 = B.off[ic + 1];
@@ -2133,36 +2232,41 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
     ld(0, v0, w0);
 #pragma unroll 1
     for (uint32_t q = 0; q < mmax; q += 4) {
+      ASM_MARK("E_BODY");
       ld(q + 4, v1, w1);
-      double Wn[4], y[4];
+      double Wn[4], y[4], wd[4];
       bool in[4];
+      uint32_t at[4];
 #pragma unroll
       for (uint32_t u = 0; u < 4; u++) {  // the W chain and the reciprocals
         in[u] = q + u < m;
-        Wn[u] = dadd(u ? Wn[u - 1] : W, in[u] ? (double)w0[u] : 0.0);
+        const uint32_t wz = in[u] ? w0[u] : 0u;
+        wd[u] = (double)wz;
+        gain += wz;
+        at[u] = in[u] ? o + q + u : nt_all;  // (an idle lane's store goes to the spare slot: no branch)
+        Wn[u] = dadd(u ? Wn[u - 1] : W, wd[u]);
         const double r0 = __builtin_amdgcn_rcp(Wn[u]);
         const double e0_ = __builtin_fma(-Wn[u], r0, 1.0);
         const double r1 = __builtin_fma(r0, e0_, r0);
         const double e1_ = __builtin_fma(-Wn[u], r1, 1.0);
         y[u] = __builtin_fma(r1, e1_, r1);
+        B.lw[at[u]] = gain;
       }
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (uint32_t u = 0; u < 4; u++) {  // the mean chain
-        const double tq = dmul(dsub(v0[u], mean), (double)w0[u]);
+        const double tq = dmul(dsub(v0[u], mean), wd[u]);
         tiny |= tq != 0.0 && __builtin_fabs(tq) < 1e-250;
+        // the correctly rounded quotient tq / W: with no operand special (A's range checks, the
+        // tiny test above) v_div_fixup would return the fma's result unchanged
         const double q0 = dmul(tq, y[u]);
         const double rr = __builtin_fma(-Wn[u], q0, tq);
-        const double qq = __builtin_amdgcn_div_fixup(__builtin_fma(rr, y[u], q0), Wn[u], tq);
+        const double qq = __builtin_fma(rr, y[u], q0);
         const double m2 = dadd(mean, qq);
         mean = in[u] ? m2 : mean;
-        gain += in[u] ? w0[u] : 0u;
-        if (in[u]) {
-          B.lv[o + q + u] = mean;
-          B.lw[o + q + u] = gain;
-        }
-        lo = __builtin_fmin(lo, mean);
-        hi = __builtin_fmax(hi, mean);
+        B.lv[at[u]] = mean;
+        lo = mean < lo ? mean : lo;
+        hi = mean > hi ? mean : hi;
       }
       __builtin_amdgcn_sched_barrier(0);
       W = Wn[3];
@@ -2216,8 +2320,9 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
   PROF_T(e1);
   PROF_ADD(14, e0, e1);
   PROF_ADDW(36, e0, e1);
-  // C2 of wave 2's own columns (128..), after its (short, tail) lists
-  if (wv == 2 && i < nm) c2_column(i, ra, re);
+  c2_queue();
+  PROF_T(e2);
+  PROF_ADDW(44, e1, e2);
   fast_sync<NW>();
   PROF_T(b6);
   // ---- F: decisions per temp against the columns' mean ranges (the exact mean merge j saw
@@ -2247,9 +2352,27 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const Lds
   }
   if (i < nm) {
     if (i + 1 < nm && !(B.hi[i] <= B.lo[i + 1])) B.ctl[4] = 1u;
+    // k(a) - k(b) = delta / pi * (asin xa - asin xb) with x = 2q - 1: compared with kHi / kLo
+    // through D = asin xa - asin xb, sin D = xa cb - xb ca and cos D = ca cb + xa xb (c = sqrt(1 - x^2)
+    // = 2 sqrt(q (1 - q))); with cos D > 0, D is in (-pi/2, pi/2) where sin is increasing, so
+    // D > theta iff sin D > sin theta.  No arcsine: the band (kBand in k, about 3e-11 in sin)
+    // dwarfs these few roundings, and whatever it does not decide is tested exactly in G
+    auto xc = [](double qv, double& x, double& c) {
+      qv = __builtin_fmin(qv, 1.0);  // (q <= 1: the reciprocal's rounding)
+      x = 2.0 * qv - 1.0;
+      c = 2.0 * __builtin_sqrt(qv * (1.0 - qv));
+    };
+    double xa, ca, xb, cb;
     bool sure = true;
-    if (i >= 1) sure = B.kb[i] - B.kb[kBN + i - 1] > kHi;         // main i starts
-    sure = sure && B.kb[kBN + i + 1] - B.kb[2 * kBN + i] < kLo;  // its temps join
+    if (i >= 1) {  // main i starts: k(min qe_i) - k(max qb_i-1) > kHi
+      xc(B.kb[i], xa, ca);
+      xc(B.kb[kBN + i - 1], xb, cb);
+      sure = ca * cb + xa * xb > 0.0 && xa * cb - xb * ca > sin_hi;
+    }
+    // its temps join: k(max qb_i+1) - k(min qb_i) < kLo
+    xc(B.kb[kBN + i + 1], xa, ca);
+    xc(B.kb[2 * kBN + i], xb, cb);
+    sure = sure && ca * cb + xa * xb > 0.0 && xa * cb - xb * ca < sin_lo;
     if (!sure) B.flagged[lds_inc(&B.ctl[1])] = (uint16_t)i;
   }
   fast_sync<NW>();
@@ -2498,6 +2621,13 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       for (; e < ne; e += NT) stat(gv[e], __builtin_fabs(gw[e]), gw[e] > 0.0);
     }
 #endif
+    // sin(pi kHi / delta), sin(pi kLo / delta): merge_batch's certain k tests (F)
+    // (a short series: theta = pi k / delta is small, and the band dwarfs its error)
+    auto sin_small = [](double th) {
+      const double t2 = th * th;
+      return th * (1.0 - t2 / 6.0 * (1.0 - t2 / 20.0 * (1.0 - t2 / 42.0 * (1.0 - t2 / 72.0))));
+    };
+    const double sin_hi = sin_small(kPi * (1.0 + kBand) / mp.delta), sin_lo = sin_small(kPi * (1.0 - kBand) / mp.delta);
     uint32_t ring_lo = 0, ring_hi = 0;  // chunks [ring_lo, ring_hi) are in the ring (or on their way)
     uint32_t c = 0;
     while (c < sp.npure) {
@@ -2531,7 +2661,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       }
       ring_lo = max(c, ring_hi > kRing ? ring_hi - kRing : 0u);
       PROF_T(s0);
-      const BatchResult r = merge_batch<NW>(mp.delta, L, F, Bt, nm, mainW, c, b, tcap);
+      const BatchResult r = merge_batch<NW>(mp.delta, sin_hi, sin_lo, L, F, Bt, nm, mainW, c, b, tcap);
       PROF_T(s1);
       PROF_ADD(27, s0, s1);
       c += r.js;
