@@ -479,6 +479,9 @@ def main():
                     help="engines per GPU taking the windows in turn (window i + 1 ingested and combined while "
                          "window i's longest replays finish; one communicator per engine, the combines entered in "
                          "window order); 1: one engine, windows back to back; 0 (default): 2")
+    ap.add_argument("--reserved-cus", type=int, default=-1,
+                    help="CUs kept for the longest exact replays (vn_config.replay_reserved_cus); -1 (default): "
+                         "8 per engine taking windows in turn when there are several, else 0")
     ap.add_argument("--hot-stride", type=int, default=256,
                     help="hot-key detector: count every hot_stride-th record (vn_hot_detect)")
     ap.add_argument("--no-split", action="store_true", help="route every key by digest %% N (no hot keys)")
@@ -557,12 +560,15 @@ def main():
     # collectives (one communicator per engine) in the same order.
     D = max(1, args.pipeline if args.pipeline > 0 else 2)
 
+    reserved = args.reserved_cus if args.reserved_cus >= 0 else (8 * D if D > 1 else 0)
+
     def make_engine():
         e = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,
                      max_batch_records=max(stream.counts) + 1,
                      max_batch_member_bytes=stream.counts[3] * 11 + 64, device=local_rank,
                      exact_threshold=args.exact_threshold, hot_prefix=args.hot_prefix,
-                     piece_growth=args.piece_growth, split_max_records=max(stream.split_counts) + 1)
+                     piece_growth=args.piece_growth, split_max_records=max(stream.split_counts) + 1,
+                     replay_reserved_cus=reserved)
         if detect is not None:
             e.hot_detect(args.hot_stride)  # the live detector keeps counting inside the timed steps
         return e
@@ -746,6 +752,7 @@ def main():
                                   (world, sum(len(split[c]) for c in split)),
                    "split_keys": {"counter": len(split[0]), "histo": len(split[2]), "set": len(split[3])},
                    "windows_in_flight": D,
+                   "replay_reserved_cus": reserved,
                    "pipeline": ("%d engines per GPU take the windows in turn: window i + 1 is ingested while window "
                                 "i's longest replays finish; every window ingested, replayed and flushed inside the "
                                 "timed region (ms_per_step = timed region / steps; window_latency_ms = one window's "

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VN_ABI_VERSION 3
+#define VN_ABI_VERSION 4
 
 enum {
   VN_OK = 0,
@@ -80,6 +80,12 @@ typedef struct {
   /* compression of the micro-centroids a rank sends for its share of a split histogram's
    * piece (tools/split_study.py); 0 -> 5 * compression */
   double split_compression;
+  /* CUs kept for the longest exact replays (a hot key's chain is one workgroup of four waves,
+   * latency-bound for hundreds of ms): rounded up to whole groups of 8 (one CU per XCC), at
+   * most a quarter of the device; every other stream of this engine (and of its split engine)
+   * is masked off them.  0 (default): none -- the chains share their CUs with whatever else
+   * runs.  Worth it when windows overlap (several engines taking the windows in turn). */
+  uint32_t replay_reserved_cus;
 } vn_config;
 
 /* One ingest batch: per-class SoA streams in arrival order (the order ProcessMetric saw

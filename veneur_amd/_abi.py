@@ -57,7 +57,8 @@ class Config(C.Structure):
                 ("max_batch_records", C.c_uint64), ("max_batch_member_bytes", C.c_uint64),
                 ("histo_exact_threshold", C.c_uint32),
                 ("histo_hot_prefix", C.c_uint32), ("histo_piece_growth", C.c_uint32),
-                ("split_max_records", C.c_uint64), ("split_compression", C.c_double)]
+                ("split_max_records", C.c_uint64), ("split_compression", C.c_double),
+                ("replay_reserved_cus", C.c_uint32)]
 
 
 class SplitBatch(C.Structure):
@@ -178,7 +179,7 @@ def _sig(name, res, *args):
 vp = C.c_void_p
 _sig("vn_abi_version", C.c_int)
 _sig("vn_struct_size", C.c_size_t, C.c_int)
-ABI_VERSION = 3
+ABI_VERSION = 4
 _sig("vn_engine_create", C.c_int, C.POINTER(Config), C.POINTER(vp))
 _sig("vn_engine_destroy", None, vp)
 _sig("vn_last_error", C.c_char_p, vp)

@@ -130,25 +130,30 @@ void create_impl(vn_engine* e) {
     }
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork5, hipEventDisableTiming));
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join5, hipEventDisableTiming));
-#ifdef VN_TOP_EXCL
-    // (opt-in build) the longest batched replays (one workgroup each, hundreds of ms) on the last
-    // 16th of the CUs (two per XCC), which every other stream leaves alone: the main stream takes
-    // the rest.  Measured at C4 (profiles/r03_v6_*, r03_v7_*, r03_v8_*): two engines in turn 305-316
-    // ms per window against 359 without it, one engine 395 against 385 -- but with it the other
-    // engines of the process slowed down (the C5 leg 510 ms against 311), so it is not the default
-    if (e->st2 && ncu >= 64) {
-      std::vector<uint32_t> tmask((ncu + 31) / 32, 0u), amask((ncu + 31) / 32, 0u);
-      for (uint32_t i = 0; i < ncu; i++) (i >= ncu - ncu / 16 ? tmask : amask)[i / 32] |= 1u << (i % 32);
+    // vn_config.replay_reserved_cus: the longest batched replays (one workgroup each, hundreds of
+    // ms, latency-bound at one wave per SIMD) on the last CUs, which every other stream of the
+    // engine leaves alone -- the other windows' sorts and scatters no longer share those CUs'
+    // SIMDs with them.  Whole groups of 8 CUs (one per XCC), at most a quarter of the chip (the
+    // quarter the replay masks above already leave to the main stream)
+    e->reserved_cus = 0;
+    if (e->cfg.replay_reserved_cus && e->st2 && ncu >= 64) {
+      const uint32_t r = std::min<uint32_t>((e->cfg.replay_reserved_cus + 7u) & ~7u, ncu / 4);
+      std::vector<uint32_t> tmask((ncu + 31) / 32, 0u);
+      e->amask.assign((ncu + 31) / 32, 0u);
+      for (uint32_t i = 0; i < ncu; i++) (i >= ncu - r ? tmask : e->amask)[i / 32] |= 1u << (i % 32);
       VN_HIP_CHECK(hipStreamDestroy(e->st));
-      VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st, (uint32_t)amask.size(), amask.data()));
+      VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st, (uint32_t)e->amask.size(), e->amask.data()));
       VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st6, (uint32_t)tmask.size(), tmask.data()));
       VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join6, hipEventDisableTiming));
+      e->reserved_cus = r;
     }
-#endif
   }
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
-  VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st4, hipStreamNonBlocking, prio_hi));
+  if (e->reserved_cus)  // (off the reserved CUs too)
+    VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st4, (uint32_t)e->amask.size(), e->amask.data()));
+  else
+    VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st4, hipStreamNonBlocking, prio_hi));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join4, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork3, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_h2d, hipEventDisableTiming));
@@ -499,16 +504,21 @@ void destroy_impl(vn_engine* e) {
 }
 
 // throws on the engine's invariant flags; returns the caller-error flags (cleared on the device)
+// (every copy here is ordered on the engine's own stream: a plain hipMemcpy runs on the null
+// stream, which waits for every blocking stream of the device -- the CU-masked ones, whatever
+// engine they belong to -- and so would hold this flush behind another engine's replays)
 uint32_t check_error_flags(vn_engine* e) {
   uint32_t flags = 0;
-  VN_HIP_CHECK(hipMemcpy(&flags, e->h_err, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  VN_HIP_CHECK(hipMemcpyAsync(&flags, e->h_err, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
+  VN_HIP_CHECK(hipStreamSynchronize(e->st));
   if (flags & 1u) throw std::runtime_error("t-digest centroid tile overflow (compression too large for cap_cent)");
   if (flags & 2u) throw std::runtime_error("HLL rebase invariant violated");
   if (flags & 4u) throw std::runtime_error("t-digest chain window hand-off stalled");
   const uint32_t caller = flags & kErrSplitTouched;  // the caller's error, not the engine's: reported once
   if (caller) {
     flags &= ~caller;
-    VN_HIP_CHECK(hipMemcpy(e->h_err, &flags, sizeof(uint32_t), hipMemcpyHostToDevice));
+    VN_HIP_CHECK(hipMemcpyAsync(e->h_err, &flags, sizeof(uint32_t), hipMemcpyHostToDevice, e->st));
+    VN_HIP_CHECK(hipStreamSynchronize(e->st));
   }
   return caller;
 }
@@ -793,10 +803,12 @@ void ensure_export_bytes(vn_engine* e, ExportBuffers& x, uint64_t nbytes) {
 }
 void take_decode_error(vn_engine* e) {
   uint32_t flags = 0;
-  VN_HIP_CHECK(hipMemcpy(&flags, e->h_err, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  VN_HIP_CHECK(hipMemcpyAsync(&flags, e->h_err, sizeof(uint32_t), hipMemcpyDeviceToHost, e->st));
+  VN_HIP_CHECK(hipStreamSynchronize(e->st));
   if (flags & kErrDecode) {
     flags &= ~kErrDecode;
-    VN_HIP_CHECK(hipMemcpy(e->h_err, &flags, sizeof(uint32_t), hipMemcpyHostToDevice));
+    VN_HIP_CHECK(hipMemcpyAsync(e->h_err, &flags, sizeof(uint32_t), hipMemcpyHostToDevice, e->st));
+    VN_HIP_CHECK(hipStreamSynchronize(e->st));
     throw DecodeError("malformed import payload");
   }
 }

@@ -124,7 +124,9 @@ struct vn_engine {
   hipStream_t st5 = nullptr;
   hipEvent_t ev_fork5 = nullptr, ev_join5 = nullptr;
   // the few longest batched replays on CUs no other stream uses (null: st5 takes them all)
-  hipStream_t st6 = nullptr;
+  hipStream_t st6 = nullptr;     // the reserved CUs (vn_config.replay_reserved_cus), or none
+  uint32_t reserved_cus = 0;
+  std::vector<uint32_t> amask;   // every CU but the reserved ones
   hipEvent_t ev_join6 = nullptr;
   // set segment merge held back (ingest_device): the grouped set records are merged once the
   // histo path's remainder sort is done, so the long set kernel does not crowd it out

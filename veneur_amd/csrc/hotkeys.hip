@@ -119,7 +119,10 @@ uint32_t hot_collect(vn_engine* e, int cls, uint64_t min_count, uint32_t cap, ui
   VN_HIP_CHECK(hipMemcpyAsync(&n, nout, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipStreamSynchronize(st));
   std::vector<uint64_t> h(n);
-  if (n) VN_HIP_CHECK(hipMemcpy(h.data(), list, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (n) {
+    VN_HIP_CHECK(hipMemcpyAsync(h.data(), list, (size_t)n * sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    VN_HIP_CHECK(hipStreamSynchronize(st));
+  }
   // hottest first, ties by ascending slot
   std::sort(h.begin(), h.end(), [](uint64_t a, uint64_t b) {
     const uint32_t ca = (uint32_t)(a >> 32), cb = (uint32_t)(b >> 32);

@@ -1375,7 +1375,11 @@ int vn_split_keys(vn_engine* e, int cls, const uint32_t* slot, const uint32_t* o
       VN_HIP_CHECK(hipMalloc(&S.d_slot[cls], n * sizeof(uint32_t)));
       S.d_cap[cls] = n;
     }
-    if (n) VN_HIP_CHECK(hipMemcpy(S.d_slot[cls], slot, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    // (on the engine's stream, not the null stream: see check_error_flags)
+    if (n) {
+      VN_HIP_CHECK(hipMemcpyAsync(S.d_slot[cls], slot, n * sizeof(uint32_t), hipMemcpyHostToDevice, e->st));
+      VN_HIP_CHECK(hipStreamSynchronize(e->st));
+    }
   });
 }
 

@@ -53,8 +53,9 @@ def _arr(ptr, n, dt, shape=None):
 class Engine:
     def __init__(self, capacity, compression=100.0, percentiles=(0.5, 0.9, 0.99, 0.999), max_batch_records=1 << 20,
                  max_batch_member_bytes=0, device=0, exact_threshold=0, hot_prefix=0, piece_growth=0,
-                 split_max_records=0, split_compression=0.0):
+                 split_max_records=0, split_compression=0.0, replay_reserved_cus=0):
         cfg = A.Config()
+        cfg.replay_reserved_cus = int(replay_reserved_cus)
         cfg.split_max_records = int(split_max_records)
         cfg.split_compression = float(split_compression)
         cfg.histo_exact_threshold = int(exact_threshold)
