@@ -482,6 +482,8 @@ def main():
     ap.add_argument("--reserved-cus", type=int, default=-1,
                     help="CUs kept for the longest exact replays (vn_config.replay_reserved_cus); -1 (default): "
                          "8 per engine taking windows in turn when there are several, else 0")
+    ap.add_argument("--no-stagger", dest="stagger", action="store_false",
+                    help="D > 1: let the engines' ingests start together (default: in window order)")
     ap.add_argument("--hot-stride", type=int, default=256,
                     help="hot-key detector: count every hot_stride-th record (vn_hot_detect)")
     ap.add_argument("--no-split", action="store_true", help="route every key by digest %% N (no hot keys)")
@@ -589,24 +591,30 @@ def main():
     pipe = InTurn(D)
     lat = []  # per window: host ms from its first call to its flush's return
 
+    import contextlib
+
     def step(k=0, i=None, turn=None):
         e = engines[k]
+        # the ingests in window order (D > 1): the engines' long replays, which start as an
+        # ingest ends, follow one another instead of all starting together
+        gate = turn(i, 1) if (turn is not None and D > 1 and args.stagger) else contextlib.nullcontext()
         t = [time.perf_counter()] if args.host_trace and D == 1 else None
         ts = time.perf_counter()
-        for c, slots, owners in split_lists:
-            if len(slots):
-                e.split_keys(c, slots, owners)
-        # split records first: they are buffered on the split engine's stream, so the split
-        # combine at flush does not wait behind this engine's ingest
-        if sum(stream.split_counts):
-            e.ingest_split_device(stream.split)
-            if D == 1:
-                e.split_close()  # their combine runs beside this engine's ingest
-            if args.split_delay_ms:
-                time.sleep(args.split_delay_ms * 1e-3)
-        if t:
-            t.append(time.perf_counter())
-        e.ingest_device(stream.batch)
+        with gate:
+            for c, slots, owners in split_lists:
+                if len(slots):
+                    e.split_keys(c, slots, owners)
+            # split records first: they are buffered on the split engine's stream, so the split
+            # combine at flush does not wait behind this engine's ingest
+            if sum(stream.split_counts):
+                e.ingest_split_device(stream.split)
+                if D == 1:
+                    e.split_close()  # their combine runs beside this engine's ingest
+                if args.split_delay_ms:
+                    time.sleep(args.split_delay_ms * 1e-3)
+            if t:
+                t.append(time.perf_counter())
+            e.ingest_device(stream.batch)
         if t:
             t.append(time.perf_counter())
         if turn is not None and D > 1:
@@ -778,6 +786,10 @@ def main():
     if sim:
         result["simulated"] = "rank %d of %d on one GPU, no exchange partners: not a bench result" % (
             args.sim_rank, args.sim_world)
+        dh = stream.to_host()
+        hs = dh["h_slot"][:stream.counts[2]]
+        result["sim"] = {"rank": args.sim_rank, "world": args.sim_world, "records": int(stream.n_records),
+                         "largest_timer_key_samples": int(np.bincount(hs).max()) if len(hs) else 0}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not sim:
         t1 = time.time()
         d = stream.to_host()

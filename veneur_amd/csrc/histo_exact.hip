@@ -94,6 +94,17 @@ struct NmW {
 };
 
 __device__ __forceinline__ bool is_int_weight(double w) { return w == __builtin_floor(w) && w <= 4503599627370496.0; }
+// Weights whose sums are exact in any order.  Integers below 2^52: any partial sum below 2^53
+// is an integer.  Or multiples of 2^-23 up to 2^30 -- every 1/rate a float32 sample rate gives
+// (float32 values >= 1 are such multiples), and sums of them, like an imported centroid's
+// weight: a partial sum below 2^30 is then k * 2^-23 with k < 2^53.  The total bound that goes
+// with a set of weights: exact_total_limit(all integers).
+__device__ __forceinline__ bool is_exact_weight(double w) {
+  const double s = w * 8388608.0;  // (a power of two: exact)
+  // (and >= 1, as every weight a sampler adds: merge_fast's monotone-k argument needs it)
+  return (w == __builtin_floor(w) && w <= 4503599627370496.0) || (s == __builtin_floor(s) && w >= 1.0 && w <= 1073741824.0);
+}
+__device__ __forceinline__ double exact_total_limit(bool all_int) { return all_int ? 9007199254740992.0 : 1073741824.0; }
 
 __device__ __forceinline__ double rl_d(double v, int i) {
   int lo = __builtin_amdgcn_readlane(__double2loint(v), i);
@@ -294,17 +305,19 @@ __device__ __forceinline__ uint32_t temps_le(const ldsf64* sv, uint32_t np, doub
 // every weight is an integer and the total stays below 2^53 (then every order is exact).
 __device__ double temp_weight(const ldsf64* tw, uint32_t np) {
   const uint32_t lane = threadIdx.x & 63;
-  bool tint = true;
+  bool tint = true, tex = true;
   double part = 0.0;
   for (uint32_t t = lane; t < np; t += 64) {
     double w = __builtin_fabs(tw[t]);  // the chunk sorter marks imported centroids by a negative weight
     tint &= is_int_weight(w);
+    tex &= is_exact_weight(w);
     part = dadd(part, w);
   }
   double tempW = 0.0;
   tint = __all(tint);
-  if (tint) tempW = wave_sum(part);
-  if (!tint || !(tempW <= 9007199254740992.0)) {
+  tex = __all(tex);
+  if (tex) tempW = wave_sum(part);
+  if (!tex || !(tempW <= exact_total_limit(tint))) {
     tempW = 0.0;
     for (uint32_t b = 0; b < np; b += 64) {
       double w = (b + lane < np) ? tw[b + lane] : 0.0;
@@ -386,9 +399,12 @@ __device__ __noinline__ NmW merge_sorted(const MergeParams x, const Lds L, const
   PROF_T(p1);
   const uint32_t m = nm + np;
   // ---- mergedWeight prefix (inclusive), then the k-index of every element
-  bool wint = true;
-  for (uint32_t j = lane; j < m; j += 64) wint &= is_int_weight(L.gw[j]);
-  wint = __all(wint) && T <= 9007199254740992.0;
+  bool wint = true, wex = true;
+  for (uint32_t j = lane; j < m; j += 64) {
+    wint &= is_int_weight(L.gw[j]);
+    wex &= is_exact_weight(L.gw[j]);
+  }
+  wint = __all(wex) && T <= exact_total_limit(__all(wint));  // (sums exact in any order)
   double carry = 0.0;
   for (uint32_t b = 0; b < m; b += 64) {
     const uint32_t j = b + lane;
@@ -600,15 +616,16 @@ __device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds
   double kv[kR];
   {
     double w[kR];
-    bool wint = true;
+    bool wint = true, wex = true;
 #pragma unroll
     for (int r = 0; r < kR; r++) {
       const uint32_t j = 64 * r + lane;
       const double g = L.gw[j];
       w[r] = j < m ? g : 0.0;
       wint &= is_int_weight(w[r]);
+      wex &= is_exact_weight(w[r]);
     }
-    wint = __all(wint) && T <= 9007199254740992.0;
+    wint = __all(wex) && T <= exact_total_limit(__all(wint));  // (sums exact in any order)
     if (wint) {
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
@@ -904,12 +921,13 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
   // the first record, the Add-order tempW at it (negated when a weight is not an integer)
   // and for the batched replay (cpk) the same prefix as a u16 beside |w| as a u16, slot 0 carrying
   // tempW -- or 0xffffffff when some weight is not an integer or tempW >= 2^16
-  bool tint = true;
+  bool tint = true, tex = true;
   double carry = 0.0;
   for (uint32_t b = 0; b < tcap; b += 64) {
     const uint32_t t = b + lane;
     const double w = t < tcap ? __builtin_fabs(sw[t]) : 0.0;
     tint &= is_int_weight(w);
+    tex &= is_exact_weight(w);
     double v = w;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -926,8 +944,10 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
     carry = dadd(carry, rl_d(v, 63));
   }
   tint = __all(tint);
+  tex = __all(tex) && tempW <= exact_total_limit(tint);
   if (lane == 0) {
-    x.ctw[base] = tint ? tempW : -tempW;
+    // (the four-wave merge needs exact prefixes only; the batched one integers below 2^16)
+    x.ctw[base] = tex ? tempW : -tempW;
     // (every weight is at least 1, so tempW < 2^16 bounds each weight and prefix below 2^16 too)
     if (x.cpk) x.cpk[base] = tint && tempW < 65536.0 ? (uint32_t)tempW << 16 | (uint32_t)__builtin_fabs(sw[0]) : 0xffffffffu;
   }
@@ -1246,11 +1266,12 @@ __device__ __forceinline__ double wave_incl_add_d(double v) {
 __device__ __noinline__ void prefix_main_w0(const Lds L, const FastLds F, uint32_t nm, double mainW) {
   const uint32_t lane = threadIdx.x & 63;
   double carry = 0.0;
-  bool ok = true;
+  bool ok = true, allint = true;
   for (uint32_t b = 0; b < nm; b += 64) {
     const uint32_t j = b + lane;
     const double w = j < nm ? L.mw[j] : 0.0;
-    ok &= is_int_weight(w);
+    ok &= is_exact_weight(w);
+    allint &= is_int_weight(w);
     // (integers: exact in any order).  DPP reads other lanes' registers, so it needs every lane
     // of the wave active: a caller that reaches here with some masked off (the compiler may
     // keep a uniform condition as a lane mask) takes the shuffle scan instead
@@ -1267,7 +1288,7 @@ __device__ __noinline__ void prefix_main_w0(const Lds L, const FastLds F, uint32
     if (j < nm) F.mp[j] = dadd(carry, dsub(v, w));
     carry = dadd(carry, rl_d(v, 63));
   }
-  ok = __all(ok) && carry == mainW && mainW <= 9007199254740992.0;
+  ok = __all(ok) && carry == mainW && mainW <= exact_total_limit(__all(allint));
   if (lane == 0) {
     F.mp[nm] = mainW;
     F.misc[1] = ok ? 1u : 0u;
@@ -1278,7 +1299,7 @@ __device__ __noinline__ void prefix_main_w0(const Lds L, const FastLds F, uint32
 __device__ __noinline__ void prefix_temps_w0(const Lds L, const FastLds F, uint32_t np) {
   const uint32_t lane = threadIdx.x & 63;
   const double w = lane < np ? L.sw[lane] : 0.0;
-  const bool ok = __all(is_int_weight(w));
+  const bool allint = __all(is_int_weight(w)), ex = __all(is_exact_weight(w));
   double v = w;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -1286,6 +1307,7 @@ __device__ __noinline__ void prefix_temps_w0(const Lds L, const FastLds F, uint3
     v = (int)lane >= d ? dadd(v, o) : v;
   }
   const double tot = rl_d(v, 63);
+  const bool ok = ex && tot <= exact_total_limit(allint);
   if (lane < np) F.sp[lane] = dsub(v, w);
   if (lane == 0) {
     F.sp[np] = tot;
@@ -1362,7 +1384,7 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
   // Every comparison below is taken only when its difference lies outside 1 +- kBand, where the
   // close and the exact k certainly agree (their k differ by < 1e-13); one inside the band sends
   // the merge to the walks and then, if still inside it there, to exact k and the sequential walk.
-  // With integer weights >= 1 and T <= 2^40 (the fast merge's conditions) consecutive exact k
+  // With weights >= 1 and T <= 2^40 (the fast merge's conditions) consecutive exact k
   // differ by more than 5e-11, far above asin's ulps, so exact k is increasing and the
   // forced-start argument holds.
 #pragma unroll
@@ -2664,10 +2686,28 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       const BatchResult r = merge_batch<NW>(mp.delta, sin_hi, sin_lo, L, F, Bt, nm, mainW, c, b, tcap);
       PROF_T(s1);
       PROF_ADD(27, s0, s1);
+      const uint32_t cb_end = c + b;  // (the batch's chunks: landed in the ring)
       c += r.js;
       if (r.js < b && r.structural) {  // that merge alone (after a batch that took nothing: a run)
         const uint32_t c1 = min(sp.npure, c + (r.js == 0 ? kBatchBackoff : 1u));
-        singles(c, c1);
+        // from the ring where the chunk is there and batchable (no global round trip: under a
+        // busy memory system that latency would sit on the chain), else from the sorter's arrays
+        uint32_t cs = c;
+        for (; cs < c1 && cs < cb_end; cs++) {
+          const uint32_t sb = (cs % kRing) * tcap;
+          const uint32_t p0 = Bt.rp[sb];
+          if (p0 == 0xffffffffu) break;
+          if (t < tcap) {
+            const uint32_t pk = Bt.rp[sb + t];
+            L.sv[t] = Bt.rv[sb + t];
+            L.sw[t] = (double)(pk & 0xffffu);
+            F.sp[t] = t ? (double)(pk >> 16) : 0.0;
+          }
+          if (t == tcap) F.sp[tcap] = (double)(p0 >> 16);
+          fast_sync<NW>();
+          merge_sorted_any(tcap, (double)(p0 >> 16), true);
+        }
+        if (cs < c1) singles(cs, c1);
         PROF_T(s2);
         PROF_ADD(28, s1, s2);
         PROF_ADD(29, 0, (long long)(c1 - c));

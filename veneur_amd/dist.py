@@ -164,28 +164,32 @@ class InTurn:
     combine, one communicator per engine), so every rank enters them in window order: engine k's
     communicator sees windows k, k + D, ... on every rank, and no two communicators' collectives
     are ever issued in different orders on two ranks.  run(n) returns the n results in window
-    order; a failure in any window ends the others' waits."""
+    order; a failure in any window ends the others' waits.
 
-    def __init__(self, D):
+    turn(i, section) keeps one such order per section: `with turn(i, 1):` around window i's
+    ingest staggers the engines (window i + 1's ingest starts once window i's has been issued),
+    so their long replays, which start at the end of an ingest, do not all run at once."""
+
+    def __init__(self, D, sections=2):
         self.D = D
         self.cv = threading.Condition()
-        self.next = 0
+        self.next = [0] * sections
         self.failed = False
 
-    def turn(self, i):
+    def turn(self, i, section=0):
         pipe = self
 
         class _T:
             def __enter__(self):
                 with pipe.cv:
-                    pipe.cv.wait_for(lambda: pipe.next == i or pipe.failed)
+                    pipe.cv.wait_for(lambda: pipe.next[section] == i or pipe.failed)
                     if pipe.failed:
                         raise RuntimeError("an earlier window failed")
 
             def __exit__(self, *exc):
                 with pipe.cv:
                     if exc[0] is None:
-                        pipe.next = i + 1
+                        pipe.next[section] = i + 1
                     else:
                         pipe.failed = True  # (the other engines' waits end)
                     pipe.cv.notify_all()
@@ -194,7 +198,7 @@ class InTurn:
         return _T()
 
     def run(self, n, work):
-        self.next, self.failed = 0, False
+        self.next, self.failed = [0] * len(self.next), False
         out, errs = [None] * n, []
         if self.D == 1:
             for i in range(n):
