@@ -562,7 +562,9 @@ def main():
     # collectives (one communicator per engine) in the same order.
     D = max(1, args.pipeline if args.pipeline > 0 else 2)
 
-    reserved = args.reserved_cus if args.reserved_cus >= 0 else (8 * D if D > 1 else 0)
+    # (measured, DESIGN.md §4: at N = 1 the other windows' work is large and the reservation
+    # costs more than it gains; a rank of an N-GPU split is dominated by its chains)
+    reserved = args.reserved_cus if args.reserved_cus >= 0 else (8 * D if D > 1 and (world > 1 or sim) else 0)
 
     def make_engine():
         e = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,

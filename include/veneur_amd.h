@@ -398,7 +398,10 @@ int vn_ingest_split(vn_engine* eng, const vn_split_batch* device_batch);
 int vn_split_close(vn_engine* eng);
 /* Combine the split keys now (collective over the group; vn_flush does it when they are still
  * pending): afterwards the owners hold each split key's state in its slot, the other ranks
- * have cleared theirs, and the split lists are empty. */
+ * have cleared theirs, and the split lists are empty.  Returns once the exchange is issued
+ * (every later operation of the engine is ordered after it); it does not wait for the
+ * window's own replays, so engines taking windows in turn can enter their combines in window
+ * order without one window's replays holding up the next. */
 int vn_split_combine(vn_engine* eng);
 
 /* DogStatsD metric lines (host code, no GPU): samplers/parser.go:186-307 ParseMetric over a

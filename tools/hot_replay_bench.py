@@ -26,6 +26,10 @@ def main():
     ap.add_argument("--cold-keys", type=int, default=0, help="extra short keys in the same batch")
     ap.add_argument("--cold-n", type=int, default=100, help="samples per short key")
     ap.add_argument("--rates", action="store_true", help="10%% of samples at rate 0.5 or 0.1 (C4's mix)")
+    ap.add_argument("--engines", type=int, default=1,
+                    help="D > 1: D engines take 4 * D windows in turn (host threads, veneur_amd.dist.InTurn); "
+                         "reports ms per window of that run as well")
+    ap.add_argument("--reserved-cus", type=int, default=0)
     a = ap.parse_args()
     import veneur_amd as V
     import veneur_amd._abi as A
@@ -60,10 +64,37 @@ def main():
             e.ingest_device(b)
             gobs = e.export_histos(np.arange(min(a.keys, 4), dtype=np.uint32))
             e.flush()
+    pipe_ms = None
+    if a.engines > 1:
+        from veneur_amd.dist import InTurn
+        engs = [V.Engine((1, 1, nk, 1), percentiles=pct, max_batch_records=len(slot) + 1,
+                         replay_reserved_cus=a.reserved_cus) for _ in range(a.engines)]
+        b = A.Batch()
+        b.n_histo = len(slot)
+        b.histo_slot, b.histo_value, b.histo_rate = (x.ptr.value for x in bufs)
+
+        def work(k, i, turn):
+            with turn(i, 1):
+                engs[k].ingest_device(b)
+            return engs[k].flush_raw()
+
+        pipe = InTurn(a.engines)
+        pipe.run(a.engines, work)
+        A.lib.vn_device_synchronize(0)
+        nwin = 4 * a.engines
+        t0 = time.perf_counter()
+        pipe.run(nwin, work)
+        A.lib.vn_device_synchronize(0)
+        pipe_ms = (time.perf_counter() - t0) * 1e3 / nwin
+        for x in engs:
+            x.close()
     merges = a.n // 42
     out = {"mode": "fast" if a.fast else "exact", "keys": a.keys, "samples_per_key": a.n, "cold_keys": a.cold_keys,
            "rates": a.rates, "ms_window": ms,
            "us_per_merge_longest": ms * 1e3 / max(1, merges)}
+    if pipe_ms is not None:
+        out["engines"] = a.engines
+        out["ms_per_window_engines_in_turn"] = pipe_ms
     if not a.no_check:
         import oracle
         w = oracle.Worker(1, 1, nk, 1)

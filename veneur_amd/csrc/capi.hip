@@ -155,6 +155,12 @@ void create_impl(vn_engine* e) {
   else
     VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st4, hipStreamNonBlocking, prio_hi));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join4, hipEventDisableTiming));
+  if (e->reserved_cus)
+    VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st_ctr, (uint32_t)e->amask.size(), e->amask.data()));
+  else
+    VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st_ctr, hipStreamNonBlocking, prio_hi));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_ctr0, hipEventDisableTiming));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_ctr1, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork3, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_h2d, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreate(&e->ev_w0));
@@ -488,6 +494,16 @@ void destroy_impl(vn_engine* e) {
     e->st5 = nullptr;
   }
   if (e->st4) (void)hipStreamSynchronize(e->st4);
+  if (e->st_ctr) {
+    (void)hipStreamSynchronize(e->st_ctr);
+    (void)hipStreamDestroy(e->st_ctr);
+    e->st_ctr = nullptr;
+  }
+  for (hipEvent_t* ev : {&e->ev_ctr0, &e->ev_ctr1})
+    if (*ev) {
+      (void)hipEventDestroy(*ev);
+      *ev = nullptr;
+    }
   if (e->ev_join4) (void)hipEventDestroy(e->ev_join4);
   if (e->st4) (void)hipStreamDestroy(e->st4);
   if (e->ev_fork) (void)hipEventDestroy(e->ev_fork);

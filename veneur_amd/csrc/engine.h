@@ -119,6 +119,10 @@ struct vn_engine {
   // hot-prefix stream: the hot keys' short replays run here while st gathers and sorts their
   // remainders
   hipStream_t st4 = nullptr;
+  // the split counters' combine: after the window's counter aggregation (on the side stream),
+  // not behind the main stream's replays, so vn_split_combine returns without waiting for them
+  hipStream_t st_ctr = nullptr;
+  hipEvent_t ev_ctr0 = nullptr, ev_ctr1 = nullptr;
   hipEvent_t ev_join4 = nullptr;
   // long-key replay stream (CU mask of st3): the longest keys' four-wave replays
   hipStream_t st5 = nullptr;

@@ -43,7 +43,9 @@ enum ScratchId {
   kSSegT, kSStarts, kSNcNew, kSAccXw, kSAccW, kSHst, kSHnc, kSHcur, kSHspn, kSCm0, kSCm1, kSCw0, kSCw1, kSElem,
   kSSend, kSRecv, kSKeyOff, kSCntMat, kSCntAll, kSOwnList, kSImpA, kSImpB, kSImpA1, kSImpB1, kSImpSlot, kSImpVal,
   kSImpW, kSMicW, kSCP, kSCM, kSPcnt, kSFF, kSW32, kSCand, kSTfull, kSP0, kSDone, kSR2, kSPre, kSDev1,
-  kSLocalStats, kSCtr, kSTouch, kSIota, kSFuseV, kSFuseW, kSFuseK, kSCount
+  kSLocalStats, kSCtr, kSTouch, kSIota, kSFuseV, kSFuseW, kSFuseK,
+  kSCtrTouch, kSCtrOwn,  // (the counters' own: their combine runs on st_ctr beside the others)
+  kSCount
 };
 
 template <class T>
@@ -225,14 +227,21 @@ __global__ void k_sc_scatter(uint32_t n, const uint32_t* __restrict__ slot, cons
   touch[slot[i]] = own ? t[i] : 0u;
 }
 
+// the owner list on the device (kSCtrOwn), the host list free to change when this returns
+void split_counter_owners(vn_engine* e, hipStream_t st) {
+  SplitState& S = e->sp;
+  const uint32_t H = (uint32_t)S.slot[VN_COUNTER].size();
+  if (!H) return;
+  to_dev(sbuf<uint32_t>(e, kSCtrOwn, H), S.owner[VN_COUNTER].data(), H, st);
+  VN_HIP_CHECK(hipStreamSynchronize(st));
+}
 void split_counters(vn_engine* e, vn_comm* c, hipStream_t st) {
   SplitState& S = e->sp;
   const uint32_t H = (uint32_t)S.slot[VN_COUNTER].size();
   if (!H) return;
   int64_t* v = sbuf<int64_t>(e, kSCtr, H);
-  uint32_t* t = sbuf<uint32_t>(e, kSTouch, H);
-  uint32_t* own = sbuf<uint32_t>(e, kSOwnList, H);
-  to_dev(own, S.owner[VN_COUNTER].data(), H, st);
+  uint32_t* t = sbuf<uint32_t>(e, kSCtrTouch, H);
+  uint32_t* own = sbuf<uint32_t>(e, kSCtrOwn, H);  // (split_counter_owners)
   hipLaunchKernelGGL(k_sc_gather, dim3(blocks_for(H, 256)), dim3(256), 0, st, H, S.d_slot[VN_COUNTER], e->cval,
                      e->ctouch, v, t);
   comm_allreduce(c, v, v, H, kI64, kSum, st);
@@ -1281,7 +1290,17 @@ void split_flush(vn_engine* e) {
     S.mv_set = SplitState::SetMove{};
   }
   S.closed = false;
-  split_counters(e, c, e->st);
+  if (!S.slot[VN_COUNTER].empty()) {
+    // on their own stream, after the window's counter aggregation (the side stream's work so
+    // far), then the main stream waits for them: not behind this window's long replays
+    hipStream_t src = e->timing ? e->st : e->st2;
+    split_counter_owners(e, e->st_ctr);  // (before the wait: the stream is idle)
+    VN_HIP_CHECK(hipEventRecord(e->ev_ctr0, src));
+    VN_HIP_CHECK(hipStreamWaitEvent(e->st_ctr, e->ev_ctr0, 0));
+    split_counters(e, c, e->st_ctr);
+    VN_HIP_CHECK(hipEventRecord(e->ev_ctr1, e->st_ctr));
+    VN_HIP_CHECK(hipStreamWaitEvent(e->st, e->ev_ctr1, 0));
+  }
   for (int k = 0; k < VN_NCLASS; k++) {
     S.slot[k].clear();
     S.owner[k].clear();
@@ -1406,8 +1425,9 @@ int vn_split_close(vn_engine* e) {
 int vn_split_combine(vn_engine* e) {
   if (!e) return VN_EINVAL;
   return split_guarded(e, [&] {
+    // (returns once the group's exchange is issued: the engine's stream orders everything
+    // after it, and vn_flush / the state reads wait for it -- not for this window's replays)
     split_flush(e);
-    VN_HIP_CHECK(hipStreamSynchronize(e->st));
     VN_HIP_CHECK(hipGetLastError());
   });
 }
