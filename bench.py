@@ -479,9 +479,8 @@ def main():
                     help="engines per GPU taking the windows in turn (window i + 1 ingested and combined while "
                          "window i's longest replays finish; one communicator per engine, the combines entered in "
                          "window order); 1: one engine, windows back to back; 0 (default): 2")
-    ap.add_argument("--reserved-cus", type=int, default=-1,
-                    help="CUs kept for the longest exact replays (vn_config.replay_reserved_cus); -1 (default): "
-                         "8 per engine taking windows in turn when there are several, else 0")
+    ap.add_argument("--reserved-cus", type=int, default=0,
+                    help="CUs kept for the longest exact replays (vn_config.replay_reserved_cus); 0 (default): none")
     ap.add_argument("--no-stagger", dest="stagger", action="store_false",
                     help="D > 1: let the engines' ingests start together (default: in window order)")
     ap.add_argument("--hot-stride", type=int, default=256,
@@ -562,9 +561,8 @@ def main():
     # collectives (one communicator per engine) in the same order.
     D = max(1, args.pipeline if args.pipeline > 0 else 2)
 
-    # (measured, DESIGN.md §4: at N = 1 the other windows' work is large and the reservation
-    # costs more than it gains; a rank of an N-GPU split is dominated by its chains)
-    reserved = args.reserved_cus if args.reserved_cus >= 0 else (8 * D if D > 1 and (world > 1 or sim) else 0)
+    # (measured, DESIGN.md §4: the reservation costs the other windows more than it gains)
+    reserved = max(0, args.reserved_cus)
 
     def make_engine():
         e = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,
@@ -642,7 +640,10 @@ def main():
     def sync():
         A.lib.vn_device_synchronize(local_rank)
 
-    run_windows(args.warmup)
+    # every engine's first window sizes its scratch (hipMalloc / hipFree: a hipFree waits for the
+    # whole device, the other engines' replays included), so each engine warms up at least once
+    warm = max(args.warmup, D)
+    run_windows(warm)
     sync()
     ctrl.barrier()
     lat.clear()
@@ -762,6 +763,7 @@ def main():
                                   (world, sum(len(split[c]) for c in split)),
                    "split_keys": {"counter": len(split[0]), "histo": len(split[2]), "set": len(split[3])},
                    "windows_in_flight": D,
+                   "warmup_windows_run": warm,
                    "replay_reserved_cus": reserved,
                    "pipeline": ("%d engines per GPU take the windows in turn: window i + 1 is ingested while window "
                                 "i's longest replays finish; every window ingested, replayed and flushed inside the "

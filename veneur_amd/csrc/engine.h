@@ -228,6 +228,7 @@ struct vn_engine {
   double* h_csv = nullptr;       // pre-sorted pure chunks: means, weights (per record)
   double* h_csw = nullptr;
   uint32_t* h_cpk = nullptr;     // ... the batched replay's packed weights (ExactCtx::cpk)
+  double* h_lstat = nullptr;     // ... the batched keys' Local* partials (ExactCtx::lstat)
   uint32_t* h_tl2 = nullptr;     // slots of hot keys
   uint32_t* h_ccnt = nullptr;    // per touched key: pure chunks to pre-sort
   uint32_t* h_coff = nullptr;    // scan of h_ccnt (touched + 1)

@@ -73,7 +73,12 @@ struct ExactCtx {
   // integer, or a tempW of 65536 or more)
   uint32_t* cpk;
   uint32_t* cown;  // [chunks] the key index of every pure chunk (null: searched in coff)
+  // the batched keys' pure-chunk Local* statistics, reduced in parallel before their replays
+  // (k_exact_long_stats): [kLongStatKeys][kLongStatSlices][8] partials (null: the replay's own)
+  double* lstat;
 };
+constexpr uint32_t kLongStatSlices = 64;
+constexpr uint32_t kLongStatKeys = 1024;  // entries of the longest-first order with partials (the rest: in-replay)
 
 size_t exact_smem_bytes(uint32_t capc, uint32_t tcap);
 size_t exact_fast_smem_bytes(uint32_t capc, uint32_t tcap);  // the long replays' (k_histo_exact_mw)

@@ -2474,7 +2474,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
 // replay of one key with NW waves (tcap <= 64, ingest only: no flush-mode adoption); BATCH:
 // merge_batch where the key's state allows (the dynamic LDS then holds the batch tables)
 template <int NW, bool BATCH>
-__device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& S) {
+__device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& S, const uint32_t pos = 0xffffffffu) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr uint32_t NT = 64 * NW;
   const uint32_t t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -2627,7 +2627,20 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     // the pure chunks' Local* statistics first, every thread streaming its share (off the merge
     // chain: the replay below adds none); the loads of four records in flight per thread
 #ifndef VN_NO_PROLOGUE
-    {
+    if (x.lstat && pos < kLongStatKeys) {
+      // reduced beforehand over the whole GPU (k_exact_long_stats): slice t's partials into
+      // thread t's accumulators, folded with the rest below
+      if (t < kLongStatSlices) {
+        const double* q = x.lstat + ((uint64_t)pos * kLongStatSlices + t) * 8;
+        sw = dadd(sw, q[0]);
+        sxw = dadd(sxw, q[1]);
+        srw = dadd(srw, q[2]);
+        mn = min_go(mn, q[3]);
+        mx = max_go(mx, q[4]);
+        dmn = min_go(dmn, q[5]);
+        dmx = max_go(dmx, q[6]);
+      }
+    } else {
       const uint64_t ne = (uint64_t)sp.npure * tcap;
       uint64_t e = t;
       for (; e + 3 * NT < ne; e += 4 * NT) {
@@ -2816,7 +2829,7 @@ __device__ __forceinline__ void replay_long(const ExactCtx& x, const uint32_t* _
   const uint32_t n = min(BATCH ? nmw[1] : nmw[0], last);
   for (uint32_t i = (BATCH ? first : nmw[1]) + blockIdx.x; i < n; i += gridDim.x) {
     const uint32_t k = x.order64 ? (uint32_t)x.order64[i] : x.order ? x.order[i] : i;
-    if (k < x.nkeys) replay_key_fast<kMW, BATCH>(x, k, *(MwSharedL*)&S);
+    if (k < x.nkeys) replay_key_fast<kMW, BATCH>(x, k, *(MwSharedL*)&S, BATCH ? i : 0xffffffffu);
     __syncthreads();  // the next key reuses the LDS
   }
 }
@@ -2827,6 +2840,83 @@ __global__ __launch_bounds__(kMWThreads) void k_histo_exact_mwb(ExactCtx x, cons
                                                                  uint32_t first, uint32_t last) {
   replay_long<true>(x, nmw, first, last);
 }
+// The Local* statistics of the batched keys' pure chunks (Histo.Sample, samplers.go:346-356:
+// weight, min, max, sum(x w), sum(w / x) of the samples; min / max of every record for the
+// digest), reduced over the whole GPU before their replays: block (slice, y) takes one of
+// kLongStatSlices contiguous slices of entry y's pure chunks and writes its partials.  (Reduced
+// inside the replay's own workgroup, this stream of a hot key's records -- hundreds of MB --
+// ran at one CU's memory-level parallelism, on the key's critical path.)  Entries [y0, y1) of
+// the longest-first order that are batched (< mw_count[1]).
+__device__ __forceinline__ void long_stats_entry(const ExactCtx& x, const uint32_t y, double (&red)[7][4]) {
+  const uint32_t k = (uint32_t)x.order64[y];
+  double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf, dmn = kInf, dmx = -kInf;
+  if (k < x.nkeys) {
+    const uint32_t s = x.keys[k];
+    const ExactSplit sp = exact_split(x.hpend[s], x.nex[k], x.tcap);
+    const uint64_t base = (uint64_t)x.start[s] + sp.off0, ne = (uint64_t)sp.npure * x.tcap;
+    const uint64_t per = (ne + kLongStatSlices - 1) / kLongStatSlices;
+    const uint64_t a = min(ne, per * blockIdx.x), b = min(ne, a + per);
+    for (uint64_t e = a + threadIdx.x; e < b; e += 256) {
+      const double v = x.csv[base + e], w = x.csw[base + e], wt = __builtin_fabs(w);
+      dmn = min_go(dmn, v);
+      dmx = max_go(dmx, v);
+      if (w > 0.0) {  // (an imported centroid: negative, the digest's min / max only)
+        sw = dadd(sw, wt);
+        mn = min_go(mn, v);
+        mx = max_go(mx, v);
+        sxw = dadd(sxw, dmul(v, wt));
+        srw = dadd(srw, dmul(ddiv(1.0, v), wt));
+      }
+    }
+  }
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    sw = dadd(sw, __shfl_xor(sw, d, 64));
+    sxw = dadd(sxw, __shfl_xor(sxw, d, 64));
+    srw = dadd(srw, __shfl_xor(srw, d, 64));
+    mn = min_go(mn, __shfl_xor(mn, d, 64));
+    mx = max_go(mx, __shfl_xor(mx, d, 64));
+    dmn = min_go(dmn, __shfl_xor(dmn, d, 64));
+    dmx = max_go(dmx, __shfl_xor(dmx, d, 64));
+  }
+  if (lane == 0) {
+    red[0][wv] = sw;
+    red[1][wv] = sxw;
+    red[2][wv] = srw;
+    red[3][wv] = mn;
+    red[4][wv] = mx;
+    red[5][wv] = dmn;
+    red[6][wv] = dmx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < 4; q++) {
+      sw = dadd(sw, red[0][q]);
+      sxw = dadd(sxw, red[1][q]);
+      srw = dadd(srw, red[2][q]);
+      mn = min_go(mn, red[3][q]);
+      mx = max_go(mx, red[4][q]);
+      dmn = min_go(dmn, red[5][q]);
+      dmx = max_go(dmx, red[6][q]);
+    }
+    double* o = x.lstat + ((uint64_t)y * kLongStatSlices + blockIdx.x) * 8;
+    o[0] = sw;
+    o[1] = sxw;
+    o[2] = srw;
+    o[3] = mn;
+    o[4] = mx;
+    o[5] = dmn;
+    o[6] = dmx;
+  }
+  __syncthreads();  // (red is reused by the next entry)
+}
+__global__ __launch_bounds__(256) void k_exact_long_stats(ExactCtx x, uint32_t y0, uint32_t y1) {
+  __shared__ double red[7][4];
+  const uint32_t yn = min(y1, min(x.mw_count[1], kLongStatKeys));
+  for (uint32_t y = y0 + blockIdx.y; y < yn; y += gridDim.y) long_stats_entry(x, y, red);
+}
+
 // how many entries of the longest-first order replay at least min_len samples (out[0]), and at
 // least batch_len (out[1], <= out[0])
 __global__ void k_exact_count_long(uint32_t n, const uint64_t* __restrict__ order64, uint32_t min_len,
@@ -2930,7 +3020,15 @@ void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_r
   if (x.cpk && x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024) {
     const size_t sm = exact_batch_smem_bytes(x.capc, x.tcap);
     const uint32_t top = st_top ? std::min<uint32_t>(kTopExcl, x.norder) : 0u;
-    if (top) hipLaunchKernelGGL(k_histo_exact_mwb, dim3(top), dim3(kMWThreads), sm, st_top, x, x.mw_count, 0u, top);
+    const uint32_t nl = std::min<uint32_t>(x.norder, kLongStatKeys);
+    if (top) {
+      if (x.lstat)
+        hipLaunchKernelGGL(k_exact_long_stats, dim3(kLongStatSlices, top), dim3(256), 0, st_top, x, 0u, top);
+      hipLaunchKernelGGL(k_histo_exact_mwb, dim3(top), dim3(kMWThreads), sm, st_top, x, x.mw_count, 0u, top);
+    }
+    if (x.lstat && nl > top)
+      hipLaunchKernelGGL(k_exact_long_stats, dim3(kLongStatSlices, std::min<uint32_t>(nl - top, 32u)), dim3(256), 0,
+                         st, x, top, nl);
     hipLaunchKernelGGL(k_histo_exact_mwb, dim3(grid), dim3(kMWThreads), sm, st, x, x.mw_count, top, 0xffffffffu);
   }
   hipLaunchKernelGGL(k_histo_exact_mw, dim3(grid), dim3(kMWThreads), exact_fast_smem_bytes(x.capc, x.tcap), st_rest, x,

@@ -1308,6 +1308,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.csw = e->h_csw;
   xc.ctw = e->h_tw;
   xc.cpk = e->h_cpk;
+  xc.lstat = e->h_lstat;
   histo_exact_presort(xc, st, &e->ss, n / e->temp_cap + 1);
   // The hot keys' prefixes run on st4 (short) while st gathers and sorts the remainders; the
   // cold and warm keys (long) on st3 after the sort, whose passes would otherwise wait for CUs
