@@ -1772,7 +1772,7 @@ struct BatchLds {
 __host__ __device__ inline uint32_t batch_bytes(uint32_t tcap) {
   const uint32_t nl = kBB * tcap;
   return 12u * kRing * tcap + 16u * kBB + 16u * kBM + 24u * kBN + 8u * (nl + 1) + 4u * (nl + 1) + 4u * (kBN + 1) + 32u +
-         2u * kBM + nl + nl + 16u + kBN * kRS + kBM * kRS + 16u;
+         2u * kBM + (nl + 16u) + (nl + 16u) + 16u + kBN * kRS + kBM * kRS + 16u;
 }
 __host__ __device__ inline uint32_t batch_offset(uint32_t capc, uint32_t tcap) {
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = capc + TP + 1 > 320u ? capc + TP + 1 : 320u;
@@ -1794,8 +1794,8 @@ __device__ __forceinline__ BatchLds batch_layout(char* p, uint32_t tcap) {
   B.ctl = B.off + (kBN + 1);
   B.flagged = (ldsu16*)(B.ctl + 8);
   B.lj = (ldsu8*)(B.flagged + kBM);
-  B.pos = B.lj + nl;
-  B.nT = (ldsu8*)(((uintptr_t)(B.pos + nl) + 15u) & ~(uintptr_t)15u);
+  B.pos = B.lj + nl + 16;  // (lj[nl], pos[nl]: spare slots for idle lanes' stores)
+  B.nT = (ldsu8*)(((uintptr_t)(B.pos + nl + 16) + 15u) & ~(uintptr_t)15u);
   B.kT = B.nT + kBN * kRS;
   return B;
 }
@@ -1944,6 +1944,8 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       B.kb[2 * kBN + nm] = 1.0;
     }
   }
+  // +inf past the last mean: A's searches need no bound checks (they read below index 255)
+  for (uint32_t j = nm + t; j < 256u; j += NT) L.mm[j] = kInf;
   fast_sync<NW>();
   PROF_T(b1);
   ASM_MARK("A_BEGIN");
@@ -1958,9 +1960,8 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   uint32_t gj[kA], gp[kA], ps[kA];
   double gv[kA];
   {
-    const double p0 = L.mm[min(128u, nm) - 1], p1 = L.mm[min(64u, nm) - 1], p2 = L.mm[min(192u, nm) - 1];
-    const double p3 = L.mm[min(32u, nm) - 1], p4 = L.mm[min(96u, nm) - 1], p5 = L.mm[min(160u, nm) - 1],
-                 p6 = L.mm[min(224u, nm) - 1];
+    const double p0 = L.mm[127], p1 = L.mm[63], p2 = L.mm[191];
+    const double p3 = L.mm[31], p4 = L.mm[95], p5 = L.mm[159], p6 = L.mm[223];
     bool safe = true;
 #pragma unroll
     for (uint32_t u = 0; u < kA; u++) {
@@ -1972,25 +1973,27 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       safe &= div_safe(gv[u]);
     }
 #pragma unroll
-    for (uint32_t u = 0; u < kA; u++) {
+    for (uint32_t u = 0; u < kA; u++) {  // (the +inf sentinels past nm bound every level)
       const double v = gv[u];
-      uint32_t l = (128u <= nm && p0 < v) ? 128u : 0u;
-      l = (l + 64u <= nm && (l ? p2 : p1) < v) ? l + 64u : l;
+      uint32_t l = p0 < v ? 128u : 0u;
+      l = (l ? p2 : p1) < v ? l + 64u : l;
       const double q = l >= 128u ? (l >= 192u ? p6 : p5) : (l >= 64u ? p4 : p3);
-      l = (l + 32u <= nm && q < v) ? l + 32u : l;
+      l = q < v ? l + 32u : l;
       ps[u] = l;
     }
 #pragma unroll
     for (uint32_t step = 16; step >= 1; step >>= 1) {
       double mv[kA];
 #pragma unroll
-      for (uint32_t u = 0; u < kA; u++) mv[u] = L.mm[min(ps[u] + step, nm) - 1];
+      for (uint32_t u = 0; u < kA; u++) mv[u] = L.mm[ps[u] + step - 1];
 #pragma unroll
-      for (uint32_t u = 0; u < kA; u++) ps[u] = (ps[u] + step <= nm && mv[u] < gv[u]) ? ps[u] + step : ps[u];
+      for (uint32_t u = 0; u < kA; u++) ps[u] = mv[u] < gv[u] ? ps[u] + step : ps[u];
     }
 #pragma unroll
-    for (uint32_t u = 0; u < kA; u++)
-      if (t + u * NT < nt) B.pos[t + u * NT] = (uint8_t)ps[u];
+    for (uint32_t u = 0; u < kA; u++) {  // (idle lanes store to the spare slot: no branch)
+      const uint32_t g = t + u * NT;
+      B.pos[g < nt ? g : kBB * tcap] = (uint8_t)ps[u];
+    }
     // the run-end rows of B (kSR bytes per chunk, in the list area, which D fills later) zeroed
     ldsu64* const sr = (ldsu64*)B.lv;
     for (uint32_t q = t; q < kBB * kSR / 8; q += NT) sr[q] = 0ull;
@@ -2015,7 +2018,8 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     for (uint32_t u = 0; u < kA; u++) {
       const uint32_t g = t + u * NT;
       const uint32_t nx = B.pos[min(g + 1, nt - 1)];
-      if (g < nt && (gp[u] + 1 == tcap || nx != ps[u])) sr[gj[u] * kSR + ps[u]] = (uint8_t)(gp[u] + 1);
+      const bool end = g < nt && (gp[u] + 1 == tcap || nx != ps[u]);
+      sr[end ? gj[u] * kSR + ps[u] : kBB * kSR] = (uint8_t)(gp[u] + 1);  // (else: a spare byte)
     }
   }
   fast_sync<NW>();
@@ -2206,13 +2210,11 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       wq[u] = B.rp[sbase(jc) + gp[u]] & 0xffffu;
     }
 #pragma unroll
-    for (uint32_t u = 0; u < kA; u++) {
-      if (t + u * NT < nt) {
-        const uint32_t x = oo[u] + kk[u] + gp[u] - nn[u];
-        B.lv[x] = gv[u];
-        B.lw[x] = wq[u];
-        B.lj[x] = (uint8_t)(gj[u] | (ps[u] == 0 ? 0x80u : 0u));
-      }
+    for (uint32_t u = 0; u < kA; u++) {  // (idle lanes store to the spare slot: no branch)
+      const uint32_t x = t + u * NT < nt ? oo[u] + kk[u] + gp[u] - nn[u] : kBB * tcap;
+      B.lv[x] = gv[u];
+      B.lw[x] = wq[u];
+      B.lj[x] = (uint8_t)(gj[u] | (ps[u] == 0 ? 0x80u : 0u));
     }
   }
   fast_sync<NW>();
@@ -2667,7 +2669,8 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     uint32_t c = 0;
     while (c < sp.npure) {
       const uint32_t left = sp.npure - c;
-      if (!(fok && nm >= 1 && nm <= kBM && left >= 2 && mainW >= kBatchMinW && tcap <= kBTmax && 8 * tcap >= kSR)) {
+      if (!(fok && nm >= 1 && nm <= kBM && left >= 2 && mainW >= kBatchMinW && tcap <= kBTmax && 8 * tcap >= kSR &&
+            capc >= 256)) {
         // not (yet) batchable: a run of single merges, then look again
         const uint32_t c1 = min(sp.npure, c + kBatchBackoff);
         PROF_T(s3);
