@@ -1850,6 +1850,16 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);
 }
 
+// inclusive sum over the wave's 64 lanes by DPP (row shifts, then the row broadcasts of lanes 15
+// and 31; lanes without a source add 0)
+__device__ __forceinline__ uint32_t wave_incl_add_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);
+  return v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);
+}
 // inclusive sum over the 16 lanes of each DPP row (row_shr 1, 2, 4, 8; lanes without a source add 0)
 __device__ __forceinline__ uint32_t row_incl_add(uint32_t v) {
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);
@@ -1919,13 +1929,8 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   if (wv == 0) {
     const uint32_t tw0 = B.rp[sbase(min(lane, b - 1))], tw = lane < b ? tw0 : 0xffffffffu;
     bool ok = lane < b && tw != 0xffffffffu;
-    double v = ok ? (double)(tw >> 16) : 0.0;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const double o = __shfl_up(v, d, 64);
-      v = (int)lane >= d ? dadd(v, o) : v;
-    }
-    const double T = dadd(mainW, v);
+    const uint32_t v = wave_incl_add_u32(ok ? tw >> 16 : 0u);  // (< 2^22: exact)
+    const double T = dadd(mainW, (double)v);
     ok = ok && T <= 1099511627776.0;
     const uint64_t bad = __ballot(!ok);
     const uint32_t nb = min(bad ? (uint32_t)__builtin_ctzll(bad) : 64u, b);
@@ -2243,12 +2248,13 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     bool tiny = false;  // a numerator near the hardware's rescaling range (then no batch)
     uint32_t mmax = wave_incl_max(m);
     mmax = __builtin_amdgcn_readlane(mmax, 63);
+    // (entries past a list's end are read too -- the next list's, or the layout after the
+    // lists, all inside the workgroup's LDS -- and masked by q + u < m below)
     auto ld = [&](uint32_t q, double (&v)[4], uint32_t (&w)[4]) {
 #pragma unroll
       for (uint32_t u = 0; u < 4; u++) {
-        const uint32_t x = o + min(q + u, m ? m - 1 : 0u);
-        v[u] = B.lv[x];
-        w[u] = B.lw[x];
+        v[u] = B.lv[o + q + u];
+        w[u] = B.lw[o + q + u];
       }
     };
     double v0[4], v1[4];
@@ -2410,16 +2416,8 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     const uint32_t nP = ic >= 1 ? B.nT[(ic - 1) * kRS + jj] : 0u, nI = ic >= 1 ? B.nT[ic * kRS + jj] : 0u,
                    nN = B.nT[(ic + 1) * kRS + jj];
     const uint32_t xP = in ? tw_of(jj, nP) : 0u, xI = in ? tw_of(jj, nI) : 0u, xN = in ? tw_of(jj, nN) : 0u;
-    uint32_t cP = xP, cI = xI, cN = xN;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t a = __shfl_up(cP, d, 64), bI = __shfl_up(cI, d, 64), e = __shfl_up(cN, d, 64);
-      if ((int)lane >= d) {
-        cP += a;
-        cI += bI;
-        cN += e;
-      }
-    }
+    // (inclusive prefixes over the chunks: DPP wave scans, every lane of the wave active)
+    const uint32_t cP = wave_incl_add_u32(xP), cI = wave_incl_add_u32(xI), cN = wave_incl_add_u32(xN);
     const double T = B.bT[jj];
     const double Pi = dadd(F.mp[ic], (double)cI), Pn = dadd(F.mp[ic + 1], (double)cN);
     const double Wi = dadd(L.mw[ic], (double)((cN - xN) - (cI - xI)));  // weight before merge j
