@@ -2295,8 +2295,9 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
         const double m2 = dadd(mean, qq);
         mean = in[u] ? m2 : mean;
         B.lv[at[u]] = mean;
-        lo = mean < lo ? mean : lo;
-        hi = mean > hi ? mean : hi;
+        // (no NaN here: the hardware min / max, without the canonicalisation fmin / fmax add)
+        asm("v_min_f64 %0, %1, %2" : "=v"(lo) : "v"(lo), "v"(mean));
+        asm("v_max_f64 %0, %1, %2" : "=v"(hi) : "v"(hi), "v"(mean));
       }
       __builtin_amdgcn_sched_barrier(0);
       W = Wn[3];
