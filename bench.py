@@ -26,6 +26,11 @@ import os
 import sys
 import time
 
+# Every engine stream its own hardware queue (HIP's default is 4 per process): with two engines in
+# turn there are ~14 streams, and streams sharing a queue run one after another, a 200 ms replay
+# in front holding back the other window's work.  Set before HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+
 import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
