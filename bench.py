@@ -4,9 +4,11 @@
 C4: ONE global DogStatsD-shaped stream of 1e9 samples per flush window
 (counters / gauges / timers / sets over 1M keys, Zipf(1.0) popularity, already parsed),
 key-sharded over the N GPUs of one node by veneur's worker routing, FNV-1a digest % N
-(server.go:655), with the hot keys split: the counter / timer / set keys whose window count
-passes a share of the per-GPU load are dealt round-robin over every GPU by their window arrival
-index and combined on their owner at flush over RCCL (include/veneur_amd.h "multi-GPU").  Every
+(server.go:655).  In the opt-in fast mode (or with --split) the hot keys are split: the counter /
+timer / set keys whose window count passes a share of the per-GPU load are dealt round-robin over
+every GPU by their window arrival index and combined on their owner at flush over RCCL
+(include/veneur_amd.h "multi-GPU"); in the default exact mode every key stays on its owner -- the
+window is bound by the hottest timer's sequential chain, which no split can shorten.  Every
 rank generates the whole stream on its GPU and keeps its own records, so the N ranks together
 hold exactly the one stream (strong scaling: the total work is fixed, N = 1 processes all 1e9).
 
@@ -491,6 +493,10 @@ def main():
     ap.add_argument("--hot-stride", type=int, default=256,
                     help="hot-key detector: count every hot_stride-th record (vn_hot_detect)")
     ap.add_argument("--no-split", action="store_true", help="route every key by digest %% N (no hot keys)")
+    ap.add_argument("--split", action="store_true",
+                    help="exact mode: split the hot counter / set keys as the fast mode does (default: off -- "
+                         "measured, DESIGN.md §6: the window is bound by the hottest timer's chain, which a "
+                         "split cannot shorten, and the combine costs every rank more than the balance gains)")
     ap.add_argument("--exact-threshold", type=int, default=0,
                     help="0 (default): every histogram merge replayed exactly; N: the opt-in fast mode "
                          "(geometric pieces past N samples per key, rank-error parity only)")
@@ -542,6 +548,9 @@ def main():
     t0 = time.time()
     split = {0: np.zeros(0, np.uint32), 2: np.zeros(0, np.uint32), 3: np.zeros(0, np.uint32)}
     detect = None
+    # hot keys split over the GPUs: the fast mode's default; in the exact mode only with --split
+    if args.exact_threshold == 0 and not args.split:
+        args.no_split = True
     if not args.no_split:
         thr = args.samples / ((args.sim_world if sim else world) * args.hot_div)
         if sim:
@@ -756,8 +765,9 @@ def main():
         "dtype": "f64/u64",
         "data": "synthetic (one global DogStatsD-shaped C4 stream generated in HBM, seeded)",
         "config": {"workload": "C4 mixed counters/gauges/timers/sets, %d keys, %d samples per flush window over %d "
-                               "GPU(s), Zipf(1.0), hot counter/set keys split, %s" % (
+                               "GPU(s), Zipf(1.0), %s, %s" % (
                                    args.keys, args.samples, world,
+                                   "hot keys split over the GPUs" if not args.no_split else "every key on its owner",
                                    "t-digest fast mode (geometric pieces past %d samples)" % args.exact_threshold
                                    if args.exact_threshold else "every t-digest merge replayed exactly"),
                    "histo_mode": "fast (non-conforming: rank-error bound 3e-3, not the reference's digests)"
