@@ -265,6 +265,14 @@ def c5_leg(args, rank, world, ctrl, device):
         f = g.flush_raw()
         A.lib.vn_device_synchronize(device)
         phases["flush"] = (time.perf_counter() - tp) * 1e3
+        # one more window with the engine's kernel timing (HIP events, phases run one after another):
+        # the replay's own kernel time, to set against a profiler's trace of the same leg
+        g.timing_enable(True)
+        window()
+        tmg = g.timing()
+        g.timing_enable(False)
+        kernel_ms = {k: round(float(tmg[k]), 2) for k in ("ms_import_decode", "ms_import_drain", "ms_histo_replay",
+                                                          "ms_radix_scatter_total", "ms_flush")}
         hq = np.ctypeslib.as_array(f.histo_quantiles, shape=(f.n_histo * len(PCT),)).reshape(-1, len(PCT)).copy() \
             if f.n_histo else np.zeros((0, len(PCT)))
         hst = np.ctypeslib.as_array(f.histo_stats, shape=(f.n_histo * 8,)).reshape(-1, 8).copy() \
@@ -321,6 +329,7 @@ def c5_leg(args, rank, world, ctrl, device):
             "n_gpus": world, "imports_per_s": n_imp / (ms * 1e-3), "payload_GBs": all_bytes / (ms * 1e-3) / 1e9,
             "ms_per_window": ms, "windows": args.c5_windows, "payloads_per_window": n_imp,
             "phases_ms_synchronised": {k: round(v, 2) for k, v in per_rank[0]["phases"].items()},
+            "kernel_ms_timing_mode_rank0": kernel_ms,
             "ranks": {"ms_per_window": [round(r["ms"], 2) for r in per_rank],
                       "histo_set_keys": [r["keys"] for r in per_rank]},
             "payload_bytes_per_window": all_bytes,

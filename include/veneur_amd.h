@@ -328,6 +328,10 @@ typedef struct {
   float ms_part_scatter;
   uint64_t part_scatter_launches;
   uint64_t part_scatter_bytes;
+  /* imports (vn_import_histos*): the digest decode's kernels (count and emit passes), and the
+   * drains of the imported centroids through the exact replay (grouping sort, chunk sort, replay) */
+  float ms_import_decode;
+  float ms_import_drain;
 } vn_timing;
 int vn_timing_enable(vn_engine* eng, int enable);
 int vn_get_timing(vn_engine* eng, vn_timing* out);

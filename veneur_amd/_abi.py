@@ -125,7 +125,8 @@ class Timing(C.Structure):
                 ("ms_main_ready", C.c_float), ("ms_split_ready", C.c_float),
                 ("ms_split_histo_ready", C.c_float), ("ms_split_set_prefix_ready", C.c_float),
                 ("ms_part_scatter", C.c_float), ("part_scatter_launches", C.c_uint64),
-                ("part_scatter_bytes", C.c_uint64)]
+                ("part_scatter_bytes", C.c_uint64), ("ms_import_decode", C.c_float),
+                ("ms_import_drain", C.c_float)]
 
 
 class SynthConfig(C.Structure):

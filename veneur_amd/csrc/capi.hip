@@ -515,6 +515,8 @@ void destroy_impl(vn_engine* e) {
   for (auto ev : e->pool_rp_storage) (void)hipEventDestroy(ev);
   for (auto ev : e->pool_ss_storage) (void)hipEventDestroy(ev);
   for (auto ev : e->pool_ps_storage) (void)hipEventDestroy(ev);
+  for (auto ev : e->pool_id_storage) (void)hipEventDestroy(ev);
+  for (auto ev : e->pool_im_storage) (void)hipEventDestroy(ev);
   for (auto& ev : e->ev)
     if (ev) (void)hipEventDestroy(ev);
   if (e->st) (void)hipStreamDestroy(e->st);
@@ -705,16 +707,20 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
     e->rstat_h = RadixStats{&e->pool, 0, 0};
     e->rstat_s = RadixStats{&e->pool, 0, 0};
     VN_HIP_CHECK(hipEventRecord(e->ev[0], st));
+    e->ev_rec |= 1u << 0;
   }
   if (tm) {
     // measured: one phase at a time on the main stream
     side_begin(e);
     ingest_counters(e, b->n_counter, b->counter_slot, b->counter_value, b->counter_rate);
     VN_HIP_CHECK(hipEventRecord(e->ev[1], st));
+    e->ev_rec |= 1u << 1;
     ingest_gauges(e, b->n_gauge, b->gauge_slot, b->gauge_value);
     VN_HIP_CHECK(hipEventRecord(e->ev[2], st));
+    e->ev_rec |= 1u << 2;
     ingest_sets(e, b->n_set, b->set_slot, b->set_member_off, b->set_member_bytes, b->set_hash);
     VN_HIP_CHECK(hipEventRecord(e->ev[3], st));
+    e->ev_rec |= 1u << 3;
     ingest_histos(e, b->n_histo, b->histo_slot, b->histo_value, b->histo_rate);
     side_join(e);
   } else {
@@ -739,7 +745,10 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
     set_finish(e);
     side_join(e);
   }
-  if (tm) VN_HIP_CHECK(hipEventRecord(e->ev[4], st));
+  if (tm) {
+    VN_HIP_CHECK(hipEventRecord(e->ev[4], st));
+    e->ev_rec |= 1u << 4;
+  }
   VN_HIP_CHECK(hipGetLastError());  // a launch that could not start (e.g. LDS over budget) fails loudly
   e->processed += b->n_counter + b->n_gauge + b->n_histo + b->n_set;
 }
@@ -891,6 +900,7 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
     return VN_EINVAL;
   }
   e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 0xFFFFFFFFu;  // exact
+  if (const char* lr = getenv("VN_LONG_REPLAY")) e->long_replay = (uint32_t)strtoul(lr, nullptr, 10);  // (A/B knob)
   e->hot_prefix = std::min(e->exact_threshold, cfg->histo_hot_prefix ? cfg->histo_hot_prefix : 4096u);
   e->piece_growth = cfg->histo_piece_growth ? std::min(cfg->histo_piece_growth, 1000u) : 25u;
   e->temp_cap = temp_buffer_cap(e->cfg.compression);
@@ -1128,10 +1138,15 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
       VN_HIP_CHECK(hipEventSynchronize(e->ev[6]));
       vn_timing& t = e->last;
       t = vn_timing{};
-      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_counter, e->ev[0], e->ev[1]));
-      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_gauge, e->ev[1], e->ev[2]));
-      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_set, e->ev[2], e->ev[3]));
-      VN_HIP_CHECK(hipEventElapsedTime(&t.ms_ingest_histo, e->ev[3], e->ev[4]));
+      // (a window with no vn_ingest -- imports only -- recorded none of the ingest events)
+      auto span = [&](float* o, int a, int b) {
+        if ((e->ev_rec >> a & 1u) && (e->ev_rec >> b & 1u)) VN_HIP_CHECK(hipEventElapsedTime(o, e->ev[a], e->ev[b]));
+      };
+      span(&t.ms_ingest_counter, 0, 1);
+      span(&t.ms_ingest_gauge, 1, 2);
+      span(&t.ms_ingest_set, 2, 3);
+      span(&t.ms_ingest_histo, 3, 4);
+      e->ev_rec = 0;
       VN_HIP_CHECK(hipEventElapsedTime(&t.ms_flush, e->ev[5], e->ev[6]));
       t.sort_passes_histo = e->rstat_h.launches;
       t.sort_passes_set = e->rstat_s.launches;
@@ -1160,6 +1175,9 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
       t.set_segment_launches = e->kstat_ss.launches;
       t.set_segment_bytes = e->kstat_ss.bytes;
       t.ms_part_scatter = pool_ms(e->pool_ps);
+      t.ms_import_decode = pool_ms(e->pool_id);
+      t.ms_import_drain = pool_ms(e->pool_im);
+      e->pool_id.used = e->pool_im.used = 0;
       t.part_scatter_launches = e->rstat_c.launches;
       t.part_scatter_bytes = e->rstat_c.bytes;
     }
@@ -1205,6 +1223,14 @@ int vn_timing_enable(vn_engine* e, int enable) {
         ps->resize(64);
         for (auto& ev : *ps) VN_HIP_CHECK(hipEventCreate(&ev));
       }
+      for (auto* ps : {&e->pool_id_storage, &e->pool_im_storage}) {
+        ps->resize(256);
+        for (auto& ev : *ps) VN_HIP_CHECK(hipEventCreate(&ev));
+      }
+      e->pool_id.ev = e->pool_id_storage.data();
+      e->pool_id.cap = (int)e->pool_id_storage.size();
+      e->pool_im.ev = e->pool_im_storage.data();
+      e->pool_im.cap = (int)e->pool_im_storage.size();
       e->pool_rp.ev = e->pool_rp_storage.data();
       e->pool_rp.cap = (int)e->pool_rp_storage.size();
       e->pool_ss.ev = e->pool_ss_storage.data();

@@ -128,6 +128,7 @@ struct vn_engine {
   hipStream_t st5 = nullptr;
   hipEvent_t ev_fork5 = nullptr, ev_join5 = nullptr;
   // the few longest batched replays on CUs no other stream uses (null: st5 takes them all)
+  uint32_t ev_rec = 0;           // timing: which of ev[0..4] this window recorded
   hipStream_t st6 = nullptr;     // the reserved CUs (vn_config.replay_reserved_cus), or none
   uint32_t reserved_cus = 0;
   std::vector<uint32_t> amask;   // every CU but the reserved ones
@@ -320,6 +321,7 @@ struct vn_engine {
   vn::RadixStats rstat_c, rstat_h, rstat_s;
   // timed launches of the exact replay and of the set state machine (timing mode)
   vn::EventPool pool_rp, pool_ss, pool_ps;
-  std::vector<hipEvent_t> pool_rp_storage, pool_ss_storage, pool_ps_storage;
+  std::vector<hipEvent_t> pool_rp_storage, pool_ss_storage, pool_ps_storage, pool_id_storage, pool_im_storage;
+  vn::EventPool pool_id, pool_im;  // timing: import decode kernels, import drains
   vn::RadixStats kstat_rp, kstat_ss;
 };

@@ -345,8 +345,17 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   if (!n) return;
   hipStream_t st = e->st;
   ImportScratch& s = e->imp;
-  hipLaunchKernelGGL(k_gob_count, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, e->cap[VN_HISTO], off, bytes,
-                     s.cnt, e->h_err);
+  // (timing: each decode kernel between a pair of events)
+  auto ev_pair = [&](EventPool& p, auto&& launch) {
+    hipEvent_t a = e->timing ? p.next() : nullptr, b = e->timing ? p.next() : nullptr;
+    if (a && b) VN_HIP_CHECK(hipEventRecord(a, st));
+    launch();
+    if (a && b) VN_HIP_CHECK(hipEventRecord(b, st));
+  };
+  ev_pair(e->pool_id, [&] {
+    hipLaunchKernelGGL(k_gob_count, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, e->cap[VN_HISTO], off, bytes,
+                       s.cnt, e->h_err);
+  });
   scan_exclusive_u32(s.cnt, s.coff, n, e->ss, st);
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 9, s.coff + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipStreamSynchronize(st));
@@ -355,8 +364,10 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   if (!nc) return;
   if (nc <= s.cap_cent) {
     if (s.acc + nc > s.cap_cent) histo_imports_drain(e);
-    hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.acc,
-                       s.cslot, s.cmean, s.cw, e->h_err);
+    ev_pair(e->pool_id, [&] {
+      hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.acc,
+                         s.cslot, s.cmean, s.cw, e->h_err);
+    });
     s.acc += nc;
     return;
   }
@@ -374,8 +385,10 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
     const uint64_t c0 = co[b0], c1 = co[b1];
     if (c1 > c0) {
       if (s.acc + (c1 - c0) > s.cap_cent) histo_imports_drain(e);
-      hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
-                         slot + b0, s.coff + b0, s.acc - c0, s.cslot, s.cmean, s.cw, e->h_err);
+      ev_pair(e->pool_id, [&] {
+        hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
+                           slot + b0, s.coff + b0, s.acc - c0, s.cslot, s.cmean, s.cw, e->h_err);
+      });
       s.acc += c1 - c0;
     }
     b0 = b1;
@@ -387,7 +400,10 @@ void histo_imports_drain(vn_engine* e) {
   if (!s.acc) return;
   const uint64_t n = s.acc;
   s.acc = 0;
+  hipEvent_t a = e->timing ? e->pool_im.next() : nullptr, b = e->timing ? e->pool_im.next() : nullptr;
+  if (a && b) VN_HIP_CHECK(hipEventRecord(a, e->st));
   ingest_histos(e, n, s.cslot, s.cmean, nullptr, s.cw);
+  if (a && b) VN_HIP_CHECK(hipEventRecord(b, e->st));
 }
 
 }  // namespace vn
