@@ -3,6 +3,8 @@
 
     python tools/pmc_traffic.py gpurun_out/TAG_pmc_fetch gpurun_out/TAG_pmc_write TAG [KERNEL BENCH_JSON WINDOWS]
 
+WINDOWS 0 (default): the ingest windows of the run, counted as its k_exact_chunk_owner dispatches.
+
 Each pass is its own `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE` run of the same bench
 command (FETCH_SIZE uses 3 TCC slots, WRITE_SIZE 2: they cannot share a pass).  Both counters
 are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the
@@ -60,7 +62,10 @@ def other_kernel(fetch, write, kernel, bench_json, tag, windows):
     with open(bench_json) as fh:
         line = [ln for ln in fh.read().splitlines() if ln.startswith("{")][-1]
     kern = {k["kernel"]: k for k in json.loads(line)["roofline"]["kernels"]}[kernel]
-    match = lambda name: kernel in name and "_list" not in name
+    fam = (kernel, "k_exact_long_stats") if kernel == "k_histo_exact" else (kernel,)
+    match = lambda name: any(k in name for k in fam) and "_list" not in name
+    if windows <= 0:  # one k_exact_chunk_owner per ingest window with exact replays
+        windows = sum(1 for (name, _, _) in fetch.values() if "k_exact_chunk_owner" in name)
     fb = [v * 1024.0 for (name, _, v) in fetch.values() if match(name)]
     wb = [v * 1024.0 for (name, _, v) in write.values() if match(name)]
     if not fb or len(fb) != len(wb):
@@ -88,7 +93,7 @@ def main():
     fetch = read_pass(fetch_dir, "FETCH_SIZE")
     write = read_pass(write_dir, "WRITE_SIZE")
     if len(sys.argv) > 5 and sys.argv[4] != KERNEL:
-        res = other_kernel(fetch, write, sys.argv[4], sys.argv[5], tag, int(sys.argv[6]) if len(sys.argv) > 6 else 1)
+        res = other_kernel(fetch, write, sys.argv[4], sys.argv[5], tag, int(sys.argv[6]) if len(sys.argv) > 6 else 0)
         root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
         for p in (os.path.join(root, "roofline_traffic.json"),
                   os.path.join(root, "profiles", "%s_pmc_traffic.json" % tag)):
