@@ -494,7 +494,8 @@ def main():
     ap.add_argument("--pipeline", type=int, default=0,
                     help="engines per GPU taking the windows in turn (window i + 1 ingested and combined while "
                          "window i's longest replays finish; one communicator per engine, the combines entered in "
-                         "window order); 1: one engine, windows back to back; 0 (default): 2")
+                         "window order); 1: one engine, windows back to back; 0 (default): 3 (C4 at N = 1: 87 ms per window "
+                         "against 113 at 2, 4 does not fit in HBM beside the generated window)")
     ap.add_argument("--reserved-cus", type=int, default=0,
                     help="CUs kept for the longest exact replays (vn_config.replay_reserved_cus); 0 (default): none")
     ap.add_argument("--no-stagger", dest="stagger", action="store_false",
@@ -582,7 +583,7 @@ def main():
     # reference's flush goroutine works on the swapped maps while the workers take the next
     # interval.  Flushes are entered in window order, so every rank issues the split combine's
     # collectives (one communicator per engine) in the same order.
-    D = max(1, args.pipeline if args.pipeline > 0 else 2)
+    D = max(1, args.pipeline if args.pipeline > 0 else 3)
 
     # (measured, DESIGN.md §4: the reservation costs the other windows more than it gains)
     reserved = max(0, args.reserved_cus)

@@ -245,6 +245,12 @@ struct MergeParams {
   uint32_t capc;
   uint32_t* err;
 };
+// Out-of-line functions take MergeParams as three scalars: the AMDGPU calling convention passes
+// at most 16 registers of aggregates directly, and MergeParams (5) + Lds (13) would put Lds on the
+// private stack -- 52 B per lane written before every call and read back by the callee
+#define MP_PARAMS const double mp_delta_, const uint32_t mp_capc_, uint32_t* const mp_err_
+#define MP_ARGS(m) (m).delta, (m).capc, (m).err
+#define MP_UNPACK(name) const MergeParams name{mp_delta_, mp_capc_, mp_err_}
 
 struct Lds {
   ldsf64 *mm, *mw;        // main centroids [capc]
@@ -377,8 +383,9 @@ __device__ __noinline__ void sort_temps(const ldsf64* tv, const ldsf64* tw, ldsf
 
 // mergeAllTemps of the sorted temps L.sv/L.sw (np of them, Add-order weight sum tempW)
 // into main L.mm/L.mw.  One wave; every step is a parallel pass of O(log) depth.
-__device__ __noinline__ NmW merge_sorted(const MergeParams x, const Lds L, const uint32_t nm, const double mainW,
-                                        uint32_t np, double tempW) {
+__device__ __noinline__ NmW merge_sorted(const Lds L, MP_PARAMS, const uint32_t nm, const double mainW, uint32_t np,
+                                        double tempW) {
+  MP_UNPACK(x);
   const uint32_t lane = threadIdx.x;
   PROF_T(p0);
   const double T = dadd(mainW, tempW);  // totalWeight := td.mainWeight + td.tempWeight
@@ -817,7 +824,7 @@ __device__ __forceinline__ void merge_any(const MergeParams x, const Lds L, uint
   // nc <= m < 64 * R: the fast merge's start enumeration (t < 64 * R) covers every centroid
   const uint32_t m = nm + np;
   if (np > 64 || m >= 64u * kR) {
-    const NmW r = merge_sorted(x, L, nm, mainW, np, tempW);
+    const NmW r = merge_sorted(L, MP_ARGS(x), nm, mainW, np, tempW);
     nm = r.nm;
     mainW = r.w;
   } else if (m < 128) merge_sorted_fast<2>(x, L, nm, mainW, np, tempW);
@@ -827,14 +834,15 @@ __device__ __forceinline__ void merge_any(const MergeParams x, const Lds L, uint
 }
 
 // merge_any out of line: the long replays' rare fallback, kept out of their merge loop's code
-__device__ __noinline__ NmW merge_any_v(const MergeParams x, const Lds L, uint32_t nm, double mainW, uint32_t np,
-                                       double tempW) {
+__device__ __noinline__ NmW merge_any_v(const Lds L, MP_PARAMS, uint32_t nm, double mainW, uint32_t np, double tempW) {
+  MP_UNPACK(x);
   merge_any(x, L, nm, mainW, np, tempW);
   return NmW{nm, mainW};
 }
 
 // sort the pending temps in LDS and merge them
-__device__ __noinline__ NmW merge_pending_v(const MergeParams x, const Lds L, uint32_t nm, double mainW, uint32_t np) {
+__device__ __noinline__ NmW merge_pending_v(const Lds L, MP_PARAMS, uint32_t nm, double mainW, uint32_t np) {
+  MP_UNPACK(x);
   PROF_T(a0);
   const double tempW = temp_weight(L.tw, np);
   sort_temps(L.tv, L.tw, L.sv, L.sw, np);
@@ -844,7 +852,7 @@ __device__ __noinline__ NmW merge_pending_v(const MergeParams x, const Lds L, ui
   return NmW{nm, mainW};
 }
 __device__ __forceinline__ void merge_pending(const MergeParams x, const Lds L, uint32_t& nm, double& mainW, uint32_t np) {
-  const NmW r = merge_pending_v(x, L, nm, mainW, np);
+  const NmW r = merge_pending_v(L, MP_ARGS(x), nm, mainW, np);
   nm = r.nm;
   mainW = r.w;
 }
@@ -1192,9 +1200,9 @@ struct FastLds {
 __host__ __device__ inline uint32_t fast_extra_bytes(uint32_t capc, uint32_t TP, uint32_t JW) {
   return 8u * (capc + 2) + 8u * TP + 8u * JW + 8u * 4 + 8u * 2 + 4u * JW + 4u * JW + 4u * 8 + 16u;
 }
-__device__ __forceinline__ FastLds fast_layout(char* p, uint32_t capc, uint32_t TP, uint32_t JW) {
+__device__ __forceinline__ FastLds fast_layout_at(ldsf64* base, uint32_t capc, uint32_t TP, uint32_t JW) {
   FastLds F;
-  F.mp = (ldsf64*)p;
+  F.mp = base;
   F.sp = F.mp + (capc + 2);
   F.kk = F.sp + TP;
   F.gmask = (ldsu64*)(F.kk + JW);
@@ -1203,6 +1211,14 @@ __device__ __forceinline__ FastLds fast_layout(char* p, uint32_t capc, uint32_t 
   F.ism = F.flag + JW;
   F.misc = F.ism + JW;
   return F;
+}
+__device__ __forceinline__ FastLds fast_layout(char* p, uint32_t capc, uint32_t TP, uint32_t JW) {
+  return fast_layout_at((ldsf64*)p, capc, TP, JW);
+}
+// FastLds again from its base and the Lds layout (capc = mw - mm, TP = tw - tv): out-of-line
+// callees take the base, not the 8-register struct (see MP_PARAMS)
+__device__ __forceinline__ FastLds fast_of(const Lds& L, ldsf64* base) {
+  return fast_layout_at(base, (uint32_t)(L.mw - L.mm), (uint32_t)(L.tw - L.tv), L.JW);
 }
 
 template <int NW>
@@ -1655,7 +1671,7 @@ __device__ __forceinline__ MergeState merge_step(const MergeParams mp, const Lds
     return st;
   }
   if (wv == 0) {
-    const NmW r = merge_any_v(mp, L, st.nm, st.w, n_, tempW);
+    const NmW r = merge_any_v(L, MP_ARGS(mp), st.nm, st.w, n_, tempW);
     if (lane == 0) {
       S.fb_nm = r.nm;
       S.fb_w = r.w;
@@ -1675,9 +1691,11 @@ __device__ __forceinline__ MergeState merge_step(const MergeParams mp, const Lds
   return st;
 }
 template <int NW>
-__device__ __noinline__ MergeState merge_step_cold(const MergeParams mp, const Lds L, const FastLds F, MwSharedL& S,
-                                                   MergeState st, uint32_t n_, double tempW, bool tint, double k0) {
-  return merge_step<NW>(mp, L, F, S, st, n_, tempW, tint, k0);
+__device__ __noinline__ MergeState merge_step_cold(const Lds L, ldsf64* fbase, MwSharedL& S, MP_PARAMS, uint32_t st_nm,
+                                                   double st_w, bool st_fok, uint32_t n_, double tempW, bool tint,
+                                                   double k0) {
+  MP_UNPACK(mp);
+  return merge_step<NW>(mp, L, fast_of(L, fbase), S, MergeState{st_nm, st_w, st_fok}, n_, tempW, tint, k0);
 }
 
 // ---- batched replay of consecutive pure chunks (the long replays' steady state).
@@ -2553,7 +2571,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     fok = r.fok;
   };
   auto merge_sorted_cold = [&](uint32_t n_, double tempW, bool tint) {
-    const MergeState r = merge_step_cold<NW>(mp, L, F, S, MergeState{nm, mainW, fok}, n_, tempW, tint, k0);
+    const MergeState r = merge_step_cold<NW>(L, F.mp, S, MP_ARGS(mp), nm, mainW, fok, n_, tempW, tint, k0);
     nm = r.nm;
     mainW = r.w;
     fok = r.fok;
