@@ -99,8 +99,9 @@ def detect_split(args, V, ctrl, world, rank, local_rank, thr):
     on every rank (detection stride args.hot_stride)."""
     s0 = V.DeviceStream(args.seed, args.keys, args.samples, rank, world, device=local_rank, split=None)
     with V.Engine(tuple(max(1, x) for x in s0.n_slots), compression=100.0, percentiles=PCT,
-                  max_batch_records=max(s0.counts) + 1, max_batch_member_bytes=s0.counts[3] * 11 + 64,
-                  device=local_rank, exact_threshold=args.exact_threshold) as e0:
+                  max_batch_records=max(s0.counts) + 1, max_class_records=tuple(int(c) + 1 for c in s0.counts),
+                  max_batch_member_bytes=s0.counts[3] * 11 + 64, device=local_rank,
+                  exact_threshold=args.exact_threshold) as e0:
         e0.hot_detect(args.hot_stride)
         e0.ingest_device(s0.batch)
         e0.flush_raw()
@@ -591,6 +592,7 @@ def main():
     def make_engine():
         e = V.Engine(tuple(max(1, x) for x in n_slots), compression=100.0, percentiles=PCT,
                      max_batch_records=max(stream.counts) + 1,
+                     max_class_records=tuple(int(c) + 1 for c in stream.counts),
                      max_batch_member_bytes=stream.counts[3] * 11 + 64, device=local_rank,
                      exact_threshold=args.exact_threshold, hot_prefix=args.hot_prefix,
                      piece_growth=args.piece_growth, split_max_records=max(stream.split_counts) + 1,

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define VN_ABI_VERSION 4
+#define VN_ABI_VERSION 5
 
 enum {
   VN_OK = 0,
@@ -84,8 +84,14 @@ typedef struct {
    * latency-bound for hundreds of ms): rounded up to whole groups of 8 (one CU per XCC), at
    * most a quarter of the device; every other stream of this engine (and of its split engine)
    * is masked off them.  0 (default): none -- the chains share their CUs with whatever else
-   * runs.  Worth it when windows overlap (several engines taking the windows in turn). */
+   * runs.  Measured on C4 with several engines taking the windows in turn: slower at 8-32
+   * CUs, kept as an option. */
   uint32_t replay_reserved_cus;
+  /* per class (counter, gauge, histo, set): records of that class one ingest or import call
+   * may carry, and so the size of that class's sort and partition buffers; 0 ->
+   * max_batch_records.  A mixed stream's classes differ by 2-4x (C4: 425M counters, 216M
+   * timers per window), and the histo buffers (9 sort arrays) dominate an engine's HBM. */
+  uint64_t max_batch_class_records[VN_NCLASS];
 } vn_config;
 
 /* One ingest batch: per-class SoA streams in arrival order (the order ProcessMetric saw

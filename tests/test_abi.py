@@ -24,14 +24,14 @@ def test_library_exports_every_declared_symbol():
     for s in sorted(syms):
         assert hasattr(A.lib, s), "missing export %s" % s
     assert set(A.EXPORTED) == syms
-    assert A.lib.vn_abi_version() == 4
+    assert A.lib.vn_abi_version() == 5
 
 
 def test_struct_layouts_match_header():
     import ctypes as C
     import veneur_amd._abi as A
     # sizes derived from the C declarations (LP64)
-    assert C.sizeof(A.Config) == 4 + 16 + 4 + 8 + 4 + 4 + 16 * 8 + 8 + 8 + 4 + 4 + 4 + 4 + 8 + 8 + 4 + 4  # (+ tail padding)
+    assert C.sizeof(A.Config) == 4 + 16 + 4 + 8 + 4 + 4 + 16 * 8 + 8 + 8 + 4 + 4 + 4 + 4 + 8 + 8 + 4 + 4 + 4 * 8  # (+ padding)
     assert C.sizeof(A.Batch) == 16 * 8
     assert C.sizeof(A.SplitBatch) == 9 * 8
     assert C.sizeof(A.SetState) == 4 + 5 * 4

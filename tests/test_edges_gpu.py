@@ -234,3 +234,47 @@ def test_submit_counter_only_batch_then_refill_stage():
         np.add.at(exp, s, v.astype(np.int64))
     assert f.counter_slot.tolist() == np.nonzero(exp)[0].tolist()
     np.testing.assert_array_equal(f.counter_value, exp[f.counter_slot])
+
+
+def test_per_class_record_caps():
+    """vn_config.max_batch_class_records: each class's batch is held to its own cap (its buffers
+    are sized by it); a class cap above max_batch_records is refused at creation."""
+    caps, cls = (64,) * 4, (300, 200, 500, 100)
+    rng = np.random.default_rng(11)
+
+    def recs(n):
+        return rng.integers(0, 64, n).astype(np.uint32), np.round(rng.lognormal(2, 1, n), 3)
+
+    cs, cv = recs(cls[0])
+    gs, gv = recs(cls[1])
+    hs, hv = recs(cls[2])
+    ss, _ = recs(cls[3])
+    members = [("u%d" % i).encode() for i in rng.integers(0, 1000, cls[3])]
+    off = np.zeros(cls[3] + 1, np.uint32)
+    off[1:] = np.cumsum([len(m) for m in members])
+    mb = np.frombuffer(b"".join(members), np.uint8)
+    one = lambda n: np.ones(n, np.float32)
+    d = stream(c_slot=cs, c_val=cv, c_rate=one(len(cs)), g_slot=gs, g_val=gv, h_slot=hs, h_val=hv,
+               h_rate=one(len(hs)), s_slot=ss, s_off=off, s_bytes=mb)
+    w = run_oracle(d, caps)
+    with V.Engine(caps, percentiles=PCT, max_batch_records=512, max_batch_member_bytes=1 << 16,
+                  max_class_records=cls) as e:
+        assert e.max_class_records == cls
+        # every class at exactly its cap
+        e.ingest(counters=(cs, cv, one(len(cs))), gauges=(gs, gv), histos=(hs, hv, one(len(hs))), sets=(ss, off, mb))
+        for over in ({"gauges": recs(cls[1] + 1)},
+                     {"sets": (np.zeros(cls[3] + 1, np.uint32), np.arange(cls[3] + 2, dtype=np.uint32), mb)},
+                     {"histos": recs(cls[2] + 1) + (one(cls[2] + 1),)}):
+            with pytest.raises(V.EngineError):  # one record over the class's cap, within max_batch_records
+                e.ingest(**over)
+        f = e.flush()
+    # every record of the capped batch landed (the rejected ones left no trace)
+    assert dict(zip(f.counter_slot.tolist(), f.counter_value.tolist())) == \
+        {s: w.counter_value(s) for s in range(64) if w.touched(0, s)}
+    assert dict(zip(f.gauge_slot.tolist(), f.gauge_value.tolist())) == \
+        {s: w.gauge_value(s) for s in range(64) if w.touched(1, s)}
+    assert f.set_estimate.tolist() == [w.set_estimate(int(s)) for s in f.set_slot]
+    oq = np.array([[w.histo_quantile(int(s), p) for p in PCT] for s in f.histo_slot])
+    np.testing.assert_array_equal(f.histo_quantiles, oq)
+    with pytest.raises(V.EngineError):
+        V.Engine(caps, max_batch_records=256, max_class_records=(300, 0, 0, 0))

@@ -58,7 +58,7 @@ class Config(C.Structure):
                 ("histo_exact_threshold", C.c_uint32),
                 ("histo_hot_prefix", C.c_uint32), ("histo_piece_growth", C.c_uint32),
                 ("split_max_records", C.c_uint64), ("split_compression", C.c_double),
-                ("replay_reserved_cus", C.c_uint32)]
+                ("replay_reserved_cus", C.c_uint32), ("max_batch_class_records", C.c_uint64 * 4)]
 
 
 class SplitBatch(C.Structure):
@@ -180,7 +180,7 @@ def _sig(name, res, *args):
 vp = C.c_void_p
 _sig("vn_abi_version", C.c_int)
 _sig("vn_struct_size", C.c_size_t, C.c_int)
-ABI_VERSION = 4
+ABI_VERSION = 5
 _sig("vn_engine_create", C.c_int, C.POINTER(Config), C.POINTER(vp))
 _sig("vn_engine_destroy", None, vp)
 _sig("vn_last_error", C.c_char_p, vp)

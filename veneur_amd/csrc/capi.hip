@@ -130,6 +130,7 @@ void create_impl(vn_engine* e) {
     }
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork5, hipEventDisableTiming));
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join5, hipEventDisableTiming));
+    VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_rest5, hipEventDisableTiming));
     // vn_config.replay_reserved_cus: the longest batched replays (one workgroup each, hundreds of
     // ms, latency-bound at one wave per SIMD) on the last CUs, which every other stream of the
     // engine leaves alone -- the other windows' sorts and scatters no longer share those CUs'
@@ -146,6 +147,11 @@ void create_impl(vn_engine* e) {
       VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st6, (uint32_t)tmask.size(), tmask.data()));
       VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join6, hipEventDisableTiming));
       e->reserved_cus = r;
+    }
+    if (!e->st6) {  // the longest batched replays' stream: they start once their own chunks are sorted
+      if (e->side_cus != ncu) VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st6, (uint32_t)rmask.size(), rmask.data()));
+      else VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st6, hipStreamNonBlocking, prio_hi));
+      VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join6, hipEventDisableTiming));
     }
   }
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
@@ -167,7 +173,9 @@ void create_impl(vn_engine* e) {
   VN_HIP_CHECK(hipEventCreate(&e->ev_wmain));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join3, hipEventDisableTiming));
   hipStream_t st = e->st;
-  const uint64_t R = e->max_records;
+  // each class's buffers sized by its own record cap
+  const uint64_t R = e->max_cls[VN_HISTO], Rcg = std::max(e->max_cls[VN_COUNTER], e->max_cls[VN_GAUGE]),
+                 Rs = e->max_cls[VN_SET];
   const uint32_t cc = e->cap[VN_COUNTER], cg = e->cap[VN_GAUGE], ch = e->cap[VN_HISTO], cs = e->cap[VN_SET];
   const uint32_t capc = e->cap_cent;
   const uint32_t capmax = std::max(std::max(cc, cg), std::max(ch, cs));
@@ -177,8 +185,8 @@ void create_impl(vn_engine* e) {
   dalloc(e->gseq, cg); dzero(e->gseq, cg, st);
   dalloc(e->gval, cg); dzero(e->gval, cg, st);
   dalloc(e->gtouch, cg); dzero(e->gtouch, cg, st);
-  dalloc(e->pk, (cc || cg) ? R : 0);
-  dalloc(e->pp, (cc || cg) ? R : 0);
+  dalloc(e->pk, (cc || cg) ? Rcg : 0);
+  dalloc(e->pp, (cc || cg) ? Rcg : 0);
 
   dalloc(e->hst, (size_t)ch * VN_HISTO_STATS);
   dalloc(e->hncent, ch); dzero(e->hncent, ch, st);
@@ -277,8 +285,8 @@ void create_impl(vn_engine* e) {
   dalloc(e->stouch, cs); dzero(e->stouch, cs, st);
   dalloc(e->stmp, (size_t)cs * kTmpCap);
   dalloc(e->sarena, (size_t)cs * kArenaWords);
-  dalloc(e->sR0, cs ? R : 0);
-  dalloc(e->sR1, cs ? R : 0);
+  dalloc(e->sR0, cs ? Rs : 0);
+  dalloc(e->sR1, cs ? Rs : 0);
   dalloc(e->s_bt, cs); dzero(e->s_bt, cs, st);
   dalloc(e->s_pos, (size_t)cs + 1);
   dalloc(e->s_tl, cs);
@@ -310,22 +318,29 @@ void create_impl(vn_engine* e) {
                               hipMemcpyHostToDevice, st));
   halloc(e->hf_cnt, 16);
 
-  radix_scratch_reserve(e->rs, std::max<uint64_t>(e->h_sort_cap, (cs || cc || cg) ? R : 0));
-  radix_scratch_reserve(e->rs2, (cs || cc || cg) ? R : 1);
+  const uint64_t Rside = std::max(cs ? Rs : 0, (cc || cg) ? Rcg : 0);
+  radix_scratch_reserve(e->rs, std::max<uint64_t>(e->h_sort_cap, Rside));
+  radix_scratch_reserve(e->rs2, std::max<uint64_t>(Rside, 1));
   radix_scratch_reserve(e->rs3, std::max<uint64_t>(touch_max, 1));
   init_state(e);
   VN_HIP_CHECK(hipStreamSynchronize(st));
+}
+
+// a batch with more records of some class than that class's cap
+static bool over_class_caps(const vn_engine* e, const vn_batch* b) {
+  return b->n_counter > e->max_cls[VN_COUNTER] || b->n_gauge > e->max_cls[VN_GAUGE] ||
+         b->n_histo > e->max_cls[VN_HISTO] || b->n_set > e->max_cls[VN_SET];
 }
 
 // device staging for host-provided batches (vn_ingest_host / vn_submit / imports)
 void ensure_device_stage(vn_engine* e) {
   DeviceBatch& d = e->dstage;
   if (d.c_slot) return;
-  const uint64_t R = e->max_records;
-  dalloc(d.c_slot, R); dalloc(d.c_val, R); dalloc(d.c_rate, R);
-  dalloc(d.g_slot, R); dalloc(d.g_val, R);
-  dalloc(d.h_slot, R); dalloc(d.h_val, R); dalloc(d.h_rate, R);
-  dalloc(d.s_slot, R); dalloc(d.s_off, R + 1); dalloc(d.s_bytes, e->max_member_bytes);
+  const uint64_t* R = e->max_cls;
+  dalloc(d.c_slot, R[VN_COUNTER]); dalloc(d.c_val, R[VN_COUNTER]); dalloc(d.c_rate, R[VN_COUNTER]);
+  dalloc(d.g_slot, R[VN_GAUGE]); dalloc(d.g_val, R[VN_GAUGE]);
+  dalloc(d.h_slot, R[VN_HISTO]); dalloc(d.h_val, R[VN_HISTO]); dalloc(d.h_rate, R[VN_HISTO]);
+  dalloc(d.s_slot, R[VN_SET]); dalloc(d.s_off, R[VN_SET] + 1); dalloc(d.s_bytes, e->max_member_bytes);
 }
 
 // pinned host staging the Go side appends ProcessMetric records to (vn_stage_acquire)
@@ -360,7 +375,7 @@ void ensure_import(vn_engine* e, uint64_t n, uint64_t nbytes) {
     dalloc(s.in_bytes, s.cap_bytes);
   }
   if (!s.cap_cent) {
-    s.cap_cent = e->max_records;
+    s.cap_cent = e->max_cls[VN_HISTO];  // the drains ingest them as histo records
     dalloc(s.cslot, s.cap_cent);
     dalloc(s.cmean, s.cap_cent);
     dalloc(s.cw, s.cap_cent);
@@ -485,7 +500,7 @@ void destroy_impl(vn_engine* e) {
     (void)hipEventDestroy(e->ev_join6);
     e->ev_join6 = nullptr;
   }
-  for (hipEvent_t* ev : {&e->ev_fork5, &e->ev_join5})
+  for (hipEvent_t* ev : {&e->ev_fork5, &e->ev_join5, &e->ev_rest5})
     if (*ev) {
       (void)hipEventDestroy(*ev);
       *ev = nullptr;
@@ -685,8 +700,7 @@ constexpr bool kSetsFirst = VN_SETS_FIRST;  // side-stream order (compile-time A
 
 void ingest_device(vn_engine* e, const vn_batch* b) {
   histo_imports_drain(e);  // imports that came first merge first
-  if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
-      b->n_set > e->max_records)
+  if (over_class_caps(e, b))
     throw std::invalid_argument("batch larger than max_batch_records");
   if ((b->n_counter && !e->cap[VN_COUNTER]) || (b->n_gauge && !e->cap[VN_GAUGE]) ||
       (b->n_histo && !e->cap[VN_HISTO]) || (b->n_set && !e->cap[VN_SET]))
@@ -756,8 +770,7 @@ void ingest_device(vn_engine* e, const vn_batch* b) {
 
 void ingest_host(vn_engine* e, const vn_batch* b) {
   histo_imports_drain(e);
-  if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
-      b->n_set > e->max_records)
+  if (over_class_caps(e, b))
     throw std::invalid_argument("batch larger than max_batch_records");
   check_slots_host(b->counter_slot, b->n_counter, e->cap[VN_COUNTER], "counter");
   check_slots_host(b->gauge_slot, b->n_gauge, e->cap[VN_GAUGE], "gauge");
@@ -909,6 +922,13 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
     delete e;
     return VN_EINVAL;
   }
+  for (int c = 0; c < VN_NCLASS; c++) {
+    e->max_cls[c] = cfg->max_batch_class_records[c] ? cfg->max_batch_class_records[c] : e->max_records;
+    if (e->max_cls[c] > e->max_records) {  // a class cap narrows max_batch_records, never widens it
+      delete e;
+      return VN_EINVAL;
+    }
+  }
   e->max_member_bytes = cfg->max_batch_member_bytes ? cfg->max_batch_member_bytes : e->max_records * 16;
   if (e->max_member_bytes < e->max_records * 8) e->max_member_bytes = e->max_records * 8;
   int rc = guarded(e, [&] { create_impl(e); });
@@ -967,8 +987,7 @@ int vn_ingest_host(vn_engine* e, const vn_batch* b) {
 int vn_ingest(vn_engine* e, const vn_batch* b) {
   if (!e || !b) return VN_EINVAL;
   return guarded(e, [&] {
-    if (b->n_counter > e->max_records || b->n_gauge > e->max_records || b->n_histo > e->max_records ||
-        b->n_set > e->max_records)
+    if (over_class_caps(e, b))
       throw std::invalid_argument("batch larger than max_batch_records");
     validate_device_batch(e, b);
     window_open(e, e->st);
@@ -979,7 +998,7 @@ int vn_ingest(vn_engine* e, const vn_batch* b) {
 int vn_import_counters(vn_engine* e, const uint32_t* slot, const int64_t* value, uint64_t n) {
   if (!e) return VN_EINVAL;
   return guarded(e, [&] {
-    if (n > e->max_records) throw std::invalid_argument("import batch too large");
+    if (n > e->max_cls[VN_COUNTER]) throw std::invalid_argument("import batch too large");
     check_slots_host(slot, n, e->cap[VN_COUNTER], "counter");
     ensure_device_stage(e);
     h2d(e->dstage.c_slot, slot, n, e->st);
@@ -994,7 +1013,7 @@ int vn_import_counters(vn_engine* e, const uint32_t* slot, const int64_t* value,
 int vn_import_gauges(vn_engine* e, const uint32_t* slot, const double* value, uint64_t n) {
   if (!e) return VN_EINVAL;
   return guarded(e, [&] {
-    if (n > e->max_records) throw std::invalid_argument("import batch too large");
+    if (n > e->max_cls[VN_GAUGE]) throw std::invalid_argument("import batch too large");
     check_slots_host(slot, n, e->cap[VN_GAUGE], "gauge");
     ensure_device_stage(e);
     h2d(e->dstage.g_slot, slot, n, e->st);
@@ -1025,7 +1044,8 @@ __global__ void k_check_payloads(uint64_t n, const uint32_t* __restrict__ slot, 
   if (slot[i] >= cap || off[i + 1] < off[i]) atomicOr(err, kErrDecode);
 }
 void import_device(vn_engine* e, int cls, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n) {
-  if (n > e->max_records) throw std::invalid_argument("import batch larger than max_batch_records");
+  if (n > e->max_records || (cls == VN_SET && n > e->max_cls[VN_SET]))
+    throw std::invalid_argument("import batch larger than max_batch_records");
   ensure_import(e, n, 0);
   if (cls == VN_HISTO) {
     import_histos(e, n, slot, off, bytes);  // (its count pass validates slots and offsets)
@@ -1055,6 +1075,7 @@ int vn_import_sets(vn_engine* e, const uint32_t* slot, const uint64_t* off, cons
   if (!e || (n && (!slot || !off || !bytes))) return VN_EINVAL;
   return guarded(e, [&] {
     if (!n) return;
+    if (n > e->max_cls[VN_SET]) throw std::invalid_argument("import batch larger than the set class's record cap");
     stage_import(e, slot, off, bytes, n, e->cap[VN_SET]);
     import_sets(e, n, e->imp.in_slot, e->imp.in_off, e->imp.in_bytes);
     VN_HIP_CHECK(hipGetLastError());

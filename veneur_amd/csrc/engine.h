@@ -126,7 +126,7 @@ struct vn_engine {
   hipEvent_t ev_join4 = nullptr;
   // long-key replay stream (CU mask of st3): the longest keys' four-wave replays
   hipStream_t st5 = nullptr;
-  hipEvent_t ev_fork5 = nullptr, ev_join5 = nullptr;
+  hipEvent_t ev_fork5 = nullptr, ev_join5 = nullptr, ev_rest5 = nullptr;
   // the few longest batched replays on CUs no other stream uses (null: st5 takes them all)
   uint32_t ev_rec = 0;           // timing: which of ev[0..4] this window recorded
   hipStream_t st6 = nullptr;     // the reserved CUs (vn_config.replay_reserved_cus), or none
@@ -153,6 +153,7 @@ struct vn_engine {
   uint32_t cap_cent = 256;      // centroids per histo slot (>= 2*compression + 4)
   int slot_bits[VN_NCLASS] = {1, 1, 1, 1};
   uint64_t max_records = 0, max_member_bytes = 0;
+  uint64_t max_cls[VN_NCLASS] = {};  // per class: vn_config.max_batch_class_records (0 -> max_records)
 
   // ---- counters
   int64_t* cval = nullptr;

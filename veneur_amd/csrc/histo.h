@@ -86,6 +86,10 @@ size_t exact_fast_smem_bytes(uint32_t capc, uint32_t tcap);  // the long replays
 void launch_histo_exact(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks);
 // the pure-chunk pre-sort alone, and the replay alone (over x.order when set)
 void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks);
+// histo_exact_presort in parts: the chunk counts and owners, then the sorts -- the first `top`
+// keys of x.order64 alone (top_only), or every other chunk (top keys skipped)
+void histo_exact_chunk_plan(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks);
+void histo_exact_chunk_sort(const ExactCtx& x, hipStream_t st, uint64_t max_chunks, uint32_t top, bool top_only);
 void histo_exact_replay(const ExactCtx& x, hipStream_t st);
 // The longest keys of x.order64 (>= min_len samples to replay, at most 4096) replay with four
 // waves each: histo_exact_count_long counts them into count[0] (and those of at least
@@ -94,7 +98,13 @@ void histo_exact_replay(const ExactCtx& x, hipStream_t st);
 bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipStream_t st);
 // the batched kernel (the longest keys) on st, the rest of the long keys on st_rest
 // st_top (or null): the kTopExcl longest batched keys there, the other batched ones on st
-void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest, hipStream_t st_top = nullptr);
+void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest, hipStream_t st_top = nullptr,
+                             uint32_t top_done = 0);
+// The longest keys first: the number of leading keys of the order (x.order64, after
+// histo_exact_count_long) whose batched replays histo_exact_replay_top launches on their own
+// stream (0: none); histo_exact_replay_long then skips them (top_done).
+uint32_t histo_exact_top_keys(const ExactCtx& x);
+void histo_exact_replay_top(const ExactCtx& x, hipStream_t st_top, uint32_t top);
 // the replay over x.keys[0, *dev_count) (count known on the device only; <= max_keys)
 void histo_exact_replay_list(const ExactCtx& x, const uint32_t* dev_count, uint32_t max_keys, hipStream_t st);
 // replay list[0..n) longest first: sorts the order into buf0/buf1 (n each) on st and sets x

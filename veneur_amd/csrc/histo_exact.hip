@@ -895,24 +895,22 @@ __global__ void k_exact_chunk_count(ExactCtx x) {
   x.ccnt[k] = exact_split(x.hpend[x.keys[k]], nex, x.tcap).npure;
 }
 
-// owner key of every pure chunk, so a sorting wave starts without a dependent binary search
+// owner key of every pure chunk, so a sorting wave starts without a dependent binary search:
+// one thread per chunk (a thread per key would write a 17M-sample key's 400k chunks alone)
 __global__ void k_exact_chunk_owner(ExactCtx x) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= x.nkeys) return;
-  const uint32_t a = x.coff[k], b = x.coff[k + 1];
-  for (uint32_t g = a; g < b; g++) x.cown[g] = k;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= x.coff[x.nkeys]) return;
+  x.cown[g] = last_le_u32(x.coff, x.nkeys, g);
 }
 
-__global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const uint32_t g = blockIdx.x, lane = threadIdx.x;
-  if (g >= x.coff[x.nkeys]) return;
+// sort pure chunk g of key k (one wave)
+__device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t g, const uint32_t k, char* smem) {
+  const uint32_t lane = threadIdx.x;
   const uint32_t tcap = x.tcap, TP = round64(tcap + 1);
   ldsf64* tv = (ldsf64*)smem;
   ldsf64* tw = tv + TP;
   ldsf64* sv = tw + TP;
   ldsf64* sw = sv + TP;
-  const uint32_t k = x.cown ? x.cown[g] : last_le_u32(x.coff, x.nkeys, g);
   const uint32_t s = x.keys[k];
   const ExactSplit sp = exact_split(x.hpend[s], x.nex[k], tcap);
   const uint64_t base = (uint64_t)x.start[s] + sp.off0 + (uint64_t)(g - x.coff[k]) * tcap;
@@ -958,6 +956,35 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x) {
     x.ctw[base] = tex ? tempW : -tempW;
     // (every weight is at least 1, so tempW < 2^16 bounds each weight and prefix below 2^16 too)
     if (x.cpk) x.cpk[base] = tint && tempW < 65536.0 ? (uint32_t)tempW << 16 | (uint32_t)__builtin_fabs(sw[0]) : 0xffffffffu;
+  }
+}
+
+// the first `top` keys of the longest-first order (x.order64): their chunks are sorted first, so
+// their replays (the window's longest chains) start before the other keys' chunks are sorted
+__device__ __forceinline__ bool is_top_key(const ExactCtx& x, uint32_t k, uint32_t top) {
+  bool t = false;
+  for (uint32_t y = 0; y < top; y++) t |= (uint32_t)x.order64[y] == k;
+  return t;
+}
+
+// every pure chunk (one wave each), skipping the first `top` keys of x.order64 (sorted already)
+__global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x, uint32_t top) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t g = blockIdx.x;
+  if (g >= x.coff[x.nkeys]) return;
+  const uint32_t k = x.cown ? x.cown[g] : last_le_u32(x.coff, x.nkeys, g);
+  if (top && is_top_key(x, k, top)) return;
+  chunk_sort_one(x, g, k, smem);
+}
+
+// the chunks of the first `top` keys of x.order64: block (b, y) takes key y's chunks b, b + G, ...
+__global__ __launch_bounds__(64) void k_exact_chunk_sort_top(ExactCtx x) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t k = (uint32_t)x.order64[blockIdx.y];
+  const uint32_t a = x.coff[k], b = x.coff[k + 1];
+  for (uint32_t g = a + blockIdx.x; g < b; g += gridDim.x) {
+    chunk_sort_one(x, g, k, smem);
+    wave_lds_sync();  // (the next chunk reuses the LDS tiles)
   }
 }
 
@@ -1742,6 +1769,7 @@ static_assert(kBB <= 64, "list entries and the flagged-column scan hold a chunk 
 #endif
 constexpr uint32_t kRing = VN_BATCH_RING;  // chunk slots in LDS
 constexpr uint32_t kTopExcl = 8;             // longest batched keys on CUs no other stream uses (st6)
+constexpr uint32_t kTopSortBlocks = 4096;    // blocks per top key sorting its chunks first (grid-stride)
 constexpr uint32_t kBM = 160;               // most centroids a batch takes (delta 100: ~135)
 constexpr uint32_t kBN = kBM + 1;           // columns + the end
 constexpr uint32_t kBTmax = 48;             // largest temp buffer batched (delta <= ~110)
@@ -3010,16 +3038,34 @@ extern "C" int vn_prof_exact_read(unsigned long long* out16, int reset) {
 }
 #endif
 
-void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks) {
+void histo_exact_chunk_plan(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks) {
   if (!x.nkeys || !x.nex) return;
-  // sort every pure chunk in parallel first
   hipLaunchKernelGGL(k_exact_chunk_count, dim3(blocks_for(x.nkeys, 256)), dim3(256), 0, st, x);
   scan_exclusive_u32(x.ccnt, x.coff, x.nkeys, *ss, st);
   if (x.cown && max_chunks)
-    hipLaunchKernelGGL(k_exact_chunk_owner, dim3(blocks_for(x.nkeys, 256)), dim3(256), 0, st, x);
-  if (max_chunks)
-    hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)max_chunks), dim3(64),
-                       sizeof(double) * 4 * ((x.tcap + 1 + 63u) & ~63u), st, x);
+    hipLaunchKernelGGL(k_exact_chunk_owner, dim3(blocks_for(max_chunks, 256)), dim3(256), 0, st, x);
+}
+
+void histo_exact_chunk_sort(const ExactCtx& x, hipStream_t st, uint64_t max_chunks, uint32_t top, bool top_only) {
+  if (!x.nkeys || !x.nex || !max_chunks) return;
+  const size_t sm = sizeof(double) * 4 * ((x.tcap + 1 + 63u) & ~63u);
+  if (top && (!x.order64 || top > x.norder || top > kTopExcl)) throw std::logic_error("chunk sort: bad top keys");
+  if (top_only) {
+    if (top) hipLaunchKernelGGL(k_exact_chunk_sort_top, dim3(kTopSortBlocks, top), dim3(64), sm, st, x);
+    return;
+  }
+  hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)max_chunks), dim3(64), sm, st, x, top);
+}
+
+uint32_t histo_exact_top_keys(const ExactCtx& x) {
+  const bool batch = x.cpk && x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024;
+  return x.mw_count && batch ? std::min<uint32_t>(kTopExcl, x.norder) : 0u;
+}
+
+void histo_exact_presort(const ExactCtx& x, hipStream_t st, ScanScratch* ss, uint64_t max_chunks) {
+  // sort every pure chunk in parallel first
+  histo_exact_chunk_plan(x, st, ss, max_chunks);
+  histo_exact_chunk_sort(x, st, max_chunks, 0, false);
 }
 
 bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipStream_t st) {
@@ -3034,14 +3080,22 @@ bool histo_exact_count_long(ExactCtx& x, uint32_t min_len, uint32_t* count, hipS
   return true;
 }
 
-void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest, hipStream_t st_top) {
+void histo_exact_replay_top(const ExactCtx& x, hipStream_t st_top, uint32_t top) {
+  if (!top) return;
+  const size_t sm = exact_batch_smem_bytes(x.capc, x.tcap);
+  if (x.lstat) hipLaunchKernelGGL(k_exact_long_stats, dim3(kLongStatSlices, top), dim3(256), 0, st_top, x, 0u, top);
+  hipLaunchKernelGGL(k_histo_exact_mwb, dim3(top), dim3(kMWThreads), sm, st_top, x, x.mw_count, 0u, top);
+}
+
+void histo_exact_replay_long(const ExactCtx& x, hipStream_t st, hipStream_t st_rest, hipStream_t st_top,
+                             uint32_t top_done) {
   if (!x.mw_count) return;
   const uint32_t grid = std::min<uint32_t>(x.norder, kMaxLongKeys / 2);
   if (x.cpk && x.tcap <= kBTmax && exact_batch_smem_bytes(x.capc, x.tcap) <= 160 * 1024) {
     const size_t sm = exact_batch_smem_bytes(x.capc, x.tcap);
-    const uint32_t top = st_top ? std::min<uint32_t>(kTopExcl, x.norder) : 0u;
+    const uint32_t top = top_done ? top_done : st_top ? std::min<uint32_t>(kTopExcl, x.norder) : 0u;
     const uint32_t nl = std::min<uint32_t>(x.norder, kLongStatKeys);
-    if (top) {
+    if (top && !top_done) {
       if (x.lstat)
         hipLaunchKernelGGL(k_exact_long_stats, dim3(kLongStatSlices, top), dim3(256), 0, st_top, x, 0u, top);
       hipLaunchKernelGGL(k_histo_exact_mwb, dim3(top), dim3(kMWThreads), sm, st_top, x, x.mw_count, 0u, top);

@@ -1309,7 +1309,12 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.ctw = e->h_tw;
   xc.cpk = e->h_cpk;
   xc.lstat = e->h_lstat;
-  histo_exact_presort(xc, st, &e->ss, n / e->temp_cap + 1);
+  const uint64_t max_chunks = n / e->temp_cap + 1;
+  // (exact mode, no hot key, not timing: the longest keys' chunks are sorted first and their
+  // replays start while the other chunks sort, in replay_cold)
+  const bool early = !nhot && !e->timing && e->st5 && e->st6;
+  histo_exact_chunk_plan(xc, st, &e->ss, max_chunks);
+  if (!early) histo_exact_chunk_sort(xc, st, max_chunks, 0, false);
   // The hot keys' prefixes run on st4 (short) while st gathers and sorts the remainders; the
   // cold and warm keys (long) on st3 after the sort, whose passes would otherwise wait for CUs
   // behind 100k+ replay workgroups -- then the held-back set merge on the side stream.  With
@@ -1334,19 +1339,43 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
     const bool side5 = longk && !e->timing && e->st5;
     hipEvent_t a = e->timing ? e->pool_rp.next() : nullptr, b = e->timing ? e->pool_rp.next() : nullptr;
     if (a && b) VN_HIP_CHECK(hipEventRecord(a, s));
-    if (side5) {  // the batched longest keys on st5, the other long keys ahead of the rest on s
+    if (early) {
+      // the window's longest chains first: the top keys' chunks, their replays on st6, then
+      // every other chunk while they run, then the other long keys (st5, s) and the rest (s)
+      const uint32_t top = side5 ? histo_exact_top_keys(xc) : 0u;
+      if (top) {
+        histo_exact_chunk_sort(xc, s, max_chunks, top, true);
+        VN_HIP_CHECK(hipEventRecord(e->ev_fork5, s));
+        VN_HIP_CHECK(hipStreamWaitEvent(e->st6, e->ev_fork5, 0));
+        histo_exact_replay_top(xc, e->st6, top);
+        VN_HIP_CHECK(hipEventRecord(e->ev_join6, e->st6));
+      }
+      histo_exact_chunk_sort(xc, s, max_chunks, top, false);
+      if (side5) {
+        VN_HIP_CHECK(hipEventRecord(e->ev_rest5, s));
+        VN_HIP_CHECK(hipStreamWaitEvent(e->st5, e->ev_rest5, 0));
+        histo_exact_replay_long(xc, e->st5, s, top ? e->st6 : nullptr, top);
+        VN_HIP_CHECK(hipEventRecord(e->ev_join5, e->st5));
+      } else if (longk) {
+        histo_exact_replay_long(xc, s, s);
+      }
+      histo_exact_replay(xc, s);
+      if (side5) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join5, 0));
+      if (top) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join6, 0));
+    } else if (side5) {  // the batched longest keys on st5, the other long keys ahead of the rest on s
       VN_HIP_CHECK(hipEventRecord(e->ev_fork5, s));
       VN_HIP_CHECK(hipStreamWaitEvent(e->st5, e->ev_fork5, 0));
       if (e->st6) VN_HIP_CHECK(hipStreamWaitEvent(e->st6, e->ev_fork5, 0));
       histo_exact_replay_long(xc, e->st5, s, e->st6);
       VN_HIP_CHECK(hipEventRecord(e->ev_join5, e->st5));
       if (e->st6) VN_HIP_CHECK(hipEventRecord(e->ev_join6, e->st6));
-    } else if (longk) {
-      histo_exact_replay_long(xc, s, s);
+      histo_exact_replay(xc, s);
+      VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join5, 0));
+      if (e->st6) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join6, 0));
+    } else {
+      if (longk) histo_exact_replay_long(xc, s, s);
+      histo_exact_replay(xc, s);
     }
-    histo_exact_replay(xc, s);
-    if (side5) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join5, 0));
-    if (side5 && e->st6) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join6, 0));
     if (a && b) VN_HIP_CHECK(hipEventRecord(b, s));
     if (e->timing) e->kstat_rp.launches++;
     xc.mw_count = nullptr;

@@ -449,7 +449,7 @@ void make_batch(vn_intake* in, uint64_t n) {
 extern "C" {
 
 int vn_intake_create(vn_engine* eng, uint64_t max_bytes, uint64_t max_lines, vn_intake** out) {
-  if (!eng || !out || !max_bytes || !max_lines || max_bytes >= (1ull << 32) || max_lines > eng->max_records)
+  if (!eng || !out || !max_bytes || !max_lines || max_bytes >= (1ull << 32) || max_lines > *std::min_element(eng->max_cls, eng->max_cls + VN_NCLASS))
     return VN_EINVAL;
   *out = nullptr;
   vn_intake* in = new vn_intake;

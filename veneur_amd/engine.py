@@ -53,7 +53,9 @@ def _arr(ptr, n, dt, shape=None):
 class Engine:
     def __init__(self, capacity, compression=100.0, percentiles=(0.5, 0.9, 0.99, 0.999), max_batch_records=1 << 20,
                  max_batch_member_bytes=0, device=0, exact_threshold=0, hot_prefix=0, piece_growth=0,
-                 split_max_records=0, split_compression=0.0, replay_reserved_cus=0):
+                 split_max_records=0, split_compression=0.0, replay_reserved_cus=0, max_class_records=None):
+        """max_class_records: (counter, gauge, histo, set) record caps of one ingest call, each <=
+        max_batch_records (0 or None: max_batch_records); they size each class's buffers."""
         cfg = A.Config()
         cfg.replay_reserved_cus = int(replay_reserved_cus)
         cfg.split_max_records = int(split_max_records)
@@ -70,11 +72,14 @@ class Engine:
             cfg.percentiles[i] = float(p)
         cfg.max_batch_records = int(max_batch_records)
         cfg.max_batch_member_bytes = int(max_batch_member_bytes)
+        for i, c in enumerate(max_class_records or ()):
+            cfg.max_batch_class_records[i] = int(c)
         self.percentiles = tuple(float(p) for p in percentiles)
         self.capacity = tuple(int(c) for c in capacity)
         self.device = device
         # the engine's effective limits (capi.hip vn_engine_create)
         self.max_batch_records = int(max_batch_records) or (1 << 20)
+        self.max_class_records = tuple(int(c) or self.max_batch_records for c in (max_class_records or (0,) * 4))
         self.max_batch_member_bytes = max(int(max_batch_member_bytes) or self.max_batch_records * 16,
                                           self.max_batch_records * 8)
         h = C.c_void_p()

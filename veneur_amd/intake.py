@@ -168,7 +168,7 @@ class Intake:
     def __init__(self, engine, max_bytes=1 << 24, max_lines=None):
         self.engine = engine
         self.max_bytes = int(max_bytes)
-        self.max_lines = int(max_lines or min(engine.max_batch_records, max(1, self.max_bytes // 4)))
+        self.max_lines = int(max_lines or min(min(engine.max_class_records), max(1, self.max_bytes // 4)))
         self.h = C.c_void_p()
         rc = A.lib.vn_intake_create(engine.h, self.max_bytes, self.max_lines, C.byref(self.h))
         if rc != 0:
