@@ -148,7 +148,10 @@ void create_impl(vn_engine* e) {
       VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join6, hipEventDisableTiming));
       e->reserved_cus = r;
     }
-    if (!e->st6) {  // the longest batched replays' stream: they start once their own chunks are sorted
+    // A/B knob (VN_EARLY_TOP=1): the longest batched replays on a stream of their own, started
+    // once their own chunks are sorted (ingest_histo.hip).  Measured on C4 with three engines in
+    // turn: 99.4 ms per window against 86.0 (one more stream per engine), not kept
+    if (!e->st6 && getenv("VN_EARLY_TOP")) {
       if (e->side_cus != ncu) VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st6, (uint32_t)rmask.size(), rmask.data()));
       else VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st6, hipStreamNonBlocking, prio_hi));
       VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join6, hipEventDisableTiming));
