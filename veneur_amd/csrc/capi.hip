@@ -151,7 +151,8 @@ void create_impl(vn_engine* e) {
     // A/B knob (VN_EARLY_TOP=1): the longest batched replays on a stream of their own, started
     // once their own chunks are sorted (ingest_histo.hip).  Measured on C4 with three engines in
     // turn: 99.4 ms per window against 86.0 (one more stream per engine), not kept
-    if (!e->st6 && getenv("VN_EARLY_TOP")) {
+    e->early_top = getenv("VN_EARLY_TOP") != nullptr;
+    if (!e->st6 && e->early_top) {
       if (e->side_cus != ncu) VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st6, (uint32_t)rmask.size(), rmask.data()));
       else VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st6, hipStreamNonBlocking, prio_hi));
       VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join6, hipEventDisableTiming));

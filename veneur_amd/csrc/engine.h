@@ -153,7 +153,8 @@ struct vn_engine {
   uint32_t cap_cent = 256;      // centroids per histo slot (>= 2*compression + 4)
   int slot_bits[VN_NCLASS] = {1, 1, 1, 1};
   uint64_t max_records = 0, max_member_bytes = 0;
-  uint64_t max_cls[VN_NCLASS] = {};  // per class: vn_config.max_batch_class_records (0 -> max_records)
+  uint64_t max_cls[VN_NCLASS] = {};
+  bool early_top = false;  // VN_EARLY_TOP A/B knob (capi.hip)  // per class: vn_config.max_batch_class_records (0 -> max_records)
 
   // ---- counters
   int64_t* cval = nullptr;

@@ -1312,7 +1312,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   const uint64_t max_chunks = n / e->temp_cap + 1;
   // (exact mode, no hot key, not timing: the longest keys' chunks are sorted first and their
   // replays start while the other chunks sort, in replay_cold)
-  const bool early = !nhot && !e->timing && e->st5 && e->st6;
+  const bool early = e->early_top && !nhot && !e->timing && e->st5 && e->st6;
   histo_exact_chunk_plan(xc, st, &e->ss, max_chunks);
   if (!early) histo_exact_chunk_sort(xc, st, max_chunks, 0, false);
   // The hot keys' prefixes run on st4 (short) while st gathers and sorts the remainders; the
