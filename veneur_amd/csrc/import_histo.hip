@@ -65,6 +65,36 @@ struct GobIn {
     const uint64_t m = 0ull - (uint64_t)((a >> 3) & 1u), h = (c0 & ~m) | (c1 & m);
     return (uint32_t)(h >> ((a & 7u) * 8u)) & 0xffu;
   }
+#ifdef VN_GOB_WINDOW
+  // 8 bytes from byte o (< 24) of the held blocks c0:c1 (this one) and n0:n1 (the next), by
+  // mask blends (no register indexing: it would put the reader in scratch)
+  __device__ __forceinline__ uint64_t win64(uint32_t o) const {
+    const uint32_t w = o >> 3, s = (o & 7u) * 8u;
+    const uint64_t m0 = 0ull - (uint64_t)(w == 0), m1 = 0ull - (uint64_t)(w == 1), m2 = 0ull - (uint64_t)(w == 2);
+    const uint64_t lo_w = (c0 & m0) | (c1 & m1) | (n0 & m2) | (n1 & ~(m0 | m1 | m2));
+    const uint64_t hi_w = (c1 & m0) | (n0 & m1) | (n1 & m2);
+    return s ? (lo_w >> s) | (hi_w << (64u - s)) : lo_w;
+  }
+  __device__ __forceinline__ uint64_t u() {  // gob unsigned integer
+    if (i >= n) {
+      err = true;
+      return 0;
+    }
+    const uint32_t b = at(i);  // (also moves the held blocks to byte i)
+    i++;
+    if (b < 0x80u) return b;
+    const uint32_t cnt = 256u - b;  // byte count, sent negated
+    if (cnt > 8u || cnt > n - i) {
+      err = true;
+      return 0;
+    }
+    // the cnt big-endian bytes after the count byte, read at once: they lie within the held
+    // blocks (byte offset <= 16 + 8 of the current block's start)
+    const uint64_t y = win64(((lo + i - 1) & 15u) + 1u);
+    i += cnt;
+    return __builtin_bswap64(y) >> (64u - 8u * cnt);
+  }
+#else
   __device__ __forceinline__ uint64_t u() {  // gob unsigned integer
     if (i >= n) {
       err = true;
@@ -81,6 +111,7 @@ struct GobIn {
     for (uint32_t k = 0; k < cnt; k++) v = (v << 8) | at(i++);
     return v;
   }
+#endif
   __device__ __forceinline__ int64_t s() {  // gob signed integer: sign in bit 0
     const uint64_t x = u();
     return (x & 1) ? ~(int64_t)(x >> 1) : (int64_t)(x >> 1);
