@@ -65,7 +65,6 @@ struct GobIn {
     const uint64_t m = 0ull - (uint64_t)((a >> 3) & 1u), h = (c0 & ~m) | (c1 & m);
     return (uint32_t)(h >> ((a & 7u) * 8u)) & 0xffu;
   }
-#ifdef VN_GOB_WINDOW
   // 8 bytes from byte o (< 24) of the held blocks c0:c1 (this one) and n0:n1 (the next), by
   // mask blends (no register indexing: it would put the reader in scratch)
   __device__ __forceinline__ uint64_t win64(uint32_t o) const {
@@ -94,24 +93,6 @@ struct GobIn {
     i += cnt;
     return __builtin_bswap64(y) >> (64u - 8u * cnt);
   }
-#else
-  __device__ __forceinline__ uint64_t u() {  // gob unsigned integer
-    if (i >= n) {
-      err = true;
-      return 0;
-    }
-    const uint32_t b = at(i++);
-    if (b < 0x80u) return b;
-    const uint32_t cnt = 256u - b;  // byte count, sent negated
-    if (cnt > 8u || cnt > n - i) {
-      err = true;
-      return 0;
-    }
-    uint64_t v = 0;
-    for (uint32_t k = 0; k < cnt; k++) v = (v << 8) | at(i++);
-    return v;
-  }
-#endif
   __device__ __forceinline__ int64_t s() {  // gob signed integer: sign in bit 0
     const uint64_t x = u();
     return (x & 1) ? ~(int64_t)(x >> 1) : (int64_t)(x >> 1);
