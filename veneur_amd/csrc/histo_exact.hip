@@ -55,7 +55,16 @@ __device__ __forceinline__ long long prof_stamp() {  // a scheduling fence aroun
   __builtin_amdgcn_sched_barrier(0);
   return (long long)t;
 }
+#ifdef VN_PROF_NOSTAMP  // (diagnosing the profiling build: counters without the clock stamps)
+#define PROF_T(v) const long long v = 0
+#else
 #define PROF_T(v) const long long v = prof_stamp()
+#endif
+#ifdef VN_PROF_NOATOMIC  // (... or the stamps without the counters' atomics)
+#define PROF_ADD(i, a, b) (void)((b) - (a))
+#define PROF_ADDW(i, a, b) (void)((b) - (a))
+#define PROF_CNT(i, pred)
+#else
 #define PROF_ADD(i, a, b) \
   if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_exact_prof[i], (unsigned long long)((b) - (a)))
 // per wave (lane 0 of each wave of block 0): slot i + wave
@@ -67,6 +76,7 @@ __device__ __forceinline__ long long prof_stamp() {  // a scheduling fence aroun
     const uint64_t _m = __ballot(pred);                                                                \
     if (blockIdx.x == 0 && (threadIdx.x & 63) == 0) atomicAdd(&g_exact_prof[i], (unsigned long long)__popcll(_m)); \
   }
+#endif
 #else
 #define PROF_CNT(i, pred)
 #define PROF_ADDW(i, a, b)
