@@ -2202,53 +2202,6 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       }
     }
   };
-#ifdef VN_C2_LANE
-  // C2 one lane per column: the same integers and operations per chunk, walked in chunk order by
-  // the column's lane (no row scans or row reductions); 64 columns per queue entry
-  auto c2_cols = [&](uint32_t g0) {
-    ASM_MARK("C2_COLS");
-    const uint32_t ci = g0 + lane;
-    if (ci < nm) {
-      const double mp0 = F.mp[ci], mpw = dadd(mp0, L.mw[ci]);
-      const ldsu32* ra = (const ldsu32*)(B.nT + ci * kRS);
-      const ldsu32* re = (const ldsu32*)(B.nT + (ci + 1) * kRS);
-      uint32_t C = 0, X = 0;
-      double qemin = 2.0, qbmin = 2.0, qbmax = -1.0;
-      for (uint32_t q = 0; 4 * q < b; q++) {
-        const uint32_t wa = ra[q], we = re[q];
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
-          const uint32_t j = 4 * q + u;
-          if (j < b) {
-            const uint32_t x = tw_of(j, (wa >> (8 * u)) & 0xffu), y = tw_of(j, (we >> (8 * u)) & 0xffu);
-            const double rT = B.brT[j];
-            C += x;
-            const double qe = dadd(mpw, (double)(X + x)) * rT;
-            const double qb = dadd(mp0, (double)C) * rT;
-            X += y;
-            qemin = __builtin_fmin(qemin, qe);
-            qbmin = __builtin_fmin(qbmin, qb);
-            qbmax = __builtin_fmax(qbmax, qb);
-          }
-        }
-      }
-      B.kb[ci] = qemin;
-      B.kb[kBN + ci] = ci ? qbmax : 0.0;
-      B.kb[2 * kBN + ci] = ci ? qbmin : 0.0;
-    }
-  };
-  auto c2_queue = [&]() {
-    uint32_t g = 0;
-    if (lane == 0) g = lds_inc(&B.ctl[5]);
-    g = 64u * __builtin_amdgcn_readfirstlane(g);
-    while (g < nm) {
-      uint32_t gn = 0;
-      if (lane == 0) gn = lds_inc(&B.ctl[5]);
-      c2_cols(g);
-      g = 64u * __builtin_amdgcn_readfirstlane(gn);
-    }
-  };
-#else
   // column groups taken from a queue by whichever wave is free (after its Welford lists); the
   // next entry is drawn before this one is worked
   auto c2_queue = [&]() {
@@ -2262,7 +2215,6 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       g = kC2Cols * __builtin_amdgcn_readfirstlane(gn);
     }
   };
-#endif
   const uint32_t i = t;
   uint32_t ra[kW], re[kW];
   if (wv < 3) {
