@@ -82,3 +82,11 @@ def test_oracle_processes_synth_stream():
     # counters are integers 1..10 times 1, 2 or 10
     vals = [w.counter_value(int(x)) for x in np.unique(d["c_slot"])]
     assert all(v > 0 for v in vals)
+
+
+def test_graft_build_entry_checks_the_current_abi():
+    """__graft_entry__.build() compares the library's ABI with the binding's, not a fixed number."""
+    import inspect
+    import __graft_entry__ as g
+    src = inspect.getsource(g.build)
+    assert "A.ABI_VERSION" in src
