@@ -2135,7 +2135,10 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   // scan, the min / max a row reduction.  Same integers and operations per chunk as a sequential
   // walk over the chunks, so the same bounds bit for bit
   // (two groups per queue entry, interleaved: their LDS round trips overlap)
-  constexpr uint32_t kC2H = 2, kC2Cols = 4 * kC2H;
+#ifndef VN_C2_GROUPS
+#define VN_C2_GROUPS 2
+#endif
+  constexpr uint32_t kC2H = VN_C2_GROUPS, kC2Cols = 4 * kC2H;
   const uint32_t c2q = lane & 15;
   uint32_t c2base[4];
   double c2rT[4];
