@@ -540,6 +540,11 @@ def main():
     ap.add_argument("--split-delay-ms", type=float, default=0.0, help="development only: host delay after split_close")
     ap.add_argument("--host-trace", action="store_true",
                     help="development only: report host ms in split_keys+ingest_split / ingest / flush")
+    ap.add_argument("--worker-windows", type=int, default=-1,
+                    help="windows of the Worker-level leg (veneur_amd.Worker over the same D engines: Flush "
+                         "hands the window's engine to its flush thread and ingest moves to the next one); "
+                         "-1 (default): --steps, 0: off")
+    ap.add_argument("--c5-only", action="store_true", help="run the C5 leg alone (for its rocprof trace)")
     ap.add_argument("--pcie-steps", type=int, default=1,
                     help="extra steps from host arrays (vn_ingest_host), reported as pcie_inclusive; 0: off")
     args = ap.parse_args()
@@ -551,6 +556,12 @@ def main():
     world, rank, local_rank = env_world()
     sim = args.sim_world > 1 and world == 1
     ctrl = Group(backend="gloo")  # host control plane: barrier, max / sum of scalars, the RCCL id
+    if args.c5_only:
+        c5 = c5_leg(args, rank, world, ctrl, local_rank)
+        if rank == 0:
+            print(json.dumps({"c5": c5}), flush=True)
+        ctrl.close()
+        return
     comm = make_comm(ctrl, local_rank)  # the engines' RCCL group (None at N = 1)
 
     # ---- hot keys: chosen by the engines' own detector (vn_hot_detect / vn_hot_keys) from a
@@ -709,6 +720,41 @@ def main():
               "histo_weight_rel_err": abs(sum(i[2] for i in inv) - sum(i[3] for i in inv)) /
               max(1.0, sum(i[3] for i in inv))}
 
+    # ---- the same windows through the operator interface: veneur_amd.Worker over the same D
+    # engines (Worker.Flush hands the window's engine to its flush thread, as the reference's
+    # Worker.Flush swaps the maps for the flusher, worker.go:276-284 / flusher.go:115-230; ingest
+    # moves to the next engine at once).  One host thread drives it, as one Go worker would.
+    worker_leg = None
+    nw = args.steps if args.worker_windows < 0 else args.worker_windows
+    if nw > 0 and not any(len(sl) for _, sl, _ in split_lists) and not sum(stream.split_counts):
+        from veneur_amd.worker import Worker
+        wk = Worker(engines=engines, percentiles=PCT)
+        for _ in range(D):
+            wk.process_batch(stream.batch)
+            wk.flush_raw()
+        wk.wait()
+        sync()
+        ctrl.barrier()
+        tw = time.perf_counter()
+        for _ in range(nw):
+            wk.process_batch(stream.batch)
+            fut = wk.flush_raw()
+        wk.wait()
+        sync()
+        tw = time.perf_counter() - tw
+        ctrl.barrier()
+        tw = ctrl.max(tw)
+        last = fut.result() if D > 1 else fut
+        wk.close(close_engines=False)
+        worker_leg = {"value": float(args.samples) * nw / tw, "unit": "samples/s", "ms_per_step": tw * 1e3 / nw,
+                      "windows": nw, "engines": D,
+                      "path": "veneur_amd.Worker(engines=D).process_batch(device batch) + flush_raw() per window: "
+                              "Flush hands the window's engine to that engine's flush thread and returns, the "
+                              "next window's ingest goes to the next engine (worker.go:276-284, "
+                              "flusher.go:115-230); one host thread drives the worker",
+                      "vs_harness": (float(args.samples) * nw / tw) / value}
+        log(rank, "[bench] worker leg: %s" % json.dumps(worker_leg))
+
     # per-kernel timing (HIP events on the engine's stream) from extra, untimed steps: with
     # timing on, the phases run one after another so every launch is measured alone
     eng.timing_enable(True)
@@ -744,6 +790,14 @@ def main():
                              "k_part_scatter) + k_counter_runs (LDS sums per slot range, one device add per "
                              "touched slot per 128Ki-record slice)"})
     kern.sort(key=lambda k: -k["ms_per_step"])
+    # the throughput view: each kernel class's algorithmic bytes per window over the window period
+    # (ms_per_step, D windows in flight) -- what the class sustains in the pipelined headline,
+    # against the latency view above (the class's own time in a serialised timing step)
+    thr = [{"kernel": k["kernel"], "algorithmic_bytes_per_window": k["algorithmic_bytes_per_launch"] *
+            k["launches_per_step"], "achieved": k["algorithmic_bytes_per_launch"] * k["launches_per_step"] /
+            (ms_per_step * 1e-3) / 1e9} for k in kern]
+    for t in thr:
+        t["frac"] = t["achieved"] / HBM_PEAK_GBS
     phase = {k: round(mean(k), 4) for k in
              ("ms_ingest_counter", "ms_ingest_gauge", "ms_ingest_histo", "ms_ingest_set", "ms_flush")}
     top = kern[0] if kern else {}
@@ -805,7 +859,13 @@ def main():
                      "traffic_over_algorithmic": traffic_ratio, "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": top.get("algorithmic_bytes_per_launch"),
                      "launches_per_step": top.get("launches_per_step"), "ms_per_step": top.get("ms_per_step"),
+                     "view": "latency: the kernel's algorithmic bytes over its own HIP-event time in a serialised "
+                             "timing step (one engine, every launch measured alone, on the engine's stream)",
                      "kernels": kern},
+        "roofline_throughput": {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "window_ms": ms_per_step,
+                                "view": "throughput: each kernel class's algorithmic bytes per window over the "
+                                        "pipelined window period ms_per_step (%d windows in flight)" % D,
+                                "kernels": thr},
         "path": {"algorithmic_bytes_per_step": path_bytes, "effective_GBs_per_gpu": path_gbs,
                  "frac_of_hbm_peak": path_gbs / HBM_PEAK_GBS, "phase_ms_serialised_rank0": phase},
         "ranks": {"ms_per_step": rank_ms, "records": rank_records,
@@ -813,6 +873,8 @@ def main():
                   "imbalance_ms_max_over_mean": max(rank_ms) / (sum(rank_ms) / len(rank_ms))},
         "checks": checks,
     }
+    if worker_leg is not None:
+        result["worker_rotation"] = worker_leg
 
     # ---- PCIe-inclusive rate, CPU baseline and full-window parity (rank 0, N=1)
     if sim:

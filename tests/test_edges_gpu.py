@@ -164,8 +164,7 @@ def _device_batch(bufs, misalign=False, **cls):
 
 @pytest.mark.parametrize("where", ["mid", "quad_lane3", "tail", "misaligned"])
 @pytest.mark.parametrize("fault", ["counter_slot", "gauge_slot", "histo_slot", "set_slot", "histo_nan",
-                                   "histo_inf", "histo_rate_zero", "counter_rate_big", "counter_rate_nan",
-                                   "set_offsets"])
+                                   "histo_inf", "histo_rate_zero", "histo_rate_nan", "set_offsets"])
 def test_device_batch_validation_rejects_and_leaves_state(fault, where):
     """vn_ingest validates a device-resident batch before applying anything (VN_EINVAL): a fault in
     a 16-byte quad (either lane), in the records past the last full quad, or in arrays that are not
@@ -191,10 +190,8 @@ def test_device_batch_validation_rejects_and_leaves_state(fault, where):
         bad["histos"][1][i] = -np.inf
     elif fault == "histo_rate_zero":
         bad["histos"][2][i] = 0.0
-    elif fault == "counter_rate_big":
-        bad["counters"][2][i] = 1.5
-    elif fault == "counter_rate_nan":
-        bad["counters"][2][i] = np.nan
+    elif fault == "histo_rate_nan":
+        bad["histos"][2][i] = np.nan
     elif fault == "set_offsets":
         bad["sets"][1][i] = bad["sets"][1][i + 1] + 1
     bufs = []
@@ -278,3 +275,30 @@ def test_per_class_record_caps():
     np.testing.assert_array_equal(f.histo_quantiles, oq)
     with pytest.raises(V.EngineError):
         V.Engine(caps, max_batch_records=256, max_class_records=(300, 0, 0, 0))
+
+
+@pytest.mark.parametrize("path", ["host", "device"])
+def test_counter_any_sample_rate_as_go(path):
+    """Counter.Sample (samplers.go:133) is defined for every float32 rate: int64(float32(1/rate))
+    is MinInt64 on amd64 for NaN (which the parser lets through), 0 (+Inf) and rates whose
+    reciprocal passes 2^63, and a plain truncation otherwise (rates above 1 give 0); the product
+    with int64(sample) wraps.  Both ingest paths take such records and equal the oracle."""
+    rng = np.random.default_rng(21)
+    n, cap = 16000, 97
+    slots = rng.integers(0, cap, n).astype(np.uint32)
+    vals = rng.integers(-9, 10, n).astype(np.float64) + rng.choice([0.0, 0.5, 0.99], n)
+    odd = np.array([np.nan, 0.0, -0.0, 1.5, 3.0, -0.25, 1e-30, np.inf, -np.inf, 0.1, 0.3], np.float32)
+    rates = np.where(rng.random(n) < 0.3, rng.choice(odd, n), np.float32(1.0)).astype(np.float32)
+    w = oracle.Worker(cap, 1, 1, 1)
+    w.counter(slots, vals, rates)
+    bufs = []
+    with make_engine((cap, 1, 1, 1)) as e:
+        if path == "host":
+            e.ingest(counters=(slots, vals, rates))
+        else:
+            e.ingest_device(_device_batch(bufs, counters=(slots, vals, rates)))
+        f = e.flush()
+    for b in bufs:
+        b.free()
+    want = {s: w.counter_value(s) for s in range(cap) if w.touched(0, s)}
+    assert dict(zip(f.counter_slot.tolist(), f.counter_value.tolist())) == want

@@ -414,3 +414,77 @@ def test_go_math_log_pow_known_values():
     for x in xs:
         assert oracle.lib.or_go_log(float(x)) == pytest.approx(np.log(x), rel=2e-16)
         assert oracle.lib.or_go_asin(float(x / 20)) == pytest.approx(np.arcsin(x / 20), rel=1e-15)
+
+
+# ---------------------------------------------------------------- NaN sample rates
+def _merge_all_temps_bounded(main, temps, main_weight, max_steps):
+    """mergeAllTemps (merging_digest.go:121-205) restated loop for loop over (mean, weight) pairs,
+    with a step bound: returns (new main, new main weight) or None when the loop has run
+    max_steps iterations without ending.  indexEstimate's asin is math.asin (NaN in, NaN out)."""
+    import math
+    temps = sorted(temps, key=lambda c: c[0])
+    total = main_weight + sum(w for _, w in temps)  # td.mainWeight + td.tempWeight
+    k = lambda q: 100.0 * (math.asin(2 * q - 1) / math.pi + 0.5) if q == q and -1 <= 2 * q - 1 <= 1 else float("nan")
+    out, merged_w, last_idx = [], 0.0, 0.0
+
+    def merge_one(before, nxt, before_idx):  # mergeOne, merging_digest.go:210-236
+        if (k((before + nxt[1]) / total) - before_idx > 1) or not out:
+            out.append(list(nxt))
+            return k(before / total)
+        c = out[-1]
+        c[1] += nxt[1]
+        c[0] += (nxt[0] - c[0]) * nxt[1] / c[1]
+        return before_idx
+
+    actual, swapped, ti, steps = list(main), [], 0, 0
+    while len(actual) + len(swapped) != 0 or ti < len(temps):
+        steps += 1
+        if steps > max_steps:
+            return None
+        nt = temps[ti] if ti < len(temps) else (float("inf"), 0.0)
+        nm = swapped[0] if swapped else (actual[0] if actual else (float("inf"), 0.0))
+        if nm[0] < nt[0]:
+            if actual:
+                if swapped:
+                    swapped = swapped[1:] + [actual[0]]
+                actual = actual[1:]
+            else:
+                swapped = swapped[1:]
+            last_idx = merge_one(merged_w, nm, last_idx)
+            merged_w += nm[1]
+        else:
+            if actual:
+                swapped.append(actual[0])
+                actual = actual[1:]
+            ti += 1
+            last_idx = merge_one(merged_w, nt, last_idx)
+            merged_w += nt[1]
+    return [tuple(c) for c in out], total
+
+
+def test_nan_weight_merge_never_ends():
+    """Why a histogram sample with a NaN rate is refused ("NaN sample rates").
+
+    The parser lets @nan through (parser.go:262-272: both comparisons false); Histo.Sample's weight
+    float64(1/NaN) is NaN and MergingDigest.Add accepts it (merging_digest.go:98 checks weight <= 0).
+    The merge that takes it has totalWeight NaN, so mergeOne never starts a new centroid: every
+    element joins the first, whose mean turns NaN.  At the next mergeAllTemps the main centroid's
+    NaN mean loses every `nextMain.Mean < nextTemp.Mean` test -- also against the +Inf sentinel
+    once the temps are used up -- so it is never consumed and the loop never ends: Go's worker
+    spins holding its mutex.  No output exists to match; the engine refuses the record and the
+    Worker drops it (counted).  The restated loop is checked on a normal digest first."""
+    ok = _merge_all_temps_bounded([], [(float(v), 1.0) for v in range(42)], 0.0, 10_000)
+    assert ok is not None and len(ok[0]) > 1 and ok[1] == 42.0
+    # 41 samples at rate 1 and one at rate NaN: the first merge collapses them into one NaN centroid
+    temps = [(float(v), 1.0) for v in range(41)] + [(17.5, float("nan"))]
+    first = _merge_all_temps_bounded([], temps, 0.0, 10_000)
+    assert first is not None and len(first[0]) == 1
+    (mean, weight), = first[0]
+    assert mean != mean and weight != weight and first[1] != first[1]
+    # the next 42 samples' merge: bounded at 100k steps against the ~43 a merge needs
+    assert _merge_all_temps_bounded(first[0], [(float(v), 1.0) for v in range(42)], first[1], 100_000) is None
+    # a counter's NaN rate is defined: int64(float32(1/NaN)) = MinInt64 on amd64, times the
+    # truncated sample, wrapping (samplers.go:133)
+    w = oracle.Worker(3, 0, 0, 0)
+    w.counter([0, 1, 2], [2.0, 3.0, 5.0], np.array([np.nan, np.nan, 0.0], np.float32))
+    assert [w.counter_value(s) for s in range(3)] == [0, -(1 << 63), -(1 << 63)]

@@ -18,6 +18,13 @@ from veneur_amd.engine import EngineError, FlushOutput
 K = W.MetricKey
 
 
+def go_i64(x):
+    """Go's float64 -> int64 conversion on amd64 (CVTTSD2SQ): NaN and out-of-range give MinInt64."""
+    if x != x or not (-9.223372036854775808e18 < x < 9.223372036854775808e18):
+        return -(1 << 63)
+    return int(x)
+
+
 class RecordingEngine:
     """Stands in for veneur_amd.Engine: records the calls, flushes counters as sums."""
 
@@ -33,7 +40,10 @@ class RecordingEngine:
                 self.hvals.setdefault(int(s), []).append(float(v))
         if "counters" in kw:
             for s, v, r in zip(*kw["counters"]):
-                self.cval[int(s)] = self.cval.get(int(s), 0) + int(v) * int(np.float32(1) / r)
+                with np.errstate(divide="ignore", invalid="ignore"):
+                    inv = float(np.float32(1) / np.float32(r))
+                x = self.cval.get(int(s), 0) + go_i64(float(v)) * go_i64(inv)
+                self.cval[int(s)] = (x + (1 << 63)) % (1 << 64) - (1 << 63)  # wrapping int64
 
     def import_counters(self, slot, v):
         self.calls.append(("import_counters", slot.tolist(), v.tolist()))
@@ -351,18 +361,22 @@ def test_generate_inter_metrics_local_and_global_rules():
         assert n in names
 
 
-def test_nan_sample_rate_drops_one_record_not_the_batch():
-    """A NaN rate passes the parser (parser.go:262-272, both comparisons false); the Worker
-    drops that one record and keeps the rest of the staged batch."""
+def test_nan_sample_rate_counter_sampled_histogram_dropped():
+    """A NaN rate passes the parser (parser.go:262-272, both comparisons false).  A counter samples
+    it as Go does: int64(sample) * int64(float32(1/NaN)) = sample * MinInt64, wrapping
+    (samplers.go:133) -- 2 * MinInt64 wraps to 0, 3 * MinInt64 to MinInt64.  A histogram's NaN
+    weight would never finish Go's next merge (test_oracle_kats.py::test_nan_weight_merge_never_ends):
+    the Worker drops that one record and keeps the rest of the staged batch."""
     from veneur_amd import parser as P
     w = W.Worker(engine=RecordingEngine(capacity=(8, 8, 8, 8)), batch_records=4)
-    lines = [b"a:1|c", b"a:2|c|@nan", b"b:5|h|@nan", b"a:3|c", b"a:4|c", b"a:5|c"]
+    lines = [b"a:1|c", b"a:2|c|@nan", b"b:5|h|@nan", b"a:3|c", b"a:4|c", b"a:5|c", b"c:3|c|@nan"]
     for ln in lines:
         m = P.parse_metric(ln)
         w.ProcessMetric(m)
-    assert w.dropped == 2
+    assert w.dropped == 1
     wm = w.Flush()
     assert wm.counters[K("a", "counter")].value == 1 + 3 + 4 + 5
+    assert wm.counters[K("c", "counter")].value == -(1 << 63)
     assert K("b", "histogram") not in wm.histograms
 
 
@@ -548,10 +562,123 @@ def test_invalid_records_screened_so_valid_batch_mates_are_kept():
     beside them reach the engine."""
     w = W.Worker(engine=RecordingEngine(), batch_records=4)
     w.ProcessMetric(W.UDPMetric(K("c", "counter"), 1.0))
-    w.ProcessMetric(W.UDPMetric(K("c", "counter"), 2.0, sample_rate=float("nan")))
+    w.ProcessMetric(W.UDPMetric(K("h", "histogram"), 2.0, sample_rate=float("nan")))
     with pytest.raises(ValueError):
         w.ProcessMetric(W.UDPMetric(K("h", "histogram"), float("inf")))
     w.ProcessMetric(W.UDPMetric(K("h", "histogram"), 3.0))
     w.Flush()
     ing = [c for c in w.engine.calls if c[0] == "ingest"]
     assert len(ing) == 1 and w.dropped == 1 and w.dropped_batches == 0
+
+
+# ---------------------------------------------------------------- engines in turn (Worker.Flush)
+class SlowEngine(RecordingEngine):
+    """A RecordingEngine whose flush takes `delay` seconds and which asserts that it never takes
+    records while its flush runs."""
+
+    def __init__(self, name, delay, log, **kw):
+        super().__init__(**kw)
+        self.name, self.delay, self.log, self.busy = name, delay, log, False
+
+    def ingest(self, **kw):
+        assert not self.busy, "engine %d took records during its flush" % self.name
+        self.log.append(("ingest", self.name))
+        super().ingest(**kw)
+
+    def import_counters(self, slot, v):
+        assert not self.busy
+        super().import_counters(slot, v)
+
+    def flush(self, histo_quantile_mask=None, set_estimate_mask=None):
+        self.busy = True
+        import time as _t
+        _t.sleep(self.delay)
+        self.log.append(("flush", self.name))
+        out = super().flush(histo_quantile_mask, set_estimate_mask)
+        self.busy = False
+        return out
+
+
+def test_worker_engines_in_turn_flush_returns_at_once():
+    """Worker(engines=D): Flush swaps the window out (worker.go:276-284) and returns a
+    PendingWorkerMetrics at once; window i runs on engine i % D; an engine takes records again
+    only after its flush; each window's maps hold that window's values."""
+    import time as _t
+    log = []
+    D, delay = 3, 0.3
+    w = W.Worker(engines=[SlowEngine(k, delay, log) for k in range(D)], batch_records=1000)
+    wms, returns = [], []
+    for i in range(7):
+        w.ProcessMetric(W.UDPMetric(K("a", "counter"), float(i + 1)))
+        w.ProcessMetric(W.UDPMetric(K("b%d" % i, "counter"), 10.0, sample_rate=0.5))
+        w.ImportMetric(W.JSONMetric(K("g", "counter"), [], struct.pack("<q", 100 + i)))
+        t0 = _t.perf_counter()
+        wms.append(w.Flush())
+        returns.append(_t.perf_counter() - t0)
+    # the first D flushes find their engines idle: they return before any flush has finished
+    assert max(returns[:D]) < delay / 2, returns
+    assert all(isinstance(m, W.PendingWorkerMetrics) for m in wms)
+    for i, wm in enumerate(wms):
+        assert wm.counters[K("a", "counter")].value == i + 1
+        assert wm.counters[K("b%d" % i, "counter")].value == 20
+        assert wm.global_counters[K("g", "counter")].value == 100 + i
+        assert len(wm) == 3
+    ing = [n for what, n in log if what == "ingest"]
+    assert ing == [i % D for i in range(7)]
+    w.close()
+    assert w.stats.calls[1] == ("count", "worker.metrics_processed_total", 2, [], 1.0)
+
+
+def test_worker_flush_raw_in_turn_and_server_flush():
+    """flush_raw(copy=True) under rotation is a Future of the window's FlushOutput; server_flush
+    over a rotating Worker still yields each window's InterMetrics."""
+    log = []
+    w = W.Worker(engines=[SlowEngine(k, 0.05, log) for k in range(2)], batch_records=1000)
+    futs = []
+    for i in range(4):
+        w.process_batch(counters=(np.array([0, 1], np.uint32), np.array([i, 2 * i], np.float64),
+                                  np.ones(2, np.float32)))
+        futs.append(w.flush_raw(copy=True))
+    for i, f in enumerate(futs):
+        out = f.result()
+        assert out.counter_value.tolist() == [i, 2 * i]
+    w.ProcessMetric(W.UDPMetric(K("x", "counter"), 4.0))
+    final, fwd = W.server_flush([w], False, (0.5,))
+    assert [(m.name, m.value) for m in final] == [("x", 4.0)]
+    w.close()
+
+
+def test_worker_drains_at_class_cap_and_pieces_imports():
+    """a class's staged records never exceed the engine's max_class_records (the engine
+    refuses such a call), and import_chunk sends each class in pieces of at most its cap."""
+    class Capped(RecordingEngine):
+        max_batch_records = 8
+        max_class_records = (2, 8, 8, 3)
+        max_batch_member_bytes = 1 << 10
+
+        def ingest(self, **kw):
+            for c, k in enumerate(("counters", "gauges", "histos", "sets")):
+                if k in kw:
+                    assert len(kw[k][0]) <= self.max_class_records[c], (k, len(kw[k][0]))
+            super().ingest(**kw)
+
+        def import_counters(self, slot, v):
+            assert len(slot) <= self.max_class_records[0]
+            super().import_counters(slot, v)
+
+        def import_sets(self, slot, p):
+            assert len(slot) <= self.max_class_records[3]
+            super().import_sets(slot, p)
+
+    w = W.Worker(engine=Capped(), batch_records=1 << 16)
+    assert w.batch_records == 8 and w.class_records == (2, 8, 8, 3)
+    for i in range(5):
+        w.ProcessMetric(W.UDPMetric(K("c", "counter"), 1.0))
+    assert w._staged == 1  # drained at 2 and 4
+    for i in range(7):
+        w.ProcessMetric(W.UDPMetric(K("s", "set"), "m%d" % i))
+    w.import_chunk([W.JSONMetric(K("c%d" % i, "counter"), [], struct.pack("<q", i)) for i in range(5)] +
+                   [W.JSONMetric(K("s%d" % i, "set"), [], b"x") for i in range(7)])
+    calls = [c[0] for c in w.engine.calls]
+    assert calls.count("import_counters") == 3 and calls.count("import_sets") == 3
+    assert w.Flush().counters[K("c", "counter")].value == 5

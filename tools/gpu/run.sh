@@ -1,0 +1,64 @@
+#!/bin/bash
+# The one GPU-box script: every gpurun call of the build runs one or more of its steps.
+#   gpurun -- bash tools/gpu/run.sh TAG STEP [STEP ...]
+# Steps (outputs under gpurun_out/TAG_*):
+#   tests    every -m gpu test (stops the call at the first failure)
+#   smoke    __graft_entry__.smoke()
+#   bench    the default bench line (python bench.py)
+#   bench1   the bench with one engine (--pipeline 1), windows back to back
+#   prof     rocprofv3 --kernel-trace --stats of a short bench with ONE engine, so every kernel's
+#            duration is its own (no other window's kernels beside it); roofline_check over it
+#   c5prof   rocprofv3 --kernel-trace --stats of the C5 leg alone
+#   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) for the replay's HBM traffic
+#   hot      batched-replay parity tests, phase cycles (profiling build) and the 17M-sample key
+# Each step runs under its own time limit; the first failure, fault, abort or timeout ends
+# the call (no retries).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=$1
+shift
+O=gpurun_out/$TAG
+SHORT="--steps 2 --warmup 1 --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0 --parity-keys 64"
+for step in "$@"; do
+  echo "[run.sh] $TAG: $step ($(date +%T))"
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > ${O}_tests.log 2>&1 ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > ${O}_smoke.txt 2>&1 ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > ${O}_bench.json 2> ${O}_bench.log ;;
+    bench1)
+      timeout -k 10 600 python -u bench.py --pipeline 1 --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 \
+        --text-lines 0 > ${O}_bench1.json 2> ${O}_bench1.log ;;
+    prof)
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/${O}_prof" \
+        -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --pipeline 1 $SHORT > "$GRAFT_REPO_ROOT/${O}_prof.log" 2>&1) &&
+      python3 tools/roofline_check.py ${O}_prof ${O}_prof.log 1 ${O}_timing_step_kernel_stats.csv \
+        > ${O}_roofline_check.txt 2>&1 ;;
+    c5prof)
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/${O}_c5prof" \
+        -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --c5-only > "$GRAFT_REPO_ROOT/${O}_c5prof.log" 2>&1) ;;
+    pmc)
+      A="--steps 1 --warmup 0 --timing-steps 1 --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0 --parity-keys 64"
+      timeout -k 10 300 python bench.py $A > ${O}_pmcbench.json 2> ${O}_pmcbench.log &&
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$GRAFT_REPO_ROOT/${O}_fetch" -o run \
+        -- python3 "$GRAFT_REPO_ROOT/bench.py" $A > "$GRAFT_REPO_ROOT/${O}_fetch.log" 2>&1) &&
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$GRAFT_REPO_ROOT/${O}_write" -o run \
+        -- python3 "$GRAFT_REPO_ROOT/bench.py" $A > "$GRAFT_REPO_ROOT/${O}_write.log" 2>&1) ;;
+    hot)
+      timeout -k 10 300 python -u -m pytest tests/test_batch_replay_gpu.py -x -q --timeout 150 --timeout-method thread \
+        > ${O}_hot_tests.log 2>&1 &&
+      VN_LIB=libveneur_amd_prof.so timeout -k 10 120 python -u tools/exact_profile.py 4000000 > ${O}_hot_prof.log 2>&1 &&
+      timeout -k 10 300 python -u tools/hot_replay_bench.py --n 17000000 --keys 1 --rates --reps 2 > ${O}_hot_17M.log 2>&1 ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+  rc=$?
+  echo "[run.sh] $TAG: $step rc=$rc ($(date +%T))"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
+exit 0

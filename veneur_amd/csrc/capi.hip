@@ -148,10 +148,15 @@ void create_impl(vn_engine* e) {
       VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join6, hipEventDisableTiming));
       e->reserved_cus = r;
     }
-    // A/B knob (VN_EARLY_TOP=1): the longest batched replays on a stream of their own, started
-    // once their own chunks are sorted (ingest_histo.hip).  Measured on C4 with three engines in
-    // turn: 99.4 ms per window against 86.0 (one more stream per engine), not kept
-    e->early_top = getenv("VN_EARLY_TOP") != nullptr;
+    // A/B build knob (make variant VARIANT_FLAGS=-DVN_EARLY_TOP=1): the longest batched replays on
+    // a stream of their own, started once their own chunks are sorted (ingest_histo.hip).  Measured
+    // on C4 with three engines in turn: 99.4 ms per window against 86.0 (one more stream per engine,
+    // DESIGN.md §8), not kept.  A build flag, not the environment: production behaviour must not
+    // change with a variable set in the caller's environment.
+#ifndef VN_EARLY_TOP
+#define VN_EARLY_TOP 0
+#endif
+    e->early_top = VN_EARLY_TOP != 0;
     if (!e->st6 && e->early_top) {
       if (e->side_cus != ncu) VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st6, (uint32_t)rmask.size(), rmask.data()));
       else VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st6, hipStreamNonBlocking, prio_hi));
@@ -568,9 +573,13 @@ void throw_caller_errors(uint32_t caller) {
 
 // Validation of a device-resident batch (vn_ingest), where the reference would panic or the
 // parser would have rejected the line: slots within capacity (an interned key), histo values
-// neither NaN nor +-Inf (MergingDigest.Add panics, merging_digest.go:98-100), sample rates in
-// (0, 1] (parser.go:262-272; Counter.Sample / Histo.Sample divide by them), set member offsets
-// non-decreasing.  One pass over the batch, flags in h_err[1]; the host reads them before any
+// neither NaN nor +-Inf (MergingDigest.Add panics, merging_digest.go:98-100), histogram sample
+// rates in (0, 1] (parser.go:262-272; see below), set member offsets non-decreasing.  Counter
+// rates are not checked: Counter.Sample's int64(sample) * int64(float32(1/rate)) is defined for
+// every float32 rate -- a NaN rate (which the parser lets through: both of its comparisons are
+// false) or 0 gives int64(NaN / +Inf) = MinInt64 on amd64, which f64_to_i64_go reproduces.  A
+// histogram's NaN rate is refused: Go's digest takes the NaN weight (Add checks weight <= 0) and
+// its next mergeAllTemps over a NaN-mean centroid never terminates (NaN rates).  One pass over the batch, flags in h_err[1]; the host reads them before any
 // state-mutating kernel is queued, so a rejected batch leaves the window untouched.
 constexpr uint32_t kBadSlot = 1u, kBadValue = 2u, kBadRate = 4u, kBadOffsets = 8u;
 __global__ void k_validate_batch(vn_batch b, uint32_t cc, uint32_t cg, uint32_t ch, uint32_t cs,
@@ -578,11 +587,7 @@ __global__ void k_validate_batch(vn_batch b, uint32_t cc, uint32_t cg, uint32_t 
   const uint64_t nmax = max(max(b.n_counter, b.n_gauge), max(b.n_histo, b.n_set));
   uint32_t f = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nmax; i += (uint64_t)gridDim.x * blockDim.x) {
-    if (i < b.n_counter) {
-      const float r = b.counter_rate[i];
-      if (b.counter_slot[i] >= cc) f |= kBadSlot;
-      if (!(r > 0.0f && r <= 1.0f)) f |= kBadRate;
-    }
+    if (i < b.n_counter && b.counter_slot[i] >= cc) f |= kBadSlot;
     if (i < b.n_gauge && b.gauge_slot[i] >= cg) f |= kBadSlot;
     if (i < b.n_histo) {
       const double v = b.histo_value[i];
@@ -615,14 +620,10 @@ __global__ void k_validate_batch4(vn_batch b, uint32_t cc, uint32_t cg, uint32_t
     const uint64_t i0 = 4 * q;
     if (i0 + 4 <= b.n_counter) {
       const uint4 sl = reinterpret_cast<const uint4*>(b.counter_slot)[q];
-      const float4 r = reinterpret_cast<const float4*>(b.counter_rate)[q];
       if (max(max(sl.x, sl.y), max(sl.z, sl.w)) >= cc) f |= kBadSlot;
-      if (bad_rate(r.x) || bad_rate(r.y) || bad_rate(r.z) || bad_rate(r.w)) f |= kBadRate;
     } else {
-      for (uint64_t i = i0; i < b.n_counter && i < i0 + 4; i++) {
+      for (uint64_t i = i0; i < b.n_counter && i < i0 + 4; i++)
         if (b.counter_slot[i] >= cc) f |= kBadSlot;
-        if (bad_rate(b.counter_rate[i])) f |= kBadRate;
-      }
     }
     if (i0 + 4 <= b.n_gauge) {
       const uint4 sl = reinterpret_cast<const uint4*>(b.gauge_slot)[q];
@@ -786,9 +787,6 @@ void ingest_host(vn_engine* e, const vn_batch* b) {
     if (v != v || v - v != 0) throw std::invalid_argument("invalid value added");  // merging_digest.go:98-100
     if (!(r > 0.0f && r <= 1.0f)) throw std::invalid_argument("sample rate must be >0 and <=1");
   }
-  for (uint64_t i = 0; i < b->n_counter; i++)
-    if (!(b->counter_rate[i] > 0.0f && b->counter_rate[i] <= 1.0f))
-      throw std::invalid_argument("sample rate must be >0 and <=1");
   hipStream_t st = e->st;
   ensure_device_stage(e);
   DeviceBatch& d = e->dstage;
@@ -917,7 +915,9 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
     return VN_EINVAL;
   }
   e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 0xFFFFFFFFu;  // exact
-  if (const char* lr = getenv("VN_LONG_REPLAY")) e->long_replay = (uint32_t)strtoul(lr, nullptr, 10);  // (A/B knob)
+#ifdef VN_LONG_REPLAY
+  e->long_replay = VN_LONG_REPLAY;  // (A/B build knob: replays of at least this many samples take four waves)
+#endif
   e->hot_prefix = std::min(e->exact_threshold, cfg->histo_hot_prefix ? cfg->histo_hot_prefix : 4096u);
   e->piece_growth = cfg->histo_piece_growth ? std::min(cfg->histo_piece_growth, 1000u) : 25u;
   e->temp_cap = temp_buffer_cap(e->cfg.compression);

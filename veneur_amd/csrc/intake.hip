@@ -6,8 +6,9 @@
 //   1. vn_parse_dogstatsd_device (parse_device.hip): one parsed record per non-empty line;
 //   2. k_in_class: the Upsert map of each line that parses (worker.go:81-138: counters/gauges with
 //      veneurglobalonly -> global maps, histograms/timers/sets with veneurlocalonly -> local
-//      maps); counter and histogram/timer lines whose sample rate is NaN are dropped (the parser
-//      lets NaN through, parser.go:265; the engine rejects it -- the host Worker drops them too);
+//      maps); histogram/timer lines whose sample rate is NaN are dropped (the parser lets NaN
+//      through, parser.go:265; Go's digest would never finish its next merge, DESIGN.md §4 -- the
+//      host Worker drops them too); a counter's NaN rate is sampled as Go does (MinInt64 factor);
 //   3. the window's key table, a device hash table MetricKey -> slot with linear probing:
 //      k_in_probe finds resident keys; k_in_claim makes each missing key one pending entry by
 //      compare-and-swap (lines that find a pending entry compare their key with the pending line's
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(256) void k_in_class(const vn_parsed_line* __restri
   if (o.status == VN_PARSE_OK) {
     m = map_for(o.type, o.scope);
     const uint8_t c = c_map_class[m];
-    if ((c == 0 || c == 2) && o.rate != o.rate) {  // NaN sample rate
+    if (c == 2 && o.rate != o.rate) {  // a histogram/timer with a NaN sample rate
       m = kNoMap;
       atomicAdd(dropped, 1u);
     }

@@ -361,28 +361,7 @@ class Engine:
     def flush(self, histo_quantile_mask=None, set_estimate_mask=None) -> FlushOutput:
         """Worker.Flush + sampler flush math; the masks (per slot, 1 = compute) select which
         histograms get percentiles and which sets an estimate (a local veneur, vn_flush_masked)."""
-        o = self.flush_raw(histo_quantile_mask, set_estimate_mask)
-        npct = len(self.percentiles)
-        out = FlushOutput(
-            counter_slot=_arr(o.counter_slot, o.n_counter, np.uint32),
-            counter_value=_arr(o.counter_value, o.n_counter, np.int64),
-            gauge_slot=_arr(o.gauge_slot, o.n_gauge, np.uint32),
-            gauge_value=_arr(o.gauge_value, o.n_gauge, np.float64),
-            histo_slot=_arr(o.histo_slot, o.n_histo, np.uint32),
-            histo_stats=_arr(o.histo_stats, o.n_histo, np.float64, (A.VN_HISTO_STATS,)),
-            histo_quantiles=(_arr(o.histo_quantiles, o.n_histo, np.float64, (npct,)) if npct
-                             else np.zeros((o.n_histo, 0))),
-            set_slot=_arr(o.set_slot, o.n_set, np.uint32),
-            set_estimate=_arr(o.set_estimate, o.n_set, np.uint64),
-            set_sparse=_arr(o.set_sparse, o.n_set, np.uint8),
-            samples_processed=o.samples_processed,
-            samples_imported=o.samples_imported,
-            warn_flags=int(o.warn_flags),
-        )
-        if out.warn_flags & A.VN_WARN_SPLIT_TOUCHED:
-            warnings.warn("a split key's slot also received vn_ingest records or imports this window (its "
-                          "records go through vn_ingest_split); the split combine's state was kept", RuntimeWarning)
-        return out
+        return flush_output(self.flush_raw(histo_quantile_mask, set_estimate_mask), len(self.percentiles))
 
     # ---------------------------------------------------------------- introspection
     def read_histo(self, slot, cap=4096):
@@ -415,6 +394,31 @@ class Engine:
         t = A.Timing()
         self._check(A.lib.vn_get_timing(self.h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in A.Timing._fields_}
+
+
+def flush_output(o, npct) -> FlushOutput:
+    """A vn_flush_result (engine-owned pinned arrays, valid until that engine's next flush) copied
+    into a FlushOutput of numpy arrays."""
+    out = FlushOutput(
+        counter_slot=_arr(o.counter_slot, o.n_counter, np.uint32),
+        counter_value=_arr(o.counter_value, o.n_counter, np.int64),
+        gauge_slot=_arr(o.gauge_slot, o.n_gauge, np.uint32),
+        gauge_value=_arr(o.gauge_value, o.n_gauge, np.float64),
+        histo_slot=_arr(o.histo_slot, o.n_histo, np.uint32),
+        histo_stats=_arr(o.histo_stats, o.n_histo, np.float64, (A.VN_HISTO_STATS,)),
+        histo_quantiles=(_arr(o.histo_quantiles, o.n_histo, np.float64, (npct,)) if npct
+                         else np.zeros((o.n_histo, 0))),
+        set_slot=_arr(o.set_slot, o.n_set, np.uint32),
+        set_estimate=_arr(o.set_estimate, o.n_set, np.uint64),
+        set_sparse=_arr(o.set_sparse, o.n_set, np.uint8),
+        samples_processed=o.samples_processed,
+        samples_imported=o.samples_imported,
+        warn_flags=int(o.warn_flags),
+    )
+    if out.warn_flags & A.VN_WARN_SPLIT_TOUCHED:
+        warnings.warn("a split key's slot also received vn_ingest records or imports this window (its "
+                      "records go through vn_ingest_split); the split combine's state was kept", RuntimeWarning)
+    return out
 
 
 class Comm:

@@ -214,6 +214,9 @@ def DeviceWorker(*args, intake_bytes=1 << 24, **kw):
     class _DeviceWorker(Worker):
         def __init__(self, *a, **k):
             super().__init__(*a, **k)
+            if self.pipeline > 1:
+                # the device key table lives beside one engine, and Flush reads it back at once
+                raise ValueError("DeviceWorker drives one engine (pipeline=1)")
             self.intake = Intake(self.engine, intake_bytes)
             self._win = _DeviceWindow(self.intake)
             self.parse_errors = 0

@@ -343,38 +343,129 @@ class WorkerStats:
         self.calls.append(("count", name, int(value), tags, rate))
 
 
+class PendingWorkerMetrics(WorkerMetrics):
+    """The WorkerMetrics of a window whose engine is still flushing (Worker(pipeline=D > 1)).
+
+    The reference's Worker.Flush only swaps the maps under the lock (worker.go:276-284); the
+    flusher reads the swapped maps afterwards (flusher.go:115-230).  Here Flush hands the window's
+    engine to a flush thread of its own and returns at once; the ten maps are filled the first
+    time any of them is read, which waits for that engine's vn_flush."""
+
+    def __init__(self, future):
+        self._future = future
+
+    def done(self):
+        return self._future.done()
+
+    def wait(self, timeout=None):
+        """The flushed window's maps (blocks until the engine's flush has returned)."""
+        if "counters" not in self.__dict__:
+            wm = self._future.result(timeout)
+            self.__dict__.update({m: getattr(wm, m) for m in _MAPS})
+        return self
+
+    def __getattr__(self, name):
+        if name in _MAPS:
+            self.wait()
+            return self.__dict__[name]
+        raise AttributeError(name)
+
+
 class Worker:
     """veneur Worker (worker.go) whose samplers live in HBM.
 
     engine: a veneur_amd.Engine (or anything with its ingest/import/export/flush methods);
     created from `capacity`/`percentiles` when omitted.  percentiles: the quantiles Flush
-    computes (0.5 is always added for the median aggregate)."""
+    computes (0.5 is always added for the median aggregate).
+
+    pipeline / engines: D engines on the GPU taking the flush windows in turn, as the
+    reference's Worker.Flush swaps in fresh maps and the flusher works on the old ones while the
+    worker takes the next interval (worker.go:276-284, flusher.go:115-230).  Flush() drains the
+    window into the current engine, starts that engine's flush on a thread of its own and returns
+    a PendingWorkerMetrics; ProcessMetric and ImportMetric move to the next engine at once.  An
+    engine takes records again only after its previous flush has returned (the first call that
+    needs it waits), so D windows at most are in flight.  D > 1 needs every engine stream on a
+    hardware queue of its own: GPU_MAX_HW_QUEUES=16 in the environment before HIP starts
+    (INTEGRATION.md); Worker sets it when it creates the engines and HIP has not started yet."""
 
     def __init__(self, id=0, capacity=(1 << 16, 1 << 16, 1 << 16, 1 << 16), percentiles=(0.5, 0.9, 0.99),
-                 batch_records=1 << 16, engine=None, stats=None, **engine_kw):
+                 batch_records=1 << 16, engine=None, stats=None, pipeline=1, engines=None, **engine_kw):
         self.id = id
         # the worker's own statsd client (worker.go:30,286-295); a WorkerStats recorder by default
         self.stats = stats if stats is not None else WorkerStats()
         pct = tuple(sorted(set(float(p) for p in percentiles) | {0.5}))
-        if engine is None:
-            from .engine import Engine
-            engine = Engine(capacity, percentiles=pct, max_batch_records=max(batch_records, 1),
-                            max_batch_member_bytes=max(batch_records, 1) * 64, **engine_kw)
-        self.engine = engine
+        if engines is None:
+            if engine is not None:
+                engines = [engine]
+            else:
+                from .engine import Engine
+                if pipeline > 1:
+                    import os
+                    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+                engines = [Engine(capacity, percentiles=pct, max_batch_records=max(batch_records, 1),
+                                  max_batch_member_bytes=max(batch_records, 1) * 64, **engine_kw)
+                           for _ in range(max(1, int(pipeline)))]
+        self._engines = list(engines)
+        self._cur = 0
+        self._pending = [None] * len(self._engines)  # each engine's last flush (a Future), D > 1
+        self._flushers = None
+        if len(self._engines) > 1:
+            from concurrent.futures import ThreadPoolExecutor
+            self._flushers = [ThreadPoolExecutor(1, thread_name_prefix="veneur-flush-%s-%d" % (id, k))
+                              for k in range(len(self._engines))]
+        engine = self._engines[0]
         self.capacity = tuple(int(c) for c in getattr(engine, "capacity", capacity))
         self.percentiles = tuple(float(p) for p in getattr(engine, "percentiles", pct))
+        # one ingest call carries at most the engines' max_batch_records, and of each class at most
+        # its max_class_records (vn_config.max_batch_class_records): the stage drains at either
         self.batch_records = int(batch_records)
+        caps = [getattr(e, "max_class_records", None) for e in self._engines]
+        mbr = [int(getattr(e, "max_batch_records", 0) or 0) for e in self._engines]
+        if all(mbr):
+            self.batch_records = min([self.batch_records] + mbr)
+        self.class_records = tuple(min([self.batch_records] + [int(c[k]) for c in caps if c]) for k in range(4))
         self.processed = 0
         self.imported = 0
-        self.dropped = 0  # records with a NaN sample rate (see process_metric)
+        self.dropped = 0  # histogram records with a NaN sample rate (see process_metric)
         # whole staged batches the engine refused (ingest raised), and their records: every value
         # the engine validates is screened in process_metric first, so these stay exceptional
         self.dropped_batches = 0
         self.dropped_batch_records = 0
         # set member bytes one ingest call may carry (the engine's max_batch_member_bytes)
-        self.max_member_bytes = int(getattr(engine, "max_batch_member_bytes", 0) or max(batch_records, 1) * 64)
+        self.max_member_bytes = min(int(getattr(e, "max_batch_member_bytes", 0) or max(batch_records, 1) * 64)
+                                    for e in self._engines)
         self._win = _Window()
         self._reset_stage()
+
+    # ------------------------------------------------------------ engines in turn
+    @property
+    def engine(self):
+        """The engine taking this window's records."""
+        return self._engines[self._cur]
+
+    @property
+    def pipeline(self):
+        return len(self._engines)
+
+    def _eng(self):
+        """The current engine, once its previous flush (D windows ago) has returned."""
+        p = self._pending[self._cur]
+        if p is not None:
+            from concurrent.futures import wait
+            wait([p])
+            self._pending[self._cur] = None
+        return self._engines[self._cur]
+
+    def _hand_off(self, job):
+        """Run job (the flush of the current engine) now (D = 1) or on that engine's flush thread,
+        and move ingest to the next engine (D > 1): the map swap of worker.go:276-284."""
+        if self._flushers is None:
+            return job()
+        self._eng()
+        fut = self._flushers[self._cur].submit(job)
+        self._pending[self._cur] = fut
+        self._cur = (self._cur + 1) % len(self._engines)
+        return fut
 
     # ------------------------------------------------------------ staging
     def _reset_stage(self):
@@ -383,6 +474,7 @@ class Worker:
         self._h = ([], [], [])
         self._s = ([], [])
         self._staged = 0
+        self._cls_staged = [0, 0, 0, 0]
         self._member_bytes = 0
 
     def _drain(self):
@@ -405,7 +497,7 @@ class Worker:
             kw["sets"] = (np.array(self._s[0], np.uint32), off, np.frombuffer(b"".join(mem) or b"\0", np.uint8))
         from .engine import EngineError
         try:
-            self.engine.ingest(**kw)
+            self._eng().ingest(**kw)
         except EngineError as err:
             # a batch the engine rejects is dropped and counted, never resubmitted: one bad batch
             # must not block every later ProcessMetric and the window's flush
@@ -431,12 +523,15 @@ class Worker:
             if cls == 2 and (v != v or v in (float("inf"), float("-inf"))):
                 raise ValueError("invalid value added")  # MergingDigest.Add panics (merging_digest.go:98-100)
         rate = np.float32(m.sample_rate)
-        if cls in (0, 2) and not (0.0 < rate <= 1.0):
+        if cls == 2 and not (0.0 < rate <= 1.0):
             # The parser rejects rates outside (0, 1] but lets NaN through (parser.go:262-272:
-            # both comparisons are false), and Go then samples with NaN arithmetic -- int64(NaN)
-            # for a counter, a NaN digest weight for a histogram.  The engine rejects such a
-            # record (VN_EINVAL); it is dropped and counted here, one record, so the rest of
-            # the batch is unaffected.
+            # both comparisons are false).  A counter samples any rate as Go does
+            # (int64(float32(1/NaN)) = MinInt64 on amd64; the engine reproduces it).  A histogram's
+            # NaN weight passes MergingDigest.Add (it checks weight <= 0), and Go's next
+            # mergeAllTemps over the NaN-mean centroid that follows never terminates
+            # ("NaN sample rates"; tests/test_oracle_kats.py): the engine refuses
+            # such a record (VN_EINVAL), so it is dropped and counted here, one record, and the
+            # rest of the batch is unaffected.
             self.dropped += 1
             log.warning("dropping %s sample with sample rate %r", m.key.name, m.sample_rate)
             return
@@ -457,7 +552,8 @@ class Worker:
             self._s[0].append(slot), self._s[1].append(member)
             self._member_bytes += len(member)
         self._staged += 1
-        if self._staged >= self.batch_records:
+        self._cls_staged[cls] += 1
+        if self._staged >= self.batch_records or self._cls_staged[cls] >= self.class_records[cls]:
             self._drain()
 
     ProcessMetric = process_metric
@@ -481,23 +577,22 @@ class Worker:
         self._drain()  # samples staged before this import are aggregated first
         cls = _MAPS[map_name][0]
         from .engine import EngineError
+        eng = self._eng()
         try:
             # Counter/Gauge.Combine decode with binary.Read, which reads the first 8 bytes and
             # fails only on a shorter payload (samplers.go:171-183, 237-249)
             if cls == 0:
                 if len(other.value) < 8:
                     raise EngineError("counter payload is %d bytes, fewer than 8" % len(other.value))
-                self.engine.import_counters(np.array([slot], np.uint32),
-                                            np.array(struct.unpack("<q", bytes(other.value[:8]))))
+                eng.import_counters(np.array([slot], np.uint32), np.array(struct.unpack("<q", bytes(other.value[:8]))))
             elif cls == 1:
                 if len(other.value) < 8:
                     raise EngineError("gauge payload is %d bytes, fewer than 8" % len(other.value))
-                self.engine.import_gauges(np.array([slot], np.uint32),
-                                          np.array(struct.unpack("<d", bytes(other.value[:8]))))
+                eng.import_gauges(np.array([slot], np.uint32), np.array(struct.unpack("<d", bytes(other.value[:8]))))
             elif cls == 2:
-                self.engine.import_histos(np.array([slot], np.uint32), [bytes(other.value)])
+                eng.import_histos(np.array([slot], np.uint32), [bytes(other.value)])
             else:
-                self.engine.import_sets(np.array([slot], np.uint32), [bytes(other.value)])
+                eng.import_sets(np.array([slot], np.uint32), [bytes(other.value)])
         except EngineError as err:
             log.error("Could not merge %s: %s", map_name.replace("global_", ""), err)
 
@@ -505,9 +600,10 @@ class Worker:
 
     def import_chunk(self, metrics):
         """ImportMetric for every metric of a chunk (worker.go:230-268), with one engine call per
-        sampler class: same Upsert, same arrival order within a class (the only order that can
-        matter: a key belongs to one class), and a payload that fails to decode is logged and
-        skipped alone -- a failing batch is retried metric by metric."""
+        sampler class and piece of at most that class's record cap (max_class_records): same Upsert,
+        same arrival order within a class (the only order that can matter: a key belongs to one
+        class), and a payload that fails to decode is logged and skipped alone -- a failing piece is
+        retried metric by metric."""
         from .engine import EngineError
         groups = {0: [], 1: [], 2: [], 3: []}
         for m in metrics:
@@ -526,26 +622,45 @@ class Worker:
                 continue
             groups[cls].append((slot, m, map_name))
         self._drain()  # samples staged before the chunk are aggregated first
-        if groups[0]:
-            self.engine.import_counters(np.array([g[0] for g in groups[0]], np.uint32),
-                                        np.array([struct.unpack("<q", bytes(g[1].value[:8]))[0] for g in groups[0]],
-                                                 np.int64))
-        if groups[1]:
-            self.engine.import_gauges(np.array([g[0] for g in groups[1]], np.uint32),
-                                      np.array([struct.unpack("<d", bytes(g[1].value[:8]))[0] for g in groups[1]],
-                                               np.float64))
-        for cls, fn in ((2, self.engine.import_histos), (3, self.engine.import_sets)):
+        eng = self._eng()
+        for cls in (0, 1, 2, 3):
             items = groups[cls]
-            if not items:
-                continue
-            try:
-                fn(np.array([g[0] for g in items], np.uint32), [bytes(g[1].value) for g in items])
-            except EngineError:  # find the bad payload(s): the engine applied nothing of the batch
-                for slot, m, map_name in items:
-                    try:
-                        fn(np.array([slot], np.uint32), [bytes(m.value)])
-                    except EngineError as err:
-                        log.error("Could not merge %s: %s", map_name, err)
+            cap = max(1, self.class_records[cls])
+            for i in range(0, len(items), cap):
+                piece = items[i:i + cap]
+                slots = np.array([g[0] for g in piece], np.uint32)
+                if cls == 0:
+                    eng.import_counters(slots, np.array([struct.unpack("<q", bytes(g[1].value[:8]))[0] for g in piece],
+                                                        np.int64))
+                    continue
+                if cls == 1:
+                    eng.import_gauges(slots, np.array([struct.unpack("<d", bytes(g[1].value[:8]))[0] for g in piece],
+                                                      np.float64))
+                    continue
+                fn = eng.import_histos if cls == 2 else eng.import_sets
+                try:
+                    fn(slots, [bytes(g[1].value) for g in piece])
+                except EngineError:  # find the bad payload(s): the engine applied nothing of the piece
+                    for slot, m, map_name in piece:
+                        try:
+                            fn(np.array([slot], np.uint32), [bytes(m.value)])
+                        except EngineError as err:
+                            log.error("Could not merge %s: %s", map_name, err)
+
+    def process_batch(self, batch=None, **arrays):
+        """A batch of ProcessMetric calls whose keys the caller has interned itself -- the cgo
+        binding's path (Go fills the engine's pinned stage, vn_submit) or the device
+        intake's: an A.Batch whose arrays are in device memory (vn_ingest), or host arrays as
+        Engine.ingest takes them (counters=(slot, value, rate), gauges=, histos=, sets= or
+        set_hashes=; arrival order per class).  Those keys have no MetricKey on the host, so they
+        appear in flush_raw()'s result, not in Flush()'s maps."""
+        self._drain()
+        if batch is not None:
+            self._eng().ingest_device(batch)
+            self.processed += int(batch.n_counter + batch.n_gauge + batch.n_histo + batch.n_set)
+        else:
+            self._eng().ingest(**arrays)
+            self.processed += sum(len(v[0]) for v in arrays.values())
 
     def flush(self, forward=False, is_local=False, need_median=False) -> WorkerMetrics:
         """Worker.Flush (worker.go:271-298): the window's samplers, and a fresh window.  With
@@ -554,26 +669,53 @@ class Worker:
         local veneur, whose Server.Flush asks no percentiles of mixed-scope histograms/timers
         and flushes no mixed-scope sets (flusher.go:41-48,181-211) -- the engine then skips
         those quantiles and estimates (vn_flush_masked); need_median keeps the quantiles, as
-        Histo.Flush evaluates Quantile(0.5) for the median aggregate regardless."""
+        Histo.Flush evaluates Quantile(0.5) for the median aggregate regardless.
+
+        With D > 1 engines (pipeline) the engine's flush runs on its flush thread and this
+        returns a PendingWorkerMetrics at once (the class docstring)."""
         start = time.perf_counter_ns()
         self._drain()
         win = self._take_window()
-        payload = {}
-        if forward:
-            for cls, names, fn in ((2, ("histograms", "timers"), self.engine.export_histos),
-                                   (3, ("sets",), self.engine.export_sets)):
-                slots = [s for n in names for (s, _) in win.maps[n].values()]
-                if slots:
-                    for s, p in zip(slots, fn(np.array(slots, np.uint32))):
-                        payload[(cls, s)] = p
-        if is_local:
-            qmask, emask = self._masks(win, need_median)
-            f = self.engine.flush(histo_quantile_mask=qmask, set_estimate_mask=emask)
-        else:
-            f = self.engine.flush()
-        wm = self._worker_metrics(win, f, payload)
+        eng = self._eng()
+
+        def job():
+            payload = {}
+            if forward:
+                for cls, names, fn in ((2, ("histograms", "timers"), eng.export_histos),
+                                       (3, ("sets",), eng.export_sets)):
+                    slots = [s for n in names for (s, _) in win.maps[n].values()]
+                    if slots:
+                        for s, p in zip(slots, fn(np.array(slots, np.uint32))):
+                            payload[(cls, s)] = p
+            if is_local:
+                qmask, emask = self._masks(win, need_median)
+                f = eng.flush(histo_quantile_mask=qmask, set_estimate_mask=emask)
+            else:
+                f = eng.flush()
+            return self._worker_metrics(win, f, payload)
+
+        out = self._hand_off(job)
         self._flush_stats(start)
-        return wm
+        return out if self._flushers is None else PendingWorkerMetrics(out)
+
+    def flush_raw(self, histo_quantile_mask=None, set_estimate_mask=None, copy=False):
+        """Worker.Flush returning the engine's flush result itself (per class: touched slots and
+        their values, histogram stats and quantiles, set estimates) instead of the ten maps: for
+        callers that interned their keys themselves (process_batch).  copy=False: the
+        vn_flush_result, whose arrays live in the engine's pinned memory until that engine's next
+        flush (D windows later); copy=True: a FlushOutput of numpy copies.  With D > 1 engines it
+        returns a concurrent.futures.Future of the result."""
+        start = time.perf_counter_ns()
+        self._drain()
+        self._take_window()
+        eng = self._eng()
+
+        def job():
+            return (eng.flush if copy else eng.flush_raw)(histo_quantile_mask, set_estimate_mask)
+
+        out = self._hand_off(job)
+        self._flush_stats(start)
+        return out
 
     def _flush_stats(self, start):
         """The end of Worker.Flush (worker.go:286-295): reset processed/imported and report the
@@ -608,18 +750,24 @@ class Worker:
         bodies (veneur_amd.sink, vn_datadog_flush): generateInterMetrics (flusher.go:168-230) +
         finalizeMetrics and chunking (sinks/datadog/datadog.go:77-106,160-213) + PostHelper's JSON
         (http/http.go:116-135) in C++, with no per-key Python objects.  Returns ([(ok, body)],
-        (n_intermetrics, n_metrics))."""
+        (n_intermetrics, n_metrics)); with D > 1 engines, a concurrent.futures.Future of it."""
         aggregates = aggregates or DEFAULT_AGGREGATES
         start = time.perf_counter_ns()
         self._drain()
         win = self._take_window()
-        if is_local:
-            qm, em = self._masks(win, bool(Aggregate(aggregates.value) & Aggregate.AggregateMedian))
-            f = self.engine.flush_raw(histo_quantile_mask=qm, set_estimate_mask=em)
-        else:
-            f = self.engine.flush_raw()
+        eng = self._eng()
+
+        def job():
+            if is_local:
+                qm, em = self._masks(win, bool(Aggregate(aggregates.value) & Aggregate.AggregateMedian))
+                f = eng.flush_raw(histo_quantile_mask=qm, set_estimate_mask=em)
+            else:
+                f = eng.flush_raw()
+            return sink.bodies(f, win.maps, self.percentiles, histogram_percentiles, aggregates, is_local, timestamp)
+
+        out = self._hand_off(job)
         self._flush_stats(start)
-        return sink.bodies(f, win.maps, self.percentiles, histogram_percentiles, aggregates, is_local, timestamp)
+        return out
 
     def _worker_metrics(self, win, f, payload):
         by_cls = [dict(zip(f.counter_slot.tolist(), f.counter_value.tolist())),
@@ -653,9 +801,21 @@ class Worker:
 
     Flush = flush
 
-    def close(self):
-        if hasattr(self.engine, "close"):
-            self.engine.close()
+    def wait(self):
+        """Wait for every engine's pending flush (D > 1)."""
+        from concurrent.futures import wait
+        wait([p for p in self._pending if p is not None])
+
+    def close(self, close_engines=True):
+        if self._flushers is not None:
+            self.wait()
+            for x in self._flushers:
+                x.shutdown(wait=True)
+            self._flushers = None
+        if close_engines:
+            for e in self._engines:
+                if hasattr(e, "close"):
+                    e.close()
 
 
 # ---------------------------------------------------------------- Server.Flush (metrics part)
