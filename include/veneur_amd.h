@@ -37,7 +37,14 @@
 extern "C" {
 #endif
 
-#define VN_ABI_VERSION 5
+/* ABI history (vn_abi_version; the binding refuses a library of another version):
+ *   5  vn_config.max_batch_class_records; vn_flush no longer fails when a split key's slot also
+ *      got vn_ingest records or imports -- it drops them, returns VN_OK and sets
+ *      VN_WARN_SPLIT_TOUCHED in vn_flush_result.warn_flags (check it after every flush).
+ *   6  counter records take any sample rate (Counter.Sample's int64(float32(1/rate)) is defined
+ *      for all of them: NaN, 0 and out-of-range reciprocals give MinInt64, as Go on amd64);
+ *      histogram rates must still be in (0, 1] (VN_EINVAL otherwise). */
+#define VN_ABI_VERSION 6
 
 enum {
   VN_OK = 0,

@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
     for s in sorted(syms):
         assert hasattr(A.lib, s), "missing export %s" % s
     assert set(A.EXPORTED) == syms
-    assert A.lib.vn_abi_version() == 5
+    assert A.lib.vn_abi_version() == 6
 
 
 def test_struct_layouts_match_header():

@@ -180,7 +180,7 @@ def _sig(name, res, *args):
 vp = C.c_void_p
 _sig("vn_abi_version", C.c_int)
 _sig("vn_struct_size", C.c_size_t, C.c_int)
-ABI_VERSION = 5
+ABI_VERSION = 6
 _sig("vn_engine_create", C.c_int, C.POINTER(Config), C.POINTER(vp))
 _sig("vn_engine_destroy", None, vp)
 _sig("vn_last_error", C.c_char_p, vp)
