@@ -418,7 +418,9 @@ int vn_split_close(vn_engine* eng);
  * have cleared theirs, and the split lists are empty.  Returns once the exchange is issued
  * (every later operation of the engine is ordered after it); it does not wait for the
  * window's own replays, so engines taking windows in turn can enter their combines in window
- * order without one window's replays holding up the next. */
+ * order without one window's replays holding up the next.  (With an RCCL group; the in-process
+ * group of vn_comm_init_local, a test device, copies between its ranks' buffers and waits for
+ * the counters' stream, which holds only the counter aggregation and the combine itself.) */
 int vn_split_combine(vn_engine* eng);
 
 /* DogStatsD metric lines (host code, no GPU): samplers/parser.go:186-307 ParseMetric over a

@@ -6,8 +6,11 @@
 #   smoke    __graft_entry__.smoke()
 #   bench    the default bench line (python bench.py)
 #   bench1   the bench with one engine (--pipeline 1), windows back to back
+#   benchq   the default bench line without the CPU baseline / parity / C5 / text legs (timing only)
+#   benchqvar  the same with the A/B variant library (VN_LIB=libveneur_amd_variant.so)
 #   prof     rocprofv3 --kernel-trace --stats of a short bench with ONE engine, so every kernel's
 #            duration is its own (no other window's kernels beside it); roofline_check over it
+#   c5       the C5 leg alone (bench.py --c5-only)
 #   c5prof   rocprofv3 --kernel-trace --stats of the C5 leg alone
 #   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) for the replay's HBM traffic
 #   hot      batched-replay parity tests, phase cycles (profiling build) and the 17M-sample key
@@ -34,11 +37,19 @@ for step in "$@"; do
     bench1)
       timeout -k 10 600 python -u bench.py --pipeline 1 --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 \
         --text-lines 0 > ${O}_bench1.json 2> ${O}_bench1.log ;;
+    benchq)
+      timeout -k 10 400 python -u bench.py --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0 \
+        > ${O}_benchq.json 2> ${O}_benchq.log ;;
+    benchqvar)
+      VN_LIB=libveneur_amd_variant.so timeout -k 10 400 python -u bench.py --no-cpu-baseline --pcie-steps 0 \
+        --c5-hosts 0 --text-lines 0 > ${O}_benchqvar.json 2> ${O}_benchqvar.log ;;
     prof)
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/${O}_prof" \
         -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --pipeline 1 $SHORT > "$GRAFT_REPO_ROOT/${O}_prof.log" 2>&1) &&
       python3 tools/roofline_check.py ${O}_prof ${O}_prof.log 1 ${O}_timing_step_kernel_stats.csv \
         > ${O}_roofline_check.txt 2>&1 ;;
+    c5)
+      timeout -k 10 300 python -u bench.py --c5-only > ${O}_c5.json 2> ${O}_c5.log ;;
     c5prof)
       (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/${O}_c5prof" \
         -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --c5-only > "$GRAFT_REPO_ROOT/${O}_c5prof.log" 2>&1) ;;

@@ -1362,7 +1362,11 @@ int vn_copy_to_host(int device, void* dst, const void* src, uint64_t bytes) {
 }
 int vn_device_copy(int device, void* dst, const void* src, uint64_t bytes) {
   if (hipSetDevice(device) != hipSuccess) return VN_EHIP;
-  return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToDevice) == hipSuccess ? VN_OK : VN_EHIP;
+  // a device-to-device hipMemcpy may return before the copy is done, and the null stream it runs
+  // on does not order against the engines' non-blocking streams: the caller may reuse src (an
+  // engine's export buffer) or read dst from an engine stream as soon as this returns, so wait
+  if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, nullptr) != hipSuccess) return VN_EHIP;
+  return hipStreamSynchronize(nullptr) == hipSuccess ? VN_OK : VN_EHIP;
 }
 int vn_device_count(int* n) { return hipGetDeviceCount(n) == hipSuccess ? VN_OK : VN_EHIP; }
 int vn_device_synchronize(int device) {

@@ -1314,8 +1314,9 @@ __device__ __forceinline__ double wave_incl_add_d(double v) {
   v = dadd(v, dpp_d<0x142, 0xa>(v, 0.0));
   return dadd(v, dpp_d<0x143, 0xc>(v, 0.0));
 }
-// mp[0..nm] from the main weights (wave 0); misc[1] = every weight an integer and their sum
-// equal to mainW (then every prefix is exact)
+// mp[0..nm] from the main weights (wave 0); misc[1] = every weight exact (an integer, or a multiple
+// of 2^-23 with a total up to 2^30) and their sum equal to mainW (then every prefix is exact);
+// misc[4] = misc[1] and every weight an integer (the fast paths' totals may then reach 2^40)
 __device__ __noinline__ void prefix_main_w0(const Lds L, const FastLds F, uint32_t nm, double mainW) {
   const uint32_t lane = threadIdx.x & 63;
   double carry = 0.0;
@@ -1341,10 +1342,12 @@ __device__ __noinline__ void prefix_main_w0(const Lds L, const FastLds F, uint32
     if (j < nm) F.mp[j] = dadd(carry, dsub(v, w));
     carry = dadd(carry, rl_d(v, 63));
   }
-  ok = __all(ok) && carry == mainW && mainW <= exact_total_limit(__all(allint));
+  const bool ai = __all(allint);
+  ok = __all(ok) && carry == mainW && mainW <= exact_total_limit(ai);
   if (lane == 0) {
     F.mp[nm] = mainW;
     F.misc[1] = ok ? 1u : 0u;
+    F.misc[4] = ok && ai ? 1u : 0u;
   }
 }
 
@@ -1688,23 +1691,31 @@ __host__ __device__ inline uint32_t fast_offset(uint32_t capc, uint32_t tcap) {
 struct MergeState {
   uint32_t nm;
   double w;
-  bool fok;  // the key's weights are all integers: the fast merge applies
+  bool fok;   // the main weights are exact (integers, or 2^-23 multiples up to 2^30): fast merges apply
+  bool fint;  // ... and all integers: the fast merges' totals may reach 2^40 (else 2^30)
 };
+// The largest total weight a fast merge or a batch takes: sums of 2^-23 multiples are exact in any
+// order only up to 2^30 (is_exact_weight), sums of integers up to 2^40 here (the batch's ranges).
+__device__ __forceinline__ double fast_total_limit(bool all_int) { return all_int ? 1099511627776.0 : 1073741824.0; }
 
 // one mergeAllTemps of the sorted temps sv/sw (with sp when tint): the fast merge when it
 // applies, else wave 0's one-wave merge (out of line) and the main prefix rebuilt after it
+// tint: the temps' weights are exact (prefixes in any order); cint: ... and known to be integers
 template <int NW>
 __device__ __forceinline__ MergeState merge_step(const MergeParams mp, const Lds L, const FastLds F, MwSharedL& S,
-                                                 MergeState st, uint32_t n_, double tempW, bool tint, double k0) {
+                                                 MergeState st, uint32_t n_, double tempW, bool tint, bool cint,
+                                                 double k0) {
   constexpr uint32_t NT = 64 * NW, R = 4 / NW;
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t m = st.nm + n_;
 #ifdef VN_FAST_MERGE_OFF
   if (false) {  // A/B and debugging variant: every merge by wave 0's one-wave merge
 #else
-  if (st.fok && tint && n_ <= 64 && m < NT * R && m <= mp.capc && dadd(st.w, tempW) <= 1099511627776.0) {
+  if (st.fok && tint && n_ <= 64 && m < NT * R && m <= mp.capc &&
+      dadd(st.w, tempW) <= fast_total_limit(st.fint && cint)) {
 #endif
     merge_fast<NW>(mp, L, F, st.nm, st.w, n_, tempW, k0);
+    st.fint = st.fint && cint;  // (a main weight that took a non-integer temp may not be one)
     return st;
   }
   if (wv == 0) {
@@ -1721,18 +1732,21 @@ __device__ __forceinline__ MergeState merge_step(const MergeParams mp, const Lds
     if (wv == 0) prefix_main_w0(L, F, st.nm, st.w);
     fast_sync<NW>();
     st.fok = F.misc[1] != 0u;
+    st.fint = F.misc[4] != 0u;
   } else {
     st.fok = false;
+    st.fint = false;
   }
   fast_sync<NW>();  // S and misc are read before anyone writes them again
   return st;
 }
 template <int NW>
 __device__ __noinline__ MergeState merge_step_cold(const Lds L, ldsf64* fbase, MwSharedL& S, MP_PARAMS, uint32_t st_nm,
-                                                   double st_w, bool st_fok, uint32_t n_, double tempW, bool tint,
-                                                   double k0) {
+                                                   double st_w, bool st_fok, bool st_fint, uint32_t n_, double tempW,
+                                                   bool tint, bool cint, double k0) {
   MP_UNPACK(mp);
-  return merge_step<NW>(mp, L, fast_of(L, fbase), S, MergeState{st_nm, st_w, st_fok}, n_, tempW, tint, k0);
+  return merge_step<NW>(mp, L, fast_of(L, fbase), S, MergeState{st_nm, st_w, st_fok, st_fint}, n_, tempW, tint, cint,
+                        k0);
 }
 
 // ---- batched replay of consecutive pure chunks (the long replays' steady state).
@@ -1782,7 +1796,10 @@ constexpr uint32_t kTopExcl = 8;             // longest batched keys on CUs no o
 constexpr uint32_t kTopSortBlocks = 4096;    // blocks per top key sorting its chunks first (grid-stride)
 constexpr uint32_t kBM = 160;               // most centroids a batch takes (delta 100: ~135)
 constexpr uint32_t kBN = kBM + 1;           // columns + the end
-constexpr uint32_t kBTmax = 48;             // largest temp buffer batched (delta <= ~110)
+#ifndef VN_CHAIN_PRIO
+#define VN_CHAIN_PRIO 0
+#endif
+constexpr uint32_t kBTmax = 42;             // largest temp buffer batched: veneur's delta 100 (samplers.go:364)
 constexpr uint32_t kBMinAvail = 32;         // chunks in the ring below which a batch waits for more
 #ifndef VN_BATCH_MIN_W
 #define VN_BATCH_MIN_W 8192.0
@@ -1961,7 +1978,7 @@ template <int NW>
 __device__ __forceinline__ BatchResult merge_batch(const double delta, const double sin_hi, const double sin_lo,
                                                    const Lds L, const FastLds F, const BatchLds B,
                                                    const uint32_t nm_in, double& mainW, const uint32_t c_in,
-                                                   uint32_t b, const uint32_t tcap) {
+                                                   uint32_t b, const uint32_t tcap, const bool fint) {
   // (wave-uniform values in scalar registers: every chunk address below is then scalar math)
   const uint32_t nm = __builtin_amdgcn_readfirstlane(nm_in), c = __builtin_amdgcn_readfirstlane(c_in);
   constexpr uint32_t NT = 64 * NW;
@@ -1981,13 +1998,14 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   };
   PROF_T(b0);
   // ---- totals: the usable chunks are the leading batchable ones with T <= 2^40 (every prefix
-  // below is then an exact u32 / f64 integer: a chunk's tempW < 2^16, the batch's < 2^22)
+  // below is then an exact u32 / f64 integer: a chunk's tempW < 2^16, the batch's < 2^22), or
+  // T <= 2^30 when some main weight is not an integer (a 2^-23 multiple: sums exact up to 2^30)
   if (wv == 0) {
     const uint32_t tw0 = B.rp[sbase(min(lane, b - 1))], tw = lane < b ? tw0 : 0xffffffffu;
     bool ok = lane < b && tw != 0xffffffffu;
     const uint32_t v = wave_incl_add_u32(ok ? tw >> 16 : 0u);  // (< 2^22: exact)
     const double T = dadd(mainW, (double)v);
-    ok = ok && T <= 1099511627776.0;
+    ok = ok && T <= fast_total_limit(fint);
     const uint64_t bad = __ballot(!ok);
     const uint32_t nb = min(bad ? (uint32_t)__builtin_ctzll(bad) : 64u, b);
     if (lane < b) {
@@ -2024,11 +2042,19 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     const double p0 = L.mm[127], p1 = L.mm[63], p2 = L.mm[191];
     const double p3 = L.mm[31], p4 = L.mm[95], p5 = L.mm[159], p6 = L.mm[223];
     bool safe = true;
+    // (chunk, position) of temp g = t + u * NT: one division, then steps of NT = qs * tcap + rs
+    const uint32_t qs = NT / tcap, rs = NT - qs * tcap;
+    uint32_t jg = t / tcap, pg = t - jg * tcap;
 #pragma unroll
     for (uint32_t u = 0; u < kA; u++) {
       const uint32_t g = t + u * NT;
-      gj[u] = g / tcap;
-      gp[u] = g - gj[u] * tcap;
+      gj[u] = jg;
+      gp[u] = pg;
+      pg += rs;
+      jg += qs;
+      const bool wrap = pg >= tcap;  // (rs < tcap: one step at most)
+      pg = wrap ? pg - tcap : pg;
+      jg = wrap ? jg + 1u : jg;
       const double x = B.rv[sbase(min(gj[u], kBB - 1)) + gp[u]];  // (unconditional: see D)
       gv[u] = g < nt ? x : 0.0;
       safe &= div_safe(gv[u]);
@@ -2111,6 +2137,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   }
   fast_sync<NW>();
   PROF_T(b3);
+  ASM_MARK("C_BEGIN");
   // ---- C.  A column lane holds rows n[.][i] and n[.][i+1] as words (chunks j < b count):
   // the list offset off_i = sum_j n[j][i] (the temps of the columns before it, Z included;
   // column 0 at 0), the K row (a prefix over the chunks of its per-chunk counts), and the k
@@ -2258,6 +2285,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     fast_sync<NW>();
     return BatchResult{0u, true};
   }
+  ASM_MARK("D_BEGIN");
   // ---- D: every temp into its column's list at off_c + K[j][c] + its place in the chunk's run
   // (column 0: Z temps and main 0's own temps, p itself), with its mean and weight
   {
@@ -2295,6 +2323,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   // Columns 1.. on waves 0-2 (lane = column); column 0, whose list also holds the Z temps, on
   // lane 0 of wave 3 beside them: a chunk's Z temps start a fresh centroid (main 0, the column
   // so far, waiting) and main 0 joins it after the chunk's last Z temp.
+  ASM_MARK("E_BEGIN");
   PROF_T(e0);
   const uint32_t nt_all = kBB * tcap;  // the lists' spare slot
   if (wv < 3) {
@@ -2407,6 +2436,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     B.lo[0] = lo;
     B.hi[0] = hi;
   }
+  ASM_MARK("C2Q_BEGIN");
   PROF_T(e1);
   PROF_ADD(14, e0, e1);
   PROF_ADDW(36, e0, e1);
@@ -2415,6 +2445,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   PROF_ADDW(44, e1, e2);
   fast_sync<NW>();
   PROF_T(b6);
+  ASM_MARK("F_BEGIN");
   // ---- F: decisions per temp against the columns' mean ranges (the exact mean merge j saw
   // only for a temp inside a range); bound tests per column
   auto mean_before = [&](uint32_t ci, uint32_t j) {
@@ -2467,6 +2498,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   }
   fast_sync<NW>();
   PROF_T(b7);
+  ASM_MARK("G_BEGIN");
   // ---- G: exact tests of the flagged columns, one wave per column, lane = chunk
   const uint32_t nflag = __builtin_amdgcn_readfirstlane(B.ctl[1]);
   for (uint32_t f = wv; f < nflag; f += NW) {
@@ -2493,6 +2525,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   }
   fast_sync<NW>();
   PROF_T(b8);
+  ASM_MARK("H_BEGIN");
   uint32_t jd = __builtin_amdgcn_readfirstlane(B.ctl[0]);
   const uint32_t jst = __builtin_amdgcn_readfirstlane(B.ctl[3]);
   if (B.ctl[4]) jd = 0;  // (means out of order somewhere: no batch)
@@ -2514,6 +2547,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   }
   fast_sync<NW>();
   PROF_T(b9);
+  ASM_MARK("MB_END");
   PROF_ADD(16, b0, b1);
   PROF_ADD(17, b1, b2);
   PROF_ADD(18, b2, b3);
@@ -2578,7 +2612,8 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
   fast_sync<NW>();
   if (wv == 0) prefix_main_w0(L, F, nm, mainW);
   fast_sync<NW>();
-  bool fok = F.misc[1] != 0u;  // the key's weights are all integers: the fast merge applies
+  bool fok = F.misc[1] != 0u;   // the main weights are exact: the fast merges apply
+  bool fint = F.misc[4] != 0u;  // ... and integers (fast_total_limit)
 
   double sw = 0.0, sxw = 0.0, srw = 0.0, mn = kInf, mx = -kInf, dmn = kInf, dmx = -kInf;
   auto stat = [&](double v, double wt, bool sample) {
@@ -2605,17 +2640,20 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
   };
   // a merge of the sorted temps sv/sw (with sp when tint): the fast merge when it applies, else
   // wave 0's one-wave merge (and the main prefix rebuilt after it)
-  auto merge_sorted_any = [&](uint32_t n_, double tempW, bool tint) {
-    const MergeState r = merge_step<NW>(mp, L, F, S, MergeState{nm, mainW, fok}, n_, tempW, tint, k0);
+  auto merge_sorted_any = [&](uint32_t n_, double tempW, bool tint, bool cint) {
+    const MergeState r = merge_step<NW>(mp, L, F, S, MergeState{nm, mainW, fok, fint}, n_, tempW, tint, cint, k0);
     nm = r.nm;
     mainW = r.w;
     fok = r.fok;
+    fint = r.fint;
   };
   auto merge_sorted_cold = [&](uint32_t n_, double tempW, bool tint) {
-    const MergeState r = merge_step_cold<NW>(L, F.mp, S, MP_ARGS(mp), nm, mainW, fok, n_, tempW, tint, k0);
+    const MergeState r =
+        merge_step_cold<NW>(L, F.mp, S, MP_ARGS(mp), nm, mainW, fok, fint, n_, tempW, tint, false, k0);
     nm = r.nm;
     mainW = r.w;
     fok = r.fok;
+    fint = r.fint;
   };
   auto merge_pend = [&]() {  // sort the pending temps (wave 0), then merge them
     if (wv == 0) {
@@ -2648,6 +2686,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     // imported centroid negative), and in ctw the temps' Add-order weight sum at the first
     // record (negative when a weight is not an integer), their sorted exclusive prefix after it
     double cv = 0.0, cw = 0.0, cp = 0.0, ctw = 0.0;
+    uint32_t ccpk = 0xffffffffu;  // the batched replay's packing of slot 0: not all-ones = integer weights
     auto load = [&](uint32_t c) {
       const uint64_t base = (uint64_t)lo + sp.off0 + (uint64_t)c * tcap;
       if (t < tcap) {
@@ -2656,12 +2695,14 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
         cp = xctw[base + t];
       }
       ctw = xctw[base];
+      ccpk = x.cpk ? x.cpk[base] : 0xffffffffu;
     };
     // chunks [c0, c1) one merge at a time, the next chunk's loads in flight during each merge
     auto singles = [&](uint32_t c0, uint32_t c1) {
       load(c0);
       for (uint32_t c = c0; c < c1; c++) {
-        double tempW = __builtin_fabs(ctw), tintd = ctw >= 0.0 ? 1.0 : 0.0;
+        // 0: some weight not exact; 1: exact; 2: exact and integers
+        double tempW = __builtin_fabs(ctw), tintd = ctw >= 0.0 ? (ccpk != 0xffffffffu ? 2.0 : 1.0) : 0.0;
         if (t < tcap) {
           L.sv[t] = cv;
           L.sw[t] = __builtin_fabs(cw);
@@ -2673,7 +2714,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
         hold_stats(sw, sxw, srw, mn, mx, dmn, dmx);
         if (c + 1 < c1) load(c + 1);
         fast_sync<NW>();
-        merge_sorted_any(tcap, tempW, tintd != 0.0);
+        merge_sorted_any(tcap, tempW, tintd != 0.0, tintd == 2.0);
       }
     };
     if constexpr (!BATCH) {
@@ -2723,6 +2764,11 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       return th * (1.0 - t2 / 6.0 * (1.0 - t2 / 20.0 * (1.0 - t2 / 42.0 * (1.0 - t2 / 72.0))));
     };
     const double sin_hi = sin_small(kPi * (1.0 + kBand) / mp.delta), sin_lo = sin_small(kPi * (1.0 - kBand) / mp.delta);
+#if VN_CHAIN_PRIO
+    // the batched keys are the window's longest chains: their waves win instruction issue over
+    // other kernels' waves sharing their SIMDs (windows in flight put such waves beside them)
+    __builtin_amdgcn_s_setprio(VN_CHAIN_PRIO);
+#endif
     uint32_t ring_lo = 0, ring_hi = 0;  // chunks [ring_lo, ring_hi) are in the ring (or on their way)
     uint32_t c = 0;
     while (c < sp.npure) {
@@ -2757,7 +2803,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       }
       ring_lo = max(c, ring_hi > kRing ? ring_hi - kRing : 0u);
       PROF_T(s0);
-      const BatchResult r = merge_batch<NW>(mp.delta, sin_hi, sin_lo, L, F, Bt, nm, mainW, c, b, tcap);
+      const BatchResult r = merge_batch<NW>(mp.delta, sin_hi, sin_lo, L, F, Bt, nm, mainW, c, b, tcap, fint);
       PROF_T(s1);
       PROF_ADD(27, s0, s1);
       const uint32_t cb_end = c + b;  // (the batch's chunks: landed in the ring)
@@ -2779,7 +2825,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
           }
           if (t == tcap) F.sp[tcap] = (double)(p0 >> 16);
           fast_sync<NW>();
-          merge_sorted_any(tcap, (double)(p0 >> 16), true);
+          merge_sorted_any(tcap, (double)(p0 >> 16), true, true);
         }
         if (cs < c1) singles(cs, c1);
         PROF_T(s2);

@@ -256,6 +256,14 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
   bool have = false;
   int floats = 0;
   int64_t cnt = 0;
+  // EMIT: the centroids go out eight at a time from a register queue.  On gfx950 one counter
+  // (vmcnt) tracks loads and stores in issue order, so the wait for the reader's next block
+  // also waits for every store issued before that block's load: with a store per centroid the
+  // reader stalled on store latency every 16 bytes (the emit pass ran ~5x slower than the count
+  // pass over the same bytes); batched, it stalls once per eight centroids
+  constexpr int kQ = 8;
+  double qm[kQ], qw[kQ];
+  int nq = 0;
   while (r.i < r.n && floats < 3) {
     const uint64_t mlen = r.u();
     if (r.err || mlen > r.n - r.i) return -1;
@@ -291,13 +299,36 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
             else gob_skip(r, T, T.fid[f]);
           }
           if (EMIT) {
-            mean[cnt] = m;
-            w[cnt] = wt;
-            oslot[cnt] = slot;
+#pragma unroll
+            for (int q = 0; q < kQ - 1; q++) {
+              qm[q] = qm[q + 1];
+              qw[q] = qw[q + 1];
+            }
+            qm[kQ - 1] = m;
+            qw[kQ - 1] = wt;
+            if (++nq == kQ) {  // centroids cnt - 7 .. cnt
+#pragma unroll
+              for (int q = 0; q < kQ; q++) {
+                mean[cnt - (kQ - 1) + q] = qm[q];
+                w[cnt - (kQ - 1) + q] = qw[q];
+                oslot[cnt - (kQ - 1) + q] = slot;
+              }
+              nq = 0;
+            }
           } else if (d_isnan(m) || d_isinf(m) || wt <= 0.0) {
             return -1;  // Merge's Add would panic (merging_digest.go:98-100)
           }
           cnt++;
+        }
+        if (EMIT) {  // the queue's last nq centroids: cnt - nq .. cnt - 1
+#pragma unroll
+          for (int q = 0; q < kQ; q++)
+            if (q >= kQ - nq) {
+              mean[cnt - kQ + q] = qm[q];
+              w[cnt - kQ + q] = qw[q];
+              oslot[cnt - kQ + q] = slot;
+            }
+          nq = 0;
         }
         have = true;
       } else {

@@ -5,7 +5,9 @@
 // is a wrapping int64 sum, so any grouping of the adds is bit-exact.  Gauge.Sample
 // (198-200) keeps the last write in arrival order.
 //
-// Counters: k_scalar_direct -- each block hashes a 16384-record chunk of the batch into an LDS
+// Counters (default): a key-range partition pass writing one packed dword per record (KPackDst),
+// then k_counter_runs sums each bucket run in LDS.  (k_scalar_direct, the former path: each
+// block hashes a 16384-record chunk of the batch into an LDS
 // table keyed by slot (wrapping i64 sums), then one device atomic per entry; a record that finds no
 // free entry within 8 probes adds to its device word directly.
 // Gauges avoid per-record device atomics (a Zipf-hot key would serialise them):
@@ -187,6 +189,29 @@ constexpr uint64_t kRunChunk = 131072;
 constexpr uint32_t kRunMaxW = 4096;  // slots per bucket (LDS: 8 B + 1 B each)
 constexpr int kRunUnroll = 4;
 
+// The partition pass writes each counter record as ONE dword: the slot's low `shift` bits (its
+// place in the bucket; the bucket is the record's run) and the record's contribution
+// int64(v) * int64(float32(1/rate)) as a two's-complement field in the other 32 - shift bits.  A
+// contribution outside the field (or equal to its minimum, the escape) is stored whole in the
+// payload array at the same position: 4 B per record written and read back instead of 12, the
+// 8-byte payload only for the rare large ones.
+struct KPackDst {
+  uint32_t* key;
+  uint64_t* pay;
+  int shift;
+  __device__ __forceinline__ void store(uint64_t pos, uint32_t k, uint64_t p) const {
+    const int fb = 32 - shift;
+    const int64_t v = (int64_t)p, lim = (int64_t)1 << (fb - 1);
+    const uint32_t lowk = shift ? k & ((1u << shift) - 1u) : 0u;
+    if (v > -lim && v < lim) {
+      key[pos] = lowk | ((uint32_t)v << shift);
+    } else {
+      key[pos] = lowk | ((uint32_t)lim << shift);  // (the field's minimum: escape)
+      pay[pos] = p;
+    }
+  }
+};
+
 __global__ __launch_bounds__(kRunThreads) void k_counter_runs(uint64_t n, const uint32_t* __restrict__ pk,
                                                               const uint64_t* __restrict__ pp,
                                                               const uint32_t* __restrict__ offsets, uint32_t nparts,
@@ -195,10 +220,25 @@ __global__ __launch_bounds__(kRunThreads) void k_counter_runs(uint64_t n, const 
   __shared__ unsigned long long s_sum[kRunMaxW];
   __shared__ uint8_t s_hit[kRunMaxW];
   const uint32_t W = 1u << shift, t = threadIdx.x;
+  const int32_t esc = (int32_t)(0u - (1u << (31 - shift)));  // KPackDst's escape field
+  // one packed record (KPackDst): its slot within the bucket and its contribution
+  auto unpack = [&](uint64_t r, uint32_t& k, uint64_t& p) {
+    const uint32_t x = pk[r];
+    const int32_t f = (int32_t)x >> shift;
+    k = x & (W - 1u);
+    p = f == esc ? pp[r] : (uint64_t)(int64_t)f;
+  };
   const uint64_t c0 = (uint64_t)blockIdx.x * kRunChunk, c1 = min(n, c0 + kRunChunk);
   for (uint64_t i = c0; i < c1;) {
-    // the bucket of record i and where its run ends in this slice (every thread alike)
-    const uint32_t d = pk[i] >> shift;
+    // the bucket of record i -- the last bucket starting at or before it -- and where its run
+    // ends in this slice (every thread alike)
+    uint32_t lo = 0, hi = 256;
+    while (hi - lo > 1) {
+      const uint32_t m = (lo + hi) >> 1;
+      if ((uint64_t)offsets[(uint64_t)m * nparts] <= i) lo = m;
+      else hi = m;
+    }
+    const uint32_t d = lo;
     const uint64_t e = min(c1, (uint64_t)offsets[(uint64_t)(d + 1) * nparts]);
     for (uint32_t j = t; j < W; j += kRunThreads) {
       s_sum[j] = 0;
@@ -210,10 +250,7 @@ __global__ __launch_bounds__(kRunThreads) void k_counter_runs(uint64_t n, const 
       uint32_t k[kRunUnroll];
       uint64_t p[kRunUnroll];
 #pragma unroll
-      for (int u = 0; u < kRunUnroll; u++) {
-        k[u] = pk[r + u * kRunThreads] & (W - 1);
-        p[u] = pp[r + u * kRunThreads];
-      }
+      for (int u = 0; u < kRunUnroll; u++) unpack(r + u * kRunThreads, k[u], p[u]);
 #pragma unroll
       for (int u = 0; u < kRunUnroll; u++) {
         atomicAdd(&s_sum[k[u]], (unsigned long long)p[u]);
@@ -221,8 +258,10 @@ __global__ __launch_bounds__(kRunThreads) void k_counter_runs(uint64_t n, const 
       }
     }
     for (; r < e; r += kRunThreads) {
-      const uint32_t k = pk[r] & (W - 1);
-      atomicAdd(&s_sum[k], (unsigned long long)pp[r]);
+      uint32_t k;
+      uint64_t p;
+      unpack(r, k, p);
+      atomicAdd(&s_sum[k], (unsigned long long)p);
       s_hit[k] = 1;
     }
     __syncthreads();
@@ -273,7 +312,8 @@ void ingest_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const doubl
   if (kCounterRuns && (1u << shift) <= kRunMaxW) {
     RadixStats* rs = e->timing ? &e->rstat_c : nullptr;
     const uint32_t nparts =
-        partition_pass(CounterSrc{slot, val, rate}, KV64Dst{e->pk, e->pp}, n, shift, *e->side_rs, e->side, rs, 16 + 12);
+        partition_pass(CounterSrc{slot, val, rate}, KPackDst{e->pk, e->pp, shift}, n, shift, *e->side_rs, e->side, rs,
+                       16 + 4);
     hipLaunchKernelGGL(k_counter_runs, dim3((uint32_t)((n + kRunChunk - 1) / kRunChunk)), dim3(kRunThreads), 0,
                        e->side, n, e->pk, e->pp, e->side_rs->offsets, nparts, shift, (uint64_t*)e->cval, e->ctouch);
     return;

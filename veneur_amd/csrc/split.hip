@@ -227,14 +227,9 @@ __global__ void k_sc_scatter(uint32_t n, const uint32_t* __restrict__ slot, cons
   touch[slot[i]] = own ? t[i] : 0u;
 }
 
-// the owner list on the device (kSCtrOwn), the host list free to change when this returns
-void split_counter_owners(vn_engine* e, hipStream_t st) {
-  SplitState& S = e->sp;
-  const uint32_t H = (uint32_t)S.slot[VN_COUNTER].size();
-  if (!H) return;
-  to_dev(sbuf<uint32_t>(e, kSCtrOwn, H), S.owner[VN_COUNTER].data(), H, st);
-  VN_HIP_CHECK(hipStreamSynchronize(st));
-}
+// the owner list is on the device since vn_split_keys (kSCtrOwn): nothing to copy or wait for at
+// flush, so vn_split_combine returns once the exchange is issued
+void split_counter_owners(vn_engine*, hipStream_t) {}
 void split_counters(vn_engine* e, vn_comm* c, hipStream_t st) {
   SplitState& S = e->sp;
   const uint32_t H = (uint32_t)S.slot[VN_COUNTER].size();
@@ -1394,9 +1389,13 @@ int vn_split_keys(vn_engine* e, int cls, const uint32_t* slot, const uint32_t* o
       VN_HIP_CHECK(hipMalloc(&S.d_slot[cls], n * sizeof(uint32_t)));
       S.d_cap[cls] = n;
     }
-    // (on the engine's stream, not the null stream: see check_error_flags)
+    // (on the engine's stream, not the null stream: see check_error_flags); the split counters'
+    // owners go to the device here too, so the flush's combine issues no host copy or wait
     if (n) {
       VN_HIP_CHECK(hipMemcpyAsync(S.d_slot[cls], slot, n * sizeof(uint32_t), hipMemcpyHostToDevice, e->st));
+      if (cls == VN_COUNTER)
+        VN_HIP_CHECK(hipMemcpyAsync(sbuf<uint32_t>(e, kSCtrOwn, n), owner, n * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                    e->st));
       VN_HIP_CHECK(hipStreamSynchronize(e->st));
     }
   });
