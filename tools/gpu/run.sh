@@ -14,6 +14,8 @@
 #   c5prof   rocprofv3 --kernel-trace --stats of the C5 leg alone
 #   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) for the replay's HBM traffic
 #   hot      batched-replay parity tests, phase cycles (profiling build) and the 17M-sample key
+#   short    the one-wave replay's throughput (20k keys of 6000 samples, C5's per-drain size)
+#            with this build and with the A/B variant library; then 64 such keys checked
 # Each step runs under its own time limit; the first failure, fault, abort or timeout ends
 # the call (no retries).
 set -o pipefail
@@ -65,6 +67,11 @@ for step in "$@"; do
         > ${O}_hot_tests.log 2>&1 &&
       VN_LIB=libveneur_amd_prof.so timeout -k 10 120 python -u tools/exact_profile.py 4000000 > ${O}_hot_prof.log 2>&1 &&
       timeout -k 10 300 python -u tools/hot_replay_bench.py --n 17000000 --keys 1 --rates --reps 2 > ${O}_hot_17M.log 2>&1 ;;
+    short)
+      H="tools/hot_replay_bench.py --n 6000 --keys 1 --cold-keys 20000 --cold-n 6000 --no-check --reps 3"
+      timeout -k 10 200 python -u $H > ${O}_short.log 2>&1 &&
+      VN_LIB=libveneur_amd_variant.so timeout -k 10 200 python -u $H > ${O}_short_var.log 2>&1 &&
+      timeout -k 10 200 python -u tools/hot_replay_bench.py --n 6000 --keys 64 --reps 1 > ${O}_short_check.log 2>&1 ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

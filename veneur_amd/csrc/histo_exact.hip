@@ -36,8 +36,9 @@ __host__ __device__ inline size_t exact_smem_bytes_hd(uint32_t capc, uint32_t tc
   uint32_t levels = 1;
   while ((1u << levels) <= capc) levels++;
   const uint32_t kin = JW <= 2 * capc ? 0 : JW;  // lds_layout: kin in the main tile when it fits
-  return sizeof(double) * (2 * capc + 4 * TP + 2 * JW + kin) + sizeof(uint16_t) * JW +
-         sizeof(uint16_t) * (levels > 9u ? levels : 9u) * JW + 16 + VN_EXACT_LDS_PAD;
+  (void)levels;
+  return sizeof(double) * (2 * capc + 4 * TP + 2 * JW + kin) + sizeof(uint16_t) * JW + sizeof(uint16_t) * 2 * JW + 16 +
+         VN_EXACT_LDS_PAD;
 }
 
 #ifdef VN_ASM_MARK  // (reading the assembly: a comment at a phase boundary)
@@ -267,7 +268,7 @@ struct Lds {
   ldsf64 *tv, *tw;        // pending temps in Add order [TP]
   ldsf64 *sv, *sw;        // sorted temps of the merge being done [TP]
   ldsf64 *gm, *gw, *kin;  // merged elements [JW]
-  ldsu16* jump16;         // next-start tables, levels x [JW] u16 (entries <= JW < 65536)
+  ldsu16* jump16;         // next-start tables next^(2^lv), two [JW] u16 in turn (entries <= JW < 65536)
   ldsu16* starts;         // [JW]
   uint32_t JW, levels;
 };
@@ -464,9 +465,10 @@ __device__ __noinline__ NmW merge_sorted(const Lds L, MP_PARAMS, const uint32_t 
   PROF_T(p2);
   // ---- greedy chain of mergeOne (210-236).  A centroid starting at element s ends before
   // next(s) = the first j > s with k_j - k_{s-1} > 1 (k_{-1} = k(0)).  next() depends on s
-  // alone, so the starts 0, next(0), next(next(0)), ... follow by pointer doubling.  The
-  // binary search needs k monotone; a non-monotone k (ulp-level asin wiggle) takes the
-  // sequential walk instead, so the result is always the reference's.
+  // alone, so the starts 0, next(0), next(next(0)), ... follow by pointer doubling: the starts
+  // t < 2^lv extend to t < 2^(lv+1) through the table of next^(2^lv), squared beside them (two
+  // tables in turn).  The binary search needs k monotone; a non-monotone k (ulp-level asin
+  // wiggle) takes the sequential walk instead, so the result is always the reference's.
   const double k0 = index_estimate(x.delta, 0.0);
   bool mono = true;
   for (uint32_t j = lane + 1; j < m; j += 64) mono &= !(L.kin[j] < L.kin[j - 1]);
@@ -490,20 +492,20 @@ __device__ __noinline__ NmW merge_sorted(const Lds L, MP_PARAMS, const uint32_t 
       }
       J0[s] = (uint16_t)r;
     }
+    if (lane == 0) L.starts[0] = 0;
     wave_lds_sync();
-    for (uint32_t lv = 1; lv < L.levels; lv++) {
-      const ldsu16* Jp = L.jump16 + (lv - 1) * L.JW;
-      ldsu16* Jl = L.jump16 + lv * L.JW;
-      for (uint32_t s = lane; s <= m; s += 64) Jl[s] = (uint16_t)Jp[Jp[s]];
+    // start t = next^t(0) for t <= capc (2^levels > capc); entries past the chain's end are m
+    for (uint32_t lv = 0; lv < L.levels; lv++) {
+      const uint32_t h = 1u << lv;
+      const ldsu16* Jc = L.jump16 + (lv & 1u) * L.JW;
+      ldsu16* Jn = L.jump16 + ((lv & 1u) ^ 1u) * L.JW;
+      for (uint32_t t = h + lane; t < 2 * h && t <= capc; t += 64) L.starts[t] = Jc[L.starts[t - h]];
+      if (lv + 1 < L.levels)
+        for (uint32_t s = lane; s <= m; s += 64) Jn[s] = Jc[Jc[s]];
       wave_lds_sync();
     }
-    // start t = next^t(0), composed from the power-of-two tables; t <= capc
     for (uint32_t t = lane; t <= capc; t += 64) {
-      uint32_t p = 0;
-      for (uint32_t lv = 0; lv < L.levels && p < m; lv++)
-        if ((t >> lv) & 1u) p = L.jump16[lv * L.JW + p];
-      const bool on = p < m;
-      if (on && t < capc) L.starts[t] = p;
+      const bool on = L.starts[t] < m;
       nc += (uint32_t)__popcll(__ballot(on));
       overflow |= on && t == capc;
     }
@@ -560,6 +562,24 @@ __device__ __noinline__ NmW merge_sorted(const Lds L, MP_PARAMS, const uint32_t 
   return NmW{nc, T};
 }
 
+// a double from another lane by DPP (two dword moves); lanes without a source take ident
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_d(double v, double ident) {
+  const uint64_t b = (uint64_t)__double_as_longlong(v), z = (uint64_t)__double_as_longlong(ident);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)z, (int)(uint32_t)b, CTRL, RM, 0xf, false);
+  const uint32_t hi =
+      (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(z >> 32), (int)(uint32_t)(b >> 32), CTRL, RM, 0xf, false);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+// inclusive sum over the wave's 64 lanes (row shifts, then the row broadcasts of lanes 15 and 31)
+__device__ __forceinline__ double wave_incl_add_d(double v) {
+  v = dadd(v, dpp_d<0x111, 0xf>(v, 0.0));
+  v = dadd(v, dpp_d<0x112, 0xf>(v, 0.0));
+  v = dadd(v, dpp_d<0x114, 0xf>(v, 0.0));
+  v = dadd(v, dpp_d<0x118, 0xf>(v, 0.0));
+  v = dadd(v, dpp_d<0x142, 0xa>(v, 0.0));
+  return dadd(v, dpp_d<0x143, 0xc>(v, 0.0));
+}
 // Same merge, written branch-free for a lone wave: every per-lane loop is unrolled over kR
 // rounds with fixed trip counts, clamped indices and selects, so the independent LDS loads of
 // all rounds issue back to back instead of one exec-masked round at a time.
@@ -644,12 +664,18 @@ __device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds
     }
     wint = __all(wex) && T <= exact_total_limit(__all(wint));  // (sums exact in any order)
     if (wint) {
+      // DPP row shifts when every lane is active (see prefix_main_w0), else lane shuffles
+      if (__builtin_amdgcn_read_exec() == ~0ull) {
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
+        for (int r = 0; r < kR; r++) w[r] = wave_incl_add_d(w[r]);
+      } else {
 #pragma unroll
-        for (int r = 0; r < kR; r++) {
-          const double o = __shfl_up(w[r], d, 64);
-          w[r] = (int)lane >= d ? dadd(w[r], o) : w[r];
+        for (int d = 1; d < 64; d <<= 1) {
+#pragma unroll
+          for (int r = 0; r < kR; r++) {
+            const double o = __shfl_up(w[r], d, 64);
+            w[r] = (int)lane >= d ? dadd(w[r], o) : w[r];
+          }
         }
       }
       double carry = 0.0;
@@ -736,35 +762,42 @@ __device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds
     wave_lds_sync();
     PROF_T(cq2);
     PROF_ADD(10, cq1, cq2);
-    uint32_t levels = 1;  // t < 64 * kR needs bits 0 .. levels-1
-    while ((1u << levels) < 64u * kR) levels++;
-    for (uint32_t lv = 1; lv < levels; lv++) {
-      const ldsu16* Jp = L.jump16 + (lv - 1) * L.JW;
-      ldsu16* Jl = L.jump16 + lv * L.JW;
-      uint32_t a[kR];
+    // start t = next^t(0) for this lane's t = 64 r + lane, in registers: step lv extends the
+    // starts t < 2^lv to t < 2^(lv+1) through the table of next^(2^lv) (t - 2^lv: a lane of
+    // round 0 below, or this lane of an earlier round), and squares that table into the other
+    constexpr int kLevels = kLogR;  // 2^kLevels >= 64 kR
+    uint32_t p[kR];
 #pragma unroll
-      for (int r = 0; r < kR; r++) a[r] = Jp[cur[r]];  // J_lv[s] = J_(lv-1)[J_(lv-1)[s]]
+    for (int r = 0; r < kR; r++) p[r] = 0;
 #pragma unroll
-      for (int r = 0; r < kR; r++) {
-        Jl[64 * r + lane] = (uint16_t)a[r];
-        cur[r] = a[r];
+    for (int lv = 0; lv < kLevels; lv++) {
+      const ldsu16* Jc = L.jump16 + (lv & 1) * L.JW;
+      ldsu16* Jn = L.jump16 + ((lv & 1) ^ 1) * L.JW;
+      if (lv < 6) {
+        const uint32_t h = 1u << lv;
+        const uint32_t src = (uint32_t)__shfl_up((int)p[0], h, 64);
+        const uint32_t nx = Jc[src];
+        p[0] = (lane >= h && lane < 2 * h) ? nx : p[0];
+      } else {
+        const int hr = 1 << (lv - 6);  // rounds hr .. 2 hr - 1 from rounds 0 .. hr - 1
+#pragma unroll
+        for (int r = 0; r < kR; r++)
+          if (r >= hr && r < 2 * hr) p[r] = Jc[p[r >= hr ? r - hr : 0]];
+      }
+      if (lv + 1 < kLevels) {
+        uint32_t a[kR];
+#pragma unroll
+        for (int r = 0; r < kR; r++) a[r] = Jc[cur[r]];
+#pragma unroll
+        for (int r = 0; r < kR; r++) {
+          Jn[64 * r + lane] = (uint16_t)a[r];
+          cur[r] = a[r];
+        }
       }
       wave_lds_sync();
     }
     PROF_T(cq3);
     PROF_ADD(11, cq2, cq3);
-    uint32_t p[kR];
-#pragma unroll
-    for (int r = 0; r < kR; r++) p[r] = 0;
-    for (uint32_t lv = 0; lv < levels; lv++) {
-      const ldsu16* J = L.jump16 + lv * L.JW;
-#pragma unroll
-      for (int r = 0; r < kR; r++) {
-        const uint32_t t = 64 * r + lane;
-        const uint32_t nx = J[p[r]];
-        p[r] = ((t >> lv) & 1u) ? nx : p[r];
-      }
-    }
 #pragma unroll
     for (int r = 0; r < kR; r++) {
       const uint32_t t = 64 * r + lane;
@@ -1296,24 +1329,6 @@ __device__ __noinline__ void walk_flags(const FastLds F, uint32_t m, double k0) 
   }
 }
 
-// a double from another lane by DPP (two dword moves); lanes without a source take ident
-template <int CTRL, int RM>
-__device__ __forceinline__ double dpp_d(double v, double ident) {
-  const uint64_t b = (uint64_t)__double_as_longlong(v), z = (uint64_t)__double_as_longlong(ident);
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)z, (int)(uint32_t)b, CTRL, RM, 0xf, false);
-  const uint32_t hi =
-      (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(z >> 32), (int)(uint32_t)(b >> 32), CTRL, RM, 0xf, false);
-  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-// inclusive sum over the wave's 64 lanes (row shifts, then the row broadcasts of lanes 15 and 31)
-__device__ __forceinline__ double wave_incl_add_d(double v) {
-  v = dadd(v, dpp_d<0x111, 0xf>(v, 0.0));
-  v = dadd(v, dpp_d<0x112, 0xf>(v, 0.0));
-  v = dadd(v, dpp_d<0x114, 0xf>(v, 0.0));
-  v = dadd(v, dpp_d<0x118, 0xf>(v, 0.0));
-  v = dadd(v, dpp_d<0x142, 0xa>(v, 0.0));
-  return dadd(v, dpp_d<0x143, 0xc>(v, 0.0));
-}
 // mp[0..nm] from the main weights (wave 0); misc[1] = every weight exact (an integer, or a multiple
 // of 2^-23 with a total up to 2^30) and their sum equal to mainW (then every prefix is exact);
 // misc[4] = misc[1] and every weight an integer (the fast paths' totals may then reach 2^40)
@@ -1357,10 +1372,14 @@ __device__ __noinline__ void prefix_temps_w0(const Lds L, const FastLds F, uint3
   const double w = lane < np ? L.sw[lane] : 0.0;
   const bool allint = __all(is_int_weight(w)), ex = __all(is_exact_weight(w));
   double v = w;
+  if (__builtin_amdgcn_read_exec() == ~0ull) {
+    v = wave_incl_add_d(w);
+  } else {
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const double o = __shfl_up(v, d, 64);
-    v = (int)lane >= d ? dadd(v, o) : v;
+    for (int d = 1; d < 64; d <<= 1) {
+      const double o = __shfl_up(v, d, 64);
+      v = (int)lane >= d ? dadd(v, o) : v;
+    }
   }
   const double tot = rl_d(v, 63);
   const bool ok = ex && tot <= exact_total_limit(allint);
