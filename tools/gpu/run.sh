@@ -7,11 +7,14 @@
 #   bench    the default bench line (python bench.py)
 #   bench1   the bench with one engine (--pipeline 1), windows back to back
 #   benchq   the default bench line without the CPU baseline / parity / C5 / text legs (timing only)
+#   benchq4  benchq with four engines
 #   benchqvar  the same with the A/B variant library (VN_LIB=libveneur_amd_variant.so)
 #   prof     rocprofv3 --kernel-trace --stats of a short bench with ONE engine, so every kernel's
 #            duration is its own (no other window's kernels beside it); roofline_check over it
 #   c5       the C5 leg alone (bench.py --c5-only)
-#   c5prof   rocprofv3 --kernel-trace --stats of the C5 leg alone
+#   c5prof   rocprofv3 --kernel-trace --stats of the C5 leg alone (16 hardware queues, as bench.py sets)
+#   c5prof4  the same with HIP's default 4 hardware queues
+#   c5profvar / c5var  the C5 leg with the A/B variant library, under the profiler / alone
 #   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) for the replay's HBM traffic
 #   hot      batched-replay parity tests, phase cycles (profiling build) and the 17M-sample key
 #   short    the one-wave replay's throughput (20k keys of 6000 samples, C5's per-drain size)
@@ -42,6 +45,9 @@ for step in "$@"; do
     benchq)
       timeout -k 10 400 python -u bench.py --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0 \
         > ${O}_benchq.json 2> ${O}_benchq.log ;;
+    benchq4)
+      timeout -k 10 400 python -u bench.py --pipeline 4 --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0 \
+        > ${O}_benchq4.json 2> ${O}_benchq4.log ;;
     benchqvar)
       VN_LIB=libveneur_amd_variant.so timeout -k 10 400 python -u bench.py --no-cpu-baseline --pcie-steps 0 \
         --c5-hosts 0 --text-lines 0 > ${O}_benchqvar.json 2> ${O}_benchqvar.log ;;
@@ -50,10 +56,22 @@ for step in "$@"; do
         -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --pipeline 1 $SHORT > "$GRAFT_REPO_ROOT/${O}_prof.log" 2>&1) &&
       python3 tools/roofline_check.py ${O}_prof ${O}_prof.log 1 ${O}_timing_step_kernel_stats.csv \
         > ${O}_roofline_check.txt 2>&1 ;;
+    c5prof4)
+      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/${O}_c5prof4" \
+        -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --c5-only > "$GRAFT_REPO_ROOT/${O}_c5prof4.log" 2>&1) ;;
+    c5profvar)
+      (cd /tmp && VN_LIB=libveneur_amd_variant.so timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv \
+        -d "$GRAFT_REPO_ROOT/${O}_c5profvar" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --c5-only \
+        > "$GRAFT_REPO_ROOT/${O}_c5profvar.log" 2>&1) ;;
+    c5var)
+      VN_LIB=libveneur_amd_variant.so timeout -k 10 300 python -u bench.py --c5-only > ${O}_c5var.json 2> ${O}_c5var.log ;;
     c5)
       timeout -k 10 300 python -u bench.py --c5-only > ${O}_c5.json 2> ${O}_c5.log ;;
     c5prof)
-      (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/${O}_c5prof" \
+      # (bench.py sets GPU_MAX_HW_QUEUES=16 before HIP starts, but under the profiler HIP is up before
+      # bench.py runs: with the default 4 queues the engine's streams share hardware queues, and a
+      # CU-masked stream's mask then holds the replays sharing its queue)
+      (cd /tmp && GPU_MAX_HW_QUEUES=16 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/${O}_c5prof" \
         -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --c5-only > "$GRAFT_REPO_ROOT/${O}_c5prof.log" 2>&1) ;;
     pmc)
       A="--steps 1 --warmup 0 --timing-steps 1 --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0 --parity-keys 64"

@@ -114,7 +114,10 @@ void create_impl(vn_engine* e) {
     // columns of every XCC, as above)
     for (uint32_t i = 0; i < ncu * VN_REPLAY_EIGHTHS / 8; i++) rmask[i / 32] |= 1u << (i % 32);
     e->side_cus = ncu - ncu / 4;
-    if (ncu < 64 || hipExtStreamCreateWithCUMask(&e->st2, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
+#ifndef VN_NO_CU_MASK
+#define VN_NO_CU_MASK 0  // (build knob: every stream unmasked -- the profiling runs of DESIGN.md §8)
+#endif
+    if (VN_NO_CU_MASK || ncu < 64 || hipExtStreamCreateWithCUMask(&e->st2, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&e->st3, (uint32_t)rmask.size(), rmask.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&e->st5, (uint32_t)rmask.size(), rmask.data()) != hipSuccess) {
       (void)hipGetLastError();
@@ -385,9 +388,14 @@ void ensure_import(vn_engine* e, uint64_t n, uint64_t nbytes) {
   }
   if (!s.cap_cent) {
     s.cap_cent = e->max_cls[VN_HISTO];  // the drains ingest them as histo records
-    dalloc(s.cslot, s.cap_cent);
     dalloc(s.cmean, s.cap_cent);
     dalloc(s.cw, s.cap_cent);
+    s.cap_pay = e->max_records;  // payloads of one import call, at most
+    dalloc(s.pslot, s.cap_pay);
+    dalloc(s.pbeg, s.cap_pay + 1);
+    dalloc(s.pkey, 2 * s.cap_pay);
+    dalloc(s.pcnt, s.cap_pay + 1);
+    dalloc(s.pdst, s.cap_pay + 1);
   }
 }
 
@@ -474,6 +482,7 @@ void destroy_impl(vn_engine* e) {
   hfree(xb.h_bytes);
   ImportScratch& is = e->imp;
   dfree(is.in_slot); dfree(is.in_off); dfree(is.in_bytes); dfree(is.cnt); dfree(is.coff); dfree(is.cslot);
+  dfree(is.pslot); dfree(is.pbeg); dfree(is.pkey); dfree(is.pcnt); dfree(is.pdst);
   dfree(is.cmean); dfree(is.cw);
   if (is.parts) (void)hipFree(is.parts);
   DeviceBatch& d = e->dstage;

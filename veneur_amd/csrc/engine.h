@@ -37,6 +37,13 @@ struct ImportScratch {
   double* cmean = nullptr;
   double* cw = nullptr;
   uint64_t acc = 0;               // imported histo centroids appended, not yet merged (import_histo.hip)
+  // the run's payloads in arrival order (the drain groups them by key, not their centroids)
+  uint64_t cap_pay = 0, npay = 0;
+  uint32_t* pslot = nullptr;      // [cap_pay] slot
+  uint32_t* pbeg = nullptr;       // [cap_pay + 1] first centroid in the run (pbeg[npay] = acc at the drain)
+  uint64_t* pkey = nullptr;       // [2 cap_pay] (slot << 32 | payload) sort keys, two buffers
+  uint32_t* pcnt = nullptr;       // [cap_pay + 1] centroids per payload in key order
+  uint32_t* pdst = nullptr;       // [cap_pay + 1] their exclusive scan: each payload's place
 };
 
 // Export results (vn_export_histos / vn_export_sets): engine-owned, valid until the next export.

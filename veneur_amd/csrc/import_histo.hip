@@ -249,8 +249,7 @@ __device__ __forceinline__ void gob_skip(GobIn& r, const GobTypes& T, int64_t ti
 // One GobEncode()d MergingDigest ([]Centroid, then compression, min, max as float64):
 // the number of centroids, written to mean/w when EMIT; -1 if the stream is malformed.
 template <bool EMIT>
-__device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double* w, uint32_t* oslot = nullptr,
-                              uint32_t slot = 0) {
+__device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double* w) {
   GobIn r(d, n);
   GobTypes T;
   bool have = false;
@@ -311,7 +310,6 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
               for (int q = 0; q < kQ; q++) {
                 mean[cnt - (kQ - 1) + q] = qm[q];
                 w[cnt - (kQ - 1) + q] = qw[q];
-                oslot[cnt - (kQ - 1) + q] = slot;
               }
               nq = 0;
             }
@@ -326,7 +324,6 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
             if (q >= kQ - nq) {
               mean[cnt - kQ + q] = qm[q];
               w[cnt - kQ + q] = qw[q];
-              oslot[cnt - kQ + q] = slot;
             }
           nq = 0;
         }
@@ -360,17 +357,52 @@ __global__ void k_gob_count(uint64_t n, const uint32_t* __restrict__ slot, uint3
   }
 }
 
+// the centroids of payloads 0..n-1 appended to the run at base + coff[i]; each payload's slot and
+// first centroid into the run's payload table at pb + i
 __global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
                            const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff, uint64_t base,
-                           uint32_t* __restrict__ oslot, double* __restrict__ omean, double* __restrict__ ow,
-                           uint32_t* __restrict__ err) {
+                           double* __restrict__ omean, double* __restrict__ ow, uint32_t* __restrict__ pslot,
+                           uint32_t* __restrict__ pbeg, uint64_t pb, uint32_t* __restrict__ err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t o = base + coff[i];
+  pslot[pb + i] = slot[i];
+  pbeg[pb + i] = (uint32_t)o;
   // k_gob_count validated the payload (every centroid a valid Add), so this pass only writes
-  const int64_t c = gob_digest<true>(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), omean + o, ow + o,
-                                     oslot + o, slot[i]);
+  const int64_t c = gob_digest<true>(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), omean + o, ow + o);
   if (c < 0) atomicOr(err, kErrDecode);
+}
+
+// ---- the drain's grouping: payloads sorted by key (stable), then their centroids moved
+__global__ void k_pay_keys(uint64_t n, const uint32_t* __restrict__ pslot, uint64_t* __restrict__ key,
+                           uint32_t* __restrict__ pbeg, uint32_t total) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) key[i] = ((uint64_t)pslot[i] << 32) | i;
+  if (i == 0) pbeg[n] = total;  // (the end of the last payload)
+}
+__global__ void k_pay_counts(uint64_t n, const uint64_t* __restrict__ key, const uint32_t* __restrict__ pbeg,
+                             uint32_t* __restrict__ cnt) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = (uint32_t)key[i];
+  cnt[i] = pbeg[p + 1] - pbeg[p];
+}
+// one wave per payload in key order: its centroids as grouped histo records (A = mean bits,
+// B = slot << 32 | kTagImport | run index, the record k_histo_keys_raw makes of an import)
+__global__ __launch_bounds__(256) void k_pay_move(uint64_t n, const uint64_t* __restrict__ key,
+                                                  const uint32_t* __restrict__ pbeg, const uint32_t* __restrict__ dst,
+                                                  const double* __restrict__ mean, uint64_t* __restrict__ A,
+                                                  uint64_t* __restrict__ B) {
+  const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t k = key[i];
+  const uint32_t p = (uint32_t)k, b = pbeg[p], c = pbeg[p + 1] - b, d = dst[i];
+  const uint64_t hi = k & 0xffffffff00000000ull;
+  for (uint32_t r = lane; r < c; r += 64) {
+    A[d + r] = dbits(mean[b + r]);
+    B[d + r] = hi | (uint64_t)(kTagImport | (b + r));
+  }
 }
 
 }  // namespace
@@ -405,13 +437,14 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   take_decode_error(e);
   const uint64_t nc = e->hf_cnt[9];
   if (!nc) return;
-  if (nc <= s.cap_cent) {
-    if (s.acc + nc > s.cap_cent) histo_imports_drain(e);
+  if (nc <= s.cap_cent && n <= s.cap_pay) {
+    if (s.acc + nc > s.cap_cent || s.npay + n > s.cap_pay) histo_imports_drain(e);
     ev_pair(e->pool_id, [&] {
       hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.acc,
-                         s.cslot, s.cmean, s.cw, e->h_err);
+                         s.cmean, s.cw, s.pslot, s.pbeg, s.npay, e->h_err);
     });
     s.acc += nc;
+    s.npay += n;
     return;
   }
   // slices of whole payloads in arrival order, each at most the run, cut greedily on the host;
@@ -424,29 +457,52 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
       throw std::invalid_argument("one imported digest holds more centroids than max_batch_records");
   for (uint64_t b0 = 0; b0 < n;) {
     uint64_t b1 = b0 + 1;
-    while (b1 < n && co[b1 + 1] - co[b0] <= s.cap_cent) b1++;
+    while (b1 < n && co[b1 + 1] - co[b0] <= s.cap_cent && b1 - b0 < s.cap_pay) b1++;
     const uint64_t c0 = co[b0], c1 = co[b1];
     if (c1 > c0) {
-      if (s.acc + (c1 - c0) > s.cap_cent) histo_imports_drain(e);
+      if (s.acc + (c1 - c0) > s.cap_cent || s.npay + (b1 - b0) > s.cap_pay) histo_imports_drain(e);
       ev_pair(e->pool_id, [&] {
         hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
-                           slot + b0, s.coff + b0, s.acc - c0, s.cslot, s.cmean, s.cw, e->h_err);
+                           slot + b0, s.coff + b0, s.acc - c0, s.cmean, s.cw, s.pslot, s.pbeg, s.npay, e->h_err);
       });
       s.acc += c1 - c0;
+      s.npay += b1 - b0;
     }
     b0 = b1;
   }
 }
 
+// The run merges as one histo ingest.  Its centroids are grouped by key through their payloads:
+// the payload table (slot, first centroid; arrival order) sorted stably by slot, each payload's
+// place the scan of the counts in that order, then one wave per payload moves its centroids
+// there -- the order a stable sort of the centroids by slot gives (a payload's centroids stay
+// together and in order), at one read and one write per centroid instead of a radix sort of
+// every centroid record.
 void histo_imports_drain(vn_engine* e) {
   ImportScratch& s = e->imp;
-  if (!s.acc) return;
-  const uint64_t n = s.acc;
+  if (!s.acc) {
+    s.npay = 0;
+    return;
+  }
+  const uint64_t n = s.acc, np = s.npay;
   s.acc = 0;
+  s.npay = 0;
+  hipStream_t st = e->st;
   hipEvent_t a = e->timing ? e->pool_im.next() : nullptr, b = e->timing ? e->pool_im.next() : nullptr;
-  if (a && b) VN_HIP_CHECK(hipEventRecord(a, e->st));
-  ingest_histos(e, n, s.cslot, s.cmean, nullptr, s.cw);
-  if (a && b) VN_HIP_CHECK(hipEventRecord(b, e->st));
+  if (a && b) VN_HIP_CHECK(hipEventRecord(a, st));
+  hipLaunchKernelGGL(k_pay_keys, dim3(blocks_for(np, 256)), dim3(256), 0, st, np, s.pslot, s.pkey, s.pbeg,
+                     (uint32_t)n);
+  RadixPass passes[4];
+  const int npass = make_passes(passes, false, 32, e->slot_bits[VN_HISTO]);
+  const uint64_t* key =
+      radix_sort(s.pkey, nullptr, s.pkey + s.cap_pay, nullptr, np, passes, npass, e->rs, st, nullptr) ? s.pkey + s.cap_pay
+                                                                                                    : s.pkey;
+  hipLaunchKernelGGL(k_pay_counts, dim3(blocks_for(np, 256)), dim3(256), 0, st, np, key, s.pbeg, s.pcnt);
+  scan_exclusive_u32(s.pcnt, s.pdst, np, e->ss, st);
+  hipLaunchKernelGGL(k_pay_move, dim3(blocks_for(np, 4)), dim3(256), 0, st, np, key, s.pbeg, s.pdst, s.cmean, e->hA0,
+                     e->hB0);
+  histo_process(e, n, histo_group_sorted(e, n, e->hA0, e->hB0, e->hA1, e->hB1), s.cw);
+  if (a && b) VN_HIP_CHECK(hipEventRecord(b, st));
 }
 
 }  // namespace vn

@@ -43,6 +43,7 @@ struct HistoGroups {
   uint64_t *As, *Bs, *Ao, *Bo;  // key-grouped records and the spare pair
 };
 HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate);
+HistoGroups histo_group_sorted(vn_engine* e, uint64_t n, uint64_t* As, uint64_t* Bs, uint64_t* Ao, uint64_t* Bo);
 void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double* impw = nullptr);
 void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate,
                    const double* impw = nullptr);
