@@ -544,6 +544,12 @@ const char* vn_sink_last_error(const vn_sink* s);
 int vn_datadog_flush(vn_sink* s, const vn_flush_result* f, const vn_keys* keys, const vn_dd_config* cfg,
                      vn_dd_payload* out);
 
+/* Diagnostic (tests): indexEstimate(compression, q[i]) (merging_digest.go:240-243) as the replays
+ * evaluate it (divisions without the hardware's rescaling and fix-up steps) against the full
+ * correctly rounded division sequence, on the GPU; *mismatches = values whose bits differ. */
+int vn_diag_index_estimate(int device, double compression, const double* q, uint64_t n, uint64_t* mismatches,
+                           double* out /* optional: 2n values, the replays' and the full division's, or null */);
+
 /* strconv.ParseFloat(s, bits) of Go 1.9 (bits 64 or 32) as the device parser computes it, run on
  * the host: 0 ok, 1 syntax error, 2 out of range (ErrRange); *out the value (float32 widened). */
 int vn_go_parse_float(const char* s, uint64_t n, int bits, double* out);

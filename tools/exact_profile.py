@@ -69,6 +69,7 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     out["batch_cyc_call"] = round(p[27] / nb, 1)
     for base, nme in ((36, "E"), (40, "C_rows"), (44, "C2_queue")):
         out["batch_cyc_" + nme + "_per_wave"] = [round(p[base + w] / nb, 1) for w in range(4)]
+    out["batch_E_longest_list_per_wave"] = [round(p[56 + w] / nb, 1) for w in range(3)]
     out["study_columns"] = p[52]
     out["study_cheap_certified"] = p[53]
     out["study_exact_certified"] = p[54]
@@ -82,6 +83,12 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
 if __name__ == "__main__":
     # one hot key: with the default (exact) engine it replays on the four-wave kernel, whose
     # phases are A = merge-path positions + weight prefix, B = k values, C = forced starts and
-    # walks, D = masks + Welford (merge_fast); the one-wave kernel reports the old phase names
+    # walks, D = masks + Welford (merge_fast); the one-wave kernel reports the old phase names.
+    # "short:N:K": block 0 is one of K + 1 keys of N samples each (N < 8192: the one-wave
+    # replay, merge_sorted_fast: rank+pos, prefix+kin, chain, welford), the other K beside it
     for n in (sys.argv[1:] or ["1000000"]):
-        run(int(n), 0, 0)
+        if n.startswith("short:"):
+            _, ns, nk = n.split(":")
+            run(int(ns), int(nk), int(ns))
+        else:
+            run(int(n), 0, 0)

@@ -16,6 +16,8 @@
 #   c5prof4  the same with HIP's default 4 hardware queues
 #   c5profvar / c5var  the C5 leg with the A/B variant library, under the profiler / alone
 #   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) for the replay's HBM traffic
+#   setprof  k_set_segments phase cycles (variant library built with -DVN_SET_PROF)
+#   sim-N-R-D  rank R of an N-GPU C4 window alone, D engines in turn (bench.py --sim-world N --sim-rank R)
 #   hot      batched-replay parity tests, phase cycles (profiling build) and the 17M-sample key
 #   short    the one-wave replay's throughput (20k keys of 6000 samples, C5's per-drain size)
 #            with this build and with the A/B variant library; then 64 such keys checked
@@ -90,6 +92,23 @@ for step in "$@"; do
       timeout -k 10 200 python -u $H > ${O}_short.log 2>&1 &&
       VN_LIB=libveneur_amd_variant.so timeout -k 10 200 python -u $H > ${O}_short_var.log 2>&1 &&
       timeout -k 10 200 python -u tools/hot_replay_bench.py --n 6000 --keys 64 --reps 1 > ${O}_short_check.log 2>&1 ;;
+    setprof)
+      # (needs the variant library built with VARIANT_FLAGS=-DVN_SET_PROF)
+      VN_LIB=libveneur_amd_variant.so timeout -k 10 300 python -u tools/set_profile.py > ${O}_setprof.log 2>&1 ;;
+    shortprof)
+      # the one-wave replay's phase split (profiling build): 6000-sample keys, alone and with 20k beside
+      VN_LIB=libveneur_amd_prof.so timeout -k 10 200 python -u tools/exact_profile.py short:6000:0 short:6000:20000 \
+        > ${O}_shortprof.log 2>&1 ;;
+    sim-*|simvar-*)
+      # sim-N-R-D: rank R of an N-GPU C4 run alone on this GPU, D engines in turn (bench.py --sim-world)
+      # sim-N-R-D-C-Q: C CUs reserved for the longest replays, Q hardware queues (defaults 0, 16);
+      # simvar-...: the same with the A/B variant library
+      IFS=- read -r SK SN SR SD SC SQ <<< "$step"
+      SC=${SC:-0}; SQ=${SQ:-16}
+      LIBV=libveneur_amd.so; [ "$SK" = simvar ] && LIBV=libveneur_amd_variant.so
+      VN_LIB=$LIBV GPU_MAX_HW_QUEUES=$SQ timeout -k 10 400 python -u bench.py --sim-world $SN --sim-rank $SR \
+        --pipeline $SD --reserved-cus $SC --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0 \
+        > ${O}_${SK}_${SN}_${SR}_${SD}_${SC}_${SQ}.json 2> ${O}_${SK}_${SN}_${SR}_${SD}_${SC}_${SQ}.log ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

@@ -220,6 +220,7 @@ _sig("vn_parser_destroy", None, vp)
 _sig("vn_parser_last_error", C.c_char_p, vp)
 _sig("vn_parse_dogstatsd_device", C.c_int, vp, vp, C.c_uint64, vp, C.c_uint64, vp, C.c_uint64, u64p)
 _sig("vn_go_parse_float", C.c_int, C.c_char_p, C.c_uint64, C.c_int, f64p)
+_sig("vn_diag_index_estimate", C.c_int, C.c_int, C.c_double, f64p, C.c_uint64, u64p, f64p)
 
 
 class IntakeStats(C.Structure):  # vn_intake_stats
@@ -299,7 +300,7 @@ EXPORTED = [
     "vn_abi_version", "vn_struct_size", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
     "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_flush_masked", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_parser_create", "vn_parser_destroy",
-    "vn_parser_last_error", "vn_parse_dogstatsd_device", "vn_go_parse_float", "vn_intake_create", "vn_intake_destroy",
+    "vn_parser_last_error", "vn_parse_dogstatsd_device", "vn_go_parse_float", "vn_diag_index_estimate", "vn_intake_create", "vn_intake_destroy",
     "vn_intake_last_error", "vn_intake_process", "vn_intake_upsert", "vn_intake_keys_info", "vn_intake_read_keys",
     "vn_intake_reset", "vn_sink_create", "vn_sink_destroy", "vn_sink_last_error", "vn_datadog_flush", "vn_device_alloc", "vn_device_free", "vn_copy_to_device",
     "vn_device_copy", "vn_device_count", "vn_device_synchronize", "vn_timing_enable", "vn_get_timing", "vn_synth_generate", "vn_synth_free",

@@ -257,6 +257,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_ccnt, touch_max);
   dalloc(e->h_coff, (size_t)touch_max + 1);
   dalloc(e->h_cown, ch ? e->h_sort_cap / std::max<uint32_t>(e->temp_cap, 1) + 2 : 0);
+  dalloc(e->h_cstat, ch ? (e->h_sort_cap / std::max<uint32_t>(e->temp_cap, 1) + 2) * 8 : 0);
   dalloc(e->h_tw, e->h_sort_cap);
   dalloc(e->h_seen0, touch_max);
   dalloc(e->h_pcnt, touch_max);
@@ -468,7 +469,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
   dfree(e->hseen); dfree(e->hpend); dfree(e->hspn); dfree(e->hspw); dfree(e->hm_flag); dfree(e->hm_pos); dfree(e->hm_idx); dfree(e->hm_list); dfree(e->hm_cnt); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
-  dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw); dfree(e->h_cpk); dfree(e->h_lstat);
+  dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw); dfree(e->h_cpk); dfree(e->h_lstat); dfree(e->h_cstat);
   dfree(e->h_lpt0); dfree(e->h_lpt1); dfree(e->s_lpt0); dfree(e->s_lpt1);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_cown); dfree(e->h_tw);
   dfree(e->fz_val); dfree(e->fz_w); dfree(e->fz_k); dfree(e->fz_done);
@@ -887,6 +888,50 @@ void side_join(vn_engine* e) {
 extern "C" {
 
 int vn_abi_version(void) { return VN_ABI_VERSION; }
+
+namespace {
+__global__ void k_diag_index_estimate(double c, const double* __restrict__ q, uint64_t n,
+                                      unsigned long long* __restrict__ bad, double* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double a = vn::index_estimate<true>(c, q[i]), b = vn::index_estimate<false>(c, q[i]);
+  if (vn::dbits(a) != vn::dbits(b)) atomicAdd(bad, 1ull);
+  if (out) {
+    out[2 * i] = a;
+    out[2 * i + 1] = b;
+  }
+}
+}  // namespace
+
+int vn_diag_index_estimate(int device, double compression, const double* q, uint64_t n, uint64_t* mismatches,
+                           double* out) {
+  if (!mismatches || (n && !q)) return VN_EINVAL;
+  *mismatches = 0;
+  if (!n) return VN_OK;
+  if (hipSetDevice(device) != hipSuccess) return VN_EHIP;
+  double* dq = nullptr;
+  double* dout = nullptr;
+  unsigned long long* dbad = nullptr;
+  unsigned long long hbad = 0;
+  int rc = VN_OK;
+  if (hipMalloc(&dq, n * sizeof(double)) != hipSuccess || hipMalloc(&dbad, sizeof(unsigned long long)) != hipSuccess ||
+      hipMemcpy(dq, q, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(dbad, 0, sizeof(unsigned long long)) != hipSuccess ||
+      (out && hipMalloc(&dout, 2 * n * sizeof(double)) != hipSuccess)) {
+    rc = VN_EHIP;
+  } else {
+    hipLaunchKernelGGL(k_diag_index_estimate, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, nullptr, compression, dq,
+                       n, dbad, dout);
+    if (hipMemcpy(&hbad, dbad, sizeof(hbad), hipMemcpyDeviceToHost) != hipSuccess) rc = VN_EHIP;
+    if (out && rc == VN_OK && hipMemcpy(out, dout, 2 * n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+      rc = VN_EHIP;
+  }
+  if (dq) (void)hipFree(dq);
+  if (dout) (void)hipFree(dout);
+  if (dbad) (void)hipFree(dbad);
+  *mismatches = hbad;
+  return rc;
+}
 static_assert(kErrSplitTouched == VN_WARN_SPLIT_TOUCHED, "the flush reports the device flag as is");
 
 size_t vn_struct_size(int which) {

@@ -239,6 +239,7 @@ struct vn_engine {
   double* h_csw = nullptr;
   uint32_t* h_cpk = nullptr;     // ... the batched replay's packed weights (ExactCtx::cpk)
   double* h_lstat = nullptr;     // ... the batched keys' Local* partials (ExactCtx::lstat)
+  double* h_cstat = nullptr;     // ... every pure chunk's Local* partials (ExactCtx::cstat)
   uint32_t* h_tl2 = nullptr;     // slots of hot keys
   uint32_t* h_ccnt = nullptr;    // per touched key: pure chunks to pre-sort
   uint32_t* h_coff = nullptr;    // scan of h_ccnt (touched + 1)

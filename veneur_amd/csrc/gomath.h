@@ -20,6 +20,21 @@ VN_HD double dsub(double a, double b) { return __dsub_rn(a, b); }
 VN_HD double dmul(double a, double b) { return __dmul_rn(a, b); }
 VN_HD double ddiv(double a, double b) { return __ddiv_rn(a, b); }
 VN_HD double dsqrt(double a) { return __dsqrt_rn(a); }
+// a / b correctly rounded, as the hardware's division sequence (reciprocal, two Newton steps,
+// quotient and residual correction) without v_div_scale and v_div_fixup, which change nothing when
+// neither operand needs rescaling and the quotient is neither special nor subnormal (a zero or of
+// magnitude within [2^-500, 2^500], b within [2^-300, 2^300]: the arguments of indexEstimate's
+// divisions, whose q = P / T is 0 or at least 2^-53 away from every breakpoint)
+VN_HD double ddiv_nr(double a, double b) {
+  const double r0 = __builtin_amdgcn_rcp(b);
+  const double e0 = __builtin_fma(-b, r0, 1.0);
+  const double r1 = __builtin_fma(r0, e0, r0);
+  const double e1 = __builtin_fma(-b, r1, 1.0);
+  const double y = __builtin_fma(r1, e1, r1);
+  const double q0 = __dmul_rn(a, y);
+  const double rr = __builtin_fma(-b, q0, a);
+  return __builtin_fma(rr, y, q0);
+}
 #else
 // host build is compiled with -ffp-contract=off
 VN_HD double dadd(double a, double b) { return a + b; }
@@ -27,6 +42,7 @@ VN_HD double dsub(double a, double b) { return a - b; }
 VN_HD double dmul(double a, double b) { return a * b; }
 VN_HD double ddiv(double a, double b) { return a / b; }
 VN_HD double dsqrt(double a) { return __builtin_sqrt(a); }
+VN_HD double ddiv_nr(double a, double b) { return a / b; }
 #endif
 
 VN_HD uint64_t dbits(double x) { return __builtin_bit_cast(uint64_t, x); }
@@ -154,16 +170,20 @@ VN_HD double asin_go(double x) {
 // of asin's two and satan's three paths is one division feeding one xatan, so the paths
 // share that code (x / 1.0 == x exactly) and a wave no longer runs each path in turn.
 // Bit-identical to asin_go for every input in [-1, 1] (checked against the oracle).
+#ifndef VN_INDEX_NR
+#define VN_INDEX_NR false  // (build knob: true evaluates indexEstimate with ddiv_nr -- not kept)
+#endif
+template <bool NR = VN_INDEX_NR>  // NR: the divisions as ddiv_nr (indexEstimate's argument range); false: ddiv
 VN_HD double asin_go_sel(double x) {
   const double Morebits = 6.123233995736765886130e-17, Tan3pio8 = 2.41421356237309504880;
   const double ax = x < 0 ? -x : x;
   const double temp = dsqrt(dsub(1.0, dmul(ax, ax)));
   const bool hi = ax > 0.7;
-  const double y = ddiv(hi ? temp : ax, hi ? ax : temp);  // satan's argument (y >= 0)
+  const double y = NR ? ddiv_nr(hi ? temp : ax, hi ? ax : temp) : ddiv(hi ? temp : ax, hi ? ax : temp);  // (y >= 0)
   const bool s0 = y <= 0.66, s2 = y > Tan3pio8;
   const double an = s0 ? y : (s2 ? 1.0 : dsub(y, 1.0));
   const double ad = s0 ? 1.0 : (s2 ? y : dadd(y, 1.0));
-  const double z = xatan_go(ddiv(an, ad));
+  const double z = xatan_go(NR ? ddiv_nr(an, ad) : ddiv(an, ad));
   const double sat = s0 ? z : (s2 ? dadd(dsub(kPi / 2, z), Morebits) : dadd(dadd(kPi / 4, z), dmul(0.5, Morebits)));
   const double r = hi ? dsub(kPi / 2, sat) : sat;
   if (x == 0) return x;
@@ -202,8 +222,11 @@ VN_HD double from_ordered_bits(uint64_t k) {
 }
 
 // tdigest indexEstimate (merging_digest.go:240-243): compression * (asin(2q-1)/pi + 0.5)
+// indexEstimate (merging_digest.go:240-243) for q in [0, 1]; NR as asin_go_sel
+template <bool NR = VN_INDEX_NR>
 VN_HD double index_estimate(double compression, double q) {
-  return dmul(compression, dadd(ddiv(asin_go_sel(dsub(dmul(2.0, q), 1.0)), kPi), 0.5));
+  const double a = asin_go_sel<NR>(dsub(dmul(2.0, q), 1.0));
+  return dmul(compression, dadd(NR ? ddiv_nr(a, kPi) : ddiv(a, kPi), 0.5));
 }
 
 }  // namespace vn

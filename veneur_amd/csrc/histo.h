@@ -32,6 +32,8 @@ struct ExactCtx {
   const uint32_t* keys;      // slot of each processed key
   const uint32_t* order;     // replay only: key indices of this launch (nullptr: 0..nkeys-1)
   uint32_t norder;           // replay grid when order is set
+  double* cstat;             // per pure chunk: its Local* partials (8 doubles, as lstat), written by the chunk
+                             // sorter, summed by k_exact_long_stats; null: the latter reads the samples
   const uint32_t* mw_count;  // replay: the first *mw_count entries of order64 are replayed by the four-wave kernel,
                              // the first mw_count[1] of them batched (k_histo_exact_mwb)
   const uint64_t* order64;   // replay only: key index in the low 32 bits, longest first (norder)

@@ -351,6 +351,46 @@ __device__ double temp_weight(const ldsf64* tw, uint32_t np) {
 // (different weights or signed zeros) lane 0 runs Go's quickSort instead.  One wave.
 __device__ __noinline__ void sort_temps(const ldsf64* tv, const ldsf64* tw, ldsf64* sv, ldsf64* sw, uint32_t np) {
   const uint32_t lane = threadIdx.x & 63;
+  // Temps made of at most four ascending runs with no value repeated (an imported digest's
+  // centroids arrive in ascending order: a chunk of them holds one or two runs): a temp's rank
+  // is its place in its run plus, per other run, the run's temps below it (a binary search).
+  // Without repeats the order is the one below, repeats or more runs take the general path.
+  if (np <= 64) {
+    const bool in = lane < np;
+    const double v = in ? tv[lane] : 0.0;
+    const double vp = __shfl_up(v, 1, 64);
+    const bool desc = in && lane > 0 && v < vp, eq = in && lane > 0 && v == vp;
+    const uint64_t starts = __ballot(desc) | 1ull;
+    if (!__any(eq) && __popcll(starts) <= 4) {
+      const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+      const uint32_t mine = 63u - (uint32_t)__builtin_clzll(starts & upto);
+      uint32_t rank = lane - mine;
+      bool rep = false;
+      uint64_t rest = starts;
+      while (rest) {
+        const uint32_t a = (uint32_t)__builtin_ctzll(rest);
+        rest &= rest - 1;
+        const uint32_t b = rest ? (uint32_t)__builtin_ctzll(rest) : np;
+        if (a == mine || !in) continue;
+        uint32_t l = a, h = b;  // first temp of the run not below v
+        while (l < h) {
+          const uint32_t md = (l + h) >> 1;
+          if (tv[md] < v) l = md + 1;
+          else h = md;
+        }
+        rep |= l < b && tv[l] == v;
+        rank += l - a;
+      }
+      if (!__any(rep)) {
+        if (in) {
+          sv[rank] = v;
+          sw[rank] = tw[lane];
+        }
+        wave_lds_sync();
+        return;
+      }
+    }
+  }
   uint32_t rank[kMaxTempPerLane];
   double vr[kMaxTempPerLane], wr[kMaxTempPerLane];
   bool tie = false;
@@ -964,6 +1004,43 @@ __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t
     tw[t] = tag_is_sample(tag) ? wt : -wt;  // sign: an imported centroid (no Local* statistics)
   }
   wave_lds_sync();
+  if (x.cstat) {
+    // the chunk's Local* partials (Histo.Sample, samplers.go:346-356; min / max of every record for
+    // the digest), for the batched keys' statistics: read here once, with the chunk
+    double lsw = 0.0, lsxw = 0.0, lsrw = 0.0, lmn = kInf, lmx = -kInf, ldmn = kInf, ldmx = -kInf;
+    for (uint32_t t = lane; t < tcap; t += 64) {
+      const double v = tv[t], w = tw[t], wt = __builtin_fabs(w);
+      ldmn = min_go(ldmn, v);
+      ldmx = max_go(ldmx, v);
+      if (w > 0.0) {
+        lsw = dadd(lsw, wt);
+        lmn = min_go(lmn, v);
+        lmx = max_go(lmx, v);
+        lsxw = dadd(lsxw, dmul(v, wt));
+        lsrw = dadd(lsrw, dmul(ddiv(1.0, v), wt));
+      }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      lsw = dadd(lsw, __shfl_xor(lsw, d, 64));
+      lsxw = dadd(lsxw, __shfl_xor(lsxw, d, 64));
+      lsrw = dadd(lsrw, __shfl_xor(lsrw, d, 64));
+      lmn = min_go(lmn, __shfl_xor(lmn, d, 64));
+      lmx = max_go(lmx, __shfl_xor(lmx, d, 64));
+      ldmn = min_go(ldmn, __shfl_xor(ldmn, d, 64));
+      ldmx = max_go(ldmx, __shfl_xor(ldmx, d, 64));
+    }
+    if (lane == 0) {
+      double* o = x.cstat + (uint64_t)g * 8;
+      o[0] = lsw;
+      o[1] = lsxw;
+      o[2] = lsrw;
+      o[3] = lmn;
+      o[4] = lmx;
+      o[5] = ldmn;
+      o[6] = ldmx;
+    }
+  }
   const double tempW = temp_weight(tw, tcap);
   sort_temps(tv, tw, sv, sw, tcap);
   // for the long replays (replay_key_fast): the exclusive prefix of the sorted |weights| after
@@ -2355,6 +2432,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     bool tiny = false;  // a numerator near the hardware's rescaling range (then no batch)
     uint32_t mmax = wave_incl_max(m);
     mmax = __builtin_amdgcn_readlane(mmax, 63);
+    PROF_ADDW(56, 0, (long long)mmax);
     // (entries past a list's end are read too -- the next list's, or the layout after the
     // lists, all inside the workgroup's LDS -- and masked by q + u < m below)
     auto ld = [&](uint32_t q, double (&v)[4], uint32_t (&w)[4]) {
@@ -2392,15 +2470,18 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (uint32_t u = 0; u < 4; u++) {  // the mean chain
-        const double tq = dmul(dsub(v0[u], mean), wd[u]);
+        // (an entry past the list's end: weight 0 and value 0, so the step adds a zero and no
+        // select sits on the chain -- a -0 mean may become +0 there, which only the lane's
+        // [lo, hi], compared with <= / >, and the spare slot see)
+        const double vz = in[u] ? v0[u] : 0.0;
+        const double tq = dmul(dsub(vz, mean), wd[u]);
         tiny |= tq != 0.0 && __builtin_fabs(tq) < 1e-250;
         // the correctly rounded quotient tq / W: with no operand special (A's range checks, the
         // tiny test above) v_div_fixup would return the fma's result unchanged
         const double q0 = dmul(tq, y[u]);
         const double rr = __builtin_fma(-Wn[u], q0, tq);
         const double qq = __builtin_fma(rr, y[u], q0);
-        const double m2 = dadd(mean, qq);
-        mean = in[u] ? m2 : mean;
+        mean = dadd(mean, qq);
         B.lv[at[u]] = mean;
         // (no NaN here: the hardware min / max, without the canonicalisation fmin / fmax add)
         asm("v_min_f64 %0, %1, %2" : "=v"(lo) : "v"(lo), "v"(mean));
@@ -2979,7 +3060,22 @@ __device__ __forceinline__ void long_stats_entry(const ExactCtx& x, const uint32
   if (k < x.nkeys) {
     const uint32_t s = x.keys[k];
     const ExactSplit sp = exact_split(x.hpend[s], x.nex[k], x.tcap);
-    const uint64_t base = (uint64_t)x.start[s] + sp.off0, ne = (uint64_t)sp.npure * x.tcap;
+    if (x.cstat) {  // the chunk sorter's per-chunk partials: 64 B per chunk instead of 16 B per sample
+      const uint64_t g0 = x.coff[k], ng = sp.npure;
+      const uint64_t per = (ng + kLongStatSlices - 1) / kLongStatSlices;
+      const uint64_t a = min(ng, per * blockIdx.x), b = min(ng, a + per);
+      for (uint64_t g = a + threadIdx.x; g < b; g += 256) {
+        const double* q = x.cstat + (g0 + g) * 8;
+        sw = dadd(sw, q[0]);
+        sxw = dadd(sxw, q[1]);
+        srw = dadd(srw, q[2]);
+        mn = min_go(mn, q[3]);
+        mx = max_go(mx, q[4]);
+        dmn = min_go(dmn, q[5]);
+        dmx = max_go(dmx, q[6]);
+      }
+    }
+    const uint64_t base = (uint64_t)x.start[s] + sp.off0, ne = x.cstat ? 0ull : (uint64_t)sp.npure * x.tcap;
     const uint64_t per = (ne + kLongStatSlices - 1) / kLongStatSlices;
     const uint64_t a = min(ne, per * blockIdx.x), b = min(ne, a + per);
     for (uint64_t e = a + threadIdx.x; e < b; e += 256) {

@@ -1322,6 +1322,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.ctw = e->h_tw;
   xc.cpk = e->h_cpk;
   xc.lstat = e->h_lstat;
+  xc.cstat = e->h_cstat;
   const uint64_t max_chunks = n / e->temp_cap + 1;
   // (exact mode, no hot key, not timing: the longest keys' chunks are sorted first and their
   // replays start while the other chunks sort, in replay_cold)

@@ -182,7 +182,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
   __shared__ uint32_t s_red[4];
   __shared__ uint32_t s_rec[kScanStage];  // the records of the current scan window
   __shared__ uint32_t s_pos, s_trig, s_tc, s_lc, s_mode, s_b, s_nz, s_wbase, s_wend;
-  __shared__ uint32_t s_filled, s_tfull, s_pstar, s_newfill, s_min;
+  __shared__ uint32_t s_filled, s_tfull, s_pstar, s_newfill, s_min, s_take;
 
   SPROF_T(p_begin);
   const uint32_t t = threadIdx.x;
@@ -237,44 +237,56 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
       }
       lds_barrier();
       const uint32_t wbase = s_wbase, wend = s_wend;
-      // wave 0 advances to the next mergeSparse trigger -- the record that makes the tmpSet
-      // hold kHllTmpTrigger distinct codes -- 64 records per step: a record counts if its
-      // code is neither in the tmpSet nor held by a lower lane of the same step.
-      if (t < 64) {
-        uint32_t pos = s_pos, tc = s_tc, trig = 0;
-        const uint64_t below = (t == 0) ? 0ull : (~0ull >> (64 - t));
+      // the workgroup advances kBlock records per step to the next mergeSparse trigger -- the
+      // record that makes the tmpSet hold kHllTmpTrigger distinct codes: a record counts if its
+      // code is neither in the tmpSet nor held by a lower thread of the same step (the lowest
+      // claimer of a new code's hash entry), its rank among the step's counted records a
+      // block-wide prefix count
+      {
+        uint32_t pos = s_pos, tc = s_tc;
+        bool trig = false;
+        const uint32_t lane = t & 63, w = t >> 6;
+        const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
         while (pos < wend) {
           const uint32_t p = pos + t;
           const bool valid = p < wend;
           const uint32_t c = valid ? s_rec[p - wbase] : kHllNoCode;
           const bool fresh = valid && !hash_contains(s_hash, c);
+          lds_barrier();  // every lookup before any claim of this step
           uint32_t hi = 0;
           if (fresh) {
             hi = hash_claim(s_hash, c);
             atomicMin(&s_first[hi], t);
           }
+          lds_barrier();
           const bool first = fresh && s_first[hi] == t;
           const uint64_t bal = __ballot(first);
-          const uint32_t cnt = (uint32_t)__popcll(bal);
-          const uint32_t need = kHllTmpTrigger - tc;
-          uint32_t take = 64, add = cnt;
-          if (cnt >= need) {  // the need-th first occurrence triggers the merge
-            uint64_t b = bal;
-            for (uint32_t q = 1; q < need; q++) b &= b - 1;
-            const uint32_t L = (uint32_t)__builtin_ctzll(b);
-            take = L + 1;
-            add = need;
-            trig = 1;
+          if (lane == 0) s_red[w] = (uint32_t)__popcll(bal);
+          lds_barrier();
+          uint32_t before = 0, cnt = 0;
+#pragma unroll
+          for (uint32_t i = 0; i < 4; i++) {
+            before += i < w ? s_red[i] : 0u;
+            cnt += s_red[i];
           }
-          if (first && t < take) s_tmp[tc + (uint32_t)__popcll(bal & below)] = c;
-          tc += add;
+          const uint32_t rank = before + (uint32_t)__popcll(bal & below);
+          const uint32_t need = kHllTmpTrigger - tc;
+          if (first && rank < need) s_tmp[tc + rank] = c;
+          uint32_t take = kBlock;
+          if (cnt >= need) {  // the need-th counted record triggers the merge
+            if (first && rank == need - 1) s_take = t + 1;
+            trig = true;
+          }
+          lds_barrier();  // (s_red and s_take are read before the next step writes them)
+          if (trig) take = s_take;
+          tc += min(cnt, need);
           pos = min(pos + take, wend);
           if (trig) break;
         }
         if (t == 0) {
           s_pos = pos;
           s_tc = tc;
-          s_trig = trig;
+          s_trig = trig ? 1u : 0u;
         }
       }
       lds_barrier();
