@@ -986,6 +986,31 @@ __global__ void k_exact_chunk_owner(ExactCtx x) {
   x.cown[g] = last_le_u32(x.coff, x.nkeys, g);
 }
 
+#ifndef VN_BATCH_MIN_LEN
+#define VN_BATCH_MIN_LEN 65536u
+#endif
+// keys replaying at least this many samples take the batched kernel (its LDS: one block per CU)
+constexpr uint32_t kBatchMinLen = VN_BATCH_MIN_LEN;
+
+// min / max over the wave's 64 lanes (Go's math.Min / Max order: -0 below +0), complete in lane
+// 63: the DPP row shifts and row broadcasts of wave_incl_add_d, every lane active
+__device__ __forceinline__ double wave_min_go(double v) {
+  v = min_go(v, dpp_d<0x111, 0xf>(v, kInf));
+  v = min_go(v, dpp_d<0x112, 0xf>(v, kInf));
+  v = min_go(v, dpp_d<0x114, 0xf>(v, kInf));
+  v = min_go(v, dpp_d<0x118, 0xf>(v, kInf));
+  v = min_go(v, dpp_d<0x142, 0xa>(v, kInf));
+  return min_go(v, dpp_d<0x143, 0xc>(v, kInf));
+}
+__device__ __forceinline__ double wave_max_go(double v) {
+  v = max_go(v, dpp_d<0x111, 0xf>(v, -kInf));
+  v = max_go(v, dpp_d<0x112, 0xf>(v, -kInf));
+  v = max_go(v, dpp_d<0x114, 0xf>(v, -kInf));
+  v = max_go(v, dpp_d<0x118, 0xf>(v, -kInf));
+  v = max_go(v, dpp_d<0x142, 0xa>(v, -kInf));
+  return max_go(v, dpp_d<0x143, 0xc>(v, -kInf));
+}
+
 // sort pure chunk g of key k (one wave)
 __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t g, const uint32_t k, char* smem) {
   const uint32_t lane = threadIdx.x;
@@ -1004,9 +1029,11 @@ __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t
     tw[t] = tag_is_sample(tag) ? wt : -wt;  // sign: an imported centroid (no Local* statistics)
   }
   wave_lds_sync();
-  if (x.cstat) {
+  if (x.cstat && x.nex[k] >= kBatchMinLen) {
     // the chunk's Local* partials (Histo.Sample, samplers.go:346-356; min / max of every record for
-    // the digest), for the batched keys' statistics: read here once, with the chunk
+    // the digest), for the batched keys' statistics (only they read them): read here once, with the
+    // chunk; reduced over the wave by DPP (lane 63 holds the totals; sums need no fixed order: their
+    // parity bound is 1e-12, weights are exact)
     double lsw = 0.0, lsxw = 0.0, lsrw = 0.0, lmn = kInf, lmx = -kInf, ldmn = kInf, ldmx = -kInf;
     for (uint32_t t = lane; t < tcap; t += 64) {
       const double v = tv[t], w = tw[t], wt = __builtin_fabs(w);
@@ -1020,17 +1047,14 @@ __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t
         lsrw = dadd(lsrw, dmul(ddiv(1.0, v), wt));
       }
     }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-      lsw = dadd(lsw, __shfl_xor(lsw, d, 64));
-      lsxw = dadd(lsxw, __shfl_xor(lsxw, d, 64));
-      lsrw = dadd(lsrw, __shfl_xor(lsrw, d, 64));
-      lmn = min_go(lmn, __shfl_xor(lmn, d, 64));
-      lmx = max_go(lmx, __shfl_xor(lmx, d, 64));
-      ldmn = min_go(ldmn, __shfl_xor(ldmn, d, 64));
-      ldmx = max_go(ldmx, __shfl_xor(ldmx, d, 64));
-    }
-    if (lane == 0) {
+    lsw = wave_incl_add_d(lsw);
+    lsxw = wave_incl_add_d(lsxw);
+    lsrw = wave_incl_add_d(lsrw);
+    lmn = wave_min_go(lmn);
+    lmx = wave_max_go(lmx);
+    ldmn = wave_min_go(ldmn);
+    ldmx = wave_max_go(ldmx);
+    if (lane == 63) {
       double* o = x.cstat + (uint64_t)g * 8;
       o[0] = lsw;
       o[1] = lsxw;
@@ -1902,11 +1926,6 @@ constexpr uint32_t kBMinAvail = 32;         // chunks in the ring below which a 
 #endif
 constexpr double kBatchMinW = VN_BATCH_MIN_W;  // batches start once the digest holds this weight
 constexpr uint32_t kBatchBackoff = 4;          // single merges after a batch that took none
-#ifndef VN_BATCH_MIN_LEN
-#define VN_BATCH_MIN_LEN 65536u
-#endif
-// keys replaying at least this many samples take the batched kernel (its LDS: one block per CU)
-constexpr uint32_t kBatchMinLen = VN_BATCH_MIN_LEN;
 
 typedef __attribute__((address_space(3))) uint8_t ldsu8;
 

@@ -199,16 +199,15 @@ struct KPackDst {
   uint32_t* key;
   uint64_t* pay;
   int shift;
-  __device__ __forceinline__ void store(uint64_t pos, uint32_t k, uint64_t p) const {
+  static constexpr bool kPacked = true;  // (partition.h: the tile is staged as packed dwords)
+  // the dword of record (k, p) bound for position pos; an escaped p is written to pay[pos] now
+  __device__ __forceinline__ uint32_t pack(uint64_t pos, uint32_t k, uint64_t p) const {
     const int fb = 32 - shift;
     const int64_t v = (int64_t)p, lim = (int64_t)1 << (fb - 1);
     const uint32_t lowk = shift ? k & ((1u << shift) - 1u) : 0u;
-    if (v > -lim && v < lim) {
-      key[pos] = lowk | ((uint32_t)v << shift);
-    } else {
-      key[pos] = lowk | ((uint32_t)lim << shift);  // (the field's minimum: escape)
-      pay[pos] = p;
-    }
+    if (v > -lim && v < lim) return lowk | ((uint32_t)v << shift);
+    pay[pos] = p;
+    return lowk | ((uint32_t)lim << shift);  // (the field's minimum: escape)
   }
 };
 

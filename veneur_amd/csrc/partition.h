@@ -40,13 +40,27 @@ __device__ __forceinline__ uint64_t part_match8(uint32_t d, bool active) {
 // Each wave owns a contiguous quarter of the tile: its records are loaded up front (all loads
 // in flight together) and ranked with wave ballots against a per-wave running count per digit
 // in LDS (a wave's DS operations execute in order: no workgroup barrier while ranking).
+// A Dst with kPacked = true stores each record as the one dword pack() makes of it (its rare
+// out-of-line payload written at once, at the record's final place): the tile is staged as
+// those dwords alone, 16 KiB of LDS instead of 48, and more tiles fit a CU.
+template <class Dst, class = void>
+struct DstPacked {
+  static constexpr bool value = false;
+};
+template <class Dst>
+struct DstPacked<Dst, decltype((void)Dst::kPacked)> {
+  static constexpr bool value = Dst::kPacked;
+};
+
 template <class Src, class Dst>
 __global__ __launch_bounds__(kBlock) void k_part_scatter(Src src, Dst dst, uint64_t n, int shift,
                                                          const uint32_t* __restrict__ counts,
                                                          const uint32_t* __restrict__ offsets, uint32_t nblocks) {
   using P = typename Src::P;
+  constexpr bool kPack = DstPacked<Dst>::value;
   __shared__ uint32_t s_key[kTile];
-  __shared__ P s_pay[kTile];
+  __shared__ P s_pay[kPack ? 1 : kTile];
+  __shared__ uint8_t s_dig[kPack ? kTile : 1];  // (packed: each record's digit beside its dword)
   __shared__ uint32_t s_run[4][256];
   __shared__ uint32_t s_loc[256];
   __shared__ uint32_t s_glob[256];
@@ -110,16 +124,29 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(Src src, Dst dst, uint6
   for (int j = 0; j < kItems; j++) {
     const uint32_t li = wbase + (uint32_t)j * 64 + lane;
     if (li < tile_n) {
-      const uint32_t pos = s_run[w][(key[j] >> shift) & 0xffu] + rank[j];
-      s_key[pos] = key[j];
-      s_pay[pos] = pay[j];
+      const uint32_t d = (key[j] >> shift) & 0xffu;
+      const uint32_t pos = s_run[w][d] + rank[j];
+      if constexpr (kPack) {
+        s_key[pos] = dst.pack((uint64_t)s_glob[d] + (pos - s_loc[d]), key[j], pay[j]);
+        s_dig[pos] = (uint8_t)d;
+      } else {
+        s_key[pos] = key[j];
+        s_pay[pos] = pay[j];
+      }
     }
   }
   __syncthreads();
-  for (uint32_t li = t; li < tile_n; li += kBlock) {
-    uint32_t k = s_key[li];
-    uint32_t d = (k >> shift) & 0xffu;
-    dst.store((uint64_t)s_glob[d] + (li - s_loc[d]), k, s_pay[li]);
+  if constexpr (kPack) {
+    for (uint32_t li = t; li < tile_n; li += kBlock) {
+      const uint32_t d = s_dig[li];
+      dst.key[(uint64_t)s_glob[d] + (li - s_loc[d])] = s_key[li];
+    }
+  } else {
+    for (uint32_t li = t; li < tile_n; li += kBlock) {
+      uint32_t k = s_key[li];
+      uint32_t d = (k >> shift) & 0xffu;
+      dst.store((uint64_t)s_glob[d] + (li - s_loc[d]), k, s_pay[li]);
+    }
   }
 }
 
