@@ -40,6 +40,14 @@ def _key(kind, n, rng):
     elif kind == "seven":
         v = rng.integers(0, 7, n).astype(np.float64)
         r = np.ones(n, np.float32)
+    elif kind == "past2_30":
+        # integer weights of 2^20 (rate 2^-20) carry the digest's total past 2^30 within a few
+        # thousand samples; a few samples at rate 0.3 (weight float32(1/0.3), a 2^-23 multiple)
+        # make some main weights non-integer: sums of such weights are exact only up to 2^30, so
+        # the fast merges and batches must step aside there (MergeState::fint)
+        v = rng.lognormal(np.log(50.0), 1.0, n)
+        c = rng.choice(3, n, p=(0.6, 0.399, 0.001))
+        r = np.asarray((1.0, 2.0 ** -20, 0.3), np.float32)[c]
     elif kind == "heavy":
         v = rng.normal(0.0, 1.0, n)
         r = np.asarray((1.0, 0.01, 0.001), np.float32)[rng.choice(3, n, p=(0.98, 0.01, 0.01))]
@@ -99,6 +107,14 @@ def _check(kinds, n, seed, batches):
 @pytest.mark.parametrize("batches", [1, 3])
 def test_batched_replay_whole_digest_bit_exact(batches):
     _check(["lognormal", "falling", "rising", "ints", "seven", "heavy"], 300_000, 11 + batches, batches)
+
+
+def test_weights_past_2_30_with_non_integer_weights_bit_exact():
+    """a digest holding non-integer (2^-23-grid) weights whose total passes 2^30 --
+    the fast paths' exact-sum bound for such weights -- stays the reference's digest, bit for bit
+    (the batched and four-wave replays step aside past the bound)."""
+    _check(["past2_30", "past2_30"], 200_000, 7, 1)
+    _check(["past2_30"], 30_000, 8, 2)
 
 
 def test_batched_replay_one_long_key_bit_exact():

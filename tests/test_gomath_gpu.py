@@ -45,3 +45,28 @@ def test_index_estimate_divisions_bit_identical():
     assert ((q >= 0) & (q <= 1)).all()
     for delta in (100.0, 50.0, 1000.0):
         assert _mismatches(q, delta) == 0
+
+
+def test_index_estimate_device_equals_go_restatement():
+    """The device's indexEstimate (the replays' form) against Go's expression evaluated on the host
+    -- compression * (math.Asin(2*q - 1)/math.Pi + 0.5) with the oracle's math.Asin restatement --
+    bit for bit, over q = P / T of large totals (T past 2^30 and 2^31, P stepping by small
+    weights: consecutive k values an ulp apart, where a difference would flip a chain decision)."""
+    import math
+
+    import oracle
+    rng = np.random.default_rng(12)
+    qs = [rng.random(200_000)]
+    for T in (2344619302.3333325, 2.0 ** 31 + 0.5, 1.5 * 2.0 ** 30, 8.4e10, 123456.0):
+        P = np.floor(rng.random(100_000) * T)
+        P[:2000] = np.arange(2000) + np.floor(T * 0.3)
+        qs.append(P / T)
+    q = np.concatenate(qs)
+    vals = np.zeros(2 * len(q))
+    out = C.c_uint64(0)
+    assert A.lib.vn_diag_index_estimate(0, 100.0, q.ctypes.data_as(C.POINTER(C.c_double)), len(q), C.byref(out),
+                                        vals.ctypes.data_as(C.POINTER(C.c_double))) == 0
+    dev = vals[1::2]
+    host = np.array([100.0 * (oracle.lib.or_go_asin(2.0 * x - 1.0) / math.pi + 0.5) for x in q])
+    bad = np.nonzero(dev.view(np.uint64) != host.view(np.uint64))[0]
+    assert len(bad) == 0, (len(bad), [(float(q[i]).hex(), dev[i], host[i]) for i in bad[:8]])

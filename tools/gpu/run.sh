@@ -16,6 +16,7 @@
 #   c5prof4  the same with HIP's default 4 hardware queues
 #   c5profvar / c5var  the C5 leg with the A/B variant library, under the profiler / alone
 #   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) for the replay's HBM traffic
+#   c5setprof  k_set_merge cycles per payload kind over the C5 leg (variant built with -DVN_SET_PROF)
 #   setprof  k_set_segments phase cycles (variant library built with -DVN_SET_PROF)
 #   sim-N-R-D  rank R of an N-GPU C4 window alone, D engines in turn (bench.py --sim-world N --sim-rank R)
 #   hot      batched-replay parity tests, phase cycles (profiling build) and the 17M-sample key
@@ -95,10 +96,38 @@ for step in "$@"; do
     setprof)
       # (needs the variant library built with VARIANT_FLAGS=-DVN_SET_PROF)
       VN_LIB=libveneur_amd_variant.so timeout -k 10 300 python -u tools/set_profile.py > ${O}_setprof.log 2>&1 ;;
+    c5setprof)
+      # (needs the variant library built with VARIANT_FLAGS=-DVN_SET_PROF)
+      VN_LIB=libveneur_amd_variant.so timeout -k 10 300 python -u tools/c5_set_profile.py > ${O}_c5setprof.log 2>&1 ;;
     shortprof)
       # the one-wave replay's phase split (profiling build): 6000-sample keys, alone and with 20k beside
       VN_LIB=libveneur_amd_prof.so timeout -k 10 200 python -u tools/exact_profile.py short:6000:0 short:6000:20000 \
         > ${O}_shortprof.log 2>&1 ;;
+    simlib:*)
+      # simlib:LIB:N:R:D -- the per-rank C4 sim with libveneur_amd_LIB.so (LIB "main": the product)
+      IFS=: read -r _ SL SN SR SD <<< "$step"
+      LIBV=libveneur_amd_$SL.so; [ "$SL" = main ] && LIBV=libveneur_amd.so
+      VN_LIB=$LIBV timeout -k 10 400 python -u bench.py --sim-world $SN --sim-rank $SR --pipeline $SD \
+        --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0 \
+        > ${O}_simlib_${SL}_${SN}_${SR}_${SD}.json 2> ${O}_simlib_${SL}_${SN}_${SR}_${SD}.log ;;
+    batchlib:*)
+      # batchlib:LIB -- the batched replay's first whole-digest test with that library; an assertion
+      # failure is reported and the call goes on, a GPU fault ends it
+      IFS=: read -r _ SL <<< "$step"
+      VN_LIB=libveneur_amd_$SL.so timeout -k 10 200 python -u -m pytest \
+        "tests/test_batch_replay_gpu.py::test_batched_replay_whole_digest_bit_exact[1]" -x -q --timeout 150 \
+        --timeout-method thread > ${O}_batchlib_$SL.log 2>&1
+      echo "[run.sh] batchlib $SL pytest rc=$?"
+      if grep -q "illegal memory access\|Memory access fault\|Aborted" ${O}_batchlib_$SL.log; then (exit 3); else (exit 0); fi ;;
+    testlib:*)
+      # testlib:LIB:TESTID -- one test with libveneur_amd_LIB.so ("main": the product); an assertion
+      # failure is reported and the call goes on, a GPU fault ends it
+      IFS=: read -r _ SL ST <<< "$step"
+      LIBV=libveneur_amd_$SL.so; [ "$SL" = main ] && LIBV=libveneur_amd.so
+      VN_LIB=$LIBV timeout -k 10 300 python -u -m pytest "$ST" -x -q --timeout 250 --timeout-method thread \
+        > ${O}_testlib_${SL}.log 2>&1
+      echo "[run.sh] testlib $SL pytest rc=$?"
+      if grep -q "illegal memory access\|Memory access fault\|Aborted" ${O}_testlib_${SL}.log; then (exit 3); else (exit 0); fi ;;
     sim-*|simvar-*)
       # sim-N-R-D: rank R of an N-GPU C4 run alone on this GPU, D engines in turn (bench.py --sim-world)
       # sim-N-R-D-C-Q: C CUs reserved for the longest replays, Q hardware queues (defaults 0, 16);

@@ -27,6 +27,16 @@
 
 namespace vn {
 
+// indexEstimate's division form per call site (gomath.h VN_INDEX_NR; diagnostics builds only)
+#ifndef VN_NR_ONE
+#define VN_NR_ONE VN_INDEX_NR
+#endif
+#ifndef VN_NR_FOUR
+#define VN_NR_FOUR VN_INDEX_NR
+#endif
+#ifndef VN_NR_G
+#define VN_NR_G VN_INDEX_NR
+#endif
 #ifndef VN_EXACT_LDS_PAD
 #define VN_EXACT_LDS_PAD 0  // occupancy experiments only (tools/ab_variant.sh)
 #endif
@@ -511,7 +521,9 @@ __device__ __noinline__ NmW merge_sorted(const Lds L, MP_PARAMS, const uint32_t 
   // wiggle) takes the sequential walk instead, so the result is always the reference's.
   const double k0 = index_estimate(x.delta, 0.0);
   bool mono = true;
-  for (uint32_t j = lane + 1; j < m; j += 64) mono &= !(L.kin[j] < L.kin[j - 1]);
+  // (a NaN k is not monotone either: past 2^30 with non-integer weights the in-order prefix can
+  // pass T by an ulp, q > 1 and asin NaN -- Go's comparisons then merge, which the walk reproduces)
+  for (uint32_t j = lane + 1; j < m; j += 64) mono &= L.kin[j] >= L.kin[j - 1];
   mono = __all(mono);
   uint32_t nc = 0;
   bool overflow = false;
@@ -739,7 +751,7 @@ __device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds
       }
     }
 #pragma unroll
-    for (int r = 0; r < kR; r++) kv[r] = index_estimate(x.delta, ddiv(kv[r], T));
+    for (int r = 0; r < kR; r++) kv[r] = index_estimate<VN_NR_ONE>(x.delta, ddiv(kv[r], T));
 #pragma unroll
     for (int r = 0; r < kR; r++) L.kin[64 * r + lane] = kv[r];
   }
@@ -753,7 +765,7 @@ __device__ __forceinline__ void merge_sorted_fast(const MergeParams x, const Lds
   for (int r = 0; r < kR; r++) {
     const uint32_t j = 64 * r + lane;
     const double prev = L.kin[j ? j - 1 : 0];
-    mono &= !(j >= 1 && j < m && kv[r] < prev);
+    mono &= !(j >= 1 && j < m && !(kv[r] >= prev));  // (NaN: not monotone, see merge_sorted)
   }
   mono = __all(mono);
 #ifdef VN_CHAIN_WALK
@@ -1704,7 +1716,7 @@ __device__ __forceinline__ void merge_fast(const MergeParams x, const Lds L, con
 #pragma unroll
       for (int r = 0; r < R; r++) {
         const uint32_t e = r * NT + t;
-        if (e < m) F.kk[e] = index_estimate(x.delta, ddiv(dadd(wb[r], xw[r]), T));
+        if (e < m) F.kk[e] = index_estimate<VN_NR_FOUR>(x.delta, ddiv(dadd(wb[r], xw[r]), T));
       }
       fast_sync<NW>();
       if (wv == 0) walk_flags(F, m, k0);
@@ -2635,10 +2647,11 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     bool ok = true;
     if (ic >= 1) {
       const double qp = ic == 1 ? 0.0 : ddiv(dadd(F.mp[ic - 1], (double)cP), T);
-      ok = dsub(index_estimate(delta, ddiv(dadd(Pi, Wi), T)), index_estimate(delta, qp)) > 1.0;
+      ok = dsub(index_estimate<VN_NR_G>(delta, ddiv(dadd(Pi, Wi), T)), index_estimate<VN_NR_G>(delta, qp)) > 1.0;
     }
     if (nN > nI)
-      ok = ok && !(dsub(index_estimate(delta, ddiv(Pn, T)), index_estimate(delta, ic == 0 ? 0.0 : ddiv(Pi, T))) > 1.0);
+      ok = ok && !(dsub(index_estimate<VN_NR_G>(delta, ddiv(Pn, T)),
+                        index_estimate<VN_NR_G>(delta, ic == 0 ? 0.0 : ddiv(Pi, T))) > 1.0);
     const uint64_t fail = __ballot(in && !ok);
     if (fail && lane == 0) lds_min(&B.ctl[3], (uint32_t)__builtin_ctzll(fail));
   }

@@ -49,26 +49,35 @@ __device__ __forceinline__ uint32_t be32(const uint8_t* d) {
   return ((uint32_t)d[0] << 24) | ((uint32_t)d[1] << 16) | ((uint32_t)d[2] << 8) | d[3];
 }
 
-// f(byte) over global bytes [p, p + len) in order, read as aligned 16-byte blocks with the next
-// block's load in flight while this one is consumed (one lane walking its own payload).  The
-// blocks never leave the 16-byte-aligned span holding the bytes (so no page the bytes do not touch).
-template <class F>
+// f(byte) over global bytes [p, p + len) in order, read as aligned 16-byte blocks, G of them per
+// step with the next G blocks' loads in flight while these are consumed (one lane walking its own
+// payload: with one block ahead, a lane waited a memory latency every 16 bytes).  The blocks never
+// leave the 16-byte-aligned span holding the bytes (so no page the bytes do not touch).
+template <uint32_t G = 1, class F>
 __device__ __forceinline__ void for_bytes(const uint8_t* p, uint32_t len, F&& f) {
   if (!len) return;
   const uintptr_t s = reinterpret_cast<uintptr_t>(p), a0 = s & ~(uintptr_t)15;
   const uint32_t lo = (uint32_t)(s - a0), end = lo + len, nblk = (end + 15u) >> 4;
   const uint4* b = reinterpret_cast<const uint4*>(a0);
-  uint4 cur = b[0];
-  for (uint32_t k = 0; k < nblk; k++) {
-    const uint4 nxt = b[min(k + 1u, nblk - 1u)];
-    const uint32_t base = k << 4;
+  uint4 cur[G];
 #pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const uint32_t w = j < 4 ? cur.x : j < 8 ? cur.y : j < 12 ? cur.z : cur.w;
-      const uint32_t pos = base + (uint32_t)j;
-      if (pos >= lo && pos < end) f((w >> ((j & 3) * 8)) & 0xffu);
+  for (uint32_t g = 0; g < G; g++) cur[g] = b[min(g, nblk - 1u)];
+  for (uint32_t k = 0; k < nblk; k += G) {
+    uint4 nxt[G];
+#pragma unroll
+    for (uint32_t g = 0; g < G; g++) nxt[g] = b[min(k + G + g, nblk - 1u)];
+#pragma unroll
+    for (uint32_t g = 0; g < G; g++) {
+      const uint32_t base = (k + g) << 4;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint32_t w = j < 4 ? cur[g].x : j < 8 ? cur[g].y : j < 12 ? cur[g].z : cur[g].w;
+        const uint32_t pos = base + (uint32_t)j;
+        if (pos >= lo && pos < end) f((w >> ((j & 3) * 8)) & 0xffu);
+      }
     }
-    cur = nxt;
+#pragma unroll
+    for (uint32_t g = 0; g < G; g++) cur[g] = nxt[g];
   }
 }
 
@@ -359,6 +368,23 @@ __device__ uint32_t to_normal(uint32_t* U, const uint32_t* A, uint32_t na, const
   return block_allreduce_u32_sum(z, s_red);
 }
 
+#ifdef VN_SET_PROF
+// profiling build only (tools/c5_set_profile.py): k_set_merge cycles and counts, summed over
+// workgroups: 0 workgroup, 1 sparse <- sparse payloads (2 count), 3 dense runs of sparse payloads
+// (4 runs, 5 payloads in them), 6 dense <- sparse one at a time (7 count), 8 dense payloads (9 count),
+// 10 toNormal count, 11 payloads in all
+__device__ unsigned long long g_imp_prof[16];
+#define IPROF_T(v) const long long v = clock64()
+#define IPROF_ADD(i, a, b) \
+  if (threadIdx.x == 0) atomicAdd(&g_imp_prof[i], (unsigned long long)((b) - (a)))
+#define IPROF_INC(i, v) \
+  if (threadIdx.x == 0) atomicAdd(&g_imp_prof[i], (unsigned long long)(v))
+#else
+#define IPROF_T(v)
+#define IPROF_ADD(i, a, b)
+#define IPROF_INC(i, v)
+#endif
+
 struct MergeCtx {
   const uint32_t* tl;
   const uint32_t* start;
@@ -386,8 +412,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   __shared__ uint32_t s_red[4];
   __shared__ uint32_t s_b, s_nz, s_filled, s_tfull, s_pstar, s_newfill, s_min, s_nh;
   const uint32_t k = blockIdx.x, t = threadIdx.x;
+  IPROF_T(w0);
   const uint32_t slot = x.tl[k];
   const uint32_t p0 = x.start[slot], p1 = x.end[slot];
+  IPROF_INC(11, p1 - p0);
   uint32_t* arena = x.arena + (uint64_t)slot * kArenaWords;
   uint8_t* regs8 = reinterpret_cast<uint8_t*>(arena);
 
@@ -409,6 +437,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const DenseLds S{U, &s_b, &s_nz, &s_filled, &s_tfull, &s_pstar, &s_newfill, &s_min, s_red};
 
   for (uint32_t q = p0; q < p1; q++) {
+    IPROF_T(q0);
     if (dense) {
       // A dense key and a run of sparse payloads none of whose inserts can rebase: a rebase
       // needs an overflow code (uint8(rho - b) >= capacity, hyperloglog.go:169-176) while no
@@ -444,7 +473,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
             s_ptmp[atomicAdd(&s_nh, 1u)] = t;
           } else {
             uint32_t c = 0, nb = 0;
-            for_bytes(x.bytes + R.tmp_off, 4u * R.ntmp, [&](uint32_t by) {
+            for_bytes<8>(x.bytes + R.tmp_off, 4u * R.ntmp, [&](uint32_t by) {
               c = (c << 8) | by;
               if (++nb == 4) {
                 ins(c);
@@ -452,7 +481,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
               }
             });
             uint32_t prev = 0, v = 0, sh = 0;
-            for_bytes(x.bytes + R.list_off, R.list_len, [&](uint32_t by) {
+            for_bytes<8>(x.bytes + R.list_off, R.list_len, [&](uint32_t by) {
               if (sh < 32) v |= (by & 0x7fu) << sh;
               sh += 7;
               if (!(by & 0x80u)) {
@@ -479,6 +508,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         if (t == 0) s_nz = z;
         __syncthreads();
         q += nrun - 1;
+        IPROF_T(q1);
+        IPROF_ADD(3, q0, q1);
+        IPROF_INC(4, 1);
+        IPROF_INC(5, nrun);
         continue;
       }
     }
@@ -527,11 +560,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
             dense = true;
           }
           __syncthreads();
+          IPROF_INC(10, dense ? 1 : 0);
         } else {
           tc = union_unique<1, kCPer>(s_tmp, tc, Cb, nd, s_tmp, s_red);
           s_tmp[t] = t < tc ? s_tmp[t] : kHllNoCode;
           __syncthreads();
         }
+        IPROF_T(q1);
+        IPROF_ADD(1, q0, q1);
+        IPROF_INC(2, 1);
       } else {
         // dense <- sparse: insert every code, tmpSet first (ascending), then the list
         const uint32_t nt = P.ntmp;
@@ -539,6 +576,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         const uint32_t* cl = Cb;
         dense_insert_codes(S, [pt, cl, nt](uint32_t p) { return p < nt ? pt[p] : cl[p - nt]; }, 0, nt + nl, x.err);
         __syncthreads();
+        IPROF_T(q1);
+        IPROF_ADD(6, q0, q1);
+        IPROF_INC(7, 1);
       }
       continue;
     }
@@ -585,8 +625,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
     fills = block_allreduce_u32_sum(fills, s_red);
     if (t == 0) s_nz -= fills;
     __syncthreads();
+    IPROF_T(q1);
+    IPROF_ADD(8, q0, q1);
+    IPROF_INC(9, 1);
   }
   __syncthreads();
+  IPROF_T(w1);
+  IPROF_ADD(0, w0, w1);
   // ---- write back
   if (dense) {
     for (uint32_t i = t; i < kHllM; i += kBlock) regs8[i] = (uint8_t)U[i];
@@ -626,6 +671,17 @@ __global__ void k_set_clear_bt(uint32_t n, const uint32_t* __restrict__ list, ui
 }
 
 }  // namespace
+
+#ifdef VN_SET_PROF
+extern "C" int vn_prof_import_set_read(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_imp_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_imp_prof), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 void import_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes) {
   if (!n) return;

@@ -1322,7 +1322,9 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.ctw = e->h_tw;
   xc.cpk = e->h_cpk;
   xc.lstat = e->h_lstat;
-  xc.cstat = e->h_cstat;
+#ifndef VN_NO_CSTAT
+  xc.cstat = e->h_cstat;  // (A/B build VN_NO_CSTAT: k_exact_long_stats re-reads the samples)
+#endif
   const uint64_t max_chunks = n / e->temp_cap + 1;
   // (exact mode, no hot key, not timing: the longest keys' chunks are sorted first and their
   // replays start while the other chunks sort, in replay_cold)

@@ -237,6 +237,48 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
       }
       lds_barrier();
       const uint32_t wbase = s_wbase, wend = s_wend;
+#ifdef VN_SET_WAVESCAN  // (A/B build: round 4's scan, wave 0 alone, 64 records per step)
+      // wave 0 advances to the next mergeSparse trigger -- the record that makes the tmpSet
+      // hold kHllTmpTrigger distinct codes -- 64 records per step: a record counts if its
+      // code is neither in the tmpSet nor held by a lower lane of the same step.
+      if (t < 64) {
+        uint32_t pos = s_pos, tc = s_tc, trig = 0;
+        const uint64_t below = (t == 0) ? 0ull : (~0ull >> (64 - t));
+        while (pos < wend) {
+          const uint32_t p = pos + t;
+          const bool valid = p < wend;
+          const uint32_t c = valid ? s_rec[p - wbase] : kHllNoCode;
+          const bool fresh = valid && !hash_contains(s_hash, c);
+          uint32_t hi = 0;
+          if (fresh) {
+            hi = hash_claim(s_hash, c);
+            atomicMin(&s_first[hi], t);
+          }
+          const bool first = fresh && s_first[hi] == t;
+          const uint64_t bal = __ballot(first);
+          const uint32_t cnt = (uint32_t)__popcll(bal);
+          const uint32_t need = kHllTmpTrigger - tc;
+          uint32_t take = 64, add = cnt;
+          if (cnt >= need) {  // the need-th first occurrence triggers the merge
+            uint64_t b = bal;
+            for (uint32_t q = 1; q < need; q++) b &= b - 1;
+            const uint32_t L = (uint32_t)__builtin_ctzll(b);
+            take = L + 1;
+            add = need;
+            trig = 1;
+          }
+          if (first && t < take) s_tmp[tc + (uint32_t)__popcll(bal & below)] = c;
+          tc += add;
+          pos = min(pos + take, wend);
+          if (trig) break;
+        }
+        if (t == 0) {
+          s_pos = pos;
+          s_tc = tc;
+          s_trig = trig;
+        }
+      }
+#else
       // the workgroup advances kBlock records per step to the next mergeSparse trigger -- the
       // record that makes the tmpSet hold kHllTmpTrigger distinct codes: a record counts if its
       // code is neither in the tmpSet nor held by a lower thread of the same step (the lowest
@@ -289,6 +331,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
           s_trig = trig ? 1u : 0u;
         }
       }
+#endif
       lds_barrier();
       SPROF_T(p_scan1);
       SPROF_ADD(1, p_scan0, p_scan1);
