@@ -273,7 +273,7 @@ def overflow_payload(rng, n, n_over):
 
 def test_import_sets_dense_keys_many_sparse_payloads_bit_exact():
     """Dense keys (fresh, nearly full, rebased b > 0) receiving hundreds of sparse payloads of
-    Lomax sizes in one call -- the run of plain register maxes, its long payloads block-wide --
+    Lomax sizes in one call -- the run of plain register maxes, a wave per payload --
     mixed with payloads carrying overflow codes, dense payloads and skipped precisions, so the
     runs are cut where a rebase may happen; registers, b, nz and estimates bit-exact."""
     rng = np.random.default_rng(24)

@@ -22,6 +22,7 @@
 // merges staged in registers, registers are LDS atomic maxes, and inserts into a dense key
 // run the exact insert machinery of set_dense.h (rebase epochs included).
 #include "set_dense.h"
+#include "wave_dpp.h"
 
 namespace vn {
 
@@ -43,7 +44,9 @@ constexpr uint32_t kMaxImportTmp = 256;   // tmpSet codes per payload (Go keeps 
 constexpr uint32_t kPer = (kArenaWords + kBlock - 1) / kBlock;  // 65 codes per thread
 constexpr uint32_t kCWords = kArenaWords + 512;                 // payload codes + the key's tmpSet
 constexpr uint32_t kCPer = (kCWords + kBlock - 1) / kBlock;     // 67
+#ifdef VN_SET_LANE_RUNS
 constexpr uint32_t kLaneBytes = 2048;  // a dense key's plain run: longer sparse payloads go block-wide
+#endif
 
 __device__ __forceinline__ uint32_t be32(const uint8_t* d) {
   return ((uint32_t)d[0] << 24) | ((uint32_t)d[1] << 16) | ((uint32_t)d[2] << 8) | d[3];
@@ -78,6 +81,58 @@ __device__ __forceinline__ void for_bytes(const uint8_t* p, uint32_t len, F&& f)
     }
 #pragma unroll
     for (uint32_t g = 0; g < G; g++) cur[g] = nxt[g];
+  }
+}
+
+// ins(code) for every code of a sparse payload, by one whole wave (lanes in step, exec full): the
+// tmpSet's big-endian codes a lane each, then the varint list 256 bytes per step, four bytes per
+// lane. compressedList.decode (compressed.go:157-165) makes a code the running uint32 sum of the
+// varint values, and a varint's value the OR of (byte & 0x7f) << 7 d over its bytes (d = the byte's
+// place in it; from d = 5 on Go's uint32 shift adds nothing). The bit ranges are disjoint, so a
+// code is the sum, over every list byte up to its terminator, of that byte's contribution: each
+// byte finds where its varint starts (the last terminator before it: within the lane, else a wave
+// max-scan of the lanes' last terminators, else the one carried from the previous step), and the
+// codes are a wave sum-scan of the contributions read at the terminators. A trailing unterminated
+// varint inserts nothing, as the per-lane parse.
+template <class Ins>
+__device__ __forceinline__ void wave_insert_sparse(const uint8_t* bytes, const HllPart& R, Ins&& ins) {
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t i = lane; i < R.ntmp; i += 64) ins(be32(bytes + R.tmp_off + 4ull * i));
+  if (!R.list_len) return;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(bytes + R.list_off), a0 = s & ~(uintptr_t)3;
+  const uint32_t lo = (uint32_t)(s - a0), end = lo + R.list_len;  // positions relative to a0
+  const uint32_t* w32 = reinterpret_cast<const uint32_t*>(a0);
+  uint32_t carry = 0, vstart = lo;  // the code so far; the first byte of the varint in progress
+  uint32_t nxt = 4 * lane < end ? w32[lane] : 0u;
+  for (uint32_t base = 0; base < end; base += 256) {
+    const uint32_t p0 = base + 4 * lane, w = nxt;
+    nxt = p0 + 256 < end ? w32[(p0 + 256) >> 2] : 0u;  // the next step's dword in flight
+    uint32_t tm = 0;  // bit j: byte j is a list byte and a terminator
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t pos = p0 + (uint32_t)j;
+      if (pos >= lo && pos < end && !((w >> (8 * j)) & 0x80u)) tm |= 1u << j;
+    }
+    const uint32_t mine = tm ? p0 + 32u - (uint32_t)__builtin_clz(tm) : 0u;  // my last terminator + 1
+    const uint32_t upto = wave_incl_max(mine);
+    uint32_t st = max(wave_shr1(upto), vstart);
+    uint32_t c[4], sum = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t pos = p0 + (uint32_t)j, by = (w >> (8 * j)) & 0xffu, d = pos - st;
+      c[j] = (pos >= lo && pos < end && d < 5u) ? (by & 0x7fu) << (7u * d) : 0u;
+      sum += c[j];
+      if (tm & (1u << j)) st = pos + 1;
+    }
+    const uint32_t incl = wave_incl_add_u32(sum);
+    uint32_t run = incl - sum + carry;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      run += c[j];
+      if (tm & (1u << j)) ins(run);
+    }
+    carry += (uint32_t)__shfl((int)incl, 63);
+    vstart = max(vstart, (uint32_t)__shfl((int)upto, 63));
   }
 }
 
@@ -468,6 +523,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           decode_hash(code, &ri, &r);
           if (r > b) atomicMax(&U[ri], min(r - b, kHllCapacity - 1));
         };
+#ifdef VN_SET_LANE_RUNS
         if (t < nrun && R.kind == 0) {
           if (4u * R.ntmp + R.list_len > kLaneBytes) {
             s_ptmp[atomicAdd(&s_nh, 1u)] = t;
@@ -502,6 +558,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           for (uint32_t i = t; i < nl; i += kBlock) ins(Cb[i]);
           __syncthreads();
         }
+#else
+        // the run's payloads a wave each, drawn in turn from s_nh (a lane per payload walked its
+        // whole list alone: the run waited for its longest payload, ≈40 cycles per byte)
+        for (;;) {
+          uint32_t i = 0;
+          if ((t & 63u) == 0) i = atomicAdd(&s_nh, 1u);
+          i = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)__shfl((int)i, 0));
+          if (i >= nrun) break;
+          const HllPart H = x.parts[(uint32_t)x.keys[q + i]];
+          if (H.kind == 0) wave_insert_sparse(x.bytes, H, ins);
+        }
+        __syncthreads();
+#endif
         uint32_t z = 0;
         for (uint32_t i = t; i < kHllM; i += kBlock) z += U[i] == 0;
         z = block_allreduce_u32_sum(z, s_red);
