@@ -29,10 +29,10 @@ struct GobIn {
   uint32_t lo;       // payload start within blk[0]
   uint32_t n, i;
   bool err;
-  uint32_t nb, cb;   // blocks, block held in c0:c1
-  uint64_t c0, c1, n0, n1;  // the current block and the next one (low, high 8 bytes)
+  uint32_t nb, cb;   // blocks; the first held block
+  uint64_t c0, c1, n0, n1, m0, m1;  // blocks cb, cb + 1, cb + 2 (low, high 8 bytes; clamped to nb - 1)
   __device__ __forceinline__ void load(uint32_t k, uint64_t& a, uint64_t& b) const {
-    const uint4 v = blk[k];
+    const uint4 v = blk[min(k, nb - 1u)];
     a = (uint64_t)v.x | ((uint64_t)v.y << 32);
     b = (uint64_t)v.z | ((uint64_t)v.w << 32);
   }
@@ -42,24 +42,37 @@ struct GobIn {
     lo = (uint32_t)(s - a0);
     nb = (lo + len + 15u) >> 4;
     cb = 0;
-    c0 = c1 = n0 = n1 = 0;
+    c0 = c1 = n0 = n1 = m0 = m1 = 0;
     if (nb) {
       load(0, c0, c1);
-      load(min(1u, nb - 1u), n0, n1);
+      load(1, n0, n1);
+      load(2, m0, m1);
     }
   }
-  __device__ __forceinline__ uint32_t at(uint32_t pos) {  // byte pos (< n)
-    const uint32_t a = lo + pos, k = a >> 4;
-    if (k != cb) {
-      if (k == cb + 1) {
-        c0 = n0;
-        c1 = n1;
-      } else {
-        load(k, c0, c1);
-      }
-      load(min(k + 1u, nb - 1u), n0, n1);
-      cb = k;
+  // hold blocks k, k + 1, k + 2 (the two after the current one in flight while it is parsed)
+  __device__ __forceinline__ void seek(uint32_t k) {
+    if (k == cb) return;
+    if (k == cb + 1) {
+      c0 = n0;
+      c1 = n1;
+      n0 = m0;
+      n1 = m1;
+      load(k + 2, m0, m1);
+    } else if (k == cb + 2) {
+      c0 = m0;
+      c1 = m1;
+      load(k + 1, n0, n1);
+      load(k + 2, m0, m1);
+    } else {
+      load(k, c0, c1);
+      load(k + 1, n0, n1);
+      load(k + 2, m0, m1);
     }
+    cb = k;
+  }
+  __device__ __forceinline__ uint32_t at(uint32_t pos) {  // byte pos (< n)
+    const uint32_t a = lo + pos;
+    seek(a >> 4);
     // mask blend, not a select: a select of two fields can become a load through a selected
     // pointer, which keeps the reader in scratch memory
     const uint64_t m = 0ull - (uint64_t)((a >> 3) & 1u), h = (c0 & ~m) | (c1 & m);
@@ -69,10 +82,63 @@ struct GobIn {
   // mask blends (no register indexing: it would put the reader in scratch)
   __device__ __forceinline__ uint64_t win64(uint32_t o) const {
     const uint32_t w = o >> 3, s = (o & 7u) * 8u;
-    const uint64_t m0 = 0ull - (uint64_t)(w == 0), m1 = 0ull - (uint64_t)(w == 1), m2 = 0ull - (uint64_t)(w == 2);
-    const uint64_t lo_w = (c0 & m0) | (c1 & m1) | (n0 & m2) | (n1 & ~(m0 | m1 | m2));
-    const uint64_t hi_w = (c1 & m0) | (n0 & m1) | (n1 & m2);
+    const uint64_t m0_ = 0ull - (uint64_t)(w == 0), m1_ = 0ull - (uint64_t)(w == 1), m2_ = 0ull - (uint64_t)(w == 2);
+    const uint64_t lo_w = (c0 & m0_) | (c1 & m1_) | (n0 & m2_) | (n1 & ~(m0_ | m1_ | m2_));
+    const uint64_t hi_w = (c1 & m0_) | (n0 & m1_) | (n1 & m2_);
     return s ? (lo_w >> s) | (hi_w << (64u - s)) : lo_w;
+  }
+  // One centroid in the layout GobEncode gives a tdigest Centroid {Mean, Weight float64, ...}
+  // whose type lists Mean and Weight first: {1, mean, 1, weight, 0}, or {2, weight, 0} when the
+  // mean is zero (gob omits zero fields). Parsed from a 24-byte window at byte i without
+  // per-token branches; false (nothing consumed) for any other form, which the general field
+  // loop then reads -- so both give the same values and the same errors.
+  __device__ __forceinline__ bool centroid(double& mean, double& weight) {
+    const uint32_t a = lo + i;
+    seek(a >> 4);
+    const uint32_t o = a & 15u, sh = (o & 7u) * 8u;
+    const uint64_t mk = 0ull - (uint64_t)(o >> 3);  // the window starts in c1
+    const uint64_t w0 = (c0 & ~mk) | (c1 & mk), w1 = (c1 & ~mk) | (n0 & mk), w2 = (n0 & ~mk) | (n1 & mk),
+                   w3 = (n1 & ~mk) | (m0 & mk);
+    const uint64_t W0 = sh ? (w0 >> sh) | (w1 << (64u - sh)) : w0, W1 = sh ? (w1 >> sh) | (w2 << (64u - sh)) : w1,
+                   W2 = sh ? (w2 >> sh) | (w3 << (64u - sh)) : w2;
+    auto byte = [&](uint32_t p) -> uint32_t {  // byte p < 24 of the window
+      const uint64_t q0 = 0ull - (uint64_t)((p >> 3) == 0), q1 = 0ull - (uint64_t)((p >> 3) == 1);
+      const uint64_t x = (W0 & q0) | (W1 & q1) | (W2 & ~(q0 | q1));
+      return (uint32_t)(x >> ((p & 7u) * 8u)) & 0xffu;
+    };
+    // a gob unsigned at p read as float64 bits (f(): the value's bytes reversed); its length, 0 if
+    // the count byte is over 8
+    auto fl = [&](uint32_t p, uint64_t& bits) -> uint32_t {
+      const uint32_t b = byte(p);
+      if (b < 0x80u) {
+        bits = (uint64_t)b << 56;
+        return 1;
+      }
+      const uint32_t cnt = 256u - b, q = p + 1, s2 = (q & 7u) * 8u;  // q <= 12
+      const uint64_t qm = 0ull - (uint64_t)(q >> 3);
+      const uint64_t lw = (W0 & ~qm) | (W1 & qm), hw = (W1 & ~qm) | (W2 & qm);
+      const uint64_t y = s2 ? (lw >> s2) | (hw << (64u - s2)) : lw;  // the cnt bytes, little-endian
+      bits = cnt <= 8u ? y << (64u - 8u * cnt) : 0ull;
+      return cnt <= 8u ? 1u + cnt : 0u;
+    };
+    const uint32_t d1 = byte(0);
+    uint64_t mb = 0, wb = 0;
+    uint32_t p = 1;
+    if (d1 == 1u) {
+      const uint32_t lm = fl(1, mb);
+      if (!lm || byte(1 + lm) != 1u) return false;
+      p = 2 + lm;
+    } else if (d1 != 2u) {
+      return false;
+    }
+    const uint32_t lw = fl(p, wb);
+    if (!lw || byte(p + lw) != 0u) return false;
+    const uint32_t len = p + lw + 1;
+    if (len > n - i) return false;
+    i += len;
+    mean = bitsd(mb);
+    weight = bitsd(wb);
+    return true;
   }
   __device__ __forceinline__ uint64_t u() {  // gob unsigned integer
     if (i >= n) {
@@ -280,11 +346,12 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
         uint32_t fk = 0;  // per field: 1 Mean, 2 Weight (float64), 0 skipped -- 2 bits each
         for (int k = 0; k < T.nf; k++)
           fk |= (uint32_t)(T.fid[k] == 4 ? (T.fname[k] == 1 ? 1 : T.fname[k] == 2 ? 2 : 0) : 0) << (2 * k);
+        const bool common = T.nf >= 2 && (fk & 15u) == (1u | 2u << 2);  // Mean, Weight first
         const uint64_t c = r.u();
         for (uint64_t j = 0; j < c && !r.err; j++) {
           double m = 0.0, wt = 0.0;  // gob omits zero fields
           int64_t f = -1;
-          for (;;) {
+          if (!(common && r.i < r.n && r.centroid(m, wt))) for (;;) {
             const uint64_t dl = r.u();
             if (r.err || dl == 0) break;
             f += (int64_t)dl;

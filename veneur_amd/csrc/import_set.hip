@@ -322,45 +322,74 @@ __device__ uint32_t unique_sorted(uint32_t* A, uint32_t n, uint32_t* s_red) {
   return total;
 }
 
-// OUT = sorted A[0..na) U sorted B[0..nb), both free of repeats; OUT may alias A or B (every
-// input is staged in registers before anything is written).  An element's place is its index
-// plus the elements of the other list below it, minus the common elements below it (an
-// exclusive scan of the "also in the other list" flags).  Capacity: na <= 256*KA, nb <= 256*KB.
-template <int KA, int KB>
+// lower_bound of v in sorted a[0..n) knowing it is at least l (the bound of a smaller value): a
+// thread's elements are consecutive, so the next bound is usually a step or two on -- up to four
+// linear steps, then a binary search over the rest (a search per element from 0 was ~14
+// dependent LDS reads each for a 16k-code list)
+__device__ __forceinline__ uint32_t lower_bound_after(const uint32_t* a, uint32_t l, uint32_t n, uint32_t v) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if (l >= n || a[l] >= v) return l;
+    l++;
+  }
+  uint32_t h = n;
+  while (l < h) {
+    const uint32_t m = (l + h) >> 1;
+    if (a[m] < v) l = m + 1;
+    else h = m;
+  }
+  return l;
+}
+
+// OUT = sorted A[0..na) U sorted B[0..nb), both free of repeats.  An element's place is its index
+// plus the elements of the other list below it, minus the common elements below it (an exclusive
+// scan of the "also in the other list" flags).  OUT may be A (ALIAS 1) or B (ALIAS 2): that side's
+// values are staged in registers before anything is written, the other side is read again after
+// the scan's barriers; places are kept as u16 pairs (< 2^16: na + nb <= 256 (KA + KB)) and the
+// flags as bits, so the 16k-code union (KA = 65, KB = 67) stays in registers.
+template <int KA, int KB, int ALIAS>
 __device__ uint32_t union_unique(const uint32_t* A, uint32_t na, const uint32_t* B, uint32_t nb, uint32_t* OUT,
                                  uint32_t* s_red) {
+  static_assert(kBlock * (KA + KB) <= 65536, "u16 places");
   const uint32_t t = threadIdx.x;
   const uint32_t pa = (na + kBlock - 1) / kBlock, loA = min(na, t * pa), hiA = min(na, loA + pa);
   const uint32_t pb = (nb + kBlock - 1) / kBlock, loB = min(nb, t * pb), hiB = min(nb, loB + pb);
-  uint32_t av[KA], apos[KA], bv[KB], bpos[KB];
-  bool ain[KA], bin[KB];
-  uint32_t ca = 0, cb = 0;
+  uint32_t av[ALIAS == 1 ? KA : 1], bv[ALIAS == 2 ? KB : 1];
+  uint32_t apos[(KA + 1) / 2], bpos[(KB + 1) / 2], ain[(KA + 31) / 32], bin[(KB + 31) / 32];
+#pragma unroll
+  for (int q = 0; q < (KA + 1) / 2; q++) apos[q] = 0;
+#pragma unroll
+  for (int q = 0; q < (KB + 1) / 2; q++) bpos[q] = 0;
+#pragma unroll
+  for (int q = 0; q < (KA + 31) / 32; q++) ain[q] = 0;
+#pragma unroll
+  for (int q = 0; q < (KB + 31) / 32; q++) bin[q] = 0;
+  uint32_t ca = 0, cb = 0, l = 0;
 #pragma unroll
   for (int q = 0; q < KA; q++) {
     const uint32_t i = loA + q;
-    ain[q] = false;
-    av[q] = 0;
-    apos[q] = 0;
     if (i < hiA) {
-      av[q] = A[i];
-      const uint32_t l = lower_bound_u32(B, nb, av[q]);
-      ain[q] = l < nb && B[l] == av[q];
-      apos[q] = i + l;
-      ca += ain[q];
+      const uint32_t v = A[i];
+      if (ALIAS == 1) av[q] = v;
+      l = q == 0 ? lower_bound_u32(B, nb, v) : lower_bound_after(B, l, nb, v);
+      const uint32_t in = l < nb && B[l] == v;
+      ain[q >> 5] |= in << (q & 31);
+      apos[q >> 1] |= (i + l) << (16 * (q & 1));
+      ca += in;
     }
   }
+  l = 0;
 #pragma unroll
   for (int q = 0; q < KB; q++) {
     const uint32_t j = loB + q;
-    bin[q] = false;
-    bv[q] = 0;
-    bpos[q] = 0;
     if (j < hiB) {
-      bv[q] = B[j];
-      const uint32_t l = lower_bound_u32(A, na, bv[q]);
-      bin[q] = l < na && A[l] == bv[q];
-      bpos[q] = j + l;
-      cb += bin[q];
+      const uint32_t v = B[j];
+      if (ALIAS == 2) bv[q] = v;
+      l = q == 0 ? lower_bound_u32(A, na, v) : lower_bound_after(A, l, na, v);
+      const uint32_t in = l < na && A[l] == v;
+      bin[q >> 5] |= in << (q & 31);
+      bpos[q >> 1] |= (j + l) << (16 * (q & 1));
+      cb += in;
     }
   }
   uint32_t common, common2;
@@ -369,14 +398,16 @@ __device__ uint32_t union_unique(const uint32_t* A, uint32_t na, const uint32_t*
 #pragma unroll
   for (int q = 0; q < KA; q++)
     if (loA + q < hiA) {
-      OUT[apos[q] - exa] = av[q];
-      exa += ain[q];
+      const uint32_t v = ALIAS == 1 ? av[q] : A[loA + q];
+      OUT[((apos[q >> 1] >> (16 * (q & 1))) & 0xffffu) - exa] = v;
+      exa += (ain[q >> 5] >> (q & 31)) & 1u;
     }
 #pragma unroll
   for (int q = 0; q < KB; q++)
     if (loB + q < hiB) {
-      if (!bin[q]) OUT[bpos[q] - exb] = bv[q];
-      exb += bin[q];
+      const uint32_t in = (bin[q >> 5] >> (q & 31)) & 1u;
+      if (!in) OUT[((bpos[q >> 1] >> (16 * (q & 1))) & 0xffffu) - exb] = ALIAS == 2 ? bv[q] : B[loB + q];
+      exb += in;
     }
   __syncthreads();
   return na + nb - common;
@@ -427,7 +458,8 @@ __device__ uint32_t to_normal(uint32_t* U, const uint32_t* A, uint32_t na, const
 // profiling build only (tools/c5_set_profile.py): k_set_merge cycles and counts, summed over
 // workgroups: 0 workgroup, 1 sparse <- sparse payloads (2 count), 3 dense runs of sparse payloads
 // (4 runs, 5 payloads in them), 6 dense <- sparse one at a time (7 count), 8 dense payloads (9 count),
-// 10 toNormal count, 11 payloads in all
+// 10 toNormal count, 11 payloads in all; sparse <- sparse phases: 12 tmpSet load and sort, 13 list
+// decode, 14 unique + union + tmpSet lookup, 15 mergeSparse triggers
 __device__ unsigned long long g_imp_prof[16];
 #define IPROF_T(v) const long long v = clock64()
 #define IPROF_ADD(i, a, b) \
@@ -591,11 +623,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       s_ptmp[t] = t < P.ntmp ? be32(x.bytes + P.tmp_off + 4ull * t) : kHllNoCode;
       __syncthreads();
       bitonic256(s_ptmp);
+      IPROF_T(qa);
       const uint32_t nl = decode_list(x.bytes + P.list_off, P.list_len, Cb, s_red);
+      IPROF_T(qb);
       if (!dense) {
         // sparse <- sparse: tmpSet gets every code, then maybeToNormal
         const uint32_t npt = unique_sorted<1>(s_ptmp, P.ntmp, s_red);
-        const uint32_t nd = union_unique<1, kCPer>(s_ptmp, npt, Cb, nl, Cb, s_red);
+        const uint32_t nd = union_unique<1, kCPer, 2>(s_ptmp, npt, Cb, nl, Cb, s_red);
         uint32_t hit = 0;
         if (t < tc) {
           const uint32_t c = s_tmp[t], l = lower_bound_u32(Cb, nd, c);
@@ -603,9 +637,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         }
         const uint32_t inter = block_allreduce_u32_sum(hit, s_red);
         const uint32_t total = tc + nd - inter;
+        IPROF_T(qc);
+        IPROF_ADD(12, q0, qa);
+        IPROF_ADD(13, qa, qb);
+        IPROF_ADD(14, qb, qc);
+        IPROF_INC(15, total * 100u > kHllM ? 1 : 0);
         if (total * 100u > kHllM) {
           // mergeSparse: list = list U tmpSet; then toNormal if its byte length > m
-          const uint32_t nd2 = union_unique<1, kCPer>(s_tmp, tc, Cb, nd, Cb, s_red);
+          const uint32_t nd2 = union_unique<1, kCPer, 2>(s_tmp, tc, Cb, nd, Cb, s_red);
           uint32_t hit2 = 0;
           for (uint32_t i = t; i < nd2; i += kBlock) {
             const uint32_t c = Cb[i], l = lower_bound_u32(U, lc, c);
@@ -615,7 +654,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           s_tmp[t] = kHllNoCode;
           tc = 0;
           if (cnt <= kArenaWords) {
-            lc = union_unique<kPer, kCPer>(U, lc, Cb, nd2, U, s_red);
+            lc = union_unique<kPer, kCPer, 1>(U, lc, Cb, nd2, U, s_red);
             lbytes = list_bytes(U, lc, s_red);
             list_dirty = true;
             if (lbytes > kHllM) {
@@ -631,7 +670,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           __syncthreads();
           IPROF_INC(10, dense ? 1 : 0);
         } else {
-          tc = union_unique<1, kCPer>(s_tmp, tc, Cb, nd, s_tmp, s_red);
+          tc = union_unique<1, kCPer, 1>(s_tmp, tc, Cb, nd, s_tmp, s_red);
           s_tmp[t] = t < tc ? s_tmp[t] : kHllNoCode;
           __syncthreads();
         }
