@@ -962,7 +962,7 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
     return VN_EINVAL;
   }
   uint32_t need = (uint32_t)(2.0 * e->cfg.compression) + 4;
-  e->cap_cent = ((need + 63) / 64) * 64;
+  e->cap_cent = ((need + 15) / 16) * 16;  // (delta 100: 208, whose replay tile gives 14 waves per CU)
   if (e->cap_cent < 64) e->cap_cent = 64;
   if (e->cap_cent > 2048 || (uint64_t)e->cap[VN_HISTO] * e->cap_cent >= (1ull << 31)) {
     delete e;

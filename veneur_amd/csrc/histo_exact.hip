@@ -48,8 +48,9 @@ __host__ __device__ inline size_t exact_smem_bytes_hd(uint32_t capc, uint32_t tc
   while ((1u << levels) <= capc) levels++;
   const uint32_t kin = JW <= 2 * capc ? 0 : JW;  // lds_layout: kin in the main tile when it fits
   (void)levels;
-  return sizeof(double) * (2 * capc + 4 * TP + 2 * JW + kin) + sizeof(uint16_t) * JW + sizeof(uint16_t) * 2 * JW + 16 +
-         VN_EXACT_LDS_PAD;
+  // lds_layout: the pending temps in the chain tables' region when it holds them
+  const uint32_t tables = sizeof(uint16_t) * 3 * JW, temps = 6 * JW >= 16 * TP ? 0u : 16u * TP + 8u;
+  return sizeof(double) * (2 * capc + 2 * TP + 2 * JW + kin) + tables + temps + 16 + VN_EXACT_LDS_PAD;
 }
 
 #ifdef VN_ASM_MARK  // (reading the assembly: a comment at a phase boundary)
@@ -292,9 +293,7 @@ __device__ __forceinline__ Lds lds_layout(char* smem, uint32_t capc, uint32_t TP
   while ((1u << L.levels) <= capc) L.levels++;
   L.mm = (ldsf64*)smem;
   L.mw = L.mm + capc;
-  L.tv = L.mw + capc;
-  L.tw = L.tv + TP;
-  L.sv = L.tw + TP;
+  L.sv = L.mw + capc;
   L.sw = L.sv + TP;
   L.gm = L.sw + TP;
   L.gw = L.gm + L.JW;
@@ -305,6 +304,12 @@ __device__ __forceinline__ Lds lds_layout(char* smem, uint32_t capc, uint32_t TP
   L.kin = kin_in_main ? L.mm : L.gw + L.JW;
   L.starts = (ldsu16*)(L.gw + L.JW + (kin_in_main ? 0 : L.JW));
   L.jump16 = L.starts + L.JW;
+  // the pending temps (Add order) are dead during every merge -- a merge takes all of them, after
+  // sort_temps has read them into sv/sw, and appends resume after it -- so they live in the chain
+  // tables' region when it holds them (1 KiB less per key at delta 100)
+  L.tv = 6 * L.JW >= 16 * TP ? (ldsf64*)L.starts
+                             : (ldsf64*)((reinterpret_cast<uintptr_t>(L.jump16 + 2 * L.JW) + 7) & ~(uintptr_t)7);
+  L.tw = L.tv + TP;
   return L;
 }
 
@@ -2125,8 +2130,9 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       B.kb[2 * kBN + nm] = 1.0;
     }
   }
-  // +inf past the last mean: A's searches need no bound checks (they read below index 255)
-  for (uint32_t j = nm + t; j < 256u; j += NT) L.mm[j] = kInf;
+  // +inf past the last mean up to 192 (nm <= kBM = 160): A's searches read index min(i, 191), so
+  // they need no other bound checks, and the tile needs only 192 entries (capc >= 192)
+  for (uint32_t j = nm + t; j < 192u; j += NT) L.mm[j] = kInf;
   fast_sync<NW>();
   PROF_T(b1);
   ASM_MARK("A_BEGIN");
@@ -2142,7 +2148,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   double gv[kA];
   {
     const double p0 = L.mm[127], p1 = L.mm[63], p2 = L.mm[191];
-    const double p3 = L.mm[31], p4 = L.mm[95], p5 = L.mm[159], p6 = L.mm[223];
+    const double p3 = L.mm[31], p4 = L.mm[95], p5 = L.mm[159], p6 = kInf;  // (223 >= nm)
     bool safe = true;
     // (chunk, position) of temp g = t + u * NT: one division, then steps of NT = qs * tcap + rs
     const uint32_t qs = NT / tcap, rs = NT - qs * tcap;
@@ -2174,7 +2180,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     for (uint32_t step = 16; step >= 1; step >>= 1) {
       double mv[kA];
 #pragma unroll
-      for (uint32_t u = 0; u < kA; u++) mv[u] = L.mm[ps[u] + step - 1];
+      for (uint32_t u = 0; u < kA; u++) mv[u] = L.mm[min(ps[u] + step - 1, 191u)];
 #pragma unroll
       for (uint32_t u = 0; u < kA; u++) ps[u] = mv[u] < gv[u] ? ps[u] + step : ps[u];
     }
@@ -2881,7 +2887,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     while (c < sp.npure) {
       const uint32_t left = sp.npure - c;
       if (!(fok && nm >= 1 && nm <= kBM && left >= 2 && mainW >= kBatchMinW && tcap <= kBTmax && 8 * tcap >= kSR &&
-            capc >= 256)) {
+            capc >= 192)) {
         // not (yet) batchable: a run of single merges, then look again
         const uint32_t c1 = min(sp.npure, c + kBatchBackoff);
         PROF_T(s3);
