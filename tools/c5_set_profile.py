@@ -17,19 +17,20 @@ import veneur_amd._abi as A  # noqa: E402
 NAMES = {0: "workgroups", 1: "sparse <- sparse", 2: "  payloads", 3: "dense <- runs of sparse", 4: "  runs",
          5: "  payloads", 6: "dense <- sparse, one at a time", 7: "  payloads", 8: "dense payloads", 9: "  payloads",
          10: "toNormal", 11: "payloads in all", 12: "  sparse: tmpSet load + sort", 13: "  sparse: list decode",
-         14: "  sparse: unique + union + lookup", 15: "  sparse: mergeSparse triggers"}
+         14: "  sparse: unique + union + lookup", 15: "  sparse: mergeSparse triggers",
+         16: "    trigger: tmpSet union + lookups", 17: "    trigger: list union", 18: "  sparse: tmpSet union (no trigger)"}
 
 
 def main():
     A.lib.vn_prof_import_set_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 24)()
     A.lib.vn_prof_import_set_read(buf, 1)
     sys.argv = ["bench.py", "--c5-only"]
     bench.main()
     A.lib.vn_prof_import_set_read(buf, 0)
     tot = max(1, buf[0])
     for i, name in NAMES.items():
-        cyc = i in (0, 1, 3, 6, 8, 12, 13, 14)
+        cyc = i in (0, 1, 3, 6, 8, 12, 13, 14, 16, 17, 18)
         print("%-34s %16d %s" % (name, buf[i], ("%5.1f%%" % (100.0 * buf[i] / tot)) if cyc else ""), flush=True)
 
 

@@ -243,7 +243,7 @@ struct vn_engine {
   uint32_t* h_tl2 = nullptr;     // slots of hot keys
   uint32_t* h_ccnt = nullptr;    // per touched key: pure chunks to pre-sort
   uint32_t* h_coff = nullptr;    // scan of h_ccnt (touched + 1)
-  uint32_t* h_cown = nullptr;    // owner key index of every pure chunk
+  uint64_t* h_cown = nullptr;    // owner key index << 32 | first record, of every pure chunk
   double* h_tw = nullptr;        // per chunk (at its first record): Add-order weight sum
   // geometric remainder of hot keys (ingest_histo.hip)
   uint64_t* h_geo = nullptr;     // piece boundaries b_0 = hot_prefix, b_{i+1} = b_i + max(1, b_i / 10)

@@ -74,7 +74,7 @@ struct ExactCtx {
   // tempW as the prefix, or 0xffffffff when the chunk cannot be batched (a weight that is not an
   // integer, or a tempW of 65536 or more)
   uint32_t* cpk;
-  uint32_t* cown;  // [chunks] the key index of every pure chunk (null: searched in coff)
+  uint64_t* cown;  // [chunks] key index << 32 | first record of every pure chunk (null: searched in coff)
   // the batched keys' pure-chunk Local* statistics, reduced in parallel before their replays
   // (k_exact_long_stats): [kLongStatKeys][kLongStatSlices][8] partials (null: the replay's own)
   double* lstat;

@@ -997,11 +997,20 @@ __global__ void k_exact_chunk_count(ExactCtx x) {
 }
 
 // owner key of every pure chunk, so a sorting wave starts without a dependent binary search:
-// one thread per chunk (a thread per key would write a 17M-sample key's 400k chunks alone)
+// the first record of pure chunk g of key k
+__device__ __forceinline__ uint32_t chunk_base(const ExactCtx& x, uint32_t g, uint32_t k) {
+  const uint32_t s = x.keys[k];
+  const ExactSplit sp = exact_split(x.hpend[s], x.nex[k], x.tcap);
+  return x.start[s] + sp.off0 + (g - x.coff[k]) * x.tcap;
+}
+
+// one thread per chunk (a thread per key would write a 17M-sample key's 400k chunks alone): its
+// key and first record, so the sorter's wave starts with one load instead of a chain of five
 __global__ void k_exact_chunk_owner(ExactCtx x) {
   const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= x.coff[x.nkeys]) return;
-  x.cown[g] = last_le_u32(x.coff, x.nkeys, g);
+  const uint32_t k = last_le_u32(x.coff, x.nkeys, g);
+  x.cown[g] = (uint64_t)k << 32 | chunk_base(x, g, k);
 }
 
 #ifndef VN_BATCH_MIN_LEN
@@ -1029,17 +1038,15 @@ __device__ __forceinline__ double wave_max_go(double v) {
   return max_go(v, dpp_d<0x143, 0xc>(v, -kInf));
 }
 
-// sort pure chunk g of key k (one wave)
-__device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t g, const uint32_t k, char* smem) {
+// sort pure chunk g of key k, whose first record is base (one wave)
+__device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t g, const uint32_t k,
+                                               const uint64_t base, char* smem) {
   const uint32_t lane = threadIdx.x;
   const uint32_t tcap = x.tcap, TP = round64(tcap + 1);
   ldsf64* tv = (ldsf64*)smem;
   ldsf64* tw = tv + TP;
   ldsf64* sv = tw + TP;
   ldsf64* sw = sv + TP;
-  const uint32_t s = x.keys[k];
-  const ExactSplit sp = exact_split(x.hpend[s], x.nex[k], tcap);
-  const uint64_t base = (uint64_t)x.start[s] + sp.off0 + (uint64_t)(g - x.coff[k]) * tcap;
   for (uint32_t t = lane; t < tcap; t += 64) {
     const uint32_t tag = (uint32_t)x.B[base + t];
     const double wt = tag_weight(tag, x.impw);
@@ -1134,9 +1141,17 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x, uint32_t to
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t g = blockIdx.x;
   if (g >= x.coff[x.nkeys]) return;
-  const uint32_t k = x.cown ? x.cown[g] : last_le_u32(x.coff, x.nkeys, g);
+  uint32_t k, base;
+  if (x.cown) {
+    const uint64_t o = x.cown[g];
+    k = (uint32_t)(o >> 32);
+    base = (uint32_t)o;
+  } else {
+    k = last_le_u32(x.coff, x.nkeys, g);
+    base = chunk_base(x, g, k);
+  }
   if (top && is_top_key(x, k, top)) return;
-  chunk_sort_one(x, g, k, smem);
+  chunk_sort_one(x, g, k, base, smem);
 }
 
 // the chunks of the first `top` keys of x.order64: block (b, y) takes key y's chunks b, b + G, ...
@@ -1145,7 +1160,7 @@ __global__ __launch_bounds__(64) void k_exact_chunk_sort_top(ExactCtx x) {
   const uint32_t k = (uint32_t)x.order64[blockIdx.y];
   const uint32_t a = x.coff[k], b = x.coff[k + 1];
   for (uint32_t g = a + blockIdx.x; g < b; g += gridDim.x) {
-    chunk_sort_one(x, g, k, smem);
+    chunk_sort_one(x, g, k, chunk_base(x, g, k), smem);
     wave_lds_sync();  // (the next chunk reuses the LDS tiles)
   }
 }

@@ -408,12 +408,7 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
 
 // per payload: its centroid count, the whole payload validated (slot in range, offsets
 // non-decreasing, a well-formed digest, every centroid a valid Add), so the emit cannot fail
-#ifdef VN_GOB_WAVES  // (A/B build knob: waves per SIMD the gob passes are compiled for)
-#define GOB_ATTR __attribute__((amdgpu_waves_per_eu(VN_GOB_WAVES)))
-#else
-#define GOB_ATTR
-#endif
-__global__ GOB_ATTR void k_gob_count(uint64_t n, const uint32_t* __restrict__ slot, uint32_t cap,
+__global__ void k_gob_count(uint64_t n, const uint32_t* __restrict__ slot, uint32_t cap,
                             const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -431,7 +426,7 @@ __global__ GOB_ATTR void k_gob_count(uint64_t n, const uint32_t* __restrict__ sl
 
 // the centroids of payloads 0..n-1 appended to the run at base + coff[i]; each payload's slot and
 // first centroid into the run's payload table at pb + i
-__global__ GOB_ATTR void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+__global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
                            const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff, uint64_t base,
                            double* __restrict__ omean, double* __restrict__ ow, uint32_t* __restrict__ pslot,
                            uint32_t* __restrict__ pbeg, uint64_t pb, uint32_t* __restrict__ err) {

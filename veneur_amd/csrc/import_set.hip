@@ -459,8 +459,9 @@ __device__ uint32_t to_normal(uint32_t* U, const uint32_t* A, uint32_t na, const
 // workgroups: 0 workgroup, 1 sparse <- sparse payloads (2 count), 3 dense runs of sparse payloads
 // (4 runs, 5 payloads in them), 6 dense <- sparse one at a time (7 count), 8 dense payloads (9 count),
 // 10 toNormal count, 11 payloads in all; sparse <- sparse phases: 12 tmpSet load and sort, 13 list
-// decode, 14 unique + union + tmpSet lookup, 15 mergeSparse triggers
-__device__ unsigned long long g_imp_prof[16];
+// decode, 14 unique + union + tmpSet lookup, 15 mergeSparse triggers; of which 16 tmpSet union +
+// list lookups, 17 the list union; 18 the tmpSet union of the other payloads
+__device__ unsigned long long g_imp_prof[24];
 #define IPROF_T(v) const long long v = clock64()
 #define IPROF_ADD(i, a, b) \
   if (threadIdx.x == 0) atomicAdd(&g_imp_prof[i], (unsigned long long)((b) - (a)))
@@ -653,8 +654,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           const uint32_t cnt = lc + nd2 - block_allreduce_u32_sum(hit2, s_red);
           s_tmp[t] = kHllNoCode;
           tc = 0;
+          IPROF_T(qd);
+          IPROF_ADD(16, qc, qd);
           if (cnt <= kArenaWords) {
             lc = union_unique<kPer, kCPer, 1>(U, lc, Cb, nd2, U, s_red);
+            IPROF_T(qe);
+            IPROF_ADD(17, qd, qe);
             lbytes = list_bytes(U, lc, s_red);
             list_dirty = true;
             if (lbytes > kHllM) {
@@ -673,6 +678,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           tc = union_unique<1, kCPer, 1>(s_tmp, tc, Cb, nd, s_tmp, s_red);
           s_tmp[t] = t < tc ? s_tmp[t] : kHllNoCode;
           __syncthreads();
+          IPROF_T(qf);
+          IPROF_ADD(18, qc, qf);
         }
         IPROF_T(q1);
         IPROF_ADD(1, q0, q1);
@@ -781,10 +788,10 @@ __global__ void k_set_clear_bt(uint32_t n, const uint32_t* __restrict__ list, ui
 }  // namespace
 
 #ifdef VN_SET_PROF
-extern "C" int vn_prof_import_set_read(unsigned long long* out16, int reset) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_imp_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+extern "C" int vn_prof_import_set_read(unsigned long long* out24, int reset) {
+  if (hipMemcpyFromSymbol(out24, HIP_SYMBOL(g_imp_prof), sizeof(unsigned long long) * 24) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[24] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_imp_prof), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;
