@@ -22,6 +22,7 @@ namespace vn {
 
 constexpr uint32_t kArenaWords = 16640;  // == kHllListCap
 constexpr uint32_t kTmpCap = 164;
+constexpr uint32_t kImportCuts = 1024;  // slices of one histo import call found per device pass
 
 // Import staging (vn_import_histos / vn_import_sets): payloads as received, per-payload
 // parse results, and the decoded centroids.  Grown on demand.
@@ -32,6 +33,8 @@ struct ImportScratch {
   uint8_t* in_bytes = nullptr;    // [cap_bytes]
   uint32_t* cnt = nullptr;        // [cap_n + 1] per payload: centroids
   uint32_t* coff = nullptr;       // [cap_n + 1] scan of cnt
+  uint32_t* cpos = nullptr;       // [cap_n] per payload: where its centroids start when all are in the
+                                  // one-window layout (k_gob_emit_fast), else ~0
   void* parts = nullptr;          // [cap_n] parsed HLL payload headers (import_set.hip)
   uint32_t* cslot = nullptr;      // [cap_cent] decoded centroids: slot, mean, weight
   double* cmean = nullptr;
@@ -44,6 +47,9 @@ struct ImportScratch {
   uint64_t* pkey = nullptr;       // [2 cap_pay] (slot << 32 | payload) sort keys, two buffers
   uint32_t* pcnt = nullptr;       // [cap_pay + 1] centroids per payload in key order
   uint32_t* pdst = nullptr;       // [cap_pay + 1] their exclusive scan: each payload's place
+  uint32_t* cuts = nullptr;       // [2 (kImportCuts + 1) + 2] a call's slices: first payloads, their
+                                  // first centroids, then the count and an oversize flag
+  uint32_t* hcuts = nullptr;      // pinned host copy of cuts
 };
 
 // Export results (vn_export_histos / vn_export_sets): engine-owned, valid until the next export.

@@ -314,11 +314,15 @@ __device__ __forceinline__ void gob_skip(GobIn& r, const GobTypes& T, int64_t ti
 
 // One GobEncode()d MergingDigest ([]Centroid, then compression, min, max as float64):
 // the number of centroids, written to mean/w when EMIT; -1 if the stream is malformed.
+// Counting (!EMIT), *fast_at gets the byte where the centroids start when every one of them took
+// the one-window parse (GobIn::centroid), else ~0u: k_gob_emit_fast then emits them from there.
 template <bool EMIT>
-__device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double* w) {
+__device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double* w,
+                                              uint32_t* fast_at = nullptr) {
   GobIn r(d, n);
   GobTypes T;
-  bool have = false;
+  bool have = false, allfast = false;
+  uint32_t at = ~0u;
   int floats = 0;
   int64_t cnt = 0;
   // EMIT: the centroids go out eight at a time from a register queue.  On gfx950 one counter
@@ -348,10 +352,14 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
           fk |= (uint32_t)(T.fid[k] == 4 ? (T.fname[k] == 1 ? 1 : T.fname[k] == 2 ? 2 : 0) : 0) << (2 * k);
         const bool common = T.nf >= 2 && (fk & 15u) == (1u | 2u << 2);  // Mean, Weight first
         const uint64_t c = r.u();
+        at = r.i;
+        allfast = common;
         for (uint64_t j = 0; j < c && !r.err; j++) {
           double m = 0.0, wt = 0.0;  // gob omits zero fields
           int64_t f = -1;
-          if (!(common && r.i < r.n && r.centroid(m, wt))) for (;;) {
+          const bool fast = common && r.i < r.n && r.centroid(m, wt);
+          allfast &= fast;
+          if (!fast) for (;;) {
             const uint64_t dl = r.u();
             if (r.err || dl == 0) break;
             f += (int64_t)dl;
@@ -403,19 +411,50 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
     }
     if (r.err || r.i != end) return -1;
   }
-  return (have && floats == 3) ? cnt : -1;
+  if (!(have && floats == 3)) return -1;
+  if (fast_at) *fast_at = allfast ? at : ~0u;
+  return cnt;
+}
+
+// A validated payload's centroids from byte at on, every one in the one-window layout (the
+// count pass checked it): a loop without the type parse or the general field loop, so the
+// kernel needs fewer registers (more waves hide the stores' waits) than k_gob_emit.
+__device__ __forceinline__ void gob_centroids_fast(const uint8_t* d, uint32_t n, uint32_t at, uint32_t c, double* mean,
+                                                   double* w) {
+  GobIn r(d, n);
+  r.i = at;
+  constexpr int kQ = 8;  // (stores batched as in gob_digest)
+  double qm[kQ], qw[kQ];
+  uint32_t j = 0;
+  for (; j + kQ <= c; j += kQ) {
+#pragma unroll
+    for (int q = 0; q < kQ; q++) (void)r.centroid(qm[q], qw[q]);
+#pragma unroll
+    for (int q = 0; q < kQ; q++) {
+      mean[j + q] = qm[q];
+      w[j + q] = qw[q];
+    }
+  }
+  for (; j < c; j++) {
+    double m, wt;
+    (void)r.centroid(m, wt);
+    mean[j] = m;
+    w[j] = wt;
+  }
 }
 
 // per payload: its centroid count, the whole payload validated (slot in range, offsets
 // non-decreasing, a well-formed digest, every centroid a valid Add), so the emit cannot fail
 __global__ void k_gob_count(uint64_t n, const uint32_t* __restrict__ slot, uint32_t cap,
                             const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
-                            uint32_t* __restrict__ cnt, uint32_t* __restrict__ err) {
+                            uint32_t* __restrict__ cnt, uint32_t* __restrict__ cpos, uint32_t* __restrict__ err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t len = off[i + 1] - off[i];
   const bool ok = slot[i] < cap && off[i + 1] >= off[i] && len <= 0xffffffffull;
-  const int64_t c = ok ? gob_digest<false>(bytes + off[i], (uint32_t)len, nullptr, nullptr) : -1;
+  uint32_t at = ~0u;
+  const int64_t c = ok ? gob_digest<false>(bytes + off[i], (uint32_t)len, nullptr, nullptr, &at) : -1;
+  cpos[i] = c < 0 ? ~0u : at;
   if (c < 0 || c > (int64_t)kTagIndex) {
     atomicOr(err, kErrDecode);
     cnt[i] = 0;
@@ -427,17 +466,65 @@ __global__ void k_gob_count(uint64_t n, const uint32_t* __restrict__ slot, uint3
 // the centroids of payloads 0..n-1 appended to the run at base + coff[i]; each payload's slot and
 // first centroid into the run's payload table at pb + i
 __global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
-                           const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff, uint64_t base,
+                           const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff,
+                           const uint32_t* __restrict__ cpos, uint64_t base,
                            double* __restrict__ omean, double* __restrict__ ow, uint32_t* __restrict__ pslot,
                            uint32_t* __restrict__ pbeg, uint64_t pb, uint32_t* __restrict__ err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= n || cpos[i] != ~0u) return;  // (those: k_gob_emit_fast)
   const uint64_t o = base + coff[i];
   pslot[pb + i] = slot[i];
   pbeg[pb + i] = (uint32_t)o;
   // k_gob_count validated the payload (every centroid a valid Add), so this pass only writes
   const int64_t c = gob_digest<true>(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), omean + o, ow + o);
   if (c < 0) atomicOr(err, kErrDecode);
+}
+
+// the payloads whose centroids all take the one-window parse (cpos: where they start)
+__global__ void k_gob_emit_fast(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+                                const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff,
+                                const uint32_t* __restrict__ cpos, uint64_t base, double* __restrict__ omean,
+                                double* __restrict__ ow, uint32_t* __restrict__ pslot, uint32_t* __restrict__ pbeg,
+                                uint64_t pb) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t at = cpos[i];
+  if (at == ~0u) return;
+  const uint64_t o = base + coff[i];
+  pslot[pb + i] = slot[i];
+  pbeg[pb + i] = (uint32_t)o;
+  gob_centroids_fast(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), at, coff[i + 1] - coff[i], omean + o, ow + o);
+}
+
+// A call's payloads [b0, n) cut greedily into slices of whole payloads, each at most cap centroids
+// and cap_pay payloads (the run): one thread, a binary search over the centroid scan co per slice.
+// out: cuts[j] = first payload of slice j, cuts[kImportCuts + 1 + j] = co at it, j <= count; then
+// the count and a flag (1: a payload alone is over cap).  At most kImportCuts slices per pass.
+__global__ void k_import_cuts(const uint32_t* __restrict__ co, uint64_t n, uint64_t b0, uint64_t cap, uint64_t cap_pay,
+                              uint32_t* __restrict__ out) {
+  uint32_t* const cc = out + kImportCuts + 1;
+  uint32_t j = 0, flag = 0;
+  while (b0 < n && j < kImportCuts) {
+    const uint32_t c0 = co[b0];
+    if (co[b0 + 1] - c0 > cap) {
+      flag = 1;
+      break;
+    }
+    uint64_t lo = b0 + 1, hi = min(n, b0 + cap_pay);  // the largest b1 in [lo, hi] with co[b1] - c0 <= cap
+    while (lo < hi) {
+      const uint64_t m = (lo + hi + 1) >> 1;
+      if (co[m] - c0 <= cap) lo = m;
+      else hi = m - 1;
+    }
+    out[j] = (uint32_t)b0;
+    cc[j] = c0;
+    j++;
+    b0 = lo;
+  }
+  out[j] = (uint32_t)b0;
+  cc[j] = co[b0];
+  out[2 * (kImportCuts + 1)] = j;
+  out[2 * (kImportCuts + 1) + 1] = flag;
 }
 
 // ---- the drain's grouping: payloads sorted by key (stable), then their centroids moved
@@ -496,7 +583,7 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   };
   ev_pair(e->pool_id, [&] {
     hipLaunchKernelGGL(k_gob_count, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, e->cap[VN_HISTO], off, bytes,
-                       s.cnt, e->h_err);
+                       s.cnt, s.cpos, e->h_err);
   });
   scan_exclusive_u32(s.cnt, s.coff, n, e->ss, st);
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 9, s.coff + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -507,35 +594,46 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   if (nc <= s.cap_cent && n <= s.cap_pay) {
     if (s.acc + nc > s.cap_cent || s.npay + n > s.cap_pay) histo_imports_drain(e);
     ev_pair(e->pool_id, [&] {
-      hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.acc,
-                         s.cmean, s.cw, s.pslot, s.pbeg, s.npay, e->h_err);
+      hipLaunchKernelGGL(k_gob_emit_fast, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff,
+                         s.cpos, s.acc, s.cmean, s.cw, s.pslot, s.pbeg, s.npay);
+      hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.cpos,
+                         s.acc, s.cmean, s.cw, s.pslot, s.pbeg, s.npay, e->h_err);
     });
     s.acc += nc;
     s.npay += n;
     return;
   }
-  // slices of whole payloads in arrival order, each at most the run, cut greedily on the host;
-  // a payload larger than the run is refused before anything is emitted
-  std::vector<uint32_t> co((size_t)n + 1);
-  VN_HIP_CHECK(hipMemcpyAsync(co.data(), s.coff, co.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipStreamSynchronize(st));
-  for (uint64_t i = 0; i < n; i++)
-    if (co[i + 1] - co[i] > s.cap_cent)
-      throw std::invalid_argument("one imported digest holds more centroids than max_batch_records");
+  // slices of whole payloads in arrival order, each at most the run, cut greedily on the device
+  // (k_import_cuts: only the cuts come back, not the 4-byte scan of every payload -- that copy and
+  // a host loop over it held the GPU idle ≈9 ms per C5 window); a payload larger than the run is
+  // refused before anything is emitted
+  const size_t ncut = 2 * (kImportCuts + 1) + 2;
+  std::vector<std::pair<uint32_t, uint32_t>> cuts;  // (first payload, its first centroid); n last
   for (uint64_t b0 = 0; b0 < n;) {
-    uint64_t b1 = b0 + 1;
-    while (b1 < n && co[b1 + 1] - co[b0] <= s.cap_cent && b1 - b0 < s.cap_pay) b1++;
-    const uint64_t c0 = co[b0], c1 = co[b1];
+    hipLaunchKernelGGL(k_import_cuts, dim3(1), dim3(1), 0, st, s.coff, n, b0, s.cap_cent, s.cap_pay, s.cuts);
+    VN_HIP_CHECK(hipMemcpyAsync(s.hcuts, s.cuts, ncut * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    VN_HIP_CHECK(hipStreamSynchronize(st));
+    const uint32_t j = s.hcuts[2 * (kImportCuts + 1)];
+    if (s.hcuts[2 * (kImportCuts + 1) + 1])
+      throw std::invalid_argument("one imported digest holds more centroids than max_batch_records");
+    for (uint32_t q = 0; q < j; q++) cuts.emplace_back(s.hcuts[q], s.hcuts[kImportCuts + 1 + q]);
+    b0 = s.hcuts[j];
+    if (b0 >= n) cuts.emplace_back((uint32_t)n, s.hcuts[kImportCuts + 1 + j]);
+  }
+  for (size_t q = 0; q + 1 < cuts.size(); q++) {
+    const uint64_t b0 = cuts[q].first, b1 = cuts[q + 1].first, c0 = cuts[q].second, c1 = cuts[q + 1].second;
     if (c1 > c0) {
       if (s.acc + (c1 - c0) > s.cap_cent || s.npay + (b1 - b0) > s.cap_pay) histo_imports_drain(e);
       ev_pair(e->pool_id, [&] {
+        hipLaunchKernelGGL(k_gob_emit_fast, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
+                           slot + b0, s.coff + b0, s.cpos + b0, s.acc - c0, s.cmean, s.cw, s.pslot, s.pbeg, s.npay);
         hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
-                           slot + b0, s.coff + b0, s.acc - c0, s.cmean, s.cw, s.pslot, s.pbeg, s.npay, e->h_err);
+                           slot + b0, s.coff + b0, s.cpos + b0, s.acc - c0, s.cmean, s.cw, s.pslot, s.pbeg, s.npay,
+                           e->h_err);
       });
       s.acc += c1 - c0;
       s.npay += b1 - b0;
     }
-    b0 = b1;
   }
 }
 
