@@ -373,7 +373,7 @@ void ensure_pinned_stage(vn_engine* e) {
 void ensure_import(vn_engine* e, uint64_t n, uint64_t nbytes) {
   ImportScratch& s = e->imp;
   if (n > s.cap_n) {
-    dfree(s.in_slot); dfree(s.in_off); dfree(s.cnt); dfree(s.coff); dfree(s.cpos);
+    dfree(s.in_slot); dfree(s.in_off); dfree(s.cnt); dfree(s.coff); dfree(s.cpos); dfree(s.ckpt);
     if (s.parts) (void)hipFree(s.parts);
     s.cap_n = std::max<uint64_t>(n, 1024);
     dalloc(s.in_slot, s.cap_n);
@@ -381,6 +381,7 @@ void ensure_import(vn_engine* e, uint64_t n, uint64_t nbytes) {
     dalloc(s.cnt, s.cap_n + 1);
     dalloc(s.coff, s.cap_n + 1);
     dalloc(s.cpos, s.cap_n);
+    dalloc(s.ckpt, s.cap_n * 16);
     VN_HIP_CHECK(hipMalloc(&s.parts, s.cap_n * 64));
   }
   if (nbytes > s.cap_bytes) {
@@ -485,7 +486,7 @@ void destroy_impl(vn_engine* e) {
   dfree(xb.d_slot); dfree(xb.d_keys); dfree(xb.d_size); dfree(xb.d_off); hfree(xb.h_off); dfree(xb.d_bytes);
   hfree(xb.h_bytes);
   ImportScratch& is = e->imp;
-  dfree(is.in_slot); dfree(is.in_off); dfree(is.in_bytes); dfree(is.cnt); dfree(is.coff); dfree(is.cpos); dfree(is.cuts); hfree(is.hcuts); dfree(is.cslot);
+  dfree(is.in_slot); dfree(is.in_off); dfree(is.in_bytes); dfree(is.cnt); dfree(is.coff); dfree(is.cpos); dfree(is.ckpt); dfree(is.cuts); hfree(is.hcuts); dfree(is.cslot);
   dfree(is.pslot); dfree(is.pbeg); dfree(is.pkey); dfree(is.pcnt); dfree(is.pdst);
   dfree(is.cmean); dfree(is.cw);
   if (is.parts) (void)hipFree(is.parts);

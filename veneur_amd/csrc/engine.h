@@ -34,7 +34,8 @@ struct ImportScratch {
   uint32_t* cnt = nullptr;        // [cap_n + 1] per payload: centroids
   uint32_t* coff = nullptr;       // [cap_n + 1] scan of cnt
   uint32_t* cpos = nullptr;       // [cap_n] per payload: where its centroids start when all are in the
-                                  // one-window layout (k_gob_emit_fast), else ~0
+                                  // one-window layout (k_gob_emit_seg), else ~0
+  uint16_t* ckpt = nullptr;       // [cap_n * 16] per payload: the byte of every 16th centroid (k_gob_emit_seg)
   void* parts = nullptr;          // [cap_n] parsed HLL payload headers (import_set.hip)
   uint32_t* cslot = nullptr;      // [cap_cent] decoded centroids: slot, mean, weight
   double* cmean = nullptr;

@@ -49,6 +49,17 @@ struct GobIn {
       load(2, m0, m1);
     }
   }
+  // (a reader placed at byte pos: its first three blocks are those around pos)
+  __device__ GobIn(const uint8_t* d, uint32_t len, uint32_t pos) : n(len), i(pos), err(false) {
+    const uintptr_t s = reinterpret_cast<uintptr_t>(d), a0 = s & ~(uintptr_t)15;
+    blk = reinterpret_cast<const uint4*>(a0);
+    lo = (uint32_t)(s - a0);
+    nb = (lo + len + 15u) >> 4;
+    cb = (lo + pos) >> 4;
+    load(cb, c0, c1);
+    load(cb + 1, n0, n1);
+    load(cb + 2, m0, m1);
+  }
   // hold blocks k, k + 1, k + 2 (the two after the current one in flight while it is parsed)
   __device__ __forceinline__ void seek(uint32_t k) {
     if (k == cb) return;
@@ -316,9 +327,12 @@ __device__ __forceinline__ void gob_skip(GobIn& r, const GobTypes& T, int64_t ti
 // the number of centroids, written to mean/w when EMIT; -1 if the stream is malformed.
 // Counting (!EMIT), *fast_at gets the byte where the centroids start when every one of them took
 // the one-window parse (GobIn::centroid), else ~0u: k_gob_emit_fast then emits them from there.
+// ... and ckpt[q] the byte of centroid kSeg q (q < kSegs; a payload of more centroids, or of 64 KiB
+// or more, is not "fast")
+constexpr uint32_t kSeg = 16, kSegs = 16;
 template <bool EMIT>
 __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, double* mean, double* w,
-                                              uint32_t* fast_at = nullptr) {
+                                              uint32_t* fast_at = nullptr, uint16_t* ckpt = nullptr) {
   GobIn r(d, n);
   GobTypes T;
   bool have = false, allfast = false;
@@ -353,10 +367,11 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
         const bool common = T.nf >= 2 && (fk & 15u) == (1u | 2u << 2);  // Mean, Weight first
         const uint64_t c = r.u();
         at = r.i;
-        allfast = common;
+        allfast = common && c <= kSeg * kSegs && n < 65536u;
         for (uint64_t j = 0; j < c && !r.err; j++) {
           double m = 0.0, wt = 0.0;  // gob omits zero fields
           int64_t f = -1;
+          if (!EMIT && ckpt && allfast && j % kSeg == 0) ckpt[j / kSeg] = (uint16_t)r.i;
           const bool fast = common && r.i < r.n && r.centroid(m, wt);
           allfast &= fast;
           if (!fast) for (;;) {
@@ -416,44 +431,19 @@ __device__ __forceinline__ int64_t gob_digest(const uint8_t* d, uint32_t n, doub
   return cnt;
 }
 
-// A validated payload's centroids from byte at on, every one in the one-window layout (the
-// count pass checked it): a loop without the type parse or the general field loop, so the
-// kernel needs fewer registers (more waves hide the stores' waits) than k_gob_emit.
-__device__ __forceinline__ void gob_centroids_fast(const uint8_t* d, uint32_t n, uint32_t at, uint32_t c, double* mean,
-                                                   double* w) {
-  GobIn r(d, n);
-  r.i = at;
-  constexpr int kQ = 8;  // (stores batched as in gob_digest)
-  double qm[kQ], qw[kQ];
-  uint32_t j = 0;
-  for (; j + kQ <= c; j += kQ) {
-#pragma unroll
-    for (int q = 0; q < kQ; q++) (void)r.centroid(qm[q], qw[q]);
-#pragma unroll
-    for (int q = 0; q < kQ; q++) {
-      mean[j + q] = qm[q];
-      w[j + q] = qw[q];
-    }
-  }
-  for (; j < c; j++) {
-    double m, wt;
-    (void)r.centroid(m, wt);
-    mean[j] = m;
-    w[j] = wt;
-  }
-}
-
 // per payload: its centroid count, the whole payload validated (slot in range, offsets
 // non-decreasing, a well-formed digest, every centroid a valid Add), so the emit cannot fail
 __global__ void k_gob_count(uint64_t n, const uint32_t* __restrict__ slot, uint32_t cap,
                             const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
-                            uint32_t* __restrict__ cnt, uint32_t* __restrict__ cpos, uint32_t* __restrict__ err) {
+                            uint32_t* __restrict__ cnt, uint32_t* __restrict__ cpos, uint16_t* __restrict__ ckpt,
+                            uint32_t* __restrict__ err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t len = off[i + 1] - off[i];
   const bool ok = slot[i] < cap && off[i + 1] >= off[i] && len <= 0xffffffffull;
   uint32_t at = ~0u;
-  const int64_t c = ok ? gob_digest<false>(bytes + off[i], (uint32_t)len, nullptr, nullptr, &at) : -1;
+  const int64_t c =
+      ok ? gob_digest<false>(bytes + off[i], (uint32_t)len, nullptr, nullptr, &at, ckpt + (uint64_t)i * kSegs) : -1;
   cpos[i] = c < 0 ? ~0u : at;
   if (c < 0 || c > (int64_t)kTagIndex) {
     atomicOr(err, kErrDecode);
@@ -480,20 +470,43 @@ __global__ void k_gob_emit(uint64_t n, const uint64_t* __restrict__ off, const u
   if (c < 0) atomicOr(err, kErrDecode);
 }
 
-// the payloads whose centroids all take the one-window parse (cpos: where they start)
-__global__ void k_gob_emit_fast(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
-                                const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff,
-                                const uint32_t* __restrict__ cpos, uint64_t base, double* __restrict__ omean,
-                                double* __restrict__ ow, uint32_t* __restrict__ pslot, uint32_t* __restrict__ pbeg,
-                                uint64_t pb) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t at = cpos[i];
-  if (at == ~0u) return;
-  const uint64_t o = base + coff[i];
-  pslot[pb + i] = slot[i];
-  pbeg[pb + i] = (uint32_t)o;
-  gob_centroids_fast(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), at, coff[i + 1] - coff[i], omean + o, ow + o);
+// The payloads whose centroids all take the one-window parse (cpos: where they start), kSeg
+// centroids per thread from the count pass's checkpoints, kSegs threads per payload: a payload's
+// threads are adjacent lanes writing adjacent kSeg-centroid runs, so the wave completes its output
+// lines within a few stores (one lane per payload left every lane's line half written across
+// long stretches of its parse: the stores, not the parse, set that kernel's time)
+__global__ void k_gob_emit_seg(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
+                               const uint32_t* __restrict__ slot, const uint32_t* __restrict__ coff,
+                               const uint32_t* __restrict__ cpos, const uint16_t* __restrict__ ckpt, uint64_t base,
+                               double* __restrict__ omean, double* __restrict__ ow, uint32_t* __restrict__ pslot,
+                               uint32_t* __restrict__ pbeg, uint64_t pb) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, i = t / kSegs;
+  const uint32_t q = (uint32_t)(t % kSegs);
+  if (i >= n || cpos[i] == ~0u) return;
+  const uint32_t c0 = coff[i], c = coff[i + 1] - c0;
+  const uint64_t o = base + c0;
+  if (q == 0) {
+    pslot[pb + i] = slot[i];
+    pbeg[pb + i] = (uint32_t)o;
+  }
+  if (q * kSeg >= c) return;
+  const uint32_t m = min(kSeg, c - q * kSeg);
+  GobIn r(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), ckpt[i * kSegs + q]);
+  double qm[kSeg], qw[kSeg];
+#pragma unroll
+  for (uint32_t j = 0; j < kSeg; j++) {
+    qm[j] = 0.0;
+    qw[j] = 0.0;
+    if (j < m) (void)r.centroid(qm[j], qw[j]);
+  }
+  double* const dm = omean + o + q * kSeg;
+  double* const dw = ow + o + q * kSeg;
+#pragma unroll
+  for (uint32_t j = 0; j < kSeg; j++)
+    if (j < m) {
+      dm[j] = qm[j];
+      dw[j] = qw[j];
+    }
 }
 
 // A call's payloads [b0, n) cut greedily into slices of whole payloads, each at most cap centroids
@@ -583,7 +596,7 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   };
   ev_pair(e->pool_id, [&] {
     hipLaunchKernelGGL(k_gob_count, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, e->cap[VN_HISTO], off, bytes,
-                       s.cnt, s.cpos, e->h_err);
+                       s.cnt, s.cpos, s.ckpt, e->h_err);
   });
   scan_exclusive_u32(s.cnt, s.coff, n, e->ss, st);
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 9, s.coff + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
@@ -594,8 +607,8 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   if (nc <= s.cap_cent && n <= s.cap_pay) {
     if (s.acc + nc > s.cap_cent || s.npay + n > s.cap_pay) histo_imports_drain(e);
     ev_pair(e->pool_id, [&] {
-      hipLaunchKernelGGL(k_gob_emit_fast, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff,
-                         s.cpos, s.acc, s.cmean, s.cw, s.pslot, s.pbeg, s.npay);
+      hipLaunchKernelGGL(k_gob_emit_seg, dim3(blocks_for(n * kSegs, 256)), dim3(256), 0, st, n, off, bytes, slot,
+                         s.coff, s.cpos, s.ckpt, s.acc, s.cmean, s.cw, s.pslot, s.pbeg, s.npay);
       hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.cpos,
                          s.acc, s.cmean, s.cw, s.pslot, s.pbeg, s.npay, e->h_err);
     });
@@ -625,8 +638,9 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
     if (c1 > c0) {
       if (s.acc + (c1 - c0) > s.cap_cent || s.npay + (b1 - b0) > s.cap_pay) histo_imports_drain(e);
       ev_pair(e->pool_id, [&] {
-        hipLaunchKernelGGL(k_gob_emit_fast, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
-                           slot + b0, s.coff + b0, s.cpos + b0, s.acc - c0, s.cmean, s.cw, s.pslot, s.pbeg, s.npay);
+        hipLaunchKernelGGL(k_gob_emit_seg, dim3(blocks_for((b1 - b0) * kSegs, 256)), dim3(256), 0, st, b1 - b0,
+                           off + b0, bytes, slot + b0, s.coff + b0, s.cpos + b0, s.ckpt + b0 * kSegs, s.acc - c0,
+                           s.cmean, s.cw, s.pslot, s.pbeg, s.npay);
         hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
                            slot + b0, s.coff + b0, s.cpos + b0, s.acc - c0, s.cmean, s.cw, s.pslot, s.pbeg, s.npay,
                            e->h_err);

@@ -15,7 +15,7 @@
 // worker logs it and moves on (worker.go:248-252) -- the key is still Upserted, nothing merges.
 // A payload UnmarshalBinary would panic on (truncated) fails the whole call (VN_EDECODE).
 //
-// MI355X formulation: one lane per payload parses and validates it (k_hll_parse); payloads
+// MI355X formulation: one wave per payload parses and validates it (k_hll_parse); payloads
 // are grouped by key with a stable radix sort; one 256-thread workgroup per key then applies
 // its payloads in arrival order with the key's list or registers in LDS: varint lists decode
 // in parallel (scan of terminator bytes, then a scan of the deltas), unions are merge-path
@@ -84,25 +84,26 @@ __device__ __forceinline__ void for_bytes(const uint8_t* p, uint32_t len, F&& f)
   }
 }
 
-// ins(code) for every code of a sparse payload, by one whole wave (lanes in step, exec full): the
-// tmpSet's big-endian codes a lane each, then the varint list 256 bytes per step, four bytes per
-// lane. compressedList.decode (compressed.go:157-165) makes a code the running uint32 sum of the
-// varint values, and a varint's value the OR of (byte & 0x7f) << 7 d over its bytes (d = the byte's
-// place in it; from d = 5 on Go's uint32 shift adds nothing). The bit ranges are disjoint, so a
-// code is the sum, over every list byte up to its terminator, of that byte's contribution: each
-// byte finds where its varint starts (the last terminator before it: within the lane, else a wave
-// max-scan of the lanes' last terminators, else the one carried from the previous step), and the
-// codes are a wave sum-scan of the contributions read at the terminators. A trailing unterminated
-// varint inserts nothing, as the per-lane parse.
-template <class Ins>
-__device__ __forceinline__ void wave_insert_sparse(const uint8_t* bytes, const HllPart& R, Ins&& ins) {
+// The codes of a compressedList's varint bytes [p, p + len), by one whole wave (lanes in step, exec
+// full), 256 bytes per step, four bytes per lane; f(code, prev, has_prev) at each code (PREV: the
+// code before it in the list, if any).  compressedList.decode (compressed.go:157-165) makes a code
+// the running uint32 sum of the varint values, and a varint's value the OR of (byte & 0x7f) << 7 d
+// over its bytes (d = the byte's place in it; from d = 5 on Go's uint32 shift adds nothing).  The
+// bit ranges are disjoint, so a code is the sum, over every list byte up to its terminator, of that
+// byte's contribution: each byte finds where its varint starts (the last terminator before it:
+// within the lane, else a wave max-scan of the lanes' last terminators, else the one carried from
+// the previous step), and the codes are a wave sum-scan of the contributions read at the
+// terminators.  A trailing unterminated varint gives no code.  Returns the number of codes.
+template <bool PREV, class F>
+__device__ __forceinline__ uint32_t wave_list_codes(const uint8_t* p, uint32_t len, F&& f) {
   const uint32_t lane = threadIdx.x & 63u;
-  for (uint32_t i = lane; i < R.ntmp; i += 64) ins(be32(bytes + R.tmp_off + 4ull * i));
-  if (!R.list_len) return;
-  const uintptr_t s = reinterpret_cast<uintptr_t>(bytes + R.list_off), a0 = s & ~(uintptr_t)3;
-  const uint32_t lo = (uint32_t)(s - a0), end = lo + R.list_len;  // positions relative to a0
+  if (!len) return 0;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(p), a0 = s & ~(uintptr_t)3;
+  const uint32_t lo = (uint32_t)(s - a0), end = lo + len;  // positions relative to a0
   const uint32_t* w32 = reinterpret_cast<const uint32_t*>(a0);
   uint32_t carry = 0, vstart = lo;  // the code so far; the first byte of the varint in progress
+  uint32_t lastc = 0, ncodes = 0;   // (PREV) the last code of the steps before
+  bool haslast = false;
   uint32_t nxt = 4 * lane < end ? w32[lane] : 0u;
   for (uint32_t base = 0; base < end; base += 256) {
     const uint32_t p0 = base + 4 * lane, w = nxt;
@@ -125,22 +126,69 @@ __device__ __forceinline__ void wave_insert_sparse(const uint8_t* bytes, const H
       if (tm & (1u << j)) st = pos + 1;
     }
     const uint32_t incl = wave_incl_add_u32(sum);
+    uint32_t ph = 0, pc = 0;  // (PREV) the last code at or below this lane, if any
+    if (PREV) {
+      uint32_t run = incl - sum + carry;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        run += c[j];
+        if (tm & (1u << j)) pc = run;
+      }
+      ph = tm != 0;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t oh = (uint32_t)__shfl_up((int)ph, d, 64), oc = (uint32_t)__shfl_up((int)pc, d, 64);
+        if ((int)lane >= d && !ph) {
+          ph = oh;
+          pc = oc;
+        }
+      }
+    }
+    uint32_t eh = PREV ? (uint32_t)__shfl_up((int)ph, 1, 64) : 0u, ec = PREV ? (uint32_t)__shfl_up((int)pc, 1, 64) : 0u;
+    if (lane == 0 || !eh) {
+      eh = haslast;
+      ec = lastc;
+    }
     uint32_t run = incl - sum + carry;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
       run += c[j];
-      if (tm & (1u << j)) ins(run);
+      if (tm & (1u << j)) {
+        f(run, ec, eh != 0);
+        ec = run;
+        eh = 1;
+      }
+    }
+    ncodes += (uint32_t)__shfl((int)wave_incl_add_u32((uint32_t)__builtin_popcount(tm)), 63);
+    if (PREV && __shfl((int)ph, 63)) {
+      haslast = true;
+      lastc = (uint32_t)__shfl((int)pc, 63);
     }
     carry += (uint32_t)__shfl((int)incl, 63);
     vstart = max(vstart, (uint32_t)__shfl((int)upto, 63));
   }
+  return ncodes;
 }
 
-// parse + validate one MarshalBinary payload (hyperloglog.go:318-376, compressed.go:83-97)
-__global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const uint8_t* __restrict__ bytes,
-                            HllPart* __restrict__ parts, uint32_t* __restrict__ err) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// ins(code) for every code of a sparse payload, by one whole wave: the tmpSet's big-endian codes a
+// lane each, then the list (wave_list_codes)
+template <class Ins>
+__device__ __forceinline__ void wave_insert_sparse(const uint8_t* bytes, const HllPart& R, Ins&& ins) {
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t i = lane; i < R.ntmp; i += 64) ins(be32(bytes + R.tmp_off + 4ull * i));
+  (void)wave_list_codes<false>(bytes + R.list_off, R.list_len, [&](uint32_t c, uint32_t, bool) { ins(c); });
+}
+
+// parse + validate one MarshalBinary payload per wave (hyperloglog.go:318-376, compressed.go:83-97):
+// the header by every lane, the tmpSet's codes a lane each, the list by wave_list_codes; the rho
+// range and the checks (the list decodes completely into strictly increasing codes) reduced over
+// the wave.  (A lane per payload walked 8.5 ms of C5's payloads byte by byte.)
+__global__ __launch_bounds__(256) void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off,
+                                                   const uint8_t* __restrict__ bytes, HllPart* __restrict__ parts,
+                                                   uint32_t* __restrict__ err) {
+  const uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;  // (wave-uniform)
+  const uint32_t lane = threadIdx.x & 63u;
   const uint64_t o = off[i], len = off[i + 1] - o;
   const uint8_t* d = bytes + o;
   HllPart p{};
@@ -157,44 +205,32 @@ __global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const 
           const uint64_t sz = be32(d + last + 8);
           bad = sz > kHllM || len < last + 12 + sz;
           if (!bad) {
-            // the list must decode completely into strictly increasing codes
             const uint8_t* lb = d + last + 12;
-            uint32_t prev = 0, x = 0, sh = 0, k = 0, rmin = 0xffu, rmax = 0u, tc = 0, tn = 0, lastb = 0;
-            // (both read as 16-byte blocks, the next in flight: one lane walks the payload)
-            for_bytes(d + 8, 4u * (uint32_t)tssz, [&](uint32_t b) {
-              tc = (tc << 8) | b;
-              if (++tn == 4) {
-                uint32_t ri, r;
-                decode_hash(tc, &ri, &r);
-                rmin = min(rmin, r);
-                rmax = max(rmax, r);
-                tn = 0;
-              }
+            uint32_t rlo = 0, rmax = 0;  // (rlo: 255 - the smallest rho, so both reduce by max)
+            bool lbad = false;
+            for (uint32_t t = lane; t < (uint32_t)tssz; t += 64) {
+              uint32_t ri, r;
+              decode_hash(be32(d + 8 + 4ull * t), &ri, &r);
+              rlo = max(rlo, 255u - r);
+              rmax = max(rmax, r);
+            }
+            const uint32_t k = wave_list_codes<true>(lb, (uint32_t)sz, [&](uint32_t c, uint32_t prev, bool has_prev) {
+              if (has_prev && c <= prev) lbad = true;  // the list must be strictly increasing
+              uint32_t ri, r;
+              decode_hash(c, &ri, &r);
+              rlo = max(rlo, 255u - r);
+              rmax = max(rmax, r);
             });
-            for_bytes(lb, (uint32_t)sz, [&](uint32_t b) {
-              if (sh < 32) x |= (b & 0x7fu) << sh;
-              sh += 7;
-              lastb = b;
-              if (!(b & 0x80u)) {
-                const uint32_t c = prev + x;
-                if (k > 0 && c <= prev) bad = true;
-                uint32_t ri, r;
-                decode_hash(c, &ri, &r);
-                rmin = min(rmin, r);
-                rmax = max(rmax, r);
-                prev = c;
-                k++;
-                x = 0;
-                sh = 0;
-              }
-            });
-            if (sz && (lastb & 0x80u)) bad = true;  // a code without its last byte
+            if (sz && (lb[sz - 1] & 0x80u)) lbad = true;  // a code without its last byte
+            bad = __any(lbad);
+            rlo = (uint32_t)__shfl((int)wave_incl_max(rlo), 63);
+            rmax = (uint32_t)__shfl((int)wave_incl_max(rmax), 63);
             p.kind = 0;
             p.ntmp = (uint32_t)tssz;
             p.tmp_off = o + 8;
             p.list_off = o + last + 12;
             p.list_len = (uint32_t)sz;
-            p.rr = rmin | (rmax << 8);
+            p.rr = (rlo || rmax ? 255u - rlo : 0xffu) | (rmax << 8);
             p.ncodes = (uint32_t)tssz + k;
           }
         }
@@ -208,8 +244,10 @@ __global__ void k_hll_parse(uint64_t n, const uint64_t* __restrict__ off, const 
       }
     }
   }
-  if (bad) atomicOr(err, kErrDecode);
-  parts[i] = p;
+  if (lane == 0) {
+    if (bad) atomicOr(err, kErrDecode);
+    parts[i] = p;
+  }
 }
 
 __global__ void k_hll_keys(uint64_t n, const uint32_t* __restrict__ slot, uint64_t* __restrict__ keys,
@@ -802,7 +840,7 @@ void import_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t*
   if (!n) return;
   hipStream_t st = e->st;
   HllPart* parts = reinterpret_cast<HllPart*>(e->imp.parts);
-  hipLaunchKernelGGL(k_hll_parse, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, parts, e->h_err);
+  hipLaunchKernelGGL(k_hll_parse, dim3(blocks_for(n, 4)), dim3(256), 0, st, n, off, bytes, parts, e->h_err);  // a wave each
   VN_HIP_CHECK(hipStreamSynchronize(st));
   take_decode_error(e);  // a truncated payload: nothing is applied
   // group the payloads by key, arrival order kept
