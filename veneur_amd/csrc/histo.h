@@ -29,6 +29,9 @@ __device__ __forceinline__ double tag_weight(uint32_t tag, const double* impw) {
 
 struct ExactCtx {
   uint32_t nkeys;
+  uint32_t long_min;  // chunk sorter: every record's ctw / cpk only for keys of at least this many exact records
+                      // (the four-wave and batched replays read them; the one-wave replay only a chunk's
+                      // first); 0: for every key
   const uint32_t* keys;      // slot of each processed key
   const uint32_t* order;     // replay only: key indices of this launch (nullptr: 0..nkeys-1)
   uint32_t norder;           // replay grid when order is set

@@ -1091,6 +1091,7 @@ __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t
     }
   }
   const double tempW = temp_weight(tw, tcap);
+  const bool wide = x.nex[k] >= x.long_min;  // (every record's prefix: a four-wave or batched replay)
   sort_temps(tv, tw, sv, sw, tcap);
   // for the long replays (replay_key_fast): the exclusive prefix of the sorted |weights| after
   // the first record, the Add-order tempW at it (negated when a weight is not an integer)
@@ -1113,8 +1114,8 @@ __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t
       const double ex = dadd(carry, dsub(v, w));
       x.csv[base + t] = sv[t];
       x.csw[base + t] = sw[t];
-      if (t) x.ctw[base + t] = ex;
-      if (x.cpk && t) x.cpk[base + t] = (ex < 65536.0 ? (uint32_t)ex << 16 : 0xffff0000u) | (w < 65536.0 ? (uint32_t)w : 0xffffu);
+      if (t && wide) x.ctw[base + t] = ex;
+      if (x.cpk && t && wide) x.cpk[base + t] = (ex < 65536.0 ? (uint32_t)ex << 16 : 0xffff0000u) | (w < 65536.0 ? (uint32_t)w : 0xffffu);
     }
     carry = dadd(carry, rl_d(v, 63));
   }

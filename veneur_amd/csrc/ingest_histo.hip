@@ -1326,6 +1326,10 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.cstat = e->h_cstat;  // (A/B build VN_NO_CSTAT: k_exact_long_stats re-reads the samples)
 #endif
   const uint64_t max_chunks = n / e->temp_cap + 1;
+  // the four-wave replay's threshold (replay_cold below): shorter keys take the one-wave replay
+  const uint32_t long_min =
+      e->long_replay ? e->long_replay : std::min<uint32_t>(std::max<uint32_t>(e->exact_threshold / 4, 1024u), 8192u);
+  xc.long_min = long_min;
   // (exact mode, no hot key, not timing: the longest keys' chunks are sorted first and their
   // replays start while the other chunks sort, in replay_cold)
   const bool early = e->early_top && !nhot && !e->timing && e->st5 && e->st6;
@@ -1349,8 +1353,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   // replay of the rest on the same CUs
   auto replay_cold = [&](hipStream_t s, RadixScratch& rs) {
     histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
-    const uint32_t min_len =
-        e->long_replay ? e->long_replay : std::min<uint32_t>(std::max<uint32_t>(e->exact_threshold / 4, 1024u), 8192u);
+    const uint32_t min_len = long_min;
     const bool longk = maxex >= min_len && histo_exact_count_long(xc, min_len, e->h_cnt + 15, s);
     const bool side5 = longk && !e->timing && e->st5;
     hipEvent_t a = e->timing ? e->pool_rp.next() : nullptr, b = e->timing ? e->pool_rp.next() : nullptr;
