@@ -786,6 +786,8 @@ def main():
         kern.append({"kernel": "counter aggregation", "ms_per_step": ms_c, "launches_per_step": 1.0,
                      "algorithmic_bytes_per_launch": by_c, "achieved": by_c / (ms_c * 1e-3) / 1e9,
                      "frac": by_c / (ms_c * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     # (tools/roofline_check.py: the trace's kernels of this phase, every launch summed)
+                     "trace_kernels": ["k_part_count&CounterSrc", "k_part_scatter&CounterSrc", "k_counter_runs"],
                      "note": "the serialised counter phase: key-range partition pass (k_part_count, "
                              "k_part_scatter) + k_counter_runs (LDS sums per slot range, one device add per "
                              "touched slot per 128Ki-record slice)"})
