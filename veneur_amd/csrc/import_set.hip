@@ -384,10 +384,11 @@ __device__ __forceinline__ uint32_t lower_bound_after(const uint32_t* a, uint32_
 // scan of the "also in the other list" flags).  OUT may be A (ALIAS 1) or B (ALIAS 2): that side's
 // values are staged in registers before anything is written, the other side is read again after
 // the scan's barriers; places are kept as u16 pairs (< 2^16: na + nb <= 256 (KA + KB)) and the
-// flags as bits, so the 16k-code union (KA = 65, KB = 67) stays in registers.
+// flags as bits, so the 16k-code union (KA = 65, KB = 67) stays in registers.  A union of more
+// than cap codes writes nothing and returns its size.
 template <int KA, int KB, int ALIAS>
 __device__ uint32_t union_unique(const uint32_t* A, uint32_t na, const uint32_t* B, uint32_t nb, uint32_t* OUT,
-                                 uint32_t* s_red) {
+                                 uint32_t* s_red, uint32_t cap = 0xffffffffu) {
   static_assert(kBlock * (KA + KB) <= 65536, "u16 places");
   const uint32_t t = threadIdx.x;
   const uint32_t pa = (na + kBlock - 1) / kBlock, loA = min(na, t * pa), hiA = min(na, loA + pa);
@@ -433,6 +434,10 @@ __device__ uint32_t union_unique(const uint32_t* A, uint32_t na, const uint32_t*
   uint32_t common, common2;
   uint32_t exa = block_scan_u32<false>(ca, s_red, common);
   uint32_t exb = block_scan_u32<false>(cb, s_red, common2);
+  if (na + nb - common > cap) {  // over the output's capacity: the size only, nothing written
+    __syncthreads();
+    return na + nb - common;
+  }
 #pragma unroll
   for (int q = 0; q < KA; q++)
     if (loA + q < hiA) {
@@ -449,6 +454,15 @@ __device__ uint32_t union_unique(const uint32_t* A, uint32_t na, const uint32_t*
     }
   __syncthreads();
   return na + nb - common;
+}
+
+// a tmpSet-sized A (<= 256 codes) with B: one element per thread when B fits too (the unrolled
+// 67-element staging costs ~10k cycles even for a few codes)
+template <int ALIAS>
+__device__ __forceinline__ uint32_t union_small(const uint32_t* A, uint32_t na, const uint32_t* B, uint32_t nb,
+                                                uint32_t* OUT, uint32_t* s_red) {
+  if (nb <= kBlock) return union_unique<1, 1, ALIAS>(A, na, B, nb, OUT, s_red);
+  return union_unique<1, kCPer, ALIAS>(A, na, B, nb, OUT, s_red);
 }
 
 // varint byte length of sorted unique codes (compressedList.Append deltas from 0)
@@ -497,8 +511,8 @@ __device__ uint32_t to_normal(uint32_t* U, const uint32_t* A, uint32_t na, const
 // workgroups: 0 workgroup, 1 sparse <- sparse payloads (2 count), 3 dense runs of sparse payloads
 // (4 runs, 5 payloads in them), 6 dense <- sparse one at a time (7 count), 8 dense payloads (9 count),
 // 10 toNormal count, 11 payloads in all; sparse <- sparse phases: 12 tmpSet load and sort, 13 list
-// decode, 14 unique + union + tmpSet lookup, 15 mergeSparse triggers; of which 16 tmpSet union +
-// list lookups, 17 the list union; 18 the tmpSet union of the other payloads
+// decode, 14 unique + the two unions (payload, then tmpSet), 15 mergeSparse triggers; of which 16 (none
+// now), 17 the list union; 18 the tmpSet copy of the other payloads
 __device__ unsigned long long g_imp_prof[24];
 #define IPROF_T(v) const long long v = clock64()
 #define IPROF_ADD(i, a, b) \
@@ -668,14 +682,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
       if (!dense) {
         // sparse <- sparse: tmpSet gets every code, then maybeToNormal
         const uint32_t npt = unique_sorted<1>(s_ptmp, P.ntmp, s_red);
-        const uint32_t nd = union_unique<1, kCPer, 2>(s_ptmp, npt, Cb, nl, Cb, s_red);
-        uint32_t hit = 0;
-        if (t < tc) {
-          const uint32_t c = s_tmp[t], l = lower_bound_u32(Cb, nd, c);
-          hit = l < nd && Cb[l] == c;
-        }
-        const uint32_t inter = block_allreduce_u32_sum(hit, s_red);
-        const uint32_t total = tc + nd - inter;
+        const uint32_t nd = union_small<2>(s_ptmp, npt, Cb, nl, Cb, s_red);
+        // the new tmpSet, tmpSet U the payload's codes, in Cb (its 512 spare words hold the tmpSet)
+        const uint32_t total = union_small<2>(s_tmp, tc, Cb, nd, Cb, s_red);
         IPROF_T(qc);
         IPROF_ADD(12, q0, qa);
         IPROF_ADD(13, qa, qb);
@@ -683,21 +692,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         IPROF_INC(15, total * 100u > kHllM ? 1 : 0);
         if (total * 100u > kHllM) {
           // mergeSparse: list = list U tmpSet; then toNormal if its byte length > m
-          const uint32_t nd2 = union_unique<1, kCPer, 2>(s_tmp, tc, Cb, nd, Cb, s_red);
-          uint32_t hit2 = 0;
-          for (uint32_t i = t; i < nd2; i += kBlock) {
-            const uint32_t c = Cb[i], l = lower_bound_u32(U, lc, c);
-            hit2 += l < lc && U[l] == c;
-          }
-          const uint32_t cnt = lc + nd2 - block_allreduce_u32_sum(hit2, s_red);
           s_tmp[t] = kHllNoCode;
           tc = 0;
           IPROF_T(qd);
           IPROF_ADD(16, qc, qd);
+          const uint32_t cnt = union_unique<kPer, kCPer, 1>(U, lc, Cb, total, U, s_red, kArenaWords);
+          IPROF_T(qe);
+          IPROF_ADD(17, qd, qe);
           if (cnt <= kArenaWords) {
-            lc = union_unique<kPer, kCPer, 1>(U, lc, Cb, nd2, U, s_red);
-            IPROF_T(qe);
-            IPROF_ADD(17, qd, qe);
+            lc = cnt;
             lbytes = list_bytes(U, lc, s_red);
             list_dirty = true;
             if (lbytes > kHllM) {
@@ -705,16 +708,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
               if (t == 0) s_nz = z;
               dense = true;
             }
-          } else {  // more codes than a sparse list can hold: certainly over m bytes
-            const uint32_t z = to_normal(U, U, lc, Cb, nd2, s_b, s_red);
+          } else {  // more codes than a sparse list can hold (U untouched): certainly over m bytes
+            const uint32_t z = to_normal(U, U, lc, Cb, total, s_b, s_red);
             if (t == 0) s_nz = z;
             dense = true;
           }
           __syncthreads();
           IPROF_INC(10, dense ? 1 : 0);
         } else {
-          tc = union_unique<1, kCPer, 1>(s_tmp, tc, Cb, nd, s_tmp, s_red);
-          s_tmp[t] = t < tc ? s_tmp[t] : kHllNoCode;
+          tc = total;
+          s_tmp[t] = t < tc ? Cb[t] : kHllNoCode;
           __syncthreads();
           IPROF_T(qf);
           IPROF_ADD(18, qc, qf);
