@@ -696,7 +696,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
           tc = 0;
           IPROF_T(qd);
           IPROF_ADD(16, qc, qd);
-          const uint32_t cnt = union_unique<kPer, kCPer, 1>(U, lc, Cb, total, U, s_red, kArenaWords);
+          // (staging sized to the operands: a list or payload of at most 2048 codes takes 8 per thread)
+          const uint32_t cnt =
+              lc <= 8 * kBlock
+                  ? (total <= 8 * kBlock ? union_unique<8, 8, 1>(U, lc, Cb, total, U, s_red, kArenaWords)
+                                         : union_unique<8, kCPer, 1>(U, lc, Cb, total, U, s_red, kArenaWords))
+                  : (total <= 8 * kBlock ? union_unique<kPer, 8, 1>(U, lc, Cb, total, U, s_red, kArenaWords)
+                                         : union_unique<kPer, kCPer, 1>(U, lc, Cb, total, U, s_red, kArenaWords));
           IPROF_T(qe);
           IPROF_ADD(17, qd, qe);
           if (cnt <= kArenaWords) {
