@@ -141,6 +141,25 @@ def test_import_histos_sliced_through_a_small_run_bit_exact():
         _check_histos(e, w, range(nk))
 
 
+def test_import_histos_more_slices_than_one_cut_pass_bit_exact():
+    """A call cut into more slices than one device pass of k_import_cuts finds (1024): the histo
+    class capped at 64 records, so each slice holds one or two 20-40-sample digests; 1300 payloads,
+    merged in arrival order, bit-exact against the restated Go's per-payload Merge."""
+    rng = np.random.default_rng(29)
+    nk, npay = 5, 1300
+    w = oracle.Worker(1, 1, nk, 1)
+    slots = rng.integers(0, nk, npay).astype(np.uint32)
+    pays = [digest_payload(rng, int(rng.integers(20, 40))) for _ in slots]
+    for s, p in zip(slots, pays):
+        t = oracle.MergingDigest(100.0)
+        t.gob_decode(p)
+        assert w.import_histo(int(s), p, identity(len(t.centroids()[0]))) == 0
+    with V.Engine((1, 1, nk, 1), percentiles=PCT, max_batch_records=1 << 14, max_batch_member_bytes=1 << 18,
+                  max_class_records=(0, 0, 64, 0)) as e:
+        e.import_histos(slots, pays)
+        _check_histos(e, w, range(nk))
+
+
 def test_import_histos_oversize_digest_refused_before_anything_applies():
     """a payload larger than the run is refused up front: nothing of the call is applied"""
     rng = np.random.default_rng(24)
