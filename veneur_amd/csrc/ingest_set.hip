@@ -48,6 +48,46 @@ struct SetCtx {
   uint32_t* bt;         // touched flags: k_set_small marks the keys it took with 2
 };
 
+// mergeSparse's move: list U[0, lc) shifted up by the new codes inserted below each element
+// (s_lbs: the new codes' insertion points, ascending); thread t moves rows [t*jmax, (t+1)*jmax),
+// KP >= jmax of them staged in registers before the barrier and written after it
+template <int KP>
+__device__ __forceinline__ void shift_list_up(uint32_t* U, uint32_t lc, uint32_t nnew, const uint32_t* s_lbs, int jmax,
+                                              uint32_t t) {
+  const uint32_t i0 = t * (uint32_t)jmax;
+  uint32_t keep[KP];
+#pragma unroll
+  for (int j = 0; j < KP; j++) {
+    if (j >= jmax) break;
+    const uint32_t i = i0 + (uint32_t)j;
+    keep[j] = i < lc ? U[i] : 0u;
+  }
+  uint32_t r = 0;  // new codes inserted at or before i0
+  {
+    uint32_t l = 0, h = nnew;
+    while (l < h) {
+      const uint32_t m = (l + h) >> 1;
+      if (s_lbs[m] <= i0) l = m + 1;
+      else h = m;
+    }
+    r = l;
+  }
+  uint32_t nextlb = r < nnew ? s_lbs[r] : 0xffffffffu;
+  lds_barrier();
+#pragma unroll
+  for (int j = 0; j < KP; j++) {
+    if (j >= jmax) break;
+    const uint32_t i = i0 + (uint32_t)j;
+    if (i < lc) {
+      while (nextlb <= i) {
+        r++;
+        nextlb = r < nnew ? s_lbs[r] : 0xffffffffu;
+      }
+      U[i + r] = keep[j];
+    }
+  }
+}
+
 // A key that stays sparse and cannot reach a mergeSparse trigger in this batch (tmpSet codes +
 // batch records < 164): Insert only adds the batch's new codes to the tmpSet (hyperloglog.go:
 // 186-200), in arrival order as k_set_segments stores them.  One wave per key, 2.6 KiB of LDS,
@@ -389,41 +429,13 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
         if (last_in_gap && lb < lc) dbytes += varint_len(succS - code) - varint_len(succS - predS);
       }
       // move list elements up by the number of new codes below them: thread t moves the
-      // contiguous rows [t*jmax, (t+1)*jmax), walking the insertion points alongside
+      // contiguous rows [t*jmax, (t+1)*jmax), walking the insertion points alongside (staged in
+      // registers: 8 rows per thread while the list holds at most 2048 codes -- the 65-row staging
+      // of a full list lives partly in scratch)
       constexpr int kPer = (kArenaWords + kBlock - 1) / kBlock;
       const int jmax = (int)((lc + kBlock - 1) / kBlock);  // list elements per thread (uniform)
-      const uint32_t i0 = t * (uint32_t)jmax;
-      uint32_t keep[kPer];
-#pragma unroll
-      for (int j = 0; j < kPer; j++) {
-        if (j >= jmax) break;
-        const uint32_t i = i0 + (uint32_t)j;
-        keep[j] = i < lc ? U[i] : 0u;
-      }
-      uint32_t r = 0;  // new codes inserted at or before i0
-      {
-        uint32_t l = 0, h = nnew;
-        while (l < h) {
-          const uint32_t m = (l + h) >> 1;
-          if (s_lbs[m] <= i0) l = m + 1;
-          else h = m;
-        }
-        r = l;
-      }
-      uint32_t nextlb = r < nnew ? s_lbs[r] : 0xffffffffu;
-      lds_barrier();
-#pragma unroll
-      for (int j = 0; j < kPer; j++) {
-        if (j >= jmax) break;
-        const uint32_t i = i0 + (uint32_t)j;
-        if (i < lc) {
-          while (nextlb <= i) {
-            r++;
-            nextlb = r < nnew ? s_lbs[r] : 0xffffffffu;
-          }
-          U[i + r] = keep[j];
-        }
-      }
+      if (jmax <= 8) shift_list_up<8>(U, lc, nnew, s_lbs, jmax, t);
+      else shift_list_up<kPer>(U, lc, nnew, s_lbs, jmax, t);
       if (isnew) U[lb + rank] = code;
       lds_barrier();
       const uint32_t nlc = lc + nnew;
@@ -443,6 +455,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
       SPROF_ADD(2, p_scan1, p_merge1);
       if (bytes > kHllM) {
         // toNormal: registers from the merged list (b stays; nz > 0 so no rebase can occur)
+        uint32_t keep[kPer];
 #pragma unroll
         for (int j = 0; j < kPer; j++) {
           uint32_t i = t + j * kBlock;
