@@ -92,3 +92,32 @@ def test_c4_window_through_engine_matches_oracle():
     assert err.max() <= 1e-3, err.max()
     np.testing.assert_array_equal(f.histo_quantiles, oq)
     st.free()
+
+
+def test_c4_window_tenth_scale_every_key_bit_exact():
+    """The C4 window at a tenth of its size -- 100k keys, 100M samples, the bench's stream, every key
+    on its owner (the default exact mode, no split) -- against the restated Go worker over every
+    key of every class: counters, gauges and set estimates bit-exact, histogram min/max/weight
+    exact, sums within 1e-12, every histogram key's quantiles bit-identical (the hottest timer key
+    here holds ~1.9M samples: the batched replay)."""
+    keys, n_samples = 100_000, 100_000_000
+    st = V.DeviceStream(SEED, keys, n_samples, 0, 1)
+    d = st.to_host()
+    n = st.n_slots
+    with V.Engine(n, percentiles=PCT, max_batch_records=max(st.counts) + 1,
+                  max_batch_member_bytes=st.counts[3] * 11 + 64) as e:
+        e.ingest_device(st.batch)
+        f = e.flush()
+    st.free()
+    w = run_oracle(d, n)
+    assert dict(zip(f.counter_slot.tolist(), f.counter_value.tolist())) == \
+        {s: w.counter_value(s) for s in range(n[0]) if w.touched(0, s)}
+    assert dict(zip(f.gauge_slot.tolist(), f.gauge_value.tolist())) == \
+        {s: w.gauge_value(s) for s in range(n[1]) if w.touched(1, s)}
+    assert dict(zip(f.set_slot.tolist(), f.set_estimate.tolist())) == \
+        {s: w.set_estimate(s) for s in range(n[3]) if w.touched(3, s)}
+    ost = np.array([w.histo_stats(int(s)) for s in f.histo_slot])
+    np.testing.assert_array_equal(f.histo_stats[:, [0, 1, 2]], ost[:, [0, 1, 2]])
+    np.testing.assert_allclose(f.histo_stats[:, 3:5], ost[:, 3:5], rtol=1e-12)
+    oq = np.array([[w.histo_quantile(int(s), p) for p in PCT] for s in f.histo_slot])
+    np.testing.assert_array_equal(f.histo_quantiles, oq)

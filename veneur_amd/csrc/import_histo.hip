@@ -492,21 +492,26 @@ __global__ void k_gob_emit_seg(uint64_t n, const uint64_t* __restrict__ off, con
   if (q * kSeg >= c) return;
   const uint32_t m = min(kSeg, c - q * kSeg);
   GobIn r(bytes + off[i], (uint32_t)(off[i + 1] - off[i]), ckpt[i * kSegs + q]);
-  double qm[kSeg], qw[kSeg];
-#pragma unroll
-  for (uint32_t j = 0; j < kSeg; j++) {
-    qm[j] = 0.0;
-    qw[j] = 0.0;
-    if (j < m) (void)r.centroid(qm[j], qw[j]);
-  }
   double* const dm = omean + o + q * kSeg;
   double* const dw = ow + o + q * kSeg;
+  // two halves of eight: parsed into registers, then stored (fewer registers than one queue of
+  // sixteen: more waves per SIMD; each half still fills 64 contiguous bytes per array)
 #pragma unroll
-  for (uint32_t j = 0; j < kSeg; j++)
-    if (j < m) {
-      dm[j] = qm[j];
-      dw[j] = qw[j];
+  for (uint32_t h = 0; h < kSeg; h += 8) {
+    double qm[8], qw[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++) {
+      qm[j] = 0.0;
+      qw[j] = 0.0;
+      if (h + j < m) (void)r.centroid(qm[j], qw[j]);
     }
+#pragma unroll
+    for (uint32_t j = 0; j < 8; j++)
+      if (h + j < m) {
+        dm[h + j] = qm[j];
+        dw[h + j] = qw[j];
+      }
+  }
 }
 
 // A call's payloads [b0, n) cut greedily into slices of whole payloads, each at most cap centroids
@@ -553,6 +558,27 @@ __global__ void k_pay_counts(uint64_t n, const uint64_t* __restrict__ key, const
   if (i >= n) return;
   const uint32_t p = (uint32_t)key[i];
   cnt[i] = pbeg[p + 1] - pbeg[p];
+}
+// the key segments of the grouped run at payload granularity (the payloads in key order, pdst
+// their places): a key starts at its first payload's place and ends after its last payload, both
+// among the payloads with centroids -- what k_seg_mark finds from every record
+__global__ void k_pay_seg_mark(uint64_t n, const uint64_t* __restrict__ key, const uint32_t* __restrict__ pdst,
+                               const uint32_t* __restrict__ pcnt, uint32_t* __restrict__ start, uint32_t* __restrict__ end,
+                               uint32_t* __restrict__ bt, uint32_t* __restrict__ touch) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || !pcnt[i]) return;  // (a digest without centroids makes no record: no segment)
+  const uint32_t s = (uint32_t)(key[i] >> 32);
+  // the key's first and last payload with centroids (empty digests are rare: short walks)
+  uint64_t j = i;
+  while (j > 0 && (uint32_t)(key[j - 1] >> 32) == s && !pcnt[j - 1]) j--;
+  if (j == 0 || (uint32_t)(key[j - 1] >> 32) != s) {
+    start[s] = pdst[i];
+    bt[s] = 1;
+    touch[s] = 1;
+  }
+  j = i + 1;
+  while (j < n && (uint32_t)(key[j] >> 32) == s && !pcnt[j]) j++;
+  if (j == n || (uint32_t)(key[j] >> 32) != s) end[s] = pdst[i] + pcnt[i];
 }
 // one wave per payload in key order: its centroids as grouped histo records (A = mean bits,
 // B = slot << 32 | kTagImport | run index, the record k_histo_keys_raw makes of an import)
@@ -680,7 +706,9 @@ void histo_imports_drain(vn_engine* e) {
   scan_exclusive_u32(s.pcnt, s.pdst, np, e->ss, st);
   hipLaunchKernelGGL(k_pay_move, dim3(blocks_for(np, 4)), dim3(256), 0, st, np, key, s.pbeg, s.pdst, s.cmean, e->hA0,
                      e->hB0);
-  histo_process(e, n, histo_group_sorted(e, n, e->hA0, e->hB0, e->hA1, e->hB1), s.cw);
+  hipLaunchKernelGGL(k_pay_seg_mark, dim3(blocks_for(np, 256)), dim3(256), 0, st, np, key, s.pdst, s.pcnt, e->h_start,
+                     e->h_end, e->h_bt, e->htouch);
+  histo_process(e, n, histo_group_sorted(e, n, e->hA0, e->hB0, e->hA1, e->hB1, true), s.cw);
   if (a && b) VN_HIP_CHECK(hipEventRecord(b, st));
 }
 

@@ -1222,12 +1222,14 @@ HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const do
 
 // records already grouped by key in arrival order (As / Bs as histo_group leaves them, e.g. the
 // import drain's payload-ordered move): the segment bounds and touched keys only
-HistoGroups histo_group_sorted(vn_engine* e, uint64_t n, uint64_t* As, uint64_t* Bs, uint64_t* Ao, uint64_t* Bo) {
+HistoGroups histo_group_sorted(vn_engine* e, uint64_t n, uint64_t* As, uint64_t* Bs, uint64_t* Ao, uint64_t* Bo,
+                               bool marked) {
   HistoGroups g{As, Bs, Ao, Bo};
   if (!n) return g;
   hipStream_t st = e->st;
-  hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, g.Bs, e->h_start, e->h_end, e->h_bt,
-                     e->htouch);
+  if (!marked)  // (marked: the caller set start / end / bt / touch already)
+    hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, g.Bs, e->h_start, e->h_end, e->h_bt,
+                       e->htouch);
   compact_flags(e->h_bt, e->h_pos, e->h_tl, e->h_cnt, e->cap[VN_HISTO], e->ss, st);
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt, e->h_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   return g;

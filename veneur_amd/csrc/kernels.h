@@ -43,7 +43,10 @@ struct HistoGroups {
   uint64_t *As, *Bs, *Ao, *Bo;  // key-grouped records and the spare pair
 };
 HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate);
-HistoGroups histo_group_sorted(vn_engine* e, uint64_t n, uint64_t* As, uint64_t* Bs, uint64_t* Ao, uint64_t* Bo);
+// records already grouped by key in As/Bs: per-key segments (k_seg_mark, unless the caller marked
+// them: marked), the touched-key list
+HistoGroups histo_group_sorted(vn_engine* e, uint64_t n, uint64_t* As, uint64_t* Bs, uint64_t* Ao, uint64_t* Bo,
+                               bool marked = false);
 void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double* impw = nullptr);
 void ingest_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate,
                    const double* impw = nullptr);
