@@ -52,7 +52,7 @@ def main(prof_dir, bench_json, nsteps=1, stats_out=None):
         if row.get("trace_kernels"):  # a phase of several kernels: every launch of each ("a&b": both in the name)
             pick = [(d, 0) for name, v in per.items() for d in v
                     if any(all(tok in name for tok in pat.split("&")) for pat in row["trace_kernels"])]
-            ls = pick
+            ls, nb = pick, len(pick)
         ms_trace = sum(d for d, _ in pick) / 1e6 / nsteps
         rest = sum(d for d, _ in ls[nb:]) / 1e6 / nsteps
         print("%-16s trace %.3f ms/step over its %d largest launches (+%.3f ms in %d others), bench %.3f ms/step: "
