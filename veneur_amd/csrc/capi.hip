@@ -184,6 +184,9 @@ void create_impl(vn_engine* e) {
   VN_HIP_CHECK(hipEventCreate(&e->ev_w0));
   VN_HIP_CHECK(hipEventCreate(&e->ev_wmain));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join3, hipEventDisableTiming));
+  VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st_imp, hipStreamNonBlocking, prio_hi));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_imp_free, hipEventDisableTiming));
+  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_imp_emit, hipEventDisableTiming));
   hipStream_t st = e->st;
   // each class's buffers sized by its own record cap
   const uint64_t R = e->max_cls[VN_HISTO], Rcg = std::max(e->max_cls[VN_COUNTER], e->max_cls[VN_GAUGE]),
@@ -393,6 +396,7 @@ void ensure_import(vn_engine* e, uint64_t n, uint64_t nbytes) {
     s.cap_cent = e->max_cls[VN_HISTO];  // the drains ingest them as histo records
     dalloc(s.cmean, s.cap_cent);
     dalloc(s.cw, s.cap_cent);
+    dalloc(s.cw_alt, s.cap_cent);
     s.cap_pay = e->max_records;  // payloads of one import call, at most
     dalloc(s.pslot, s.cap_pay);
     dalloc(s.pbeg, s.cap_pay + 1);
@@ -488,7 +492,7 @@ void destroy_impl(vn_engine* e) {
   ImportScratch& is = e->imp;
   dfree(is.in_slot); dfree(is.in_off); dfree(is.in_bytes); dfree(is.cnt); dfree(is.coff); dfree(is.cpos); dfree(is.ckpt); dfree(is.cuts); hfree(is.hcuts); dfree(is.cslot);
   dfree(is.pslot); dfree(is.pbeg); dfree(is.pkey); dfree(is.pcnt); dfree(is.pdst);
-  dfree(is.cmean); dfree(is.cw);
+  dfree(is.cmean); dfree(is.cw); dfree(is.cw_alt);
   if (is.parts) (void)hipFree(is.parts);
   DeviceBatch& d = e->dstage;
   dfree(d.c_slot); dfree(d.c_val); dfree(d.c_rate); dfree(d.g_slot); dfree(d.g_val);
@@ -510,6 +514,16 @@ void destroy_impl(vn_engine* e) {
   if (e->ss2.partials) (void)hipFree(e->ss2.partials);
   if (e->st2) (void)hipStreamSynchronize(e->st2);
   if (e->st3) (void)hipStreamSynchronize(e->st3);
+  if (e->st_imp) {
+    (void)hipStreamSynchronize(e->st_imp);
+    (void)hipStreamDestroy(e->st_imp);
+    e->st_imp = nullptr;
+  }
+  for (hipEvent_t* ev : {&e->ev_imp_free, &e->ev_imp_emit})
+    if (*ev) {
+      (void)hipEventDestroy(*ev);
+      *ev = nullptr;
+    }
   if (e->ev_fork3) (void)hipEventDestroy(e->ev_fork3);
   if (e->ev_join3) (void)hipEventDestroy(e->ev_join3);
   if (e->st3) (void)hipStreamDestroy(e->st3);

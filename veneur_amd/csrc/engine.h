@@ -40,6 +40,8 @@ struct ImportScratch {
   uint32_t* cslot = nullptr;      // [cap_cent] decoded centroids: slot, mean, weight
   double* cmean = nullptr;
   double* cw = nullptr;
+  double* cw_alt = nullptr;       // the other weights buffer: a drain's replay reads one while the
+                                  // next slice's emit fills the other
   uint64_t acc = 0;               // imported histo centroids appended, not yet merged (import_histo.hip)
   // the run's payloads in arrival order (the drain groups them by key, not their centroids)
   uint64_t cap_pay = 0, npay = 0;
@@ -120,6 +122,8 @@ struct vn_engine {
   int device = 0;
   hipStream_t st = nullptr;       // main stream (histos, flush, staging copies)
   hipStream_t st2 = nullptr;      // side stream: counters, gauges and sets overlap the histo path
+  hipStream_t st_imp = nullptr;   // histo import emits: the next slice beside the previous drain's replay
+  hipEvent_t ev_imp_free = nullptr, ev_imp_emit = nullptr;  // the run read by its drain / its emits done
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_h2d = nullptr;    // recorded after a host batch's copies into HBM (vn_submit waits on it)
   // window milestones (vn_timing.ms_main_ready / ms_split_ready): first ingest call of the

@@ -630,17 +630,29 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   take_decode_error(e);
   const uint64_t nc = e->hf_cnt[9];
   if (!nc) return;
+  // The emits run on their own stream (in timing mode on st, between their events): once the
+  // previous drain has read the run (ev_imp_free, after its k_pay_move), a slice's emit goes on
+  // beside that drain's replay, filling the other weights buffer; the next drain waits for it
+  // (ev_imp_emit).  The count pass, the scan and the cuts above ran on st and were waited for.
+  hipStream_t se = e->timing ? st : e->st_imp;
+  auto emit = [&](uint64_t m, uint64_t b0, uint64_t base) {
+    VN_HIP_CHECK(hipStreamWaitEvent(se, e->ev_imp_free, 0));
+    ev_pair(e->pool_id, [&] {
+      hipLaunchKernelGGL(k_gob_emit_seg, dim3(blocks_for(m * kSegs, 256)), dim3(256), 0, se, m, off + b0, bytes,
+                         slot + b0, s.coff + b0, s.cpos + b0, s.ckpt + b0 * kSegs, base, s.cmean, s.cw, s.pslot,
+                         s.pbeg, s.npay);
+      hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(m, 256)), dim3(256), 0, se, m, off + b0, bytes, slot + b0,
+                         s.coff + b0, s.cpos + b0, base, s.cmean, s.cw, s.pslot, s.pbeg, s.npay, e->h_err);
+    });
+    VN_HIP_CHECK(hipEventRecord(e->ev_imp_emit, se));
+  };
   if (nc <= s.cap_cent && n <= s.cap_pay) {
     if (s.acc + nc > s.cap_cent || s.npay + n > s.cap_pay) histo_imports_drain(e);
-    ev_pair(e->pool_id, [&] {
-      hipLaunchKernelGGL(k_gob_emit_seg, dim3(blocks_for(n * kSegs, 256)), dim3(256), 0, st, n, off, bytes, slot,
-                         s.coff, s.cpos, s.ckpt, s.acc, s.cmean, s.cw, s.pslot, s.pbeg, s.npay);
-      hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, off, bytes, slot, s.coff, s.cpos,
-                         s.acc, s.cmean, s.cw, s.pslot, s.pbeg, s.npay, e->h_err);
-    });
+    emit(n, 0, s.acc);
     s.acc += nc;
     s.npay += n;
-    return;
+    VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_imp_emit, 0));  // (later work on st -- a staging copy
+    return;                                                    // over these payloads -- after the emits)
   }
   // slices of whole payloads in arrival order, each at most the run, cut greedily on the device
   // (k_import_cuts: only the cuts come back, not the 4-byte scan of every payload -- that copy and
@@ -663,18 +675,12 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
     const uint64_t b0 = cuts[q].first, b1 = cuts[q + 1].first, c0 = cuts[q].second, c1 = cuts[q + 1].second;
     if (c1 > c0) {
       if (s.acc + (c1 - c0) > s.cap_cent || s.npay + (b1 - b0) > s.cap_pay) histo_imports_drain(e);
-      ev_pair(e->pool_id, [&] {
-        hipLaunchKernelGGL(k_gob_emit_seg, dim3(blocks_for((b1 - b0) * kSegs, 256)), dim3(256), 0, st, b1 - b0,
-                           off + b0, bytes, slot + b0, s.coff + b0, s.cpos + b0, s.ckpt + b0 * kSegs, s.acc - c0,
-                           s.cmean, s.cw, s.pslot, s.pbeg, s.npay);
-        hipLaunchKernelGGL(k_gob_emit, dim3(blocks_for(b1 - b0, 256)), dim3(256), 0, st, b1 - b0, off + b0, bytes,
-                           slot + b0, s.coff + b0, s.cpos + b0, s.acc - c0, s.cmean, s.cw, s.pslot, s.pbeg, s.npay,
-                           e->h_err);
-      });
+      emit(b1 - b0, b0, s.acc - c0);
       s.acc += c1 - c0;
       s.npay += b1 - b0;
     }
   }
+  VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_imp_emit, 0));
 }
 
 // The run merges as one histo ingest.  Its centroids are grouped by key through their payloads:
@@ -693,6 +699,7 @@ void histo_imports_drain(vn_engine* e) {
   s.acc = 0;
   s.npay = 0;
   hipStream_t st = e->st;
+  VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_imp_emit, 0));  // the run's emits (st_imp) are done
   hipEvent_t a = e->timing ? e->pool_im.next() : nullptr, b = e->timing ? e->pool_im.next() : nullptr;
   if (a && b) VN_HIP_CHECK(hipEventRecord(a, st));
   hipLaunchKernelGGL(k_pay_keys, dim3(blocks_for(np, 256)), dim3(256), 0, st, np, s.pslot, s.pkey, s.pbeg,
@@ -708,7 +715,10 @@ void histo_imports_drain(vn_engine* e) {
                      e->hB0);
   hipLaunchKernelGGL(k_pay_seg_mark, dim3(blocks_for(np, 256)), dim3(256), 0, st, np, key, s.pdst, s.pcnt, e->h_start,
                      e->h_end, e->h_bt, e->htouch);
-  histo_process(e, n, histo_group_sorted(e, n, e->hA0, e->hB0, e->hA1, e->hB1, true), s.cw);
+  VN_HIP_CHECK(hipEventRecord(e->ev_imp_free, st));  // the payload table and the means are read
+  double* const w = s.cw;
+  std::swap(s.cw, s.cw_alt);  // the next emits fill the other weights buffer while this replay reads w
+  histo_process(e, n, histo_group_sorted(e, n, e->hA0, e->hB0, e->hA1, e->hB1, true), w);
   if (a && b) VN_HIP_CHECK(hipEventRecord(b, st));
 }
 
