@@ -184,9 +184,6 @@ void create_impl(vn_engine* e) {
   VN_HIP_CHECK(hipEventCreate(&e->ev_w0));
   VN_HIP_CHECK(hipEventCreate(&e->ev_wmain));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join3, hipEventDisableTiming));
-  VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st_imp, hipStreamNonBlocking, prio_hi));
-  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_imp_free, hipEventDisableTiming));
-  VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_imp_emit, hipEventDisableTiming));
   hipStream_t st = e->st;
   // each class's buffers sized by its own record cap
   const uint64_t R = e->max_cls[VN_HISTO], Rcg = std::max(e->max_cls[VN_COUNTER], e->max_cls[VN_GAUGE]),

@@ -634,6 +634,14 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   // previous drain has read the run (ev_imp_free, after its k_pay_move), a slice's emit goes on
   // beside that drain's replay, filling the other weights buffer; the next drain waits for it
   // (ev_imp_emit).  The count pass, the scan and the cuts above ran on st and were waited for.
+  if (!e->st_imp) {
+    // created at the first histo import, not with the engine: hardware queues are dealt to streams
+    // in creation order, and one more stream per engine made two engines' streams share a queue
+    // (windows in flight then ran in lock step: C4 80.6 -> 140.9 ms per window)
+    VN_HIP_CHECK(hipStreamCreateWithFlags(&e->st_imp, hipStreamNonBlocking));
+    VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_imp_free, hipEventDisableTiming));
+    VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_imp_emit, hipEventDisableTiming));
+  }
   hipStream_t se = e->timing ? st : e->st_imp;
   auto emit = [&](uint64_t m, uint64_t b0, uint64_t base) {
     VN_HIP_CHECK(hipStreamWaitEvent(se, e->ev_imp_free, 0));
@@ -699,7 +707,7 @@ void histo_imports_drain(vn_engine* e) {
   s.acc = 0;
   s.npay = 0;
   hipStream_t st = e->st;
-  VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_imp_emit, 0));  // the run's emits (st_imp) are done
+  if (e->ev_imp_emit) VN_HIP_CHECK(hipStreamWaitEvent(st, e->ev_imp_emit, 0));  // the run's emits (st_imp) are done
   hipEvent_t a = e->timing ? e->pool_im.next() : nullptr, b = e->timing ? e->pool_im.next() : nullptr;
   if (a && b) VN_HIP_CHECK(hipEventRecord(a, st));
   hipLaunchKernelGGL(k_pay_keys, dim3(blocks_for(np, 256)), dim3(256), 0, st, np, s.pslot, s.pkey, s.pbeg,
@@ -715,7 +723,7 @@ void histo_imports_drain(vn_engine* e) {
                      e->hB0);
   hipLaunchKernelGGL(k_pay_seg_mark, dim3(blocks_for(np, 256)), dim3(256), 0, st, np, key, s.pdst, s.pcnt, e->h_start,
                      e->h_end, e->h_bt, e->htouch);
-  VN_HIP_CHECK(hipEventRecord(e->ev_imp_free, st));  // the payload table and the means are read
+  if (e->ev_imp_free) VN_HIP_CHECK(hipEventRecord(e->ev_imp_free, st));  // the payload table and the means are read
   double* const w = s.cw;
   std::swap(s.cw, s.cw_alt);  // the next emits fill the other weights buffer while this replay reads w
   histo_process(e, n, histo_group_sorted(e, n, e->hA0, e->hB0, e->hA1, e->hB1, true), w);
