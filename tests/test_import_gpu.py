@@ -160,6 +160,30 @@ def test_import_histos_more_slices_than_one_cut_pass_bit_exact():
         _check_histos(e, w, range(nk))
 
 
+def test_import_histos_empty_digests_among_others_bit_exact():
+    """Digests without centroids (a local veneur's key that received nothing) mixed into a call,
+    some keys receiving only those: the drain's key segments come from the payload table, where an
+    empty digest is a payload with no records -- every key's state, and which keys flush, as the
+    restated Go's per-payload Merge."""
+    rng = np.random.default_rng(31)
+    nk, npay = 8, 300
+    w = oracle.Worker(1, 1, nk, 1)
+    slots = rng.integers(0, nk, npay).astype(np.uint32)
+    slots[rng.random(npay) < 0.1] = nk - 1  # key nk-1: empty digests only
+    pays = []
+    for s in slots:
+        empty = s == nk - 1 or rng.random() < 0.25
+        pays.append(digest_payload(rng, 0 if empty else int(rng.integers(5, 120))))
+    for s, p in zip(slots, pays):
+        t = oracle.MergingDigest(100.0)
+        t.gob_decode(p)
+        assert w.import_histo(int(s), p, identity(len(t.centroids()[0]))) == 0
+    with V.Engine((1, 1, nk, 1), percentiles=PCT, max_batch_records=1 << 14, max_batch_member_bytes=1 << 18,
+                  max_class_records=(0, 0, 512, 0)) as e:  # (a run of 512 centroids: several drains)
+        e.import_histos(slots, pays)
+        _check_histos(e, w, range(nk))
+
+
 def test_import_histos_oversize_digest_refused_before_anything_applies():
     """a payload larger than the run is refused up front: nothing of the call is applied"""
     rng = np.random.default_rng(24)

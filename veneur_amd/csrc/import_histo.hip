@@ -514,6 +514,13 @@ __global__ void k_gob_emit_seg(uint64_t n, const uint64_t* __restrict__ off, con
   }
 }
 
+// Worker.ImportMetric Upserts the key before Combine (worker.go:241): every payload's key is in the
+// window, a digest without centroids included (it makes no record, so no segment marks it)
+__global__ void k_import_touch(uint64_t n, const uint32_t* __restrict__ slot, uint32_t* __restrict__ touch) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) touch[slot[i]] = 1;
+}
+
 // A call's payloads [b0, n) cut greedily into slices of whole payloads, each at most cap centroids
 // and cap_pay payloads (the run): one thread, a binary search over the centroid scan co per slice.
 // out: cuts[j] = first payload of slice j, cuts[kImportCuts + 1 + j] = co at it, j <= count; then
@@ -629,7 +636,15 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   VN_HIP_CHECK(hipStreamSynchronize(st));
   take_decode_error(e);
   const uint64_t nc = e->hf_cnt[9];
-  if (!nc) return;
+  // (once the call can no longer be refused: after the validation, and in the sliced path after
+  // the oversize check)
+  auto touch_all = [&] {
+    hipLaunchKernelGGL(k_import_touch, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, e->htouch);
+  };
+  if (!nc) {
+    touch_all();
+    return;
+  }
   // The emits run on their own stream (in timing mode on st, between their events): once the
   // previous drain has read the run (ev_imp_free, after its k_pay_move), a slice's emit goes on
   // beside that drain's replay, filling the other weights buffer; the next drain waits for it
@@ -655,6 +670,7 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
     VN_HIP_CHECK(hipEventRecord(e->ev_imp_emit, se));
   };
   if (nc <= s.cap_cent && n <= s.cap_pay) {
+    touch_all();
     if (s.acc + nc > s.cap_cent || s.npay + n > s.cap_pay) histo_imports_drain(e);
     emit(n, 0, s.acc);
     s.acc += nc;
@@ -679,6 +695,7 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
     b0 = s.hcuts[j];
     if (b0 >= n) cuts.emplace_back((uint32_t)n, s.hcuts[kImportCuts + 1 + j]);
   }
+  touch_all();
   for (size_t q = 0; q + 1 < cuts.size(); q++) {
     const uint64_t b0 = cuts[q].first, b1 = cuts[q + 1].first, c0 = cuts[q].second, c1 = cuts[q + 1].second;
     if (c1 > c0) {
