@@ -232,16 +232,20 @@ int vn_import_histos(vn_engine* eng, const uint32_t* slot, const uint64_t* off, 
  * only logged; a truncated payload fails the whole call with VN_EDECODE and applies nothing. */
 int vn_import_sets(vn_engine* eng, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n);
 
-/* MergingDigest.Quantile (kind 0, merging_digest.go:283-313) or CDF (kind 1, 247-279) of
- * histo slot[i]'s digest in the current window at arg[i], into out[i] (host arrays).  As in
- * the reference the pending temps are merged first (mergeAllTemps mutates the digest).
- * Quantile arguments outside [0, 1] are rejected (the reference panics). */
 /* The same two imports with slot/off/bytes already in device memory (HBM), e.g. payloads
- * another GPU's export sent by an RCCL all-gather (veneur_amd/dist.py hot-key exchange). */
+ * another GPU's export sent by an RCCL all-gather (veneur_amd/dist.py hot-key exchange).
+ * The call returns once the work is queued on the engine's streams, and the histo import's
+ * centroid emits read the payload buffers on a stream of their own after it returns: the caller
+ * keeps slot/off/bytes allocated and unmodified until the engine's next synchronizing call
+ * (vn_flush / vn_flush_masked, vn_sync, a host-array import or query) has returned. */
 int vn_import_histos_device(vn_engine* eng, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes,
                             uint64_t n);
 int vn_import_sets_device(vn_engine* eng, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes, uint64_t n);
 
+/* MergingDigest.Quantile (kind 0, merging_digest.go:283-313) or CDF (kind 1, 247-279) of
+ * histo slot[i]'s digest in the current window at arg[i], into out[i] (host arrays).  As in
+ * the reference the pending temps are merged first (mergeAllTemps mutates the digest).
+ * Quantile arguments outside [0, 1] are rejected (the reference panics). */
 int vn_histo_query(vn_engine* eng, int kind, const uint32_t* slot, const double* arg, uint64_t n, double* out);
 
 /* Forward encoders (flushForward, flusher.go:264-353): one payload per requested slot, in

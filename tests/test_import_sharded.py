@@ -144,3 +144,70 @@ def test_sharded_import_two_ranks_gloo_equals_single_consumer():
     ref = {(k.name, k.type, k.joined_tags): v for k, v in oracle_import(ms).items()}
     assert merged == ref
     assert all(len(r) > 0 for r in allres)  # both ranks own keys
+
+
+def _routed_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank))
+    try:
+        g = D.Group(backend="gloo")
+        router = D.ImportRouter(g, src=0)
+        mine, statuses = [], []
+        reqs = bodies() + [(b"[1,2", ""), (b"[]", ""), (b"x", "gzip")]  # + three rejected bodies
+        for body, enc in reqs:
+            st, part = router.route(body if rank == 0 else None, enc)
+            statuses.append(st)
+            mine += part
+        keys = [(m.key.name, m.key.type, m.key.joined_tags, tuple(m.tags), bytes(m.value)) for m in mine]
+        res = {(k.name, k.type, k.joined_tags): v for k, v in oracle_import(mine).items()}
+        allres = g.gather_object((router.decoded, statuses, keys, res))
+        g.barrier()
+        g.close()
+        if rank == 0:
+            q.put(allres)
+    except Exception as ex:  # surface the failure in the parent
+        q.put(repr(ex))
+        raise
+
+
+def test_import_router_decodes_each_body_once_two_ranks_gloo():
+    """one decode per /import body (on the listener's rank), its JSONMetrics
+    routed by digest % N to the ranks as newJSONMetricsByWorker routes them to workers
+    (http.go:52-139): each rank's share is route_imports' partition of the decoded body, bit for
+    bit, and the ranks' merges together equal the single consumer."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_routed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        allres = q.get(timeout=600)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert not isinstance(allres, str), allres
+    assert all(p.exitcode == 0 for p in procs)
+    n_bodies = len(bodies()) + 3
+    assert [a[0] for a in allres] == [n_bodies, 0]  # every body decoded once, on rank 0 only
+    for a in allres:
+        assert a[1] == [202] * len(bodies()) + [400, 400, 415]
+    ms = [m for body, enc in bodies() for m in H.unmarshal_metrics_from_http(body, enc)]
+    for r in range(world):
+        want = [(m.key.name, m.key.type, m.key.joined_tags, tuple(m.tags), bytes(m.value))
+                for m in D.route_imports(ms, r, world)]
+        assert allres[r][2] == want
+    merged = {}
+    for a in allres:
+        assert not set(a[3]) & set(merged)
+        merged.update(a[3])
+    ref = {(k.name, k.type, k.joined_tags): v for k, v in oracle_import(ms).items()}
+    assert merged == ref
+
+
+def test_pack_metrics_round_trip():
+    ms = [W.JSONMetric(K("a\u00e9", "timer", "x:1,y:\ufffd"), ["x:1", "y:\ufffd"], b"\x00\x01"),
+          W.JSONMetric(K("", "", ""), [], b""), W.JSONMetric(K("c", "counter", ""), [""], bytes(range(256)))]
+    back = D.unpack_metrics(D.pack_metrics(ms))
+    assert [(m.key, m.tags, m.value) for m in back] == [(m.key, m.tags, bytes(m.value)) for m in ms]

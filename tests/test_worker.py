@@ -682,3 +682,32 @@ def test_worker_drains_at_class_cap_and_pieces_imports():
     calls = [c[0] for c in w.engine.calls]
     assert calls.count("import_counters") == 3 and calls.count("import_sets") == 3
     assert w.Flush().counters[K("c", "counter")].value == 5
+
+
+def test_engine_with_pipeline_is_refused():
+    with pytest.raises(ValueError):
+        W.Worker(engine=RecordingEngine(), pipeline=3)
+
+
+def test_failed_flush_on_a_flush_thread_is_raised_when_its_engine_is_reused(caplog):
+    """D = 2: a flush that fails on its flush thread is raised (and counted) by the next call that
+    would hand that engine new records, instead of the window silently staying unflushed."""
+    class Failing(RecordingEngine):
+        def flush(self, *a, **k):
+            raise EngineError("hip error (rc=-3)")
+    bad, good = Failing(), RecordingEngine()
+    w = W.Worker(engines=[bad, good], batch_records=1000)
+    try:
+        key = W.MetricKey("a", "counter", "")
+        w.ProcessMetric(W.UDPMetric(key, 1.0, tags=[]))
+        fut = w.Flush()              # engine 0's flush fails on its thread
+        w.ProcessMetric(W.UDPMetric(key, 2.0, tags=[]))
+        w.Flush()                    # engine 1
+        with pytest.raises(EngineError):
+            w.ProcessMetric(W.UDPMetric(key, 3.0, tags=[]))
+            w.Flush()                # back to engine 0: its failed flush surfaces here
+        assert w.flush_errors == 1
+        with pytest.raises(EngineError):
+            fut.wait()
+    finally:
+        w.close()

@@ -92,3 +92,37 @@ def test_worker_in_turn_maps_equal_single_engine():
         finally:
             w.close()
     assert res[0] == res[1]
+
+
+def test_worker_in_turn_flush_datadog_shared_sink_equals_single_engine():
+    """One DatadogSink serving D = 3 engines' flush threads (their flushes overlap, each calls
+    vn_datadog_flush on the same vn_sink): every window's bodies equal those of D = 1."""
+    from veneur_amd.sink import DatadogSink
+    rng = np.random.default_rng(11)
+    windows = []
+    for i in range(8):
+        ms = []
+        for j in range(4000):
+            k = int(rng.integers(0, 300))
+            t = ("counter", "gauge", "timer", "set", "histogram")[k % 5]
+            v = ("m%d" % rng.integers(0, 900)) if t == "set" else float(np.round(rng.lognormal(2, 1), 3))
+            ms.append(W.UDPMetric(W.MetricKey("k%d" % k, t, "env:%d" % (k % 3)), v, tags=["env:%d" % (k % 3)]))
+        windows.append(ms)
+    agg = W.HistogramAggregates(W.Aggregate.AggregateMin | W.Aggregate.AggregateMax | W.Aggregate.AggregateCount |
+                                W.Aggregate.AggregateMedian)
+    res = []
+    for D in (1, 3):
+        w = W.Worker(capacity=(512,) * 4, percentiles=PCT, batch_records=1 << 10, pipeline=D)
+        sink = DatadogSink(10.0, "h", ["dc:1"], 50)
+        try:
+            outs = []
+            for ms in windows:
+                for m in ms:
+                    w.ProcessMetric(m)
+                outs.append(w.flush_datadog(sink, (0.9, 0.99), agg, timestamp=1234))
+            res.append([o.result(timeout=120) if D > 1 else o for o in outs])
+        finally:
+            w.close()
+            sink.close()
+    assert res[0] == res[1]
+    assert all(r[1][0] > 0 for r in res[0])

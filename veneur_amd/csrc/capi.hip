@@ -57,6 +57,9 @@ int fail(vn_engine* e, int code, const std::string& msg) {
 template <class F>
 int guarded(vn_engine* e, F&& f) {
   try {
+    // every entry point runs on the engine's device, whatever thread calls it (a Worker's flush
+    // threads, a cgo goroutine's OS thread): allocations made inside a call land on that device
+    if (e) VN_HIP_CHECK(hipSetDevice(e->device));
     f();
     return VN_OK;
   } catch (const HipError& h) {

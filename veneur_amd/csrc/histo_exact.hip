@@ -2405,6 +2405,13 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   PROF_ADDW(40, cw1, cw2);
   fast_sync<NW>();
   PROF_T(b4);
+#ifdef VN_REPLAY_CHECK
+  if (t == 0 && !B.ctl[4] && B.off[nm] != nt) {
+    printf("VN_REPLAY_CHECK merge_batch chunk %u: lists hold %u entries, %u temps (nm %u, b %u)\n", c, B.off[nm], nt, nm, b);
+    B.ctl[4] = 1u;
+  }
+  fast_sync<NW>();
+#endif
   if (B.ctl[4]) {
     fast_sync<NW>();
     return BatchResult{0u, true};
@@ -2694,6 +2701,39 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   return BatchResult{js, structural};
 }
 
+#ifdef VN_REPLAY_CHECK
+// Diagnostics build (VARIANT_FLAGS=-DVN_REPLAY_CHECK): the digest's invariants after every merge of
+// the long replays -- 1 <= nm <= capc, the means in order, and (exact weights) the main weights
+// summing to mainW in any order.  The first violation of a key is printed with where it happened
+// and the key is abandoned (its state in HBM left as it was before the call), so a broken merge
+// is named instead of feeding later merges.
+template <int NW>
+__device__ bool replay_check(const Lds L, const FastLds F, uint32_t nm, double mainW, uint32_t capc, bool fok,
+                             uint32_t s, uint32_t c, int where, uint32_t a0, uint32_t a1) {
+  constexpr uint32_t NT = 64 * NW;
+  const uint32_t t = threadIdx.x, wv = t >> 6, lane = t & 63;
+  if (t == 0) F.misc[6] = 0u;
+  fast_sync<NW>();
+  const uint32_t n = min(nm, capc);
+  bool bad = nm == 0 || nm > capc;
+  for (uint32_t j = t; j + 1 < n; j += NT)
+    if (!(L.mm[j] <= L.mm[j + 1])) bad = true;
+  if (bad) __atomic_fetch_or(&F.misc[6], 1u, __ATOMIC_RELAXED);
+  if (wv == 0 && fok) {
+    double acc = 0.0;
+    for (uint32_t b = 0; b < n; b += 64) acc = dadd(acc, wave_sum(b + lane < n ? L.mw[b + lane] : 0.0));
+    if (lane == 0 && acc != mainW) __atomic_fetch_or(&F.misc[6], 2u, __ATOMIC_RELAXED);
+  }
+  fast_sync<NW>();
+  const uint32_t r = F.misc[6];
+  fast_sync<NW>();
+  if (r && t == 0)
+    printf("VN_REPLAY_CHECK slot %u chunk %u where %d (%u, %u): flags %u nm %u mainW %.17g mm0 %.17g mw0 %.17g\n", s, c,
+           where, a0, a1, r, nm, mainW, L.mm[0], L.mw[0]);
+  return r != 0u;
+}
+#endif
+
 // replay of one key with NW waves (tcap <= 64, ingest only: no flush-mode adoption); BATCH:
 // merge_batch where the key's state allows (the dynamic LDS then holds the batch tables)
 template <int NW, bool BATCH>
@@ -2827,7 +2867,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       ccpk = x.cpk ? x.cpk[base] : 0xffffffffu;
     };
     // chunks [c0, c1) one merge at a time, the next chunk's loads in flight during each merge
-    auto singles = [&](uint32_t c0, uint32_t c1) {
+    auto singles = [&](uint32_t c0, uint32_t c1) -> bool {  // (false: VN_REPLAY_CHECK abandoned the key)
       load(c0);
       for (uint32_t c = c0; c < c1; c++) {
         // 0: some weight not exact; 1: exact; 2: exact and integers
@@ -2843,11 +2883,18 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
         hold_stats(sw, sxw, srw, mn, mx, dmn, dmx);
         if (c + 1 < c1) load(c + 1);
         fast_sync<NW>();
+#ifdef VN_REPLAY_CHECK
+        const uint32_t nm_was = nm;
+#endif
         merge_sorted_any(tcap, tempW, tintd != 0.0, tintd == 2.0);
+#ifdef VN_REPLAY_CHECK
+        if (replay_check<NW>(L, F, nm, mainW, capc, fok, s, c, 1, nm_was, (uint32_t)tintd)) return false;
+#endif
       }
+      return true;
     };
     if constexpr (!BATCH) {
-      singles(0, sp.npure);
+      if (!singles(0, sp.npure)) return;
     } else {
     const BatchLds Bt = batch_layout(smem + batch_offset(capc, tcap), tcap);
     const uint64_t cb = (uint64_t)lo + sp.off0;
@@ -2907,7 +2954,10 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
         // not (yet) batchable: a run of single merges, then look again
         const uint32_t c1 = min(sp.npure, c + kBatchBackoff);
         PROF_T(s3);
-        singles(c, c1);
+        if (!singles(c, c1)) {
+          dma_wait();
+          return;
+        }
         PROF_T(s4);
         PROF_ADD(30, s3, s4);
         PROF_ADD(31, 0, (long long)(c1 - c));
@@ -2932,7 +2982,16 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       }
       ring_lo = max(c, ring_hi > kRing ? ring_hi - kRing : 0u);
       PROF_T(s0);
+#ifdef VN_REPLAY_CHECK
+      const uint32_t nm_was = nm;
+#endif
       const BatchResult r = merge_batch<NW>(mp.delta, sin_hi, sin_lo, L, F, Bt, nm, mainW, c, b, tcap, fint);
+#ifdef VN_REPLAY_CHECK
+      if (r.js && replay_check<NW>(L, F, nm, mainW, capc, fok, s, c, 2, r.js, b | (nm_was << 8))) {
+        dma_wait();
+        return;
+      }
+#endif
       PROF_T(s1);
       PROF_ADD(27, s0, s1);
       const uint32_t cb_end = c + b;  // (the batch's chunks: landed in the ring)
@@ -2954,9 +3013,21 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
           }
           if (t == tcap) F.sp[tcap] = (double)(p0 >> 16);
           fast_sync<NW>();
+#ifdef VN_REPLAY_CHECK
+          const uint32_t nm_was2 = nm;
+#endif
           merge_sorted_any(tcap, (double)(p0 >> 16), true, true);
+#ifdef VN_REPLAY_CHECK
+          if (replay_check<NW>(L, F, nm, mainW, capc, fok, s, cs, 3, nm_was2, 0u)) {
+            dma_wait();
+            return;
+          }
+#endif
         }
-        if (cs < c1) singles(cs, c1);
+        if (cs < c1 && !singles(cs, c1)) {
+          dma_wait();
+          return;
+        }
         PROF_T(s2);
         PROF_ADD(28, s1, s2);
         PROF_ADD(29, 0, (long long)(c1 - c));

@@ -1338,6 +1338,7 @@ int split_fail(vn_engine* e, int code, const std::string& m) {
 template <class F>
 int split_guarded(vn_engine* e, F&& f) {
   try {
+    if (e) VN_HIP_CHECK(hipSetDevice(e->device));  // as capi.hip's guarded: the engine's device
     f();
     return VN_OK;
   } catch (const HipError& h) {

@@ -131,6 +131,106 @@ def route_imports(metrics, rank, world):
     return [m for m in metrics if metric_digest(m.key) % int(world) == int(rank)]
 
 
+def pack_metrics(metrics):
+    """JSONMetrics as one byte string (the chunk a rank is sent): per metric the five fields of
+    samplers.JSONMetric, each length-prefixed -- name, type, tagstring, the tags, value."""
+    import struct
+    out = [struct.pack("<I", len(metrics))]
+    for m in metrics:
+        f = [m.key.name.encode("utf-8", "surrogatepass"), m.key.type.encode("utf-8", "surrogatepass"),
+             m.key.joined_tags.encode("utf-8", "surrogatepass")]
+        tags = [t.encode("utf-8", "surrogatepass") for t in m.tags]
+        val = bytes(m.value) if m.value is not None else b""
+        out.append(struct.pack("<IIIII", len(f[0]), len(f[1]), len(f[2]), len(tags), len(val)))
+        out += f
+        out += [struct.pack("<I", len(t)) + t for t in tags]
+        out.append(val)
+    return b"".join(out)
+
+
+def unpack_metrics(buf):
+    """pack_metrics' inverse: the JSONMetrics in their order."""
+    import struct
+    from .worker import JSONMetric, MetricKey
+    mv = memoryview(buf)
+    n, = struct.unpack_from("<I", mv, 0)
+    p = 4
+    out = []
+    for _ in range(n):
+        ln, lt, lj, nt, lv = struct.unpack_from("<IIIII", mv, p)
+        p += 20
+        name = bytes(mv[p:p + ln]).decode("utf-8", "surrogatepass")
+        p += ln
+        typ = bytes(mv[p:p + lt]).decode("utf-8", "surrogatepass")
+        p += lt
+        joined = bytes(mv[p:p + lj]).decode("utf-8", "surrogatepass")
+        p += lj
+        tags = []
+        for _ in range(nt):
+            l, = struct.unpack_from("<I", mv, p)
+            tags.append(bytes(mv[p + 4:p + 4 + l]).decode("utf-8", "surrogatepass"))
+            p += 4 + l
+        out.append(JSONMetric(MetricKey(name, typ, joined), tags, bytes(mv[p:p + lv])))
+        p += lv
+    return out
+
+
+class ImportRouter:
+    """/import for a global veneur spread over the ranks of `group` (one process per GPU).
+
+    The reference decodes a body once and hands each worker its chunk (handleImport ->
+    unmarshalMetricsFromHTTP -> ImportMetrics -> newJSONMetricsByWorker, handlers_global.go:53-63,
+    http.go:52-139).  Here the GPUs are the workers: the rank holding the HTTP listener (src)
+    decodes every body once -- zlib and JSON on its host -- routes the JSONMetrics by digest % N
+    (route_imports: the sort newJSONMetricsByWorker does, arrival order kept within a rank), and
+    sends each rank its chunk over the host control plane.  Every rank then imports only the keys
+    it owns, so no imported key spans ranks and the payload merge on the GPUs needs no collective.
+
+    route(body, content_encoding) is called by every rank for every body (src passes the body,
+    the others None); it returns (HTTP status, this rank's JSONMetrics).  decoded counts the
+    bodies this rank decoded."""
+
+    def __init__(self, group, src=0):
+        self.group, self.src, self.decoded = group, int(src), 0
+
+    def route(self, body=None, content_encoding=""):
+        from .http_import import ImportRequestError, StatusAccepted, unmarshal_metrics_from_http
+        g = self.group
+        world, rank = max(1, g.world), g.rank if g.dist is not None else 0
+        chunks, status = None, StatusAccepted
+        if rank == self.src:
+            self.decoded += 1
+            try:
+                ms = unmarshal_metrics_from_http(body, content_encoding)
+            except ImportRequestError as e:
+                import logging
+                logging.getLogger("veneur_amd.http_import").error("Could not decode /import request (%s): %s",
+                                                                  e.cause or "empty", e)
+                ms, status = [], e.status
+            chunks = [route_imports(ms, r, world) for r in range(world)]
+        if g.dist is None:
+            return status, chunks[0]
+        import torch
+        td = g.dist
+        # the status and every chunk's size first, then each rank's chunk (gloo point to point)
+        hdr = torch.zeros(world + 1, dtype=torch.int64)
+        packed = None
+        if rank == self.src:
+            packed = [pack_metrics(c) for c in chunks]
+            hdr[0] = status
+            hdr[1:] = torch.tensor([len(b) for b in packed], dtype=torch.int64)
+        td.broadcast(hdr, src=self.src)
+        status = int(hdr[0])
+        if rank == self.src:
+            for r in range(world):
+                if r != self.src:
+                    td.send(torch.frombuffer(bytearray(packed[r]), dtype=torch.uint8), dst=r)
+            return status, chunks[rank]
+        buf = torch.empty(int(hdr[1 + rank]), dtype=torch.uint8)
+        td.recv(buf, src=self.src)
+        return status, unpack_metrics(buf.numpy().tobytes())
+
+
 def hot_keys(counts, classes, thresholds, max_split=64):
     """Top keys by window count above their class threshold: {class: sorted key ids}.
     counts: records per key (e.g. the previous window's), classes: class of every key,

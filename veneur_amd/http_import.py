@@ -225,6 +225,17 @@ def handle_import(workers, body: bytes, content_encoding: str = "", shard=None) 
 HandleImport = handle_import
 
 
+def handle_import_routed(workers, router, body: Optional[bytes] = None, content_encoding: str = "") -> Tuple[int, int]:
+    """handleImport for a global veneur over N GPUs with one decode per body: the router's source
+    rank decodes the body and sends every rank its digest % N chunk (dist.ImportRouter); each rank
+    imports its chunk into its workers.  Every rank calls this for every body (the source with the
+    body, the others with None); returns (HTTP status, metrics imported on this rank)."""
+    status, mine = router.route(body, content_encoding)
+    if status == StatusAccepted and mine:
+        import_metrics(workers, mine)
+    return status, len(mine)
+
+
 # ------------------------------------------------------------------ the local side: forwarding
 def _go_json_string(s: str) -> str:
     """encoding/json's string encoder with HTML escaping (Go 1.9 encode.go: control bytes as

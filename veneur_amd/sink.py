@@ -8,6 +8,7 @@ result and the window's keys -- no InterMetric objects per key.  Worker.flush_da
 operator API; tests/dd_restated.py restates the same chain in Python as the checker.
 """
 import ctypes as C
+import threading
 import time
 
 import numpy as np
@@ -41,12 +42,16 @@ def keys_from_maps(maps):
 
 
 class DatadogSink:
-    """vn_sink: owns the bodies of its last flush."""
+    """vn_sink: owns the bodies of its last flush.  One sink may serve several flush threads (a
+    Worker with D > 1 engines flushes each engine on its own thread): the vn_sink's body buffers
+    are rewritten by every vn_datadog_flush, so a lock is held from the call until its bodies are
+    copied out."""
 
     def __init__(self, interval=10.0, hostname="", tags=(), flush_max_per_body=5000):
         self.interval, self.hostname, self.tags = float(interval), hostname, list(tags)
         self.flush_max_per_body = int(flush_max_per_body)
         self.h = C.c_void_p()
+        self._lock = threading.Lock()
         if A.lib.vn_sink_create(C.byref(self.h)) != 0:
             raise SinkError("vn_sink_create failed")
 
@@ -75,12 +80,13 @@ class DatadogSink:
         cfg.hostname, cfg.sink_tags, cfg.n_sink_tags = hn, st, len(self.tags)
         cfg.flush_max_per_body = self.flush_max_per_body
         out = A.DDPayload()
-        rc = A.lib.vn_datadog_flush(self.h, C.byref(flush_result), C.byref(keys), C.byref(cfg), C.byref(out))
-        if rc != 0:
-            raise SinkError("vn_datadog_flush: %s" % A.lib.vn_sink_last_error(self.h).decode(errors="replace"))
-        off = np.ctypeslib.as_array(out.body_off, shape=(out.n_bodies + 1,)).copy()
-        status = np.ctypeslib.as_array(out.body_status, shape=(out.n_bodies,)).copy()
-        raw = C.string_at(out.bytes, int(off[-1])) if off[-1] else b""
+        with self._lock:  # (ctypes releases the GIL inside the call)
+            rc = A.lib.vn_datadog_flush(self.h, C.byref(flush_result), C.byref(keys), C.byref(cfg), C.byref(out))
+            if rc != 0:
+                raise SinkError("vn_datadog_flush: %s" % A.lib.vn_sink_last_error(self.h).decode(errors="replace"))
+            off = np.ctypeslib.as_array(out.body_off, shape=(out.n_bodies + 1,)).copy()
+            status = np.ctypeslib.as_array(out.body_status, shape=(out.n_bodies,)).copy()
+            raw = C.string_at(out.bytes, int(off[-1])) if off[-1] else b""
         del keep
         return ([(status[i] == 0, raw[off[i]:off[i + 1]]) for i in range(out.n_bodies)],
                 (int(out.n_intermetrics), int(out.n_metrics)))

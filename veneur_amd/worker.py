@@ -396,6 +396,8 @@ class Worker:
         pct = tuple(sorted(set(float(p) for p in percentiles) | {0.5}))
         if engines is None:
             if engine is not None:
+                if int(pipeline) > 1:
+                    raise ValueError("engine= runs one engine; pass engines=[...] for pipeline > 1")
                 engines = [engine]
             else:
                 from .engine import Engine
@@ -427,6 +429,7 @@ class Worker:
         self.processed = 0
         self.imported = 0
         self.dropped = 0  # histogram records with a NaN sample rate (see process_metric)
+        self.flush_errors = 0  # engine flushes that failed on a flush thread (D > 1, see _eng)
         # whole staged batches the engine refused (ingest raised), and their records: every value
         # the engine validates is screened in process_metric first, so these stay exceptional
         self.dropped_batches = 0
@@ -448,12 +451,20 @@ class Worker:
         return len(self._engines)
 
     def _eng(self):
-        """The current engine, once its previous flush (D windows ago) has returned."""
+        """The current engine, once its previous flush (D windows ago) has returned.  If that flush
+        failed, its error is raised here (the engine's window was never flushed, so it must not
+        take the next window's records on top of it) and counted in flush_errors; the engine is
+        taken again only after a flush of it succeeds (the caller may call Flush again)."""
         p = self._pending[self._cur]
         if p is not None:
             from concurrent.futures import wait
             wait([p])
             self._pending[self._cur] = None
+            err = p.exception()
+            if err is not None:
+                self.flush_errors += 1
+                log.error("flush of engine %d failed: %s", self._cur, err)
+                raise err
         return self._engines[self._cur]
 
     def _hand_off(self, job):
@@ -496,8 +507,9 @@ class Worker:
             off[1:] = np.cumsum([len(m) for m in mem])
             kw["sets"] = (np.array(self._s[0], np.uint32), off, np.frombuffer(b"".join(mem) or b"\0", np.uint8))
         from .engine import EngineError
+        eng = self._eng()  # (a failed earlier flush of this engine is raised here, not dropped below)
         try:
-            self._eng().ingest(**kw)
+            eng.ingest(**kw)
         except EngineError as err:
             # a batch the engine rejects is dropped and counted, never resubmitted: one bad batch
             # must not block every later ProcessMetric and the window's flush
