@@ -72,7 +72,9 @@ typedef struct {
    * MergingDigest's 42-sample incremental merge bit-for-bit (every merge of the reference,
    * in arrival order).  0 (the default) or UINT32_MAX -> every sample of every key: the
    * digests are the reference's.  A smaller value is the opt-in fast mode: samples beyond
-   * it are merged in geometric pieces (rank-error parity only). */
+   * it are merged in geometric pieces (rank-error parity only).  The shipped
+   * library is built without it (vn_build_flags): any other value fails vn_engine_create with
+   * VN_EINVAL; a variant build (-DVN_FAST_MODE=1) carries it. */
   uint32_t histo_exact_threshold;
   /* a key that passes the threshold is not bit-exact anyway: only its first
    * `histo_hot_prefix` samples are replayed exactly, the rest merge in geometric pieces
@@ -194,6 +196,10 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out);
 void vn_engine_destroy(vn_engine* eng);
 const char* vn_last_error(const vn_engine* eng);
 int vn_abi_version(void);
+/* Compile-time options of this library: VN_BUILD_FAST_MODE when the t-digest fast mode
+ * (histo_exact_threshold > 0) is built in -- never in the shipped library. */
+enum { VN_BUILD_FAST_MODE = 1 };
+int vn_build_flags(void);
 /* sizeof the library's structs, so a binding built against another header revision fails at
  * load time instead of passing a short vn_config or receiving a long vn_timing.  Returns 0
  * for an unknown id. */

@@ -18,6 +18,7 @@ import oracle
 import veneur_amd as V
 from veneur_amd.dist import Group
 from tests.util import PCT, engine_ingest, rank_errors, run_oracle
+from tests.util import FAST_ONLY
 
 pytestmark = pytest.mark.gpu
 
@@ -97,7 +98,7 @@ def _c5_hosts(n_hosts, nh, ns, seed):
         yield [loc.histo_gob(s) for s in range(nh)], [loc.set_sketch(s).marshal() for s in range(ns)]
 
 
-@pytest.mark.parametrize("exact_threshold", [0, 32768])
+@pytest.mark.parametrize("exact_threshold", [0, pytest.param(32768, marks=FAST_ONLY)])
 def test_c5_global_import_1000_hosts(exact_threshold):
     """Default (exact) mode: every key re-Adds ~10^5 imported centroids, replayed merge by merge,
     so the quantiles are the reference's bit for bit; with the opt-in fast mode (threshold 32768)

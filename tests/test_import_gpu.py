@@ -16,6 +16,7 @@ import pytest
 import oracle
 import veneur_amd as V
 from tests.util import PCT, run_oracle
+from tests.util import FAST_ONLY
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
@@ -92,6 +93,7 @@ def test_import_histos_many_hosts_bit_exact():
         _check_histos(e, w, range(nk))
 
 
+@FAST_ONLY
 def test_import_histos_hot_key_rank_error():
     """One key imports far more centroids than the exact threshold: the hot-key batch merge
     applies the remainder; quantiles within 1e-3 rank error of the restated Go."""

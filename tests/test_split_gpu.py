@@ -21,6 +21,7 @@ import oracle
 import veneur_amd as V
 from veneur_amd.engine import Comm
 from tests.util import PCT
+from tests.util import FAST_ONLY
 
 pytestmark = pytest.mark.gpu
 
@@ -191,7 +192,8 @@ def _rank_err(vals, w, q_eng, q_ref):
     return max(abs(F(a) - F(b)) for a, b in zip(q_eng, q_ref))
 
 
-@pytest.mark.parametrize("N,fast", [(1, False), (2, False), (4, False), (1, True), (2, True), (4, True)])
+@pytest.mark.parametrize("N,fast", [(1, False), (2, False), (4, False)] +
+                         [pytest.param(n, True, marks=FAST_ONLY) for n in (1, 2, 4)])
 def test_split_histos_within_rank_error(N, fast):
     """default (exact) mode: every record of a split key is gathered to its owner in window order
     and replayed, so the owner's quantiles are a single consumer's bit for bit; the opt-in fast

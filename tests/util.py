@@ -1,7 +1,21 @@
 """Shared helpers for the parity tests: run the CPU oracle on a stream, compare results."""
 import numpy as np
+import pytest
 
 import oracle
+
+
+def _fast_mode_built():
+    try:
+        from veneur_amd import _abi
+        return _abi.FAST_MODE
+    except ImportError:
+        return False
+
+
+# the opt-in t-digest fast mode (exact_threshold > 0) is not in the shipped library
+# (include/veneur_amd.h vn_build_flags): its tests run only against a VN_FAST_MODE=1 variant build
+FAST_ONLY = pytest.mark.skipif(not _fast_mode_built(), reason="t-digest fast mode is a variant build (VN_FAST_MODE=1)")
 
 PCT = (0.5, 0.9, 0.99, 0.999)
 

@@ -180,6 +180,7 @@ def _sig(name, res, *args):
 vp = C.c_void_p
 _sig("vn_abi_version", C.c_int)
 _sig("vn_struct_size", C.c_size_t, C.c_int)
+_sig("vn_build_flags", C.c_int)
 ABI_VERSION = 6
 _sig("vn_engine_create", C.c_int, C.POINTER(Config), C.POINTER(vp))
 _sig("vn_engine_destroy", None, vp)
@@ -297,7 +298,7 @@ _sig("vn_synth_hosts_free", None, C.POINTER(SynthHostsOut))
 
 # every symbol include/*.h declares (checked by tests/test_abi.py on CPU)
 EXPORTED = [
-    "vn_abi_version", "vn_struct_size", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
+    "vn_abi_version", "vn_build_flags", "vn_struct_size", "vn_engine_create", "vn_engine_destroy", "vn_last_error", "vn_stage_acquire", "vn_submit",
     "vn_ingest_host", "vn_ingest", "vn_import_counters", "vn_import_gauges", "vn_import_histos", "vn_import_sets", "vn_import_histos_device", "vn_import_sets_device", "vn_histo_query", "vn_export_histos", "vn_export_sets", "vn_flush", "vn_flush_masked", "vn_sync",
     "vn_read_histo", "vn_read_set", "vn_metro64", "vn_parse_dogstatsd", "vn_parser_create", "vn_parser_destroy",
     "vn_parser_last_error", "vn_parse_dogstatsd_device", "vn_go_parse_float", "vn_diag_index_estimate", "vn_intake_create", "vn_intake_destroy",
@@ -325,3 +326,5 @@ def _check_abi():
 
 
 _check_abi()
+# the t-digest fast mode (histo_exact_threshold > 0) is a variant build only (include/veneur_amd.h)
+FAST_MODE = bool(lib.vn_build_flags() & 1)

@@ -906,6 +906,7 @@ void side_join(vn_engine* e) {
 extern "C" {
 
 int vn_abi_version(void) { return VN_ABI_VERSION; }
+int vn_build_flags(void) { return VN_FAST_MODE ? VN_BUILD_FAST_MODE : 0; }
 
 namespace {
 __global__ void k_diag_index_estimate(double c, const double* __restrict__ q, uint64_t n,
@@ -987,6 +988,10 @@ int vn_engine_create(const vn_config* cfg, vn_engine** out) {
     return VN_EINVAL;
   }
   e->exact_threshold = cfg->histo_exact_threshold ? cfg->histo_exact_threshold : 0xFFFFFFFFu;  // exact
+  if (!VN_FAST_MODE && e->exact_threshold != 0xFFFFFFFFu) {  // (the fast mode is a variant build: histo.h)
+    delete e;
+    return VN_EINVAL;
+  }
 #ifdef VN_LONG_REPLAY
   e->long_replay = VN_LONG_REPLAY;  // (A/B build knob: replays of at least this many samples take four waves)
 #endif

@@ -1,5 +1,11 @@
 // histo.h -- shared declarations of the t-digest (Histo) kernels.
 #pragma once
+// The opt-in fast mode (histo_exact_threshold > 0: past the threshold a key's window is merged
+// in geometric pieces, not replayed -- DESIGN.md §4) is not in the shipped library: it cannot meet
+// north_star's 1e-3 rank bound.  A variant build with VARIANT_FLAGS=-DVN_FAST_MODE=1 carries it.
+#ifndef VN_FAST_MODE
+#define VN_FAST_MODE 0
+#endif
 #include <stdexcept>
 
 #include "kernels.h"

@@ -25,7 +25,7 @@
 
 namespace vn {
 
-constexpr uint32_t kMaxCent = 2048;  // supports compression <= ~1000
+[[maybe_unused]] constexpr uint32_t kMaxCent = 2048;  // supports compression <= ~1000
 
 struct HistoCtx {
   uint32_t ntouched;         // grid bound on segments
@@ -84,6 +84,7 @@ __global__ void k_seg_mark(uint64_t n, const uint64_t* __restrict__ B, uint32_t*
   if (i == n - 1 || next != s) end[s] = (uint32_t)(i + 1);
 }
 
+#if VN_FAST_MODE  // (the opt-in fast mode's segment compression: VARIANT_FLAGS=-DVN_FAST_MODE=1)
 __device__ __forceinline__ uint32_t find_seg(const uint32_t* chb, uint32_t ntouched, uint32_t c) {
   uint32_t lo = 0, hi = ntouched;
   while (hi - lo > 1) {
@@ -511,6 +512,7 @@ __global__ __launch_bounds__(kBlock) void k_finalize(HistoCtx x) {
   }
 }
 
+#endif  // VN_FAST_MODE
 __global__ void k_clear_flags(uint32_t n, const uint32_t* __restrict__ list, uint32_t* __restrict__ flags) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < n) flags[list[k]] = 0;
@@ -528,6 +530,7 @@ __global__ void k_histo_keys_raw(uint64_t n, const uint32_t* __restrict__ slot, 
   B[i] = ((uint64_t)s << 32) | (uint64_t)tag;
 }
 
+#if VN_FAST_MODE
 // After the (piece, top 40 value bits) sort: each run of records with equal piece and equal top
 // 40 bits (values within 2^-28 relative of each other) of at most kTieRun records is
 // insertion-sorted by the full ordered 64-bit value, stably -- the record order a full 64-bit LSD
@@ -571,6 +574,7 @@ __global__ void k_fix_ties(uint64_t* __restrict__ A, uint64_t* __restrict__ B, u
   }
 }
 
+#endif  // VN_FAST_MODE
 // Per touched key: how many of its batch samples the exact replay takes, by the key's window
 // count after this batch, tot:
 //   cold  tot <= E            the whole batch replays exactly (bit-exact);
@@ -666,6 +670,7 @@ __global__ void k_histo_pieces(uint32_t ntouched, const uint32_t* __restrict__ e
   if (!warmflag[k]) atomicMax(maxp + 2, 1 + (i1 - i0) - fused_pieces(i0, 1 + (i1 - i0), fuse));
 }
 
+#if VN_FAST_MODE
 // copy the hot remainder into the piece-sort input: A = ordered value bits, B = piece id << 32 |
 // float32 rate bits.  Output record o belongs to the touched key k with hotoff[k] <= o < hotoff[k+1]
 // (a block of 4096 outputs spans few keys, so each thread searches between the block's first
@@ -1189,6 +1194,7 @@ void histo_compress_segments(const SegCompress& c, ScanScratch& ss, hipStream_t 
   hipLaunchKernelGGL(k_finalize, dim3(c.nseg), dim3(kBlock), 0, st, x);
 }
 
+#endif  // VN_FAST_MODE
 // timing mode: sum over the replayed keys of min(replayed samples, 160) (centroids written)
 __global__ void k_replay_state(uint32_t n, const uint32_t* __restrict__ ex, unsigned long long* __restrict__ out) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1434,6 +1440,10 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
     hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
     return;
   }
+#if !VN_FAST_MODE
+  (void)Ao, (void)Bo, (void)npieces, (void)maxp_hot, (void)maxp_warm, (void)maxp_hot_left, (void)nwarm;
+  throw std::logic_error("histo remainder without the fast mode (VN_FAST_MODE) built");
+#else
   // sort the remainders by (piece, value): every piece contiguous and value-sorted
   hipLaunchKernelGGL(k_histo_gather_hot, dim3(blocks_for(nremrec, kTile)), dim3(kBlock), 0, st, ntouched, nremrec,
                      e->h_tl, e->h_start, e->h_ex, e->h_hotoff, e->h_seen0, e->h_pbase, e->h_pi0, e->h_geo,
@@ -1527,6 +1537,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
     rounds(e->h_warmlist, nwarm, maxp_warm);
   }
   hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
+#endif  // VN_FAST_MODE
 }
 
 }  // namespace vn

@@ -689,9 +689,13 @@ void split_histos(vn_engine* e, vn_comm* c) {
   sc.cw1 = sbuf<double>(e, kSCw1, (size_t)nseg * capc);
   sc.err = a->h_err;
   if (nseg) {
+#if VN_FAST_MODE
     hipLaunchKernelGGL(k_sh_seg_ranges, dim3(blocks_for(nseg, 256)), dim3(256), 0, st, nseg, ids, ps, pe, ss, se, tl,
                        hcur, sc.hst);
     histo_compress_segments(sc, a->ss, st);
+#else
+    throw std::logic_error("split histo pieces without the fast mode (VN_FAST_MODE) built");
+#endif
   }
   // 5. per key element counts -> send layout grouped by owner
   uint32_t* cP = sbuf<uint32_t>(e, kSCP, H);
@@ -809,6 +813,9 @@ void split_histos(vn_engine* e, vn_comm* c) {
   // merge the pending temps (the single-GPU hot path does the same after the prefix)
   histo_merge_pending(a, olist, K);
   if (nmic) {
+#if !VN_FAST_MODE
+    throw std::logic_error("split histo pieces without the fast mode (VN_FAST_MODE) built");
+#else
     // pieces: (piece id, mean)-sorted micro-centroids, one mergeAllTemps per piece and round
     VN_HIP_CHECK(hipMemcpyAsync(a->h_tl, otl, K * 4, hipMemcpyDeviceToDevice, st));
     VN_HIP_CHECK(hipMemcpyAsync(a->h_pcnt, opcnt, K * 4, hipMemcpyDeviceToDevice, st));
@@ -837,6 +844,7 @@ void split_histos(vn_engine* e, vn_comm* c) {
       const uint32_t maxp = *std::max_element(hpc.begin(), hpc.end());
       histo_rounds(a, a->h_hotlist, K, maxp, nmic, K, MA_, MB_, a->hA2, a->hB2, micw, st);
     }
+#endif  // VN_FAST_MODE
   }
   S.mv_histo = SplitState::HistoMove{K, dok, tot, sums, mins, maxs};  // (moved by split_flush)
 }

@@ -60,6 +60,9 @@ class Engine:
         cfg.replay_reserved_cus = int(replay_reserved_cus)
         cfg.split_max_records = int(split_max_records)
         cfg.split_compression = float(split_compression)
+        if exact_threshold and exact_threshold != 0xFFFFFFFF and not A.FAST_MODE:
+            raise EngineError("exact_threshold=%d is the t-digest fast mode, which %s is built without "
+                              "(a VARIANT_FLAGS=-DVN_FAST_MODE=1 build carries it)" % (exact_threshold, A.LIB_PATH))
         cfg.histo_exact_threshold = int(exact_threshold)
         cfg.histo_hot_prefix = int(hot_prefix)
         cfg.histo_piece_growth = int(piece_growth)
