@@ -269,8 +269,10 @@ def c5_leg(args, rank, world, ctrl, device):
         # one more window with the engine's kernel timing (HIP events, phases run one after another):
         # the replay's own kernel time, to set against a profiler's trace of the same leg
         g.timing_enable(True)
+        g.import_counts(reset=True)
         window()
         tmg = g.timing()
+        icnt = g.import_counts()
         g.timing_enable(False)
         kernel_ms = {k: round(float(tmg[k]), 2) for k in ("ms_import_decode", "ms_import_drain", "ms_histo_replay",
                                                           "ms_radix_scatter_total", "ms_flush")}
@@ -316,12 +318,20 @@ def c5_leg(args, rank, world, ctrl, device):
             w.import_set(i, pl)
     spos = {int(s_): j for j, s_ in enumerate(ssl)}
     set_exact = all(int(ses[spos[int(k)]]) == w.set_estimate(i) for i, k in enumerate(ks))
+    # SURVEY §8(d)'s C5 bytes: the decoded contributions (16 B per centroid, 8192 B per dense sketch,
+    # 4 B per sparse code) plus the output state written once (per histo key 40 B of statistics and
+    # 16 B per centroid, at most 160 at delta 100; per set key its 8192 registers or 4 B per code,
+    # bounded here by the dense size)
+    decoded_bytes = 16 * icnt["centroids"] + 8192 * icnt["dense_sets"] + 4 * icnt["sparse_codes"] + \
+        nown[2] * (40 + 16 * 160) + nown[3] * 8192
     per_rank = ctrl.gather_object({"ms": ms_rank, "keys": [nown[2], nown[3]], "payload_bytes": payload_bytes,
+                                   "decoded_bytes": decoded_bytes, "import_counts": icnt,
                                    "phases": phases, "checked": [len(kh), len(ks)], "st_exact": st_exact,
                                    "st_diff": st_diff.tolist(), "bit_exact": bit_exact, "rank_err": rank_err,
                                    "set_exact": bool(set_exact)})
     n_imp = hosts * (H + S)
     all_bytes = sum(r["payload_bytes"] for r in per_rank)
+    dec_bytes = sum(r["decoded_bytes"] for r in per_rank)
     return {"config": "C5 global import: %d distinct hosts x (%d histo digests + %d set sketches), every key from "
                       "every host; host windows generated, ingested and exported on the GPU (%d local samples per "
                       "rank); payloads in HBM, each rank keeping its keys' (digest %% %d), ONE "
@@ -334,9 +344,15 @@ def c5_leg(args, rank, world, ctrl, device):
             "ranks": {"ms_per_window": [round(r["ms"], 2) for r in per_rank],
                       "histo_set_keys": [r["keys"] for r in per_rank]},
             "payload_bytes_per_window": all_bytes,
-            "roofline": {"bound": "hbm", "achieved_GBs": all_bytes / (ms * 1e-3) / 1e9 / world, "peak": HBM_PEAK_GBS,
-                         "frac": all_bytes / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS,
-                         "unit": "payload bytes decoded per second per GPU over the window"},
+            "roofline": {"bound": "hbm", "achieved_GBs": dec_bytes / (ms * 1e-3) / 1e9 / world, "peak": HBM_PEAK_GBS,
+                         "frac": dec_bytes / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS, "unit": "GB/s",
+                         "bytes": "SURVEY §8(d): decoded contributions (16 B per centroid, 8192 B per dense sketch, "
+                                  "4 B per sparse code) + output state, per window",
+                         "algorithmic_bytes_per_window": dec_bytes,
+                         "import_counts_rank0": per_rank[0]["import_counts"]},
+            "roofline_payload": {"bound": "hbm", "achieved_GBs": all_bytes / (ms * 1e-3) / 1e9 / world,
+                                 "peak": HBM_PEAK_GBS, "frac": all_bytes / (ms * 1e-3) / 1e9 / world / HBM_PEAK_GBS,
+                                 "unit": "encoded payload bytes per second per GPU over the window"},
             "generated_in_s": round(gen_s, 2), "parity_checked_in_s": round(time.time() - t1, 2),
             "parity": {"keys_checked": {"histo": int(sum(r["checked"][0] for r in per_rank)),
                                         "set": int(sum(r["checked"][1] for r in per_rank))},

@@ -357,6 +357,11 @@ typedef struct {
   float ms_import_drain;
 } vn_timing;
 int vn_timing_enable(vn_engine* eng, int enable);
+/* The import contributions decoded while timing is on (SURVEY.md §8(d)'s C5 bytes: 16 B per
+ * centroid, 8192 B per dense sketch, 4 B per sparse code): out5 = {histo payloads, their
+ * centroids, set payloads, dense set payloads, sparse set codes}, summed since the last reset;
+ * reset != 0 zeroes them after the read. */
+int vn_import_counts(vn_engine* eng, uint64_t* out5, int reset);
 int vn_get_timing(vn_engine* eng, vn_timing* out);
 
 /* ---------------------------------------------------------------- multi-GPU

@@ -288,6 +288,7 @@ _sig("vn_device_count", C.c_int, C.POINTER(C.c_int))
 _sig("vn_device_synchronize", C.c_int, C.c_int)
 _sig("vn_timing_enable", C.c_int, vp, C.c_int)
 _sig("vn_get_timing", C.c_int, vp, C.POINTER(Timing))
+_sig("vn_import_counts", C.c_int, vp, C.POINTER(C.c_uint64), C.c_int)
 _sig("vn_synth_generate", C.c_int, C.POINTER(SynthConfig), C.POINTER(SynthOut))
 _sig("vn_synth_free", None, C.POINTER(SynthOut))
 _sig("vn_synth_device", C.c_int, C.POINTER(SynthDevConfig), C.POINTER(SynthDevOut))
@@ -309,7 +310,7 @@ EXPORTED = [
     "vn_synth_hosts_free",
     "vn_copy_to_host", "vn_comm_unique_id", "vn_comm_init", "vn_comm_init_local", "vn_comm_destroy", "vn_comm_last_error", "vn_comm_rank",
     "vn_comm_nranks", "vn_comm_allreduce", "vn_engine_set_comm", "vn_split_keys", "vn_ingest_split", "vn_split_close", "vn_split_combine",
-    "vn_hot_detect", "vn_hot_keys",
+    "vn_hot_detect", "vn_hot_keys", "vn_import_counts",
 ]
 
 

@@ -505,7 +505,7 @@ void destroy_impl(vn_engine* e) {
   for (int c = 0; c < VN_NCLASS; c++) { dfree(e->f_list[c]); hfree(e->hf_list[c]); }
   dfree(e->f_cnt); dfree(e->f_cval); hfree(e->hf_cval); dfree(e->f_gval); hfree(e->hf_gval);
   dfree(e->f_hstats); hfree(e->hf_hstats); dfree(e->f_hq); hfree(e->hf_hq); dfree(e->f_sest); hfree(e->hf_sest);
-  dfree(e->f_ssparse); hfree(e->hf_ssparse); dfree(e->d_pct); hfree(e->hf_cnt);
+  dfree(e->d_imp_counts); dfree(e->f_ssparse); hfree(e->hf_ssparse); dfree(e->d_pct); hfree(e->hf_cnt);
   dfree(e->f_hmask); dfree(e->f_smask);
   radix_scratch_free(e->rs);
   radix_scratch_free(e->rs2);
@@ -1299,6 +1299,24 @@ int vn_flush_masked(vn_engine* e, const uint8_t* histo_quantile_mask, const uint
     }
     e->sp.ran = false;
     out->warn_flags = caller;  // (the window is flushed; the misuse is reported, not thrown)
+  });
+}
+
+int vn_import_counts(vn_engine* e, uint64_t* out5, int reset) {
+  if (!e || !out5) return VN_EINVAL;
+  return guarded(e, [&] {
+    unsigned long long d[2] = {0, 0};
+    if (e->d_imp_counts) {
+      VN_HIP_CHECK(hipMemcpyAsync(d, e->d_imp_counts, sizeof d, hipMemcpyDeviceToHost, e->st));
+      VN_HIP_CHECK(hipStreamSynchronize(e->st));
+    }
+    e->imp_counts[3] = d[0];
+    e->imp_counts[4] = d[1];
+    for (int i = 0; i < 5; i++) out5[i] = e->imp_counts[i];
+    if (reset) {
+      for (uint64_t& c : e->imp_counts) c = 0;
+      if (e->d_imp_counts) VN_HIP_CHECK(hipMemsetAsync(e->d_imp_counts, 0, sizeof d, e->st));
+    }
   });
 }
 

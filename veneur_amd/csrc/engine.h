@@ -334,6 +334,10 @@ struct vn_engine {
 
   // ---- timing
   bool timing = false;
+  // decoded import contributions (SURVEY.md §8(d)'s C5 bytes), counted while timing is on:
+  // histo payloads, their centroids, set payloads, dense ones, sparse codes (vn_import_counts)
+  uint64_t imp_counts[5] = {0, 0, 0, 0, 0};
+  unsigned long long* d_imp_counts = nullptr;  // device [2]: dense set payloads, sparse set codes
   hipEvent_t ev[16] = {};
   vn::EventPool pool;
   vn::SplitState sp;

@@ -3143,8 +3143,17 @@ __device__ __forceinline__ void replay_long(const ExactCtx& x, const uint32_t* _
 __global__ __launch_bounds__(kMWThreads) void k_histo_exact_mw(ExactCtx x, const uint32_t* __restrict__ nmw) {
   replay_long<false>(x, nmw);
 }
+#ifndef VN_CHAIN_EXCLUSIVE
+#define VN_CHAIN_EXCLUSIVE 1
+#endif
 __global__ __launch_bounds__(kMWThreads) void k_histo_exact_mwb(ExactCtx x, const uint32_t* __restrict__ nmw,
                                                                  uint32_t first, uint32_t last) {
+#if VN_CHAIN_EXCLUSIVE
+  // The batched replay is issue-bound at one wave per SIMD: a wave of another
+  // kernel sharing its SIMD takes issue slots from the chain.  Claiming the whole register file
+  // (the last accumulation register) leaves no room for one: the CU runs this workgroup alone.
+  asm volatile("" ::: "a255");
+#endif
   replay_long<true>(x, nmw, first, last);
 }
 // The Local* statistics of the batched keys' pure chunks (Histo.Sample, samplers.go:346-356:

@@ -636,6 +636,10 @@ void import_histos(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_
   VN_HIP_CHECK(hipStreamSynchronize(st));
   take_decode_error(e);
   const uint64_t nc = e->hf_cnt[9];
+  if (e->timing) {
+    e->imp_counts[0] += n;
+    e->imp_counts[1] += nc;
+  }
   // (once the call can no longer be refused: after the validation, and in the sliced path after
   // the oversize check)
   auto touch_all = [&] {

@@ -845,6 +845,24 @@ extern "C" int vn_prof_import_set_read(unsigned long long* out24, int reset) {
 }
 #endif
 
+// timing mode: dense payloads and sparse codes of a parsed batch (vn_import_counts)
+__global__ void k_hll_counts(uint64_t n, const HllPart* __restrict__ parts, unsigned long long* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long d = 0, c = 0;
+  if (i < n) {
+    d = parts[i].kind == 1u ? 1ull : 0ull;
+    c = parts[i].kind == 0u ? parts[i].ncodes : 0ull;
+  }
+  for (int s = 32; s >= 1; s >>= 1) {
+    d += __shfl_xor(d, s, 64);
+    c += __shfl_xor(c, s, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && (d || c)) {
+    atomicAdd(out, d);
+    atomicAdd(out + 1, c);
+  }
+}
+
 void import_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t* off, const uint8_t* bytes) {
   if (!n) return;
   hipStream_t st = e->st;
@@ -852,6 +870,14 @@ void import_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t*
   hipLaunchKernelGGL(k_hll_parse, dim3(blocks_for(n, 4)), dim3(256), 0, st, n, off, bytes, parts, e->h_err);  // a wave each
   VN_HIP_CHECK(hipStreamSynchronize(st));
   take_decode_error(e);  // a truncated payload: nothing is applied
+  if (e->timing) {
+    if (!e->d_imp_counts) {
+      VN_HIP_CHECK(hipMalloc(&e->d_imp_counts, 2 * sizeof(unsigned long long)));
+      VN_HIP_CHECK(hipMemsetAsync(e->d_imp_counts, 0, 2 * sizeof(unsigned long long), st));
+    }
+    e->imp_counts[2] += n;
+    hipLaunchKernelGGL(k_hll_counts, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, parts, e->d_imp_counts);
+  }
   // group the payloads by key, arrival order kept
   hipLaunchKernelGGL(k_hll_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, slot, e->sR0, e->s_bt, e->stouch);
   RadixPass passes[4];
