@@ -398,6 +398,14 @@ class Engine:
         self._check(A.lib.vn_get_timing(self.h, C.byref(t)))
         return {k: getattr(t, k) for k, _ in A.Timing._fields_}
 
+    def import_counts(self, reset=False):
+        """Import contributions decoded while timing was on (vn_import_counts): histo payloads,
+        their centroids, set payloads, dense set payloads, sparse set codes."""
+        out = (C.c_uint64 * 5)()
+        self._check(A.lib.vn_import_counts(self.h, out, int(bool(reset))))
+        return dict(zip(("histo_payloads", "centroids", "set_payloads", "dense_sets", "sparse_codes"),
+                        (int(v) for v in out)))
+
 
 def flush_output(o, npct) -> FlushOutput:
     """A vn_flush_result (engine-owned pinned arrays, valid until that engine's next flush) copied
@@ -427,14 +435,6 @@ def flush_output(o, npct) -> FlushOutput:
 class Comm:
     """A group of engines exchanging split keys: RCCL (one process per GPU) or in-process."""
 
-
-    def import_counts(self, reset=False):
-        """Import contributions decoded while timing was on (vn_import_counts): histo payloads,
-        their centroids, set payloads, dense set payloads, sparse set codes."""
-        out = (C.c_uint64 * 5)()
-        self._check(A.lib.vn_import_counts(self.h, out, int(bool(reset))))
-        return dict(zip(("histo_payloads", "centroids", "set_payloads", "dense_sets", "sparse_codes"),
-                        (int(v) for v in out)))
     def __init__(self, h):
         self.h = h
 
