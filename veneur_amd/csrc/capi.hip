@@ -261,7 +261,6 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_coff, (size_t)touch_max + 1);
   dalloc(e->h_cown, ch ? e->h_sort_cap / std::max<uint32_t>(e->temp_cap, 1) + 2 : 0);
   dalloc(e->h_cstat, ch ? (e->h_sort_cap / std::max<uint32_t>(e->temp_cap, 1) + 2) * 8 : 0);
-  dalloc(e->h_cpo, ch ? (e->h_sort_cap / std::max<uint32_t>(e->temp_cap, 1) + 2) : 0);
   dalloc(e->h_tw, e->h_sort_cap);
   dalloc(e->h_seen0, touch_max);
   dalloc(e->h_pcnt, touch_max);
@@ -478,7 +477,7 @@ void destroy_impl(vn_engine* e) {
   dfree(e->ch_sum); dfree(e->ch_pre); dfree(e->ch_stats); dfree(e->seg_T);
   dfree(e->starts); dfree(e->nc_new); dfree(e->acc_xw); dfree(e->acc_w); dfree(e->h_err);
   dfree(e->hseen); dfree(e->hpend); dfree(e->hspn); dfree(e->hspw); dfree(e->hm_flag); dfree(e->hm_pos); dfree(e->hm_idx); dfree(e->hm_list); dfree(e->hm_cnt); dfree(e->hpv); dfree(e->hpw); dfree(e->h_ex); dfree(e->h_hotflag);
-  dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw); dfree(e->h_cpk); dfree(e->h_lstat); dfree(e->h_cstat); dfree(e->h_cpo);
+  dfree(e->h_coldflag); dfree(e->h_coldlist); dfree(e->h_vhflag); dfree(e->h_warmflag); dfree(e->h_warmlist); dfree(e->hA2); dfree(e->hB2); dfree(e->h_csv); dfree(e->h_csw); dfree(e->h_cpk); dfree(e->h_lstat); dfree(e->h_cstat);
   dfree(e->h_lpt0); dfree(e->h_lpt1); dfree(e->s_lpt0); dfree(e->s_lpt1);
   dfree(e->h_hotcnt); dfree(e->h_hotoff); dfree(e->h_hotlist); dfree(e->h_tl2); dfree(e->h_ccnt); dfree(e->h_coff); dfree(e->h_cown); dfree(e->h_tw);
   dfree(e->fz_val); dfree(e->fz_w); dfree(e->fz_k); dfree(e->fz_done);

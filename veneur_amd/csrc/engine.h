@@ -249,7 +249,6 @@ struct vn_engine {
   double* h_csv = nullptr;       // pre-sorted pure chunks: means, weights (per record)
   double* h_csw = nullptr;
   uint32_t* h_cpk = nullptr;     // ... the batched replay's packed weights (ExactCtx::cpk)
-  uint8_t* h_cpo = nullptr;      // ... every pure chunk's packed-only flag (ExactCtx::cpo)
   double* h_lstat = nullptr;     // ... the batched keys' Local* partials (ExactCtx::lstat)
   double* h_cstat = nullptr;     // ... every pure chunk's Local* partials (ExactCtx::cstat)
   uint32_t* h_tl2 = nullptr;     // slots of hot keys

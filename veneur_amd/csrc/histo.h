@@ -83,11 +83,6 @@ struct ExactCtx {
   // tempW as the prefix, or 0xffffffff when the chunk cannot be batched (a weight that is not an
   // integer, or a tempW of 65536 or more)
   uint32_t* cpk;
-  // per pure chunk (global chunk index): 1 when the chunk is "packed only" -- a long key's chunk of
-  // samples (no imported centroid) whose cpk is valid: the sorter then writes neither csw nor
-  // ctw past the chunk's first record, and readers take |w| and the prefixes from cpk (weights
-  // positive).  null: every chunk writes csw / ctw
-  uint8_t* cpo;
   uint64_t* cown;  // [chunks] key index << 32 | first record of every pure chunk (null: searched in coff)
   // the batched keys' pure-chunk Local* statistics, reduced in parallel before their replays
   // (k_exact_long_stats): [kLongStatKeys][kLongStatSlices][8] partials (null: the replay's own)

@@ -1097,22 +1097,13 @@ __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t
   // the first record, the Add-order tempW at it (negated when a weight is not an integer)
   // and for the batched replay (cpk) the same prefix as a u16 beside |w| as a u16, slot 0 carrying
   // tempW -- or 0xffffffff when some weight is not an integer or tempW >= 2^16
-  bool tint = true, tex = true, samples = true;
-  for (uint32_t t = lane; t < tcap; t += 64) {
-    const double w = sw[t];
-    tint &= is_int_weight(__builtin_fabs(w));
-    tex &= is_exact_weight(__builtin_fabs(w));
-    samples &= w > 0.0;
-  }
-  tint = __all(tint);
-  tex = __all(tex) && tempW <= exact_total_limit(tint);
-  // a long key's chunk of samples with integer weights below 2^16 in all: cpk holds every |w| and
-  // prefix, so csw and ctw past the first record are not written (ExactCtx::cpo; 16 B per record)
-  const bool po = x.cpo && x.cpk && wide && tint && tempW < 65536.0 && __all(samples);
+  bool tint = true, tex = true;
   double carry = 0.0;
   for (uint32_t b = 0; b < tcap; b += 64) {
     const uint32_t t = b + lane;
     const double w = t < tcap ? __builtin_fabs(sw[t]) : 0.0;
+    tint &= is_int_weight(w);
+    tex &= is_exact_weight(w);
     double v = w;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -1122,15 +1113,14 @@ __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t
     if (t < tcap) {
       const double ex = dadd(carry, dsub(v, w));
       x.csv[base + t] = sv[t];
-      if (!po) {
-        x.csw[base + t] = sw[t];
-        if (t && wide) x.ctw[base + t] = ex;
-      }
+      x.csw[base + t] = sw[t];
+      if (t && wide) x.ctw[base + t] = ex;
       if (x.cpk && t && wide) x.cpk[base + t] = (ex < 65536.0 ? (uint32_t)ex << 16 : 0xffff0000u) | (w < 65536.0 ? (uint32_t)w : 0xffffu);
     }
     carry = dadd(carry, rl_d(v, 63));
   }
-  if (lane == 0 && x.cpo) x.cpo[g] = po ? 1u : 0u;
+  tint = __all(tint);
+  tex = __all(tex) && tempW <= exact_total_limit(tint);
   if (lane == 0) {
     // (the four-wave merge needs exact prefixes only; the batched one integers below 2^16)
     x.ctw[base] = tex ? tempW : -tempW;
@@ -1280,14 +1270,12 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
     double cv[TPL], cw[TPL], ctw = 0.0;
     auto load = [&](uint32_t c) {
       const uint64_t base = (uint64_t)lo + sp.off0 + (uint64_t)c * tcap;
-      // (a packed-only chunk, ExactCtx::cpo: |w| from cpk, every weight a sample's)
-      const bool po = x.cpo && x.cpo[x.coff[k] + c];
 #pragma unroll
       for (uint32_t q = 0; q < (uint32_t)TPL; q++) {
         const uint32_t t = q * 64 + lane;
         if (t < tcap) {
           cv[q] = xcsv[base + t];
-          cw[q] = po ? (double)(x.cpk[base + t] & 0xffffu) : xcsw[base + t];
+          cw[q] = xcsw[base + t];
         }
       }
       ctw = __builtin_fabs(xctw[base]);  // (negative: not all weights integers)
@@ -2870,17 +2858,10 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     uint32_t ccpk = 0xffffffffu;  // the batched replay's packing of slot 0: not all-ones = integer weights
     auto load = [&](uint32_t c) {
       const uint64_t base = (uint64_t)lo + sp.off0 + (uint64_t)c * tcap;
-      const bool po = x.cpo && x.cpo[x.coff[k] + c];  // (packed-only: weights and prefixes from cpk)
       if (t < tcap) {
         cv = xcsv[base + t];
-        if (po) {
-          const uint32_t pk = x.cpk[base + t];
-          cw = (double)(pk & 0xffffu);
-          cp = (double)(pk >> 16);
-        } else {
-          cw = xcsw[base + t];
-          cp = xctw[base + t];
-        }
+        cw = xcsw[base + t];
+        cp = xctw[base + t];
       }
       ctw = xctw[base];
       ccpk = x.cpk ? x.cpk[base] : 0xffffffffu;
@@ -2938,7 +2919,7 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
       }
     } else if (x.cstat) {
       // past the pre-reduced keys: the chunk sorter's per-chunk partials of this key, 64 B per
-      // chunk (its packed-only chunks hold no csw to re-read)
+      // chunk instead of 16 B per sample
       for (uint64_t g = t; g < sp.npure; g += NT) {
         const double* q = x.cstat + ((uint64_t)x.coff[k] + g) * 8;
         sw = dadd(sw, q[0]);

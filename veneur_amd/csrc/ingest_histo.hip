@@ -1332,9 +1332,6 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.lstat = e->h_lstat;
 #ifndef VN_NO_CSTAT
   xc.cstat = e->h_cstat;  // (A/B build VN_NO_CSTAT: k_exact_long_stats re-reads the samples)
-#ifndef VN_NO_PACKED_ONLY
-  if (xc.cstat) xc.cpo = e->h_cpo;  // (long keys' integer-weight chunks: cpk alone, no csw / ctw; VN_NO_PACKED_ONLY: both)
-#endif
 #endif
   const uint64_t max_chunks = n / e->temp_cap + 1;
   // the four-wave replay's threshold (replay_cold below): shorter keys take the one-wave replay
