@@ -566,6 +566,8 @@ def main():
     args = ap.parse_args()
 
     import veneur_amd as V
+    import ctypes as C
+
     import veneur_amd._abi as A
     from veneur_amd.dist import Group, InTurn, env_world, make_comm
 
@@ -699,12 +701,33 @@ def main():
     warm = max(args.warmup, D)
     run_windows(warm)
     sync()
+    # the profiling build (VN_LIB=libveneur_amd_prof.so): the batched replay's phase cycles of each
+    # window's longest key (block 0), summed over the timed windows (tools/exact_profile.py's fields)
+    prof_read = getattr(A.lib, "vn_prof_exact_read", None)
+    prof_buf = None
+    if prof_read is not None:
+        prof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+        prof_buf = (C.c_ulonglong * 64)()
+        prof_read(prof_buf, 1)
     ctrl.barrier()
     lat.clear()
     t0 = time.perf_counter()
     last = run_windows(args.steps)
     sync()
     t_rank = time.perf_counter() - t0
+    exact_prof = None
+    if prof_buf is not None:
+        prof_read(prof_buf, 0)
+        pv = list(prof_buf)
+        nb = max(1, pv[23])
+        exact_prof = {"batches": pv[23], "avg_committed": round(pv[24] / nb, 2), "avg_usable": round(pv[26] / nb, 2),
+                      "avg_flagged": round(pv[25] / nb, 2), "structural": pv[22],
+                      "avg_repairs": round(pv[32] / nb, 2), "cyc_repair": round(pv[33] / nb, 1),
+                      "cyc_batch_call": round(pv[27] / nb, 1)}
+        for i, nme in zip((16, 17, 18, 19, 15, 20, 21, 48, 13), ("totals", "A", "B", "C", "D", "E_C2", "F", "G", "H")):
+            exact_prof["cyc_" + nme] = round(pv[i] / nb, 1)
+        exact_prof["cyc_E_per_wave"] = [round(pv[36 + w] / nb, 1) for w in range(4)]
+        exact_prof["cyc_C2_per_wave"] = [round(pv[44 + w] / nb, 1) for w in range(4)]
     ctrl.barrier()
     elapsed = time.perf_counter() - t0
     elapsed = ctrl.max(elapsed)
@@ -1047,6 +1070,8 @@ def main():
             result["c5"] = c5
             log(rank, "[bench] C5 leg in %.1fs: %s" % (time.time() - t1, json.dumps(c5)))
     if rank == 0:
+        if exact_prof is not None:
+            result["exact_prof_block0"] = exact_prof
         print(json.dumps(result), flush=True)
     for e in engines:
         e.close()

@@ -87,6 +87,7 @@ _sig("or_td_max", C.c_double, C.c_void_p)
 _sig("or_td_count", C.c_double, C.c_void_p)
 _sig("or_td_merge", None, C.c_void_p, C.c_void_p, i64p)
 _sig("or_td_centroids", C.c_size_t, C.c_void_p, f64p, f64p, C.c_size_t)
+_sig("or_td_main", C.c_size_t, C.c_void_p, f64p, f64p, C.c_size_t)
 _sig("or_td_temp_len", C.c_size_t, C.c_void_p)
 _sig("or_td_gob_encode", C.c_size_t, C.c_void_p, u8p, C.c_size_t)
 _sig("or_td_gob_decode", C.c_int, C.c_void_p, C.c_char_p, C.c_size_t)
@@ -330,6 +331,14 @@ class MergingDigest:
         m = np.zeros(max(n, 1))
         w = np.zeros(max(n, 1))
         lib.or_td_centroids(self.td, ptr(m, f64p), ptr(w, f64p), n)
+        return m[:n], w[:n]
+
+    def main_centroids(self):
+        """The main centroids without merging the pending temps (a replay's state between calls)."""
+        n = lib.or_td_main(self.td, None, None, 0)
+        m = np.zeros(max(n, 1))
+        w = np.zeros(max(n, 1))
+        lib.or_td_main(self.td, ptr(m, f64p), ptr(w, f64p), n)
         return m[:n], w[:n]
 
     def gob_encode(self) -> bytes:

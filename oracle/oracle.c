@@ -1016,6 +1016,12 @@ void or_td_merge(or_td* td, or_td* other, const int64_t* perm) { /* merging_dige
   }
   for (size_t i = 0; i < other->ntemp; i++) or_td_add(td, other->temp[i].mean, other->temp[i].weight);
 }
+/* the main centroids as they are, pending temps not merged (diagnostics: a replay's state between
+ * two ingest calls) */
+size_t or_td_main(const or_td* td, double* means, double* weights, size_t cap) {
+  for (size_t i = 0; i < td->nmain && i < cap; i++) { means[i] = td->main[i].mean; weights[i] = td->main[i].weight; }
+  return td->nmain;
+}
 size_t or_td_centroids(or_td* td, double* means, double* weights, size_t cap) {
   td_merge_all_temps(td);
   for (size_t i = 0; i < td->nmain && i < cap; i++) { means[i] = td->main[i].mean; weights[i] = td->main[i].weight; }

@@ -90,7 +90,8 @@ double or_td_count(const or_td* td);
 /* Merge: perm = order in which other's main centroids are re-Added (rand.Perm in Go);
  * NULL -> identity order. */
 void or_td_merge(or_td* td, or_td* other, const int64_t* perm);
-size_t or_td_centroids(or_td* td, double* means, double* weights, size_t cap); /* merges temps */
+size_t or_td_centroids(or_td* td, double* means, double* weights, size_t cap);
+size_t or_td_main(const or_td* td, double* means, double* weights, size_t cap); /* pending temps not merged */
 size_t or_td_temp_len(const or_td* td);
 /* study helper (not in the reference): one mergeAllTemps of n samples, as the engine's
  * hot-key batch merge does */

@@ -129,3 +129,27 @@ def test_four_wave_replay_new_last_centroid_bit_exact():
     when no later start exists (a bug found by the whole-digest comparison in round 4)."""
     _check(["rising", "rising", "falling", "lognormal"], 25_362, 1, 1)
     _check(["rising"] * 3, 37_000, 2, 2)
+
+
+@pytest.mark.parametrize("calls", [2, 3])
+def test_replay_state_after_every_call_bit_exact(calls):
+    """Round 6: a long key continuing in a later ingest call starts by merging its pending temps
+    with the call's first samples.  After every call each key's main centroids (vn_read_histo,
+    pending temps not merged) equal the restated Go digest fed the same prefix of its samples --
+    the out-of-line four-wave merge that this first merge used to take halved the centroids of
+    continuing keys (tools/probe/repro_batch3_calls.py)."""
+    kinds = ["lognormal", "falling", "rising", "ints", "seven", "heavy"]
+    slot, val, rate, nk = _stream(kinds, 300_000, 11 + calls)
+    wts = (np.float32(1.0) / rate).astype(np.float64)
+    cuts = np.linspace(0, len(slot), calls + 1).astype(int)
+    with V.Engine((1, 1, nk, 1), percentiles=PCT, max_batch_records=len(slot) + 1) as e:
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            e.ingest(histos=(slot[a:b], val[a:b], rate[a:b]))
+            for k, kind in enumerate(kinds):
+                sel = slot[:b] == k
+                td = oracle.MergingDigest(100.0)
+                td.add_many(val[:b][sel], wts[:b][sel])
+                om, ow = td.main_centroids()
+                gm, gw, st = e.read_histo(k)
+                assert np.array_equal(gm, om) and np.array_equal(gw, ow), (kind, b, len(gm), len(om))
+                assert st[7] == float(np.sum(ow))

@@ -73,6 +73,10 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     out["study_columns"] = p[52]
     out["study_cheap_certified"] = p[53]
     out["study_exact_certified"] = p[54]
+    out["batch_repair_rounds"] = p[32]
+    out["batch_avg_repairs"] = round(p[32] / nb, 2)
+    out["batch_cyc_repair"] = round(p[33] / nb, 1)
+    out["batch_redone_columns"] = p[35]
     out["singles_after_reject"] = p[29]
     out["singles_after_reject_cyc"] = p[28]
     out["singles_unbatchable"] = p[31]

@@ -13,10 +13,13 @@
  *      (exact check against the mean merge j saw only for temps inside a bound), and sortedness
  *      hi_i <= lo_{i+1}, which makes the per-temp checks cover every main's decisions
  *   G  exact k tests of flagged columns, merge by merge
- *   H  commit the merges before the first failure.  A decision failure (a flip) restarts the
- *      next batch at that merge; a structural failure runs it alone.
+ *   F' (round 6) flip repair, at most REPAIR_CAP rounds per batch: the first chunk jp with a decision
+ *      failure gets every boundary's exact count from the means merge jp saw, and the batch is
+ *      re-run with those counts (the GPU re-does only the columns beside the changed boundaries)
+ *   H  commit the merges before the first failure.  A decision failure (a flip) left after the
+ *      repairs restarts the next batch at that merge; a structural failure runs it alone.
  *
- *   gcc -O2 -o /tmp/b2s tools/study/batch2_sim.c -lm && /tmp/b2s 4000000 64 0               */
+ *   gcc -O2 -o /tmp/b2s tools/study/batch2_sim.c -lm && /tmp/b2s 4000000 64 0 [repair_cap]   */
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -71,7 +74,7 @@ static void merge_ref(C* main_, int* nm, double* T0, const C* t, int np, double 
 }
 
 /* statistics */
-static long st_flip, st_struct, st_flagged_cols, st_atrisk, st_unsorted, st_zmerges;
+static long st_repairs, st_repair_rounds; static int REPAIR_CAP = 0; static long st_flip, st_struct, st_flagged_cols, st_atrisk, st_unsorted, st_zmerges;
 
 /* returns committed merges; *structural = the failure at the returned index is structural */
 static int merge_batch2(C* main_, int nm, double* T0, C t[][TC], const double* tempW, int B, int* structural) {
@@ -104,6 +107,10 @@ static int merge_batch2(C* main_, int nm, double* T0, C t[][TC], const double* t
       while (l < h) { int md = (l + h) / 2; if (main_[md].m < t[j][p].m) l = md + 1; else h = md; }
       pos[j][p] = (uint8_t)l;
     }
+  static int nfix[MAXB][MAXM + 1]; /* -1: no override of n[i][j] (stored [j][i]) */
+  for (int j = 0; j < B; j++) for (int i = 0; i <= nm; i++) nfix[j][i] = -1;
+  int repairs = 0;
+again:;
   /* B: run fill */
   for (int j = 0; j < B; j++)
     for (int p = 0; p < TC; p++) {
@@ -111,6 +118,7 @@ static int merge_batch2(C* main_, int nm, double* T0, C t[][TC], const double* t
       if (p == 0) for (int i = 0; i < c0; i++) n[i][j] = 0;
       for (int i = c0; i < c1; i++) n[i][j] = (uint8_t)(p + 1);
     }
+  for (int j = 0; j < B; j++) for (int i = 0; i <= nm; i++) if (nfix[j][i] >= 0) n[i][j] = (uint8_t)nfix[j][i];
   /* list offsets: off[i] = sum_j n[i][j] (column -1 = Z first: column 0's list holds them) */
   for (int i = 0; i <= nm; i++) {
     uint32_t s = 0;
@@ -205,7 +213,9 @@ static int merge_batch2(C* main_, int nm, double* T0, C t[][TC], const double* t
   for (int j = 0; j < B; j++)
     for (int p = 0; p < TC; p++) {
       double v = t[j][p].m;
-      int c = pos[j][p] - 1, bad = 0;
+      int pj = pos[j][p];
+      if (nfix[j][0] >= 0) { pj = 0; while (pj < nm && n[pj][j] <= p) pj++; }
+      int c = pj - 1, bad = 0;
       if (c >= 0 && v <= hi[c]) {
         double mb;
         st_atrisk++;
@@ -220,6 +230,22 @@ static int merge_batch2(C* main_, int nm, double* T0, C t[][TC], const double* t
       }
       if (bad && j < jp) jp = j;
     }
+  if (jp < B && repairs < REPAIR_CAP) {
+    /* repair: the exact boundaries of chunk jp from the means merge jp saw, then everything again */
+    repairs++;
+    st_repairs++;
+    for (int i = 1; i <= nm; i++) {
+      double mb;
+      if (i < nm) { MEAN_BEFORE(i, jp, mb); } else mb = INFINITY;
+      int c = 0;
+      while (c < TC && t[jp][c].m <= mb) c++;
+      /* (monotone in i only if the means merge jp saw are sorted: they are, given hi <= lo) */
+      nfix[jp][i] = c;
+    }
+    /* n[0][j]: Z temps: v <= mean_0 */
+    { double mb; MEAN_BEFORE(0, jp, mb); int c = 0; while (c < TC && t[jp][c].m <= mb) c++; nfix[jp][0] = c; }
+    goto again;
+  }
   /* G: flagged columns' exact tests for merges < jp; also the bound tests */
   int jsf = B;
   for (int i = 0; i < nm; i++) {
@@ -261,6 +287,7 @@ static int merge_batch2(C* main_, int nm, double* T0, C t[][TC], const double* t
 int main(int argc, char** argv) {
   long N = argc > 1 ? atol(argv[1]) : 1000000;
   int B = argc > 2 ? atoi(argv[2]) : 64;
+  REPAIR_CAP = argc > 4 ? atoi(argv[4]) : 0;
   int dist = argc > 3 ? atoi(argv[3]) : 0; /* 0 lognormal+rates, 1 few distinct values, 2 uniform ints, 3 rising, 4 falling */
   long merges = N / TC;
   C (*chunks)[TC] = malloc(sizeof(C[TC]) * merges);
@@ -304,5 +331,6 @@ int main(int argc, char** argv) {
          "singles=%ld flips=%ld structural=%ld zbatches=%ld flagged_cols=%ld atrisk=%ld unsorted=%ld\n",
          N, B, dist, merges, nr, same, batches, committed, (double)committed / (batches ? batches : 1), singles, st_flip,
          st_struct, st_zmerges, st_flagged_cols, st_atrisk, st_unsorted);
+  printf("repairs %ld (%.2f per batch)\n", st_repairs, (double)st_repairs / batches);
   return !same;
 }

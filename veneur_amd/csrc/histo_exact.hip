@@ -1894,14 +1894,6 @@ __device__ __forceinline__ MergeState merge_step(const MergeParams mp, const Lds
   fast_sync<NW>();  // S and misc are read before anyone writes them again
   return st;
 }
-template <int NW>
-__device__ __noinline__ MergeState merge_step_cold(const Lds L, ldsf64* fbase, MwSharedL& S, MP_PARAMS, uint32_t st_nm,
-                                                   double st_w, bool st_fok, bool st_fint, uint32_t n_, double tempW,
-                                                   bool tint, bool cint, double k0) {
-  MP_UNPACK(mp);
-  return merge_step<NW>(mp, L, fast_of(L, fbase), S, MergeState{st_nm, st_w, st_fok, st_fint}, n_, tempW, tint, cint,
-                        k0);
-}
 
 // ---- batched replay of consecutive pure chunks (the long replays' steady state).
 //
@@ -1960,6 +1952,14 @@ constexpr uint32_t kBMinAvail = 32;         // chunks in the ring below which a 
 #endif
 constexpr double kBatchMinW = VN_BATCH_MIN_W;  // batches start once the digest holds this weight
 constexpr uint32_t kBatchBackoff = 4;          // single merges after a batch that took none
+#ifndef VN_BATCH_REPAIRS
+#define VN_BATCH_REPAIRS 0
+#endif
+// flip repairs per batch (merge_batch, F'): a chunk whose temps the moving means put in another
+// column than the batch-start means did is re-done for the columns it touches instead of ending
+// the batch there; 0: every flip ends the batch (rounds 3-5)
+constexpr uint32_t kRepairs = VN_BATCH_REPAIRS;
+constexpr uint32_t kRepCols = 8;  // columns a batch may re-do (their per-chunk means in LDS)
 
 typedef __attribute__((address_space(3))) uint8_t ldsu8;
 
@@ -1989,12 +1989,23 @@ struct BatchLds {
   ldsu8* pos;       // [kBB * tcap] #means < v of temp p of chunk j (j * tcap + p)
   ldsu8* nT;        // [kBN][kRS] n[j][i] -- temps of chunk j before main i -- at i * kRS + j
   ldsu8* kT;        // [kBM][kRS] K[j][i] -- column i's list entries from chunks before j
+  // flip repair (F'): per boundary i (the count n[j][i] of temps <= mean i) the first chunk where
+  // it is wrong (kBB: none); per column its bound tests not certain; re-done columns' per-chunk
+  // mean and gain after each chunk from rfirst[slot] on, slot rslot[i] (0xff: not re-done)
+  ldsu32* ffl;      // [kBN + 1]
+  ldsf64* rmean;    // [kRepCols * kBB]
+  ldsu32* rgain;    // [kRepCols * kBB]
+  ldsu16* rlist;    // [kRepCols] the columns re-done in the current repair round
+  ldsu8* fl;        // [kBM]
+  ldsu8* rslot;     // [kBM]
+  ldsu8* rfirst;    // [kRepCols]
 };
 
 __host__ __device__ inline uint32_t batch_bytes(uint32_t tcap) {
   const uint32_t nl = kBB * tcap;
   return 12u * kRing * tcap + 16u * kBB + 16u * kBM + 24u * kBN + 8u * (nl + 1) + 4u * (nl + 1) + 4u * (kBN + 1) + 32u +
-         2u * kBM + (nl + 16u) + (nl + 16u) + 16u + kBN * kRS + kBM * kRS + 16u;
+         2u * kBM + (nl + 16u) + (nl + 16u) + 16u + kBN * kRS + kBM * kRS + 16u +
+         (kRepairs ? 4u * (kBN + 1) + 12u * kRepCols * kBB + 2u * kRepCols + 2u * kBM + kRepCols + 32u : 0u);
 }
 __host__ __device__ inline uint32_t batch_offset(uint32_t capc, uint32_t tcap) {
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = capc + TP + 1 > 320u ? capc + TP + 1 : 320u;
@@ -2019,10 +2030,22 @@ __device__ __forceinline__ BatchLds batch_layout(char* p, uint32_t tcap) {
   B.pos = B.lj + nl + 16;  // (lj[nl], pos[nl]: spare slots for idle lanes' stores)
   B.nT = (ldsu8*)(((uintptr_t)(B.pos + nl + 16) + 15u) & ~(uintptr_t)15u);
   B.kT = B.nT + kBN * kRS;
+  B.rmean = (ldsf64*)(((uintptr_t)(B.kT + kBM * kRS) + 15u) & ~(uintptr_t)15u);
+  B.rgain = (ldsu32*)(B.rmean + kRepCols * kBB);
+  B.ffl = B.rgain + kRepCols * kBB;
+  B.rlist = (ldsu16*)(B.ffl + kBN + 1);
+  B.fl = (ldsu8*)(B.rlist + kRepCols);
+  B.rslot = B.fl + kBM;
+  B.rfirst = B.rslot + kBM;
   return B;
 }
 
 __device__ __forceinline__ void lds_min(ldsu32* p, uint32_t v) { __atomic_fetch_min(p, v, __ATOMIC_RELAXED); }
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {  // (every lane active)
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, 64));
+  return v;
+}
 __device__ __forceinline__ uint32_t lds_inc(ldsu32* p) { return __atomic_fetch_add(p, 1u, __ATOMIC_RELAXED); }
 
 // n dwords from global src into LDS dst by global->LDS dword loads: each wave instruction moves
@@ -2149,6 +2172,14 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   // +inf past the last mean up to 192 (nm <= kBM = 160): A's searches read index min(i, 191), so
   // they need no other bound checks, and the tile needs only 192 entries (capc >= 192)
   for (uint32_t j = nm + t; j < 192u; j += NT) L.mm[j] = kInf;
+  if constexpr (kRepairs > 0) {  // (F': no boundary known wrong, no column re-done, none flagged)
+    for (uint32_t j = t; j <= kBN; j += NT) B.ffl[j] = kBB;
+    for (uint32_t j = t; j < kBM; j += NT) {
+      B.rslot[j] = 0xffu;
+      B.fl[j] = 0u;
+    }
+    if (t == 0) B.ctl[6] = 0u;
+  }
   fast_sync<NW>();
   PROF_T(b1);
   ASM_MARK("A_BEGIN");
@@ -2583,9 +2614,23 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
   ASM_MARK("F_BEGIN");
   // ---- F: decisions per temp against the columns' mean ranges (the exact mean merge j saw
   // only for a temp inside a range); bound tests per column
-  auto mean_before = [&](uint32_t ci, uint32_t j) {
+  // column ci's mean and gain (weight added since the batch start) before merge j: after its last
+  // list entry from a chunk < j, or (F') from its re-done means once past the chunk it was re-done from
+  auto mean_before = [&](uint32_t ci, uint32_t j) -> double {
+    if constexpr (kRepairs > 0) {
+      const uint32_t sl = B.rslot[ci];
+      if (sl != 0xffu && j > B.rfirst[sl]) return B.rmean[sl * kBB + j - 1];
+    }
     const uint32_t kq = B.kT[ci * kRS + j];
     return kq ? B.lv[B.off[ci] + kq - 1] : L.mm[ci];
+  };
+  auto gain_before = [&](uint32_t ci, uint32_t j) -> uint32_t {
+    if constexpr (kRepairs > 0) {
+      const uint32_t sl = B.rslot[ci];
+      if (sl != 0xffu && j > B.rfirst[sl]) return B.rgain[sl * kBB + j - 1];
+    }
+    const uint32_t kq = B.kT[ci * kRS + j];
+    return kq ? B.lw[B.off[ci] + kq - 1] : 0u;
   };
   {
     double hl[kA], lr[kA];
@@ -2599,20 +2644,24 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       const bool in = t + u * NT < nt;
       const bool rl = in && ps[u] >= 1 && gv[u] <= hl[u], rr = in && ps[u] < nm && gv[u] > lr[u];
       if (rl || rr) {  // (rare) inside a column's range: the exact order against the mean merge j saw
-        bool bad = false;
-        if (rl) bad = !(mean_before(ps[u] - 1, gj[u]) < gv[u]);     // main ps-1 before it
-        if (rr) bad = bad || !(gv[u] <= mean_before(ps[u], gj[u]));  // it before main ps
-        if (bad) lds_min(&B.ctl[0], gj[u]);
+        // (a failure is a flip: boundary ps-1 -- the count of temps up to mean ps-1 -- or boundary ps
+        // is wrong in chunk j; F' records the first such chunk per boundary)
+        const bool badl = rl && !(mean_before(ps[u] - 1, gj[u]) < gv[u]);  // main ps-1 before it
+        const bool badr = rr && !(gv[u] <= mean_before(ps[u], gj[u]));     // it before main ps
+        if (badl || badr) lds_min(&B.ctl[0], gj[u]);
+        if constexpr (kRepairs > 0) {
+          if (badl) lds_min(&B.ffl[ps[u] - 1], gj[u]);
+          if (badr) lds_min(&B.ffl[ps[u]], gj[u]);
+        }
       }
     }
   }
-  if (i < nm) {
-    if (i + 1 < nm && !(B.hi[i] <= B.lo[i + 1])) B.ctl[4] = 1u;
-    // k(a) - k(b) = delta / pi * (asin xa - asin xb) with x = 2q - 1: compared with kHi / kLo
-    // through D = asin xa - asin xb, sin D = xa cb - xb ca and cos D = ca cb + xa xb (c = sqrt(1 - x^2)
-    // = 2 sqrt(q (1 - q))); with cos D > 0, D is in (-pi/2, pi/2) where sin is increasing, so
-    // D > theta iff sin D > sin theta.  No arcsine: the band (kBand in k, about 3e-11 in sin)
-    // dwarfs these few roundings, and whatever it does not decide is tested exactly in G
+  // k(a) - k(b) = delta / pi * (asin xa - asin xb) with x = 2q - 1: compared with kHi / kLo
+  // through D = asin xa - asin xb, sin D = xa cb - xb ca and cos D = ca cb + xa xb (c = sqrt(1 - x^2)
+  // = 2 sqrt(q (1 - q))); with cos D > 0, D is in (-pi/2, pi/2) where sin is increasing, so
+  // D > theta iff sin D > sin theta.  No arcsine: the band (kBand in k, about 3e-11 in sin)
+  // dwarfs these few roundings, and whatever it does not decide is tested exactly in G
+  auto sure_col = [&](uint32_t ic) -> bool {
     auto xc = [](double qv, double& x, double& c) {
       qv = __builtin_fmin(qv, 1.0);  // (q <= 1: the reciprocal's rounding)
       x = 2.0 * qv - 1.0;
@@ -2620,19 +2669,160 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     };
     double xa, ca, xb, cb;
     bool sure = true;
-    if (i >= 1) {  // main i starts: k(min qe_i) - k(max qb_i-1) > kHi
-      xc(B.kb[i], xa, ca);
-      xc(B.kb[kBN + i - 1], xb, cb);
+    if (ic >= 1) {  // main i starts: k(min qe_i) - k(max qb_i-1) > kHi
+      xc(B.kb[ic], xa, ca);
+      xc(B.kb[kBN + ic - 1], xb, cb);
       sure = ca * cb + xa * xb > 0.0 && xa * cb - xb * ca > sin_hi;
     }
     // its temps join: k(max qb_i+1) - k(min qb_i) < kLo
-    xc(B.kb[kBN + i + 1], xa, ca);
-    xc(B.kb[2 * kBN + i], xb, cb);
-    sure = sure && ca * cb + xa * xb > 0.0 && xa * cb - xb * ca < sin_lo;
-    if (!sure) B.flagged[lds_inc(&B.ctl[1])] = (uint16_t)i;
+    xc(B.kb[kBN + ic + 1], xa, ca);
+    xc(B.kb[2 * kBN + ic], xb, cb);
+    return sure && ca * cb + xa * xb > 0.0 && xa * cb - xb * ca < sin_lo;
+  };
+  if (i < nm) {
+    if (i + 1 < nm && !(B.hi[i] <= B.lo[i + 1])) B.ctl[4] = 1u;
+    const bool sure = sure_col(i);
+    if constexpr (kRepairs > 0) B.fl[i] = sure ? 0u : 1u;
+    else if (!sure) B.flagged[lds_inc(&B.ctl[1])] = (uint16_t)i;
   }
   fast_sync<NW>();
   PROF_T(b7);
+  if constexpr (kRepairs > 0) {
+    // ---- F': flip repair.  The first chunk jf whose count at some boundary i (the temps up to mean
+    // i in merge jf) differs from the batch-start one: every such boundary of chunk jf is set to its
+    // exact count from the means merge jf saw, the two columns beside each (i - 1 and i, whose temps
+    // change) are re-done from chunk jf on -- their Welford chains, their C2 bounds -- and the
+    // boundaries of the re-done columns are checked again for the chunks after jf, where their means
+    // now differ.  Other columns' lists, means and first wrong chunks stand: a boundary depends only
+    // on its own column's mean.  Up to kRepairs rounds; a flip at boundary 0 or 1 (column 0's, with
+    // its Z temps) or past kRepCols re-done columns ends the batch there as before.
+    // tools/study/batch2_sim.c (repair cap) restates it on the CPU: bit-identical digests.
+    PROF_T(r0);
+    uint32_t nrep = 0;
+    for (; nrep < kRepairs; nrep++) {
+      const uint32_t jf = __builtin_amdgcn_readfirstlane(B.ctl[0]);
+      if (jf >= b || B.ctl[4]) break;
+      // R1 (wave 0): columns to re-do (boundary c or c + 1 fixed), their slots, the exact counts
+      if (wv == 0) {
+        const uint32_t nslot0 = B.ctl[6];
+        uint32_t nneed = 0, nnew = 0;
+        bool bad = false;
+        for (uint32_t c0 = 0; c0 < nm; c0 += 64) {
+          const uint32_t c = c0 + lane;
+          const bool fixc = c < nm && B.ffl[c] == jf, fixn = c < nm && B.ffl[c + 1] == jf;
+          bad |= fixc && c < 2;  // (boundaries 0 and 1: column 0 is not re-done)
+          const bool need = fixc || fixn, isnew = need && B.rslot[min(c, kBM - 1)] == 0xffu;
+          nneed += (uint32_t)__popcll(__ballot(need));
+          nnew += (uint32_t)__popcll(__ballot(isnew));
+        }
+        bad = __any(bad) || nneed > kRepCols || nslot0 + nnew > kRepCols;
+        if (!bad) {
+          const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+          uint32_t kn = 0, ks = nslot0;
+          for (uint32_t c0 = 0; c0 < nm; c0 += 64) {
+            const uint32_t c = c0 + lane;
+            const bool fixc = c < nm && B.ffl[c] == jf, fixn = c < nm && B.ffl[c + 1] == jf;
+            const bool need = fixc || fixn, isnew = need && B.rslot[min(c, kBM - 1)] == 0xffu;
+            const uint64_t bn = __ballot(need), bw = __ballot(isnew);
+            if (need) B.rlist[kn + (uint32_t)__popcll(bn & below)] = (uint16_t)c;
+            if (isnew) {
+              const uint32_t sl = ks + (uint32_t)__popcll(bw & below);
+              B.rslot[c] = (uint8_t)sl;
+              B.rfirst[sl] = (uint8_t)jf;
+            }
+            kn += (uint32_t)__popcll(bn);
+            ks += (uint32_t)__popcll(bw);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (this wave reads the slots below)
+          // the exact count of every fixed boundary in chunk jf (the means merge jf saw are those
+          // before the re-done chunks: the slots' rfirst is jf or earlier)
+          const uint32_t base = sbase(jf);
+          for (uint32_t c0 = 2; c0 < nm; c0 += 64) {
+            const uint32_t bi = c0 + lane;
+            if (bi < nm && B.ffl[bi] == jf) {
+              const double mb = mean_before(bi, jf);
+              uint32_t cn = B.nT[bi * kRS + jf];
+              while (cn > 0u && B.rv[base + cn - 1] > mb) cn--;
+              while (cn < tcap && B.rv[base + cn] <= mb) cn++;
+              B.nT[bi * kRS + jf] = (uint8_t)cn;
+            }
+          }
+        }
+        if (lane == 0) {
+          B.ctl[7] = bad ? 0xffffffffu : nneed;
+          if (!bad) B.ctl[6] = nslot0 + nnew;
+        }
+      }
+      fast_sync<NW>();
+      const uint32_t nredo = __builtin_amdgcn_readfirstlane(B.ctl[7]);
+      if (nredo == 0xffffffffu) break;
+      // R2: each re-done column's Welford chain from chunk jf (wave 0, a lane each: Go's
+      // sequence, the same operations as E); their C2 bounds on the other waves
+      if (wv == 0) {
+        if (lane < nredo) {
+          const uint32_t c = B.rlist[lane], sl = B.rslot[c];
+          double mean = mean_before(c, jf), lo = B.lo[c], hi = B.hi[c];
+          uint32_t gain = gain_before(c, jf);
+          double W = dadd(L.mw[c], (double)gain);
+          for (uint32_t j = jf; j < b; j++) {
+            const uint32_t a = B.nT[c * kRS + j], e = B.nT[(c + 1) * kRS + j], base = sbase(j);
+            for (uint32_t pq = a; pq < e; pq++) {
+              const double v = B.rv[base + pq];
+              const uint32_t w = B.rp[base + pq] & 0xffffu;
+              gain += w;
+              W = dadd(W, (double)w);
+              mean = dadd(mean, ddiv(dmul(dsub(v, mean), (double)w), W));
+              lo = __builtin_fmin(lo, mean);
+              hi = __builtin_fmax(hi, mean);
+            }
+            B.rmean[sl * kBB + j] = mean;
+            B.rgain[sl * kBB + j] = gain;
+          }
+          B.lo[c] = lo;
+          B.hi[c] = hi;
+        }
+      } else {
+        for (uint32_t f = wv - 1; f < nredo; f += NW - 1) c2_group(kC2Cols * (B.rlist[f] / kC2Cols));
+      }
+      fast_sync<NW>();
+      // R3: the re-done columns' boundaries checked again for every chunk after jf (a wave per
+      // column, lane = chunk: the count of temps up to the column's mean must be the table's), the
+      // means still in order, the bound tests of the columns beside them again
+      for (uint32_t f = wv; f < nredo; f += NW) {
+        const uint32_t c = B.rlist[f], j = lane;
+        const bool in = j > jf && j < b;
+        const uint32_t jj = in ? j : jf + 1u;
+        const double mb = mean_before(c, min(jj, b - 1));
+        const uint32_t a = B.nT[c * kRS + min(jj, kBB - 1)], base = sbase(min(jj, b - 1));
+        const double vlo = B.rv[base + (a ? a - 1u : 0u)], vhi = B.rv[base + min(a, tcap - 1)];
+        const bool wrong = in && ((a > 0u && vlo > mb) || (a < tcap && vhi <= mb));
+        const uint64_t fail = __ballot(wrong);
+        if (lane == 0) {
+          B.ffl[c] = fail ? (uint32_t)__builtin_ctzll(fail) : kBB;
+          if ((c >= 1 && !(B.hi[c - 1] <= B.lo[c])) || (c + 1 < nm && !(B.hi[c] <= B.lo[c + 1]))) B.ctl[4] = 1u;
+        }
+        if (lane < 3) {
+          const uint32_t ic = c + lane - 1u;  // columns c - 1, c, c + 1
+          if (ic < nm) B.fl[ic] = sure_col(ic) ? 0u : 1u;
+        }
+      }
+      fast_sync<NW>();
+      // R4 (wave 0): the first wrong chunk over every boundary
+      if (wv == 0) {
+        uint32_t m = kBB;
+        for (uint32_t c0 = 0; c0 < nm; c0 += 64) m = min(m, c0 + lane < nm ? B.ffl[c0 + lane] : kBB);
+        m = wave_min_u32(m);
+        if (lane == 0) B.ctl[0] = m;
+      }
+      fast_sync<NW>();
+    }
+    if (i < nm && B.fl[i]) B.flagged[lds_inc(&B.ctl[1])] = (uint16_t)i;
+    fast_sync<NW>();
+    PROF_T(r1);
+    PROF_ADD(32, 0, (long long)nrep);
+    PROF_ADD(33, r0, r1);
+    PROF_ADD(35, 0, (long long)B.ctl[6]);
+  }
   ASM_MARK("G_BEGIN");
   // ---- G: exact tests of the flagged columns, one wave per column, lane = chunk
   const uint32_t nflag = __builtin_amdgcn_readfirstlane(B.ctl[1]);
@@ -2672,7 +2862,12 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     if (i < nm) {
       const uint32_t o = B.off[i];
       const uint32_t kq = js < b ? (uint32_t)B.kT[i * kRS + js] : B.off[i + 1] - o;
-      if (kq) {
+      uint32_t sl = 0xffu;
+      if constexpr (kRepairs > 0) sl = B.rslot[i];
+      if (sl != 0xffu && js > B.rfirst[sl]) {  // (F': a re-done column)
+        L.mm[i] = B.rmean[sl * kBB + js - 1];
+        L.mw[i] = dadd(L.mw[i], (double)B.rgain[sl * kBB + js - 1]);
+      } else if (kq) {
         L.mm[i] = B.lv[o + kq - 1];
         L.mw[i] = dadd(L.mw[i], (double)B.lw[o + kq - 1]);
       }
@@ -2816,27 +3011,29 @@ __device__ void replay_key_fast(const ExactCtx& x, const uint32_t k, MwSharedL& 
     fok = r.fok;
     fint = r.fint;
   };
-  auto merge_sorted_cold = [&](uint32_t n_, double tempW, bool tint) {
-    const MergeState r =
-        merge_step_cold<NW>(L, F.mp, S, MP_ARGS(mp), nm, mainW, fok, fint, n_, tempW, tint, false, k0);
-    nm = r.nm;
-    mainW = r.w;
-    fok = r.fok;
-    fint = r.fint;
-  };
-  auto merge_pend = [&]() {  // sort the pending temps (wave 0), then merge them
+  // the pending temps (a call's first merge of a continuing key, a final or flush-ready merge):
+  // wave 0 sorts them and merges them with the one-wave merge (Go's mergeAllTemps restated), then
+  // rebuilds the main prefix.  (The four-wave fast merge out of line here, merge_step_cold, gave
+  // wrong digests in continuing calls in some builds -- tools/probe/repro_batch3_calls.py, DESIGN.md
+  // §4 -- while the same merge inlined for every chunk stayed exact: this merge, once per key and
+  // call, takes the plain path.)
+  auto merge_pend = [&]() {
     if (wv == 0) {
       const double tw_ = temp_weight(L.tw, np);
       sort_temps(L.tv, L.tw, L.sv, L.sw, np);
-      if (np <= 64) prefix_temps_w0(L, F, np);
-      else if (lane == 0) F.misc[2] = 0u;
-      if (lane == 0) F.miscd[0] = tw_;
+      const NmW r = merge_any_v(L, MP_ARGS(mp), nm, mainW, np, tw_);
+      prefix_main_w0(L, F, r.nm, r.w);
+      if (lane == 0) {
+        S.fb_nm = r.nm;
+        S.fb_w = r.w;
+      }
     }
     fast_sync<NW>();
-    const double tempW = F.miscd[0];
-    const bool tint = F.misc[2] != 0u;
-    fast_sync<NW>();
-    merge_sorted_cold(np, tempW, tint);
+    nm = S.fb_nm;
+    mainW = S.fb_w;
+    fok = F.misc[1] != 0u;
+    fint = F.misc[4] != 0u;
+    fast_sync<NW>();  // (S and misc are read before anyone writes them again)
   };
 
   if (nex && np == tcap) {

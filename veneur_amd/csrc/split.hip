@@ -814,6 +814,7 @@ void split_histos(vn_engine* e, vn_comm* c) {
   histo_merge_pending(a, olist, K);
   if (nmic) {
 #if !VN_FAST_MODE
+    (void)MicA1, (void)MicB1;
     throw std::logic_error("split histo pieces without the fast mode (VN_FAST_MODE) built");
 #else
     // pieces: (piece id, mean)-sorted micro-centroids, one mergeAllTemps per piece and round
