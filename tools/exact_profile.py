@@ -77,6 +77,11 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     out["batch_avg_repairs"] = round(p[32] / nb, 2)
     out["batch_cyc_repair"] = round(p[33] / nb, 1)
     out["batch_redone_columns"] = p[35]
+    nr = max(1, p[32])
+    out["repair_round_cyc"] = {"R1_counts": round(p[49] / nr, 1), "R2_welford_c2": round(p[50] / nr, 1),
+                               "R3_recheck": round(p[51] / nr, 1), "R4_first": round(p[55] / nr, 1),
+                               "R2_per_wave": [round(p[60 + w] / nr, 1) for w in range(4)],
+                               "chunks_after_flip": round(p[59] / nr, 1)}
     out["singles_after_reject"] = p[29]
     out["singles_after_reject_cyc"] = p[28]
     out["singles_unbatchable"] = p[31]

@@ -2702,6 +2702,8 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     for (; nrep < kRepairs; nrep++) {
       const uint32_t jf = __builtin_amdgcn_readfirstlane(B.ctl[0]);
       if (jf >= b || B.ctl[4]) break;
+      PROF_T(q0);
+      PROF_ADD(59, 0, (long long)(b - jf));
       // R1 (wave 0): columns to re-do (boundary c or c + 1 fixed), their slots, the exact counts
       if (wv == 0) {
         const uint32_t nslot0 = B.ctl[6];
@@ -2755,36 +2757,60 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       }
       fast_sync<NW>();
       const uint32_t nredo = __builtin_amdgcn_readfirstlane(B.ctl[7]);
+      PROF_T(q1);
+      PROF_ADD(49, q0, q1);
       if (nredo == 0xffffffffu) break;
       // R2: each re-done column's Welford chain from chunk jf (wave 0, a lane each: Go's
       // sequence, the same operations as E); their C2 bounds on the other waves
       if (wv == 0) {
+        bool tiny = false;
         if (lane < nredo) {
           const uint32_t c = B.rlist[lane], sl = B.rslot[c];
           double mean = mean_before(c, jf), lo = B.lo[c], hi = B.hi[c];
           uint32_t gain = gain_before(c, jf);
           double W = dadd(L.mw[c], (double)gain);
+          // (E's division: the reciprocal of W off the mean chain, the same operand-range argument;
+          // the next chunk's counts loaded while this chunk's temps run)
+          uint32_t a = B.nT[c * kRS + jf], e = B.nT[(c + 1) * kRS + jf];
           for (uint32_t j = jf; j < b; j++) {
-            const uint32_t a = B.nT[c * kRS + j], e = B.nT[(c + 1) * kRS + j], base = sbase(j);
+            const uint32_t jn = min(j + 1u, kBB - 1u);
+            const uint32_t an = B.nT[c * kRS + jn], en = B.nT[(c + 1) * kRS + jn], base = sbase(j);
             for (uint32_t pq = a; pq < e; pq++) {
               const double v = B.rv[base + pq];
               const uint32_t w = B.rp[base + pq] & 0xffffu;
+              const double wd = (double)w;
               gain += w;
-              W = dadd(W, (double)w);
-              mean = dadd(mean, ddiv(dmul(dsub(v, mean), (double)w), W));
-              lo = __builtin_fmin(lo, mean);
-              hi = __builtin_fmax(hi, mean);
+              W = dadd(W, wd);
+              const double r0 = __builtin_amdgcn_rcp(W);
+              const double e0_ = __builtin_fma(-W, r0, 1.0);
+              const double r1 = __builtin_fma(r0, e0_, r0);
+              const double e1_ = __builtin_fma(-W, r1, 1.0);
+              const double y = __builtin_fma(r1, e1_, r1);
+              const double tq = dmul(dsub(v, mean), wd);
+              tiny |= tq != 0.0 && __builtin_fabs(tq) < 1e-250;
+              const double q0 = dmul(tq, y);
+              const double rr = __builtin_fma(-W, q0, tq);
+              mean = dadd(mean, __builtin_fma(rr, y, q0));
+              asm("v_min_f64 %0, %1, %2" : "=v"(lo) : "v"(lo), "v"(mean));
+              asm("v_max_f64 %0, %1, %2" : "=v"(hi) : "v"(hi), "v"(mean));
             }
             B.rmean[sl * kBB + j] = mean;
             B.rgain[sl * kBB + j] = gain;
+            a = an;
+            e = en;
           }
           B.lo[c] = lo;
           B.hi[c] = hi;
         }
+        if (__any(tiny) && lane == 0) B.ctl[4] = 1u;  // (a numerator near the rescaling range: no batch)
       } else {
         for (uint32_t f = wv - 1; f < nredo; f += NW - 1) c2_group(kC2Cols * (B.rlist[f] / kC2Cols));
       }
+      PROF_T(q2w);
+      PROF_ADDW(60, q1, q2w);
       fast_sync<NW>();
+      PROF_T(q2);
+      PROF_ADD(50, q1, q2);
       // R3: the re-done columns' boundaries checked again for every chunk after jf (a wave per
       // column, lane = chunk: the count of temps up to the column's mean must be the table's), the
       // means still in order, the bound tests of the columns beside them again
@@ -2807,6 +2833,8 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
         }
       }
       fast_sync<NW>();
+      PROF_T(q3);
+      PROF_ADD(51, q2, q3);
       // R4 (wave 0): the first wrong chunk over every boundary
       if (wv == 0) {
         uint32_t m = kBB;
@@ -2815,6 +2843,8 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
         if (lane == 0) B.ctl[0] = m;
       }
       fast_sync<NW>();
+      PROF_T(q4);
+      PROF_ADD(55, q3, q4);
     }
     if (i < nm && B.fl[i]) B.flagged[lds_inc(&B.ctl[1])] = (uint16_t)i;
     fast_sync<NW>();

@@ -10,7 +10,10 @@
 // block hashes a 16384-record chunk of the batch into an LDS
 // table keyed by slot (wrapping i64 sums), then one device atomic per entry; a record that finds no
 // free entry within 8 probes adds to its device word directly.
-// Gauges avoid per-record device atomics (a Zipf-hot key would serialise them):
+// Gauges (default): the same key-range partition, carrying each record's arrival index instead
+// of its value (4 B read, 8 B written per record), then k_gauge_runs keeps each slot's last
+// record per slice in LDS and k_gauge_resolve_direct reads the winners' values from the caller's
+// array.  The former gauge path (VN_GAUGE_RUNS=0) avoids per-record device atomics too:
 //   1. one stable partition pass (partition.h) by the low 8 slot bits, fused with the
 //      per-record work (the counter contribution is computed while loading), so every
 //      bucket's records are contiguous and still in arrival order;
@@ -44,6 +47,10 @@ constexpr bool kScalarDirect = true;
 #endif
 constexpr bool kCounterRuns = VN_COUNTER_RUNS;  // k_counter_runs below (else k_scalar_direct)
 constexpr bool kGaugeDirect = false;
+#ifndef VN_GAUGE_RUNS
+#define VN_GAUGE_RUNS 1
+#endif
+constexpr bool kGaugeRuns = VN_GAUGE_RUNS;  // key-range partition + k_gauge_runs (else hashed k_scalar_agg)
 
 struct CounterSrc {
   const uint32_t* slot;
@@ -66,6 +73,18 @@ struct GaugeSrc {
   __device__ __forceinline__ void load(uint64_t i, uint32_t& k, uint64_t& p) const {
     k = slot[i];
     p = (uint64_t)__double_as_longlong(val[i]);
+  }
+};
+
+// Gauges by key range: the record's arrival index rides with its slot (the value stays in the
+// caller's array until the winner of each slot is known).
+struct GaugeIdxSrc {
+  const uint32_t* slot;
+  using P = uint32_t;
+  __device__ __forceinline__ uint32_t key(uint64_t i) const { return slot[i]; }
+  __device__ __forceinline__ void load(uint64_t i, uint32_t& k, uint32_t& p) const {
+    k = slot[i];
+    p = (uint32_t)i;
   }
 };
 
@@ -275,6 +294,54 @@ __global__ __launch_bounds__(kRunThreads) void k_counter_runs(uint64_t n, const 
   }
 }
 
+// Gauges by key range (the default): after the stable partition (GaugeIdxSrc, KV32Dst) a bucket's
+// records are in arrival order, so the last record of a slot in a slice is its largest position
+// there.  Each block takes a kRunChunk slice run by run, keeps 1 + the slice position of every
+// slot's last record in LDS, and offers the winner's arrival index to the slot's device word
+// (atomicMax of base + index + 1: across slices and batches the latest arrival wins, as
+// Gauge.Sample's plain store does, samplers.go:198-200).
+__global__ __launch_bounds__(kRunThreads) void k_gauge_runs(uint64_t n, const uint32_t* __restrict__ pk,
+                                                            const uint32_t* __restrict__ pidx,
+                                                            const uint32_t* __restrict__ offsets, uint32_t nparts,
+                                                            int shift, uint64_t base, uint64_t* __restrict__ gseq,
+                                                            uint32_t* __restrict__ gtouch) {
+  __shared__ uint32_t s_last[kRunMaxW];
+  const uint32_t W = 1u << shift, t = threadIdx.x;
+  const uint64_t c0 = (uint64_t)blockIdx.x * kRunChunk, c1 = min(n, c0 + kRunChunk);
+  for (uint64_t i = c0; i < c1;) {
+    uint32_t lo = 0, hi = 256;
+    while (hi - lo > 1) {
+      const uint32_t m = (lo + hi) >> 1;
+      if ((uint64_t)offsets[(uint64_t)m * nparts] <= i) lo = m;
+      else hi = m;
+    }
+    const uint32_t d = lo;
+    const uint64_t e = min(c1, (uint64_t)offsets[(uint64_t)(d + 1) * nparts]);
+    for (uint32_t j = t; j < W; j += kRunThreads) s_last[j] = 0;
+    __syncthreads();
+    uint64_t r = i + t;
+    for (; r + (kRunUnroll - 1) * kRunThreads < e; r += kRunUnroll * kRunThreads) {
+      uint32_t k[kRunUnroll];
+#pragma unroll
+      for (int u = 0; u < kRunUnroll; u++) k[u] = pk[r + u * kRunThreads] & (W - 1u);
+#pragma unroll
+      for (int u = 0; u < kRunUnroll; u++) atomicMax(&s_last[k[u]], (uint32_t)(r + u * kRunThreads - c0 + 1));
+    }
+    for (; r < e; r += kRunThreads) atomicMax(&s_last[pk[r] & (W - 1u)], (uint32_t)(r - c0 + 1));
+    __syncthreads();
+    const uint32_t sb = d << shift;
+    for (uint32_t j = t; j < W; j += kRunThreads) {
+      const uint32_t q = s_last[j];
+      if (q) {
+        atomicMax((unsigned long long*)&gseq[sb + j], (unsigned long long)(base + pidx[c0 + q - 1] + 1));
+        gtouch[sb + j] = 1;
+      }
+    }
+    __syncthreads();
+    i = e;
+  }
+}
+
 // gauges of the direct path: the winning position indexes the caller's value array
 __global__ void k_gauge_resolve_direct(uint32_t cap, uint64_t base, const uint64_t* __restrict__ gseq,
                                        const double* __restrict__ val, double* __restrict__ gval) {
@@ -338,6 +405,20 @@ void ingest_gauges(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
   if (!n) return;
   const uint64_t base = e->seq_base;
   e->seq_base += n;
+  const uint32_t cap = std::max<uint32_t>(e->cap[VN_GAUGE], 1u);
+  int shift = 0;
+  while (((cap - 1u) >> shift) >= 256u) shift++;
+  if (kGaugeRuns && (1u << shift) <= kRunMaxW && n < (1ull << 32)) {
+    RadixStats* rs = e->timing ? &e->rstat_c : nullptr;
+    uint32_t* pidx = reinterpret_cast<uint32_t*>(e->pp);
+    const uint32_t nparts =
+        partition_pass(GaugeIdxSrc{slot}, KV32Dst{e->pk, pidx}, n, shift, *e->side_rs, e->side, rs, 4 + 8);
+    hipLaunchKernelGGL(k_gauge_runs, dim3((uint32_t)((n + kRunChunk - 1) / kRunChunk)), dim3(kRunThreads), 0,
+                       e->side, n, e->pk, pidx, e->side_rs->offsets, nparts, shift, base, e->gseq, e->gtouch);
+    hipLaunchKernelGGL(k_gauge_resolve_direct, dim3(blocks_for(cap, 256)), dim3(256), 0, e->side, cap, base,
+                       e->gseq, val, e->gval);
+    return;
+  }
   if (kGaugeDirect) {
     hipLaunchKernelGGL(k_scalar_direct<true>, dim3(blocks_for(n, kAggChunk)), dim3(kAggThreads), 0, e->side, n, slot,
                        nullptr, nullptr, base, e->gseq, e->gtouch);

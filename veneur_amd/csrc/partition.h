@@ -9,24 +9,6 @@
 
 namespace vn {
 
-template <class Src>
-__global__ __launch_bounds__(kBlock) void k_part_count(Src src, uint64_t n, int shift, uint32_t* __restrict__ counts,
-                                                       uint32_t nblocks) {
-  __shared__ uint32_t s_hist[4][256];
-  const int w = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < 4 * 256; i += kBlock) (&s_hist[0][0])[i] = 0;
-  __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kTile;
-#pragma unroll 4
-  for (int j = 0; j < kItems; j++) {
-    uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
-    if (i < n) atomicAdd(&s_hist[w][(src.key(i) >> shift) & 0xffu], 1u);
-  }
-  __syncthreads();
-  const uint32_t d = threadIdx.x;
-  counts[(uint64_t)d * nblocks + blockIdx.x] = s_hist[0][d] + s_hist[1][d] + s_hist[2][d] + s_hist[3][d];
-}
-
 __device__ __forceinline__ uint64_t part_match8(uint32_t d, bool active) {
   uint64_t m = __ballot(active);
 #pragma unroll
@@ -35,6 +17,36 @@ __device__ __forceinline__ uint64_t part_match8(uint32_t d, bool active) {
     m &= ((d >> bit) & 1u) ? bb : ~bb;
   }
   return m;
+}
+
+// Per-tile digit counts.  The lanes of a wave that share a digit add once, through their lowest
+// lane (the wave's match mask): a Zipf-hot bucket -- most of a key-range partition's records --
+// would otherwise serialise 64 LDS atomics on one address per load.
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_part_count(Src src, uint64_t n, int shift, uint32_t* __restrict__ counts,
+                                                       uint32_t nblocks) {
+  __shared__ uint32_t s_hist[4][256];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < 4 * 256; i += kBlock) (&s_hist[0][0])[i] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kTile;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t key[kItems];
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    const uint64_t i = base + (uint64_t)j * kBlock + threadIdx.x;
+    key[j] = i < n ? src.key(i) : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < kItems; j++) {
+    const bool active = base + (uint64_t)j * kBlock + threadIdx.x < n;
+    const uint32_t d = (key[j] >> shift) & 0xffu;
+    const uint64_t peers = part_match8(d, active);
+    if (active && (peers & lt) == 0) atomicAdd(&s_hist[w][d], (uint32_t)__popcll(peers));
+  }
+  __syncthreads();
+  const uint32_t d = threadIdx.x;
+  counts[(uint64_t)d * nblocks + blockIdx.x] = s_hist[0][d] + s_hist[1][d] + s_hist[2][d] + s_hist[3][d];
 }
 
 // Each wave owns a contiguous quarter of the tile: its records are loaded up front (all loads
@@ -177,6 +189,14 @@ struct KV64Dst {  // u32 key + u64 payload
   uint32_t* key;
   uint64_t* pay;
   __device__ __forceinline__ void store(uint64_t pos, uint32_t k, uint64_t p) const {
+    key[pos] = k;
+    pay[pos] = p;
+  }
+};
+struct KV32Dst {  // u32 key + u32 payload
+  uint32_t* key;
+  uint32_t* pay;
+  __device__ __forceinline__ void store(uint64_t pos, uint32_t k, uint32_t p) const {
     key[pos] = k;
     pay[pos] = p;
   }
