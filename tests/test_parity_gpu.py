@@ -254,6 +254,34 @@ def test_set_random_members_parity_multi_batch():
     _set_parity(d, d["n_slots"], batches=5)
 
 
+@pytest.mark.parametrize("batches", [1, 3])
+def test_set_grouped_merges_and_dense_crossing(batches):
+    """mergeSparse grouped over up to six triggers (ingest_set.hip, kSetGroup; hyperloglog.go:
+    186-267): a key that stays sparse through many triggers, keys whose group's union passes m
+    (its triggers scanned again one merge each, toNormal at the reference's record), a key whose
+    list of 1-byte deltas leaves no room for a group, and repeated members across triggers."""
+    rng = np.random.default_rng(61)
+    parts = []
+    # key 0: codes two apart (idx << 1, encodeHash with the top 25 bits = idx): 1-byte deltas, so
+    # the list passes 13568 codes while sparse, then toNormal near 16384
+    idx = rng.permutation(np.arange(1, 20001, dtype=np.uint64))
+    parts.append((0, (idx << np.uint64(39)) | np.uint64(1 << 30)))
+    parts.append((1, rng.integers(0, 2**63, 12000, dtype=np.uint64)))  # dense within the batch
+    parts.append((2, rng.integers(0, 2**63, 3000, dtype=np.uint64)))   # sparse, ~18 triggers
+    rep = rng.integers(0, 2**63, 2000, dtype=np.uint64)
+    parts.append((3, rng.permutation(np.concatenate([rep, rep, rep]))))  # codes repeat across tmpSets
+    slots = np.concatenate([np.full(len(h), k, np.uint32) for k, h in parts])
+    hashes = np.concatenate([h for _, h in parts])
+    order = rng.permutation(len(slots))  # keys interleaved; each key's own order is its arrival order
+    d = {"c_slot": np.zeros(0, np.uint32), "c_val": np.zeros(0), "c_rate": np.zeros(0, np.float32),
+         "g_slot": np.zeros(0, np.uint32), "g_val": np.zeros(0),
+         "h_slot": np.zeros(0, np.uint32), "h_val": np.zeros(0), "h_rate": np.zeros(0, np.float32),
+         "s_slot": slots[order], "s_hash": hashes[order]}
+    w = run_oracle(d, (0, 0, 0, 4), hashed=True)
+    assert not w.set_sketch(0).sparse and not w.set_sketch(1).sparse and w.set_sketch(2).sparse
+    _set_parity(d, (1, 1, 1, 4), batches=batches, hashed=True)
+
+
 def test_set_dense_rebase_epochs():
     """One key receives enough distinct hashes to fill all 16384 registers, then keeps going,
     so rebases (b > 0) happen mid-stream (hyperloglog.go:168-183, registers.go:55-123)."""

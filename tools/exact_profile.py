@@ -78,7 +78,7 @@ def run(n_hot, n_cold_keys, cold_per_key, seed=1):
     out["batch_cyc_repair"] = round(p[33] / nb, 1)
     out["batch_redone_columns"] = p[35]
     nr = max(1, p[32])
-    out["repair_round_cyc"] = {"R1_counts": round(p[49] / nr, 1), "R2_welford_c2": round(p[50] / nr, 1),
+    out["repair_round_cyc"] = {"R1_flags": round(p[49] / nr, 1), "R1_slots_counts": round(p[34] / nr, 1), "R2_welford_c2": round(p[50] / nr, 1),
                                "R3_recheck": round(p[51] / nr, 1), "R4_first": round(p[55] / nr, 1),
                                "R2_per_wave": [round(p[60 + w] / nr, 1) for w in range(4)],
                                "chunks_after_flip": round(p[59] / nr, 1)}

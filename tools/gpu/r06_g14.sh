@@ -1,0 +1,12 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
+T=r06_o
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_parity_gpu.py tests/test_configs_gpu.py > gpurun_out/${T}_tests.log 2>&1 || exit 10
+VN_LIB=libveneur_amd_setprof.so timeout -k 10 200 python -u tools/set_profile.py > gpurun_out/${T}_setprof_group.log 2>&1 || exit 11
+VN_LIB=libveneur_amd_setprof0.so timeout -k 10 200 python -u tools/set_profile.py > gpurun_out/${T}_setprof_nogroup.log 2>&1 || exit 12
+Q="--no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0"
+S="$Q --worker-windows 0 --sim-world 8 --sim-rank 3 --steps 12"
+for D in 4 5 8; do
+GPU_MAX_HW_QUEUES=32 timeout -k 10 400 python -u bench.py $S --pipeline $D > gpurun_out/${T}_sim_8_3_${D}_q32.json 2> gpurun_out/${T}_sim_8_3_${D}_q32.log || exit 13
+done
+echo done

@@ -1,0 +1,12 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
+T=r06_r
+Q="--no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0"
+S="$Q --worker-windows 0 --sim-world 8 --sim-rank 3 --steps 20 --timing-steps 0"
+for D in 4 6; do for HQ in 16 32; do
+GPU_MAX_HW_QUEUES=$HQ timeout -k 10 400 python -u bench.py $S --pipeline $D > gpurun_out/${T}_sim_8_3_${D}_q${HQ}.json 2> gpurun_out/${T}_sim_8_3_${D}_q${HQ}.log || exit 13
+done; done
+for D in 4 6; do
+GPU_MAX_HW_QUEUES=16 VN_LIB=libveneur_amd_prof.so timeout -k 10 400 python -u bench.py $S --pipeline $D > gpurun_out/${T}_simprof_8_3_${D}_q16.json 2> gpurun_out/${T}_simprof_8_3_${D}_q16.log || exit 14
+done
+echo done

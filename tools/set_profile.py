@@ -14,7 +14,8 @@ import veneur_amd._abi as A  # noqa: E402
 
 A.lib.vn_prof_set_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 NAMES = ["setup", "sparse scan", "sparse merge", "toNormal", "dense", "write-back", "triggers", "heavy keys",
-         "heavy records", "workgroups"]
+         "heavy records", "workgroups", "group merges", "group codes", "group fallbacks", "single merges", "longest workgroup",
+         "its records"]
 
 
 def main():
@@ -28,7 +29,7 @@ def main():
     with V.Engine(caps, percentiles=(0.5,), max_batch_records=n_set + 1, max_batch_member_bytes=n_set * 11 + 64) as e:
         for rep in range(3):
             e.timing_enable(True)
-            buf = (C.c_ulonglong * 16)()
+            buf = (C.c_ulonglong * 32)()
             A.lib.vn_prof_set_read(buf, 1)
             assert A.lib.vn_ingest(e.h, C.byref(batch)) == 0, A.lib.vn_last_error(e.h)
             e.flush_raw()
@@ -40,6 +41,8 @@ def main():
             for i, nm in enumerate(NAMES):
                 v = buf[i]
                 print("   %-14s %16d %s" % (nm, v, ("%5.1f%%" % (100.0 * v / tot)) if i < 6 or i == 9 else ""))
+            print("   workgroup 0 (the key with the most records):",
+                  {NAMES[i]: int(buf[16 + i]) for i in (0, 1, 2, 3, 4, 5, 9)})
 
 
 if __name__ == "__main__":

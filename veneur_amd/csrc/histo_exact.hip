@@ -1953,11 +1953,13 @@ constexpr uint32_t kBMinAvail = 32;         // chunks in the ring below which a 
 constexpr double kBatchMinW = VN_BATCH_MIN_W;  // batches start once the digest holds this weight
 constexpr uint32_t kBatchBackoff = 4;          // single merges after a batch that took none
 #ifndef VN_BATCH_REPAIRS
-#define VN_BATCH_REPAIRS 0
+#define VN_BATCH_REPAIRS 4
 #endif
 // flip repairs per batch (merge_batch, F'): a chunk whose temps the moving means put in another
 // column than the batch-start means did is re-done for the columns it touches instead of ending
-// the batch there; 0: every flip ends the batch (rounds 3-5)
+// the batch there; 0: every flip ends the batch (rounds 3-5).  Measured (4M-sample key, profiling
+// build): 36.5 -> 54.3 merges committed per batch, 2590 -> 1743 batches, a repair round ~16k
+// cycles; the 17M-sample key 175.9 -> 166.9 ms (profiles/r06_*)
 constexpr uint32_t kRepairs = VN_BATCH_REPAIRS;
 constexpr uint32_t kRepCols = 8;  // columns a batch may re-do (their per-chunk means in LDS)
 
@@ -1999,13 +2001,15 @@ struct BatchLds {
   ldsu8* fl;        // [kBM]
   ldsu8* rslot;     // [kBM]
   ldsu8* rfirst;    // [kRepCols]
+  ldsu32* rctl;     // [5] a repair round's counts: 0 columns to re-do, 1 new slots, 2 boundary 0/1
+                    //     wrong, 3 the list's fill, 4 the first wrong chunk of the other boundaries
 };
 
 __host__ __device__ inline uint32_t batch_bytes(uint32_t tcap) {
   const uint32_t nl = kBB * tcap;
   return 12u * kRing * tcap + 16u * kBB + 16u * kBM + 24u * kBN + 8u * (nl + 1) + 4u * (nl + 1) + 4u * (kBN + 1) + 32u +
          2u * kBM + (nl + 16u) + (nl + 16u) + 16u + kBN * kRS + kBM * kRS + 16u +
-         (kRepairs ? 4u * (kBN + 1) + 12u * kRepCols * kBB + 2u * kRepCols + 2u * kBM + kRepCols + 32u : 0u);
+         (kRepairs ? 4u * (kBN + 1) + 12u * kRepCols * kBB + 2u * kRepCols + 2u * kBM + kRepCols + 48u : 0u);
 }
 __host__ __device__ inline uint32_t batch_offset(uint32_t capc, uint32_t tcap) {
   const uint32_t TP = (tcap + 1 + 63u) & ~63u, JW = capc + TP + 1 > 320u ? capc + TP + 1 : 320u;
@@ -2037,6 +2041,7 @@ __device__ __forceinline__ BatchLds batch_layout(char* p, uint32_t tcap) {
   B.fl = (ldsu8*)(B.rlist + kRepCols);
   B.rslot = B.fl + kBM;
   B.rfirst = B.rslot + kBM;
+  B.rctl = (ldsu32*)(((uintptr_t)(B.rfirst + kRepCols) + 3u) & ~(uintptr_t)3u);
   return B;
 }
 
@@ -2178,6 +2183,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       B.rslot[j] = 0xffu;
       B.fl[j] = 0u;
     }
+    if (t < 5) B.rctl[t] = t == 4 ? kBB : 0u;
     if (t == 0) B.ctl[6] = 0u;
   }
   fast_sync<NW>();
@@ -2704,107 +2710,130 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       if (jf >= b || B.ctl[4]) break;
       PROF_T(q0);
       PROF_ADD(59, 0, (long long)(b - jf));
-      // R1 (wave 0): columns to re-do (boundary c or c + 1 fixed), their slots, the exact counts
-      if (wv == 0) {
-        const uint32_t nslot0 = B.ctl[6];
-        uint32_t nneed = 0, nnew = 0;
-        bool bad = false;
-        for (uint32_t c0 = 0; c0 < nm; c0 += 64) {
-          const uint32_t c = c0 + lane;
-          const bool fixc = c < nm && B.ffl[c] == jf, fixn = c < nm && B.ffl[c + 1] == jf;
-          bad |= fixc && c < 2;  // (boundaries 0 and 1: column 0 is not re-done)
-          const bool need = fixc || fixn, isnew = need && B.rslot[min(c, kBM - 1)] == 0xffu;
-          nneed += (uint32_t)__popcll(__ballot(need));
-          nnew += (uint32_t)__popcll(__ballot(isnew));
-        }
-        bad = __any(bad) || nneed > kRepCols || nslot0 + nnew > kRepCols;
-        if (!bad) {
-          const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-          uint32_t kn = 0, ks = nslot0;
-          for (uint32_t c0 = 0; c0 < nm; c0 += 64) {
-            const uint32_t c = c0 + lane;
-            const bool fixc = c < nm && B.ffl[c] == jf, fixn = c < nm && B.ffl[c + 1] == jf;
-            const bool need = fixc || fixn, isnew = need && B.rslot[min(c, kBM - 1)] == 0xffu;
-            const uint64_t bn = __ballot(need), bw = __ballot(isnew);
-            if (need) B.rlist[kn + (uint32_t)__popcll(bn & below)] = (uint16_t)c;
-            if (isnew) {
-              const uint32_t sl = ks + (uint32_t)__popcll(bw & below);
-              B.rslot[c] = (uint8_t)sl;
-              B.rfirst[sl] = (uint8_t)jf;
-            }
-            kn += (uint32_t)__popcll(bn);
-            ks += (uint32_t)__popcll(bw);
-          }
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (this wave reads the slots below)
-          // the exact count of every fixed boundary in chunk jf (the means merge jf saw are those
-          // before the re-done chunks: the slots' rfirst is jf or earlier)
-          const uint32_t base = sbase(jf);
-          for (uint32_t c0 = 2; c0 < nm; c0 += 64) {
-            const uint32_t bi = c0 + lane;
-            if (bi < nm && B.ffl[bi] == jf) {
-              const double mb = mean_before(bi, jf);
-              uint32_t cn = B.nT[bi * kRS + jf];
-              while (cn > 0u && B.rv[base + cn - 1] > mb) cn--;
-              while (cn < tcap && B.rv[base + cn] <= mb) cn++;
-              B.nT[bi * kRS + jf] = (uint8_t)cn;
-            }
-          }
-        }
+      // R1 (a thread per column): the columns to re-do (boundary c or c + 1 fixed), counted
+      const uint32_t fi = i < nm ? B.ffl[i] : kBB;
+      const bool fixc = fi == jf, fixn = i < nm && B.ffl[i + 1] == jf;
+      const bool need = fixc || fixn, isnew = need && B.rslot[min(i, kBM - 1)] == 0xffu;
+      {
+        const uint64_t bn = __ballot(need), bw = __ballot(isnew), bb = __ballot(fixc && i < 2);
+        // (the first wrong chunk over the boundaries R3 does not re-check: R3 adds its own to it)
+        const uint32_t mo = wave_min_u32(need ? kBB : fi);
         if (lane == 0) {
-          B.ctl[7] = bad ? 0xffffffffu : nneed;
-          if (!bad) B.ctl[6] = nslot0 + nnew;
+          if (bn | bb) {  // (boundaries 0 and 1: column 0 is not re-done)
+            __atomic_fetch_add(&B.rctl[0], (uint32_t)__popcll(bn), __ATOMIC_RELAXED);
+            __atomic_fetch_add(&B.rctl[1], (uint32_t)__popcll(bw), __ATOMIC_RELAXED);
+            if (bb) B.rctl[2] = 1u;
+          }
+          if (mo < kBB) lds_min(&B.rctl[4], mo);
         }
       }
       fast_sync<NW>();
-      const uint32_t nredo = __builtin_amdgcn_readfirstlane(B.ctl[7]);
+      const uint32_t nneed = __builtin_amdgcn_readfirstlane(B.rctl[0]);
+      const bool bad = B.rctl[2] != 0u || nneed > kRepCols || B.ctl[6] + B.rctl[1] > kRepCols;
       PROF_T(q1);
       PROF_ADD(49, q0, q1);
-      if (nredo == 0xffffffffu) break;
-      // R2: each re-done column's Welford chain from chunk jf (wave 0, a lane each: Go's
-      // sequence, the same operations as E); their C2 bounds on the other waves
-      if (wv == 0) {
+      if (bad) break;
+      // ... their slots and list, and the exact count of every fixed boundary in chunk jf (the
+      // means merge jf saw: a slot taken now has rfirst = jf, so mean_before still reads the lists)
+      if (need) B.rlist[lds_inc(&B.rctl[3])] = (uint16_t)i;
+      if (isnew) {
+        const uint32_t sl = lds_inc(&B.ctl[6]);
+        B.rslot[i] = (uint8_t)sl;
+        B.rfirst[sl] = (uint8_t)jf;
+      }
+      if (fixc && i >= 2) {
+        const uint32_t base = sbase(jf);
+        const double mb = mean_before(i, jf);
+        uint32_t cn = B.nT[i * kRS + jf];
+        while (cn > 0u && B.rv[base + cn - 1] > mb) cn--;
+        while (cn < tcap && B.rv[base + cn] <= mb) cn++;
+        B.nT[i * kRS + jf] = (uint8_t)cn;
+      }
+      if (t == 0) B.ctl[0] = B.rctl[4];
+      fast_sync<NW>();
+      const uint32_t nredo = nneed;
+      if (t == 0) B.rctl[0] = B.rctl[1] = B.rctl[3] = 0u, B.rctl[4] = kBB;  // (all read before the barrier above)
+      PROF_T(q1b);
+      PROF_ADD(34, q1, q1b);
+      // R2: each re-done column's Welford chain from chunk jf on a wave of its own (Go's sequence,
+      // E's operations), and the C2 bounds of the re-done columns' groups on the other waves: item
+      // k < nredo is column k's chain, item nredo + k its group's bounds, wave k % NW takes item k.
+      // A chain's wave holds chunk j's first four temps of the column in lane j (one LDS round trip
+      // for the whole walk); the walk reads them with v_readlane (the chunk index is uniform), so
+      // only the mean's seven dependent operations per temp remain on the critical path, and each
+      // lane keeps the mean and gain after its chunk (a chunk without temps keeps the last ones).
+      static_assert(kBB <= 64, "a chain's wave holds one chunk per lane");
+      for (uint32_t k = wv; k < 2u * nredo; k += NW) {
+        if (k >= nredo) {
+          c2_group(kC2Cols * (B.rlist[k - nredo] / kC2Cols));
+          continue;
+        }
+        const uint32_t c = B.rlist[k], sl = B.rslot[c];
+        const uint32_t jl = min(lane, kBB - 1u), tl = tcap - 1u;
+        const uint32_t aj = B.nT[c * kRS + jl], ej = B.nT[(c + 1) * kRS + jl], bj = sbase(min(lane, b - 1u));
+        double vq[4];
+        uint32_t wq[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+          vq[u] = B.rv[bj + min(aj + u, tl)];
+          wq[u] = B.rp[bj + min(aj + u, tl)] & 0xffffu;
+        }
+        double mean = mean_before(c, jf), lo = B.lo[c], hi = B.hi[c];
+        uint32_t gain = gain_before(c, jf);
+        double W = dadd(L.mw[c], (double)gain);
+        double rm = mean;
+        uint32_t rg = gain;
         bool tiny = false;
-        if (lane < nredo) {
-          const uint32_t c = B.rlist[lane], sl = B.rslot[c];
-          double mean = mean_before(c, jf), lo = B.lo[c], hi = B.hi[c];
-          uint32_t gain = gain_before(c, jf);
-          double W = dadd(L.mw[c], (double)gain);
-          // (E's division: the reciprocal of W off the mean chain, the same operand-range argument;
-          // the next chunk's counts loaded while this chunk's temps run)
-          uint32_t a = B.nT[c * kRS + jf], e = B.nT[(c + 1) * kRS + jf];
-          for (uint32_t j = jf; j < b; j++) {
-            const uint32_t jn = min(j + 1u, kBB - 1u);
-            const uint32_t an = B.nT[c * kRS + jn], en = B.nT[(c + 1) * kRS + jn], base = sbase(j);
-            for (uint32_t pq = a; pq < e; pq++) {
-              const double v = B.rv[base + pq];
-              const uint32_t w = B.rp[base + pq] & 0xffffu;
-              const double wd = (double)w;
-              gain += w;
-              W = dadd(W, wd);
-              const double r0 = __builtin_amdgcn_rcp(W);
-              const double e0_ = __builtin_fma(-W, r0, 1.0);
-              const double r1 = __builtin_fma(r0, e0_, r0);
-              const double e1_ = __builtin_fma(-W, r1, 1.0);
-              const double y = __builtin_fma(r1, e1_, r1);
-              const double tq = dmul(dsub(v, mean), wd);
-              tiny |= tq != 0.0 && __builtin_fabs(tq) < 1e-250;
-              const double q0 = dmul(tq, y);
-              const double rr = __builtin_fma(-W, q0, tq);
-              mean = dadd(mean, __builtin_fma(rr, y, q0));
-              asm("v_min_f64 %0, %1, %2" : "=v"(lo) : "v"(lo), "v"(mean));
-              asm("v_max_f64 %0, %1, %2" : "=v"(hi) : "v"(hi), "v"(mean));
-            }
-            B.rmean[sl * kBB + j] = mean;
-            B.rgain[sl * kBB + j] = gain;
-            a = an;
-            e = en;
+        auto step = [&](double v, uint32_t w) {
+          const double wd = (double)w;
+          gain += w;
+          W = dadd(W, wd);
+          const double r0 = __builtin_amdgcn_rcp(W);
+          const double e0_ = __builtin_fma(-W, r0, 1.0);
+          const double r1 = __builtin_fma(r0, e0_, r0);
+          const double e1_ = __builtin_fma(-W, r1, 1.0);
+          const double y = __builtin_fma(r1, e1_, r1);
+          const double tq = dmul(dsub(v, mean), wd);
+          tiny |= tq != 0.0 && __builtin_fabs(tq) < 1e-250;
+          const double q0 = dmul(tq, y);
+          const double rr = __builtin_fma(-W, q0, tq);
+          mean = dadd(mean, __builtin_fma(rr, y, q0));
+          asm("v_min_f64 %0, %1, %2" : "=v"(lo) : "v"(lo), "v"(mean));
+          asm("v_max_f64 %0, %1, %2" : "=v"(hi) : "v"(hi), "v"(mean));
+        };
+        auto rl64 = [](double x, uint32_t l) {
+          const uint64_t u = (uint64_t)__double_as_longlong(x);
+          const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), (int)l);
+          const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, (int)l);
+          return __longlong_as_double((long long)(((uint64_t)h << 32) | o));
+        };
+        // the chunks jf <= j < b with temps of this column, in order
+        uint64_t todo = __ballot(lane >= jf && lane < b && ej > aj);
+        while (todo) {
+          const uint32_t jj = (uint32_t)__builtin_ctzll(todo);
+          todo &= todo - 1u;
+          const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)(ej - aj), (int)jj);
+#pragma unroll
+          for (uint32_t u = 0; u < 4; u++)
+            if (u < n) step(rl64(vq[u], jj), (uint32_t)__builtin_amdgcn_readlane((int)wq[u], (int)jj));
+          if (n > 4u) {  // (rare: more than four temps of the column in one chunk)
+            const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)aj, (int)jj), bs = sbase(jj);
+            for (uint32_t u = 4; u < n; u++) step(B.rv[bs + a0 + u], B.rp[bs + a0 + u] & 0xffffu);
           }
+          if (lane >= jj) {
+            rm = mean;
+            rg = gain;
+          }
+        }
+        if (lane >= jf && lane < b) {
+          B.rmean[sl * kBB + lane] = rm;
+          B.rgain[sl * kBB + lane] = rg;
+        }
+        if (lane == 0) {
           B.lo[c] = lo;
           B.hi[c] = hi;
+          if (tiny) B.ctl[4] = 1u;  // (a numerator near the rescaling range: no batch)
         }
-        if (__any(tiny) && lane == 0) B.ctl[4] = 1u;  // (a numerator near the rescaling range: no batch)
-      } else {
-        for (uint32_t f = wv - 1; f < nredo; f += NW - 1) c2_group(kC2Cols * (B.rlist[f] / kC2Cols));
       }
       PROF_T(q2w);
       PROF_ADDW(60, q1, q2w);
@@ -2825,6 +2854,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
         const uint64_t fail = __ballot(wrong);
         if (lane == 0) {
           B.ffl[c] = fail ? (uint32_t)__builtin_ctzll(fail) : kBB;
+          if (fail) lds_min(&B.ctl[0], (uint32_t)__builtin_ctzll(fail));
           if ((c >= 1 && !(B.hi[c - 1] <= B.lo[c])) || (c + 1 < nm && !(B.hi[c] <= B.lo[c + 1]))) B.ctl[4] = 1u;
         }
         if (lane < 3) {
@@ -2835,16 +2865,6 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       fast_sync<NW>();
       PROF_T(q3);
       PROF_ADD(51, q2, q3);
-      // R4 (wave 0): the first wrong chunk over every boundary
-      if (wv == 0) {
-        uint32_t m = kBB;
-        for (uint32_t c0 = 0; c0 < nm; c0 += 64) m = min(m, c0 + lane < nm ? B.ffl[c0 + lane] : kBB);
-        m = wave_min_u32(m);
-        if (lane == 0) B.ctl[0] = m;
-      }
-      fast_sync<NW>();
-      PROF_T(q4);
-      PROF_ADD(55, q3, q4);
     }
     if (i < nm && B.fl[i]) B.flagged[lds_inc(&B.ctl[1])] = (uint16_t)i;
     fast_sync<NW>();

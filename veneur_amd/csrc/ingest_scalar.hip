@@ -57,11 +57,28 @@ struct CounterSrc {
   const double* val;
   const float* rate;
   using P = uint64_t;
+  bool key16() const { return ((uintptr_t)slot & 15u) == 0; }
+  __device__ __forceinline__ uint4 key4(uint64_t i) const { return *reinterpret_cast<const uint4*>(slot + i); }
   __device__ __forceinline__ uint32_t key(uint64_t i) const { return slot[i]; }
   __device__ __forceinline__ void load(uint64_t i, uint32_t& k, uint64_t& p) const {
     k = slot[i];
     float inv = 1.0f / rate[i];  // float32 division, as Go's 1/sampleRate on a float32
     p = (uint64_t)f64_to_i64_go(val[i]) * (uint64_t)f64_to_i64_go((double)inv);
+  }
+  // the sums are order-free: four adjacent records per 16-byte load when every array allows it
+  bool vec16() const {
+    return ((((uintptr_t)slot) | ((uintptr_t)val) | ((uintptr_t)rate)) & 15u) == 0;
+  }
+  __device__ __forceinline__ void load4(uint64_t i, uint32_t* k, uint64_t* p) const {
+    const uint4 s4 = *reinterpret_cast<const uint4*>(slot + i);
+    const float4 r4 = *reinterpret_cast<const float4*>(rate + i);
+    const double2 v0 = *reinterpret_cast<const double2*>(val + i), v1 = *reinterpret_cast<const double2*>(val + i + 2);
+    const float r[4] = {r4.x, r4.y, r4.z, r4.w};
+    const double v[4] = {v0.x, v0.y, v1.x, v1.y};
+    k[0] = s4.x, k[1] = s4.y, k[2] = s4.z, k[3] = s4.w;
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      p[q] = (uint64_t)f64_to_i64_go(v[q]) * (uint64_t)f64_to_i64_go((double)(1.0f / r[q]));
   }
 };
 
@@ -69,6 +86,10 @@ struct GaugeSrc {
   const uint32_t* slot;
   const double* val;
   using P = uint64_t;
+  bool vec16() const { return false; }  // (arrival order kept within a digit)
+  __device__ __forceinline__ void load4(uint64_t, uint32_t*, P*) const {}
+  bool key16() const { return ((uintptr_t)slot & 15u) == 0; }
+  __device__ __forceinline__ uint4 key4(uint64_t i) const { return *reinterpret_cast<const uint4*>(slot + i); }
   __device__ __forceinline__ uint32_t key(uint64_t i) const { return slot[i]; }
   __device__ __forceinline__ void load(uint64_t i, uint32_t& k, uint64_t& p) const {
     k = slot[i];
@@ -81,6 +102,10 @@ struct GaugeSrc {
 struct GaugeIdxSrc {
   const uint32_t* slot;
   using P = uint32_t;
+  bool vec16() const { return false; }  // (arrival order kept within a digit)
+  __device__ __forceinline__ void load4(uint64_t, uint32_t*, P*) const {}
+  bool key16() const { return ((uintptr_t)slot & 15u) == 0; }
+  __device__ __forceinline__ uint4 key4(uint64_t i) const { return *reinterpret_cast<const uint4*>(slot + i); }
   __device__ __forceinline__ uint32_t key(uint64_t i) const { return slot[i]; }
   __device__ __forceinline__ void load(uint64_t i, uint32_t& k, uint32_t& p) const {
     k = slot[i];
@@ -381,7 +406,8 @@ void ingest_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const doubl
         partition_pass(CounterSrc{slot, val, rate}, KPackDst{e->pk, e->pp, shift}, n, shift, *e->side_rs, e->side, rs,
                        16 + 4);
     hipLaunchKernelGGL(k_counter_runs, dim3((uint32_t)((n + kRunChunk - 1) / kRunChunk)), dim3(kRunThreads), 0,
-                       e->side, n, e->pk, e->pp, e->side_rs->offsets, nparts, shift, (uint64_t*)e->cval, e->ctouch);
+                       e->side, n, e->pk, e->pp, partition_bounds(*e->side_rs, nparts), nparts, shift, (uint64_t*)e->cval,
+                       e->ctouch);
     return;
   }
   if (kScalarDirect) {
@@ -414,7 +440,8 @@ void ingest_gauges(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
     const uint32_t nparts =
         partition_pass(GaugeIdxSrc{slot}, KV32Dst{e->pk, pidx}, n, shift, *e->side_rs, e->side, rs, 4 + 8);
     hipLaunchKernelGGL(k_gauge_runs, dim3((uint32_t)((n + kRunChunk - 1) / kRunChunk)), dim3(kRunThreads), 0,
-                       e->side, n, e->pk, pidx, e->side_rs->offsets, nparts, shift, base, e->gseq, e->gtouch);
+                       e->side, n, e->pk, pidx, partition_bounds(*e->side_rs, nparts), nparts, shift, base, e->gseq,
+                       e->gtouch);
     hipLaunchKernelGGL(k_gauge_resolve_direct, dim3(blocks_for(cap, 256)), dim3(256), 0, e->side, cap, base,
                        e->gseq, val, e->gval);
     return;

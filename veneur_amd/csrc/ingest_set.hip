@@ -166,13 +166,23 @@ __global__ void k_set_seg_mark(uint64_t n, const uint64_t* __restrict__ R, uint3
 // profiling build only (tools/set_profile.py): k_set_segments cycles per phase, summed over
 // workgroups: 0 setup, 1 sparse scan, 2 sparse merge, 3 toNormal, 4 dense, 5 write-back,
 // 6 triggers, 7 heavy keys, 8 records of heavy keys, 9 whole workgroups
-__device__ unsigned long long g_set_prof[16];
+__device__ unsigned long long g_set_prof[32];  // 16 + i: workgroup 0 alone (the key with the most records)
 #define SPROF_T(v) const long long v = clock64()
-#define SPROF_ADD(i, a, b) \
-  if (threadIdx.x == 0) atomicAdd(&g_set_prof[i], (unsigned long long)((b) - (a)))
+#define SPROF_ADD(i, a, b)                                                                     \
+  if (threadIdx.x == 0) {                                                                      \
+    atomicAdd(&g_set_prof[i], (unsigned long long)((b) - (a)));                                \
+    if (blockIdx.x == 0) atomicAdd(&g_set_prof[16 + (i)], (unsigned long long)((b) - (a)));    \
+  }
 #define SPROF_INC(i, v) \
   if (threadIdx.x == 0) atomicAdd(&g_set_prof[i], (unsigned long long)(v))
+// the longest workgroup's cycles (slot 14) and its record count (15, the latest such key's)
+#define SPROF_MAX(a, b, nrec)                                                                  \
+  if (threadIdx.x == 0) {                                                                      \
+    const unsigned long long _c = (unsigned long long)((b) - (a));                             \
+    if (atomicMax(&g_set_prof[14], _c) < _c) g_set_prof[15] = (unsigned long long)(nrec);      \
+  }
 #else
+#define SPROF_MAX(a, b, nrec)
 #define SPROF_T(v)
 #define SPROF_ADD(i, a, b)
 #define SPROF_INC(i, v)
@@ -180,6 +190,11 @@ __device__ unsigned long long g_set_prof[16];
 
 constexpr uint32_t kScanStage = 1024;  // records staged in LDS per scan window (a trigger needs ~170)
 constexpr uint32_t kHashSlots = 512;  // LDS open-addressing table for the tmpSet (<= 163 codes)
+#ifndef VN_SET_GROUP
+#define VN_SET_GROUP 1
+#endif
+constexpr bool kSetGroup = VN_SET_GROUP;   // grouped mergeSparse (set_segment)
+constexpr uint32_t kSetGroupCap = 1024;    // pending codes of a group: six triggers' tmpSets
 
 __device__ __forceinline__ uint32_t hslot(uint32_t c) { return (c * 2654435761u) >> 23; }  // 9 bits
 
@@ -262,6 +277,157 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
       hash_insert_par(s_hash, c);
     }
     lds_barrier();
+    // Grouped mergeSparse: the list after triggers k..k+g is the list before them united with
+    // their tmpSets, and its varint byte length only grows as codes are added, so while the
+    // union stays within m no trigger in between reached toNormal -- one merge of the union
+    // (sorted and deduplicated) replaces g of them.  The trigger scan is unchanged.  The pending
+    // codes and the merge's new codes and insertion points live in the top 2 kSetGroup words of
+    // U, above the list and its growth (lc + 3 kSetGroup <= kArenaWords).  A group whose union
+    // passes m is scanned again from its first record with one merge per trigger, so toNormal
+    // comes at the same record as in the reference.  Measured (C4 window, tools/set_profile.py):
+    // see DESIGN.md §5.
+    bool gmode = kSetGroup > 0, gfirst = true;
+    uint32_t np = 0, gpos = 0, plast = 0;
+    uint32_t* const GP = U + kArenaWords - 2 * kSetGroupCap;  // pending codes, then the new ones
+    uint32_t* const GL = U + kArenaWords - kSetGroupCap;      // the new codes' insertion points
+    auto group_flush = [&]() -> bool {
+      if (!list_in_lds) {
+        for (uint32_t i = t; i < s_lc; i += kBlock) U[i] = arena[i];
+        list_in_lds = true;
+        lds_barrier();
+      }
+      // the pending tmpSets are sorted runs of kHllTmpTrigger distinct codes (sorted as they
+      // joined): each code's place in the merged order is its index in its run plus, per other
+      // run, the codes below it there (<= for runs before its own, so ties keep run order)
+      const uint32_t g = np / kHllTmpTrigger;
+      const uint32_t* S = GP;
+      if (g > 1) {
+        for (uint32_t i = t; i < np; i += kBlock) {
+          const uint32_t xc = GP[i], a = i / kHllTmpTrigger;
+          uint32_t rank = i - a * kHllTmpTrigger;
+          for (uint32_t r = 0; r < g; r++) {
+            if (r == a) continue;
+            const uint32_t* run = GP + r * kHllTmpTrigger;
+            uint32_t lo = 0, hi = kHllTmpTrigger;
+            while (lo < hi) {
+              const uint32_t m = (lo + hi) >> 1;
+              const uint32_t v = run[m];
+              if (r < a ? v <= xc : v < xc) lo = m + 1;
+              else hi = m;
+            }
+            rank += lo;
+          }
+          GL[rank] = xc;
+        }
+        lds_barrier();
+        S = GL;
+      }
+      // distinct codes not in the list, in order (four adjacent entries per thread)
+      const uint32_t lc = s_lc;
+      uint32_t code[4], lb[4], cnt = 0;
+      bool nw[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const uint32_t i = 4 * t + q;
+        code[q] = i < np ? S[i] : kHllNoCode;
+        const bool first = i < np && (i == 0 || S[i - 1] != code[q]);
+        lb[q] = first ? lower_bound_u32(U, lc, code[q]) : 0u;
+        nw[q] = first && !(lb[q] < lc && U[lb[q]] == code[q]);
+        cnt += nw[q] ? 1u : 0u;
+      }
+      const uint32_t lane = t & 63, w = t >> 6;
+      uint32_t inc = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(inc, d, 64);
+        if ((int)lane >= d) inc += o;
+      }
+      if (lane == 63) s_red[w] = inc;
+      lds_barrier();
+      uint32_t excl = inc - cnt, nnew = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < 4; i++) {
+        excl += i < w ? s_red[i] : 0u;
+        nnew += s_red[i];
+      }
+      lds_barrier();  // (every pending code read before the new ones overwrite them)
+      {
+        uint32_t r = excl;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++)
+          if (nw[q]) {
+            GP[r] = code[q];
+            GL[r] = lb[q];
+            r++;
+          }
+      }
+      lds_barrier();
+      // the list's varint byte length after the union (as the one-trigger merge below counts it)
+      uint32_t dbytes = 0;
+      {
+        uint32_t r = excl;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++)
+          if (nw[q]) {
+            const uint32_t c = code[q], l = lb[q];
+            const uint32_t predS = l > 0 ? U[l - 1] : 0u, succS = l < lc ? U[l] : 0u;
+            const uint32_t predM = (r > 0 && GL[r - 1] == l) ? GP[r - 1] : predS;
+            dbytes += varint_len(c - predM);
+            const bool last_in_gap = !(r + 1 < nnew && GL[r + 1] == l);
+            if (last_in_gap && l < lc) dbytes += varint_len(succS - c) - varint_len(succS - predS);
+            r++;
+          }
+      }
+      const uint32_t bytes = lbytes + block_allreduce_u32_sum(dbytes, s_red);
+      SPROF_INC(10, 1);
+      SPROF_INC(11, np);
+      if (bytes > kHllM) return false;  // (uniform)
+      constexpr int kPer = (kArenaWords + kBlock - 1) / kBlock;
+      const int jmax = (int)((lc + kBlock - 1) / kBlock);
+      if (jmax <= 8) shift_list_up<8>(U, lc, nnew, GL, jmax, t);
+      else shift_list_up<kPer>(U, lc, nnew, GL, jmax, t);
+      {
+        uint32_t r = excl;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++)
+          if (nw[q]) {
+            U[lb[q] + r] = code[q];
+            r++;
+          }
+      }
+      lds_barrier();
+      lbytes = bytes;
+      list_dirty = true;
+      if (t == 0) s_lc = lc + nnew;
+      np = 0;
+      gpos = plast;
+      gfirst = false;
+      lds_barrier();
+      return true;
+    };
+    // the group's union passed m: its triggers again from its first record, one merge each
+    auto group_fallback = [&]() {
+      SPROF_INC(12, 1);
+      gmode = false;
+      np = 0;
+      for (uint32_t i = t; i < kHashSlots; i += kBlock) {
+        s_hash[i] = kHllNoCode;
+        s_first[i] = 0xffffffffu;
+      }
+      lds_barrier();
+      if (gfirst && t < tc0) {
+        const uint32_t c = x.tmp[(uint64_t)slot * kTmpCap + t];
+        s_tmp[t] = c;
+        hash_insert_par(s_hash, c);
+      }
+      if (t == 0) {
+        s_pos = gpos;
+        s_tc = gfirst ? tc0 : 0u;
+        s_wbase = s_wend = 0;  // (the scan window is staged again from there)
+      }
+      lds_barrier();
+    };
+    for (;;) {
     while (s_pos < n && s_mode == 0) {
       SPROF_T(p_scan0);
       // the records are staged in LDS kScanStage at a time by the whole workgroup (coalesced);
@@ -377,7 +543,39 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
       SPROF_ADD(1, p_scan0, p_scan1);
       if (!s_trig) continue;  // window done without a trigger: the next window, or the end
       SPROF_INC(6, 1);
+      if (gmode) {
+        if (np + kHllTmpTrigger > kSetGroupCap) {
+          SPROF_T(p_g0);
+          const bool ok = group_flush();
+          SPROF_T(p_g1);
+          SPROF_ADD(2, p_g0, p_g1);
+          if (!ok) {
+            group_fallback();
+            continue;
+          }
+        }
+        if (s_lc + 3 * kSetGroupCap <= kArenaWords) {  // this trigger's tmpSet joins the group
+          if (t < kHllTmpTrigger) {  // (sorted by rank: the tmpSet's codes are distinct)
+            const uint32_t mine = s_tmp[t];
+            uint32_t rk = 0;
+            for (uint32_t j = 0; j < kHllTmpTrigger; j++) rk += s_tmp[j] < mine ? 1u : 0u;
+            GP[np + rk] = mine;
+          }
+          np += kHllTmpTrigger;
+          plast = s_pos;
+          if (t == 0) s_tc = 0;
+          for (uint32_t i = t; i < kHashSlots; i += kBlock) {
+            s_hash[i] = kHllNoCode;
+            s_first[i] = 0xffffffffu;
+          }
+          lds_barrier();
+          continue;
+        }
+        // (the list leaves no room for a group: this trigger merges alone, as every later one)
+        gmode = false;
+      }
       // mergeSparse: sorted union of the list and the tmpSet
+      SPROF_INC(13, 1);
       if (!list_in_lds) {
         for (uint32_t i = t; i < s_lc; i += kBlock) U[i] = arena[i];
         list_in_lds = true;
@@ -489,6 +687,18 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
       }
     }
     lds_barrier();
+    if (gmode && np > 0) {  // the triggers pending at the key's last record
+      SPROF_T(p_g0);
+      const bool ok = group_flush();
+      SPROF_T(p_g1);
+      SPROF_ADD(2, p_g0, p_g1);
+      if (!ok) {
+        group_fallback();
+        continue;
+      }
+    }
+    break;
+    }
     if (s_mode == 0) {
       // write back the sparse state
       SPROF_T(p_wb0);
@@ -505,6 +715,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
       SPROF_T(p_wb1);
       SPROF_ADD(5, p_wb0, p_wb1);
       SPROF_ADD(9, p_begin, p_wb1);
+      SPROF_MAX(p_begin, p_wb1, n);
       return;
     }
   } else {
@@ -534,6 +745,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
   SPROF_T(p_end);
   SPROF_ADD(5, p_dense1, p_end);
   SPROF_ADD(9, p_begin, p_end);
+  SPROF_MAX(p_begin, p_end, n);
 }
 
 // One workgroup per touched key; with an order, workgroup i takes the key with the i-th most
@@ -670,10 +882,10 @@ void set_finish(vn_engine* e) {
 }
 
 #ifdef VN_SET_PROF
-extern "C" int vn_prof_set_read(unsigned long long* out16, int reset) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_set_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+extern "C" int vn_prof_set_read(unsigned long long* out32, int reset) {
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_set_prof), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_set_prof), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

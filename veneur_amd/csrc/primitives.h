@@ -38,6 +38,8 @@ struct RadixScratch {
   uint32_t* offsets = nullptr;   // 256 * blocks + 1
   ScanScratch scan;
   size_t blocks_cap = 0;
+  uint32_t* gsum = nullptr;      // partition.h: per (digit, tile group) sums, then their scan
+  size_t gsum_cap = 0;           //   (2 * (256 * groups + 1) words)
 };
 // Sorts n records; ping-pongs between (a0,b0) and (a1,b1).  Returns true if the result
 // ended in (a1, b1).  If timing events are supplied, the scatter kernels are bracketed.

@@ -297,6 +297,7 @@ void radix_scratch_free(RadixScratch& s) {
   if (s.counts) (void)hipFree(s.counts);
   if (s.offsets) (void)hipFree(s.offsets);
   if (s.scan.partials) (void)hipFree(s.scan.partials);
+  if (s.gsum) (void)hipFree(s.gsum);
   s = RadixScratch{};
 }
 
