@@ -1,6 +1,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
 T=r06_r
+VN_LIB=libveneur_amd_setprof.so timeout -k 10 200 python -u tools/set_profile.py > gpurun_out/${T}_setprof_group.log 2>&1 || exit 15
 Q="--no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0"
 S="$Q --worker-windows 0 --sim-world 8 --sim-rank 3 --steps 20 --timing-steps 0"
 for D in 4 6; do for HQ in 16 32; do
