@@ -2735,11 +2735,16 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       if (bad) break;
       // ... their slots and list, and the exact count of every fixed boundary in chunk jf (the
       // means merge jf saw: a slot taken now has rfirst = jf, so mean_before still reads the lists)
-      if (need) B.rlist[lds_inc(&B.rctl[3])] = (uint16_t)i;
+      if (need) {
+        const uint32_t at = lds_inc(&B.rctl[3]);
+        if (!VN_BAD(at < kRepCols, "repair list", at, kRepCols)) B.rlist[at] = (uint16_t)i;
+      }
       if (isnew) {
         const uint32_t sl = lds_inc(&B.ctl[6]);
-        B.rslot[i] = (uint8_t)sl;
-        B.rfirst[sl] = (uint8_t)jf;
+        if (!VN_BAD(sl < kRepCols && i < kBM, "repair slot", sl, i)) {
+          B.rslot[i] = (uint8_t)sl;
+          B.rfirst[sl] = (uint8_t)jf;
+        }
       }
       if (fixc && i >= 2) {
         const uint32_t base = sbase(jf);
@@ -2769,6 +2774,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
           continue;
         }
         const uint32_t c = B.rlist[k], sl = B.rslot[c];
+        if (VN_BAD(c < nm && sl < kRepCols, "repair chain column", c, sl)) continue;
         const uint32_t jl = min(lane, kBB - 1u), tl = tcap - 1u;
         const uint32_t aj = B.nT[c * kRS + jl], ej = B.nT[(c + 1) * kRS + jl], bj = sbase(min(lane, b - 1u));
         double vq[4];

@@ -266,6 +266,7 @@ __global__ __launch_bounds__(kRunThreads) void k_counter_runs(uint64_t n, const 
   const int32_t esc = (int32_t)(0u - (1u << (31 - shift)));  // KPackDst's escape field
   // one packed record (KPackDst): its slot within the bucket and its contribution
   auto unpack = [&](uint64_t r, uint32_t& k, uint64_t& p) {
+    if (VN_BAD(r < n, "counter_runs record", r, n)) r = 0;
     const uint32_t x = pk[r];
     const int32_t f = (int32_t)x >> shift;
     k = x & (W - 1u);
@@ -358,6 +359,8 @@ __global__ __launch_bounds__(kRunThreads) void k_gauge_runs(uint64_t n, const ui
     for (uint32_t j = t; j < W; j += kRunThreads) {
       const uint32_t q = s_last[j];
       if (q) {
+        if (VN_BAD(c0 + q - 1 < n, "gauge_runs position", c0 + q - 1, n)) continue;
+        if (VN_BAD(pidx[c0 + q - 1] < n, "gauge_runs arrival index", pidx[c0 + q - 1], n)) continue;
         atomicMax((unsigned long long*)&gseq[sb + j], (unsigned long long)(base + pidx[c0 + q - 1] + 1));
         gtouch[sb + j] = 1;
       }
@@ -368,12 +371,13 @@ __global__ __launch_bounds__(kRunThreads) void k_gauge_runs(uint64_t n, const ui
 }
 
 // gauges of the direct path: the winning position indexes the caller's value array
-__global__ void k_gauge_resolve_direct(uint32_t cap, uint64_t base, const uint64_t* __restrict__ gseq,
+__global__ void k_gauge_resolve_direct(uint32_t cap, uint64_t base, uint64_t n, const uint64_t* __restrict__ gseq,
                                        const double* __restrict__ val, double* __restrict__ gval) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= cap) return;
   const uint64_t q = gseq[s];
-  if (q > base) gval[s] = val[q - base - 1];
+  if (q > base && !VN_BAD(q - base - 1 < n, "gauge_resolve index", q - base - 1, n)) gval[s] = val[q - base - 1];
+  (void)n;
 }
 
 __global__ void k_gauge_resolve(uint32_t cap, uint64_t base, const uint64_t* __restrict__ gseq,
@@ -442,7 +446,7 @@ void ingest_gauges(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
     hipLaunchKernelGGL(k_gauge_runs, dim3((uint32_t)((n + kRunChunk - 1) / kRunChunk)), dim3(kRunThreads), 0,
                        e->side, n, e->pk, pidx, partition_bounds(*e->side_rs, nparts), nparts, shift, base, e->gseq,
                        e->gtouch);
-    hipLaunchKernelGGL(k_gauge_resolve_direct, dim3(blocks_for(cap, 256)), dim3(256), 0, e->side, cap, base,
+    hipLaunchKernelGGL(k_gauge_resolve_direct, dim3(blocks_for(cap, 256)), dim3(256), 0, e->side, cap, base, n,
                        e->gseq, val, e->gval);
     return;
   }
@@ -450,7 +454,7 @@ void ingest_gauges(vn_engine* e, uint64_t n, const uint32_t* slot, const double*
     hipLaunchKernelGGL(k_scalar_direct<true>, dim3(blocks_for(n, kAggChunk)), dim3(kAggThreads), 0, e->side, n, slot,
                        nullptr, nullptr, base, e->gseq, e->gtouch);
     hipLaunchKernelGGL(k_gauge_resolve_direct, dim3(blocks_for(e->cap[VN_GAUGE], 256)), dim3(256), 0, e->side,
-                       e->cap[VN_GAUGE], base, e->gseq, val, e->gval);
+                       e->cap[VN_GAUGE], base, n, e->gseq, val, e->gval);
     return;
   }
   RadixStats* rs = e->timing ? &e->rstat_c : nullptr;

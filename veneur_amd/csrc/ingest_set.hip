@@ -317,6 +317,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
             }
             rank += lo;
           }
+          if (VN_BAD(rank < np, "set group merge rank", rank, np)) continue;
           GL[rank] = xc;
         }
         lds_barrier();
@@ -356,6 +357,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++)
           if (nw[q]) {
+            if (VN_BAD(r < kSetGroupCap && lb[q] <= lc, "set group new code", r, lb[q])) continue;
             GP[r] = code[q];
             GL[r] = lb[q];
             r++;
@@ -379,6 +381,8 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
           }
       }
       const uint32_t bytes = lbytes + block_allreduce_u32_sum(dbytes, s_red);
+      if (VN_BAD(lc + nnew + 2 * kSetGroupCap <= kArenaWords, "set group list growth", lc + nnew, kArenaWords))
+        return false;
       SPROF_INC(10, 1);
       SPROF_INC(11, np);
       if (bytes > kHllM) return false;  // (uniform)
@@ -559,7 +563,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
             const uint32_t mine = s_tmp[t];
             uint32_t rk = 0;
             for (uint32_t j = 0; j < kHllTmpTrigger; j++) rk += s_tmp[j] < mine ? 1u : 0u;
-            GP[np + rk] = mine;
+            if (!VN_BAD(np + rk < kSetGroupCap, "set group append", np + rk, kSetGroupCap)) GP[np + rk] = mine;
           }
           np += kHllTmpTrigger;
           plast = s_pos;

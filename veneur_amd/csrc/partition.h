@@ -212,6 +212,7 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(Src src, Dst dst, uint6
     if (li_of(j) < tile_n) {
       const uint32_t d = (key[j] >> shift) & 0xffu;
       const uint32_t pos = s_run[w][d] + rank[j];
+      if (VN_BAD(pos < kTile, "part_scatter tile position", pos, kTile)) continue;
       if constexpr (kPack) {
         s_key[pos] = dst.pack((uint64_t)s_glob[d] + (pos - s_loc[d]), key[j], pay[j]);
         s_dig[pos] = (uint8_t)d;
@@ -225,13 +226,17 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(Src src, Dst dst, uint6
   if constexpr (kPack) {
     for (uint32_t li = t; li < tile_n; li += kBlock) {
       const uint32_t d = s_dig[li];
-      dst.key[(uint64_t)s_glob[d] + (li - s_loc[d])] = s_key[li];
+      const uint64_t g = (uint64_t)s_glob[d] + (li - s_loc[d]);
+      if (VN_BAD(g < n, "part_scatter store", g, n)) continue;
+      dst.key[g] = s_key[li];
     }
   } else {
     for (uint32_t li = t; li < tile_n; li += kBlock) {
       uint32_t k = s_key[li];
       uint32_t d = (k >> shift) & 0xffu;
-      dst.store((uint64_t)s_glob[d] + (li - s_loc[d]), k, s_pay[li]);
+      const uint64_t g = (uint64_t)s_glob[d] + (li - s_loc[d]);
+      if (VN_BAD(g < n, "part_scatter store", g, n)) continue;
+      dst.store(g, k, s_pay[li]);
     }
   }
 }

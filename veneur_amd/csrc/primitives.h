@@ -5,6 +5,18 @@
 
 namespace vn {
 
+// Debug builds (VN_DEBUG_CHECKS) guard the indices of the round-6 kernels: a bad one is printed
+// and its access skipped, so a broken invariant is named instead of faulting the GPU.
+#ifdef VN_DEBUG_CHECKS
+__device__ inline bool vn_bad(bool ok, const char* what, unsigned long long a, unsigned long long b) {
+  if (!ok) printf("VN_CHECK %s: %llu vs %llu (block %u thread %u)\n", what, a, b, blockIdx.x, threadIdx.x);
+  return !ok;
+}
+#define VN_BAD(ok, what, a, b) ::vn::vn_bad((ok), (what), (unsigned long long)(a), (unsigned long long)(b))
+#else
+#define VN_BAD(ok, what, a, b) false
+#endif
+
 constexpr int kBlock = 256;               // 4 waves
 constexpr int kItems = 16;                // items per thread in a tile
 constexpr int kTile = kBlock * kItems;    // 4096 records per tile / chunk
