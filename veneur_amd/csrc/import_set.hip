@@ -736,7 +736,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 1))) 
         const uint32_t nt = P.ntmp;
         const uint32_t* pt = s_ptmp;
         const uint32_t* cl = Cb;
-        dense_insert_codes(S, [pt, cl, nt](uint32_t p) { return p < nt ? pt[p] : cl[p - nt]; }, 0, nt + nl, x.err);
+        dense_insert_codes<kItems>(S, [pt, cl, nt](uint32_t p) { return p < nt ? pt[p] : cl[p - nt]; }, 0, nt + nl, x.err);
         __syncthreads();
         IPROF_T(q1);
         IPROF_ADD(6, q0, q1);

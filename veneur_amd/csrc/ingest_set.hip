@@ -191,10 +191,17 @@ __device__ unsigned long long g_set_prof[32];  // 16 + i: workgroup 0 alone (the
 constexpr uint32_t kScanStage = 1024;  // records staged in LDS per scan window (a trigger needs ~170)
 constexpr uint32_t kHashSlots = 512;  // LDS open-addressing table for the tmpSet (<= 163 codes)
 #ifndef VN_SET_GROUP
-#define VN_SET_GROUP 1
+#define VN_SET_GROUP 0
 #endif
 constexpr bool kSetGroup = VN_SET_GROUP;   // grouped mergeSparse (set_segment)
 constexpr uint32_t kSetGroupCap = 1024;    // pending codes of a group: six triggers' tmpSets
+// A heavy key's dense phase streams its codes at one workgroup's memory parallelism (the C4
+// window's largest set key, 5.3M records, is the kernel's critical path): 32 codes per thread
+// per chunk, the next chunk in flight meanwhile
+#ifndef VN_SET_DENSE_ITEMS
+#define VN_SET_DENSE_ITEMS 32
+#endif
+constexpr int kSetDenseItems = VN_SET_DENSE_ITEMS;
 
 __device__ __forceinline__ uint32_t hslot(uint32_t c) { return (c * 2654435761u) >> 23; }  // 9 bits
 
@@ -732,7 +739,7 @@ __device__ __forceinline__ void set_segment(const SetCtx& x, const uint32_t slot
   SPROF_T(p_dense0);
   {
     const DenseLds S{U, &s_b, &s_nz, &s_filled, &s_tfull, &s_pstar, &s_newfill, &s_min, s_red};
-    dense_insert_codes(S, [R](uint32_t p) { return (uint32_t)R[p]; }, s_pos, n, x.err);
+    dense_insert_codes<kSetDenseItems>(S, [R](uint32_t p) { return (uint32_t)R[p]; }, s_pos, n, x.err);
   }
   lds_barrier();
   SPROF_T(p_dense1);

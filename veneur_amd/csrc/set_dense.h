@@ -57,26 +57,30 @@ struct DenseLds {
   uint32_t* red;  // 4
 };
 
-// insert(decode(src(p))) for p in [pos0, n), in order; src(p) -> sparse code (u32)
-template <class Src>
+// insert(decode(src(p))) for p in [pos0, n), in order; src(p) -> sparse code (u32).  DI codes per
+// thread per chunk; the next chunk's codes are loaded while a chunk is processed, so a key's
+// stream runs at one workgroup's memory parallelism: bigger chunks keep more bytes in flight
+// (and take fewer barriers per code)
+template <int DI, class Src>
 __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src& src, uint32_t pos0, uint32_t n,
                                                    uint32_t* err) {
   const uint32_t t = threadIdx.x;
+  constexpr uint32_t kDT = DI * kBlock;  // records per chunk
   uint32_t* U = S.U;
-  uint32_t raw[kItems];
+  uint32_t raw[DI];
   {
     const uint32_t c0 = pos0;
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < DI; j++) {
       uint32_t p = c0 + j * kBlock + t;
       raw[j] = p < n ? src(p) : 0u;
     }
   }
-  for (uint32_t cpos0 = pos0; cpos0 < n; cpos0 += kTile) {
-    const uint32_t cend = min(n, cpos0 + (uint32_t)kTile);
-    uint32_t ri[kItems], rr[kItems];
+  for (uint32_t cpos0 = pos0; cpos0 < n; cpos0 += kDT) {
+    const uint32_t cend = min(n, cpos0 + kDT);
+    uint32_t ri[DI], rr[DI];
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
+    for (int j = 0; j < DI; j++) {
       uint32_t p = cpos0 + j * kBlock + t;
       ri[j] = 0;
       rr[j] = 0;
@@ -84,8 +88,8 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
     }
     // prefetch the next chunk; its latency hides behind this chunk's phases
 #pragma unroll
-    for (int j = 0; j < kItems; j++) {
-      uint32_t p = cpos0 + kTile + j * kBlock + t;
+    for (int j = 0; j < DI; j++) {
+      uint32_t p = cpos0 + kDT + j * kBlock + t;
       raw[j] = p < n ? src(p) : 0u;
     }
     uint32_t cpos = cpos0;
@@ -93,30 +97,48 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
       const uint32_t b = (*S.b);
       uint32_t tfull;
       if ((*S.nz) > 0) {
-        // fast path: mark the zero registers this chunk would fill; if they do not cover
-        // all nz of them, the fill cannot complete here, so no rebase can occur in the
-        // chunk and every update is a plain max
-        if (t == 0) (*S.filled) = 0;
-        lds_barrier();
-#pragma unroll
-        for (int j = 0; j < kItems; j++) {
-          uint32_t p = cpos0 + j * kBlock + t;
-          if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == 0)
-            if (atomicOr(&U[ri[j]], kMark) == 0) atomicAdd(&(*S.filled), 1u);
+        // fast path: if the chunk cannot fill every zero register, no rebase can occur in it and
+        // every update is a plain max.  First bound: a register fills only from a code with
+        // r > b, so fewer such codes than zero registers cannot complete the fill (one wave
+        // ballot count, no LDS pass -- most chunks of a long fill end here); else mark the zero
+        // registers the chunk would fill and count them exactly
+        if (t == 0) {
+          (*S.filled) = 0;
+          (*S.newfill) = 0;
         }
         lds_barrier();
-        const bool completes = (*S.filled) >= (*S.nz);
+        {
+          uint32_t h = 0;
 #pragma unroll
-        for (int j = 0; j < kItems; j++) {
-          uint32_t p = cpos0 + j * kBlock + t;
-          if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
+          for (int j = 0; j < DI; j++) {
+            const uint32_t p = cpos0 + j * kBlock + t;
+            h += (uint32_t)__popcll(__ballot(p >= cpos && p < cend && rr[j] > b));
+          }
+          if ((t & 63) == 0 && h) atomicAdd(&(*S.filled), h);
         }
         lds_barrier();
-        if (!completes) {
-          if (t == 0) (*S.newfill) = 0;
+        bool completes = false;
+        if ((*S.filled) >= (*S.nz)) {
+          if (t == 0) (*S.filled) = 0;
           lds_barrier();
 #pragma unroll
-          for (int j = 0; j < kItems; j++) {
+          for (int j = 0; j < DI; j++) {
+            uint32_t p = cpos0 + j * kBlock + t;
+            if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == 0)
+              if (atomicOr(&U[ri[j]], kMark) == 0) atomicAdd(&(*S.filled), 1u);
+          }
+          lds_barrier();
+          completes = (*S.filled) >= (*S.nz);
+#pragma unroll
+          for (int j = 0; j < DI; j++) {
+            uint32_t p = cpos0 + j * kBlock + t;
+            if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
+          }
+          lds_barrier();
+        }
+        if (!completes) {
+#pragma unroll
+          for (int j = 0; j < DI; j++) {
             uint32_t p = cpos0 + j * kBlock + t;
             if (p >= cpos && p < cend && rr[j] > b) {
               uint32_t old = atomicMax(&U[ri[j]], min(rr[j] - b, kHllCapacity - 1));
@@ -134,7 +156,7 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
         }
         // phase A: mark the first filler of every zero register
 #pragma unroll
-        for (int j = 0; j < kItems; j++) {
+        for (int j = 0; j < DI; j++) {
           uint32_t p = cpos0 + j * kBlock + t;
           if (p >= cpos && p < cend && rr[j] > b) {
             uint32_t v = U[ri[j]];
@@ -144,7 +166,7 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
         lds_barrier();
         // phase B: count first fillers, latest fill position
 #pragma unroll
-        for (int j = 0; j < kItems; j++) {
+        for (int j = 0; j < DI; j++) {
           uint32_t p = cpos0 + j * kBlock + t;
           if (p >= cpos && p < cend && rr[j] > b && U[ri[j]] == (kMark | (0x7fffffffu - p))) {
             atomicAdd(&(*S.filled), 1u);
@@ -154,7 +176,7 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
         lds_barrier();
         tfull = ((*S.filled) == (*S.nz)) ? (*S.tfull) : 0xffffffffu;
 #pragma unroll
-        for (int j = 0; j < kItems; j++) {
+        for (int j = 0; j < DI; j++) {
           uint32_t p = cpos0 + j * kBlock + t;
           if (p >= cpos && p < cend && (U[ri[j]] & kMark)) U[ri[j]] = 0;
         }
@@ -171,7 +193,7 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
       // phase C: first rebase candidate strictly after T_full
       if (tfull != 0xffffffffu) {
 #pragma unroll
-        for (int j = 0; j < kItems; j++) {
+        for (int j = 0; j < DI; j++) {
           uint32_t p = cpos0 + j * kBlock + t;
           bool after = (tfull == 0xfffffffeu) ? true : (p > tfull);
           if (p >= cpos && p < cend && after && ((rr[j] - b) & 0xffu) >= kHllCapacity) atomicMin(&(*S.pstar), p);
@@ -181,7 +203,7 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
       const uint32_t pstar = (*S.pstar);
       // phase D: plain max updates before the rebase point
 #pragma unroll
-      for (int j = 0; j < kItems; j++) {
+      for (int j = 0; j < DI; j++) {
         uint32_t p = cpos0 + j * kBlock + t;
         if (p >= cpos && p < cend && p < pstar && rr[j] > b) {
           uint32_t old = atomicMax(&U[ri[j]], min(rr[j] - b, kHllCapacity - 1));
