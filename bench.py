@@ -646,6 +646,7 @@ def main():
     host_marks = []  # --host-trace: host clock at each call's return (development)
     pipe = InTurn(D)
     lat = []  # per window: host ms from its first call to its flush's return
+    ing = []  # per window: host ms from its first call to its ingest's return (the ingest's own syncs included)
 
     import contextlib
 
@@ -671,6 +672,7 @@ def main():
             if t:
                 t.append(time.perf_counter())
             e.ingest_device(stream.batch)
+        ing.append((time.perf_counter() - ts) * 1e3)
         if t:
             t.append(time.perf_counter())
         if turn is not None and D > 1:
@@ -711,6 +713,7 @@ def main():
         prof_read(prof_buf, 1)
     ctrl.barrier()
     lat.clear()
+    ing.clear()
     t0 = time.perf_counter()
     last = run_windows(args.steps)
     sync()
@@ -733,6 +736,7 @@ def main():
     elapsed = ctrl.max(elapsed)
     rank_ms = ctrl.gather_object(t_rank * 1e3 / args.steps)
     window_latency_ms = ctrl.max(float(np.mean(lat))) if lat else None
+    window_ingest_ms = ctrl.max(float(np.mean(ing))) if ing else None
     last_eng = engines[(args.steps - 1) % D]
     if host_marks:
         log(rank, "[bench] host ms per call (split+ingest_split, ingest, flush; split combine in flush); device ms to main / split ready / split histos / set prefix: %s" %
@@ -867,6 +871,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "window_latency_ms": window_latency_ms,
+        "window_ingest_host_ms": window_ingest_ms,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,

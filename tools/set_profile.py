@@ -29,7 +29,7 @@ def main():
     with V.Engine(caps, percentiles=(0.5,), max_batch_records=n_set + 1, max_batch_member_bytes=n_set * 11 + 64) as e:
         for rep in range(3):
             e.timing_enable(True)
-            buf = (C.c_ulonglong * 32)()
+            buf = (C.c_ulonglong * 40)()
             A.lib.vn_prof_set_read(buf, 1)
             assert A.lib.vn_ingest(e.h, C.byref(batch)) == 0, A.lib.vn_last_error(e.h)
             e.flush_raw()
@@ -43,6 +43,9 @@ def main():
                 print("   %-14s %16d %s" % (nm, v, ("%5.1f%%" % (100.0 * v / tot)) if i < 6 or i == 9 else ""))
             print("   workgroup 0 (the key with the most records):",
                   {NAMES[i]: int(buf[16 + i]) for i in (0, 1, 2, 3, 4, 5, 9)})
+            print("   workgroup 0's dense phase:", dict(zip(("chunks", "passes", "fill cycles", "marking cycles",
+                                                             "full-path cycles", "rebases", "rebase cycles",
+                                                             "chunk-top cycles"), (int(v) for v in buf[32:40]))))
 
 
 if __name__ == "__main__":

@@ -47,6 +47,9 @@ constexpr bool kScalarDirect = true;
 #endif
 constexpr bool kCounterRuns = VN_COUNTER_RUNS;  // k_counter_runs below (else k_scalar_direct)
 constexpr bool kGaugeDirect = false;
+#ifndef VN_PART_V4
+#define VN_PART_V4 1  // counters: 16-byte loads and the order-free rank in k_part_scatter
+#endif
 #ifndef VN_GAUGE_RUNS
 #define VN_GAUGE_RUNS 1
 #endif
@@ -67,7 +70,7 @@ struct CounterSrc {
   }
   // the sums are order-free: four adjacent records per 16-byte load when every array allows it
   bool vec16() const {
-    return ((((uintptr_t)slot) | ((uintptr_t)val) | ((uintptr_t)rate)) & 15u) == 0;
+    return VN_PART_V4 && ((((uintptr_t)slot) | ((uintptr_t)val) | ((uintptr_t)rate)) & 15u) == 0;
   }
   __device__ __forceinline__ void load4(uint64_t i, uint32_t* k, uint64_t* p) const {
     const uint4 s4 = *reinterpret_cast<const uint4*>(slot + i);

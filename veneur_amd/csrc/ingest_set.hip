@@ -195,11 +195,11 @@ constexpr uint32_t kHashSlots = 512;  // LDS open-addressing table for the tmpSe
 #endif
 constexpr bool kSetGroup = VN_SET_GROUP;   // grouped mergeSparse (set_segment)
 constexpr uint32_t kSetGroupCap = 1024;    // pending codes of a group: six triggers' tmpSets
-// A heavy key's dense phase streams its codes at one workgroup's memory parallelism (the C4
-// window's largest set key, 5.3M records, is the kernel's critical path): 32 codes per thread
-// per chunk, the next chunk in flight meanwhile
+// codes per thread per chunk of a key's dense phase (the C4 window's largest set key, 5.3M
+// records, is the kernel's critical path); measured: 32 (twice the bytes in flight, half the
+// barriers per code) 25.5M cycles for that key against 24.1M with 16 (profiles/r06_t_setprof*)
 #ifndef VN_SET_DENSE_ITEMS
-#define VN_SET_DENSE_ITEMS 32
+#define VN_SET_DENSE_ITEMS 16
 #endif
 constexpr int kSetDenseItems = VN_SET_DENSE_ITEMS;
 
@@ -893,11 +893,14 @@ void set_finish(vn_engine* e) {
 }
 
 #ifdef VN_SET_PROF
-extern "C" int vn_prof_set_read(unsigned long long* out32, int reset) {
-  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_set_prof), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+extern "C" int vn_prof_set_read(unsigned long long* out40, int reset) {
+  if (hipMemcpyFromSymbol(out40, HIP_SYMBOL(g_set_prof), sizeof(unsigned long long) * 32) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out40 + 32, HIP_SYMBOL(g_dense_prof), sizeof(unsigned long long) * 8) != hipSuccess)
+    return -1;
   if (reset) {
     unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_set_prof), z, sizeof z) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_dense_prof), z, sizeof(unsigned long long) * 8) != hipSuccess) return -1;
   }
   return 0;
 }

@@ -15,6 +15,22 @@ namespace vn {
 
 constexpr uint32_t kMark = 0x80000000u;
 
+// profiling build only (VN_SET_PROF, tools/set_profile.py): workgroup 0's dense phase by path --
+// 0 chunks, 1 passes, 2 fill-path cycles, 3 exact-marking cycles, 4 full-path cycles (T_full,
+// candidates, plain max), 5 rebases, 6 rebase cycles, 7 chunk-top cycles (decode, prefetch issue)
+#ifdef VN_SET_PROF
+static __device__ unsigned long long g_dense_prof[8];
+#define DPROF_T(v) const long long v = clock64()
+#define DPROF_ADD(i, a, b) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_dense_prof[i], (unsigned long long)((b) - (a)))
+#define DPROF_INC(i) \
+  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&g_dense_prof[i], 1ull)
+#else
+#define DPROF_T(v)
+#define DPROF_ADD(i, a, b)
+#define DPROF_INC(i)
+#endif
+
 // bitonic sort of 256 u32 in LDS, ascending (all 256 threads).  A step with j < 64 pairs lanes of
 // one wave, whose LDS accesses complete in order: unless the next step pairs across waves (j = 64
 // or 128) or the sort ends, it ends with a wave wait instead of a workgroup barrier (6 barriers
@@ -67,16 +83,21 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
   const uint32_t t = threadIdx.x;
   constexpr uint32_t kDT = DI * kBlock;  // records per chunk
   uint32_t* U = S.U;
-  uint32_t raw[DI];
-  {
-    const uint32_t c0 = pos0;
+  // two chunks in flight: chunk k's codes sit in rawA (k even) or rawB (k odd), loaded two
+  // chunks ahead, so a load has two chunks' phases to land in
+  uint32_t rawA[DI], rawB[DI];
+  auto load = [&](uint32_t (&raw)[DI], uint32_t c0) {
 #pragma unroll
     for (int j = 0; j < DI; j++) {
-      uint32_t p = c0 + j * kBlock + t;
+      const uint32_t p = c0 + j * kBlock + t;
       raw[j] = p < n ? src(p) : 0u;
     }
-  }
-  for (uint32_t cpos0 = pos0; cpos0 < n; cpos0 += kDT) {
+  };
+  load(rawA, pos0);
+  load(rawB, pos0 + kDT);
+  auto chunk = [&](uint32_t (&raw)[DI], const uint32_t cpos0) {
+    DPROF_T(d_top);
+    DPROF_INC(0);
     const uint32_t cend = min(n, cpos0 + kDT);
     uint32_t ri[DI], rr[DI];
 #pragma unroll
@@ -86,14 +107,13 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
       rr[j] = 0;
       if (p < cend) decode_hash(raw[j], &ri[j], &rr[j]);
     }
-    // prefetch the next chunk; its latency hides behind this chunk's phases
-#pragma unroll
-    for (int j = 0; j < DI; j++) {
-      uint32_t p = cpos0 + kDT + j * kBlock + t;
-      raw[j] = p < n ? src(p) : 0u;
-    }
+    load(raw, cpos0 + 2 * kDT);  // the chunk after next, into the registers just decoded
     uint32_t cpos = cpos0;
+    DPROF_T(d_loop);
+    DPROF_ADD(7, d_top, d_loop);
     for (;;) {
+      DPROF_T(d_p0);
+      DPROF_INC(1);
       const uint32_t b = (*S.b);
       uint32_t tfull;
       if ((*S.nz) > 0) {
@@ -118,6 +138,7 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
         }
         lds_barrier();
         bool completes = false;
+        DPROF_T(d_m0);
         if ((*S.filled) >= (*S.nz)) {
           if (t == 0) (*S.filled) = 0;
           lds_barrier();
@@ -136,6 +157,8 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
           }
           lds_barrier();
         }
+        DPROF_T(d_m1);
+        DPROF_ADD(3, d_m0, d_m1);
         if (!completes) {
 #pragma unroll
           for (int j = 0; j < DI; j++) {
@@ -148,6 +171,8 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
           lds_barrier();
           if (t == 0) (*S.nz) -= (*S.newfill);
           lds_barrier();
+          DPROF_T(d_f1);
+          DPROF_ADD(2, d_p0, d_f1);
           break;
         }
         if (t == 0) {
@@ -213,7 +238,10 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
       lds_barrier();
       if (t == 0) (*S.nz) -= (*S.newfill);
       lds_barrier();
+      DPROF_T(d_c1);
+      DPROF_ADD(4, d_p0, d_c1);
       if (pstar == 0xffffffffu) break;
+      DPROF_INC(5);
       // rebase at pstar (nz == 0 here): b += min(regs); regs -= min
       if (t == 0) (*S.mn) = 0xffffffffu;
       lds_barrier();
@@ -248,9 +276,15 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
         }
       }
       lds_barrier();
+      DPROF_T(d_r1);
+      DPROF_ADD(6, d_c1, d_r1);
       cpos = pstar + 1;
       if (cpos >= cend) break;
     }
+  };
+  for (uint32_t c = pos0; c < n; c += 2 * kDT) {
+    chunk(rawA, c);
+    if (c + kDT < n) chunk(rawB, c + kDT);
   }
 }
 
