@@ -2708,6 +2708,9 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
     for (; nrep < kRepairs; nrep++) {
       const uint32_t jf = __builtin_amdgcn_readfirstlane(B.ctl[0]);
       if (jf >= b || B.ctl[4]) break;
+      // (the slots taken so far, read before R1a's barrier: R1b's lds_inc on ctl[6] may run in a
+      // faster wave while a slower one still decides `bad` below, and every wave must decide alike)
+      const uint32_t nslot0 = __builtin_amdgcn_readfirstlane(B.ctl[6]);
       PROF_T(q0);
       PROF_ADD(59, 0, (long long)(b - jf));
       // R1 (a thread per column): the columns to re-do (boundary c or c + 1 fixed), counted
@@ -2729,7 +2732,7 @@ __device__ __forceinline__ BatchResult merge_batch(const double delta, const dou
       }
       fast_sync<NW>();
       const uint32_t nneed = __builtin_amdgcn_readfirstlane(B.rctl[0]);
-      const bool bad = B.rctl[2] != 0u || nneed > kRepCols || B.ctl[6] + B.rctl[1] > kRepCols;
+      const bool bad = B.rctl[2] != 0u || nneed > kRepCols || nslot0 + B.rctl[1] > kRepCols;
       PROF_T(q1);
       PROF_ADD(49, q0, q1);
       if (bad) break;

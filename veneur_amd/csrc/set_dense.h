@@ -139,7 +139,9 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
         lds_barrier();
         bool completes = false;
         DPROF_T(d_m0);
-        if ((*S.filled) >= (*S.nz)) {
+        const bool maybe = (*S.filled) >= (*S.nz);  // (every wave reads it before it is reset)
+        if (maybe) {
+          lds_barrier();
           if (t == 0) (*S.filled) = 0;
           lds_barrier();
 #pragma unroll
