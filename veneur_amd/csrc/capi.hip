@@ -120,19 +120,21 @@ void create_impl(vn_engine* e) {
 #ifndef VN_NO_CU_MASK
 #define VN_NO_CU_MASK 0  // (build knob: every stream unmasked -- the profiling runs of DESIGN.md §8)
 #endif
+    e->prio_hi = prio_hi;
+    e->prio_lo = prio_lo;
+    e->rmask = rmask;
     if (VN_NO_CU_MASK || ncu < 64 || hipExtStreamCreateWithCUMask(&e->st2, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&e->st3, (uint32_t)rmask.size(), rmask.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&e->st5, (uint32_t)rmask.size(), rmask.data()) != hipSuccess) {
       (void)hipGetLastError();
-      for (hipStream_t* p : {&e->st2, &e->st3, &e->st5})
+      for (hipStream_t* p : {&e->st2, &e->st5})
         if (*p) {
           (void)hipStreamDestroy(*p);
           *p = nullptr;
         }
       VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st2, hipStreamNonBlocking, prio_lo));
-      VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st3, hipStreamNonBlocking, prio_hi));
       VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st5, hipStreamNonBlocking, prio_hi));
       e->side_cus = ncu;
+      e->rmask.clear();
     }
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork5, hipEventDisableTiming));
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join5, hipEventDisableTiming));
@@ -171,15 +173,7 @@ void create_impl(vn_engine* e) {
   }
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join, hipEventDisableTiming));
-  if (e->reserved_cus)  // (off the reserved CUs too)
-    VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st4, (uint32_t)e->amask.size(), e->amask.data()));
-  else
-    VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st4, hipStreamNonBlocking, prio_hi));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join4, hipEventDisableTiming));
-  if (e->reserved_cus)
-    VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st_ctr, (uint32_t)e->amask.size(), e->amask.data()));
-  else
-    VN_HIP_CHECK(hipStreamCreateWithPriority(&e->st_ctr, hipStreamNonBlocking, prio_hi));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_ctr0, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_ctr1, hipEventDisableTiming));
   VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork3, hipEventDisableTiming));
@@ -881,6 +875,24 @@ void take_decode_error(vn_engine* e) {
     throw DecodeError("malformed import payload");
   }
 }
+// st3 / st4 (the fast mode's fork) and st_ctr (the split counters' combine), at first use
+void ensure_aux_streams(vn_engine* e, bool fork, bool ctr) {
+  auto make = [&](hipStream_t& s, bool replay_mask) {
+    if (s) return;
+    if (e->reserved_cus)
+      VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)e->amask.size(), e->amask.data()));
+    else if (replay_mask && !e->rmask.empty())
+      VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, (uint32_t)e->rmask.size(), e->rmask.data()));
+    else
+      VN_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, e->prio_hi));
+  };
+  if (fork) {
+    make(e->st3, true);
+    make(e->st4, false);
+  }
+  if (ctr) make(e->st_ctr, false);
+}
+
 void side_begin(vn_engine* e) {
   if (e->timing) {  // measured kernels run alone
     e->side = e->st;

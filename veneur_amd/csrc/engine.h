@@ -150,6 +150,12 @@ struct vn_engine {
   hipStream_t st6 = nullptr;     // the reserved CUs (vn_config.replay_reserved_cus), or none
   uint32_t reserved_cus = 0;
   std::vector<uint32_t> amask;   // every CU but the reserved ones
+  // st3, st4 and st_ctr carry work only in the fast mode (the hot keys' fork) and in the split
+  // counters' combine: they are created at first use (ensure_aux_streams), so an exact-mode
+  // engine holds three streams and several engines' active streams do not share the runtime's
+  // hardware queues (GPU_MAX_HW_QUEUES)
+  std::vector<uint32_t> rmask;   // the replay streams' CU mask (empty: unmasked)
+  int prio_hi = 0, prio_lo = 0;
   hipEvent_t ev_join6 = nullptr;
   // set segment merge held back (ingest_device): the grouped set records are merged once the
   // histo path's remainder sort is done, so the long set kernel does not crowd it out

@@ -1419,6 +1419,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
     e->kstat_rp.bytes += 16ull * (n - nremrec) + 40ull * (nreplay + nhot) + 16ull * cent;
   }
   if (fork) {
+    ensure_aux_streams(e, true, false);
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
     VN_HIP_CHECK(hipStreamWaitEvent(e->st4, e->ev_fork3, 0));
     VN_HIP_CHECK(hipStreamWaitEvent(e->st3, e->ev_fork3, 0));
@@ -1487,6 +1488,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   hipLaunchKernelGGL(k_seg_mark, dim3(blocks_for(nremrec, 256)), dim3(256), 0, st, nremrec, PB, e->p_start,
                      e->p_end, nullptr, nullptr);
   if (fork) {
+    ensure_aux_streams(e, true, false);
     VN_HIP_CHECK(hipEventRecord(e->ev_fork3, st));
     if (e->set_pending) {
       VN_HIP_CHECK(hipStreamWaitEvent(e->side, e->ev_fork3, 0));

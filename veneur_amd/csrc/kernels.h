@@ -29,6 +29,7 @@ void import_sets(vn_engine* e, uint64_t n, const uint32_t* slot, const uint64_t*
 // The side stream: work issued between side_begin and side_join runs on e->side, after
 // everything already issued on the main stream; the main stream waits for it at the join.
 void side_begin(vn_engine* e);
+void ensure_aux_streams(vn_engine* e, bool fork, bool ctr);  // st3 / st4 / st_ctr at first use
 void side_join(vn_engine* e);
 // Counter.Sample (samplers.go:132-134) / Counter.Combine (171-183)
 void ingest_counters(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate);
