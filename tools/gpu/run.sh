@@ -16,6 +16,7 @@
 #   c5prof4  the same with HIP's default 4 hardware queues
 #   c5profvar / c5var  the C5 leg with the A/B variant library, under the profiler / alone
 #   pmc      FETCH_SIZE and WRITE_SIZE passes (separate runs) for the replay's HBM traffic
+#   pmcvar   the same with the A/B variant library
 #   c5setprof  k_set_merge cycles per payload kind over the C5 leg (variant built with -DVN_SET_PROF)
 #   setprof  k_set_segments phase cycles (variant library built with -DVN_SET_PROF)
 #   sim-N-R-D  rank R of an N-GPU C4 window alone, D engines in turn (bench.py --sim-world N --sim-rank R)
@@ -83,6 +84,14 @@ for step in "$@"; do
         -- python3 "$GRAFT_REPO_ROOT/bench.py" $A > "$GRAFT_REPO_ROOT/${O}_fetch.log" 2>&1) &&
       (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$GRAFT_REPO_ROOT/${O}_write" -o run \
         -- python3 "$GRAFT_REPO_ROOT/bench.py" $A > "$GRAFT_REPO_ROOT/${O}_write.log" 2>&1) ;;
+    pmcvar)
+      # the pmc passes with the A/B variant library
+      A="--steps 1 --warmup 0 --timing-steps 1 --no-cpu-baseline --pcie-steps 0 --c5-hosts 0 --text-lines 0 --parity-keys 64"
+      VN_LIB=libveneur_amd_variant.so timeout -k 10 300 python bench.py $A > ${O}_pmcvarbench.json 2> ${O}_pmcvarbench.log &&
+      (cd /tmp && VN_LIB=libveneur_amd_variant.so timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+        -d "$GRAFT_REPO_ROOT/${O}_varfetch" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" $A > "$GRAFT_REPO_ROOT/${O}_varfetch.log" 2>&1) &&
+      (cd /tmp && VN_LIB=libveneur_amd_variant.so timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+        -d "$GRAFT_REPO_ROOT/${O}_varwrite" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" $A > "$GRAFT_REPO_ROOT/${O}_varwrite.log" 2>&1) ;;
     hot)
       timeout -k 10 300 python -u -m pytest tests/test_batch_replay_gpu.py -x -q --timeout 150 --timeout-method thread \
         > ${O}_hot_tests.log 2>&1 &&

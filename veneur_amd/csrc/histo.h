@@ -78,6 +78,8 @@ struct ExactCtx {
   double* csv;
   double* csw;
   double* ctw;
+  int tw_sum;  // 1: the one-wave replay sums a chunk's weights itself when they have an order-free sum, and
+               // the chunk sorter writes ctw's first-record slot only for the long keys and the other chunks
   // the batched replay's packed weights (null: no batched replay): per record the exclusive prefix
   // of the chunk's sorted weights (u16) << 16 | |w| (u16); a chunk's first record carries its
   // tempW as the prefix, or 0xffffffff when the chunk cannot be batched (a weight that is not an

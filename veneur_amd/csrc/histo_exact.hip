@@ -1123,7 +1123,9 @@ __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t
   tex = __all(tex) && tempW <= exact_total_limit(tint);
   if (lane == 0) {
     // (the four-wave merge needs exact prefixes only; the batched one integers below 2^16)
-    x.ctw[base] = tex ? tempW : -tempW;
+    // (with tw_sum the one-wave replay sums an exact chunk's weights itself: the slot is read
+    // only by the long replays and for a chunk whose weights have no order-free sum)
+    if (wide || !tex || !x.tw_sum) x.ctw[base] = tex ? tempW : -tempW;
     // (every weight is at least 1, so tempW < 2^16 bounds each weight and prefix below 2^16 too)
     if (x.cpk) x.cpk[base] = tint && tempW < 65536.0 ? (uint32_t)tempW << 16 | (uint32_t)__builtin_fabs(sw[0]) : 0xffffffffu;
   }
@@ -1265,9 +1267,13 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
       np = 0;
     }
   }
-  // pure chunks: pre-sorted by k_exact_chunk_sort; the next one is loaded before each merge
+  // pure chunks: pre-sorted by k_exact_chunk_sort; the next one is loaded before each merge.
+  // With tw_sum a chunk's tempW is the wave's own sum of its weights when they have an
+  // order-free sum (temp_weight's test), so no 8-byte read of a line per chunk; otherwise (and
+  // without tw_sum) the chunk sorter's Add-order sum at the chunk's first record
   if (sp.npure) {
     double cv[TPL], cw[TPL], ctw = 0.0;
+    const bool tw_sum = x.tw_sum != 0;
     auto load = [&](uint32_t c) {
       const uint64_t base = (uint64_t)lo + sp.off0 + (uint64_t)c * tcap;
 #pragma unroll
@@ -1278,7 +1284,25 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
           cw[q] = xcsw[base + t];
         }
       }
-      ctw = __builtin_fabs(xctw[base]);  // (negative: not all weights integers)
+      if (!tw_sum) ctw = __builtin_fabs(xctw[base]);  // (negative: not all weights integers)
+    };
+    auto chunk_weight = [&](uint32_t c) -> double {
+      if (!tw_sum) return ctw;
+      bool ti = true, te = true;
+      double part = 0.0;
+#pragma unroll
+      for (uint32_t q = 0; q < (uint32_t)TPL; q++) {
+        const uint32_t t = q * 64 + lane;
+        if (t < tcap) {
+          const double w = __builtin_fabs(cw[q]);
+          ti &= is_int_weight(w);
+          te &= is_exact_weight(w);
+          part = dadd(part, w);
+        }
+      }
+      const double sum = wave_sum(part);
+      if (__all(te) && sum <= exact_total_limit(__all(ti))) return sum;
+      return __builtin_fabs(xctw[(uint64_t)lo + sp.off0 + (uint64_t)c * tcap]);
     };
     load(0);
     for (uint32_t c = 0; c < sp.npure; c++) {
@@ -1291,7 +1315,7 @@ __device__ __forceinline__ void replay_key(const ExactCtx& x, const uint32_t k) 
           stat(cv[q], __builtin_fabs(cw[q]), cw[q] > 0.0);
         }
       }
-      double tempW = ctw, tpad = 0.0;
+      double tempW = chunk_weight(c), tpad = 0.0;
       hold2(tempW, tpad);
       hold_stats(sw, sxw, srw, mn, mx, dmn, dmx);
       if (c + 1 < sp.npure) load(c + 1);

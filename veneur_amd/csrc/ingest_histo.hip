@@ -1315,7 +1315,10 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.cw0 = e->cw[0];
   xc.cw1 = e->cw[1];
   xc.hpend = e->hpend;
-  xc.spec = 1;
+#ifndef VN_HISTO_SPEC
+#define VN_HISTO_SPEC 1
+#endif
+  xc.spec = VN_HISTO_SPEC;
   xc.hspn = e->hspn;
   xc.hspw = e->hspw;
   xc.hpv = e->hpv;
@@ -1328,6 +1331,10 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   xc.csv = e->h_csv;
   xc.csw = e->h_csw;
   xc.ctw = e->h_tw;
+#ifndef VN_TW_SUM
+#define VN_TW_SUM 1
+#endif
+  xc.tw_sum = VN_TW_SUM;
   xc.cpk = e->h_cpk;
   xc.lstat = e->h_lstat;
 #ifndef VN_NO_CSTAT
