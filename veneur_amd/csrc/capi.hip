@@ -712,7 +712,7 @@ void validate_device_batch(vn_engine* e, const vn_batch* b) {
                        e->cap[VN_HISTO], e->cap[VN_SET], e->h_err + 1);
   }
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 15, e->h_err + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipStreamSynchronize(st));
+  VN_HWAIT(e, 0, VN_HIP_CHECK(hipStreamSynchronize(st)));
   const uint32_t f = e->hf_cnt[15];
   if (f & kBadSlot) throw std::invalid_argument("slot out of range");
   if (f & kBadValue) throw std::invalid_argument("invalid value added");  // merging_digest.go:98-100
@@ -1080,11 +1080,20 @@ int vn_ingest_host(vn_engine* e, const vn_batch* b) {
 int vn_ingest(vn_engine* e, const vn_batch* b) {
   if (!e || !b) return VN_EINVAL;
   return guarded(e, [&] {
+#ifdef VN_HOST_PROF
+    const auto t0 = std::chrono::steady_clock::now();
+    for (double& w : e->host_wait_ms) w = 0.0;
+#endif
     if (over_class_caps(e, b))
       throw std::invalid_argument("batch larger than max_batch_records");
     validate_device_batch(e, b);
     window_open(e, e->st);
     ingest_device(e, b);
+#ifdef VN_HOST_PROF
+    const double tot = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    fprintf(stderr, "[vn_host] %p validate %.2f group %.2f plan %.2f total %.2f ms\n", (void*)e, e->host_wait_ms[0],
+            e->host_wait_ms[1], e->host_wait_ms[2], tot);
+#endif
   });
 }
 

@@ -117,7 +117,20 @@ struct SplitState {
 
 }  // namespace vn
 
+// diagnostics build (VARIANT_FLAGS=-DVN_HOST_PROF): host time of vn_ingest's waits, printed per call
+#ifdef VN_HOST_PROF
+#include <chrono>
+#define VN_HWAIT(e, i, stmt)                                                                                   \
+  do {                                                                                                         \
+    const auto _t0 = std::chrono::steady_clock::now();                                                         \
+    stmt;                                                                                                      \
+    (e)->host_wait_ms[i] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - _t0).count(); \
+  } while (0)
+#else
+#define VN_HWAIT(e, i, stmt) stmt
+#endif
 struct vn_engine {
+  double host_wait_ms[4] = {0.0, 0.0, 0.0, 0.0};  // (VN_HOST_PROF) validation, grouping, plan waits
   vn_config cfg{};
   int device = 0;
   hipStream_t st = nullptr;       // main stream (histos, flush, staging copies)

@@ -35,6 +35,8 @@ __device__ __forceinline__ double tag_weight(uint32_t tag, const double* impw) {
 
 struct ExactCtx {
   uint32_t nkeys;
+  const uint32_t* nkeys_dev;  // (null: nkeys) the live keys' count on the device when nkeys is only an upper
+                              // bound (an ingest that does not wait for the count): keys past it are absent
   uint32_t long_min;  // chunk sorter: every record's ctw / cpk only for keys of at least this many exact records
                       // (the four-wave and batched replays read them; the one-wave replay only a chunk's
                       // first); 0: for every key
@@ -122,8 +124,10 @@ void histo_exact_replay_top(const ExactCtx& x, hipStream_t st_top, uint32_t top)
 void histo_exact_replay_list(const ExactCtx& x, const uint32_t* dev_count, uint32_t max_keys, hipStream_t st);
 // replay list[0..n) longest first: sorts the order into buf0/buf1 (n each) on st and sets x
 // up for histo_exact_replay
+// (n_dev: the device's count of list entries when n is only an upper bound; the order then ends in
+// length-0 entries of key index 0xffffffff, which every replay kernel skips)
 void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* buf0, uint64_t* buf1,
-                       RadixScratch& rs, hipStream_t st);
+                       RadixScratch& rs, hipStream_t st, const uint32_t* n_dev = nullptr);
 // the geometric remainder's rounds (ingest_histo.hip): see the definition
 void histo_rounds(vn_engine* e, const uint32_t* list, uint32_t nkeys, uint32_t maxp, uint64_t nrec, uint32_t nrem,
                   const uint64_t* PA, const uint64_t* PB, uint64_t* MA, uint64_t* MB, const double* impw,

@@ -365,7 +365,11 @@ __device__ double temp_weight(const ldsf64* tw, uint32_t np) {
 // Sort np temps (tv/tw, Add order) into sv/sw as sort.Sort(centroidList) orders them:
 // counting rank over (mean, Add index); when equal means make the order observable
 // (different weights or signed zeros) lane 0 runs Go's quickSort instead.  One wave.
-__device__ __noinline__ void sort_temps(const ldsf64* tv, const ldsf64* tw, ldsf64* sv, ldsf64* sw, uint32_t np) {
+// (ties: Go's sort.Sort itself on one lane -- rare, out of line so the chunk sorter's inlined body
+// keeps a small register budget)
+__device__ __noinline__ void go_sort_lane0(ldsf64* sv, ldsf64* sw, uint32_t np) { GoSortCent{sv, sw}.sort((int)np); }
+__device__ __forceinline__ void sort_temps_body(const ldsf64* tv, const ldsf64* tw, ldsf64* sv, ldsf64* sw,
+                                                uint32_t np) {
   const uint32_t lane = threadIdx.x & 63;
   // Temps made of at most four ascending runs with no value repeated (an imported digest's
   // centroids arrive in ascending order: a chunk of them holds one or two runs): a temp's rank
@@ -436,7 +440,7 @@ __device__ __noinline__ void sort_temps(const ldsf64* tv, const ldsf64* tw, ldsf
       sw[t] = tw[t];
     }
     wave_lds_sync();
-    if (lane == 0) GoSortCent{sv, sw}.sort((int)np);
+    if (lane == 0) go_sort_lane0(sv, sw, np);
   } else {
 #pragma unroll
     for (uint32_t q = 0; q < kMaxTempPerLane; q++)
@@ -446,6 +450,11 @@ __device__ __noinline__ void sort_temps(const ldsf64* tv, const ldsf64* tw, ldsf
       }
   }
   wave_lds_sync();
+}
+// (out of line for the replays' merges; the chunk sorter inlines the body: a call there saved and
+// restored its live registers through the private stack on every chunk)
+__device__ __noinline__ void sort_temps(const ldsf64* tv, const ldsf64* tw, ldsf64* sv, ldsf64* sw, uint32_t np) {
+  sort_temps_body(tv, tw, sv, sw, np);
 }
 
 // mergeAllTemps of the sorted temps L.sv/L.sw (np of them, Add-order weight sum tempW)
@@ -987,11 +996,18 @@ __device__ __forceinline__ uint32_t last_le_u32(const uint32_t* off, uint32_t n,
 
 }  // namespace
 
+#ifndef VN_CHUNK_XCD
+#define VN_CHUNK_XCD 16  // consecutive chunks per XCD (k_exact_chunk_sort); 0: chunk g to block g
+#endif
 // ---- pure-chunk sorter: the contents of every full chunk are known before the replay, so
 // all of them are sorted here in parallel (one wave per chunk), off the replay's critical path.
 __global__ void k_exact_chunk_count(ExactCtx x) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= x.nkeys) return;
+  if (x.nkeys_dev && k >= *x.nkeys_dev) {  // (past the live keys: no chunks, and keys[k] is stale)
+    x.ccnt[k] = 0u;
+    return;
+  }
   const uint32_t nex = x.nex[k];
   x.ccnt[k] = exact_split(x.hpend[x.keys[k]], nex, x.tcap).npure;
 }
@@ -1092,7 +1108,7 @@ __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t
   }
   const double tempW = temp_weight(tw, tcap);
   const bool wide = x.nex[k] >= x.long_min;  // (every record's prefix: a four-wave or batched replay)
-  sort_temps(tv, tw, sv, sw, tcap);
+  sort_temps_body(tv, tw, sv, sw, tcap);
   // for the long replays (replay_key_fast): the exclusive prefix of the sorted |weights| after
   // the first record, the Add-order tempW at it (negated when a weight is not an integer)
   // and for the batched replay (cpk) the same prefix as a u16 beside |w| as a u16, slot 0 carrying
@@ -1140,10 +1156,24 @@ __device__ __forceinline__ bool is_top_key(const ExactCtx& x, uint32_t k, uint32
 }
 
 // every pure chunk (one wave each), skipping the first `top` keys of x.order64 (sorted already)
+// Workgroups are dealt to the 8 XCDs round-robin (block b to XCD b % 8), each XCD with its own L2.
+// Adjacent chunks share the cache lines at their ends (a chunk is 42 records of 8-byte words, not
+// a line multiple), so runs of kChunkRun consecutive chunks go to one XCD, the runs dealt to the
+// XCDs in turn: a line is read and written through one L2 instead of two, and every XCD still
+// sees the whole window's mix of chunks (one contiguous eighth each was measured slower: 7.8
+// against 6.7 ms -- chunks whose ties take Go's sort on one lane cluster by key).  The grid is a
+// multiple of 8 * kChunkRun (histo_exact_chunk_sort)
+constexpr uint32_t kChunkRun = VN_CHUNK_XCD;
 __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x, uint32_t top) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const uint32_t total = x.coff[x.nkeys];
+#if VN_CHUNK_XCD
+  const uint32_t r = blockIdx.x >> 3, q = (r / kChunkRun) * 8u + (blockIdx.x & 7u);
+  const uint32_t g = q * kChunkRun + r % kChunkRun;
+#else
   const uint32_t g = blockIdx.x;
-  if (g >= x.coff[x.nkeys]) return;
+#endif
+  if (g >= total) return;
   uint32_t k, base;
   if (x.cown) {
     const uint64_t o = x.cown[g];
@@ -3577,19 +3607,23 @@ void histo_exact_replay_list(const ExactCtx& x, const uint32_t* dev_count, uint3
 // longest-first order of the listed keys: (0xFFFFFFF - min(nex, 0xFFFFFFF)) << 32 | key index
 // (28 bits of length: a window's hot keys hold millions of samples, and the longest must start first)
 __global__ void k_exact_lpt_keys(uint32_t n, const uint32_t* __restrict__ list, const uint32_t* __restrict__ nex,
-                                 uint64_t* __restrict__ out) {
+                                 uint64_t* __restrict__ out, const uint32_t* __restrict__ n_dev) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (n_dev && i >= *n_dev) {  // length 0 (sorted last), no key
+    out[i] = (uint64_t)0xFFFFFFFu << 32 | 0xFFFFFFFFu;
+    return;
+  }
   const uint32_t k = list[i], c = min(nex[k], 0xFFFFFFFu);
   out[i] = ((uint64_t)(0xFFFFFFFu - c) << 32) | k;
 }
 
 void histo_exact_order(ExactCtx& x, const uint32_t* list, uint32_t n, uint64_t* buf0, uint64_t* buf1,
-                       RadixScratch& rs, hipStream_t st) {
+                       RadixScratch& rs, hipStream_t st, const uint32_t* n_dev) {
   x.order = list;
   x.norder = n;
   if (!n) return;
-  hipLaunchKernelGGL(k_exact_lpt_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, list, x.nex, buf0);
+  hipLaunchKernelGGL(k_exact_lpt_keys, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, list, x.nex, buf0, n_dev);
   RadixPass passes[4];
   const int np = make_passes(passes, false, 32, 28);
   x.order64 = radix_sort(buf0, nullptr, buf1, nullptr, n, passes, np, rs, st, nullptr) ? buf1 : buf0;
@@ -3630,7 +3664,9 @@ void histo_exact_chunk_sort(const ExactCtx& x, hipStream_t st, uint64_t max_chun
     if (top) hipLaunchKernelGGL(k_exact_chunk_sort_top, dim3(kTopSortBlocks, top), dim3(64), sm, st, x);
     return;
   }
-  hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)max_chunks), dim3(64), sm, st, x, top);
+  const uint64_t span = VN_CHUNK_XCD ? 8ull * VN_CHUNK_XCD : 1ull;
+  hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)((max_chunks + span - 1) / span * span)), dim3(64), sm, st, x,
+                     top);
 }
 
 uint32_t histo_exact_top_keys(const ExactCtx& x) {

@@ -513,9 +513,10 @@ __global__ __launch_bounds__(kBlock) void k_finalize(HistoCtx x) {
 }
 
 #endif  // VN_FAST_MODE
-__global__ void k_clear_flags(uint32_t n, const uint32_t* __restrict__ list, uint32_t* __restrict__ flags) {
+__global__ void k_clear_flags(uint32_t n, const uint32_t* __restrict__ list, uint32_t* __restrict__ flags,
+                              const uint32_t* __restrict__ n_dev = nullptr) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < n) flags[list[k]] = 0;
+  if (k < n && (!n_dev || k < *n_dev)) flags[list[k]] = 0;
 }
 
 // raw (arrival-order) keys: A = float64 bits, B = slot<<32 | float32 rate bits
@@ -593,8 +594,22 @@ __global__ void k_histo_plan(uint32_t ntouched, const uint32_t* __restrict__ tl,
                              uint32_t* __restrict__ ex, uint32_t* __restrict__ remflag,
                              uint32_t* __restrict__ replayflag, uint32_t* __restrict__ hotflag,
                              uint32_t* __restrict__ warmflag, uint32_t* __restrict__ hotcnt,
-                             uint32_t* __restrict__ seen0, uint32_t* __restrict__ maxex) {
+                             uint32_t* __restrict__ seen0, uint32_t* __restrict__ maxex,
+                             const uint32_t* __restrict__ nt_dev) {
   uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (nt_dev) {  // ntouched is an upper bound: the keys past the device's count replay nothing
+    const uint32_t live = *nt_dev;
+    if (k < ntouched && k >= live) {
+      ex[k] = 0u;
+      hotcnt[k] = 0u;
+      remflag[k] = 0u;
+      replayflag[k] = 0u;
+      hotflag[k] = 0u;
+      warmflag[k] = 0u;
+      seen0[k] = 0u;
+    }
+    ntouched = min(ntouched, live);
+  }
   // the longest exact part of a replayed (cold or warm) key: the host skips the long-key
   // launches when none reaches their length (one atomic per wave)
   uint32_t mx = 0;
@@ -1203,6 +1218,13 @@ __global__ void k_replay_state(uint32_t n, const uint32_t* __restrict__ ex, unsi
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, v);
 }
 
+#ifndef VN_INGEST_WAITS
+// 1: the histogram plan's two host waits (the default); 0: the wait-free plan of histo_process,
+// measured not better -- C4 at N = 1, four engines: 76.7 against 73.9 ms per window, the ingest's
+// host time 9 against 53 ms but the window's latency 303 against 278 ms: the GPU, not the host, is
+// what the windows in flight wait for
+#define VN_INGEST_WAITS 1
+#endif
 HistoGroups histo_group(vn_engine* e, uint64_t n, const uint32_t* slot, const double* val, const float* rate) {
   HistoGroups g{};
   if (!n) return g;
@@ -1254,8 +1276,15 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   uint64_t* const Bs = g.Bs;
   uint64_t* const Ao = g.Ao;
   uint64_t* const Bo = g.Bo;
-  VN_HIP_CHECK(hipStreamSynchronize(st));
-  const uint32_t ntouched = e->hf_cnt[0];
+  // Without the fast mode every touched key replays exactly (no hot or warm keys, no remainder):
+  // the host then needs no count from the device -- the launches can be sized by an upper bound
+  // (the touched keys are at most min(n, capacity)) and read the device's counts, so the call
+  // queues the whole path without waiting (VN_INGEST_WAITS 0; the timing mode keeps the waits,
+  // its byte counts need the sizes).
+  const bool async = !VN_FAST_MODE && !e->timing && !VN_INGEST_WAITS;
+  if (!async) VN_HWAIT(e, 1, VN_HIP_CHECK(hipStreamSynchronize(st)));
+  const uint32_t ntouched = async ? (uint32_t)std::min<uint64_t>(n, e->cap[VN_HISTO]) : e->hf_cnt[0];
+  const uint32_t* const nt_dev = async ? e->h_cnt : nullptr;  // (histo_group's touched count)
   if (!ntouched) return;
 
   // ---- 2. plan: exact part of every key (cold / warm / hot, k_histo_plan); the remainders
@@ -1264,7 +1293,12 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   VN_HIP_CHECK(hipMemsetAsync(e->h_cnt + 20, 0, sizeof(uint32_t), st));
   hipLaunchKernelGGL(k_histo_plan, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_start,
                      e->h_end, e->hseen, e->exact_threshold, e->hot_prefix, e->h_ex, remflag, e->h_coldflag,
-                     e->h_vhflag, e->h_warmflag, e->h_hotcnt, e->h_seen0, e->h_cnt + 20);
+                     e->h_vhflag, e->h_warmflag, e->h_hotcnt, e->h_seen0, e->h_cnt + 20, nt_dev);
+  if (async) compact_flags(e->h_coldflag, e->h_pos, e->h_coldlist, e->h_cnt + 6, ntouched, e->ss, st);
+  uint32_t nhot = 0, npieces = 0, maxp_hot = 0, maxp_warm = 0, maxp_hot_left = 0, nwarm = 0;
+  uint64_t nremrec = 0;
+  uint32_t nreplay = ntouched, maxex = 0xFFFFFFFFu;  // (async: upper bounds; the device holds the counts)
+  if (!async) {
   compact_flags(e->h_vhflag, e->h_pos, e->h_hotlist, e->h_cnt + 1, ntouched, e->ss, st);
   compact_flags(e->h_warmflag, e->h_pos, e->h_warmlist, e->h_cnt + 8, ntouched, e->ss, st);
   compact_flags(e->h_coldflag, e->h_pos, e->h_coldlist, e->h_cnt + 6, ntouched, e->ss, st);
@@ -1282,21 +1316,23 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 7, e->h_cnt + 8, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 11, e->h_cnt + 11, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   VN_HIP_CHECK(hipMemcpyAsync(e->hf_cnt + 13, e->h_cnt + 20, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  VN_HIP_CHECK(hipStreamSynchronize(st));
-  const uint32_t nhot = e->hf_cnt[1];
-  const uint64_t nremrec = e->hf_cnt[2];  // remainder records of warm and hot keys
-  const uint32_t npieces = e->hf_cnt[3];
-  const uint32_t maxp_hot = e->hf_cnt[4];
-  const uint32_t maxp_warm = e->hf_cnt[5];
-  const uint32_t maxp_hot_left = e->hf_cnt[11];  // after the fused launch of the leading pieces
-  const uint32_t nreplay = e->hf_cnt[6];  // cold + warm keys
-  const uint32_t nwarm = e->hf_cnt[7];
-  const uint32_t maxex = e->hf_cnt[13];  // longest exact part of a cold or warm key
+  VN_HWAIT(e, 2, VN_HIP_CHECK(hipStreamSynchronize(st)));
+  nhot = e->hf_cnt[1];
+  nremrec = e->hf_cnt[2];  // remainder records of warm and hot keys
+  npieces = e->hf_cnt[3];
+  maxp_hot = e->hf_cnt[4];
+  maxp_warm = e->hf_cnt[5];
+  maxp_hot_left = e->hf_cnt[11];  // after the fused launch of the leading pieces
+  nreplay = e->hf_cnt[6];  // cold + warm keys
+  nwarm = e->hf_cnt[7];
+  maxex = e->hf_cnt[13];  // longest exact part of a cold or warm key
+  }
 
   // ---- 3. exact replay of MergingDigest.Add (histo_exact.hip): every pure chunk pre-sorted,
   // then the cold and warm keys on the replay stream, the hot keys' prefixes on their own
   ExactCtx xc{};
   xc.nkeys = ntouched;
+  xc.nkeys_dev = nt_dev;
   xc.keys = e->h_tl;
   xc.start = e->h_start;
   xc.nex = e->h_ex;
@@ -1367,7 +1403,7 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   // four waves each on st5 (replay_key_fast: built for one merge's latency), beside the one-wave
   // replay of the rest on the same CUs
   auto replay_cold = [&](hipStream_t s, RadixScratch& rs) {
-    histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s);  // longest first
+    histo_exact_order(xc, e->h_coldlist, nreplay, e->h_lpt0, e->h_lpt1, rs, s, async ? e->h_cnt + 6 : nullptr);
     const uint32_t min_len = long_min;
     const bool longk = maxex >= min_len && histo_exact_count_long(xc, min_len, e->h_cnt + 15, s);
     const bool side5 = longk && !e->timing && e->st5;
@@ -1445,7 +1481,8 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
   // stay with the replay)
   if (nremrec == 0) {
     set_finish(e);
-    hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt);
+    hipLaunchKernelGGL(k_clear_flags, dim3(blocks_for(ntouched, 256)), dim3(256), 0, st, ntouched, e->h_tl, e->h_bt,
+                       nt_dev);
     return;
   }
 #if !VN_FAST_MODE
