@@ -123,6 +123,15 @@ void create_impl(vn_engine* e) {
     e->prio_hi = prio_hi;
     e->prio_lo = prio_lo;
     e->rmask = rmask;
+#ifndef VN_ST_FULLMASK
+#define VN_ST_FULLMASK 0  // (A/B build knob: the main stream CU-masked to every CU, i.e. a queue of its own)
+#endif
+    if (VN_ST_FULLMASK && ncu >= 64) {
+      std::vector<uint32_t> fmask((ncu + 31) / 32, 0u);
+      for (uint32_t i = 0; i < ncu; i++) fmask[i / 32] |= 1u << (i % 32);
+      VN_HIP_CHECK(hipStreamDestroy(e->st));
+      VN_HIP_CHECK(hipExtStreamCreateWithCUMask(&e->st, (uint32_t)fmask.size(), fmask.data()));
+    }
     if (VN_NO_CU_MASK || ncu < 64 || hipExtStreamCreateWithCUMask(&e->st2, (uint32_t)mask.size(), mask.data()) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&e->st5, (uint32_t)rmask.size(), rmask.data()) != hipSuccess) {
       (void)hipGetLastError();
@@ -136,9 +145,17 @@ void create_impl(vn_engine* e) {
       e->side_cus = ncu;
       e->rmask.clear();
     }
+#ifndef VN_SIDE_MAIN
+#define VN_SIDE_MAIN 0  // (A/B build knob: counters, gauges and sets on the main stream, no side stream)
+#endif
+    if (VN_SIDE_MAIN && e->st2) {
+      VN_HIP_CHECK(hipStreamDestroy(e->st2));
+      e->st2 = nullptr;
+    }
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_fork5, hipEventDisableTiming));
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_join5, hipEventDisableTiming));
     VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_rest5, hipEventDisableTiming));
+    VN_HIP_CHECK(hipEventCreateWithFlags(&e->ev_bulk, hipEventDisableTiming));
     // vn_config.replay_reserved_cus: the longest batched replays (one workgroup each, hundreds of
     // ms, latency-bound at one wave per SIMD) on the last CUs, which every other stream of the
     // engine leaves alone -- the other windows' sorts and scatters no longer share those CUs'
@@ -531,7 +548,7 @@ void destroy_impl(vn_engine* e) {
     (void)hipEventDestroy(e->ev_join6);
     e->ev_join6 = nullptr;
   }
-  for (hipEvent_t* ev : {&e->ev_fork5, &e->ev_join5, &e->ev_rest5})
+  for (hipEvent_t* ev : {&e->ev_fork5, &e->ev_join5, &e->ev_rest5, &e->ev_bulk})
     if (*ev) {
       (void)hipEventDestroy(*ev);
       *ev = nullptr;
@@ -894,7 +911,7 @@ void ensure_aux_streams(vn_engine* e, bool fork, bool ctr) {
 }
 
 void side_begin(vn_engine* e) {
-  if (e->timing) {  // measured kernels run alone
+  if (e->timing || !e->st2) {  // measured kernels run alone (or VN_SIDE_MAIN: one stream)
     e->side = e->st;
     e->side_rs = &e->rs;
     e->side_ss = &e->ss;

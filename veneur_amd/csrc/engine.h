@@ -158,6 +158,7 @@ struct vn_engine {
   // long-key replay stream (CU mask of st3): the longest keys' four-wave replays
   hipStream_t st5 = nullptr;
   hipEvent_t ev_fork5 = nullptr, ev_join5 = nullptr, ev_rest5 = nullptr;
+  hipEvent_t ev_bulk = nullptr;  // the short keys' replays done on the side stream (VN_BULK_SIDE)
   // the few longest batched replays on CUs no other stream uses (null: st5 takes them all)
   uint32_t ev_rec = 0;           // timing: which of ev[0..4] this window recorded
   hipStream_t st6 = nullptr;     // the reserved CUs (vn_config.replay_reserved_cus), or none

@@ -406,7 +406,7 @@ void flush_all(vn_engine* e, vn_flush_result* out, const uint8_t* histo_qmask, c
   // copies run on the side stream at once.  The sets' estimates run first on the main stream
   // (all CUs, ~0.15 ms), their copies then follow on the side stream while the main stream
   // flushes the histograms and copies their (larger) results.
-  hipStream_t s2 = e->timing ? st : e->st2;
+  hipStream_t s2 = e->timing || !e->st2 ? st : e->st2;
   for (int c : {0, 1})
     if (n[c])
       VN_HIP_CHECK(hipMemcpyAsync(e->hf_list[c], e->f_list[c], n[c] * sizeof(uint32_t), hipMemcpyDeviceToHost, s2));

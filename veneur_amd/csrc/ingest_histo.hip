@@ -1218,6 +1218,10 @@ __global__ void k_replay_state(uint32_t n, const uint32_t* __restrict__ ex, unsi
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, v);
 }
 
+#ifndef VN_BULK_SIDE
+#define VN_BULK_SIDE 0
+#endif
+constexpr bool kBulkSide = VN_BULK_SIDE != 0;
 #ifndef VN_INGEST_WAITS
 // 1: the histogram plan's two host waits (the default); 0: the wait-free plan of histo_process,
 // measured not better -- C4 at N = 1, four engines: 76.7 against 73.9 ms per window, the ingest's
@@ -1436,10 +1440,23 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
       VN_HIP_CHECK(hipEventRecord(e->ev_fork5, s));
       VN_HIP_CHECK(hipStreamWaitEvent(e->st5, e->ev_fork5, 0));
       if (e->st6) VN_HIP_CHECK(hipStreamWaitEvent(e->st6, e->ev_fork5, 0));
-      histo_exact_replay_long(xc, e->st5, s, e->st6);
+      // (VN_BULK_SIDE: the other keys' replays -- throughput work that ends long before the
+      // chain -- on the low-priority side stream, so the next windows' ingest fronts on their
+      // high-priority main streams do not queue behind them)
+      const bool bulk = kBulkSide && e->st2 && e->ev_bulk;
+      hipStream_t sb = s;
+      if (bulk) {
+        VN_HIP_CHECK(hipStreamWaitEvent(e->st2, e->ev_fork5, 0));
+        sb = e->st2;
+      }
+      histo_exact_replay_long(xc, e->st5, sb, e->st6);
       VN_HIP_CHECK(hipEventRecord(e->ev_join5, e->st5));
       if (e->st6) VN_HIP_CHECK(hipEventRecord(e->ev_join6, e->st6));
-      histo_exact_replay(xc, s);
+      histo_exact_replay(xc, sb);
+      if (bulk) {
+        VN_HIP_CHECK(hipEventRecord(e->ev_bulk, e->st2));
+        VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_bulk, 0));
+      }
       VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join5, 0));
       if (e->st6) VN_HIP_CHECK(hipStreamWaitEvent(s, e->ev_join6, 0));
     } else {

@@ -77,15 +77,26 @@ struct DenseLds {
 // thread per chunk; the next chunk's codes are loaded while a chunk is processed, so a key's
 // stream runs at one workgroup's memory parallelism: bigger chunks keep more bytes in flight
 // (and take fewer barriers per code)
+#ifndef VN_SET_DENSE_BUFS
+// chunks of codes in flight in the dense phase (2 or 3).  Three measured not better: the heavy
+// key's workgroup 7.66 ms either way, C4 74.4 / 73.7 ms per window with two against 74.7 / 75.2
+// with three (profiles/r06_sets/)
+#define VN_SET_DENSE_BUFS 2
+#endif
 template <int DI, class Src>
 __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src& src, uint32_t pos0, uint32_t n,
                                                    uint32_t* err) {
   const uint32_t t = threadIdx.x;
   constexpr uint32_t kDT = DI * kBlock;  // records per chunk
   uint32_t* U = S.U;
-  // two chunks in flight: chunk k's codes sit in rawA (k even) or rawB (k odd), loaded two
-  // chunks ahead, so a load has two chunks' phases to land in
+  // kBufs chunks in flight: chunk k's codes sit in buffer k % kBufs, loaded kBufs chunks ahead,
+  // so a load has that many chunks' phases to land in (a heavy key's workgroup is otherwise bound
+  // by its loads' latency: round 6, two buffers, ~5.2k cycles per 4096-code chunk waiting at the top)
+  constexpr uint32_t kBufs = VN_SET_DENSE_BUFS >= 3 ? 3u : 2u;
   uint32_t rawA[DI], rawB[DI];
+#if VN_SET_DENSE_BUFS >= 3
+  uint32_t rawC[DI];
+#endif
   auto load = [&](uint32_t (&raw)[DI], uint32_t c0) {
 #pragma unroll
     for (int j = 0; j < DI; j++) {
@@ -95,6 +106,9 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
   };
   load(rawA, pos0);
   load(rawB, pos0 + kDT);
+#if VN_SET_DENSE_BUFS >= 3
+  load(rawC, pos0 + 2 * kDT);
+#endif
   auto chunk = [&](uint32_t (&raw)[DI], const uint32_t cpos0) {
     DPROF_T(d_top);
     DPROF_INC(0);
@@ -107,7 +121,7 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
       rr[j] = 0;
       if (p < cend) decode_hash(raw[j], &ri[j], &rr[j]);
     }
-    load(raw, cpos0 + 2 * kDT);  // the chunk after next, into the registers just decoded
+    load(raw, cpos0 + kBufs * kDT);  // kBufs chunks ahead, into the registers just decoded
     uint32_t cpos = cpos0;
     DPROF_T(d_loop);
     DPROF_ADD(7, d_top, d_loop);
@@ -284,9 +298,12 @@ __device__ __forceinline__ void dense_insert_codes(const DenseLds& S, const Src&
       if (cpos >= cend) break;
     }
   };
-  for (uint32_t c = pos0; c < n; c += 2 * kDT) {
+  for (uint32_t c = pos0; c < n; c += kBufs * kDT) {
     chunk(rawA, c);
     if (c + kDT < n) chunk(rawB, c + kDT);
+#if VN_SET_DENSE_BUFS >= 3
+    if (c + 2 * kDT < n) chunk(rawC, c + 2 * kDT);
+#endif
   }
 }
 

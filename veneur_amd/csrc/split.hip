@@ -1297,7 +1297,7 @@ void split_flush(vn_engine* e) {
   if (!S.slot[VN_COUNTER].empty()) {
     // on their own stream, after the window's counter aggregation (the side stream's work so
     // far), then the main stream waits for them: not behind this window's long replays
-    hipStream_t src = e->timing ? e->st : e->st2;
+    hipStream_t src = e->timing || !e->st2 ? e->st : e->st2;
     ensure_aux_streams(e, false, true);
     split_counter_owners(e, e->st_ctr);  // (before the wait: the stream is idle)
     VN_HIP_CHECK(hipEventRecord(e->ev_ctr0, src));
