@@ -123,8 +123,14 @@ void create_impl(vn_engine* e) {
     e->prio_hi = prio_hi;
     e->prio_lo = prio_lo;
     e->rmask = rmask;
+// The main stream CU-masked to every CU: a CU-masked stream gets a hardware queue of its own,
+// where an unmasked one shares one of the GPU_MAX_HW_QUEUES with other streams -- with several
+// engines in turn an engine's ingest front then sat in one in-order queue behind another
+// window's 170 ms chain.  Measured: C4 at N = 1, 74.2 -> 71.7 ms per window at
+// four engines, 71.4 / 72.4 at five / six (96 / 92 before); the N = 8 owner's share 45.9 ms at
+// four engines, 36.1 at six (profiles/r06_streams/).  (It gives up the high queue priority.)
 #ifndef VN_ST_FULLMASK
-#define VN_ST_FULLMASK 0  // (A/B build knob: the main stream CU-masked to every CU, i.e. a queue of its own)
+#define VN_ST_FULLMASK 1
 #endif
     if (VN_ST_FULLMASK && ncu >= 64) {
       std::vector<uint32_t> fmask((ncu + 31) / 32, 0u);
