@@ -2,7 +2,8 @@
 digest, compared as whole digests: the GobEncode of every key (merging_digest.go:361-380, pending
 temps merged first) byte for byte, plus the quantiles.
 
-Keys of >= 65536 samples take the batched kernel (kBatchMinLen).  The distributions aim at its
+Keys of >= 262144 samples in one ingest call take the batched kernel (kBatchMinLen); every key
+below carries at least that many per call.  The distributions aim at its
 special paths:
   * lognormal with C4's rate mix -- the steady state (flips restart a batch);
   * a falling trend -- a new minimum in most chunks: Z temps before main 0 that start the first
@@ -106,7 +107,7 @@ def _check(kinds, n, seed, batches):
 
 @pytest.mark.parametrize("batches", [1, 3])
 def test_batched_replay_whole_digest_bit_exact(batches):
-    _check(["lognormal", "falling", "rising", "ints", "seven", "heavy"], 300_000, 11 + batches, batches)
+    _check(["lognormal", "falling", "rising", "ints", "seven", "heavy"], 300_000 * batches, 11 + batches, batches)
 
 
 def test_weights_past_2_30_with_non_integer_weights_bit_exact():
@@ -139,7 +140,7 @@ def test_replay_state_after_every_call_bit_exact(calls):
     the out-of-line four-wave merge that this first merge used to take halved the centroids of
     continuing keys (tools/probe/repro_batch3_calls.py)."""
     kinds = ["lognormal", "falling", "rising", "ints", "seven", "heavy"]
-    slot, val, rate, nk = _stream(kinds, 300_000, 11 + calls)
+    slot, val, rate, nk = _stream(kinds, 300_000 * calls, 11 + calls)
     wts = (np.float32(1.0) / rate).astype(np.float64)
     cuts = np.linspace(0, len(slot), calls + 1).astype(int)
     with V.Engine((1, 1, nk, 1), percentiles=PCT, max_batch_records=len(slot) + 1) as e:
