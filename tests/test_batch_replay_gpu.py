@@ -124,12 +124,12 @@ def test_batched_replay_one_long_key_bit_exact():
 
 
 def test_four_wave_replay_new_last_centroid_bit_exact():
-    """Keys of 20k-40k samples take the four-wave replay (merge_fast).  A rising stream piles its
-    temps past the last main centroid until they must start one of their own: the predicted chain
-    ("every temp joins the centroid before it") has to be checked against the last element even
-    when no later start exists (a bug found by the whole-digest comparison in round 4)."""
-    _check(["rising", "rising", "falling", "lognormal"], 25_362, 1, 1)
-    _check(["rising"] * 3, 37_000, 2, 2)
+    """Keys of 65536-262143 samples per call take the four-wave replay (merge_fast).  A rising
+    stream piles its temps past the last main centroid until they must start one of their own: the
+    predicted chain ("every temp joins the centroid before it") has to be checked against the last
+    element even when no later start exists (a bug found by the whole-digest comparison in round 4)."""
+    _check(["rising", "rising", "falling", "lognormal"], 81_362, 1, 1)
+    _check(["rising"] * 3, 150_000, 2, 2)
 
 
 @pytest.mark.parametrize("calls", [2, 3])

@@ -1218,6 +1218,10 @@ __global__ void k_replay_state(uint32_t n, const uint32_t* __restrict__ ex, unsi
   if ((threadIdx.x & 63) == 0 && v) atomicAdd(out, v);
 }
 
+#ifndef VN_LONG_MIN_EXACT
+#define VN_LONG_MIN_EXACT 65536u
+#endif
+constexpr uint32_t kLongMinExact = VN_LONG_MIN_EXACT;  // exact mode: keys replaying this many samples take four waves
 #ifndef VN_BULK_SIDE
 #define VN_BULK_SIDE 0
 #endif
@@ -1382,8 +1386,13 @@ void histo_process(vn_engine* e, uint64_t n, const HistoGroups& g, const double*
 #endif
   const uint64_t max_chunks = n / e->temp_cap + 1;
   // the four-wave replay's threshold (replay_cold below): shorter keys take the one-wave replay
+  // (exact mode: 65536 -- the short keys' one-wave replays fill the GPU with small workgroups,
+  // where each four-wave one holds a larger share of a CU; C4 at N = 1 62.2 / 62.6 -> 59.9 / 60.2
+  // ms per window against 8192, 32768: 60.5 / 60.8, 131072: 60.2 / 60.1; profiles/r06_longreplay/)
   const uint32_t long_min =
-      e->long_replay ? e->long_replay : std::min<uint32_t>(std::max<uint32_t>(e->exact_threshold / 4, 1024u), 8192u);
+      e->long_replay ? e->long_replay
+      : e->exact_threshold == 0xFFFFFFFFu ? kLongMinExact
+                                          : std::min<uint32_t>(std::max<uint32_t>(e->exact_threshold / 4, 1024u), 8192u);
   xc.long_min = long_min;
   // (exact mode, no hot key, not timing: the longest keys' chunks are sorted first and their
   // replays start while the other chunks sort, in replay_cold)
