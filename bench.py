@@ -511,9 +511,9 @@ def main():
     ap.add_argument("--pipeline", type=int, default=0,
                     help="engines per GPU taking the windows in turn (window i + 1 ingested and combined while "
                          "window i's longest replays finish; one communicator per engine, the combines entered in "
-                         "window order); 1: one engine, windows back to back; 0 (default): 4 at N = 1, 7 beyond (C4 at N = 1 "
-                         "62.1 / 61.3 / 60.6 ms per window at 4 / 5 / 6, 75.3 at 3 -- six full-size engines leave no room "
-                         "for the PCIe leg's staging; the hottest key's rank at N = 2 / 4 / 8 36.2 / 31.5 / 29.3 ms with "
+                         "window order); 1: one engine, windows back to back; 0 (default): 5 at N = 1, 7 beyond (the whole "
+                         "C4 bench at N = 1: 60.2 / 56.9 / 56.4 ms per window at 4 / 5 / 6 engines, the C5 leg beside six "
+                         "slower, 166 against 142 ms; the hottest key's rank at N = 2 / 4 / 8 35.6 / 31.0 / 29.0 ms with "
                          "7 engines against 52.4 / 47.9 / 45.7 with 4, DESIGN.md §6)")
     ap.add_argument("--reserved-cus", type=int, default=0,
                     help="CUs kept for the longest exact replays (vn_config.replay_reserved_cus); 0 (default): none")
@@ -616,7 +616,7 @@ def main():
     # interval.  Flushes are entered in window order, so every rank issues the split combine's
     # collectives (one communicator per engine) in the same order.
     nw = args.sim_world if sim else world
-    D = max(1, args.pipeline if args.pipeline > 0 else (4 if nw <= 1 else 7))
+    D = max(1, args.pipeline if args.pipeline > 0 else (5 if nw <= 1 else 7))
 
     # (measured, DESIGN.md §4: the reservation costs the other windows more than it gains)
     reserved = max(0, args.reserved_cus)

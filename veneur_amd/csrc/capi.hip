@@ -95,6 +95,9 @@ void check_slots_host(const uint32_t* slot, uint64_t n, uint32_t cap, const char
 #endif
 void create_impl(vn_engine* e) {
   VN_HIP_CHECK(hipSetDevice(e->device));
+  // the fast mode's remainder buffers (sort ping-pong, piece ranges, segment compression): none
+  // in the exact-only build -- about 10 GB per engine at C4, room for more engines in turn
+  constexpr bool kFm = VN_FAST_MODE != 0;
   // the histo path (main and replay streams) is the critical path: it gets the high queue
   // priority, the side stream's counters / gauges / sets fill whatever CUs it leaves
   int prio_lo = 0, prio_hi = 0;
@@ -112,7 +115,10 @@ void create_impl(vn_engine* e) {
     VN_HIP_CHECK(hipGetDeviceProperties(&prop, e->device));
     const uint32_t ncu = (uint32_t)prop.multiProcessorCount;
     std::vector<uint32_t> mask((ncu + 31) / 32, 0u), rmask((ncu + 31) / 32, 0u);
-    for (uint32_t i = 0; i < ncu - ncu / 4; i++) mask[i / 32] |= 1u << (i % 32);
+#ifndef VN_SIDE_ALL
+#define VN_SIDE_ALL 0  // (A/B build knob: the side stream's mask over every CU)
+#endif
+    for (uint32_t i = 0; i < (VN_SIDE_ALL ? ncu : ncu - ncu / 4); i++) mask[i / 32] |= 1u << (i % 32);
     // the replay streams' share in eighths of the CUs (bits [0, n/8 ncu): whole shader-engine
     // columns of every XCC, as above)
     for (uint32_t i = 0; i < ncu * VN_REPLAY_EIGHTHS / 8; i++) rmask[i / 32] |= 1u << (i % 32);
@@ -236,21 +242,21 @@ void create_impl(vn_engine* e) {
   e->h_sort_cap = ch ? R + touch_max * capc : 0;
   dalloc(e->hA0, e->h_sort_cap); dalloc(e->hB0, e->h_sort_cap);
   dalloc(e->hA1, e->h_sort_cap); dalloc(e->hB1, e->h_sort_cap);
-  dalloc(e->h_w, e->h_sort_cap);
-  dalloc(e->h_wk, e->h_sort_cap);
+  dalloc(e->h_w, kFm ? e->h_sort_cap : 0);
+  dalloc(e->h_wk, kFm ? e->h_sort_cap : 0);
   dalloc(e->h_start, ch);
   dalloc(e->h_end, ch);
   dalloc(e->h_nch, (size_t)touch_max + 1);
   dalloc(e->h_chb, (size_t)touch_max + 2);
   e->h_max_chunks = ch ? e->h_sort_cap / kHTile + touch_max + 2 : 0;
-  dalloc(e->ch_sum, e->h_max_chunks);
-  dalloc(e->ch_pre, e->h_max_chunks);
-  dalloc(e->ch_stats, e->h_max_chunks * kChunkStats);
+  dalloc(e->ch_sum, kFm ? e->h_max_chunks : 0);
+  dalloc(e->ch_pre, kFm ? e->h_max_chunks : 0);
+  dalloc(e->ch_stats, kFm ? e->h_max_chunks * kChunkStats : 0);
   dalloc(e->seg_T, touch_max);
-  dalloc(e->starts, (size_t)touch_max * capc);
+  dalloc(e->starts, kFm ? (size_t)touch_max * capc : 0);
   dalloc(e->nc_new, touch_max);
-  dalloc(e->acc_xw, (size_t)touch_max * capc);
-  dalloc(e->acc_w, (size_t)touch_max * capc);
+  dalloc(e->acc_xw, kFm ? (size_t)touch_max * capc : 0);
+  dalloc(e->acc_w, kFm ? (size_t)touch_max * capc : 0);
   dalloc(e->h_err, 4); dzero(e->h_err, 4, st);
   dalloc(e->hseen, ch); dzero(e->hseen, ch, st);
   dalloc(e->hpend, ch); dzero(e->hpend, ch, st);
@@ -269,7 +275,7 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_vhflag, touch_max);
   dalloc(e->h_warmflag, touch_max);
   dalloc(e->h_warmlist, touch_max);
-  dalloc(e->hA2, e->h_sort_cap); dalloc(e->hB2, e->h_sort_cap);
+  dalloc(e->hA2, kFm ? e->h_sort_cap : 0); dalloc(e->hB2, kFm ? e->h_sort_cap : 0);
   dalloc(e->h_csv, ch ? R : 0); dalloc(e->h_csw, ch ? R : 0); dalloc(e->h_cpk, ch ? R : 0);  // (u32 per record)
   dalloc(e->h_lstat, ch ? (uint64_t)kLongStatKeys * kLongStatSlices * 8 : 0);
   dalloc(e->h_lpt0, touch_max); dalloc(e->h_lpt1, touch_max);
@@ -283,8 +289,8 @@ void create_impl(vn_engine* e) {
   dalloc(e->h_pcnt, touch_max);
   dalloc(e->h_pi0, touch_max);
   dalloc(e->h_pbase, (size_t)touch_max + 1);
-  dalloc(e->p_start, ch ? R + 1 : 0);
-  dalloc(e->p_end, ch ? R + 1 : 0);
+  dalloc(e->p_start, kFm && ch ? R + 1 : 0);
+  dalloc(e->p_end, kFm && ch ? R + 1 : 0);
   dalloc(e->r_flag, touch_max);
   dalloc(e->r_len, touch_max);
   dalloc(e->r_list, touch_max);
