@@ -2,7 +2,7 @@
 digest, compared as whole digests: the GobEncode of every key (merging_digest.go:361-380, pending
 temps merged first) byte for byte, plus the quantiles.
 
-Keys of >= 262144 samples in one ingest call take the batched kernel (kBatchMinLen); every key
+Keys of >= 524288 samples in one ingest call take the batched kernel (kBatchMinLen); every key
 below carries at least that many per call.  The distributions aim at its
 special paths:
   * lognormal with C4's rate mix -- the steady state (flips restart a batch);
@@ -107,15 +107,15 @@ def _check(kinds, n, seed, batches):
 
 @pytest.mark.parametrize("batches", [1, 3])
 def test_batched_replay_whole_digest_bit_exact(batches):
-    _check(["lognormal", "falling", "rising", "ints", "seven", "heavy"], 300_000 * batches, 11 + batches, batches)
+    _check(["lognormal", "falling", "rising", "ints", "seven", "heavy"], 600_000 * batches, 11 + batches, batches)
 
 
 def test_weights_past_2_30_with_non_integer_weights_bit_exact():
     """a digest holding non-integer (2^-23-grid) weights whose total passes 2^30 --
     the fast paths' exact-sum bound for such weights -- stays the reference's digest, bit for bit
     (the batched and four-wave replays step aside past the bound)."""
-    _check(["past2_30", "past2_30"], 200_000, 7, 1)
-    _check(["past2_30"], 30_000, 8, 2)
+    _check(["past2_30", "past2_30"], 600_000, 7, 1)  # (batched)
+    _check(["past2_30"], 200_000, 8, 2)  # (four-wave: 100k per call)
 
 
 def test_batched_replay_one_long_key_bit_exact():
@@ -124,7 +124,7 @@ def test_batched_replay_one_long_key_bit_exact():
 
 
 def test_four_wave_replay_new_last_centroid_bit_exact():
-    """Keys of 65536-262143 samples per call take the four-wave replay (merge_fast).  A rising
+    """Keys of 65536-524287 samples per call take the four-wave replay (merge_fast).  A rising
     stream piles its temps past the last main centroid until they must start one of their own: the
     predicted chain ("every temp joins the centroid before it") has to be checked against the last
     element even when no later start exists (a bug found by the whole-digest comparison in round 4)."""
@@ -140,7 +140,7 @@ def test_replay_state_after_every_call_bit_exact(calls):
     the out-of-line four-wave merge that this first merge used to take halved the centroids of
     continuing keys (tools/probe/repro_batch3_calls.py)."""
     kinds = ["lognormal", "falling", "rising", "ints", "seven", "heavy"]
-    slot, val, rate, nk = _stream(kinds, 300_000 * calls, 11 + calls)
+    slot, val, rate, nk = _stream(kinds, 600_000 * calls, 11 + calls)
     wts = (np.float32(1.0) / rate).astype(np.float64)
     cuts = np.linspace(0, len(slot), calls + 1).astype(int)
     with V.Engine((1, 1, nk, 1), percentiles=PCT, max_batch_records=len(slot) + 1) as e:

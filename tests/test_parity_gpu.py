@@ -397,7 +397,7 @@ def test_histo_keys_cross_threshold_across_batches(batches):
 
 
 def test_histo_exact_replay_long_keys_multi_batch():
-    """four-wave replays (a key's batch share of 65536 .. 262143 samples) continuing from pending
+    """four-wave replays (a key's batch share of 65536 .. 524287 samples) continuing from pending
     temps, batch after batch: bit-identical quantiles"""
     d = V.synth(seed=26, n_keys=8, zipf_s=0.0, mix=(0, 0, 1, 0), n_samples=3_200_000)
     _histo_parity(d, d["n_slots"], batches=4, max_rank=0.0)

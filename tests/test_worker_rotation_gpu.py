@@ -39,7 +39,7 @@ def _check(f, d):
 
 def test_worker_three_engines_seven_windows_match_oracle_per_window():
     """D = 3 engines over 7 windows of 2M samples (the longest timer keys take the long-key
-    replays; the batched one, from 262144 samples, is covered by test_batch_replay_gpu.py): each
+    replays; the batched one, from 524288 samples, is covered by test_batch_replay_gpu.py): each
     window's flush equals the oracle of that window alone."""
     ws = _windows(7, 2000, 2_000_000)
     cap = tuple(max(max(d["n_slots"][c] for d in ws), 1) for c in range(4))

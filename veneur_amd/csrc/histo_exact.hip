@@ -1032,10 +1032,11 @@ __global__ void k_exact_chunk_owner(ExactCtx x) {
 // Keys replaying at least this many samples take the batched kernel.  Its LDS is a whole CU's,
 // so every batched key holds a CU for its chain: at C4 with 65536 about 250 keys per window took
 // nearly every CU at once and the windows in flight waited for them.  262144 (about 60 keys; the
-// rest on the four-wave kernel, each under 25 ms): C4 at N = 1 72.4 -> 61.6 / 62.2 ms per window;
-// 16384 / 32768: 106 / 87 ms; 524288 and 2^20 no better than 262144 (profiles/r06_batchlen/)
+// rest on the four-wave kernel): C4 at N = 1 72.4 -> 61.6 / 62.2 ms per window at four engines;
+// 16384 / 32768: 106 / 87 ms.  524288 (about 30 keys, each of the others under 50 ms of four-wave
+// replay): the same at four engines, 55.0 / 54.7 against 56.2 / 57.8 ms at five (profiles/r06_batchlen/)
 #ifndef VN_BATCH_MIN_LEN
-#define VN_BATCH_MIN_LEN 262144u
+#define VN_BATCH_MIN_LEN 524288u
 #endif
 constexpr uint32_t kBatchMinLen = VN_BATCH_MIN_LEN;
 
