@@ -1060,19 +1060,30 @@ __device__ __forceinline__ double wave_max_go(double v) {
 }
 
 // sort pure chunk g of key k, whose first record is base (one wave)
+// (pre: tcap <= 64 and the lane's record -- A, B at base + lane -- already loaded into pa / pb)
 __device__ __forceinline__ void chunk_sort_one(const ExactCtx& x, const uint32_t g, const uint32_t k,
-                                               const uint64_t base, char* smem) {
+                                               const uint64_t base, char* smem, const bool pre = false,
+                                               const uint64_t pa = 0, const uint64_t pb = 0) {
   const uint32_t lane = threadIdx.x;
   const uint32_t tcap = x.tcap, TP = round64(tcap + 1);
   ldsf64* tv = (ldsf64*)smem;
   ldsf64* tw = tv + TP;
   ldsf64* sv = tw + TP;
   ldsf64* sw = sv + TP;
-  for (uint32_t t = lane; t < tcap; t += 64) {
-    const uint32_t tag = (uint32_t)x.B[base + t];
-    const double wt = tag_weight(tag, x.impw);
-    tv[t] = bitsd(x.A[base + t]);
-    tw[t] = tag_is_sample(tag) ? wt : -wt;  // sign: an imported centroid (no Local* statistics)
+  if (pre) {
+    if (lane < tcap) {
+      const uint32_t tag = (uint32_t)pb;
+      const double wt = tag_weight(tag, x.impw);
+      tv[lane] = bitsd(pa);
+      tw[lane] = tag_is_sample(tag) ? wt : -wt;
+    }
+  } else {
+    for (uint32_t t = lane; t < tcap; t += 64) {
+      const uint32_t tag = (uint32_t)x.B[base + t];
+      const double wt = tag_weight(tag, x.impw);
+      tv[t] = bitsd(x.A[base + t]);
+      tw[t] = tag_is_sample(tag) ? wt : -wt;  // sign: an imported centroid (no Local* statistics)
+    }
   }
   wave_lds_sync();
   if (x.cstat && x.nex[k] >= kBatchMinLen) {
@@ -1169,27 +1180,58 @@ __device__ __forceinline__ bool is_top_key(const ExactCtx& x, uint32_t k, uint32
 // against 6.7 ms -- chunks whose ties take Go's sort on one lane cluster by key).  The grid is a
 // multiple of 8 * kChunkRun (histo_exact_chunk_sort)
 constexpr uint32_t kChunkRun = VN_CHUNK_XCD;
+// A wave takes kChunksPerWave consecutive chunks, every one's record loads issued before it sorts
+// the first.  Measured (C4, one engine, rocprofv3): 6.26 ms per window with one chunk per wave,
+// 6.85 with two, 6.87 with four (66 VGPRs: seven waves per SIMD); the whole bench 54.4-54.6 against
+// 55.4-55.5 ms per window with two (profiles/r06_chunkwave/)
+#ifndef VN_CHUNKS_PER_WAVE
+#define VN_CHUNKS_PER_WAVE 1
+#endif
+constexpr uint32_t kChunksPerWave = VN_CHUNKS_PER_WAVE;
 __global__ __launch_bounds__(64) void k_exact_chunk_sort(ExactCtx x, uint32_t top) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const uint32_t total = x.coff[x.nkeys];
 #if VN_CHUNK_XCD
   const uint32_t r = blockIdx.x >> 3, q = (r / kChunkRun) * 8u + (blockIdx.x & 7u);
-  const uint32_t g = q * kChunkRun + r % kChunkRun;
+  const uint32_t m = q * kChunkRun + r % kChunkRun;
 #else
-  const uint32_t g = blockIdx.x;
+  const uint32_t m = blockIdx.x;
 #endif
-  if (g >= total) return;
-  uint32_t k, base;
-  if (x.cown) {
-    const uint64_t o = x.cown[g];
-    k = (uint32_t)(o >> 32);
-    base = (uint32_t)o;
-  } else {
-    k = last_le_u32(x.coff, x.nkeys, g);
-    base = chunk_base(x, g, k);
+  const uint32_t lane = threadIdx.x;
+  const bool pre = x.tcap <= 64;
+  uint32_t gk[kChunksPerWave], kk[kChunksPerWave], bk[kChunksPerWave];
+  bool live[kChunksPerWave];
+  uint64_t pa[kChunksPerWave], pb[kChunksPerWave];
+#pragma unroll
+  for (uint32_t c = 0; c < kChunksPerWave; c++) {
+    const uint32_t g = m * kChunksPerWave + c;
+    gk[c] = g;
+    live[c] = g < total;
+    kk[c] = 0u;
+    bk[c] = 0u;
+    pa[c] = 0ull;
+    pb[c] = 0ull;
+    if (!live[c]) continue;
+    if (x.cown) {
+      const uint64_t o = x.cown[g];
+      kk[c] = (uint32_t)(o >> 32);
+      bk[c] = (uint32_t)o;
+    } else {
+      kk[c] = last_le_u32(x.coff, x.nkeys, g);
+      bk[c] = chunk_base(x, g, kk[c]);
+    }
+    if (top && is_top_key(x, kk[c], top)) live[c] = false;
+    if (live[c] && pre && lane < x.tcap) {
+      pa[c] = x.A[(uint64_t)bk[c] + lane];
+      pb[c] = x.B[(uint64_t)bk[c] + lane];
+    }
   }
-  if (top && is_top_key(x, k, top)) return;
-  chunk_sort_one(x, g, k, base, smem);
+#pragma unroll
+  for (uint32_t c = 0; c < kChunksPerWave; c++) {
+    if (!live[c]) continue;
+    chunk_sort_one(x, gk[c], kk[c], bk[c], smem, pre, pa[c], pb[c]);
+    wave_lds_sync();  // (the next chunk reuses the LDS tiles)
+  }
 }
 
 // the chunks of the first `top` keys of x.order64: block (b, y) takes key y's chunks b, b + G, ...
@@ -3670,8 +3712,8 @@ void histo_exact_chunk_sort(const ExactCtx& x, hipStream_t st, uint64_t max_chun
     return;
   }
   const uint64_t span = VN_CHUNK_XCD ? 8ull * VN_CHUNK_XCD : 1ull;
-  hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)((max_chunks + span - 1) / span * span)), dim3(64), sm, st, x,
-                     top);
+  const uint64_t waves = (max_chunks + kChunksPerWave - 1) / kChunksPerWave;
+  hipLaunchKernelGGL(k_exact_chunk_sort, dim3((uint32_t)((waves + span - 1) / span * span)), dim3(64), sm, st, x, top);
 }
 
 uint32_t histo_exact_top_keys(const ExactCtx& x) {
