@@ -1034,7 +1034,8 @@ __global__ void k_exact_chunk_owner(ExactCtx x) {
 // nearly every CU at once and the windows in flight waited for them.  262144 (about 60 keys; the
 // rest on the four-wave kernel): C4 at N = 1 72.4 -> 61.6 / 62.2 ms per window at four engines;
 // 16384 / 32768: 106 / 87 ms.  524288 (about 30 keys, each of the others under 50 ms of four-wave
-// replay): the same at four engines, 55.0 / 54.7 against 56.2 / 57.8 ms at five (profiles/r06_batchlen/)
+// replay): the same at four engines, 55.0 / 54.7 against 56.2 / 57.8 ms at five; 2^20 at five:
+// 56.5 / 55.9 / 55.9 against 54.9 / 54.8 / 55.0 (profiles/r06_batchlen/)
 #ifndef VN_BATCH_MIN_LEN
 #define VN_BATCH_MIN_LEN 524288u
 #endif
